@@ -1,0 +1,57 @@
+/*
+ * sdl_oracle.h -- CPU restatement of the reference Batcher hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and the
+ * cpu_baseline leg of bench.py may load this library, and only as the checker
+ * (or the timed CPU baseline) -- never as the product path.
+ *
+ * What it restates (reference = andywag/streaming_data_loader @ v1):
+ *   - HF `tokenizers` 0.13.1 (crate, not vendored; called at
+ *     rust/src/tokenizer/tokenizer_holder.rs:22) for a bert-base-uncased
+ *     tokenizer.json: AddedVocabulary split -> BertNormalizer -> BertPreTokenizer
+ *     -> WordPiece -> TemplateProcessing "[CLS] $A [SEP]".
+ *   - TokenizerWrapper::encode_mask framing (tokenizer_wrapper.rs:107-134).
+ *   - GenTokenizer::create_sync_batch / get_working_batch (gen_batcher.rs:44-98).
+ *   - BertData::put_data + mask_batch (models/bert_data.rs:40-89).
+ *   - The seeded RNG contract that replaces the reference's unseedable
+ *     thread_rng (DESIGN.md "RNG contract").
+ */
+#ifndef SDL_ORACLE_H
+#define SDL_ORACLE_H
+#include <stddef.h>
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct orc_tok orc_tok;
+typedef struct orc_batcher orc_batcher;
+
+/* Loads vocab.txt (one piece per line, id = line number) and the Unicode table
+ * (streaming_data_loader_amd/data/bert_uncased_unicode.bin). NULL on failure. */
+orc_tok *orc_tok_load(const char *vocab_txt, const char *unicode_bin);
+void orc_tok_free(orc_tok *t);
+int orc_tok_vocab_size(const orc_tok *t);
+
+/* Tokenizer::encode(text, add_special_tokens=true).get_ids()
+ * (tokenizer_holder.rs:19-28).  Returns the id count; writes at most cap. */
+long orc_bert_encode(const orc_tok *t, const uint8_t *s, size_t n, uint32_t *out, size_t cap);
+
+/* Philox4x32-10 MLM key of (seed, record, chunk, position) -- RNG contract. */
+uint32_t orc_mlm_key(uint64_t seed, uint64_t record, uint32_t chunk, uint32_t pos);
+
+/* GenTokenizer(chunk) + BertData(Mask). task 0 = mlm (only mode in round 1). */
+orc_batcher *orc_batcher_new(const orc_tok *t, int task, int batch_size, int seq_len,
+                             int mask_length, int mask_id, uint64_t seed);
+/* create_sync_batch(text).  Returns 1 and fills out (4*B*S int32: input_ids,
+ * attention_mask, token_type_ids, labels, each [B,S] row-major) and *rows when a
+ * batch is emitted, 0 when not.  Records are numbered 0,1,2,... in push order. */
+int orc_batcher_push(orc_batcher *b, const uint8_t *s, size_t n, int32_t *out, int *rows);
+/* get_working_batch(): pops the front batch (maybe partial). 1 if one existed. */
+int orc_batcher_flush(orc_batcher *b, int32_t *out, int *rows);
+void orc_batcher_free(orc_batcher *b);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
