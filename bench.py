@@ -1,0 +1,229 @@
+#!/usr/bin/env python3
+"""Device-resident tokenize+mask throughput of the MI355X Batcher.
+
+BASELINE.json metric: "device-resident tokenize+mask MB/s of input text,
+seq_len=512, 1/2/4/8 MI355X", quoted on configs[1]: task=mlm (BERT WordPiece,
+15% mask), seq_len=512, batch=256.
+
+One step = one pass of the hot path (sdl_process_device) over this rank's text
+arena already resident in HBM: tokenize every record, frame, filter, chunk
+into rows of 512, mask, and write the packed [rows, 512] int32 planes
+(input_ids, attention_mask, token_type_ids, labels) -- every batch of 256
+rows the arena yields.  Records are independent, so each rank owns a disjoint
+shard of the global record stream (weak scaling, no data-path collective);
+the barrier and the max-over-ranks time reduction are the harness's only
+communication.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+  torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU)
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "tests"))
+
+METRIC = "device-resident tokenize+mask MB/s of input text, seq_len=512, 1/2/4/8 MI355X"
+HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def fixture_records():
+    with open(os.path.join(REPO, "tests", "golden", "test_records.jsonl"), encoding="utf-8") as f:
+        return [json.loads(l)["text"] for l in f]
+
+
+def build_arena(records, nbytes, seed):
+    """Fixture records (data/test.json.gz) tiled in seeded permutations."""
+    blobs = [r.encode("utf-8") for r in records]
+    rng = np.random.default_rng(seed)
+    order, total = [], 0
+    while total < nbytes:
+        for i in rng.permutation(len(blobs)):
+            order.append(int(i))
+            total += len(blobs[i])
+            if total >= nbytes:
+                break
+    offs = np.zeros(len(order) + 1, np.uint64)
+    np.cumsum(np.array([len(blobs[i]) for i in order], np.uint64), out=offs[1:])
+    arena = np.concatenate([np.frombuffer(blobs[i], np.uint8) for i in order] + [np.zeros(16, np.uint8)])
+    return arena, offs, order
+
+
+def cpu_baseline(records, order, seconds=12.0, max_bytes=96 << 20):
+    """The CPU oracle (C restatement of the reference Batcher, one thread --
+    the reference runs one Batcher task) on a bounded prefix of the same
+    record stream, same config.  Test-infrastructure code, timed only here."""
+    import oracle_lib
+    tok = oracle_lib.Tok()
+    ob = oracle_lib.OracleBatcher(tok, 256, 512, 76, 103, seed=1234)
+    blobs = [r.encode("utf-8") for r in records]
+    done = n = 0
+    t0 = time.perf_counter()
+    for i in order:
+        ob.push(blobs[i])
+        done += len(blobs[i])
+        n += 1
+        if (n & 63) == 0 and (time.perf_counter() - t0 > seconds or done >= max_bytes):
+            break
+    dt = time.perf_counter() - t0
+    return {"value": round(done / dt / 1e6, 3), "unit": "MB/s", "cores": 1, "kind": "port",
+            "sample": f"first {n} records ({done / 1e6:.1f} MB) of rank 0's arena, mlm S=512 B=256, "
+                      f"oracle/sdl_oracle.c single-threaded, {dt:.1f} s"}
+
+
+def load_traffic():
+    """HBM bytes per tokenize launch from the committed rocprofv3 PMC summary
+    (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE, MI355X_MICROARCH.md §HBM)."""
+    p = os.path.join(REPO, "profiles", "pmc_wordpiece.json")
+    if not os.path.exists(p):
+        return None
+    try:
+        with open(p) as f:
+            return json.load(f).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--arena-mib", type=int, default=256)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--e2e", action="store_true", help="also time pinned H2D + kernels + D2H")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+
+    from streaming_data_loader_amd import build
+    from streaming_data_loader_amd.device import DeviceBatcher
+
+    if not os.path.exists(build.LIB):
+        build.build()
+    records = fixture_records()
+    arena, offs, order = build_arena(records, args.arena_mib << 20, seed=0x5D1B + rank)
+    N, R = len(arena) - 16, len(order)
+    text = torch.from_numpy(arena).to(dev)
+    offsets = torch.from_numpy(offs.astype(np.int64)).to(dev)
+    stream = torch.cuda.Stream(device=dev)
+    db = DeviceBatcher(batch_size=256, sequence_length=512, seed=1234, device=local)
+    first_record = rank * 10_000_000  # disjoint global record indices per shard
+
+    def step():
+        return db.process(text.data_ptr(), N, offsets.data_ptr(), R, first_record, stream.cuda_stream)
+
+    for _ in range(args.warmup):
+        res = step()
+    torch.cuda.synchronize(dev)
+    db.set_profiling(True)
+    stage_sum = {}
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res = step()
+        # stage times of this step (events on the stream the kernels run on)
+        for k, v in db.stage_times().items():
+            stage_sum[k] = stage_sum.get(k, 0.0) + v
+    torch.cuda.synchronize(dev)
+    barrier()
+    dt = time.perf_counter() - t0
+    db.set_profiling(False)
+    if world > 1:
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+
+    rows, toks = res.rows(), res.tokens()
+    stage_ms = {k: v / args.steps for k, v in stage_sum.items()}
+    tok_ms = stage_ms["wordpiece_chunks"]
+    step_ms = dt / args.steps * 1e3
+    total_bytes = N * world * args.steps
+    value = total_bytes / dt / 1e6
+    # algorithmic bytes of one wordpiece_chunks launch: read the text + record
+    # offsets, write the ids (4 B each)
+    tok_bytes = N + 8 * (R + 1) + 4 * toks
+    achieved = tok_bytes / (tok_ms * 1e-3) / 1e9
+    # whole path, per step: text + offsets + the four int32 [rows, 512] planes
+    path_bytes = N + 8 * (R + 1) + 16 * rows * 512
+    line = {
+        "metric": METRIC, "value": round(value, 2), "unit": "MB/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(step_ms, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "u8->int32", "data": "synthetic: data/test.json.gz records tiled (seeded)",
+        "config": {"workload": "mlm seq_len=512 batch=256 (BASELINE configs[1]), one step = one rank's "
+                               f"{args.arena_mib} MiB text arena -> all packed batches",
+                   "task": "mlm", "seq_len": 512, "batch": 256, "arena_bytes_per_gpu": N, "records_per_gpu": R,
+                   "rows_per_gpu": rows, "batches_per_gpu": -(-rows // 256), "ids_per_gpu": toks,
+                   "tokenizer": "bert-base-uncased layout, offline proxy vocab (30,522)",
+                   "parallelism": f"record shards x{world}, no collective"},
+        "roofline": {"bound": "hbm", "kernel": "k_wordpiece_chunks", "achieved": round(achieved, 2),
+                     "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 5),
+                     "traffic": load_traffic(), "algorithmic_bytes_per_launch": tok_bytes,
+                     "avg_launch_ms": round(tok_ms, 4)},
+        "stage_ms": {k: round(v, 4) for k, v in stage_ms.items()},
+        "path_GBps": round(path_bytes / (step_ms * 1e-3) / 1e9, 2),
+    }
+    if args.e2e and rank == 0:
+        line["end_to_end"] = end_to_end(db, arena, offs, N, R, torch, dev, stream)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(records, order)
+    elif rank == 0:
+        line["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def end_to_end(db, arena, offs, N, R, torch, dev, stream, reps=3):
+    """Host arena in pinned memory -> H2D -> kernels -> D2H of every row."""
+    from streaming_data_loader_amd import native
+    h_text = torch.from_numpy(arena).pin_memory()
+    h_off = torch.from_numpy(offs.astype(np.int64)).pin_memory()
+    d_text = torch.empty_like(h_text, device=dev)
+    d_off = torch.empty_like(h_off, device=dev)
+    res = db.process(d_text.data_ptr(), N, d_off.data_ptr(), R, 0, stream.cuda_stream)
+    torch.cuda.synchronize(dev)
+    rows = res.rows()
+    out = torch.empty((4, rows, 512), dtype=torch.int32).pin_memory()
+    best = None
+    for _ in range(reps):
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        with torch.cuda.stream(stream):
+            d_text.copy_(h_text, non_blocking=True)
+            d_off.copy_(h_off, non_blocking=True)
+        res = db.process(d_text.data_ptr(), N, d_off.data_ptr(), R, 0, stream.cuda_stream)
+        stream.synchronize()
+        for j, ptr in enumerate((res.r.input_ids, res.r.attention_mask, res.r.token_type_ids, res.r.labels)):
+            native.d2h(out[j].numpy(), ptr, rows * 512 * 4)
+        stream.synchronize()
+        dt = time.perf_counter() - t0
+        best = dt if best is None else min(best, dt)
+    return {"MBps": round(N / best / 1e6, 2), "ms": round(best * 1e3, 3),
+            "note": "pinned H2D of text+offsets, all kernels, D2H of the 4 int32 planes into pinned host memory"}
+
+
+if __name__ == "__main__":
+    main()

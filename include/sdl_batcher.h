@@ -1,0 +1,163 @@
+/*
+ * sdl_batcher.h -- C ABI of the MI355X-native Batcher (libsdl_batcher.so).
+ *
+ * Drop-in boundary for the reference's Batcher stage
+ * (andywag/streaming_data_loader @ v1, rust/src/batcher.rs:26-31):
+ *
+ *     pub trait Batcher { type S; type T;
+ *         fn create_sync_batch(&mut self, data: Self::S) -> Option<Self::T>;
+ *         fn get_working_batch(&mut self) -> Option<Self::T>; }
+ *
+ * implemented for the masking tasks by GenTokenizer
+ * (rust/src/tasks/gen_batcher.rs:65-98, S = String, T = DataSet) and for the
+ * multi-label task by SimpleBatcher (rust/src/models/simple_batcher.rs:31-53).
+ * INTEGRATION.md shows the Rust `impl Batcher for GpuBatcher` that binds this
+ * header through `extern "C"` so the Provider -> Batcher -> Transport channels
+ * (rust/src/tasks/runner_simple.rs:68-112) stay unchanged.
+ *
+ * Conventions: plain pointers and sizes only; every call returns an int
+ * status (SDL_OK = 0, < 0 error; never a panic across the FFI; the message is
+ * in sdl_last_error()).  One handle per host thread / GPU; handles are not
+ * thread-safe.  Input text is copied in (the caller keeps ownership, as the
+ * reference moves the String in); batches are owned by the handle until
+ * sdl_batch_release().
+ */
+#ifndef SDL_BATCHER_H
+#define SDL_BATCHER_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SDL_ABI_VERSION 1
+
+enum {
+    SDL_OK = 0,
+    SDL_ERR_ARG = -1,         /* bad argument / config (reference: panic!/todo!) */
+    SDL_ERR_IO = -2,          /* tokenizer asset unreadable */
+    SDL_ERR_HIP = -3,         /* HIP runtime error */
+    SDL_ERR_UNSUPPORTED = -4, /* task / tokenizer feature not implemented */
+    SDL_ERR_NODEV = -5,       /* no HIP device: the product never falls back to the CPU */
+    SDL_ERR_STATE = -6,       /* call out of order */
+    SDL_ERR_CAPACITY = -7     /* input larger than one call supports (>= 4 GiB of text) */
+};
+
+/* TaskType -> DataSet selection (rust/src/config.rs:20-62). */
+enum {
+    SDL_TASK_MLM = 0,        /* BertData, DataSetConfig::Mask   (models/bert_data.rs) */
+    SDL_TASK_CLM = 1,        /* GptData,  DataSetConfig::Gpt    (models/gpt_data.rs) */
+    SDL_TASK_SPAN = 2,       /* T5Data,   DataSetConfig::Span   (models/t5_data.rs) */
+    SDL_TASK_MULTI_LABEL = 3 /* BertData, DataSetConfig::MultiLabel via SimpleBatcher */
+};
+
+/* Mirrors TrainingConfig.batch + .dataset_config (rust/src/config.rs:64-72,
+ * rust/src/batcher.rs:11-14, rust/src/datasets/dataset_config.rs:7-16) plus the
+ * RNG seed that replaces the reference's unseedable thread_rng(). */
+typedef struct sdl_config {
+    int32_t task;            /* SDL_TASK_* */
+    int32_t batch_size;      /* BatchConfig.batch_size */
+    int32_t sequence_length; /* BatchConfig.sequence_length */
+    int32_t chunk;           /* GenTokenizer.chunk (1 for the masking tasks, masking_runner.rs:55-62) */
+    int32_t min_ids;         /* records with fewer framed ids are dropped (gen_batcher.rs:74): 64 */
+    int32_t mask_length;     /* DataSetConfig::Mask.mask_length = (S as f32 * 0.15) as usize */
+    int32_t mask_id;         /* DataSetConfig::Mask.mask = 103 (masking_cases.rs:60) */
+    int32_t number_labels;   /* DataSetConfig::MultiLabel.number_labels */
+    double avg_span_gap;     /* DataSetConfig::Span.avg_span_gap  (16.0) */
+    double avg_span_size;    /* DataSetConfig::Span.avg_span_size (2.0) */
+    uint64_t seed;           /* RNG contract seed */
+    uint64_t first_record;   /* global index of this handle's first record (sharding) */
+    int32_t device;          /* HIP device ordinal */
+    int32_t reserved[7];
+} sdl_config;
+
+/* A finished batch: DataSet's Serialize view (bert_data.rs:106-145,
+ * gpt_data.rs:53-62, t5_data.rs:235-249) as int32 row-major planes. */
+typedef struct sdl_batch {
+    int32_t rows;            /* rows filled (BertData.index); the MLM `labels` list has this length */
+    int32_t batch_size;
+    int32_t sequence_length;
+    int32_t label_width;     /* S (mlm/clm), S/4 (span), number_labels (multi-label) */
+    const int32_t *input_ids;      /* [batch_size, sequence_length] */
+    const int32_t *attention_mask; /* [batch_size, sequence_length] */
+    const int32_t *token_type_ids; /* [batch_size, sequence_length] or NULL (clm/span) */
+    const int32_t *labels;         /* [batch_size, label_width] or NULL (multi-label) */
+    const float *labels_f32;       /* [batch_size, number_labels] (multi-label) or NULL */
+    void *owner_;                  /* opaque, for sdl_batch_release */
+} sdl_batch;
+
+typedef struct sdl_batcher sdl_batcher;
+
+/* Defaults of the reference masking cases (masking_cases.rs:38-94) for `task`:
+ * B=4096 S=128 chunk=1 min_ids=64 mask 15%/103, span 16.0/2.0, 9 labels. */
+void sdl_config_default(sdl_config *cfg, int32_t task);
+
+/* get_tokenizer(cfg) + GenTokenizer::new / SimpleBatcher::new
+ * (tokenizer_wrapper.rs:162-189, gen_batcher.rs:23-41).  `tokenizer_path` is a
+ * HF tokenizer.json (or a WordPiece vocab.txt); `data_dir` holds the Unicode
+ * tables (NULL = directory of the library's package data). */
+int sdl_batcher_create(const sdl_config *cfg, const char *tokenizer_path, const char *data_dir,
+                       sdl_batcher **out);
+void sdl_batcher_destroy(sdl_batcher *h);
+
+/* Batcher::create_sync_batch(data) for one record (gen_batcher.rs:69-94 /
+ * simple_batcher.rs:35-43).  `labels` are the Label::Multi indices for the
+ * multi-label task (ignored otherwise).  Returns 1 and fills *out when this
+ * call emits a batch (at most one per call, as the reference), 0 when not. */
+int sdl_batcher_push(sdl_batcher *h, const uint8_t *utf8, size_t len, const uint32_t *labels,
+                     size_t n_labels, sdl_batch *out);
+
+/* Bulk create_sync_batch over n_records records laid out back to back in
+ * `arena` (record r = arena[offsets[r] .. offsets[r+1]), offsets[0] = 0,
+ * n_records+1 offsets).  Exactly the batches the reference would emit over the
+ * same sequence of calls are queued, in order, for sdl_batcher_next(). */
+int sdl_batcher_push_many(sdl_batcher *h, const uint8_t *arena, const uint64_t *offsets,
+                          size_t n_records, const uint32_t *labels, const uint64_t *label_offsets,
+                          size_t *n_emitted);
+/* Pops the next batch queued by sdl_batcher_push_many: 1 = *out filled, 0 = none. */
+int sdl_batcher_next(sdl_batcher *h, sdl_batch *out);
+/* Batcher::get_working_batch() (gen_batcher.rs:96-98): pops the front batch
+ * (possibly partial, possibly empty).  1 = *out filled, 0 = none left. */
+int sdl_batcher_flush(sdl_batcher *h, sdl_batch *out);
+void sdl_batch_release(sdl_batch *b);
+
+/* ---- Device-resident bulk path (the measured hot path) -------------------
+ * Tokenize + label every record of a device-resident arena in one sequence of
+ * kernel launches on `stream` (a hipStream_t; NULL = the handle's stream),
+ * without any host synchronisation.  Rows are packed densely in record order:
+ * batch b is rows [b*B, (b+1)*B); rows >= *d_rows up to the next multiple of B
+ * hold the reference's initial values.  Buffers are owned by the handle and
+ * stay valid until the next call.  The global record index of record r (RNG
+ * key) is first_record + r. */
+typedef struct sdl_device_rows {
+    int32_t *input_ids;      /* device [rows_capacity, S] */
+    int32_t *attention_mask; /* device [rows_capacity, S] */
+    int32_t *token_type_ids; /* device [rows_capacity, S] or NULL */
+    int32_t *labels;         /* device [rows_capacity, label_width] */
+    float *labels_f32;       /* device [rows_capacity, number_labels] or NULL */
+    uint32_t *d_rows;        /* device scalar: rows produced */
+    uint32_t *d_record_rows; /* device [n_records]: rows each record produced */
+    uint32_t *d_tokens;      /* device scalar: tokenizer ids produced (before framing) */
+    uint64_t rows_capacity;
+    int32_t label_width;
+} sdl_device_rows;
+
+int sdl_process_device(sdl_batcher *h, const uint8_t *d_text, uint64_t text_len,
+                       const uint64_t *d_offsets, uint64_t n_records, uint64_t first_record,
+                       void *stream, sdl_device_rows *out);
+
+/* Per-stage device time (ms) of the last sdl_process_device call, measured with
+ * hipEvents on the stream the kernels ran on, when enabled. */
+int sdl_set_profiling(sdl_batcher *h, int enable);
+int sdl_stage_times(sdl_batcher *h, const char **names, float *ms, int cap);
+
+/* Last error message of the calling thread. */
+const char *sdl_last_error(void);
+int sdl_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SDL_BATCHER_H */

@@ -488,3 +488,5 @@ void orc_batcher_free(orc_batcher *b) {
     free(b->q);
     free(b);
 }
+
+void orc_batcher_set_next_record(orc_batcher *b, uint64_t record) { b->n_records = record; }

@@ -50,6 +50,8 @@ int orc_batcher_push(orc_batcher *b, const uint8_t *s, size_t n, int32_t *out, i
 /* get_working_batch(): pops the front batch (maybe partial). 1 if one existed. */
 int orc_batcher_flush(orc_batcher *b, int32_t *out, int *rows);
 void orc_batcher_free(orc_batcher *b);
+/* Sets the global index the next pushed record gets (sharded streams). */
+void orc_batcher_set_next_record(orc_batcher *b, uint64_t record);
 
 #ifdef __cplusplus
 }

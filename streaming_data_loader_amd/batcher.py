@@ -1,0 +1,259 @@
+"""Python mirror of the reference Batcher interface over the HIP library.
+
+Same names, argument meaning and error behaviour as the reference's Rust:
+  BatchConfig            rust/src/batcher.rs:11-23
+  Batcher (trait)        rust/src/batcher.rs:26-31
+  create_batch (driver)  rust/src/batcher.rs:33-77
+  GenTokenizer           rust/src/tasks/gen_batcher.rs:12-98
+  DataSetConfig          rust/src/datasets/dataset_config.rs:7-16
+  ModelType / TaskType   rust/src/config.rs:20-62
+  ProviderChannel        rust/src/provider/mod.rs:21-25
+  masking cases          rust/src/tasks/masking/masking_cases.rs:34-94
+Every record's tokenize + mask runs in libsdl_batcher.so on the GPU.
+"""
+import ctypes
+import enum
+from dataclasses import dataclass, field
+from typing import Optional, Union
+
+import numpy as np
+
+from . import native
+
+
+# ---- configuration (serde structs of the reference) ----------------------------
+@dataclass
+class BatchConfig:
+    batch_size: int
+    sequence_length: int
+
+
+@dataclass
+class Mask:
+    mask_length: int
+    mask: int = 103
+
+
+@dataclass
+class Gpt:
+    pass
+
+
+@dataclass
+class Span:
+    avg_span_gap: float = 16.0
+    avg_span_size: float = 2.0
+
+
+@dataclass
+class MultiLabel:
+    number_labels: int = 9
+
+
+DataSetConfig = Union[Mask, Gpt, Span, MultiLabel]
+
+
+class ModelType(enum.Enum):
+    Bert = "bert"
+    Roberta = "roberta"
+    Gpt2 = "gpt2"
+    T5 = "t5"
+
+
+class TaskType(enum.Enum):
+    Mlm = "mlm"
+    Clm = "clm"
+    Span = "span"
+    MultiLabel = "multi-label"
+
+
+@dataclass
+class TokenizerConfig:
+    """TokenizerInternalConfig: the reference names a hub tokenizer
+    (HuggingFace("bert-base-uncased")); offline, `path` is its tokenizer.json."""
+    path: str = native.BERT_PROXY_TOKENIZER
+
+
+@dataclass
+class TrainingConfig:
+    model_config: ModelType
+    tokenizer: TokenizerConfig
+    batch: BatchConfig
+    dataset_config: DataSetConfig
+    seed: int = 0
+    device: int = 0
+
+
+def get_mask_length(sequence_length: int) -> int:
+    """masking_cases.rs:34-36: (sequence_length as f32 * 0.15) as usize."""
+    return int(np.float32(sequence_length) * np.float32(0.15))
+
+
+def get_case(task: TaskType, test: bool, sequence_length: int = 128, batch_size: Optional[int] = None,
+             seed: int = 0) -> TrainingConfig:
+    """masking_cases::get_case: B=4096 (test: 1), S=128 unless overridden."""
+    b = batch_size if batch_size is not None else (1 if test else 4096)
+    batch = BatchConfig(b, sequence_length)
+    if task == TaskType.Mlm:
+        return TrainingConfig(ModelType.Bert, TokenizerConfig(), batch, Mask(get_mask_length(sequence_length), 103),
+                              seed)
+    if task == TaskType.Clm:
+        return TrainingConfig(ModelType.Gpt2, TokenizerConfig(), batch, Gpt(), seed)
+    if task == TaskType.Span:
+        return TrainingConfig(ModelType.T5, TokenizerConfig(), batch, Span(16.0, 2.0), seed)
+    return TrainingConfig(ModelType.Bert, TokenizerConfig(), BatchConfig(2048 if batch_size is None else b,
+                                                                        sequence_length), MultiLabel(9), seed)
+
+
+# ---- channel messages --------------------------------------------------------
+class ProviderChannel:
+    @dataclass
+    class Info:
+        value: object
+
+    @dataclass
+    class Data:
+        value: object
+
+    class Complete:
+        pass
+
+
+# ---- DataSet -------------------------------------------------------------------
+@dataclass
+class DataSet:
+    """One batch; `to_dict()` is the reference's Serialize view
+    (bert_data.rs:106-145, gpt_data.rs:53-62)."""
+    kind: str
+    rows: int
+    input_ids: np.ndarray
+    attention_mask: np.ndarray
+    labels: np.ndarray
+    token_type_ids: Optional[np.ndarray] = None
+
+    def to_dict(self):
+        if self.kind == "bert":
+            # MLM labels: one Vec<i32> per filled row (label list has `index` entries)
+            return {"input_ids": self.input_ids, "attention_mask": self.attention_mask,
+                    "token_type_ids": self.token_type_ids, "labels": self.labels[:self.rows]}
+        return {"input_ids": self.input_ids, "attention_mask": self.attention_mask, "labels": self.labels}
+
+
+def _dataset_from(b: native.Batch, kind: str) -> DataSet:
+    B, S, LW = b.batch_size, b.sequence_length, b.label_width
+
+    def arr(ptr, n, cols):
+        return np.ctypeslib.as_array(ptr, shape=(n * cols,)).reshape(n, cols).copy()
+
+    ds = DataSet(kind=kind, rows=b.rows, input_ids=arr(b.input_ids, B, S), attention_mask=arr(b.attention_mask, B, S),
+                 labels=arr(b.labels, B, LW),
+                 token_type_ids=arr(b.token_type_ids, B, S) if bool(b.token_type_ids) else None)
+    native.load().sdl_batch_release(ctypes.byref(b))
+    return ds
+
+
+# ---- Batcher -------------------------------------------------------------------
+class Batcher:
+    """trait Batcher (batcher.rs:26-31)."""
+
+    def create_sync_batch(self, data):
+        raise NotImplementedError
+
+    def get_working_batch(self):
+        raise NotImplementedError
+
+
+class GenTokenizer(Batcher):
+    """GenTokenizer (gen_batcher.rs:12-98): S = String, T = DataSet.  Each call
+    tokenizes + masks on the GPU; the emission cadence is the reference's (at
+    most one batch per create_sync_batch, one batch on get_working_batch)."""
+
+    def __init__(self, model_type: ModelType, batch_config: BatchConfig, dataset_config: DataSetConfig,
+                 tokenizer: TokenizerConfig, chunk: bool = True, seed: int = 0, device: int = 0,
+                 first_record: int = 0):
+        L = native.load()
+        if isinstance(dataset_config, Mask):
+            task, self.kind = native.SDL_TASK_MLM, "bert"
+        elif isinstance(dataset_config, Gpt):
+            task, self.kind = native.SDL_TASK_CLM, "gpt2"
+        elif isinstance(dataset_config, Span):
+            task, self.kind = native.SDL_TASK_SPAN, "t5"
+        else:
+            task, self.kind = native.SDL_TASK_MULTI_LABEL, "bert"
+        c = native.default_config(task)
+        c.batch_size, c.sequence_length = batch_config.batch_size, batch_config.sequence_length
+        c.chunk = 1 if chunk else 0
+        if isinstance(dataset_config, Mask):
+            c.mask_length, c.mask_id = dataset_config.mask_length, dataset_config.mask
+        if isinstance(dataset_config, Span):
+            c.avg_span_gap, c.avg_span_size = dataset_config.avg_span_gap, dataset_config.avg_span_size
+        if isinstance(dataset_config, MultiLabel):
+            c.number_labels = dataset_config.number_labels
+        c.seed, c.device, c.first_record = seed, device, first_record
+        h = ctypes.c_void_p()
+        native.check(L.sdl_batcher_create(ctypes.byref(c), tokenizer.path.encode(), native.DATA_DIR.encode(),
+                                          ctypes.byref(h)))
+        self._h = h
+        self.batch_config = batch_config
+        self.dataset_config = dataset_config
+
+    @classmethod
+    def from_config(cls, cfg: TrainingConfig, chunk: bool = True):
+        """masking_runner::create_generator (masking_runner.rs:55-62)."""
+        return cls(cfg.model_config, cfg.batch, cfg.dataset_config, cfg.tokenizer, chunk, cfg.seed, cfg.device)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            native.load().sdl_batcher_destroy(self._h)
+            self._h = None
+
+    __del__ = close
+
+    def create_sync_batch(self, data: str) -> Optional[DataSet]:
+        b = native.Batch()
+        raw = data.encode("utf-8") if isinstance(data, str) else bytes(data)
+        got = native.check(native.load().sdl_batcher_push(self._h, raw, len(raw), None, 0, ctypes.byref(b)))
+        return _dataset_from(b, self.kind) if got else None
+
+    def create_sync_batches(self, texts):
+        """create_sync_batch over many records in one device pass; returns the
+        batches the same sequence of calls would have emitted, in order."""
+        blobs = [t.encode("utf-8") if isinstance(t, str) else bytes(t) for t in texts]
+        offs = np.zeros(len(blobs) + 1, np.uint64)
+        np.cumsum([len(x) for x in blobs], out=offs[1:])
+        arena = np.frombuffer(b"".join(blobs) + b"\0" * 16, np.uint8)
+        n = ctypes.c_size_t()
+        native.check(native.load().sdl_batcher_push_many(self._h, arena.ctypes.data, offs.ctypes.data, len(blobs),
+                                                         None, None, ctypes.byref(n)))
+        out = []
+        b = native.Batch()
+        while native.check(native.load().sdl_batcher_next(self._h, ctypes.byref(b))):
+            out.append(_dataset_from(b, self.kind))
+        return out
+
+    def get_working_batch(self) -> Optional[DataSet]:
+        b = native.Batch()
+        got = native.check(native.load().sdl_batcher_flush(self._h, ctypes.byref(b)))
+        return _dataset_from(b, self.kind) if got else None
+
+
+def create_batch(rx, tx, batcher: Batcher):
+    """batcher::create_batch (batcher.rs:33-77): Info passes through, Data is
+    batched, Complete flushes one working batch then forwards Complete.
+    rx/tx are queue-like (get()/put()); a None message ends the loop."""
+    while True:
+        msg = rx.get()
+        if msg is None:
+            break
+        if isinstance(msg, ProviderChannel.Info):
+            tx.put(msg)
+        elif isinstance(msg, ProviderChannel.Complete) or msg is ProviderChannel.Complete:
+            cur = batcher.get_working_batch()
+            if cur is not None:
+                tx.put(ProviderChannel.Data(cur))
+            tx.put(ProviderChannel.Complete())
+            break
+        elif isinstance(msg, ProviderChannel.Data):
+            batch = batcher.create_sync_batch(msg.value)
+            if batch is not None:
+                tx.put(ProviderChannel.Data(batch))

@@ -1,0 +1,74 @@
+"""Builds libsdl_batcher.so (HIP kernels + C ABI) in-tree for gfx950.
+
+    python -m streaming_data_loader_amd.build      # or __graft_entry__.build()
+
+Each translation unit is compiled with `hipcc --offload-arch=gfx950` into
+build/, then linked into streaming_data_loader_amd/libsdl_batcher.so, which is
+git-ignored but travels to the GPU box with the repo snapshot.  hipcc
+cross-compiles without a GPU.
+"""
+import concurrent.futures as cf
+import os
+import shutil
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+BUILD = os.path.join(REPO, "build", "sdl")
+LIB = os.path.join(PKG, "libsdl_batcher.so")
+ARCH = os.environ.get("SDL_OFFLOAD_ARCH", "gfx950")
+
+SOURCES = ["tokenize_wordpiece.hip", "pipeline.hip", "assets.cpp", "sdl_batcher.cpp"]
+HEADERS = ["common.hpp", "device_util.hpp", "kernels.hpp", "assets.hpp", "json.hpp"]
+FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
+         "-I", os.path.join(REPO, "include"), "-I", CSRC]
+
+
+def _hipcc():
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if c and os.path.exists(c):
+            return c
+    raise RuntimeError("hipcc not found")
+
+
+def _newer(dst, srcs):
+    if not os.path.exists(dst):
+        return False
+    t = os.path.getmtime(dst)
+    return all(os.path.getmtime(s) <= t for s in srcs)
+
+
+def build(verbose=False, force=False, jobs=4):
+    os.makedirs(BUILD, exist_ok=True)
+    hipcc = _hipcc()
+    hdrs = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(REPO, "include", "sdl_batcher.h")]
+    objs, todo = [], []
+    for s in SOURCES:
+        src = os.path.join(CSRC, s)
+        obj = os.path.join(BUILD, s + ".o")
+        objs.append(obj)
+        if force or not _newer(obj, [src] + hdrs):
+            lang = ["-x", "hip"] if s.endswith(".hip") else []
+            todo.append([hipcc] + FLAGS + lang + ["-c", src, "-o", obj])
+
+    def run(cmd):
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        p = subprocess.run(cmd, capture_output=True, text=True)
+        if p.returncode != 0:
+            raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{p.stdout}\n{p.stderr}")
+        return p.stderr
+
+    with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+        for err in ex.map(run, todo):
+            if verbose and err:
+                print(err, file=sys.stderr)
+    if force or todo or not _newer(LIB, objs):
+        run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs + ["-ldl"])
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(verbose="-v" in sys.argv, force="-f" in sys.argv))

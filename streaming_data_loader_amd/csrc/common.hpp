@@ -1,0 +1,86 @@
+// common.hpp -- definitions shared by the host library and the gfx950 kernels.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace sdl {
+
+// ---- Unicode table classes (tools/make_unicode_tables.py) -----------------
+enum : uint32_t { UC_OTHER = 0, UC_WS = 1, UC_ISO = 2, UC_DEL = 3 };
+
+// ---- visible class of a char start, as BertPreTokenizer sees it ------------
+// NONE = invisible (continuation byte, DEL char, byte covered by an added token)
+enum : uint8_t { V_NONE = 0, V_WS = 1, V_ISO = 2, V_OTHER = 3, V_SPEC = 4 };
+
+// ---- tokenize workgroup geometry -----------------------------------------
+constexpr int TOK_THREADS = 256;
+constexpr int CHUNK = 4096;                       // text bytes owned by one workgroup
+constexpr int BYTES_PER_THREAD = CHUNK / TOK_THREADS;
+constexpr int HALO_L = 16;                        // look-back bytes staged in LDS
+constexpr int HALO_R = 240;                       // look-ahead bytes staged in LDS
+constexpr int WIN = HALO_L + CHUNK + HALO_R;      // 4352 bytes of text in LDS
+constexpr int STAGE = CHUNK + 128;                // token slots per chunk (>= tokens owned)
+constexpr int RB_CAP = 256;                       // record starts listed in LDS per window
+constexpr int MAX_WORD_CHARS = 100;               // WordPiece max_input_chars_per_word
+constexpr int MAX_WORD_BYTES = 4 * MAX_WORD_CHARS + 8;
+
+constexpr int MAX_SPECIAL = 8;
+constexpr int MAX_SPECIAL_LEN = 24;
+constexpr int MAX_FRAME = 4;
+
+constexpr uint64_t FNV_BASIS = 1469598103934665603ull;
+constexpr uint64_t FNV_PRIME = 1099511628211ull;
+
+// Vocabulary hash-table slot: 32 bytes, two 16-B loads.
+//   w0 tag (hash >> 32), w1 id (-1 = empty), w2 byte length of the literal
+//   piece (incl. "##"), w3 offset of the piece bytes in the pool,
+//   w4..w7 first 16 bytes of the piece inline.
+struct alignas(32) VSlot {
+    uint32_t tag;
+    int32_t id;
+    uint32_t len;
+    uint32_t pool_off;
+    uint8_t inl[16];
+};
+static_assert(sizeof(VSlot) == 32, "VSlot must be 32 bytes");
+
+// Everything a tokenize kernel needs, passed by value as a kernel argument.
+struct DevTok {
+    const uint16_t *upage;   // Unicode page table  [0x110000/128]
+    const uint32_t *uentry;  // Unicode blocks      [n_blocks*128]
+    const uint8_t *upool;    // normalized strings  (u8 nbytes, u8 nchars, bytes)
+    const VSlot *slots;      // vocab hash table
+    const uint8_t *vpool;    // vocab piece bytes
+    uint32_t slot_mask;
+    int32_t unk_id;
+    int32_t maxlen_first;    // longest non-"##" piece (bytes)
+    int32_t maxlen_cont;     // longest "##" piece without the prefix (bytes)
+    uint64_t h_cont;         // FNV state after hashing "##"
+    int32_t n_special;       // added tokens matched on the raw text
+    int32_t max_special_len;
+    uint32_t opener;         // first byte shared by every added token
+    int32_t special_id[MAX_SPECIAL];
+    uint8_t special_len[MAX_SPECIAL];
+    uint8_t special_bytes[MAX_SPECIAL][MAX_SPECIAL_LEN];
+};
+
+// Row assembly parameters (GenTokenizer + BertData/GptData/T5Data framing).
+struct RowParams {
+    int32_t task;            // SDL_TASK_*
+    int32_t B, S;
+    int32_t chunk;           // GenTokenizer.chunk
+    int32_t min_ids;         // gen_batcher.rs:74 filter on framed length
+    int32_t mask_length, mask_id;
+    int32_t label_width;
+    int32_t n_pre, n_post;   // framing ids around the tokenizer output
+    int32_t pre[MAX_FRAME];
+    int32_t post[MAX_FRAME];
+    uint64_t seed;
+    uint64_t first_record;
+};
+
+__host__ __device__ inline uint32_t ceil_div_u32(uint32_t a, uint32_t b) { return (a + b - 1) / b; }
+
+}  // namespace sdl

@@ -1,0 +1,68 @@
+// device_util.hpp -- wave64 / workgroup scan helpers for gfx950 kernels.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace sdl {
+
+__device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
+
+// Inclusive wave64 prefix sum (6 shuffle steps).
+__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t x) {
+    const int lane = lane_id();
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        uint32_t y = __shfl_up(x, d, 64);
+        if (lane >= d) x += y;
+    }
+    return x;
+}
+
+// Exclusive prefix sum over a workgroup of NT threads; *total = sum of all.
+// `scratch` needs NT/64 words.  Contains two barriers.
+template <int NT>
+__device__ __forceinline__ uint32_t block_excl_sum(uint32_t v, uint32_t *total, uint32_t *scratch) {
+    const int lane = lane_id(), wid = (int)(threadIdx.x >> 6);
+    uint32_t x = wave_incl_sum(v);
+    if (lane == 63) scratch[wid] = x;
+    __syncthreads();
+    uint32_t wbase = 0, tot = 0;
+#pragma unroll
+    for (int k = 0; k < NT / 64; ++k) {
+        uint32_t s = scratch[k];
+        wbase += k < wid ? s : 0u;
+        tot += s;
+    }
+    __syncthreads();
+    *total = tot;
+    return wbase + x - v;
+}
+
+// "Last set value wins" scan: a value with bit 8 set replaces the carry, 0 is
+// pass-through.  Returns the exclusive scan (0 if nothing before was set).
+__device__ __forceinline__ uint32_t last_set(uint32_t a, uint32_t b) { return (b & 0x100u) ? b : a; }
+
+template <int NT>
+__device__ __forceinline__ uint32_t block_excl_last_scan(uint32_t v, uint32_t *scratch) {
+    const int lane = lane_id(), wid = (int)(threadIdx.x >> 6);
+    uint32_t x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        uint32_t y = __shfl_up(x, d, 64);
+        if (lane >= d) x = last_set(y, x);
+    }
+    uint32_t ex = __shfl_up(x, 1, 64);
+    if (lane == 0) ex = 0;
+    if (lane == 63) scratch[wid] = x;
+    __syncthreads();
+    uint32_t carry = 0;
+#pragma unroll
+    for (int k = 0; k < NT / 64; ++k)
+        if (k < wid) carry = last_set(carry, scratch[k]);
+    __syncthreads();
+    return last_set(carry, ex);
+}
+
+}  // namespace sdl

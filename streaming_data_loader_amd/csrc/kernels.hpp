@@ -1,0 +1,40 @@
+// kernels.hpp -- host-side launchers of the gfx950 kernels (all asynchronous on `st`).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "common.hpp"
+
+namespace sdl {
+
+// tokenize_wordpiece.hip: text arena -> per-chunk token lists + boundary offsets
+hipError_t launch_wordpiece_chunks(const DevTok &T, const uint8_t *text, int64_t N, const uint64_t *off, int64_t R,
+                                   uint32_t *tokc, uint32_t *chunk_cnt, uint32_t *rec_local, hipStream_t st);
+
+// pipeline.hip
+// out[0..n) = exclusive prefix sum of in[0..n), out[n] = total.  tmp needs
+// scan_tmp_words(n) words.
+int64_t scan_tmp_words(int64_t n);
+hipError_t launch_exclusive_scan(const uint32_t *in, uint32_t *out, int64_t n, uint32_t *tmp, hipStream_t st);
+
+hipError_t launch_compact_tokens(const uint32_t *tokc, const uint32_t *chunk_cnt, const uint32_t *chunk_off,
+                                 int64_t n_chunks, uint32_t *tok, hipStream_t st);
+
+// per record: token offset, token count, rows it yields (gen_batcher.rs:69-94)
+hipError_t launch_records(const RowParams &P, const uint64_t *off, int64_t R, int64_t N, const uint32_t *chunk_off,
+                          int64_t n_chunks, const uint32_t *rec_local, uint32_t *rec_tok, uint32_t *rec_cnt,
+                          uint32_t *rec_rows, hipStream_t st);
+
+struct RowOut {
+    int32_t *input_ids, *attention_mask, *token_type_ids, *labels;
+    float *labels_f32;
+};
+
+// BertData::put_data + mask_batch for every row (models/bert_data.rs:40-89)
+hipError_t launch_rows(const RowParams &P, const uint32_t *tok, const uint32_t *rec_tok, const uint32_t *rec_cnt,
+                       const uint32_t *row_off, int64_t R, const uint32_t *d_rows, int64_t rows_cap, RowOut out,
+                       hipStream_t st);
+
+}  // namespace sdl

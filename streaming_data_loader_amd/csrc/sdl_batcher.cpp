@@ -1,0 +1,502 @@
+// sdl_batcher.cpp -- C ABI of the MI355X Batcher (include/sdl_batcher.h).
+//
+// Host side of the drop-in for the reference's Batcher stage:
+//   - sdl_batcher_create  ~ masking_runner::create_generator (masking_runner.rs:55-62)
+//                           -> get_tokenizer + GenTokenizer::new (gen_batcher.rs:23-41)
+//   - sdl_batcher_push    ~ Batcher::create_sync_batch (gen_batcher.rs:69-94)
+//   - sdl_batcher_flush   ~ Batcher::get_working_batch (gen_batcher.rs:96-98)
+// The per-record arithmetic runs on the GPU (sdl_process_device); this file
+// only moves bytes and keeps GenTokenizer's VecDeque<DataSet> of batches so the
+// emission cadence (at most one batch per create_sync_batch call, one flush at
+// end of stream) is the reference's.
+#include <dlfcn.h>
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <deque>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/sdl_batcher.h"
+#include "assets.hpp"
+#include "kernels.hpp"
+
+using namespace sdl;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string &msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                              \
+    do {                                                                                           \
+        hipError_t e_ = (expr);                                                                    \
+        if (e_ != hipSuccess) throw HipError(std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+struct HipError : std::runtime_error {
+    using std::runtime_error::runtime_error;
+};
+
+template <class T>
+struct DevBuf {
+    T *p = nullptr;
+    size_t cap = 0;  // elements
+    void ensure(size_t n) {
+        if (n <= cap && p) return;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        size_t want = std::max<size_t>(n + n / 4, 64);
+        HIP_TRY(hipMalloc(&p, want * sizeof(T)));
+        cap = want;
+    }
+    ~DevBuf() {
+        if (p) (void)hipFree(p);
+    }
+};
+
+template <class T>
+struct PinBuf {
+    T *p = nullptr;
+    size_t cap = 0;
+    void ensure(size_t n) {
+        if (n <= cap && p) return;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        size_t want = std::max<size_t>(n + n / 4, 64);
+        HIP_TRY(hipHostMalloc(&p, want * sizeof(T), hipHostMallocDefault));
+        cap = want;
+    }
+    ~PinBuf() {
+        if (p) (void)hipHostFree(p);
+    }
+};
+
+// One DataSet being filled (BertData / GptData): initial values from
+// BatchConfig::create_vector (batcher.rs:17-22) and BertData::new (bert_data.rs:27-38).
+struct HostBatch {
+    std::vector<int32_t> ids, am, tt, lab;
+    int rows = 0;
+    int B, S, LW;
+    HostBatch(int B_, int S_, int LW_, bool with_tt) : B(B_), S(S_), LW(LW_) {
+        ids.assign((size_t)B * S, 0);
+        am.assign((size_t)B * S, 1);
+        if (with_tt) tt.assign((size_t)B * S, 0);
+        lab.assign((size_t)B * LW, -100);
+    }
+};
+
+const char *kStageNames[] = {"wordpiece_chunks", "scan_chunks", "compact_tokens", "records", "scan_rows", "rows"};
+constexpr int kStages = 6;
+
+}  // namespace
+
+struct sdl_batcher {
+    sdl_config cfg{};
+    RowParams P{};
+    HostTokenizer tok;
+    DevTok dt{};
+    hipStream_t stream = nullptr;
+    int device = 0;
+
+    // device-resident tokenizer tables
+    DevBuf<uint16_t> d_upage;
+    DevBuf<uint32_t> d_uentry;
+    DevBuf<uint8_t> d_upool, d_vpool;
+    DevBuf<VSlot> d_slots;
+
+    // per-call workspace
+    DevBuf<uint32_t> tokc, chunk_cnt, chunk_off, rec_local, tok_ids, rec_tok, rec_cnt, rec_rows, row_off, scan_tmp;
+    DevBuf<int32_t> o_ids, o_am, o_tt, o_lab;
+    DevBuf<uint8_t> h2d_text;
+    DevBuf<uint64_t> h2d_off;
+
+    // host streaming path (GenTokenizer.store + emitted batches)
+    std::deque<HostBatch *> store;
+    std::deque<HostBatch *> outbox;
+    PinBuf<uint8_t> pin_text;
+    PinBuf<uint64_t> pin_off;
+    PinBuf<uint32_t> pin_u32;
+    PinBuf<int32_t> pin_rows;
+    uint64_t n_records = 0;
+
+    bool profiling = false;
+    hipEvent_t ev[kStages + 1] = {};
+    float stage_ms[kStages] = {};
+
+    ~sdl_batcher() {
+        for (auto *b : store) delete b;
+        for (auto *b : outbox) delete b;
+        for (auto &e : ev)
+            if (e) (void)hipEventDestroy(e);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+
+    HostBatch *new_batch() const {
+        return new HostBatch(P.B, P.S, P.label_width, P.task == SDL_TASK_MLM || P.task == SDL_TASK_MULTI_LABEL);
+    }
+
+    int64_t rows_capacity(int64_t N, int64_t R) const {
+        // rows <= sum_r ceil((ids_r + frame) / S) with ids_r <= bytes_r
+        const int64_t F = P.n_pre + P.n_post;
+        int64_t cap = P.chunk ? (N + R * (F + P.S - 1)) / P.S + 1 : R;
+        return (cap + P.B - 1) / P.B * P.B;
+    }
+
+    void run_device(const uint8_t *d_text, int64_t N, const uint64_t *d_off, int64_t R, uint64_t first_record,
+                    hipStream_t st) {
+        const int64_t n_chunks = (N + CHUNK - 1) / CHUNK;
+        const int64_t rows_cap = rows_capacity(N, R);
+        tokc.ensure((size_t)std::max<int64_t>(n_chunks, 1) * STAGE);
+        chunk_cnt.ensure((size_t)n_chunks + 1);
+        chunk_off.ensure((size_t)n_chunks + 1);
+        rec_local.ensure((size_t)R + 1);
+        tok_ids.ensure((size_t)N + 1);
+        rec_tok.ensure((size_t)R + 1);
+        rec_cnt.ensure((size_t)R + 1);
+        rec_rows.ensure((size_t)R + 1);
+        row_off.ensure((size_t)R + 1);
+        scan_tmp.ensure((size_t)std::max(scan_tmp_words(n_chunks), scan_tmp_words(R)) + 1);
+        const size_t plane = (size_t)std::max<int64_t>(rows_cap, 1) * P.S;
+        o_ids.ensure(plane);
+        o_am.ensure(plane);
+        if (P.task == SDL_TASK_MLM || P.task == SDL_TASK_MULTI_LABEL) o_tt.ensure(plane);
+        o_lab.ensure((size_t)std::max<int64_t>(rows_cap, 1) * P.label_width);
+
+        RowParams p = P;
+        p.first_record = first_record;
+        auto mark = [&](int i) {
+            if (profiling) HIP_TRY(hipEventRecord(ev[i], st));
+        };
+        mark(0);
+        HIP_TRY(launch_wordpiece_chunks(dt, d_text, N, d_off, R, tokc.p, chunk_cnt.p, rec_local.p, st));
+        mark(1);
+        HIP_TRY(launch_exclusive_scan(chunk_cnt.p, chunk_off.p, n_chunks, scan_tmp.p, st));
+        mark(2);
+        HIP_TRY(launch_compact_tokens(tokc.p, chunk_cnt.p, chunk_off.p, n_chunks, tok_ids.p, st));
+        mark(3);
+        HIP_TRY(launch_records(p, d_off, R, N, chunk_off.p, n_chunks, rec_local.p, rec_tok.p, rec_cnt.p, rec_rows.p,
+                               st));
+        mark(4);
+        HIP_TRY(launch_exclusive_scan(rec_rows.p, row_off.p, R, scan_tmp.p, st));
+        mark(5);
+        RowOut out{o_ids.p, o_am.p, (P.task == SDL_TASK_MLM || P.task == SDL_TASK_MULTI_LABEL) ? o_tt.p : nullptr,
+                   o_lab.p, nullptr};
+        HIP_TRY(launch_rows(p, tok_ids.p, rec_tok.p, rec_cnt.p, row_off.p, R, row_off.p + R, rows_cap, out, st));
+        mark(6);
+        last_rows_cap = rows_cap;
+        last_R = R;
+    }
+    int64_t last_rows_cap = 0, last_R = 0;
+
+    // H2D a host arena, run the device path, bring back the rows; then play
+    // GenTokenizer's queue over the per-record row counts.
+    void process_host(const uint8_t *arena, const uint64_t *offsets, int64_t R, std::vector<int> *emitted_per_record) {
+        const int64_t N = (int64_t)offsets[R];
+        pin_text.ensure((size_t)N + 16);
+        pin_off.ensure((size_t)R + 1);
+        std::memcpy(pin_text.p, arena, (size_t)N);
+        std::memcpy(pin_off.p, offsets, sizeof(uint64_t) * (size_t)(R + 1));
+        h2d_text.ensure((size_t)N + 16);
+        h2d_off.ensure((size_t)R + 1);
+        HIP_TRY(hipMemcpyAsync(h2d_text.p, pin_text.p, (size_t)N, hipMemcpyHostToDevice, stream));
+        HIP_TRY(hipMemcpyAsync(h2d_off.p, pin_off.p, sizeof(uint64_t) * (size_t)(R + 1), hipMemcpyHostToDevice, stream));
+        run_device(h2d_text.p, N, h2d_off.p, R, cfg.first_record + n_records, stream);
+        pin_u32.ensure((size_t)R + 1);
+        HIP_TRY(hipMemcpyAsync(pin_u32.p, row_off.p, sizeof(uint32_t) * (size_t)(R + 1), hipMemcpyDeviceToHost, stream));
+        HIP_TRY(hipStreamSynchronize(stream));
+        const uint32_t G = pin_u32.p[R];
+        const size_t S = (size_t)P.S, LW = (size_t)P.label_width;
+        const bool with_tt = P.task == SDL_TASK_MLM || P.task == SDL_TASK_MULTI_LABEL;
+        const size_t planes = with_tt ? 3 : 2;
+        pin_rows.ensure((size_t)G * (planes * S + LW) + 1);
+        int32_t *h_ids = pin_rows.p, *h_am = h_ids + (size_t)G * S, *h_tt = h_am + (size_t)G * S;
+        int32_t *h_lab = h_am + (size_t)G * S * (planes - 1);
+        if (G) {
+            HIP_TRY(hipMemcpyAsync(h_ids, o_ids.p, sizeof(int32_t) * G * S, hipMemcpyDeviceToHost, stream));
+            HIP_TRY(hipMemcpyAsync(h_am, o_am.p, sizeof(int32_t) * G * S, hipMemcpyDeviceToHost, stream));
+            if (with_tt) HIP_TRY(hipMemcpyAsync(h_tt, o_tt.p, sizeof(int32_t) * G * S, hipMemcpyDeviceToHost, stream));
+            HIP_TRY(hipMemcpyAsync(h_lab, o_lab.p, sizeof(int32_t) * G * LW, hipMemcpyDeviceToHost, stream));
+            HIP_TRY(hipStreamSynchronize(stream));
+        }
+        // GenTokenizer::create_sync_batch per record (gen_batcher.rs:69-94)
+        for (int64_t r = 0; r < R; ++r) {
+            const uint32_t g0 = pin_u32.p[r], g1 = pin_u32.p[r + 1];
+            for (uint32_t g = g0; g < g1; ++g) {  // handle_internal_batch per chunk
+                HostBatch *b = store.back();
+                const size_t dst = (size_t)b->rows;
+                std::memcpy(&b->ids[dst * S], h_ids + (size_t)g * S, S * 4);
+                std::memcpy(&b->am[dst * S], h_am + (size_t)g * S, S * 4);
+                if (with_tt) std::memcpy(&b->tt[dst * S], h_tt + (size_t)g * S, S * 4);
+                std::memcpy(&b->lab[dst * LW], h_lab + (size_t)g * LW, LW * 4);
+                b->rows++;
+                if (b->rows == P.B) store.push_back(new_batch());
+            }
+            int emitted = 0;
+            if (!store.empty() && store.front()->rows == P.B) {  // at most one batch per call
+                outbox.push_back(store.front());
+                store.pop_front();
+                emitted = 1;
+            }
+            if (emitted_per_record) emitted_per_record->push_back(emitted);
+        }
+        n_records += (uint64_t)R;
+    }
+};
+
+namespace {
+
+void fill_batch(const sdl_batcher *h, HostBatch *b, sdl_batch *out) {
+    std::memset(out, 0, sizeof(*out));
+    out->rows = b->rows;
+    out->batch_size = b->B;
+    out->sequence_length = b->S;
+    out->label_width = b->LW;
+    out->input_ids = b->ids.data();
+    out->attention_mask = b->am.data();
+    out->token_type_ids = b->tt.empty() ? nullptr : b->tt.data();
+    out->labels = b->lab.data();
+    out->owner_ = b;
+    (void)h;
+}
+
+std::string default_data_dir() {
+    Dl_info info;
+    if (dladdr((void *)&default_data_dir, &info) && info.dli_fname) {
+        std::string p = info.dli_fname;
+        size_t s = p.rfind('/');
+        return (s == std::string::npos ? std::string(".") : p.substr(0, s)) + "/data";
+    }
+    return "data";
+}
+
+}  // namespace
+
+extern "C" {
+
+int sdl_abi_version(void) { return SDL_ABI_VERSION; }
+const char *sdl_last_error(void) { return g_err.c_str(); }
+
+void sdl_config_default(sdl_config *c, int32_t task) {
+    std::memset(c, 0, sizeof(*c));
+    c->task = task;
+    c->batch_size = 4096;  // masking_cases.rs:43
+    c->sequence_length = 128;
+    c->chunk = task == SDL_TASK_MULTI_LABEL ? 0 : 1;
+    c->min_ids = task == SDL_TASK_MULTI_LABEL ? 0 : 64;
+    c->mask_length = (int32_t)((float)c->sequence_length * 0.15f);  // masking_cases.rs:34-36
+    c->mask_id = 103;
+    c->number_labels = 9;
+    c->avg_span_gap = 16.0;
+    c->avg_span_size = 2.0;
+    c->seed = 0;
+    c->first_record = 0;
+    c->device = 0;
+}
+
+int sdl_batcher_create(const sdl_config *cfg, const char *tokenizer_path, const char *data_dir, sdl_batcher **out) {
+    if (!cfg || !tokenizer_path || !out) return fail(SDL_ERR_ARG, "null argument");
+    *out = nullptr;
+    if (cfg->task != SDL_TASK_MLM && cfg->task != SDL_TASK_CLM)
+        return fail(SDL_ERR_UNSUPPORTED, "task not implemented in this build (mlm, clm)");
+    if (cfg->batch_size <= 0 || cfg->sequence_length <= 0 || cfg->sequence_length > 2048)
+        return fail(SDL_ERR_ARG, "batch_size must be > 0 and 0 < sequence_length <= 2048");
+    if (cfg->task == SDL_TASK_MLM && (cfg->mask_length < 0 || cfg->mask_length > cfg->sequence_length))
+        return fail(SDL_ERR_ARG, "mask_length must be in [0, sequence_length]");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+        return fail(SDL_ERR_NODEV, "no HIP device visible: the Batcher runs only on the GPU (no CPU fallback)");
+    if (cfg->device < 0 || cfg->device >= ndev) return fail(SDL_ERR_ARG, "device ordinal out of range");
+    std::unique_ptr<sdl_batcher> h(new sdl_batcher());
+    try {
+        h->cfg = *cfg;
+        h->device = cfg->device;
+        load_tokenizer(tokenizer_path, data_dir ? std::string(data_dir) : default_data_dir(), h->tok);
+        HIP_TRY(hipSetDevice(h->device));
+        HIP_TRY(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+        for (auto &e : h->ev) HIP_TRY(hipEventCreate(&e));
+        auto &t = h->tok;
+        h->d_upage.ensure(t.upage.size());
+        h->d_uentry.ensure(t.uentry.size());
+        h->d_upool.ensure(t.upool.size());
+        h->d_slots.ensure(t.slots.size());
+        h->d_vpool.ensure(t.vpool.size());
+        HIP_TRY(hipMemcpy(h->d_upage.p, t.upage.data(), t.upage.size() * 2, hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(h->d_uentry.p, t.uentry.data(), t.uentry.size() * 4, hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(h->d_upool.p, t.upool.data(), t.upool.size(), hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(h->d_slots.p, t.slots.data(), t.slots.size() * sizeof(VSlot), hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(h->d_vpool.p, t.vpool.data(), t.vpool.size(), hipMemcpyHostToDevice));
+        DevTok &d = h->dt;
+        d.upage = h->d_upage.p;
+        d.uentry = h->d_uentry.p;
+        d.upool = h->d_upool.p;
+        d.slots = h->d_slots.p;
+        d.vpool = h->d_vpool.p;
+        d.slot_mask = t.slot_mask;
+        d.unk_id = t.unk_id;
+        d.maxlen_first = t.maxlen_first;
+        d.maxlen_cont = t.maxlen_cont;
+        d.h_cont = fnv1a((const uint8_t *)"##", 2);
+        d.n_special = (int)t.added.size();
+        d.max_special_len = t.max_special_len;
+        d.opener = t.opener;
+        for (size_t i = 0; i < t.added.size(); ++i) {
+            d.special_id[i] = t.added[i].second;
+            d.special_len[i] = (uint8_t)t.added[i].first.size();
+            std::memcpy(d.special_bytes[i], t.added[i].first.data(), t.added[i].first.size());
+        }
+        RowParams &P = h->P;
+        P.task = cfg->task;
+        P.B = cfg->batch_size;
+        P.S = cfg->sequence_length;
+        P.chunk = cfg->chunk;
+        P.min_ids = cfg->min_ids;
+        P.mask_length = cfg->mask_length;
+        P.mask_id = cfg->mask_id;
+        P.label_width = cfg->sequence_length;
+        P.seed = cfg->seed;
+        // encode_mask framing (tokenizer_wrapper.rs:107-116): [CLS] + template([CLS] $A [SEP]) + [SEP] [SEP]
+        P.n_pre = 2;
+        P.pre[0] = t.cls_id;
+        P.pre[1] = t.tpl_cls;
+        P.n_post = 3;
+        P.post[0] = t.tpl_sep;
+        P.post[1] = t.sep_id;
+        P.post[2] = t.sep_id;
+        h->store.push_back(h->new_batch());  // GenTokenizer::new: first DataSet
+    } catch (HipError &e) {
+        return fail(SDL_ERR_HIP, e.what());
+    } catch (std::exception &e) {
+        return fail(SDL_ERR_IO, e.what());
+    }
+    *out = h.release();
+    return SDL_OK;
+}
+
+void sdl_batcher_destroy(sdl_batcher *h) { delete h; }
+
+int sdl_batcher_push(sdl_batcher *h, const uint8_t *utf8, size_t len, const uint32_t *labels, size_t n_labels,
+                     sdl_batch *out) {
+    (void)labels;
+    (void)n_labels;
+    if (!h || (!utf8 && len)) return fail(SDL_ERR_ARG, "null argument");
+    if (len >= (1ull << 32)) return fail(SDL_ERR_CAPACITY, "record too large");
+    try {
+        uint64_t offs[2] = {0, (uint64_t)len};
+        const size_t before = h->outbox.size();
+        h->process_host(utf8 ? utf8 : (const uint8_t *)"", offs, 1, nullptr);
+        if (h->outbox.size() > before) {
+            HostBatch *b = h->outbox.back();
+            h->outbox.pop_back();
+            if (out) fill_batch(h, b, out);
+            else delete b;
+            return 1;
+        }
+        return 0;
+    } catch (HipError &e) {
+        return fail(SDL_ERR_HIP, e.what());
+    } catch (std::exception &e) {
+        return fail(SDL_ERR_ARG, e.what());
+    }
+}
+
+int sdl_batcher_push_many(sdl_batcher *h, const uint8_t *arena, const uint64_t *offsets, size_t n_records,
+                          const uint32_t *labels, const uint64_t *label_offsets, size_t *n_emitted) {
+    (void)labels;
+    (void)label_offsets;
+    if (!h || !offsets || (!arena && n_records && offsets[n_records])) return fail(SDL_ERR_ARG, "null argument");
+    if (offsets[0] != 0) return fail(SDL_ERR_ARG, "offsets[0] must be 0");
+    for (size_t r = 0; r < n_records; ++r)
+        if (offsets[r + 1] < offsets[r]) return fail(SDL_ERR_ARG, "offsets must be non-decreasing");
+    if (offsets[n_records] >= (1ull << 32)) return fail(SDL_ERR_CAPACITY, "arena must be < 4 GiB per call");
+    try {
+        const size_t before = h->outbox.size();
+        if (n_records) h->process_host(arena, offsets, (int64_t)n_records, nullptr);
+        if (n_emitted) *n_emitted = h->outbox.size() - before;
+        return SDL_OK;
+    } catch (HipError &e) {
+        return fail(SDL_ERR_HIP, e.what());
+    } catch (std::exception &e) {
+        return fail(SDL_ERR_ARG, e.what());
+    }
+}
+
+int sdl_batcher_next(sdl_batcher *h, sdl_batch *out) {
+    if (!h || !out) return fail(SDL_ERR_ARG, "null argument");
+    if (h->outbox.empty()) return 0;
+    HostBatch *b = h->outbox.front();
+    h->outbox.pop_front();
+    fill_batch(h, b, out);
+    return 1;
+}
+
+int sdl_batcher_flush(sdl_batcher *h, sdl_batch *out) {
+    if (!h || !out) return fail(SDL_ERR_ARG, "null argument");
+    if (h->store.empty()) return 0;  // get_working_batch = store.pop_front()
+    HostBatch *b = h->store.front();
+    h->store.pop_front();
+    fill_batch(h, b, out);
+    return 1;
+}
+
+void sdl_batch_release(sdl_batch *b) {
+    if (!b || !b->owner_) return;
+    delete static_cast<HostBatch *>(b->owner_);
+    std::memset(b, 0, sizeof(*b));
+}
+
+int sdl_process_device(sdl_batcher *h, const uint8_t *d_text, uint64_t text_len, const uint64_t *d_offsets,
+                       uint64_t n_records, uint64_t first_record, void *stream, sdl_device_rows *out) {
+    if (!h || !out || !d_offsets || (!d_text && text_len)) return fail(SDL_ERR_ARG, "null argument");
+    if (text_len >= (1ull << 32)) return fail(SDL_ERR_CAPACITY, "arena must be < 4 GiB per call");
+    if (((uintptr_t)d_text & 15u) != 0) return fail(SDL_ERR_ARG, "d_text must be 16-byte aligned");
+    try {
+        hipStream_t st = stream ? (hipStream_t)stream : h->stream;
+        h->run_device(d_text, (int64_t)text_len, d_offsets, (int64_t)n_records, first_record, st);
+        std::memset(out, 0, sizeof(*out));
+        out->input_ids = h->o_ids.p;
+        out->attention_mask = h->o_am.p;
+        out->token_type_ids = (h->P.task == SDL_TASK_MLM || h->P.task == SDL_TASK_MULTI_LABEL) ? h->o_tt.p : nullptr;
+        out->labels = h->o_lab.p;
+        out->d_rows = h->row_off.p + n_records;
+        out->d_record_rows = h->rec_rows.p;
+        out->d_tokens = h->chunk_off.p + (text_len + CHUNK - 1) / CHUNK;
+        out->rows_capacity = (uint64_t)h->last_rows_cap;
+        out->label_width = h->P.label_width;
+        return SDL_OK;
+    } catch (HipError &e) {
+        return fail(SDL_ERR_HIP, e.what());
+    } catch (std::exception &e) {
+        return fail(SDL_ERR_ARG, e.what());
+    }
+}
+
+int sdl_set_profiling(sdl_batcher *h, int enable) {
+    if (!h) return fail(SDL_ERR_ARG, "null argument");
+    h->profiling = enable != 0;
+    return SDL_OK;
+}
+
+int sdl_stage_times(sdl_batcher *h, const char **names, float *ms, int cap) {
+    if (!h) return fail(SDL_ERR_ARG, "null argument");
+    if (!h->profiling) return fail(SDL_ERR_STATE, "profiling not enabled");
+    if (hipEventSynchronize(h->ev[kStages]) != hipSuccess) return fail(SDL_ERR_HIP, "event sync failed");
+    int n = std::min(cap, kStages);
+    for (int i = 0; i < n; ++i) {
+        float t = 0.f;
+        if (hipEventElapsedTime(&t, h->ev[i], h->ev[i + 1]) != hipSuccess) return fail(SDL_ERR_HIP, "event time");
+        if (names) names[i] = kStageNames[i];
+        if (ms) ms[i] = t;
+    }
+    return n;
+}
+
+}  // extern "C"

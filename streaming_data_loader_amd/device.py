@@ -1,0 +1,105 @@
+"""Device-resident bulk path: a text arena already in HBM -> packed [rows, S]
+planes in HBM, through sdl_process_device (the measured hot path).
+
+PyTorch is used only to hold device memory and streams.
+"""
+import ctypes
+
+import numpy as np
+
+from . import native
+
+
+class DeviceResult:
+    def __init__(self, rows_struct, n_records, S):
+        self.r = rows_struct
+        self.n_records = n_records
+        self.S = S
+
+    def rows(self):
+        v = np.zeros(1, np.uint32)
+        native.d2h(v, self.r.d_rows, 4)
+        return int(v[0])
+
+    def tokens(self):
+        v = np.zeros(1, np.uint32)
+        native.d2h(v, self.r.d_tokens, 4)
+        return int(v[0])
+
+    def record_rows(self):
+        v = np.zeros(self.n_records, np.uint32)
+        native.d2h(v, self.r.d_record_rows, 4 * self.n_records)
+        return v
+
+    def planes(self, n_rows=None):
+        """(input_ids, attention_mask, token_type_ids|None, labels) as numpy [n, S]."""
+        n = self.rows() if n_rows is None else n_rows
+        S, LW = self.S, self.r.label_width
+
+        def get(ptr, w):
+            a = np.zeros((n, w), np.int32)
+            if ptr:
+                native.d2h(a, ptr, a.nbytes)
+                return a
+            return None
+
+        return (get(self.r.input_ids, S), get(self.r.attention_mask, S), get(self.r.token_type_ids, S),
+                get(self.r.labels, LW))
+
+
+class DeviceBatcher:
+    """Owns one sdl_batcher handle used through sdl_process_device."""
+
+    def __init__(self, task=native.SDL_TASK_MLM, batch_size=256, sequence_length=512, mask_length=None,
+                 mask_id=103, seed=0, device=0, tokenizer=native.BERT_PROXY_TOKENIZER, chunk=True, min_ids=None):
+        L = native.load()
+        c = native.default_config(task)
+        c.batch_size, c.sequence_length = batch_size, sequence_length
+        c.mask_length = int(np.float32(sequence_length) * np.float32(0.15)) if mask_length is None else mask_length
+        c.mask_id, c.seed, c.device, c.chunk = mask_id, seed, device, 1 if chunk else 0
+        if min_ids is not None:
+            c.min_ids = min_ids
+        self.cfg = c
+        h = ctypes.c_void_p()
+        native.check(L.sdl_batcher_create(ctypes.byref(c), tokenizer.encode(), native.DATA_DIR.encode(),
+                                          ctypes.byref(h)))
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            native.load().sdl_batcher_destroy(self._h)
+            self._h = None
+
+    __del__ = close
+
+    def set_profiling(self, on=True):
+        native.check(native.load().sdl_set_profiling(self._h, 1 if on else 0))
+
+    def stage_times(self):
+        names = (ctypes.c_char_p * 16)()
+        ms = (ctypes.c_float * 16)()
+        n = native.check(native.load().sdl_stage_times(self._h, names, ms, 16))
+        return {names[i].decode(): float(ms[i]) for i in range(n)}
+
+    def process(self, text_ptr, text_len, offsets_ptr, n_records, first_record=0, stream=0):
+        """Pointers are device addresses (ints), e.g. tensor.data_ptr()."""
+        out = native.DeviceRows()
+        native.check(native.load().sdl_process_device(self._h, ctypes.c_void_p(text_ptr), text_len,
+                                                      ctypes.c_void_p(offsets_ptr), n_records, first_record,
+                                                      ctypes.c_void_p(stream or None), ctypes.byref(out)))
+        return DeviceResult(out, n_records, self.cfg.sequence_length)
+
+    def process_tensors(self, text, offsets, first_record=0, stream=None):
+        """text: uint8 cuda tensor; offsets: int64 cuda tensor of n_records+1 entries."""
+        s = stream.cuda_stream if stream is not None else 0
+        return self.process(text.data_ptr(), text.numel(), offsets.data_ptr(), offsets.numel() - 1, first_record, s)
+
+
+def arena_from_texts(texts):
+    """Host arena (uint8, padded) + uint64 offsets for a list of str/bytes."""
+    blobs = [t.encode("utf-8") if isinstance(t, str) else bytes(t) for t in texts]
+    offs = np.zeros(len(blobs) + 1, np.uint64)
+    if blobs:
+        np.cumsum([len(x) for x in blobs], out=offs[1:])
+    arena = np.frombuffer(b"".join(blobs), np.uint8) if blobs else np.zeros(0, np.uint8)
+    return arena, offs

@@ -1,0 +1,136 @@
+"""ctypes binding of libsdl_batcher.so (include/sdl_batcher.h).
+
+The product path is the HIP library only: if it is missing, or no GPU is
+visible, these calls raise -- there is no CPU fallback.
+"""
+import ctypes
+import os
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG, "libsdl_batcher.so")
+DATA_DIR = os.path.join(PKG, "data")
+ASSETS = os.path.join(PKG, "assets")
+BERT_PROXY_TOKENIZER = os.path.join(ASSETS, "bert_proxy", "tokenizer.json")
+
+SDL_TASK_MLM, SDL_TASK_CLM, SDL_TASK_SPAN, SDL_TASK_MULTI_LABEL = 0, 1, 2, 3
+
+# every symbol include/sdl_batcher.h declares
+EXPORTS = [
+    "sdl_config_default", "sdl_batcher_create", "sdl_batcher_destroy", "sdl_batcher_push",
+    "sdl_batcher_push_many", "sdl_batcher_next", "sdl_batcher_flush", "sdl_batch_release",
+    "sdl_process_device", "sdl_set_profiling", "sdl_stage_times", "sdl_last_error", "sdl_abi_version",
+]
+
+
+class SDLError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"sdl error {code}: {msg}")
+        self.code = code
+
+
+class Config(ctypes.Structure):
+    _fields_ = [
+        ("task", ctypes.c_int32), ("batch_size", ctypes.c_int32), ("sequence_length", ctypes.c_int32),
+        ("chunk", ctypes.c_int32), ("min_ids", ctypes.c_int32), ("mask_length", ctypes.c_int32),
+        ("mask_id", ctypes.c_int32), ("number_labels", ctypes.c_int32),
+        ("avg_span_gap", ctypes.c_double), ("avg_span_size", ctypes.c_double),
+        ("seed", ctypes.c_uint64), ("first_record", ctypes.c_uint64),
+        ("device", ctypes.c_int32), ("reserved", ctypes.c_int32 * 7),
+    ]
+
+
+class Batch(ctypes.Structure):
+    _fields_ = [
+        ("rows", ctypes.c_int32), ("batch_size", ctypes.c_int32), ("sequence_length", ctypes.c_int32),
+        ("label_width", ctypes.c_int32),
+        ("input_ids", ctypes.POINTER(ctypes.c_int32)), ("attention_mask", ctypes.POINTER(ctypes.c_int32)),
+        ("token_type_ids", ctypes.POINTER(ctypes.c_int32)), ("labels", ctypes.POINTER(ctypes.c_int32)),
+        ("labels_f32", ctypes.POINTER(ctypes.c_float)), ("owner_", ctypes.c_void_p),
+    ]
+
+
+class DeviceRows(ctypes.Structure):
+    _fields_ = [
+        ("input_ids", ctypes.c_void_p), ("attention_mask", ctypes.c_void_p), ("token_type_ids", ctypes.c_void_p),
+        ("labels", ctypes.c_void_p), ("labels_f32", ctypes.c_void_p), ("d_rows", ctypes.c_void_p),
+        ("d_record_rows", ctypes.c_void_p), ("d_tokens", ctypes.c_void_p),
+        ("rows_capacity", ctypes.c_uint64), ("label_width", ctypes.c_int32),
+    ]
+
+
+_lib = None
+
+
+def load(path=LIB_PATH):
+    """Loads the native library (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise SDLError(-4, f"{path} missing: run `python -m streaming_data_loader_amd.build` (no CPU fallback)")
+    L = ctypes.CDLL(path)
+    vp, sz, u64, i32, i64 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_int32, ctypes.c_int
+    L.sdl_config_default.argtypes = [ctypes.POINTER(Config), i32]
+    L.sdl_config_default.restype = None
+    L.sdl_batcher_create.argtypes = [ctypes.POINTER(Config), ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(vp)]
+    L.sdl_batcher_destroy.argtypes = [vp]
+    L.sdl_batcher_destroy.restype = None
+    L.sdl_batcher_push.argtypes = [vp, ctypes.c_char_p, sz, vp, sz, ctypes.POINTER(Batch)]
+    L.sdl_batcher_push_many.argtypes = [vp, vp, vp, sz, vp, vp, ctypes.POINTER(sz)]
+    L.sdl_batcher_next.argtypes = [vp, ctypes.POINTER(Batch)]
+    L.sdl_batcher_flush.argtypes = [vp, ctypes.POINTER(Batch)]
+    L.sdl_batch_release.argtypes = [ctypes.POINTER(Batch)]
+    L.sdl_batch_release.restype = None
+    L.sdl_process_device.argtypes = [vp, vp, u64, vp, u64, u64, vp, ctypes.POINTER(DeviceRows)]
+    L.sdl_set_profiling.argtypes = [vp, i64]
+    L.sdl_stage_times.argtypes = [vp, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_float), i64]
+    L.sdl_last_error.restype = ctypes.c_char_p
+    L.sdl_last_error.argtypes = []
+    L.sdl_abi_version.restype = i64
+    for name in ("sdl_batcher_create", "sdl_batcher_push", "sdl_batcher_push_many", "sdl_batcher_next",
+                 "sdl_batcher_flush", "sdl_process_device", "sdl_set_profiling", "sdl_stage_times"):
+        getattr(L, name).restype = i64
+    _lib = L
+    return L
+
+
+def check(rc):
+    if rc < 0:
+        raise SDLError(rc, load().sdl_last_error().decode(errors="replace"))
+    return rc
+
+
+def default_config(task):
+    c = Config()
+    load().sdl_config_default(ctypes.byref(c), task)
+    return c
+
+
+# ---- raw HIP memcpy for tests/bench (device pointers produced by the library)
+_hip = None
+
+
+def hip():
+    global _hip
+    if _hip is None:
+        for name in ("libamdhip64.so", "/opt/rocm/lib/libamdhip64.so"):
+            try:
+                _hip = ctypes.CDLL(name)
+                break
+            except OSError:
+                continue
+        if _hip is None:
+            raise SDLError(-5, "libamdhip64.so not found")
+        _hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+        _hip.hipMemcpy.restype = ctypes.c_int
+    return _hip
+
+
+def d2h(dst_numpy, src_ptr, nbytes):
+    """hipMemcpy device -> host into a numpy array."""
+    if nbytes == 0:
+        return dst_numpy
+    rc = hip().hipMemcpy(dst_numpy.ctypes.data, ctypes.c_void_p(src_ptr), nbytes, 2)
+    if rc != 0:
+        raise SDLError(-3, f"hipMemcpy D2H failed ({rc})")
+    return dst_numpy

@@ -1,0 +1,61 @@
+"""The C-ABI library builds for gfx950, loads, and exports every symbol the
+header declares; config defaults mirror the reference's masking cases.  No
+compute calls here (no GPU in the build container)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from streaming_data_loader_amd import native
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_functions():
+    src = open(os.path.join(REPO, "include", "sdl_batcher.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(sdl_[a-z_0-9]+)\s*\(", src)))
+
+
+def test_header_and_exports_agree(native_lib):
+    decl = header_functions()
+    assert sorted(native.EXPORTS) == decl
+    for name in decl:
+        assert hasattr(native_lib, name), name
+
+
+def test_abi_version(native_lib):
+    assert native_lib.sdl_abi_version() == 1
+
+
+def test_config_defaults_mirror_masking_cases(native_lib):
+    c = native.default_config(native.SDL_TASK_MLM)
+    assert (c.batch_size, c.sequence_length, c.chunk, c.min_ids) == (4096, 128, 1, 64)  # masking_cases.rs:43
+    assert c.mask_length == 19 and c.mask_id == 103  # (128 as f32 * 0.15) as usize; mask 103
+    assert (c.avg_span_gap, c.avg_span_size) == (16.0, 2.0)
+    m = native.default_config(native.SDL_TASK_MULTI_LABEL)
+    assert (m.chunk, m.min_ids, m.number_labels) == (0, 0, 9)
+
+
+def test_struct_layouts():
+    assert ctypes.sizeof(native.Config) == 96  # 8 x i32, 2 x f64, 2 x u64, i32 + 7 reserved
+    assert ctypes.sizeof(native.Batch) == 4 * 4 + 8 * 6
+
+
+def test_create_without_gpu_fails_loudly(native_lib):
+    """The product path never falls back to the CPU."""
+    torch = pytest.importorskip("torch")
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is visible")
+    c = native.default_config(native.SDL_TASK_MLM)
+    h = ctypes.c_void_p()
+    rc = native_lib.sdl_batcher_create(ctypes.byref(c), native.BERT_PROXY_TOKENIZER.encode(),
+                                       native.DATA_DIR.encode(), ctypes.byref(h))
+    assert rc == -5 and not h.value
+    assert b"no HIP device" in native_lib.sdl_last_error()
+
+
+def test_kernels_are_gfx950_code_objects(native_lib):
+    data = open(native.LIB_PATH, "rb").read()
+    assert b"gfx950" in data

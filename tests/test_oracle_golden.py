@@ -1,0 +1,105 @@
+"""Pins the CPU oracle (oracle/sdl_oracle.c) before it is trusted as the checker.
+
+- token ids: against HF `tokenizers` (0.22.2 here; the reference pins the same
+  project's crate at 0.13.1, rust/Cargo.lock) on the reference's own fixture
+  records (data/test.json.gz, used by masking_cases.rs:13-21), edge cases and
+  seeded random Unicode strings -- tests/golden/bert_ids.json;
+- MLM batches: against an independent Python restatement of GenTokenizer +
+  BertData under the RNG contract at the reference CPU config (S=128, B=8) --
+  tests/golden/mlm_s128_b8.npz;
+- Philox4x32-10 known-answer vectors (Random123 kat_vectors).
+"""
+import os
+import random
+import struct
+
+import numpy as np
+import pytest
+
+import oracle_lib
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def test_oracle_matches_tokenizers_goldens(oracle_tok, bert_goldens):
+    assert bert_goldens["n_fixture_records"] == 50
+    bad = [c["text"][:60] for c in bert_goldens["cases"] if oracle_tok.encode(c["text"]) != c["ids"]]
+    assert not bad, f"{len(bad)} mismatches, e.g. {bad[:3]}"
+
+
+def test_oracle_special_ids_layout(oracle_tok):
+    # [CLS] ... [SEP] template; literal added tokens map to their ids
+    assert oracle_tok.encode("") == [101, 102]
+    assert oracle_tok.encode("[SEP]") == [101, 102, 102]
+    assert oracle_tok.encode("[MASK][PAD]") == [101, 103, 0, 102]
+    assert oracle_tok.encode("x" * 101) == [101, 100, 102]
+
+
+def test_oracle_mlm_batches_match_golden(oracle_tok, records):
+    g = np.load(os.path.join(GOLDEN, "mlm_s128_b8.npz"))
+    ob = oracle_lib.OracleBatcher(oracle_tok, 8, 128, 19, 103, seed=1234)
+    got = [r for r in (ob.push(t) for t in records) if r is not None]
+    got.append(ob.flush())
+    assert len(got) == int(g["n_batches"])
+    for i, (planes, rows) in enumerate(got):
+        assert rows == int(g[f"b{i}_rows"])
+        for j, k in enumerate(("input_ids", "attention_mask", "token_type_ids", "labels")):
+            np.testing.assert_array_equal(planes[j], g[f"b{i}_{k}"], err_msg=f"batch {i} {k}")
+
+
+def test_philox_known_answers():
+    L = oracle_lib.lib()
+    # counter (0,0,0,0), key (0,0)
+    assert [L.orc_mlm_key(0, 0, 0, p) for p in range(4)] == [0x6627E8D5, 0xE169C58D, 0xBC57AC4C, 0x9B00DBD8]
+    # counter = pi digits, key = more pi digits
+    seed = 0xA4093822 | (0x299F31D0 << 32)
+    rec = 0x13198A2E | (0x03707344 << 32)
+    base = 0x243F6A88 << 2
+    got = [L.orc_mlm_key(seed, rec, 0x85A308D3, base + k) for k in range(4)]
+    assert got == [0xD16CFE09, 0x94FDCCEB, 0x5001E420, 0x24126EA1]
+
+
+def test_mlm_masks_exact_count(oracle_tok, records):
+    """Every full row with no [PAD] ids masks exactly mask_length positions."""
+    ob = oracle_lib.OracleBatcher(oracle_tok, 4, 512, 76, 103, seed=7)
+    seen = 0
+    for t in records:
+        r = ob.push(t)
+        if r is None:
+            continue
+        planes, rows = r
+        for i in range(rows):
+            ids, am, lab = planes[0][i], planes[1][i], planes[3][i]
+            masked = lab != -100
+            assert np.all(ids[masked] == 103)
+            if am.all():
+                assert masked.sum() == 76
+                seen += 1
+    assert seen > 0
+
+
+def test_unicode_table_probe_sample():
+    """Re-probe a seeded sample of code points through tokenizers' BertNormalizer."""
+    tk = pytest.importorskip("tokenizers")
+    norm = tk.normalizers.BertNormalizer(lowercase=True)
+    path = os.path.join(oracle_lib.UNICODE_BIN)
+    d = open(path, "rb").read()
+    _, ver, npg, nbl, pl = struct.unpack("<4sIIII", d[:20])
+    pages = np.frombuffer(d, np.uint16, npg, 20)
+    ent = np.frombuffer(d, np.uint32, nbl * 128, 20 + 2 * npg)
+    pool = d[20 + 2 * npg + 4 * 128 * nbl:]
+    rng = random.Random(11)
+    cps = list(range(128)) + [rng.randrange(0x80, 0x110000) for _ in range(4000)]
+    for cp in cps:
+        if 0xD800 <= cp <= 0xDFFF:
+            continue
+        e = int(ent[int(pages[cp >> 7]) * 128 + (cp & 127)])
+        n = norm.normalize_str(chr(cp))
+        core = n.replace(" ", "")
+        if (e & 3) == 3:
+            assert n == "", hex(cp)
+        elif (e & 3) == 1:
+            assert n.strip() == "" or all(c.isspace() for c in n), hex(cp)
+        else:
+            mapped = chr(cp) if e & 4 else pool[(e >> 8) + 2:(e >> 8) + 2 + pool[e >> 8]].decode()
+            assert mapped == core, (hex(cp), mapped, core)
