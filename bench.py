@@ -33,6 +33,13 @@ METRIC = "device-resident tokenize+mask MB/s of input text, seq_len=512, 1/2/4/8
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 
 
+_T0 = time.perf_counter()
+
+
+def log(msg):
+    print(f"[bench {time.perf_counter() - _T0:7.1f}s] {msg}", file=sys.stderr, flush=True)
+
+
 def fixture_records():
     with open(os.path.join(REPO, "tests", "golden", "test_records.jsonl"), encoding="utf-8") as f:
         return [json.loads(l)["text"] for l in f]
@@ -119,6 +126,7 @@ def main():
     records = fixture_records()
     arena, offs, order = build_arena(records, args.arena_mib << 20, seed=0x5D1B + rank)
     N, R = len(arena) - 16, len(order)
+    log(f"rank {rank}: arena {N} bytes, {R} records")
     text = torch.from_numpy(arena).to(dev)
     offsets = torch.from_numpy(offs.astype(np.int64)).to(dev)
     stream = torch.cuda.Stream(device=dev)
@@ -128,9 +136,10 @@ def main():
     def step():
         return db.process(text.data_ptr(), N, offsets.data_ptr(), R, first_record, stream.cuda_stream)
 
-    for _ in range(args.warmup):
+    for i in range(args.warmup):
         res = step()
-    torch.cuda.synchronize(dev)
+        torch.cuda.synchronize(dev)
+        log(f"warmup {i} done")
     db.set_profiling(True)
     stage_sum = {}
 
@@ -149,6 +158,7 @@ def main():
     torch.cuda.synchronize(dev)
     barrier()
     dt = time.perf_counter() - t0
+    log(f"timed {args.steps} steps in {dt:.3f} s")
     db.set_profiling(False)
     if world > 1:
         t = torch.tensor([dt], device=dev, dtype=torch.float64)
@@ -184,9 +194,11 @@ def main():
         "stage_ms": {k: round(v, 4) for k, v in stage_ms.items()},
         "path_GBps": round(path_bytes / (step_ms * 1e-3) / 1e9, 2),
     }
+    log(f"stages {stage_ms}")
     if args.e2e and rank == 0:
-        line["end_to_end"] = end_to_end(db, arena, offs, N, R, torch, dev, stream)
+        line["end_to_end"] = end_to_end(records, order)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        log("cpu baseline ...")
         line["cpu_baseline"] = cpu_baseline(records, order)
     elif rank == 0:
         line["cpu_baseline"] = None
@@ -196,33 +208,29 @@ def main():
         dist.destroy_process_group()
 
 
-def end_to_end(db, arena, offs, N, R, torch, dev, stream, reps=3):
-    """Host arena in pinned memory -> H2D -> kernels -> D2H of every row."""
-    from streaming_data_loader_amd import native
-    h_text = torch.from_numpy(arena).pin_memory()
-    h_off = torch.from_numpy(offs.astype(np.int64)).pin_memory()
-    d_text = torch.empty_like(h_text, device=dev)
-    d_off = torch.empty_like(h_off, device=dev)
-    res = db.process(d_text.data_ptr(), N, d_off.data_ptr(), R, 0, stream.cuda_stream)
-    torch.cuda.synchronize(dev)
-    rows = res.rows()
-    out = torch.empty((4, rows, 512), dtype=torch.int32).pin_memory()
+def end_to_end(records, order, nbytes=64 << 20, reps=2):
+    """End-to-end rate of the drop-in host path: records in host memory ->
+    sdl_batcher_push_many (pinned staging, H2D, all kernels, D2H of every row,
+    GenTokenizer's batch queue on the host) -> finished DataSet batches."""
+    from streaming_data_loader_amd import batcher as B
+    gt = B.GenTokenizer(B.ModelType.Bert, B.BatchConfig(256, 512), B.Mask(76, 103), B.TokenizerConfig(), seed=1234)
+    texts, done = [], 0
+    for i in order:
+        texts.append(records[i])
+        done += len(records[i].encode("utf-8"))
+        if done >= nbytes:
+            break
+    blobs = [t.encode("utf-8") for t in texts]
+    gt.create_sync_batches(blobs)  # warm: workspace + pinned staging
     best = None
-    for _ in range(reps):
-        torch.cuda.synchronize(dev)
+    for r in range(reps):
         t0 = time.perf_counter()
-        with torch.cuda.stream(stream):
-            d_text.copy_(h_text, non_blocking=True)
-            d_off.copy_(h_off, non_blocking=True)
-        res = db.process(d_text.data_ptr(), N, d_off.data_ptr(), R, 0, stream.cuda_stream)
-        stream.synchronize()
-        for j, ptr in enumerate((res.r.input_ids, res.r.attention_mask, res.r.token_type_ids, res.r.labels)):
-            native.d2h(out[j].numpy(), ptr, rows * 512 * 4)
-        stream.synchronize()
+        out = gt.create_sync_batches(blobs)
         dt = time.perf_counter() - t0
         best = dt if best is None else min(best, dt)
-    return {"MBps": round(N / best / 1e6, 2), "ms": round(best * 1e3, 3),
-            "note": "pinned H2D of text+offsets, all kernels, D2H of the 4 int32 planes into pinned host memory"}
+        log(f"e2e rep {r}: {len(out)} batches in {dt:.3f} s")
+    return {"MBps": round(done / best / 1e6, 2), "ms": round(best * 1e3, 2), "bytes": done,
+            "path": "host records -> sdl_batcher_push_many: pinned H2D, kernels, D2H of all rows, host batch queue"}
 
 
 if __name__ == "__main__":

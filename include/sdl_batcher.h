@@ -148,6 +148,11 @@ int sdl_process_device(sdl_batcher *h, const uint8_t *d_text, uint64_t text_len,
                        const uint64_t *d_offsets, uint64_t n_records, uint64_t first_record,
                        void *stream, sdl_device_rows *out);
 
+/* Copies `bytes` from device memory (e.g. sdl_device_rows planes) to host
+ * memory with the handle's HIP runtime, ordered after the handle's work on
+ * `stream` (NULL = the handle's stream); returns when the copy is complete. */
+int sdl_device_to_host(sdl_batcher *h, void *dst, const void *src, size_t bytes, void *stream);
+
 /* Per-stage device time (ms) of the last sdl_process_device call, measured with
  * hipEvents on the stream the kernels ran on, when enabled. */
 int sdl_set_profiling(sdl_batcher *h, int enable);

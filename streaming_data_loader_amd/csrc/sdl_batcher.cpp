@@ -479,6 +479,16 @@ int sdl_process_device(sdl_batcher *h, const uint8_t *d_text, uint64_t text_len,
     }
 }
 
+int sdl_device_to_host(sdl_batcher *h, void *dst, const void *src, size_t bytes, void *stream) {
+    if (!h || (bytes && (!dst || !src))) return fail(SDL_ERR_ARG, "null argument");
+    if (!bytes) return SDL_OK;
+    hipStream_t st = stream ? (hipStream_t)stream : h->stream;
+    hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) return fail(SDL_ERR_HIP, std::string("sdl_device_to_host: ") + hipGetErrorString(e));
+    return SDL_OK;
+}
+
 int sdl_set_profiling(sdl_batcher *h, int enable) {
     if (!h) return fail(SDL_ERR_ARG, "null argument");
     h->profiling = enable != 0;

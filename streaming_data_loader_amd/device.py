@@ -11,24 +11,25 @@ from . import native
 
 
 class DeviceResult:
-    def __init__(self, rows_struct, n_records, S):
+    def __init__(self, handle, rows_struct, n_records, S):
+        self.h = handle
         self.r = rows_struct
         self.n_records = n_records
         self.S = S
 
     def rows(self):
         v = np.zeros(1, np.uint32)
-        native.d2h(v, self.r.d_rows, 4)
+        native.d2h(self.h, v, self.r.d_rows, 4)
         return int(v[0])
 
     def tokens(self):
         v = np.zeros(1, np.uint32)
-        native.d2h(v, self.r.d_tokens, 4)
+        native.d2h(self.h, v, self.r.d_tokens, 4)
         return int(v[0])
 
     def record_rows(self):
         v = np.zeros(self.n_records, np.uint32)
-        native.d2h(v, self.r.d_record_rows, 4 * self.n_records)
+        native.d2h(self.h, v, self.r.d_record_rows, 4 * self.n_records)
         return v
 
     def planes(self, n_rows=None):
@@ -39,7 +40,7 @@ class DeviceResult:
         def get(ptr, w):
             a = np.zeros((n, w), np.int32)
             if ptr:
-                native.d2h(a, ptr, a.nbytes)
+                native.d2h(self.h, a, ptr, a.nbytes)
                 return a
             return None
 
@@ -87,7 +88,7 @@ class DeviceBatcher:
         native.check(native.load().sdl_process_device(self._h, ctypes.c_void_p(text_ptr), text_len,
                                                       ctypes.c_void_p(offsets_ptr), n_records, first_record,
                                                       ctypes.c_void_p(stream or None), ctypes.byref(out)))
-        return DeviceResult(out, n_records, self.cfg.sequence_length)
+        return DeviceResult(self._h, out, n_records, self.cfg.sequence_length)
 
     def process_tensors(self, text, offsets, first_record=0, stream=None):
         """text: uint8 cuda tensor; offsets: int64 cuda tensor of n_records+1 entries."""

@@ -18,7 +18,8 @@ SDL_TASK_MLM, SDL_TASK_CLM, SDL_TASK_SPAN, SDL_TASK_MULTI_LABEL = 0, 1, 2, 3
 EXPORTS = [
     "sdl_config_default", "sdl_batcher_create", "sdl_batcher_destroy", "sdl_batcher_push",
     "sdl_batcher_push_many", "sdl_batcher_next", "sdl_batcher_flush", "sdl_batch_release",
-    "sdl_process_device", "sdl_set_profiling", "sdl_stage_times", "sdl_last_error", "sdl_abi_version",
+    "sdl_process_device", "sdl_device_to_host", "sdl_set_profiling", "sdl_stage_times", "sdl_last_error",
+    "sdl_abi_version",
 ]
 
 
@@ -68,6 +69,13 @@ def load(path=LIB_PATH):
         return _lib
     if not os.path.exists(path):
         raise SDLError(-4, f"{path} missing: run `python -m streaming_data_loader_amd.build` (no CPU fallback)")
+    # PyTorch-ROCm ships its own libamdhip64.so.7.  Load it first when torch is
+    # installed so this library binds to the same HIP runtime (same soname)
+    # instead of bringing a second runtime into the process.
+    try:
+        import torch  # noqa: F401
+    except Exception:
+        pass
     L = ctypes.CDLL(path)
     vp, sz, u64, i32, i64 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_int32, ctypes.c_int
     L.sdl_config_default.argtypes = [ctypes.POINTER(Config), i32]
@@ -82,13 +90,15 @@ def load(path=LIB_PATH):
     L.sdl_batch_release.argtypes = [ctypes.POINTER(Batch)]
     L.sdl_batch_release.restype = None
     L.sdl_process_device.argtypes = [vp, vp, u64, vp, u64, u64, vp, ctypes.POINTER(DeviceRows)]
+    L.sdl_device_to_host.argtypes = [vp, vp, vp, sz, vp]
     L.sdl_set_profiling.argtypes = [vp, i64]
     L.sdl_stage_times.argtypes = [vp, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_float), i64]
     L.sdl_last_error.restype = ctypes.c_char_p
     L.sdl_last_error.argtypes = []
     L.sdl_abi_version.restype = i64
     for name in ("sdl_batcher_create", "sdl_batcher_push", "sdl_batcher_push_many", "sdl_batcher_next",
-                 "sdl_batcher_flush", "sdl_process_device", "sdl_set_profiling", "sdl_stage_times"):
+                 "sdl_batcher_flush", "sdl_process_device", "sdl_device_to_host", "sdl_set_profiling",
+                 "sdl_stage_times"):
         getattr(L, name).restype = i64
     _lib = L
     return L
@@ -106,31 +116,9 @@ def default_config(task):
     return c
 
 
-# ---- raw HIP memcpy for tests/bench (device pointers produced by the library)
-_hip = None
-
-
-def hip():
-    global _hip
-    if _hip is None:
-        for name in ("libamdhip64.so", "/opt/rocm/lib/libamdhip64.so"):
-            try:
-                _hip = ctypes.CDLL(name)
-                break
-            except OSError:
-                continue
-        if _hip is None:
-            raise SDLError(-5, "libamdhip64.so not found")
-        _hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
-        _hip.hipMemcpy.restype = ctypes.c_int
-    return _hip
-
-
-def d2h(dst_numpy, src_ptr, nbytes):
-    """hipMemcpy device -> host into a numpy array."""
-    if nbytes == 0:
-        return dst_numpy
-    rc = hip().hipMemcpy(dst_numpy.ctypes.data, ctypes.c_void_p(src_ptr), nbytes, 2)
-    if rc != 0:
-        raise SDLError(-3, f"hipMemcpy D2H failed ({rc})")
+def d2h(handle, dst_numpy, src_ptr, nbytes, stream=None):
+    """Device -> host copy into a numpy array through sdl_device_to_host."""
+    if nbytes:
+        check(load().sdl_device_to_host(handle, dst_numpy.ctypes.data, ctypes.c_void_p(src_ptr), nbytes,
+                                        ctypes.c_void_p(stream or None)))
     return dst_numpy

@@ -22,9 +22,14 @@ if [[ $STEPS == *smoke* ]]; then
   tail -3 gpurun_out/smoke.log
 fi
 if [[ $STEPS == *bench* ]]; then
-  timeout -k 10 600 python bench.py --steps 10 --warmup 3 --e2e > gpurun_out/bench.json 2> gpurun_out/bench.err
+  timeout -k 10 600 python bench.py --steps 10 --warmup 3 ${BENCH_ARGS:-} > gpurun_out/bench.json 2> gpurun_out/bench.err
   stop_on_fault $? bench
   cat gpurun_out/bench.json; tail -5 gpurun_out/bench.err
+fi
+if [[ $STEPS == *e2e* ]]; then
+  timeout -k 10 300 python bench.py --steps 3 --warmup 1 --arena-mib 64 --no-cpu-baseline --e2e > gpurun_out/bench_e2e.json 2> gpurun_out/bench_e2e.err
+  stop_on_fault $? e2e
+  cat gpurun_out/bench_e2e.json
 fi
 if [[ $STEPS == *prof* ]]; then
   timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline > gpurun_out/prof_bench.json 2> gpurun_out/prof.err
