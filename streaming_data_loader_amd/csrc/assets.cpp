@@ -14,9 +14,28 @@
 
 namespace sdl {
 
-uint64_t fnv1a(const uint8_t *p, size_t n, uint64_t h) {
-    for (size_t i = 0; i < n; ++i) h = (h ^ p[i]) * FNV_PRIME;
-    return h;
+static inline uint32_t hmix(uint32_t h, uint32_t w) {
+    h ^= w;
+    h *= 0x85EBCA6Bu;
+    return h ^ (h >> 13);
+}
+
+uint32_t piece_hash(const uint8_t *payload, size_t n, uint32_t cont) {
+    // init(len, cont); then per zero-padded 16-byte block, 4 little-endian
+    // dwords mixed in; then a final avalanche (at least one block, even if empty)
+    uint32_t h = ((uint32_t)n * 2u + cont) * 0x9E3779B1u ^ 0x7F4A7C15u;
+    size_t b0 = 0;
+    do {
+        uint32_t w[4] = {0, 0, 0, 0};
+        for (size_t k = 0; k < 16 && b0 + k < n; ++k) w[k >> 2] |= (uint32_t)payload[b0 + k] << (8 * (k & 3));
+        for (int i = 0; i < 4; ++i) h = hmix(h, w[i]);
+        b0 += 16;
+    } while (b0 < n);
+    h ^= h >> 16;
+    h *= 0x7FEB352Du;
+    h ^= h >> 15;
+    h *= 0x846CA68Bu;
+    return h ^ (h >> 16);
 }
 
 static std::string read_file(const std::string &path) {
@@ -66,8 +85,15 @@ static bool is_bert_normalizer(const JValue *n) {
     return flag("clean_text", true) && flag("handle_chinese_chars", true) && flag("lowercase", true) && strip;
 }
 
+static int find_piece(const HostTokenizer &t, const std::string &s) {
+    for (size_t i = t.pieces.size(); i-- > 0;)
+        if (t.pieces[i] == s) return (int)i;  // a duplicated piece keeps its last id (HashMap insert)
+    return -1;
+}
+
 static void build_vocab_table(HostTokenizer &t) {
     const size_t n = t.pieces.size();
+    if (n > 65535) throw std::runtime_error("vocabulary larger than 65535 ids is not supported (u16 staging)");
     uint32_t slots = 1;
     while (slots < 2 * n) slots <<= 1;
     t.slot_mask = slots - 1;
@@ -79,24 +105,44 @@ static void build_vocab_table(HostTokenizer &t) {
     for (size_t id = 0; id < n; ++id) {
         const std::string &s = t.pieces[id];
         if (s.empty() || last[s] != (int)id) continue;
-        const bool cont = s.size() > 2 && s[0] == '#' && s[1] == '#';
-        if (cont) t.maxlen_cont = std::max(t.maxlen_cont, (int)s.size() - 2);
-        if (s.size() > 0) t.maxlen_first = std::max(t.maxlen_first, (int)s.size());
-        const uint64_t h = fnv1a((const uint8_t *)s.data(), s.size());
+        const uint32_t cont = (s.size() > 2 && s[0] == '#' && s[1] == '#') ? 1u : 0u;
+        const std::string pay = cont ? s.substr(2) : s;
+        if (pay.size() > 255) throw std::runtime_error("vocabulary piece longer than 255 bytes");
+        if (cont) t.maxlen_cont = std::max(t.maxlen_cont, (int)pay.size());
+        else t.maxlen_first = std::max(t.maxlen_first, (int)pay.size());
         VSlot v{};
-        v.tag = (uint32_t)(h >> 32);
+        v.key = (uint32_t)pay.size() | (cont << 8);
         v.id = (int32_t)id;
-        v.len = (uint32_t)s.size();
         v.pool_off = (uint32_t)t.vpool.size();
-        std::memcpy(v.inl, s.data(), std::min<size_t>(16, s.size()));
-        t.vpool.insert(t.vpool.end(), s.begin(), s.end());
-        uint32_t i = (uint32_t)h & t.slot_mask;
+        std::memcpy(v.inl, pay.data(), std::min<size_t>(16, pay.size()));
+        t.vpool.insert(t.vpool.end(), pay.begin(), pay.end());
+        uint32_t i = piece_hash((const uint8_t *)pay.data(), pay.size(), cont) & t.slot_mask;
         while (t.slots[i].id >= 0) i = (i + 1) & t.slot_mask;
         t.slots[i] = v;
     }
-    // a "##" piece also matches at the word start as a literal (never happens
-    // with BERT pre-tokenization, where '#' is punctuation, but stay exact)
     t.vpool.resize(t.vpool.size() + 64, 0);
+}
+
+// ASCII visible classes the kernels compute arithmetically (tokenize_wordpiece.hip:
+// ascii_vclass) must be the table's; and the one-byte ids of the ISO fast path.
+static void check_ascii_and_ids(HostTokenizer &t) {
+    t.ascii_id.assign(128, t.unk_id);
+    for (uint32_t b = 0; b < 128; ++b) {
+        const uint32_t e = t.uentry[(size_t)t.upage[0] * 128 + b];
+        uint32_t want;
+        const uint32_t l = b | 0x20u;
+        if (l - 'a' < 26u || b - '0' < 10u) want = UC_OTHER;
+        else if (b == ' ' || b == '\t' || b == '\n' || b == '\r') want = UC_WS;
+        else if (b < 32u || b == 127u) want = UC_DEL;
+        else want = UC_ISO;
+        if ((e & 3u) != want) throw std::runtime_error("unicode table: ASCII classes differ from the kernels' classifier");
+        std::string m = (e & 4u) ? std::string(1, (char)b)
+                                 : std::string((const char *)&t.upool[(e >> 8) + 2], t.upool[e >> 8]);
+        const int id = find_piece(t, m);
+        if (id >= 0) t.ascii_id[b] = id;
+    }
+    if (t.opener && (t.opener >= 0x80 || (t.uentry[(size_t)t.upage[0] * 128 + t.opener] & 3u) == UC_OTHER))
+        throw std::runtime_error("added tokens must start with an ASCII non-alphanumeric byte");
 }
 
 static void set_added(HostTokenizer &t) {
@@ -215,6 +261,7 @@ void load_tokenizer(const std::string &path, const std::string &data_dir, HostTo
     set_added(t);
     build_vocab_table(t);
     load_unicode(data_dir + "/bert_uncased_unicode.bin", t);
+    check_ascii_and_ids(t);
 }
 
 }  // namespace sdl

@@ -26,6 +26,7 @@ struct HostTokenizer {
     // ---- device image of the vocabulary ------------------------------------
     std::vector<VSlot> slots;
     std::vector<uint8_t> vpool;
+    std::vector<int32_t> ascii_id;  // id of the one-byte word b (ISO ASCII fast path)
     uint32_t slot_mask = 0;
     int maxlen_first = 0, maxlen_cont = 0;
     uint32_t opener = 0;
@@ -38,6 +39,8 @@ struct HostTokenizer {
 // anything unsupported.
 void load_tokenizer(const std::string &path, const std::string &data_dir, HostTokenizer &out);
 
-uint64_t fnv1a(const uint8_t *p, size_t n, uint64_t h = FNV_BASIS);
+// Slot hash of a vocab piece (payload bytes, cont = "##"-prefixed); the
+// kernels compute the same function (tokenize_wordpiece.hip: hinit/hmix/hfinal).
+uint32_t piece_hash(const uint8_t *payload, size_t n, uint32_t cont);
 
 }  // namespace sdl

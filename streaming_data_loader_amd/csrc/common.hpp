@@ -30,18 +30,17 @@ constexpr int MAX_SPECIAL = 8;
 constexpr int MAX_SPECIAL_LEN = 24;
 constexpr int MAX_FRAME = 4;
 
-constexpr uint64_t FNV_BASIS = 1469598103934665603ull;
-constexpr uint64_t FNV_PRIME = 1099511628211ull;
 
-// Vocabulary hash-table slot: 32 bytes, two 16-B loads.
-//   w0 tag (hash >> 32), w1 id (-1 = empty), w2 byte length of the literal
-//   piece (incl. "##"), w3 offset of the piece bytes in the pool,
-//   w4..w7 first 16 bytes of the piece inline.
+// Vocabulary hash-table slot: 32 bytes, two 16-B loads.  A piece is keyed by
+// (payload, cont) where cont = it starts with "##" (payload = the rest):
+//   w0 key = payload length | cont << 8, w1 id (-1 = empty slot),
+//   w2 offset of the payload in the pool, w3 0, w4..w7 the first 16 payload
+//   bytes (zero padded).  Slot index = piece_hash(payload, cont) & mask.
 struct alignas(32) VSlot {
-    uint32_t tag;
+    uint32_t key;
     int32_t id;
-    uint32_t len;
     uint32_t pool_off;
+    uint32_t pad;
     uint8_t inl[16];
 };
 static_assert(sizeof(VSlot) == 32, "VSlot must be 32 bytes");
@@ -52,12 +51,12 @@ struct DevTok {
     const uint32_t *uentry;  // Unicode blocks      [n_blocks*128]
     const uint8_t *upool;    // normalized strings  (u8 nbytes, u8 nchars, bytes)
     const VSlot *slots;      // vocab hash table
-    const uint8_t *vpool;    // vocab piece bytes
+    const uint8_t *vpool;    // vocab piece payload bytes
+    const int32_t *ascii_id; // id of each one-byte ASCII word (or [UNK])
     uint32_t slot_mask;
     int32_t unk_id;
     int32_t maxlen_first;    // longest non-"##" piece (bytes)
     int32_t maxlen_cont;     // longest "##" piece without the prefix (bytes)
-    uint64_t h_cont;         // FNV state after hashing "##"
     int32_t n_special;       // added tokens matched on the raw text
     int32_t max_special_len;
     uint32_t opener;         // first byte shared by every added token

@@ -10,8 +10,10 @@
 namespace sdl {
 
 // tokenize_wordpiece.hip: text arena -> per-chunk token lists + boundary offsets
+// `ranges` needs 3 words per 4096-byte chunk.
 hipError_t launch_wordpiece_chunks(const DevTok &T, const uint8_t *text, int64_t N, const uint64_t *off, int64_t R,
-                                   uint32_t *tokc, uint32_t *chunk_cnt, uint32_t *rec_local, hipStream_t st);
+                                   uint32_t *ranges, uint32_t *tokc, uint32_t *chunk_cnt, uint32_t *rec_local,
+                                   hipStream_t st);
 
 // pipeline.hip
 // out[0..n) = exclusive prefix sum of in[0..n), out[n] = total.  tmp needs

@@ -112,9 +112,11 @@ struct sdl_batcher {
     DevBuf<uint32_t> d_uentry;
     DevBuf<uint8_t> d_upool, d_vpool;
     DevBuf<VSlot> d_slots;
+    DevBuf<int32_t> d_ascii_id;
 
     // per-call workspace
-    DevBuf<uint32_t> tokc, chunk_cnt, chunk_off, rec_local, tok_ids, rec_tok, rec_cnt, rec_rows, row_off, scan_tmp;
+    DevBuf<uint32_t> ranges, tokc, chunk_cnt, chunk_off, rec_local, tok_ids, rec_tok, rec_cnt, rec_rows, row_off,
+        scan_tmp;
     DevBuf<int32_t> o_ids, o_am, o_tt, o_lab;
     DevBuf<uint8_t> h2d_text;
     DevBuf<uint64_t> h2d_off;
@@ -155,6 +157,7 @@ struct sdl_batcher {
                     hipStream_t st) {
         const int64_t n_chunks = (N + CHUNK - 1) / CHUNK;
         const int64_t rows_cap = rows_capacity(N, R);
+        ranges.ensure((size_t)std::max<int64_t>(n_chunks, 1) * 3);
         tokc.ensure((size_t)std::max<int64_t>(n_chunks, 1) * STAGE);
         chunk_cnt.ensure((size_t)n_chunks + 1);
         chunk_off.ensure((size_t)n_chunks + 1);
@@ -177,7 +180,7 @@ struct sdl_batcher {
             if (profiling) HIP_TRY(hipEventRecord(ev[i], st));
         };
         mark(0);
-        HIP_TRY(launch_wordpiece_chunks(dt, d_text, N, d_off, R, tokc.p, chunk_cnt.p, rec_local.p, st));
+        HIP_TRY(launch_wordpiece_chunks(dt, d_text, N, d_off, R, ranges.p, tokc.p, chunk_cnt.p, rec_local.p, st));
         mark(1);
         HIP_TRY(launch_exclusive_scan(chunk_cnt.p, chunk_off.p, n_chunks, scan_tmp.p, st));
         mark(2);
@@ -329,6 +332,8 @@ int sdl_batcher_create(const sdl_config *cfg, const char *tokenizer_path, const 
         h->d_upool.ensure(t.upool.size());
         h->d_slots.ensure(t.slots.size());
         h->d_vpool.ensure(t.vpool.size());
+        h->d_ascii_id.ensure(128);
+        HIP_TRY(hipMemcpy(h->d_ascii_id.p, t.ascii_id.data(), 128 * 4, hipMemcpyHostToDevice));
         HIP_TRY(hipMemcpy(h->d_upage.p, t.upage.data(), t.upage.size() * 2, hipMemcpyHostToDevice));
         HIP_TRY(hipMemcpy(h->d_uentry.p, t.uentry.data(), t.uentry.size() * 4, hipMemcpyHostToDevice));
         HIP_TRY(hipMemcpy(h->d_upool.p, t.upool.data(), t.upool.size(), hipMemcpyHostToDevice));
@@ -344,7 +349,7 @@ int sdl_batcher_create(const sdl_config *cfg, const char *tokenizer_path, const 
         d.unk_id = t.unk_id;
         d.maxlen_first = t.maxlen_first;
         d.maxlen_cont = t.maxlen_cont;
-        d.h_cont = fnv1a((const uint8_t *)"##", 2);
+        d.ascii_id = h->d_ascii_id.p;
         d.n_special = (int)t.added.size();
         d.max_special_len = t.max_special_len;
         d.opener = t.opener;

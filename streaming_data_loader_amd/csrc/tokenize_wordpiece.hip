@@ -8,21 +8,26 @@
 //   -> BertPreTokenizer (split on whitespace, isolate punctuation)
 //   -> WordPiece (greedy longest-match-first, "##" continuation, 100-char cap).
 // The template's [CLS]/[SEP] and the wrapper's framing are added at row
-// assembly (rows.hip).
+// assembly (pipeline.hip).
 //
-// One 256-thread workgroup owns CHUNK = 4096 bytes of the arena:
-//   1. stage [c0-16, c0+4096+240) in LDS with 16-B coalesced loads;
-//   2. each thread classifies its 16 bytes (ASCII from an LDS table, the rest
-//      through the two-level Unicode table in L2) into visible classes;
-//   3. a block scan carries "last visible class" across threads, so every
-//      thread knows where pieces (words, isolated chars, added tokens) start;
-//   4. piece starts are compacted into an LDS list (block prefix sum);
-//   5. each thread WordPiece-tokenizes pieces i, i+256, ... reading the word
-//      from LDS and probing the vocab hash (32-B slots, L2-resident); tokens of
-//      a piece starting at byte p are staged at stage[p-c0] (a piece never has
-//      more tokens than bytes, so these never collide);
-//   6. a second block scan compacts the staged tokens into this chunk's region
-//      of `tokc` and records where each record boundary falls.
+// One 256-thread workgroup owns CHUNK = 4096 bytes of the arena; lane t owns
+// bytes [c0 + 16t, c0 + 16t + 16):
+//   1. each lane loads its 16 bytes with one 16-B non-temporal load (they stay
+//      in VGPRs) and stores them into an LDS window [c0-16, c0+4096+240);
+//      record starts in the window become an LDS bitmap;
+//   2. classification is register-resident: an arithmetic ASCII classifier
+//      packs 16 four-bit visible classes into one u64; only lead bytes >= 0xC0
+//      (two-level Unicode table in L2) and added-token openers take a loop;
+//   3. a block scan carries the last visible class across lanes; piece starts
+//      (words, isolated chars, added tokens) are compacted into an LDS list;
+//   4. each lane WordPiece-tokenizes pieces i, i+256, ...: an ASCII word of
+//      <= 16 bytes is read from LDS as 5 aligned dwords + v_alignbyte,
+//      lower-cased and classified with SWAR, and every candidate piece is one
+//      hash of 4 dwords + one 32-B probe of the L2-resident vocab table whose
+//      slots hold the piece bytes inline; other words take a general path;
+//   5. staged ids (LDS, indexed by piece byte position: a piece never has
+//      more ids than bytes) are compacted into this chunk's slice of `tokc`,
+//      and each record boundary's local id offset is recorded.
 #include "common.hpp"
 #include "device_util.hpp"
 #include "kernels.hpp"
@@ -31,122 +36,124 @@ namespace sdl {
 
 namespace {
 
-struct Src {
-    const uint8_t *win;    // LDS copy of [w0, w0 + WIN)
-    const uint8_t *rflag;  // LDS: 1 where a record starts, same window
+typedef __attribute__((address_space(3))) uint8_t lds_u8;
+typedef __attribute__((address_space(3))) uint16_t lds_u16;
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+
+constexpr int RBITS_WORDS = WIN / 32;  // 136
+
+struct Ctx {
+    const DevTok *T;
+    const lds_u8 *win;      // LDS window [w0, w0 + WIN)
+    const lds_u32 *rbits;   // LDS bitmap: record starts in the window
+    const lds_u32 *ascii;   // LDS: Unicode-table entries for ASCII
     int64_t w0;
     const uint8_t *text;
     int64_t N;
-    const uint64_t *off;   // record offsets, R+1 entries
+    const uint64_t *off;
     int64_t R;
 
     __device__ __forceinline__ bool in_win(int64_t p) const { return (uint64_t)(p - w0) < (uint64_t)WIN; }
-    __device__ __forceinline__ uint32_t byte(int64_t p) const { return in_win(p) ? win[p - w0] : text[p]; }
-    // true when a record starts at p (p in [0, N])
+    __device__ __forceinline__ uint32_t byte(int64_t p) const {
+        uint32_t r;
+        if (in_win(p)) r = win[p - w0];
+        else r = __builtin_nontemporal_load(text + p);
+        return r;
+    }
+    // true when a record starts at p (0 <= p <= N)
     __device__ bool rstart(int64_t p) const {
-        if (in_win(p)) return rflag[p - w0] != 0;
-        int64_t lo = 0, hi = R;  // any off[r] == p ?
+        if (in_win(p)) {
+            const int i = (int)(p - w0);
+            return (rbits[i >> 5] >> (i & 31)) & 1u;
+        }
+        int64_t lo = 0, hi = R;
         while (lo < hi) {
-            int64_t mid = (lo + hi) >> 1;
+            const int64_t mid = (lo + hi) >> 1;
             if ((int64_t)off[mid] < p) lo = mid + 1; else hi = mid;
         }
-        return lo <= R && (int64_t)off[lo] == p;
+        return (int64_t)off[lo] == p;
     }
 };
 
-// Longest added token matching at p (which holds the opener byte) that does
-// not cross a record start; -1 if none.  AddedVocabulary uses leftmost-longest
-// matching; added tokens never overlap because the opener byte occurs only at
-// their start (checked on the host).
-__device__ int special_match(const DevTok &T, const Src &S, int64_t p) {
-    int best = -1, best_len = 0;
-    for (int k = 0; k < T.n_special; ++k) {
-        int l = T.special_len[k];
-        if (p + l > S.N || l <= best_len) continue;
-        bool ok = true;
-        for (int j = 1; j < l && ok; ++j) ok = S.byte(p + j) == T.special_bytes[k][j] && !S.rstart(p + j);
-        if (ok) { best = k; best_len = l; }
-    }
-    return best;
+// ---- hashing of vocab pieces (assets.cpp: piece_hash) -------------------------
+__device__ __forceinline__ uint32_t hmix(uint32_t h, uint32_t w) {
+    h ^= w;
+    h *= 0x85EBCA6Bu;
+    return h ^ (h >> 13);
+}
+__device__ __forceinline__ uint32_t hinit(uint32_t len, uint32_t cont) { return (len * 2u + cont) * 0x9E3779B1u ^ 0x7F4A7C15u; }
+__device__ __forceinline__ uint32_t hfinal(uint32_t h) {
+    h ^= h >> 16;
+    h *= 0x7FEB352Du;
+    h ^= h >> 15;
+    h *= 0x846CA68Bu;
+    return h ^ (h >> 16);
 }
 
-// End of the record containing p (first record start > p), bounded by N.
-__device__ int64_t rec_end_of(const Src &S, const int32_t *rb, int nrb, int64_t rb_next, bool rb_ok, int64_t p) {
-    if (rb_ok) {
-        int rel = (int)(p - S.w0);
-        int lo = 0, hi = nrb;
-        while (lo < hi) {
-            int mid = (lo + hi) >> 1;
-            if (rb[mid] <= rel) lo = mid + 1; else hi = mid;
-        }
-        return lo < nrb ? S.w0 + rb[lo] : rb_next;
-    }
-    int64_t lo = 0, hi = S.R;  // first off[r] > p
-    while (lo < hi) {
-        int64_t mid = (lo + hi) >> 1;
-        if ((int64_t)S.off[mid] <= p) lo = mid + 1; else hi = mid;
-    }
-    int64_t e = (int64_t)S.off[lo];
-    return e < S.N ? e : S.N;
+// ---- 16-byte register words ---------------------------------------------------
+struct W16 {
+    uint32_t x, y, z, w;
+};
+
+// bytes [k, k + 16) of a (zero beyond 16), k in [0, 16)
+__device__ __forceinline__ W16 shift_right_bytes(const W16 &a, int k) {
+    const int q = k >> 2;
+    const uint32_t r = (uint32_t)(k & 3);
+    auto word = [&](int j) -> uint32_t { return j == 0 ? a.x : j == 1 ? a.y : j == 2 ? a.z : j == 3 ? a.w : 0u; };
+    uint32_t o[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o[i] = __builtin_amdgcn_alignbyte(word(i + q + 1), word(i + q), r);
+    return W16{o[0], o[1], o[2], o[3]};
 }
 
-// Unicode table entry of code point cp.
+// keep the first n bytes (n in [0, 16])
+__device__ __forceinline__ W16 keep_bytes(const W16 &a, int n) {
+    auto m = [&](int i) -> uint32_t {
+        const int k = n - 4 * i;
+        return k >= 4 ? 0xFFFFFFFFu : k <= 0 ? 0u : (0xFFFFFFFFu >> (32 - 8 * k));
+    };
+    return W16{a.x & m(0), a.y & m(1), a.z & m(2), a.w & m(3)};
+}
+
+// SWAR: 0x80 in every byte of x that is an ASCII letter or digit
+__device__ __forceinline__ uint32_t swar_alnum(uint32_t x) {
+    const uint32_t hi = x & 0x80808080u;
+    const uint32_t l = (x | 0x20202020u) & 0x7F7F7F7Fu;
+    const uint32_t ge_a = (l + 0x1F1F1F1Fu) & 0x80808080u;   // l >= 0x61
+    const uint32_t le_z = ~(l + 0x05050505u) & 0x80808080u;  // l <= 0x7A
+    const uint32_t d = x & 0x7F7F7F7Fu;
+    const uint32_t ge_0 = (d + 0x50505050u) & 0x80808080u;   // d >= 0x30
+    const uint32_t le_9 = ~(d + 0x46464646u) & 0x80808080u;  // d <= 0x39
+    return ((ge_a & le_z) | (ge_0 & le_9)) & ~hi;
+}
+// SWAR lower-case of ASCII A-Z
+__device__ __forceinline__ uint32_t swar_lower(uint32_t x) {
+    const uint32_t d = x & 0x7F7F7F7Fu;
+    const uint32_t ge_A = (d + 0x3F3F3F3Fu) & 0x80808080u;   // d >= 0x41
+    const uint32_t le_Z = ~(d + 0x25252525u) & 0x80808080u;  // d <= 0x5A
+    const uint32_t up = ge_A & le_Z & ~(x & 0x80808080u);
+    return x | (up >> 2);
+}
+// 4-bit mask from the 0x80 bits of a SWAR result
+__device__ __forceinline__ uint32_t msb4(uint32_t m) {
+    return ((m >> 7) & 1u) | ((m >> 14) & 2u) | ((m >> 21) & 4u) | ((m >> 28) & 8u);
+}
+
+// ASCII visible class (same as the table's ASCII rows; checked on the host)
+__device__ __forceinline__ uint32_t ascii_vclass(uint32_t b) {
+    const uint32_t l = b | 0x20u;
+    if (l - 'a' < 26u || b - '0' < 10u) return V_OTHER;
+    if (b == ' ' || b == '\t' || b == '\n' || b == '\r') return V_WS;
+    if (b < 32u || b == 127u) return V_NONE;
+    return V_ISO;
+}
+
 __device__ __forceinline__ uint32_t uentry(const DevTok &T, uint32_t cp) {
     if (cp >= 0x110000u) return UC_DEL;
     return T.uentry[(uint32_t)T.upage[cp >> 7] * 128u + (cp & 127u)];
 }
 
-// Strict UTF-8 decode of the char starting at lead byte p (b = its byte);
-// the char must not cross a record start.  Invalid -> U+FFFD (class DEL), 1 byte.
-__device__ __forceinline__ uint32_t decode(const Src &S, int64_t p, uint32_t b, int *len) {
-    int n;
-    uint32_t c;
-    if ((b & 0xE0) == 0xC0) { n = 2; c = b & 0x1F; }
-    else if ((b & 0xF0) == 0xE0) { n = 3; c = b & 0x0F; }
-    else if ((b & 0xF8) == 0xF0) { n = 4; c = b & 0x07; }
-    else { *len = 1; return 0xFFFD; }
-    if (p + n > S.N) { *len = 1; return 0xFFFD; }
-    for (int k = 1; k < n; ++k) {
-        uint32_t x = S.byte(p + k);
-        if ((x & 0xC0) != 0x80 || S.rstart(p + k)) { *len = 1; return 0xFFFD; }
-        c = (c << 6) | (x & 0x3F);
-    }
-    *len = n;
-    return c;
-}
-
-// Is byte q covered by an added token that starts before q?
-__device__ bool covered(const DevTok &T, const Src &S, int64_t q) {
-    for (int d = 1; d < T.max_special_len; ++d) {
-        if (S.rstart(q - d + 1)) return false;  // q-d lies in an earlier record
-        int64_t x = q - d;
-        if (x < 0) return false;
-        if (S.byte(x) == T.opener) {
-            // the opener occurs only at token starts: this is the only candidate
-            int m = special_match(T, S, x);
-            return m >= 0 && T.special_len[m] > d;
-        }
-    }
-    return false;
-}
-
-// Visible class of the char starting at q.  `maybe_special` = an opener byte
-// occurs close enough to matter.
-__device__ uint8_t vclass(const DevTok &T, const Src &S, const uint32_t *ascii, int64_t q, bool maybe_special) {
-    uint32_t b = S.byte(q);
-    if ((b & 0xC0) == 0x80) return V_NONE;
-    if (maybe_special) {
-        if (covered(T, S, q)) return V_NONE;
-        if (b == T.opener && special_match(T, S, q) >= 0) return V_SPEC;
-    }
-    uint32_t e;
-    if (b < 0x80) {
-        e = ascii[b];
-    } else {
-        int len;
-        uint32_t cp = decode(S, q, b, &len);
-        e = uentry(T, cp);
-    }
+__device__ __forceinline__ uint32_t vclass_of_entry(uint32_t e) {
     switch (e & 3u) {
         case UC_OTHER: return V_OTHER;
         case UC_WS: return V_WS;
@@ -155,381 +162,529 @@ __device__ uint8_t vclass(const DevTok &T, const Src &S, const uint32_t *ascii, 
     }
 }
 
-// ---- WordPiece --------------------------------------------------------------
+// Strict UTF-8 decode of the char at lead byte b = byte(p); must not cross a
+// record start.  Invalid -> U+FFFD (class DEL), 1 byte.
+__device__ __forceinline__ uint32_t decode(const Ctx &C, int64_t p, uint32_t b, int *len) {
+    int n;
+    uint32_t c;
+    if ((b & 0xE0u) == 0xC0u) { n = 2; c = b & 0x1Fu; }
+    else if ((b & 0xF0u) == 0xE0u) { n = 3; c = b & 0x0Fu; }
+    else if ((b & 0xF8u) == 0xF0u) { n = 4; c = b & 0x07u; }
+    else { *len = 1; return 0xFFFDu; }
+    if (p + n > C.N) { *len = 1; return 0xFFFDu; }
+    for (int k = 1; k < n; ++k) {
+        const uint32_t x = C.byte(p + k);
+        if ((x & 0xC0u) != 0x80u || C.rstart(p + k)) { *len = 1; return 0xFFFDu; }
+        c = (c << 6) | (x & 0x3Fu);
+    }
+    *len = n;
+    return c;
+}
 
-// Probe the vocab for the literal piece (cont ? "##" : "") + w[start, end).
-template <class W>
-__device__ int vocab_find(const DevTok &T, const W &w, int start, int end, bool cont) {
-    uint64_t h = cont ? T.h_cont : FNV_BASIS;
-    for (int i = start; i < end; ++i) h = (h ^ w(i)) * FNV_PRIME;
-    const uint32_t len = (uint32_t)(end - start) + (cont ? 2u : 0u);
-    const uint32_t tag = (uint32_t)(h >> 32);
-    uint32_t s = (uint32_t)h & T.slot_mask;
-    for (;;) {
-        const uint4 *p = reinterpret_cast<const uint4 *>(T.slots + s);
-        uint4 a = p[0];
-        if ((int32_t)a.y < 0) return -1;
-        if (a.x == tag && a.z == len) {
-            uint4 in = p[1];
-            uint32_t words[4] = {in.x, in.y, in.z, in.w};
-            bool ok = true;
-            const int pre = cont ? 2 : 0;
-            for (uint32_t k = 0; k < len && ok; ++k) {
-                uint32_t q = (int)k < pre ? (uint32_t)'#' : w(start + (int)k - pre);
-                uint32_t e;
-                if (k < 16) e = (words[k >> 2] >> ((k & 3) * 8)) & 0xFF;
-                else e = T.vpool[a.w + k];
-                ok = q == e;
+// Longest added token starting at p that does not cross a record start; -1 if
+// none.  Added tokens never overlap: their first byte occurs nowhere else in
+// them (checked on the host), so leftmost-longest matching is local.
+__device__ int special_match(const Ctx &C, int64_t p) {
+    const DevTok &T = *C.T;
+    int best = -1, best_len = 0;
+    for (int k = 0; k < T.n_special; ++k) {
+        const int l = T.special_len[k];
+        if (p + l > C.N || l <= best_len) continue;
+        bool ok = true;
+        for (int j = 1; j < l && ok; ++j) ok = C.byte(p + j) == T.special_bytes[k][j] && !C.rstart(p + j);
+        if (ok) { best = k; best_len = l; }
+    }
+    return best;
+}
+
+// Full visible class of the char at q (general path).
+__device__ uint32_t vclass_general(const Ctx &C, int64_t q) {
+    const DevTok &T = *C.T;
+    const uint32_t b = C.byte(q);
+    if ((b & 0xC0u) == 0x80u) return V_NONE;
+    if (T.n_special) {
+        for (int d = 1; d < T.max_special_len; ++d) {  // covered by an earlier added token?
+            if (C.rstart(q - d + 1)) break;
+            const int64_t x = q - d;
+            if (x < 0) break;
+            if (C.byte(x) == T.opener) {
+                const int m = special_match(C, x);
+                if (m >= 0 && T.special_len[m] > d) return V_NONE;
+                break;
             }
-            if (ok) return (int)a.y;
         }
-        s = (s + 1) & T.slot_mask;
+        if (b == T.opener && special_match(C, q) >= 0) return V_SPEC;
+    }
+    if (b < 0x80u) return ascii_vclass(b);
+    int len;
+    return vclass_of_entry(uentry(T, decode(C, q, b, &len)));
+}
+
+// ---- WordPiece ------------------------------------------------------------------
+
+// Probe for the literal piece (cont ? "##" : "") + payload, payload <= 16
+// bytes held in c (zero padded).  Returns the id or -1.
+__device__ __forceinline__ int probe16(const DevTok &T, const W16 &c, uint32_t n, uint32_t cont) {
+    uint32_t h = hinit(n, cont);
+    h = hmix(h, c.x);
+    h = hmix(h, c.y);
+    h = hmix(h, c.z);
+    h = hmix(h, c.w);
+    h = hfinal(h);
+    const uint32_t key = n | (cont << 8);
+    for (uint32_t s = h & T.slot_mask;; s = (s + 1) & T.slot_mask) {
+        const uint4 *e = reinterpret_cast<const uint4 *>(T.slots + s);
+        const uint4 a = e[0];
+        if ((int32_t)a.y < 0) return -1;
+        if (a.x == key) {
+            const uint4 b = e[1];
+            if (b.x == c.x && b.y == c.y && b.z == c.z && b.w == c.w) return (int32_t)a.y;
+        }
     }
 }
 
-// WordPiece::tokenize on the normalized word w[0, L) (byte-addressed, UTF-8),
-// writing ids to out[]; returns the id count.  Candidates longer than the
-// longest vocabulary piece are skipped: they cannot match, so the greedy
-// longest-match result is unchanged.
-template <class W>
-__device__ int wordpiece(const DevTok &T, const W &w, int L, uint32_t *out) {
+// General probe: payload = w[start, end) of a byte buffer (any length).
+__device__ int probe_general(const DevTok &T, const uint8_t *w, int start, int end, uint32_t cont) {
+    const uint32_t n = (uint32_t)(end - start);
+    uint32_t h = hinit(n, cont);
+    W16 first{0, 0, 0, 0};
+    uint32_t b0 = 0;
+    do {
+        uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+        for (uint32_t k = 0; k < 16 && b0 + k < n; ++k) {
+            const uint32_t v = (uint32_t)w[start + b0 + k] << (8 * (k & 3));
+            if (k < 4) c0 |= v; else if (k < 8) c1 |= v; else if (k < 12) c2 |= v; else c3 |= v;
+        }
+        if (b0 == 0) first = W16{c0, c1, c2, c3};
+        h = hmix(h, c0);
+        h = hmix(h, c1);
+        h = hmix(h, c2);
+        h = hmix(h, c3);
+        b0 += 16;
+    } while (b0 < n);
+    h = hfinal(h);
+    const uint32_t key = n | (cont << 8);
+    for (uint32_t s = h & T.slot_mask;; s = (s + 1) & T.slot_mask) {
+        const uint4 *e = reinterpret_cast<const uint4 *>(T.slots + s);
+        const uint4 a = e[0];
+        if ((int32_t)a.y < 0) return -1;
+        if (a.x != key) continue;
+        const uint4 b = e[1];
+        if (b.x != first.x || b.y != first.y || b.z != first.z || b.w != first.w) continue;
+        bool ok = true;
+        for (uint32_t k = 16; k < n && ok; ++k) ok = T.vpool[a.z + k] == w[start + k];
+        if (ok) return (int32_t)a.y;
+    }
+}
+
+// WordPiece::tokenize over a normalized word held in a byte buffer.
+__device__ int wordpiece_general(const DevTok &T, const uint8_t *w, int L, lds_u16 *out) {
     int n = 0, start = 0;
     while (start < L) {
-        int lim = start == 0 ? T.maxlen_first : T.maxlen_cont;
+        const int lim = start == 0 ? T.maxlen_first : T.maxlen_cont;
         int end = start + lim < L ? start + lim : L;
-        while (end < L && end > start && (w(end) & 0xC0) == 0x80) --end;  // char boundary
+        while (end < L && end > start && (w[end] & 0xC0) == 0x80) --end;
         int id = -1;
         while (end > start) {
-            id = vocab_find(T, w, start, end, start > 0);
+            id = probe_general(T, w, start, end, start > 0 ? 1u : 0u);
             if (id >= 0) break;
-            do { --end; } while (end > start && (w(end) & 0xC0) == 0x80);
+            do { --end; } while (end > start && (w[end] & 0xC0) == 0x80);
         }
         if (id < 0) {
-            out[0] = (uint32_t)T.unk_id;
+            out[0] = (uint16_t)T.unk_id;
             return 1;
         }
-        out[n++] = (uint32_t)id;
+        out[n++] = (uint16_t)id;
         start = end;
     }
     return n;
 }
 
-struct LdsLower {  // ASCII fast path: word bytes straight from LDS, lower-cased
-    const uint8_t *p;
-    __device__ __forceinline__ uint32_t operator()(int i) const {
-        uint32_t b = p[i];
-        return (b - 'A' < 26u) ? b + 32 : b;
-    }
-};
-struct BufBytes {
-    const uint8_t *p;
-    __device__ __forceinline__ uint32_t operator()(int i) const { return p[i]; }
-};
-
-// Appends the normalized bytes of code point cp (table entry e, raw bytes at
-// S[p, p+len)) to buf.
-__device__ __forceinline__ int append_norm(const DevTok &T, const Src &S, uint32_t e, int64_t p, int len,
-                                           uint8_t *buf, int nb) {
+// Appends the normalized bytes of a non-ASCII OTHER/ISO char.
+__device__ __forceinline__ int append_norm(const Ctx &C, uint32_t e, int64_t p, int len, uint8_t *buf, int nb) {
     if (e & 4u) {
-        for (int k = 0; k < len; ++k) buf[nb + k] = (uint8_t)S.byte(p + k);
+        for (int k = 0; k < len; ++k) buf[nb + k] = (uint8_t)C.byte(p + k);
         return nb + len;
     }
-    const uint8_t *pe = T.upool + (e >> 8);
-    int m = pe[0];
+    const uint8_t *pe = C.T->upool + (e >> 8);
+    const int m = pe[0];
     for (int k = 0; k < m; ++k) buf[nb + k] = pe[2 + k];
     return nb + m;
 }
 
-// Tokenizes the WORD piece starting at p (an OTHER char after a non-OTHER
-// visible char).  The word runs over OTHER and invisible chars until a
-// WS/ISO char, an added token or the record end.
-__device__ int word_tokens(const DevTok &T, const Src &S, const uint32_t *ascii, int64_t p, int64_t rec_end,
-                           uint32_t *out) {
-    // pass 1: extent, normalized length, and whether the fast path applies
+// General WORD piece: runs over OTHER and invisible chars until a WS/ISO char,
+// an added token or the record end; materialized in private memory.
+__device__ int word_general(const Ctx &C, int64_t p, int64_t rec_end, lds_u16 *out) {
+    const DevTok &T = *C.T;
     int64_t i = p;
     int nchars = 0;
-    bool simple = true;  // pure ASCII OTHER chars, all inside the LDS window
-    while (i < rec_end) {
-        uint32_t b = S.byte(i);
-        if (b < 0x80) {
-            uint32_t c = ascii[b] & 3u;
+    while (i < rec_end && nchars <= MAX_WORD_CHARS) {
+        const uint32_t b = C.byte(i);
+        if (b < 0x80u) {
+            const uint32_t c = C.ascii[b] & 3u;
             if (c == UC_OTHER) {
-                if (T.n_special && b == T.opener && special_match(T, S, i) >= 0) break;
-                ++nchars; ++i;
-                if (nchars > MAX_WORD_CHARS) break;
+                if (T.n_special && b == T.opener && special_match(C, i) >= 0) break;
+                ++nchars;
+                ++i;
                 continue;
             }
-            if (c == UC_DEL) { simple = false; ++i; continue; }
-            break;  // WS or ISO
-        }
-        simple = false;
-        if ((b & 0xC0) == 0x80) { ++i; continue; }  // continuation / stray byte
-        int len;
-        uint32_t cp = decode(S, i, b, &len);
-        uint32_t e = uentry(T, cp);
-        uint32_t c = e & 3u;
-        if (c == UC_OTHER) {
-            nchars += (e & 4u) ? 1 : T.upool[(e >> 8) + 1];
-        } else if (c != UC_DEL) {
+            if (c == UC_DEL) { ++i; continue; }
             break;
         }
+        if ((b & 0xC0u) == 0x80u) { ++i; continue; }
+        int len;
+        const uint32_t e = uentry(T, decode(C, i, b, &len));
+        const uint32_t c = e & 3u;
+        if (c == UC_OTHER) nchars += (e & 4u) ? 1 : T.upool[(e >> 8) + 1];
+        else if (c != UC_DEL) break;
         i += len;
-        if (nchars > MAX_WORD_CHARS) break;
     }
     if (nchars > MAX_WORD_CHARS) {
-        out[0] = (uint32_t)T.unk_id;
+        out[0] = (uint16_t)T.unk_id;
         return 1;
     }
-    if (simple && S.in_win(p) && S.in_win(i - 1)) {
-        LdsLower w{S.win + (p - S.w0)};
-        return wordpiece(T, w, (int)(i - p), out);
-    }
-    // pass 2 (rare): materialize the normalized word in private memory
     uint8_t buf[MAX_WORD_BYTES];
     int nb = 0;
     for (int64_t q = p; q < i;) {
-        uint32_t b = S.byte(q);
-        if (b < 0x80) {
-            uint32_t e = ascii[b];
-            if ((e & 3u) == UC_OTHER) buf[nb++] = (uint8_t)((b - 'A' < 26u) ? b + 32 : b);
+        const uint32_t b = C.byte(q);
+        if (b < 0x80u) {
+            const uint32_t e = C.ascii[b];
+            if ((e & 3u) == UC_OTHER) buf[nb++] = (uint8_t)((b - 'A' < 26u) ? b + 32u : b);
             ++q;
             continue;
         }
-        if ((b & 0xC0) == 0x80) { ++q; continue; }
+        if ((b & 0xC0u) == 0x80u) { ++q; continue; }
         int len;
-        uint32_t cp = decode(S, q, b, &len);
-        uint32_t e = uentry(T, cp);
-        if ((e & 3u) == UC_OTHER) nb = append_norm(T, S, e, q, len, buf, nb);
+        const uint32_t e = uentry(T, decode(C, q, b, &len));
+        if ((e & 3u) == UC_OTHER) nb = append_norm(C, e, q, len, buf, nb);
         q += len;
     }
-    BufBytes w{buf};
-    return wordpiece(T, w, nb, out);
+    return wordpiece_general(T, buf, nb, out);
 }
 
-// Tokenizes an ISO piece: one isolated char (punctuation or CJK).
-__device__ int iso_tokens(const DevTok &T, const Src &S, const uint32_t *ascii, int64_t p, uint32_t *out) {
-    uint8_t buf[16];
-    int nb;
-    uint32_t b = S.byte(p);
-    if (b < 0x80) {
-        uint32_t e = ascii[b];
-        nb = append_norm(T, S, e, p, 1, buf, 0);
-    } else {
-        int len;
-        uint32_t cp = decode(S, p, b, &len);
-        nb = append_norm(T, S, uentry(T, cp), p, len, buf, 0);
+// WordPiece on an ASCII word of L <= 16 lower-cased bytes in registers
+// (every byte is one char, so "end -= 1 char" is "end -= 1").
+__device__ __forceinline__ int wordpiece16(const DevTok &T, const W16 &w, int L, lds_u16 *out) {
+    int n = 0, start = 0;
+    while (start < L) {
+        const int lim = start == 0 ? T.maxlen_first : T.maxlen_cont;
+        int end = start + lim < L ? start + lim : L;
+        const W16 sh = start ? shift_right_bytes(w, start) : w;
+        const uint32_t cont = start > 0 ? 1u : 0u;
+        int id = -1;
+        for (; end > start; --end) {
+            id = probe16(T, keep_bytes(sh, end - start), (uint32_t)(end - start), cont);
+            if (id >= 0) break;
+        }
+        if (id < 0) {
+            out[0] = (uint16_t)T.unk_id;
+            return 1;
+        }
+        out[n++] = (uint16_t)id;
+        start = end;
     }
-    BufBytes w{buf};
-    return wordpiece(T, w, nb, out);
+    return n;
+}
+
+// Record end (first record start > p) for the general paths.
+__device__ int64_t rec_end_of(const Ctx &C, const lds_u16 *rb, int nrb, bool rb_ok, int64_t rb_next, int64_t p) {
+    if (rb_ok) {
+        const int rel = (int)(p - C.w0);
+        int lo = 0, hi = nrb;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if ((int)rb[mid] <= rel) lo = mid + 1; else hi = mid;
+        }
+        return lo < nrb ? C.w0 + rb[lo] : rb_next;
+    }
+    int64_t lo = 0, hi = C.R;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if ((int64_t)C.off[mid] <= p) lo = mid + 1; else hi = mid;
+    }
+    const int64_t e = (int64_t)C.off[lo];
+    return e < C.N ? e : C.N;
+}
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint4 load16(const uint8_t *text, int64_t p, int64_t N) {
+    if (p >= 0 && p + 16 <= N) {
+        const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(text + p));
+        return make_uint4(x.x, x.y, x.z, x.w);
+    }
+    uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
+    for (int k = 0; k < 16; ++k) {
+        if (p + k < 0 || p + k >= N) continue;
+        const uint32_t v = (uint32_t)text[p + k] << (8 * (k & 3));
+        if (k < 4) w0 |= v; else if (k < 8) w1 |= v; else if (k < 12) w2 |= v; else w3 |= v;
+    }
+    return make_uint4(w0, w1, w2, w3);
 }
 
 }  // namespace
 
 // -----------------------------------------------------------------------------
+// Per chunk: record ranges touching its window (so the tokenize kernel never
+// binary-searches the offsets serially).
+__global__ __launch_bounds__(256) void k_chunk_ranges(const uint64_t *__restrict__ off, int64_t R, int64_t n_chunks,
+                                                      uint32_t *__restrict__ ranges) {
+    const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (c >= n_chunks) return;
+    auto lower = [&](int64_t x) {  // first r in [0, R] with off[r] >= x (R+1 if none)
+        int64_t lo = 0, hi = R + 1;
+        while (lo < hi) {
+            const int64_t m = (lo + hi) >> 1;
+            if ((int64_t)off[m] < x) lo = m + 1; else hi = m;
+        }
+        return lo;
+    };
+    const int64_t c0 = c * CHUNK;
+    ranges[3 * c + 0] = (uint32_t)lower(c0 - HALO_L);
+    ranges[3 * c + 1] = (uint32_t)lower(c0 - HALO_L + WIN);
+    ranges[3 * c + 2] = (uint32_t)lower(c0);
+}
+
 __global__ __launch_bounds__(TOK_THREADS) void k_wordpiece_chunks(
     DevTok T, const uint8_t *__restrict__ text, int64_t N, const uint64_t *__restrict__ off, int64_t R,
-    uint32_t *__restrict__ tokc, uint32_t *__restrict__ chunk_cnt, uint32_t *__restrict__ rec_local) {
-    __shared__ __attribute__((aligned(16))) uint8_t win[WIN];
-    __shared__ uint8_t rflag[WIN];
-    __shared__ uint8_t vcl[CHUNK];          // visible class per owned byte; later: tokens per piece
-    __shared__ uint32_t pieces[CHUNK];      // (pos - c0) | kind << 16
-    __shared__ uint32_t stage[STAGE];       // tokens, indexed by piece byte position
-    __shared__ uint16_t poff[CHUNK];        // token offset of each piece within the chunk
-    __shared__ uint32_t ascii[128];
-    __shared__ int32_t rb[RB_CAP];          // record starts inside the window (relative)
-    __shared__ uint32_t scratch[TOK_THREADS / 64 + 1];
-    __shared__ int64_t sh_misc[4];          // rb_next, r_lo, r_hi, state-in
-    __shared__ int sh_nrb;
+    const uint32_t *__restrict__ ranges, uint32_t *__restrict__ tokc, uint32_t *__restrict__ chunk_cnt,
+    uint32_t *__restrict__ rec_local) {
+    __shared__ __attribute__((aligned(16))) uint8_t s_win[WIN];
+    __shared__ uint32_t s_rbits[RBITS_WORDS + 1];
+    __shared__ uint16_t s_pieces[CHUNK];   // (pos - c0) | kind << 12
+    __shared__ uint16_t s_stage[STAGE];    // ids staged at their piece's byte position
+    __shared__ uint8_t s_cnt[CHUNK];       // ids per piece
+    __shared__ uint16_t s_poff[CHUNK];     // id offset of each piece in the chunk
+    __shared__ uint32_t s_ascii[128];
+    __shared__ int32_t s_ascii_id[128];
+    __shared__ uint16_t s_rb[RB_CAP];
+    __shared__ uint32_t s_scratch[TOK_THREADS / 64 + 2];
 
     const int tid = threadIdx.x;
     const int64_t c0 = (int64_t)blockIdx.x * CHUNK;
     const int64_t c1 = c0 + CHUNK < N ? c0 + CHUNK : N;
     const int64_t w0 = c0 - HALO_L;
+    const lds_u8 *win = (const lds_u8 *)s_win;
+    const lds_u32 *rbits = (const lds_u32 *)s_rbits;
 
-    // ---- 1. stage the window; ASCII table ----------------------------------
-    for (int v = tid; v < WIN / 16; v += TOK_THREADS) {
-        int64_t p = w0 + (int64_t)v * 16;
-        uint4 x;
-        if (p >= 0 && p + 16 <= N) {
-            x = *reinterpret_cast<const uint4 *>(text + p);
-        } else {
-            uint8_t tmp[16];
-            for (int k = 0; k < 16; ++k) tmp[k] = (p + k >= 0 && p + k < N) ? text[p + k] : 0;
-            x = *reinterpret_cast<uint4 *>(tmp);
+    // ---- 1. load -------------------------------------------------------------
+    const uint4 v = load16(text, c0 + 16 * tid, N);
+    *reinterpret_cast<uint4 *>(s_win + HALO_L + 16 * tid) = v;
+    if (tid < (WIN - CHUNK) / 16) {  // 1 left + 15 right halo pieces
+        const int64_t p = tid == 0 ? w0 : c0 + CHUNK + 16 * (tid - 1);
+        *reinterpret_cast<uint4 *>(s_win + (p - w0)) = load16(text, p, N);
+    }
+    if (tid <= RBITS_WORDS) s_rbits[tid] = 0;
+    if (tid < 128) {
+        s_ascii[tid] = T.uentry[(uint32_t)T.upage[0] * 128u + tid];
+        s_ascii_id[tid] = T.ascii_id[tid];
+    }
+    const int64_t ra = ranges[3 * blockIdx.x], rz = ranges[3 * blockIdx.x + 1], r_lo = ranges[3 * blockIdx.x + 2];
+    const int nrb = (int)(rz - ra);
+    const bool rb_ok = nrb <= RB_CAP;
+    int64_t rb_next = rz <= R ? (int64_t)off[rz] : N;
+    if (rb_next > N) rb_next = N;
+    __syncthreads();
+    for (int k = tid; k < nrb; k += TOK_THREADS) {
+        const int rel = (int)((int64_t)off[ra + k] - w0);
+        atomicOr(&s_rbits[rel >> 5], 1u << (rel & 31));
+        if (rb_ok) s_rb[k] = (uint16_t)rel;
+    }
+    __syncthreads();
+
+    const Ctx C{&T, win, rbits, (const lds_u32 *)s_ascii, w0, text, N, off, R};
+
+    // ---- 2. register-resident classification of the lane's 16 bytes ----------
+    const int64_t s0 = c0 + 16 * tid;
+    const int nown = s0 >= c1 ? 0 : (int)(c1 - s0 < 16 ? c1 - s0 : 16);
+    const int rel0 = HALO_L + 16 * tid;  // window index of s0 (multiple of 16)
+    const uint32_t rmask = (rbits[rel0 >> 5] >> (rel0 & 31)) & 0xFFFFu;
+    const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+    uint64_t cls = 0;
+    uint32_t leads = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const uint32_t b = (wv[i >> 2] >> (8 * (i & 3))) & 0xFFu;
+        const uint32_t c = b < 0x80u ? ascii_vclass(b) : V_NONE;
+        cls |= (uint64_t)c << (4 * i);
+        leads |= (b >= 0xC0u ? 1u : 0u) << i;
+    }
+    if (nown < 16) {
+        cls &= nown ? ((1ull << (4 * nown)) - 1ull) : 0ull;
+        leads &= (1u << nown) - 1u;
+    }
+    while (leads) {  // non-ASCII lead bytes: decode + Unicode table
+        const int i = __builtin_ctz(leads);
+        leads &= leads - 1;
+        const uint32_t c = vclass_general(C, s0 + i);
+        cls = (cls & ~(0xFull << (4 * i))) | ((uint64_t)c << (4 * i));
+    }
+    if (T.n_special) {  // added tokens: an opener in [s0 - max_special_len + 1, s0 + 16)
+        bool near = false;
+        for (int d = 1 - T.max_special_len; d < nown; ++d) near |= s0 + d >= 0 && C.byte(s0 + d) == T.opener;
+        if (near) {
+            for (int i = 0; i < nown; ++i) {
+                const uint32_t c = vclass_general(C, s0 + i);
+                cls = (cls & ~(0xFull << (4 * i))) | ((uint64_t)c << (4 * i));
+            }
         }
-        *reinterpret_cast<uint4 *>(win + v * 16) = x;
-        *reinterpret_cast<uint4 *>(rflag + v * 16) = make_uint4(0, 0, 0, 0);
     }
-    if (tid < 128) ascii[tid] = T.uentry[(uint32_t)T.upage[0] * 128u + tid];
-    if (tid == 0) {
-        // records whose start lies in [w0, w0 + WIN]: r in [ra, rb_)
-        int64_t lo = 0, hi = R + 1;
-        while (lo < hi) { int64_t m = (lo + hi) >> 1; if ((int64_t)off[m] < w0) lo = m + 1; else hi = m; }
-        int64_t ra = lo;
-        lo = ra; hi = R + 1;
-        while (lo < hi) { int64_t m = (lo + hi) >> 1; if ((int64_t)off[m] < w0 + WIN) lo = m + 1; else hi = m; }
-        int64_t rz = lo;
-        sh_misc[0] = rz <= R ? (int64_t)off[rz] : N;   // next record start after the window
-        if (sh_misc[0] > N) sh_misc[0] = N;
-        sh_misc[1] = ra;
-        sh_misc[2] = rz;
-        // owned boundaries: off[r] in [c0, c1)
-        lo = 0; hi = R + 1;
-        while (lo < hi) { int64_t m = (lo + hi) >> 1; if ((int64_t)off[m] < c0) lo = m + 1; else hi = m; }
-        sh_misc[3] = lo;
-        sh_nrb = (int)(rz - ra);
-    }
-    __syncthreads();
-    const int64_t rb_next = sh_misc[0];
-    const int64_t ra = sh_misc[1];
-    const int nrb_all = sh_nrb;
-    const bool rb_ok = nrb_all <= RB_CAP;
-    for (int k = tid; k < nrb_all; k += TOK_THREADS) {
-        int rel = (int)((int64_t)off[ra + k] - w0);
-        rflag[rel] = 1;
-        if (rb_ok) rb[k] = rel;
-    }
-    __syncthreads();
-    // rb[] is sorted; empty records repeat a start, which the "first start
-    // > p" search in rec_end_of tolerates.
-
-    Src S{win, rflag, w0, text, N, off, R};
-
-    // ---- 2. classify owned bytes; per-thread summary of the visible state --
-    const int64_t s0 = c0 + (int64_t)tid * BYTES_PER_THREAD;
-    const int64_t s1 = s0 + BYTES_PER_THREAD < c1 ? s0 + BYTES_PER_THREAD : c1;
-    bool maybe_special = false;
-    if (T.n_special) {
-        for (int64_t q = s0 - T.max_special_len; q < s1; ++q)
-            if (q >= 0 && q < N && S.byte(q) == T.opener) { maybe_special = true; break; }
-    }
-    // summary encoding: 0 = pass-through, 0x100 | v = state after segment
+    // lane summary for the carry scan: 0 = pass-through, 0x100 | v = state after
     uint32_t summ = 0;
-    for (int64_t q = s0; q < s1; ++q) {
-        if (rflag[q - w0]) summ = 0x100 | V_NONE;
-        uint8_t v = vclass(T, S, ascii, q, maybe_special);
-        vcl[q - c0] = v;
-        if (v != V_NONE) summ = 0x100 | v;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        if ((rmask >> i) & 1u) summ = 0x100u | V_NONE;
+        const uint32_t c = (uint32_t)(cls >> (4 * i)) & 0xFu;
+        if (c != V_NONE) summ = 0x100u | c;
     }
-
     // state before the chunk: last visible char of the same record before c0
     if (tid == 0) {
         uint32_t st = V_NONE;
         int64_t q = c0 - 1;
-        bool msp = T.n_special != 0;
-        while (q >= 0 && !S.rstart(q + 1)) {
+        while (q >= 0 && !C.rstart(q + 1)) {
             int64_t cs = q;
             int k = 0;
-            while (k < 3 && cs > 0 && (S.byte(cs) & 0xC0) == 0x80 && !S.rstart(cs)) { --cs; ++k; }
-            uint8_t v = vclass(T, S, ascii, cs, msp);
-            if (v != V_NONE) {
-                // a lead byte whose sequence is invalid does not cover q: its
-                // continuation bytes are invisible and the lead itself is DEL,
-                // so a visible result always belongs to a char covering q.
-                st = v;
-                break;
-            }
+            while (k < 3 && cs > 0 && (C.byte(cs) & 0xC0u) == 0x80u && !C.rstart(cs)) { --cs; ++k; }
+            const uint32_t vc = vclass_general(C, cs);
+            if (vc != V_NONE) { st = vc; break; }
             q = cs - 1;
         }
-        scratch[TOK_THREADS / 64] = st;
+        s_scratch[TOK_THREADS / 64] = st;
     }
     __syncthreads();
-    const uint32_t chunk_state = scratch[TOK_THREADS / 64];
-    const int64_t r_lo = sh_misc[3];
+    const uint32_t chunk_state = s_scratch[TOK_THREADS / 64];
     __syncthreads();
+    const uint32_t st_in = block_excl_last_scan<TOK_THREADS>(summ, s_scratch);
 
-    uint32_t st_in = block_excl_last_scan<TOK_THREADS>(summ, scratch);
-    uint32_t state = (st_in & 0x100) ? (st_in & 0xFF) : chunk_state;
-
-    // ---- 3/4. piece starts, block-compacted into pieces[] ---------------------
-    uint32_t npt = 0;
+    // ---- 3. piece starts -------------------------------------------------------
+    uint32_t pmask = 0;
     {
-        uint32_t sst = state;
-        for (int64_t q = s0; q < s1; ++q) {
-            if (rflag[q - w0]) sst = V_NONE;
-            uint8_t v = vcl[q - c0];
-            if (v == V_NONE) continue;
-            if (v == V_SPEC || v == V_ISO || (v == V_OTHER && sst != V_OTHER)) ++npt;
-            sst = v;
+        uint32_t st = (st_in & 0x100u) ? (st_in & 0xFFu) : chunk_state;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            if ((rmask >> i) & 1u) st = V_NONE;
+            const uint32_t c = (uint32_t)(cls >> (4 * i)) & 0xFu;
+            if (c != V_NONE) {
+                if (c == V_SPEC || c == V_ISO || (c == V_OTHER && st != V_OTHER)) pmask |= 1u << i;
+                st = c;
+            }
         }
     }
     uint32_t np_total;
-    uint32_t pbase = block_excl_sum<TOK_THREADS>(npt, &np_total, scratch);
-    {
-        uint32_t sst = state;
-        for (int64_t q = s0; q < s1; ++q) {
-            if (rflag[q - w0]) sst = V_NONE;
-            uint8_t v = vcl[q - c0];
-            if (v == V_NONE) continue;
-            if (v == V_SPEC || v == V_ISO || (v == V_OTHER && sst != V_OTHER))
-                pieces[pbase++] = (uint32_t)(q - c0) | ((uint32_t)v << 16);
-            sst = v;
-        }
+    uint32_t pbase = block_excl_sum<TOK_THREADS>((uint32_t)__builtin_popcount(pmask), &np_total, s_scratch);
+    for (uint32_t m = pmask; m;) {
+        const int i = __builtin_ctz(m);
+        m &= m - 1;
+        const uint32_t c = (uint32_t)(cls >> (4 * i)) & 0xFu;
+        s_pieces[pbase++] = (uint16_t)((16 * tid + i) | (c << 12));
     }
     __syncthreads();
     const int np = (int)np_total;
 
-    // ---- 5. tokenize pieces -------------------------------------------------
-    uint8_t *cnt = vcl;  // reuse: tokens per piece (<= 100)
-    for (int i = tid; i < np; i += TOK_THREADS) {
-        uint32_t pc = pieces[i];
-        int64_t p = c0 + (pc & 0xFFFF);
-        uint32_t kind = pc >> 16;
-        uint32_t *out = stage + (pc & 0xFFFF);
-        int k;
+    // ---- 4. tokenize pieces -------------------------------------------------------
+    const lds_u32 *w32 = (const lds_u32 *)s_win;
+    for (int pi = tid; pi < np; pi += TOK_THREADS) {
+        const uint32_t pc = s_pieces[pi];
+        const int prel = (int)(pc & 0xFFFu);
+        const uint32_t kind = pc >> 12;
+        const int64_t p = c0 + prel;
+        lds_u16 *ids = (lds_u16 *)s_stage + prel;
+        int k = 0;
         if (kind == V_SPEC) {
-            int m = special_match(T, S, p);
-            out[0] = (uint32_t)T.special_id[m < 0 ? 0 : m];
+            const int m = special_match(C, p);
+            ids[0] = (uint16_t)T.special_id[m < 0 ? 0 : m];
             k = 1;
         } else if (kind == V_ISO) {
-            k = iso_tokens(T, S, ascii, p, out);
+            const uint32_t b = win[prel + HALO_L];
+            if (b < 0x80u) {
+                ids[0] = (uint16_t)s_ascii_id[b];
+                k = 1;
+            } else {
+                int len;
+                const uint32_t e = uentry(T, decode(C, p, b, &len));
+                uint8_t buf[16];
+                const int nb = append_norm(C, e, p, len, buf, 0);
+                k = wordpiece_general(T, buf, nb, ids);
+            }
         } else {
-            int64_t rend = rec_end_of(S, rb, nrb_all, rb_next, rb_ok, p);
-            k = word_tokens(T, S, ascii, p, rend, out);
+            // fast path: ASCII word of <= 16 bytes (the window holds p .. p+16)
+            const int wr = prel + HALO_L;
+            const int a = wr >> 2;
+            const uint32_t sh = (uint32_t)(wr & 3);
+            const uint32_t x0 = w32[a], x1 = w32[a + 1], x2 = w32[a + 2], x3 = w32[a + 3], x4 = w32[a + 4];
+            const W16 raw{__builtin_amdgcn_alignbyte(x1, x0, sh), __builtin_amdgcn_alignbyte(x2, x1, sh),
+                          __builtin_amdgcn_alignbyte(x3, x2, sh), __builtin_amdgcn_alignbyte(x4, x3, sh)};
+            const uint32_t b16 = (x4 >> (8 * sh)) & 0xFFu;  // byte at p + 16
+            const uint32_t om = msb4(swar_alnum(raw.x)) | (msb4(swar_alnum(raw.y)) << 4) |
+                                (msb4(swar_alnum(raw.z)) << 8) | (msb4(swar_alnum(raw.w)) << 12);
+            int L = __builtin_ctz(~om);  // leading ASCII letters/digits, <= 16
+            // a record start at p+1 .. p+16 ends the word
+            const int rb0 = wr + 1;
+            const uint64_t rw = ((uint64_t)rbits[(rb0 >> 5) + 1] << 32) | rbits[rb0 >> 5];
+            const uint32_t rbm = (uint32_t)(rw >> (rb0 & 31)) & 0xFFFFu;
+            const int Lr = rbm ? __builtin_ctz(rbm) + 1 : 17;
+            bool fast;
+            if (Lr <= L) {
+                L = Lr;
+                fast = true;
+            } else {
+                const uint32_t t = L < 16 ? (((L < 4 ? raw.x : L < 8 ? raw.y : L < 12 ? raw.z : raw.w) >> (8 * (L & 3))) & 0xFFu)
+                                          : b16;
+                // the word ends at an ASCII whitespace/punctuation byte (or the arena end)
+                const uint32_t tc = t < 0x80u ? ascii_vclass(t) : V_NONE;
+                fast = tc == V_WS || tc == V_ISO || p + L >= N;
+            }
+            if (fast) {
+                const W16 lw = keep_bytes(W16{swar_lower(raw.x), swar_lower(raw.y), swar_lower(raw.z), swar_lower(raw.w)}, L);
+                k = wordpiece16(T, lw, L, ids);
+            } else {
+                k = word_general(C, p, rec_end_of(C, (const lds_u16 *)s_rb, nrb, rb_ok, rb_next, p), ids);
+            }
         }
-        cnt[i] = (uint8_t)k;
+        s_cnt[pi] = (uint8_t)k;
     }
     __syncthreads();
 
-    // ---- 6. compact staged tokens into this chunk's tokc region --------------
+    // ---- 5. compact ids into this chunk's tokc slice ------------------------------
     const int per = (np + TOK_THREADS - 1) / TOK_THREADS;
-    const int a = tid * per < np ? tid * per : np;
-    const int b = a + per < np ? a + per : np;
+    const int a0 = tid * per < np ? tid * per : np;
+    const int a1 = a0 + per < np ? a0 + per : np;
     uint32_t mine = 0;
-    for (int i = a; i < b; ++i) mine += cnt[i];
+    for (int i = a0; i < a1; ++i) mine += s_cnt[i];
     uint32_t total;
-    uint32_t base = block_excl_sum<TOK_THREADS>(mine, &total, scratch);
+    uint32_t base = block_excl_sum<TOK_THREADS>(mine, &total, s_scratch);
     uint32_t *dst = tokc + (int64_t)blockIdx.x * STAGE;
-    for (int i = a; i < b; ++i) {
-        poff[i] = (uint16_t)base;
-        const uint32_t *src = stage + (pieces[i] & 0xFFFF);
-        for (int k = 0; k < cnt[i]; ++k) dst[base + k] = src[k];
-        base += cnt[i];
+    for (int i = a0; i < a1; ++i) {
+        s_poff[i] = (uint16_t)base;
+        const int prel = s_pieces[i] & 0xFFF;
+        const int k = s_cnt[i];
+        for (int j = 0; j < k; ++j) dst[base + j] = s_stage[prel + j];
+        base += k;
     }
     __syncthreads();
     if (tid == 0) chunk_cnt[blockIdx.x] = total;
-
-    // record boundaries owned by this chunk: local token offset of the first
-    // piece at or after the boundary
     for (int64_t r = r_lo + tid; r <= R; r += TOK_THREADS) {
-        int64_t pos = (int64_t)off[r];
+        const int64_t pos = (int64_t)off[r];
         if (pos >= c1) break;
-        int rel = (int)(pos - c0);
+        const int rel = (int)(pos - c0);
         int lo = 0, hi = np;
         while (lo < hi) {
-            int m = (lo + hi) >> 1;
-            if ((int)(pieces[m] & 0xFFFF) < rel) lo = m + 1; else hi = m;
+            const int m = (lo + hi) >> 1;
+            if ((int)(s_pieces[m] & 0xFFF) < rel) lo = m + 1; else hi = m;
         }
-        rec_local[r] = lo < np ? (uint32_t)poff[lo] : total;
+        rec_local[r] = lo < np ? (uint32_t)s_poff[lo] : total;
     }
 }
 
 hipError_t launch_wordpiece_chunks(const DevTok &T, const uint8_t *text, int64_t N, const uint64_t *off, int64_t R,
-                                   uint32_t *tokc, uint32_t *chunk_cnt, uint32_t *rec_local, hipStream_t st) {
+                                   uint32_t *ranges, uint32_t *tokc, uint32_t *chunk_cnt, uint32_t *rec_local,
+                                   hipStream_t st) {
     const int64_t n_chunks = (N + CHUNK - 1) / CHUNK;
     if (n_chunks == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_chunk_ranges, dim3((unsigned)((n_chunks + 255) / 256)), dim3(256), 0, st, off, R, n_chunks,
+                       ranges);
     hipLaunchKernelGGL(k_wordpiece_chunks, dim3((unsigned)n_chunks), dim3(TOK_THREADS), 0, st, T, text, N, off, R,
-                       tokc, chunk_cnt, rec_local);
+                       ranges, tokc, chunk_cnt, rec_local);
     return hipGetLastError();
 }
 
