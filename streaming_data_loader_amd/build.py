@@ -40,18 +40,21 @@ def _newer(dst, srcs):
     return all(os.path.getmtime(s) <= t for s in srcs)
 
 
-def build(verbose=False, force=False, jobs=4):
-    os.makedirs(BUILD, exist_ok=True)
+def build(verbose=False, force=False, jobs=4, defines=(), lib=None, build_dir=None):
+    """defines: extra -D macros (diagnostic builds go to their own lib/build_dir)."""
+    lib = lib or LIB
+    bdir = build_dir or BUILD
+    os.makedirs(bdir, exist_ok=True)
     hipcc = _hipcc()
     hdrs = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(REPO, "include", "sdl_batcher.h")]
     objs, todo = [], []
     for s in SOURCES:
         src = os.path.join(CSRC, s)
-        obj = os.path.join(BUILD, s + ".o")
+        obj = os.path.join(bdir, s + ".o")
         objs.append(obj)
         if force or not _newer(obj, [src] + hdrs):
             lang = ["-x", "hip"] if s.endswith(".hip") else []
-            todo.append([hipcc] + FLAGS + lang + ["-c", src, "-o", obj])
+            todo.append([hipcc] + FLAGS + [f"-D{d}" for d in defines] + lang + ["-c", src, "-o", obj])
 
     def run(cmd):
         if verbose:
@@ -65,9 +68,20 @@ def build(verbose=False, force=False, jobs=4):
         for err in ex.map(run, todo):
             if verbose and err:
                 print(err, file=sys.stderr)
-    if force or todo or not _newer(LIB, objs):
-        run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs + ["-ldl"])
-    return LIB
+    if force or todo or not _newer(lib, objs):
+        run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib] + objs + ["-ldl"])
+    return lib
+
+
+def build_ablations(levels=(1, 3)):
+    """Diagnostic builds with phases of the tokenize kernel compiled out
+    (SDL_ABLATE=1: no WordPiece; 3: load only) -> build/abl<N>/libsdl_batcher.so."""
+    out = []
+    for n in levels:
+        d = os.path.join(REPO, "build", f"abl{n}")
+        out.append(build(defines=(f"SDL_ABLATE={n}",), lib=os.path.join(d, "libsdl_batcher.so"),
+                         build_dir=os.path.join(d, "obj")))
+    return out
 
 
 if __name__ == "__main__":

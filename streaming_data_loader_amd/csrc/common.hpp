@@ -18,8 +18,8 @@ enum : uint8_t { V_NONE = 0, V_WS = 1, V_ISO = 2, V_OTHER = 3, V_SPEC = 4 };
 constexpr int TOK_THREADS = 256;
 constexpr int CHUNK = 4096;                       // text bytes owned by one workgroup
 constexpr int BYTES_PER_THREAD = CHUNK / TOK_THREADS;
-constexpr int HALO_L = 16;                        // look-back bytes staged in LDS
-constexpr int HALO_R = 240;                       // look-ahead bytes staged in LDS
+constexpr int HALO_L = 32;                        // look-back bytes staged in LDS
+constexpr int HALO_R = 224;                       // look-ahead bytes staged in LDS
 constexpr int WIN = HALO_L + CHUNK + HALO_R;      // 4352 bytes of text in LDS
 constexpr int STAGE = CHUNK + 128;                // token slots per chunk (>= tokens owned)
 constexpr int RB_CAP = 256;                       // record starts listed in LDS per window

@@ -470,8 +470,8 @@ __global__ __launch_bounds__(TOK_THREADS) void k_wordpiece_chunks(
     // ---- 1. load -------------------------------------------------------------
     const uint4 v = load16(text, c0 + 16 * tid, N);
     *reinterpret_cast<uint4 *>(s_win + HALO_L + 16 * tid) = v;
-    if (tid < (WIN - CHUNK) / 16) {  // 1 left + 15 right halo pieces
-        const int64_t p = tid == 0 ? w0 : c0 + CHUNK + 16 * (tid - 1);
+    if (tid < (WIN - CHUNK) / 16) {  // 2 left + 14 right halo pieces
+        const int64_t p = tid < HALO_L / 16 ? w0 + 16 * tid : c0 + CHUNK + 16 * (tid - HALO_L / 16);
         *reinterpret_cast<uint4 *>(s_win + (p - w0)) = load16(text, p, N);
     }
     if (tid <= RBITS_WORDS) s_rbits[tid] = 0;
@@ -493,6 +493,12 @@ __global__ __launch_bounds__(TOK_THREADS) void k_wordpiece_chunks(
     __syncthreads();
 
     const Ctx C{&T, win, rbits, (const lds_u32 *)s_ascii, w0, text, N, off, R};
+#if defined(SDL_ABLATE) && SDL_ABLATE >= 3
+    // diagnostic: load only; every record gets 0 ids (so later stages stay in bounds)
+    if (tid == 0) chunk_cnt[blockIdx.x] = s_win[HALO_L + (blockIdx.x & 1023)] & 0u;
+    for (int64_t r = r_lo + tid; r <= R && (int64_t)off[r] < c1; r += TOK_THREADS) rec_local[r] = 0;
+    return;
+#endif
 
     // ---- 2. register-resident classification of the lane's 16 bytes ----------
     const int64_t s0 = c0 + 16 * tid;
@@ -519,9 +525,14 @@ __global__ __launch_bounds__(TOK_THREADS) void k_wordpiece_chunks(
         const uint32_t c = vclass_general(C, s0 + i);
         cls = (cls & ~(0xFull << (4 * i))) | ((uint64_t)c << (4 * i));
     }
-    if (T.n_special) {  // added tokens: an opener in [s0 - max_special_len + 1, s0 + 16)
-        bool near = false;
-        for (int d = 1 - T.max_special_len; d < nown; ++d) near |= s0 + d >= 0 && C.byte(s0 + d) == T.opener;
+    if (T.n_special) {  // added tokens: an opener byte in [s0 - 24, s0 + 16)?
+        const uint32_t ob = T.opener * 0x01010101u;
+        auto has = [&](uint32_t x) { x ^= ob; return ((x - 0x01010101u) & ~x & 0x80808080u) != 0u; };
+        const lds_u32 *w32 = (const lds_u32 *)s_win;
+        const int d0 = (rel0 - 24) >> 2;
+        bool near = has(v.x) || has(v.y) || has(v.z) || has(v.w);
+#pragma unroll
+        for (int k = 0; k < 6; ++k) near |= has(w32[d0 + k]);
         if (near) {
             for (int i = 0; i < nown; ++i) {
                 const uint32_t c = vclass_general(C, s0 + i);
@@ -581,67 +592,159 @@ __global__ __launch_bounds__(TOK_THREADS) void k_wordpiece_chunks(
     __syncthreads();
     const int np = (int)np_total;
 
-    // ---- 4. tokenize pieces -------------------------------------------------------
-    const lds_u32 *w32 = (const lds_u32 *)s_win;
-    for (int pi = tid; pi < np; pi += TOK_THREADS) {
-        const uint32_t pc = s_pieces[pi];
-        const int prel = (int)(pc & 0xFFFu);
-        const uint32_t kind = pc >> 12;
-        const int64_t p = c0 + prel;
-        lds_u16 *ids = (lds_u16 *)s_stage + prel;
-        int k = 0;
-        if (kind == V_SPEC) {
-            const int m = special_match(C, p);
-            ids[0] = (uint16_t)T.special_id[m < 0 ? 0 : m];
-            k = 1;
-        } else if (kind == V_ISO) {
-            const uint32_t b = win[prel + HALO_L];
-            if (b < 0x80u) {
-                ids[0] = (uint16_t)s_ascii_id[b];
-                k = 1;
-            } else {
-                int len;
-                const uint32_t e = uentry(T, decode(C, p, b, &len));
-                uint8_t buf[16];
-                const int nb = append_norm(C, e, p, len, buf, 0);
-                k = wordpiece_general(T, buf, nb, ids);
+    // ---- 4. tokenize pieces: one probe per lane per iteration -------------------
+    // Lanes pull pieces from a block-wide LDS queue; an ASCII word of <= 16
+    // bytes becomes a WordPiece state (word, start, end, slot) advanced by one
+    // vocab probe per iteration, so no lane idles behind a long word.  Other
+    // pieces are finished in the pull step (added tokens, one-byte punctuation)
+    // or by the general path.
+    if (tid == 0) s_scratch[TOK_THREADS / 64 + 1] = 0;
+    __syncthreads();
+#if defined(SDL_ABLATE) && SDL_ABLATE >= 1
+    for (int i = tid; i < np; i += TOK_THREADS) {
+        s_stage[s_pieces[i] & 0xFFF] = (uint16_t)i;
+        s_cnt[i] = 1;
+    }
+    if (false)
+#endif
+    {
+        const lds_u32 *w32 = (const lds_u32 *)s_win;
+        lds_u16 *stage = (lds_u16 *)s_stage;
+        const int lane = tid & 63;
+        bool exhausted = false;
+        bool active = false;  // a fast WordPiece state is live
+        int pi = 0, prel = 0, L = 0, start = 0, end = 0, nout = 0;
+        uint32_t slot = 0;
+        bool fresh = true;
+        W16 w{0, 0, 0, 0}, cand{0, 0, 0, 0};
+        uint32_t key = 0;
+        for (;;) {
+            // (a) pull: idle lanes take the next pieces of the queue
+            const bool need = !active && !exhausted;
+            const uint64_t nm = __ballot(need);
+            if (nm) {
+                const int leader = __builtin_ctzll(nm);
+                uint32_t base = 0;
+                if (lane == leader) base = atomicAdd(&s_scratch[TOK_THREADS / 64 + 1], (uint32_t)__popcll(nm));
+                base = __shfl(base, leader, 64);
+                if (need) {
+                    const int idx = (int)base + __popcll(nm & ((1ull << lane) - 1ull));
+                    if (idx >= np) {
+                        exhausted = true;
+                    } else {
+                        pi = idx;
+                        const uint32_t pc = s_pieces[idx];
+                        prel = (int)(pc & 0xFFFu);
+                        const uint32_t kind = pc >> 12;
+                        const int64_t p = c0 + prel;
+                        lds_u16 *out = stage + prel;
+                        if (kind == V_SPEC) {
+                            const int m = special_match(C, p);
+                            out[0] = (uint16_t)T.special_id[m < 0 ? 0 : m];
+                            s_cnt[idx] = 1;
+                        } else if (kind == V_ISO) {
+                            const uint32_t b = win[prel + HALO_L];
+                            if (b < 0x80u) {
+                                out[0] = (uint16_t)s_ascii_id[b];
+                                s_cnt[idx] = 1;
+                            } else {
+                                int len;
+                                const uint32_t e = uentry(T, decode(C, p, b, &len));
+                                uint8_t buf[16];
+                                const int nb = append_norm(C, e, p, len, buf, 0);
+                                s_cnt[idx] = (uint8_t)wordpiece_general(T, buf, nb, out);
+                            }
+                        } else {
+                            const int wr = prel + HALO_L;
+                            const int a = wr >> 2;
+                            const uint32_t sh = (uint32_t)(wr & 3);
+                            const uint32_t x0 = w32[a], x1 = w32[a + 1], x2 = w32[a + 2], x3 = w32[a + 3], x4 = w32[a + 4];
+                            const W16 raw{__builtin_amdgcn_alignbyte(x1, x0, sh), __builtin_amdgcn_alignbyte(x2, x1, sh),
+                                          __builtin_amdgcn_alignbyte(x3, x2, sh), __builtin_amdgcn_alignbyte(x4, x3, sh)};
+                            const uint32_t b16 = (x4 >> (8 * sh)) & 0xFFu;  // byte at p + 16
+                            const uint32_t om = msb4(swar_alnum(raw.x)) | (msb4(swar_alnum(raw.y)) << 4) |
+                                                (msb4(swar_alnum(raw.z)) << 8) | (msb4(swar_alnum(raw.w)) << 12);
+                            int Lw = __builtin_ctz(~om);  // leading ASCII letters/digits, <= 16
+                            const int rb0 = wr + 1;     // a record start at p+1 .. p+16 ends the word
+                            const uint64_t rw = ((uint64_t)rbits[(rb0 >> 5) + 1] << 32) | rbits[rb0 >> 5];
+                            const uint32_t rbm = (uint32_t)(rw >> (rb0 & 31)) & 0xFFFFu;
+                            const int Lr = rbm ? __builtin_ctz(rbm) + 1 : 17;
+                            bool fast;
+                            if (Lr <= Lw) {
+                                Lw = Lr;
+                                fast = true;
+                            } else {
+                                const uint32_t t =
+                                    Lw < 16 ? (((Lw < 4 ? raw.x : Lw < 8 ? raw.y : Lw < 12 ? raw.z : raw.w) >> (8 * (Lw & 3))) & 0xFFu)
+                                            : b16;
+                                const uint32_t tc = t < 0x80u ? ascii_vclass(t) : V_NONE;
+                                fast = tc == V_WS || tc == V_ISO || p + Lw >= N;
+                            }
+                            if (fast) {
+                                w = keep_bytes(W16{swar_lower(raw.x), swar_lower(raw.y), swar_lower(raw.z), swar_lower(raw.w)}, Lw);
+                                L = Lw;
+                                start = 0;
+                                end = L < T.maxlen_first ? L : T.maxlen_first;
+                                nout = 0;
+                                fresh = true;
+                                active = end > 0;
+                                if (!active) {  // no piece can match: the word is [UNK]
+                                    out[0] = (uint16_t)T.unk_id;
+                                    s_cnt[idx] = 1;
+                                }
+                            } else {
+                                s_cnt[idx] = (uint8_t)word_general(
+                                    C, p, rec_end_of(C, (const lds_u16 *)s_rb, nrb, rb_ok, rb_next, p), out);
+                            }
+                        }
+                    }
+                }
             }
-        } else {
-            // fast path: ASCII word of <= 16 bytes (the window holds p .. p+16)
-            const int wr = prel + HALO_L;
-            const int a = wr >> 2;
-            const uint32_t sh = (uint32_t)(wr & 3);
-            const uint32_t x0 = w32[a], x1 = w32[a + 1], x2 = w32[a + 2], x3 = w32[a + 3], x4 = w32[a + 4];
-            const W16 raw{__builtin_amdgcn_alignbyte(x1, x0, sh), __builtin_amdgcn_alignbyte(x2, x1, sh),
-                          __builtin_amdgcn_alignbyte(x3, x2, sh), __builtin_amdgcn_alignbyte(x4, x3, sh)};
-            const uint32_t b16 = (x4 >> (8 * sh)) & 0xFFu;  // byte at p + 16
-            const uint32_t om = msb4(swar_alnum(raw.x)) | (msb4(swar_alnum(raw.y)) << 4) |
-                                (msb4(swar_alnum(raw.z)) << 8) | (msb4(swar_alnum(raw.w)) << 12);
-            int L = __builtin_ctz(~om);  // leading ASCII letters/digits, <= 16
-            // a record start at p+1 .. p+16 ends the word
-            const int rb0 = wr + 1;
-            const uint64_t rw = ((uint64_t)rbits[(rb0 >> 5) + 1] << 32) | rbits[rb0 >> 5];
-            const uint32_t rbm = (uint32_t)(rw >> (rb0 & 31)) & 0xFFFFu;
-            const int Lr = rbm ? __builtin_ctz(rbm) + 1 : 17;
-            bool fast;
-            if (Lr <= L) {
-                L = Lr;
-                fast = true;
-            } else {
-                const uint32_t t = L < 16 ? (((L < 4 ? raw.x : L < 8 ? raw.y : L < 12 ? raw.z : raw.w) >> (8 * (L & 3))) & 0xFFu)
-                                          : b16;
-                // the word ends at an ASCII whitespace/punctuation byte (or the arena end)
-                const uint32_t tc = t < 0x80u ? ascii_vclass(t) : V_NONE;
-                fast = tc == V_WS || tc == V_ISO || p + L >= N;
-            }
-            if (fast) {
-                const W16 lw = keep_bytes(W16{swar_lower(raw.x), swar_lower(raw.y), swar_lower(raw.z), swar_lower(raw.w)}, L);
-                k = wordpiece16(T, lw, L, ids);
-            } else {
-                k = word_general(C, p, rec_end_of(C, (const lds_u16 *)s_rb, nrb, rb_ok, rb_next, p), ids);
+            if (!__any(active || !exhausted)) break;
+            // (b) one vocab probe for every live WordPiece state
+            if (active) {
+                if (fresh) {
+                    cand = keep_bytes(start ? shift_right_bytes(w, start) : w, end - start);
+                    const uint32_t cont = start > 0 ? 1u : 0u;
+                    uint32_t h = hinit((uint32_t)(end - start), cont);
+                    h = hmix(h, cand.x);
+                    h = hmix(h, cand.y);
+                    h = hmix(h, cand.z);
+                    h = hmix(h, cand.w);
+                    slot = hfinal(h) & T.slot_mask;
+                    key = (uint32_t)(end - start) | (cont << 8);
+                    fresh = false;
+                }
+                const uint4 *e = reinterpret_cast<const uint4 *>(T.slots + slot);
+                const uint4 ea = e[0];
+                const uint4 eb = e[1];
+                const bool empty = (int32_t)ea.y < 0;
+                const bool hit = !empty && ea.x == key && eb.x == cand.x && eb.y == cand.y && eb.z == cand.z &&
+                                 eb.w == cand.w;
+                lds_u16 *out = stage + prel;
+                if (hit) {
+                    out[nout++] = (uint16_t)ea.y;
+                    start = end;
+                    if (start >= L) {
+                        s_cnt[pi] = (uint8_t)nout;
+                        active = false;
+                    } else {
+                        end = L < start + T.maxlen_cont ? L : start + T.maxlen_cont;
+                        fresh = true;
+                    }
+                } else if (empty) {
+                    if (--end <= start) {  // no piece matches here: the whole word is [UNK]
+                        out[0] = (uint16_t)T.unk_id;
+                        s_cnt[pi] = 1;
+                        active = false;
+                    } else {
+                        fresh = true;
+                    }
+                } else {
+                    slot = (slot + 1) & T.slot_mask;  // linear probing: same candidate, next slot
+                }
             }
         }
-        s_cnt[pi] = (uint8_t)k;
     }
     __syncthreads();
 

@@ -7,7 +7,7 @@ import ctypes
 import os
 
 PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG, "libsdl_batcher.so")
+LIB_PATH = os.environ.get("SDL_LIB") or os.path.join(PKG, "libsdl_batcher.so")
 DATA_DIR = os.path.join(PKG, "data")
 ASSETS = os.path.join(PKG, "assets")
 BERT_PROXY_TOKENIZER = os.path.join(ASSETS, "bert_proxy", "tokenizer.json")
