@@ -73,6 +73,12 @@ def build(verbose=False, force=False, jobs=4, defines=(), lib=None, build_dir=No
     return lib
 
 
+def build_stamps():
+    """Diagnostic build with per-phase s_memtime stamps -> build/stamps/libsdl_batcher.so."""
+    d = os.path.join(REPO, "build", "stamps")
+    return build(defines=("SDL_STAMPS=1",), lib=os.path.join(d, "libsdl_batcher.so"), build_dir=os.path.join(d, "obj"))
+
+
 def build_ablations(levels=(1, 3)):
     """Diagnostic builds with phases of the tokenize kernel compiled out
     (SDL_ABLATE=1: no WordPiece; 3: load only) -> build/abl<N>/libsdl_batcher.so."""

@@ -14,28 +14,16 @@
 
 namespace sdl {
 
-static inline uint32_t hmix(uint32_t h, uint32_t w) {
-    h ^= w;
-    h *= 0x85EBCA6Bu;
-    return h ^ (h >> 13);
-}
-
 uint32_t piece_hash(const uint8_t *payload, size_t n, uint32_t cont) {
-    // init(len, cont); then per zero-padded 16-byte block, 4 little-endian
-    // dwords mixed in; then a final avalanche (at least one block, even if empty)
-    uint32_t h = ((uint32_t)n * 2u + cont) * 0x9E3779B1u ^ 0x7F4A7C15u;
+    uint32_t h = ph_init((uint32_t)n, cont);
     size_t b0 = 0;
-    do {
+    do {  // at least one block, even for an empty payload
         uint32_t w[4] = {0, 0, 0, 0};
         for (size_t k = 0; k < 16 && b0 + k < n; ++k) w[k >> 2] |= (uint32_t)payload[b0 + k] << (8 * (k & 3));
-        for (int i = 0; i < 4; ++i) h = hmix(h, w[i]);
+        for (int i = 0; i < 4; ++i) h = ph_mix(h, w[i]);
         b0 += 16;
     } while (b0 < n);
-    h ^= h >> 16;
-    h *= 0x7FEB352Du;
-    h ^= h >> 15;
-    h *= 0x846CA68Bu;
-    return h ^ (h >> 16);
+    return ph_final(h);
 }
 
 static std::string read_file(const std::string &path) {
@@ -91,16 +79,27 @@ static int find_piece(const HostTokenizer &t, const std::string &s) {
     return -1;
 }
 
+static bool cuckoo_insert(std::vector<VSlot> &tab, uint32_t mask, VSlot v) {
+    uint32_t pos = cuckoo_slot1(v.hash, mask);
+    for (int kick = 0; kick < 2000; ++kick) {
+        if (tab[pos].id < 0) {
+            tab[pos] = v;
+            return true;
+        }
+        std::swap(v, tab[pos]);  // evict the occupant to its other slot
+        const uint32_t a = cuckoo_slot1(v.hash, mask), b = cuckoo_slot2(v.hash, mask);
+        pos = pos == a ? b : a;
+    }
+    return false;
+}
+
 static void build_vocab_table(HostTokenizer &t) {
     const size_t n = t.pieces.size();
     if (n > 65535) throw std::runtime_error("vocabulary larger than 65535 ids is not supported (u16 staging)");
-    uint32_t slots = 1;
-    while (slots < 2 * n) slots <<= 1;
-    t.slot_mask = slots - 1;
-    t.slots.assign(slots, VSlot{0, -1, 0, 0, {0}});
-    t.vpool.clear();
     std::unordered_map<std::string, int> last;  // HF vocab is a map: duplicates keep the last id
     for (size_t id = 0; id < n; ++id) last[t.pieces[id]] = (int)id;
+    std::vector<VSlot> entries;
+    t.vpool.clear();
     t.maxlen_first = t.maxlen_cont = 0;
     for (size_t id = 0; id < n; ++id) {
         const std::string &s = t.pieces[id];
@@ -114,13 +113,23 @@ static void build_vocab_table(HostTokenizer &t) {
         v.key = (uint32_t)pay.size() | (cont << 8);
         v.id = (int32_t)id;
         v.pool_off = (uint32_t)t.vpool.size();
+        v.hash = piece_hash((const uint8_t *)pay.data(), pay.size(), cont);
         std::memcpy(v.inl, pay.data(), std::min<size_t>(16, pay.size()));
         t.vpool.insert(t.vpool.end(), pay.begin(), pay.end());
-        uint32_t i = piece_hash((const uint8_t *)pay.data(), pay.size(), cont) & t.slot_mask;
-        while (t.slots[i].id >= 0) i = (i + 1) & t.slot_mask;
-        t.slots[i] = v;
+        entries.push_back(v);
     }
     t.vpool.resize(t.vpool.size() + 64, 0);
+    uint32_t slots = 1;
+    while (slots < 4 * entries.size()) slots <<= 1;  // load <= 0.25
+    for (;; slots <<= 1) {
+        t.slot_mask = slots - 1;
+        t.slots.assign(slots, VSlot{0, -1, 0, 0, {0}});
+        bool ok = true;
+        for (const VSlot &v : entries)
+            if (!cuckoo_insert(t.slots, t.slot_mask, v)) { ok = false; break; }
+        if (ok) break;
+        if (slots >= (1u << 24)) throw std::runtime_error("cuckoo table build failed");
+    }
 }
 
 // ASCII visible classes the kernels compute arithmetically (tokenize_wordpiece.hip:
@@ -159,6 +168,27 @@ static void set_added(HostTokenizer &t) {
         t.max_special_len = std::max(t.max_special_len, (int)s.size());
     }
     t.opener = op;
+}
+
+// Device entry format: the file's entries with short normalizations (<= 3
+// bytes) moved inline -- bits 0-1 class, bit 2 identity, bit 3 inline,
+// bits 4-5 nbytes-1, 6-7 nchars-1, 8-31 the bytes; longer ones keep the pool
+// offset in bits 8-31.  Plus a flat copy of the BMP so one load resolves it.
+static void to_device_entries(HostTokenizer &t) {
+    for (uint32_t &e : t.uentry) {
+        const uint32_t cls = e & 3u;
+        if ((e & 4u) || cls == UC_WS || cls == UC_DEL) continue;
+        const uint32_t off = e >> 8;
+        const uint32_t nb = t.upool[off], nc = t.upool[off + 1];
+        if (nb >= 1 && nb <= 3 && nc >= 1 && nc <= 4) {
+            uint32_t bytes = 0;
+            for (uint32_t k = 0; k < nb; ++k) bytes |= (uint32_t)t.upool[off + 2 + k] << (8 * k);
+            if (bytes >> 24) continue;
+            e = cls | 8u | ((nb - 1) << 4) | ((nc - 1) << 6) | (bytes << 8);
+        }
+    }
+    t.ubmp.resize(0x10000);
+    for (uint32_t cp = 0; cp < 0x10000; ++cp) t.ubmp[cp] = t.uentry[(size_t)t.upage[cp >> 7] * 128 + (cp & 127)];
 }
 
 void load_tokenizer(const std::string &path, const std::string &data_dir, HostTokenizer &t) {
@@ -262,6 +292,7 @@ void load_tokenizer(const std::string &path, const std::string &data_dir, HostTo
     build_vocab_table(t);
     load_unicode(data_dir + "/bert_uncased_unicode.bin", t);
     check_ascii_and_ids(t);
+    to_device_entries(t);
 }
 
 }  // namespace sdl

@@ -15,13 +15,14 @@ enum : uint32_t { UC_OTHER = 0, UC_WS = 1, UC_ISO = 2, UC_DEL = 3 };
 enum : uint8_t { V_NONE = 0, V_WS = 1, V_ISO = 2, V_OTHER = 3, V_SPEC = 4 };
 
 // ---- tokenize workgroup geometry -----------------------------------------
-constexpr int TOK_THREADS = 256;
-constexpr int CHUNK = 4096;                       // text bytes owned by one workgroup
+constexpr int TOK_THREADS = 64;                   // one wave64 per workgroup: no cross-wave stalls
+constexpr int CHUNK = 1024;                       // text bytes owned by one workgroup (16 per lane)
 constexpr int BYTES_PER_THREAD = CHUNK / TOK_THREADS;
 constexpr int HALO_L = 32;                        // look-back bytes staged in LDS
-constexpr int HALO_R = 224;                       // look-ahead bytes staged in LDS
-constexpr int WIN = HALO_L + CHUNK + HALO_R;      // 4352 bytes of text in LDS
+constexpr int HALO_R = 32;                        // look-ahead bytes staged in LDS
+constexpr int WIN = HALO_L + CHUNK + HALO_R;      // 1088 bytes of text in LDS
 constexpr int STAGE = CHUNK + 128;                // token slots per chunk (>= tokens owned)
+constexpr int TOK_UNROLL = 4;                     // first probes in flight per lane
 constexpr int RB_CAP = 256;                       // record starts listed in LDS per window
 constexpr int MAX_WORD_CHARS = 100;               // WordPiece max_input_chars_per_word
 constexpr int MAX_WORD_BYTES = 4 * MAX_WORD_CHARS + 8;
@@ -31,22 +32,50 @@ constexpr int MAX_SPECIAL_LEN = 24;
 constexpr int MAX_FRAME = 4;
 
 
-// Vocabulary hash-table slot: 32 bytes, two 16-B loads.  A piece is keyed by
-// (payload, cont) where cont = it starts with "##" (payload = the rest):
-//   w0 key = payload length | cont << 8, w1 id (-1 = empty slot),
-//   w2 offset of the payload in the pool, w3 0, w4..w7 the first 16 payload
-//   bytes (zero padded).  Slot index = piece_hash(payload, cont) & mask.
+// Vocabulary cuckoo hash table: every piece sits in one of its two slots, so
+// any lookup (hit or miss) is one round trip of two independent 32-B reads.
+// A piece is keyed by (payload, cont), cont = it starts with "##" and payload
+// is the rest.  Slot: w0 key = payload length | cont << 8, w1 id (-1 = empty),
+// w2 offset of the payload in the pool, w3 the piece hash (host only),
+// w4..w7 the first 16 payload bytes (zero padded).
 struct alignas(32) VSlot {
     uint32_t key;
     int32_t id;
     uint32_t pool_off;
-    uint32_t pad;
+    uint32_t hash;
     uint8_t inl[16];
 };
+
+// piece hash: init(len, cont); per zero-padded 16-byte block, 4 little-endian
+// dwords mixed in; final avalanche (assets.cpp: piece_hash runs the same steps).
+__host__ __device__ inline uint32_t ph_init(uint32_t len, uint32_t cont) {
+    return (len * 2u + cont) * 0x9E3779B1u ^ 0x7F4A7C15u;
+}
+__host__ __device__ inline uint32_t ph_mix(uint32_t h, uint32_t w) {
+    h ^= w;
+    h *= 0x85EBCA6Bu;
+    return h ^ (h >> 13);
+}
+__host__ __device__ inline uint32_t ph_final(uint32_t h) {
+    h ^= h >> 16;
+    h *= 0x7FEB352Du;
+    h ^= h >> 15;
+    h *= 0x846CA68Bu;
+    return h ^ (h >> 16);
+}
+// the two cuckoo slots of a piece hash
+__host__ __device__ inline uint32_t cuckoo_slot1(uint32_t h, uint32_t mask) { return h & mask; }
+__host__ __device__ inline uint32_t cuckoo_slot2(uint32_t h, uint32_t mask) {
+    uint32_t g = (h >> 16) | (h << 16);
+    g *= 0xD35A2D97u;
+    g ^= g >> 15;
+    return g & mask;
+}
 static_assert(sizeof(VSlot) == 32, "VSlot must be 32 bytes");
 
 // Everything a tokenize kernel needs, passed by value as a kernel argument.
 struct DevTok {
+    const uint32_t *ubmp;    // device Unicode entries of U+0000..U+FFFF (flat)
     const uint16_t *upage;   // Unicode page table  [0x110000/128]
     const uint32_t *uentry;  // Unicode blocks      [n_blocks*128]
     const uint8_t *upool;    // normalized strings  (u8 nbytes, u8 nchars, bytes)

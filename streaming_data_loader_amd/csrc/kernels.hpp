@@ -15,6 +15,10 @@ hipError_t launch_wordpiece_chunks(const DevTok &T, const uint8_t *text, int64_t
                                    uint32_t *ranges, uint32_t *tokc, uint32_t *chunk_cnt, uint32_t *rec_local,
                                    hipStream_t st);
 
+#ifdef SDL_STAMPS
+void print_phase_cycles();  // diagnostic builds only
+#endif
+
 // pipeline.hip
 // out[0..n) = exclusive prefix sum of in[0..n), out[n] = total.  tmp needs
 // scan_tmp_words(n) words.
@@ -34,9 +38,12 @@ struct RowOut {
     float *labels_f32;
 };
 
+// row -> record map (row_rec needs one word per row)
+hipError_t launch_row_map(const uint32_t *row_off, int64_t R, uint32_t *row_rec, hipStream_t st);
+
 // BertData::put_data + mask_batch for every row (models/bert_data.rs:40-89)
 hipError_t launch_rows(const RowParams &P, const uint32_t *tok, const uint32_t *rec_tok, const uint32_t *rec_cnt,
-                       const uint32_t *row_off, int64_t R, const uint32_t *d_rows, int64_t rows_cap, RowOut out,
-                       hipStream_t st);
+                       const uint32_t *row_off, const uint32_t *row_rec, const uint32_t *d_rows, int64_t rows_cap,
+                       RowOut out, hipStream_t st);
 
 }  // namespace sdl

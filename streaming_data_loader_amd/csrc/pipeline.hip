@@ -96,18 +96,21 @@ hipError_t launch_exclusive_scan(const uint32_t *in, uint32_t *out, int64_t n, u
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_compact_tokens(const uint32_t *__restrict__ tokc,
                                                         const uint32_t *__restrict__ chunk_cnt,
-                                                        const uint32_t *__restrict__ chunk_off,
+                                                        const uint32_t *__restrict__ chunk_off, int64_t n_chunks,
                                                         uint32_t *__restrict__ tok) {
-    const uint32_t n = chunk_cnt[blockIdx.x];
-    const uint32_t *src = tokc + (int64_t)blockIdx.x * STAGE;
-    uint32_t *dst = tok + chunk_off[blockIdx.x];
-    for (uint32_t i = threadIdx.x; i < n; i += 256) dst[i] = src[i];
+    const int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);  // one wave per chunk
+    if (c >= n_chunks) return;
+    const uint32_t n = chunk_cnt[c];
+    const uint32_t *src = tokc + c * STAGE;
+    uint32_t *dst = tok + chunk_off[c];
+    for (uint32_t i = threadIdx.x & 63; i < n; i += 64) dst[i] = src[i];
 }
 
 hipError_t launch_compact_tokens(const uint32_t *tokc, const uint32_t *chunk_cnt, const uint32_t *chunk_off,
                                  int64_t n_chunks, uint32_t *tok, hipStream_t st) {
     if (n_chunks == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_compact_tokens, dim3((unsigned)n_chunks), dim3(256), 0, st, tokc, chunk_cnt, chunk_off, tok);
+    hipLaunchKernelGGL(k_compact_tokens, dim3((unsigned)((n_chunks + 3) / 4)), dim3(256), 0, st, tokc, chunk_cnt,
+                       chunk_off, n_chunks, tok);
     return hipGetLastError();
 }
 
@@ -144,6 +147,20 @@ hipError_t launch_records(const RowParams &P, const uint64_t *off, int64_t R, in
     return hipGetLastError();
 }
 
+// Row g -> its record (one thread per record writes its rows' entries).
+__global__ __launch_bounds__(256) void k_row_map(const uint32_t *__restrict__ row_off, int64_t R,
+                                                 uint32_t *__restrict__ row_rec) {
+    const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (r >= R) return;
+    for (uint32_t g = row_off[r]; g < row_off[r + 1]; ++g) row_rec[g] = (uint32_t)r;
+}
+
+hipError_t launch_row_map(const uint32_t *row_off, int64_t R, uint32_t *row_rec, hipStream_t st) {
+    if (R == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_row_map, dim3((unsigned)((R + 255) / 256)), dim3(256), 0, st, row_off, R, row_rec);
+    return hipGetLastError();
+}
+
 // ---------------------------------------------------------------------------
 // RNG contract: Philox4x32-10 (Salmon et al., SC'11), as oracle/sdl_oracle.c.
 // ---------------------------------------------------------------------------
@@ -166,14 +183,25 @@ __device__ __forceinline__ uint32_t mlm_key(uint64_t seed, uint64_t rec, uint32_
     return s == 0 ? c.x : s == 1 ? c.y : s == 2 ? c.z : c.w;
 }
 
-// Marks the k smallest (key, position) pairs of a row held as key[m] at
-// position lane + 64*m.  32-step radix select of the k-th smallest key with
-// wave ballots, then position-ordered tie-break among equal keys.
-template <int M>
-__device__ __forceinline__ void select_k_smallest(const uint32_t (&key)[M], int k, bool (&sel)[M]) {
+// framing id k (< MAX_FRAME) without dynamic indexing of the kernel argument
+__device__ __forceinline__ int32_t frame_id(const int32_t (&a)[MAX_FRAME], int k) {
+    return k == 0 ? a[0] : k == 1 ? a[1] : k == 2 ? a[2] : a[3];
+}
+
+// Row layout of k_rows: lane L owns positions 256*m + 4*L + w (w = 0..3), so
+// one Philox block (4 words) is exactly one lane's keys for round m and every
+// plane store is one 16-byte write per lane.
+//
+// Marks the k smallest (key, position) pairs of a row held as key[m][w]: a
+// 32-step radix select of the k-th smallest key with wave ballots, then a
+// position-ordered tie-break among keys equal to it.
+template <int MR>
+__device__ __forceinline__ void select_k_smallest(const uint32_t (&key)[MR][4], int k, bool (&sel)[MR][4]) {
     if (k <= 0) {
 #pragma unroll
-        for (int m = 0; m < M; ++m) sel[m] = false;
+        for (int m = 0; m < MR; ++m)
+#pragma unroll
+            for (int w = 0; w < 4; ++w) sel[m][w] = false;
         return;
     }
     uint32_t prefix = 0;
@@ -181,32 +209,62 @@ __device__ __forceinline__ void select_k_smallest(const uint32_t (&key)[M], int 
         const uint32_t cand = prefix | (1u << bit);
         int c = 0;
 #pragma unroll
-        for (int m = 0; m < M; ++m) c += __popcll(__ballot(key[m] < cand));
+        for (int m = 0; m < MR; ++m)
+#pragma unroll
+            for (int w = 0; w < 4; ++w) c += __popcll(__ballot(key[m][w] < cand));
         if (c < k) prefix = cand;
     }
     int c_lt = 0;
 #pragma unroll
-    for (int m = 0; m < M; ++m) c_lt += __popcll(__ballot(key[m] < prefix));
+    for (int m = 0; m < MR; ++m)
+#pragma unroll
+        for (int w = 0; w < 4; ++w) c_lt += __popcll(__ballot(key[m][w] < prefix));
     const int need = k - c_lt;
     const uint64_t lt_mask = (1ull << lane_id()) - 1ull;
-    int before = 0;
+    int before = 0;  // equal keys in earlier rounds
 #pragma unroll
-    for (int m = 0; m < M; ++m) {
-        const uint64_t eq = __ballot(key[m] == prefix);
-        const int rank = before + __popcll(eq & lt_mask);
-        sel[m] = key[m] < prefix || (key[m] == prefix && rank < need);
-        before += __popcll(eq);
+    for (int m = 0; m < MR; ++m) {
+        uint64_t eq[4];
+        int lower = 0;  // equal keys of this round in lower lanes
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            eq[w] = __ballot(key[m][w] == prefix);
+            lower += __popcll(eq[w] & lt_mask);
+        }
+        int own = 0;  // equal keys of this lane at lower w
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            const bool e = key[m][w] == prefix;
+            sel[m][w] = key[m][w] < prefix || (e && before + lower + own < need);
+            own += e ? 1 : 0;
+        }
+#pragma unroll
+        for (int w = 0; w < 4; ++w) before += __popcll(eq[w]);
     }
 }
 
-template <int M>
+__device__ __forceinline__ void store4(int32_t *p, int j0, int S, bool vec, int32_t a, int32_t b, int32_t c,
+                                       int32_t d) {
+    if (vec) {
+        if (j0 < S) *reinterpret_cast<int4 *>(p + j0) = make_int4(a, b, c, d);
+    } else {
+        if (j0 < S) p[j0] = a;
+        if (j0 + 1 < S) p[j0 + 1] = b;
+        if (j0 + 2 < S) p[j0 + 2] = c;
+        if (j0 + 3 < S) p[j0 + 3] = d;
+    }
+}
+
+template <int MR>
 __global__ __launch_bounds__(256) void k_rows(RowParams P, const uint32_t *__restrict__ tok,
                                               const uint32_t *__restrict__ rec_tok, const uint32_t *__restrict__ rec_cnt,
-                                              const uint32_t *__restrict__ row_off, int64_t R,
+                                              const uint32_t *__restrict__ row_off, const uint32_t *__restrict__ row_rec,
                                               const uint32_t *__restrict__ d_rows, int64_t rows_cap, RowOut out) {
     const int lane = lane_id();
     const int wid = (int)(threadIdx.x >> 6);
     const int S = P.S;
+    const bool vec = (S & 3) == 0;  // 16-byte aligned rows
+    const bool vec_lb = (P.label_width & 3) == 0;
     const uint32_t G = *d_rows;
     int64_t Gpad = ((int64_t)G + P.B - 1) / P.B * P.B;
     if (Gpad > rows_cap) Gpad = rows_cap;
@@ -217,24 +275,16 @@ __global__ __launch_bounds__(256) void k_rows(RowParams P, const uint32_t *__res
         int32_t *lb_o = out.labels + g * (int64_t)P.label_width;
         if (g >= (int64_t)G) {  // rows of the last batch nobody filled: initial values
 #pragma unroll
-            for (int m = 0; m < M; ++m) {
-                const int j = lane + 64 * m;
-                if (j < S) {
-                    ids_o[j] = 0;
-                    am_o[j] = 1;
-                    if (tt_o) tt_o[j] = 0;
-                }
-                if (j < P.label_width) lb_o[j] = -100;
+            for (int m = 0; m < MR; ++m) {
+                const int j0 = 256 * m + 4 * lane;
+                store4(ids_o, j0, S, vec, 0, 0, 0, 0);
+                store4(am_o, j0, S, vec, 1, 1, 1, 1);
+                if (tt_o) store4(tt_o, j0, S, vec, 0, 0, 0, 0);
+                store4(lb_o, j0, P.label_width, vec_lb, -100, -100, -100, -100);
             }
             continue;
         }
-        // record of row g: last r with row_off[r] <= g
-        int64_t lo = 0, hi = R;
-        while (hi - lo > 1) {
-            const int64_t mid = (lo + hi) >> 1;
-            if ((int64_t)row_off[mid] <= g) lo = mid; else hi = mid;
-        }
-        const int64_t r = lo;
+        const int64_t r = row_rec[g];
         const uint32_t k = (uint32_t)(g - row_off[r]);
         const uint32_t cnt = rec_cnt[r];
         const uint32_t t0 = rec_tok[r];
@@ -242,74 +292,93 @@ __global__ __launch_bounds__(256) void k_rows(RowParams P, const uint32_t *__res
         const int64_t base = P.chunk ? (int64_t)k * S : 0;
         const int l = (int)((n - base) < S ? (n - base) : S);
 
-        int32_t id[M];
+        int32_t id[MR][4];
 #pragma unroll
-        for (int m = 0; m < M; ++m) {
-            const int j = lane + 64 * m;
-            int32_t v = 0;
-            if (j < l) {
-                const int64_t f = base + j;
-                if (f < P.n_pre) v = P.pre[f];
-                else if (f < P.n_pre + (int64_t)cnt) v = (int32_t)tok[t0 + (f - P.n_pre)];
-                else v = P.post[f - P.n_pre - cnt];
+        for (int m = 0; m < MR; ++m)
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                const int j = 256 * m + 4 * lane + w;
+                int32_t v = 0;
+                if (j < l) {
+                    const int64_t f = base + j;
+                    if (f < P.n_pre) v = frame_id(P.pre, (int)f);
+                    else if (f < P.n_pre + (int64_t)cnt) v = (int32_t)tok[t0 + (f - P.n_pre)];
+                    else v = frame_id(P.post, (int)(f - P.n_pre - cnt));
+                }
+                id[m][w] = v;
             }
-            id[m] = v;
-        }
+        // attention: 0 on [S-l, S) when l < S (reversed-range quirk, bert_data.rs:58-63 / gpt_data.rs:33-41)
+        const int tail0 = l < S ? S - l : S;
         const uint64_t rec = P.first_record + (uint64_t)r;
         if (P.task == 0) {  // MLM: BertData::mask_batch
-            uint32_t key[M];
+            uint32_t key[MR][4];
 #pragma unroll
-            for (int m = 0; m < M; ++m) {
-                const int j = lane + 64 * m;
-                key[m] = j < S ? mlm_key(P.seed, rec, k, (uint32_t)j) : 0xFFFFFFFFu;
+            for (int m = 0; m < MR; ++m) {
+                const uint4 c = philox4x32_10(make_uint4((uint32_t)(64 * m + lane), k, (uint32_t)rec,
+                                                         (uint32_t)(rec >> 32)),
+                                              (uint32_t)P.seed, (uint32_t)(P.seed >> 32));
+                const int j0 = 256 * m + 4 * lane;
+                key[m][0] = j0 < S ? c.x : 0xFFFFFFFFu;
+                key[m][1] = j0 + 1 < S ? c.y : 0xFFFFFFFFu;
+                key[m][2] = j0 + 2 < S ? c.z : 0xFFFFFFFFu;
+                key[m][3] = j0 + 3 < S ? c.w : 0xFFFFFFFFu;
             }
-            bool sel[M];
-            select_k_smallest<M>(key, P.mask_length, sel);
+            bool sel[MR][4];
+            select_k_smallest<MR>(key, P.mask_length, sel);
 #pragma unroll
-            for (int m = 0; m < M; ++m) {
-                const int j = lane + 64 * m;
-                if (j >= S) continue;
-                int32_t lab = -100, v = id[m];
-                if (sel[m] && v != 0) {
-                    lab = v;
-                    v = P.mask_id;
+            for (int m = 0; m < MR; ++m) {
+                const int j0 = 256 * m + 4 * lane;
+                int32_t v[4], lab[4], am[4];
+#pragma unroll
+                for (int w = 0; w < 4; ++w) {
+                    v[w] = id[m][w];
+                    lab[w] = -100;
+                    if (sel[m][w] && v[w] != 0) {
+                        lab[w] = v[w];
+                        v[w] = P.mask_id;
+                    }
+                    am[w] = j0 + w >= tail0 ? 0 : 1;
                 }
-                ids_o[j] = v;
-                am_o[j] = (l < S && j >= S - l) ? 0 : 1;  // reversed-range quirk (bert_data.rs:58-63)
-                if (tt_o) tt_o[j] = 0;
-                lb_o[j] = lab;
+                store4(ids_o, j0, S, vec, v[0], v[1], v[2], v[3]);
+                store4(am_o, j0, S, vec, am[0], am[1], am[2], am[3]);
+                if (tt_o) store4(tt_o, j0, S, vec, 0, 0, 0, 0);
+                store4(lb_o, j0, P.label_width, vec_lb, lab[0], lab[1], lab[2], lab[3]);
             }
         } else {  // CLM: GptData::put_data, labels = row as i32 (no shift)
 #pragma unroll
-            for (int m = 0; m < M; ++m) {
-                const int j = lane + 64 * m;
-                if (j >= S) continue;
-                const bool tail = l < S && j >= S - l;  // gpt_data.rs:33-41
-                ids_o[j] = id[m];
-                am_o[j] = tail ? 0 : 1;
-                lb_o[j] = tail ? -100 : id[m];
-                if (tt_o) tt_o[j] = 0;
+            for (int m = 0; m < MR; ++m) {
+                const int j0 = 256 * m + 4 * lane;
+                int32_t am[4], lab[4];
+#pragma unroll
+                for (int w = 0; w < 4; ++w) {
+                    const bool tail = j0 + w >= tail0;
+                    am[w] = tail ? 0 : 1;
+                    lab[w] = tail ? -100 : id[m][w];
+                }
+                store4(ids_o, j0, S, vec, id[m][0], id[m][1], id[m][2], id[m][3]);
+                store4(am_o, j0, S, vec, am[0], am[1], am[2], am[3]);
+                if (tt_o) store4(tt_o, j0, S, vec, 0, 0, 0, 0);
+                store4(lb_o, j0, P.label_width, vec_lb, lab[0], lab[1], lab[2], lab[3]);
             }
         }
     }
 }
 
 hipError_t launch_rows(const RowParams &P, const uint32_t *tok, const uint32_t *rec_tok, const uint32_t *rec_cnt,
-                       const uint32_t *row_off, int64_t R, const uint32_t *d_rows, int64_t rows_cap, RowOut out,
-                       hipStream_t st) {
+                       const uint32_t *row_off, const uint32_t *row_rec, const uint32_t *d_rows, int64_t rows_cap,
+                       RowOut out, hipStream_t st) {
     if (rows_cap == 0) return hipSuccess;
     const int64_t want = (rows_cap + 3) / 4;
     const unsigned grid = (unsigned)(want < 4096 ? want : 4096);
-    const int M = (P.S + 63) / 64;
+    const int MR = (P.S + 255) / 256;
+    if (P.label_width > 256 * MR) return hipErrorInvalidValue;
 #define SDL_ROWS(MM)                                                                                                 \
-    hipLaunchKernelGGL(k_rows<MM>, dim3(grid), dim3(256), 0, st, P, tok, rec_tok, rec_cnt, row_off, R, d_rows, \
+    hipLaunchKernelGGL(k_rows<MM>, dim3(grid), dim3(256), 0, st, P, tok, rec_tok, rec_cnt, row_off, row_rec, d_rows, \
                        rows_cap, out)
-    if (M <= 1) SDL_ROWS(1);
-    else if (M <= 2) SDL_ROWS(2);
-    else if (M <= 4) SDL_ROWS(4);
-    else if (M <= 8) SDL_ROWS(8);
-    else if (M <= 16) SDL_ROWS(16);
-    else if (M <= 32) SDL_ROWS(32);
+    if (MR <= 1) SDL_ROWS(1);
+    else if (MR <= 2) SDL_ROWS(2);
+    else if (MR <= 4) SDL_ROWS(4);
+    else if (MR <= 8) SDL_ROWS(8);
     else return hipErrorInvalidValue;
 #undef SDL_ROWS
     return hipGetLastError();

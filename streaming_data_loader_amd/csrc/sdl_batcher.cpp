@@ -109,14 +109,14 @@ struct sdl_batcher {
 
     // device-resident tokenizer tables
     DevBuf<uint16_t> d_upage;
-    DevBuf<uint32_t> d_uentry;
+    DevBuf<uint32_t> d_uentry, d_ubmp;
     DevBuf<uint8_t> d_upool, d_vpool;
     DevBuf<VSlot> d_slots;
     DevBuf<int32_t> d_ascii_id;
 
     // per-call workspace
     DevBuf<uint32_t> ranges, tokc, chunk_cnt, chunk_off, rec_local, tok_ids, rec_tok, rec_cnt, rec_rows, row_off,
-        scan_tmp;
+        row_rec, scan_tmp;
     DevBuf<int32_t> o_ids, o_am, o_tt, o_lab;
     DevBuf<uint8_t> h2d_text;
     DevBuf<uint64_t> h2d_off;
@@ -134,7 +134,12 @@ struct sdl_batcher {
     hipEvent_t ev[kStages + 1] = {};
     float stage_ms[kStages] = {};
 
+#ifdef SDL_STAMPS
+    ~sdl_batcher() { print_phase_cycles(); cleanup(); }
+    void cleanup() {
+#else
     ~sdl_batcher() {
+#endif
         for (auto *b : store) delete b;
         for (auto *b : outbox) delete b;
         for (auto &e : ev)
@@ -173,6 +178,7 @@ struct sdl_batcher {
         o_am.ensure(plane);
         if (P.task == SDL_TASK_MLM || P.task == SDL_TASK_MULTI_LABEL) o_tt.ensure(plane);
         o_lab.ensure((size_t)std::max<int64_t>(rows_cap, 1) * P.label_width);
+        row_rec.ensure((size_t)std::max<int64_t>(rows_cap, 1));
 
         RowParams p = P;
         p.first_record = first_record;
@@ -190,10 +196,11 @@ struct sdl_batcher {
                                st));
         mark(4);
         HIP_TRY(launch_exclusive_scan(rec_rows.p, row_off.p, R, scan_tmp.p, st));
+        HIP_TRY(launch_row_map(row_off.p, R, row_rec.p, st));
         mark(5);
         RowOut out{o_ids.p, o_am.p, (P.task == SDL_TASK_MLM || P.task == SDL_TASK_MULTI_LABEL) ? o_tt.p : nullptr,
                    o_lab.p, nullptr};
-        HIP_TRY(launch_rows(p, tok_ids.p, rec_tok.p, rec_cnt.p, row_off.p, R, row_off.p + R, rows_cap, out, st));
+        HIP_TRY(launch_rows(p, tok_ids.p, rec_tok.p, rec_cnt.p, row_off.p, row_rec.p, row_off.p + R, rows_cap, out, st));
         mark(6);
         last_rows_cap = rows_cap;
         last_R = R;
@@ -327,6 +334,8 @@ int sdl_batcher_create(const sdl_config *cfg, const char *tokenizer_path, const 
         HIP_TRY(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
         for (auto &e : h->ev) HIP_TRY(hipEventCreate(&e));
         auto &t = h->tok;
+        h->d_ubmp.ensure(t.ubmp.size());
+        HIP_TRY(hipMemcpy(h->d_ubmp.p, t.ubmp.data(), t.ubmp.size() * 4, hipMemcpyHostToDevice));
         h->d_upage.ensure(t.upage.size());
         h->d_uentry.ensure(t.uentry.size());
         h->d_upool.ensure(t.upool.size());
@@ -340,6 +349,7 @@ int sdl_batcher_create(const sdl_config *cfg, const char *tokenizer_path, const 
         HIP_TRY(hipMemcpy(h->d_slots.p, t.slots.data(), t.slots.size() * sizeof(VSlot), hipMemcpyHostToDevice));
         HIP_TRY(hipMemcpy(h->d_vpool.p, t.vpool.data(), t.vpool.size(), hipMemcpyHostToDevice));
         DevTok &d = h->dt;
+        d.ubmp = h->d_ubmp.p;
         d.upage = h->d_upage.p;
         d.uentry = h->d_uentry.p;
         d.upool = h->d_upool.p;

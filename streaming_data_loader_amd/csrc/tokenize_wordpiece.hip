@@ -32,6 +32,8 @@
 #include "device_util.hpp"
 #include "kernels.hpp"
 
+#include <cstdio>
+
 namespace sdl {
 
 namespace {
@@ -40,13 +42,12 @@ typedef __attribute__((address_space(3))) uint8_t lds_u8;
 typedef __attribute__((address_space(3))) uint16_t lds_u16;
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 
-constexpr int RBITS_WORDS = WIN / 32;  // 136
+constexpr int RBITS_WORDS = WIN / 32;  // 34
 
 struct Ctx {
     const DevTok *T;
     const lds_u8 *win;      // LDS window [w0, w0 + WIN)
     const lds_u32 *rbits;   // LDS bitmap: record starts in the window
-    const lds_u32 *ascii;   // LDS: Unicode-table entries for ASCII
     int64_t w0;
     const uint8_t *text;
     int64_t N;
@@ -75,20 +76,9 @@ struct Ctx {
     }
 };
 
-// ---- hashing of vocab pieces (assets.cpp: piece_hash) -------------------------
-__device__ __forceinline__ uint32_t hmix(uint32_t h, uint32_t w) {
-    h ^= w;
-    h *= 0x85EBCA6Bu;
-    return h ^ (h >> 13);
-}
-__device__ __forceinline__ uint32_t hinit(uint32_t len, uint32_t cont) { return (len * 2u + cont) * 0x9E3779B1u ^ 0x7F4A7C15u; }
-__device__ __forceinline__ uint32_t hfinal(uint32_t h) {
-    h ^= h >> 16;
-    h *= 0x7FEB352Du;
-    h ^= h >> 15;
-    h *= 0x846CA68Bu;
-    return h ^ (h >> 16);
-}
+__device__ __forceinline__ uint32_t hinit(uint32_t len, uint32_t cont) { return ph_init(len, cont); }
+__device__ __forceinline__ uint32_t hmix(uint32_t h, uint32_t w) { return ph_mix(h, w); }
+__device__ __forceinline__ uint32_t hfinal(uint32_t h) { return ph_final(h); }
 
 // ---- 16-byte register words ---------------------------------------------------
 struct W16 {
@@ -148,9 +138,18 @@ __device__ __forceinline__ uint32_t ascii_vclass(uint32_t b) {
     return V_ISO;
 }
 
+// Device Unicode entry (assets.cpp: device_entry): bits 0-1 class, bit 2
+// identity, bit 3 inline (bits 4-5 nbytes-1, 6-7 nchars-1, 8-31 the bytes),
+// else bits 8-31 = pool offset.  One load for the BMP, two beyond it.
 __device__ __forceinline__ uint32_t uentry(const DevTok &T, uint32_t cp) {
+    if (cp < 0x10000u) return T.ubmp[cp];
     if (cp >= 0x110000u) return UC_DEL;
     return T.uentry[(uint32_t)T.upage[cp >> 7] * 128u + (cp & 127u)];
+}
+__device__ __forceinline__ int entry_nchars(const DevTok &T, uint32_t e) {
+    if (e & 4u) return 1;
+    if (e & 8u) return (int)((e >> 6) & 3u) + 1;
+    return T.upool[(e >> 8) + 1];
 }
 
 __device__ __forceinline__ uint32_t vclass_of_entry(uint32_t e) {
@@ -222,25 +221,31 @@ __device__ uint32_t vclass_general(const Ctx &C, int64_t q) {
 
 // ---- WordPiece ------------------------------------------------------------------
 
-// Probe for the literal piece (cont ? "##" : "") + payload, payload <= 16
-// bytes held in c (zero padded).  Returns the id or -1.
-__device__ __forceinline__ int probe16(const DevTok &T, const W16 &c, uint32_t n, uint32_t cont) {
+// Reads both cuckoo slots of hash h (4 independent 16-B loads).
+struct Probe {
+    uint4 a1, b1, a2, b2;
+};
+__device__ __forceinline__ Probe probe_load(const DevTok &T, uint32_t h) {
+    const uint4 *e1 = reinterpret_cast<const uint4 *>(T.slots + cuckoo_slot1(h, T.slot_mask));
+    const uint4 *e2 = reinterpret_cast<const uint4 *>(T.slots + cuckoo_slot2(h, T.slot_mask));
+    return Probe{e1[0], e1[1], e2[0], e2[1]};
+}
+__device__ __forceinline__ bool slot_match(const uint4 &a, const uint4 &b, uint32_t key, const W16 &c) {
+    return (int32_t)a.y >= 0 && a.x == key && b.x == c.x && b.y == c.y && b.z == c.z && b.w == c.w;
+}
+// id of the piece (payload <= 16 bytes in c, zero padded) or -1: exact
+__device__ __forceinline__ int probe_result(const Probe &P, uint32_t key, const W16 &c) {
+    if (slot_match(P.a1, P.b1, key, c)) return (int32_t)P.a1.y;
+    if (slot_match(P.a2, P.b2, key, c)) return (int32_t)P.a2.y;
+    return -1;
+}
+__device__ __forceinline__ uint32_t hash16(const W16 &c, uint32_t n, uint32_t cont) {
     uint32_t h = hinit(n, cont);
     h = hmix(h, c.x);
     h = hmix(h, c.y);
     h = hmix(h, c.z);
     h = hmix(h, c.w);
-    h = hfinal(h);
-    const uint32_t key = n | (cont << 8);
-    for (uint32_t s = h & T.slot_mask;; s = (s + 1) & T.slot_mask) {
-        const uint4 *e = reinterpret_cast<const uint4 *>(T.slots + s);
-        const uint4 a = e[0];
-        if ((int32_t)a.y < 0) return -1;
-        if (a.x == key) {
-            const uint4 b = e[1];
-            if (b.x == c.x && b.y == c.y && b.z == c.z && b.w == c.w) return (int32_t)a.y;
-        }
-    }
+    return hfinal(h);
 }
 
 // General probe: payload = w[start, end) of a byte buffer (any length).
@@ -264,17 +269,15 @@ __device__ int probe_general(const DevTok &T, const uint8_t *w, int start, int e
     } while (b0 < n);
     h = hfinal(h);
     const uint32_t key = n | (cont << 8);
-    for (uint32_t s = h & T.slot_mask;; s = (s + 1) & T.slot_mask) {
-        const uint4 *e = reinterpret_cast<const uint4 *>(T.slots + s);
-        const uint4 a = e[0];
-        if ((int32_t)a.y < 0) return -1;
-        if (a.x != key) continue;
-        const uint4 b = e[1];
-        if (b.x != first.x || b.y != first.y || b.z != first.z || b.w != first.w) continue;
+    const Probe P = probe_load(T, h);
+    for (int which = 0; which < 2; ++which) {
+        const uint4 a = which ? P.a2 : P.a1, b = which ? P.b2 : P.b1;
+        if (!slot_match(a, b, key, first)) continue;
         bool ok = true;
         for (uint32_t k = 16; k < n && ok; ++k) ok = T.vpool[a.z + k] == w[start + k];
         if (ok) return (int32_t)a.y;
     }
+    return -1;
 }
 
 // WordPiece::tokenize over a normalized word held in a byte buffer.
@@ -306,6 +309,11 @@ __device__ __forceinline__ int append_norm(const Ctx &C, uint32_t e, int64_t p, 
         for (int k = 0; k < len; ++k) buf[nb + k] = (uint8_t)C.byte(p + k);
         return nb + len;
     }
+    if (e & 8u) {
+        const int m = (int)((e >> 4) & 3u) + 1;
+        for (int k = 0; k < m; ++k) buf[nb + k] = (uint8_t)(e >> (8 + 8 * k));
+        return nb + m;
+    }
     const uint8_t *pe = C.T->upool + (e >> 8);
     const int m = pe[0];
     for (int k = 0; k < m; ++k) buf[nb + k] = pe[2 + k];
@@ -321,21 +329,21 @@ __device__ int word_general(const Ctx &C, int64_t p, int64_t rec_end, lds_u16 *o
     while (i < rec_end && nchars <= MAX_WORD_CHARS) {
         const uint32_t b = C.byte(i);
         if (b < 0x80u) {
-            const uint32_t c = C.ascii[b] & 3u;
-            if (c == UC_OTHER) {
+            const uint32_t c = ascii_vclass(b);
+            if (c == V_OTHER) {
                 if (T.n_special && b == T.opener && special_match(C, i) >= 0) break;
                 ++nchars;
                 ++i;
                 continue;
             }
-            if (c == UC_DEL) { ++i; continue; }
+            if (c == V_NONE) { ++i; continue; }
             break;
         }
         if ((b & 0xC0u) == 0x80u) { ++i; continue; }
         int len;
         const uint32_t e = uentry(T, decode(C, i, b, &len));
         const uint32_t c = e & 3u;
-        if (c == UC_OTHER) nchars += (e & 4u) ? 1 : T.upool[(e >> 8) + 1];
+        if (c == UC_OTHER) nchars += entry_nchars(T, e);
         else if (c != UC_DEL) break;
         i += len;
     }
@@ -348,8 +356,7 @@ __device__ int word_general(const Ctx &C, int64_t p, int64_t rec_end, lds_u16 *o
     for (int64_t q = p; q < i;) {
         const uint32_t b = C.byte(q);
         if (b < 0x80u) {
-            const uint32_t e = C.ascii[b];
-            if ((e & 3u) == UC_OTHER) buf[nb++] = (uint8_t)((b - 'A' < 26u) ? b + 32u : b);
+            if (ascii_vclass(b) == V_OTHER) buf[nb++] = (uint8_t)((b - 'A' < 26u) ? b + 32u : b);
             ++q;
             continue;
         }
@@ -362,28 +369,77 @@ __device__ int word_general(const Ctx &C, int64_t p, int64_t rec_end, lds_u16 *o
     return wordpiece_general(T, buf, nb, out);
 }
 
-// WordPiece on an ASCII word of L <= 16 lower-cased bytes in registers
-// (every byte is one char, so "end -= 1 char" is "end -= 1").
-__device__ __forceinline__ int wordpiece16(const DevTok &T, const W16 &w, int L, lds_u16 *out) {
-    int n = 0, start = 0;
-    while (start < L) {
-        const int lim = start == 0 ? T.maxlen_first : T.maxlen_cont;
-        int end = start + lim < L ? start + lim : L;
-        const W16 sh = start ? shift_right_bytes(w, start) : w;
-        const uint32_t cont = start > 0 ? 1u : 0u;
-        int id = -1;
-        for (; end > start; --end) {
-            id = probe16(T, keep_bytes(sh, end - start), (uint32_t)(end - start), cont);
-            if (id >= 0) break;
+// byte k (dynamic, 0..15) of a 16-byte register word
+__device__ __forceinline__ uint32_t w16_byte(const W16 &w, int k) {
+    const int q = k >> 2;
+    const uint32_t x = q == 0 ? w.x : q == 1 ? w.y : q == 2 ? w.z : w.w;
+    return (x >> (8 * (k & 3))) & 0xFFu;
+}
+__device__ __forceinline__ void w16_put(W16 &w, int k, uint32_t b) {
+    const int q = k >> 2;
+    const uint32_t v = b << (8 * (k & 3));
+    w.x |= q == 0 ? v : 0u;
+    w.y |= q == 1 ? v : 0u;
+    w.z |= q == 2 ? v : 0u;
+    w.w |= q == 3 ? v : 0u;
+}
+// start of the char that ends right before byte `end` (UTF-8 in registers)
+__device__ __forceinline__ int w16_prev_char(const W16 &w, int end, int start) {
+    int e = end - 1;
+    while (e > start && (w16_byte(w, e) & 0xC0u) == 0x80u) --e;
+    return e;
+}
+
+// BertNormalizer output of the WORD piece at p (or of the single ISO char at
+// p if iso) into registers.  Returns false if the normalized word does not fit
+// in 16 bytes (then the scratch path handles it, including the 100-char rule).
+__device__ bool normalize_w16(const Ctx &C, int64_t p, int64_t rec_end, bool iso, W16 &w, int &L) {
+    const DevTok &T = *C.T;
+    w = W16{0, 0, 0, 0};
+    int nb = 0;
+    int64_t i = p;
+    while (i < rec_end) {
+        const uint32_t b = C.byte(i);
+        if (b < 0x80u) {
+            const uint32_t c = ascii_vclass(b);
+            if (iso || c == V_OTHER) {
+                if (!iso && T.n_special && b == T.opener && special_match(C, i) >= 0) break;
+                if (nb >= 16) return false;
+                w16_put(w, nb++, (b - 'A' < 26u) ? b + 32u : b);
+                ++i;
+                if (iso) break;
+                continue;
+            }
+            if (c == V_NONE) { ++i; continue; }
+            break;
         }
-        if (id < 0) {
-            out[0] = (uint16_t)T.unk_id;
-            return 1;
+        if ((b & 0xC0u) == 0x80u) { ++i; continue; }
+        int len;
+        const uint32_t e = uentry(T, decode(C, i, b, &len));
+        const uint32_t c = e & 3u;
+        if (iso || c == UC_OTHER) {
+            if (e & 4u) {
+                if (nb + len > 16) return false;
+                for (int k = 0; k < len; ++k) w16_put(w, nb++, C.byte(i + k));
+            } else if (e & 8u) {
+                const int m = (int)((e >> 4) & 3u) + 1;
+                if (nb + m > 16) return false;
+                for (int k = 0; k < m; ++k) w16_put(w, nb++, (e >> (8 + 8 * k)) & 0xFFu);
+            } else {
+                const uint8_t *pe = T.upool + (e >> 8);
+                const int m = pe[0];
+                if (nb + m > 16) return false;
+                for (int k = 0; k < m; ++k) w16_put(w, nb++, pe[2 + k]);
+            }
+            i += len;
+            if (iso) break;
+            continue;
         }
-        out[n++] = (uint16_t)id;
-        start = end;
+        if (c == UC_DEL) { i += len; continue; }
+        break;
     }
-    return n;
+    L = nb;
+    return true;
 }
 
 // Record end (first record start > p) for the general paths.
@@ -445,6 +501,25 @@ __global__ __launch_bounds__(256) void k_chunk_ranges(const uint64_t *__restrict
     ranges[3 * c + 2] = (uint32_t)lower(c0);
 }
 
+// Diagnostic build (-DSDL_STAMPS): wave 0 of every block adds the s_memtime
+// cycles spent between phase boundaries (each right after a barrier) into
+// sdl_phase_cycles[]; the host prints them.  Never compiled into the product.
+#ifdef SDL_STAMPS
+__device__ unsigned long long sdl_phase_cycles[16];
+#define SDL_STAMP(k)                                                                  \
+    do {                                                                              \
+        if (threadIdx.x == 0) {                                                       \
+            const unsigned long long t_ = __builtin_amdgcn_s_memtime();              \
+            atomicAdd(&sdl_phase_cycles[k], t_ - stamp_prev_);                        \
+            stamp_prev_ = t_;                                                         \
+        }                                                                             \
+    } while (0)
+#else
+#define SDL_STAMP(k) \
+    do {             \
+    } while (0)
+#endif
+
 __global__ __launch_bounds__(TOK_THREADS) void k_wordpiece_chunks(
     DevTok T, const uint8_t *__restrict__ text, int64_t N, const uint64_t *__restrict__ off, int64_t R,
     const uint32_t *__restrict__ ranges, uint32_t *__restrict__ tokc, uint32_t *__restrict__ chunk_cnt,
@@ -455,12 +530,14 @@ __global__ __launch_bounds__(TOK_THREADS) void k_wordpiece_chunks(
     __shared__ uint16_t s_stage[STAGE];    // ids staged at their piece's byte position
     __shared__ uint8_t s_cnt[CHUNK];       // ids per piece
     __shared__ uint16_t s_poff[CHUNK];     // id offset of each piece in the chunk
-    __shared__ uint32_t s_ascii[128];
     __shared__ int32_t s_ascii_id[128];
     __shared__ uint16_t s_rb[RB_CAP];
     __shared__ uint32_t s_scratch[TOK_THREADS / 64 + 2];
 
     const int tid = threadIdx.x;
+#ifdef SDL_STAMPS
+    unsigned long long stamp_prev_ = __builtin_amdgcn_s_memtime();
+#endif
     const int64_t c0 = (int64_t)blockIdx.x * CHUNK;
     const int64_t c1 = c0 + CHUNK < N ? c0 + CHUNK : N;
     const int64_t w0 = c0 - HALO_L;
@@ -470,14 +547,13 @@ __global__ __launch_bounds__(TOK_THREADS) void k_wordpiece_chunks(
     // ---- 1. load -------------------------------------------------------------
     const uint4 v = load16(text, c0 + 16 * tid, N);
     *reinterpret_cast<uint4 *>(s_win + HALO_L + 16 * tid) = v;
-    if (tid < (WIN - CHUNK) / 16) {  // 2 left + 14 right halo pieces
+    if (tid < (WIN - CHUNK) / 16) {  // left and right halo pieces
         const int64_t p = tid < HALO_L / 16 ? w0 + 16 * tid : c0 + CHUNK + 16 * (tid - HALO_L / 16);
         *reinterpret_cast<uint4 *>(s_win + (p - w0)) = load16(text, p, N);
     }
     if (tid <= RBITS_WORDS) s_rbits[tid] = 0;
-    if (tid < 128) {
-        s_ascii[tid] = T.uentry[(uint32_t)T.upage[0] * 128u + tid];
-        s_ascii_id[tid] = T.ascii_id[tid];
+    for (int i = tid; i < 128; i += TOK_THREADS) {
+        s_ascii_id[i] = T.ascii_id[i];
     }
     const int64_t ra = ranges[3 * blockIdx.x], rz = ranges[3 * blockIdx.x + 1], r_lo = ranges[3 * blockIdx.x + 2];
     const int nrb = (int)(rz - ra);
@@ -491,8 +567,9 @@ __global__ __launch_bounds__(TOK_THREADS) void k_wordpiece_chunks(
         if (rb_ok) s_rb[k] = (uint16_t)rel;
     }
     __syncthreads();
+    SDL_STAMP(1);
 
-    const Ctx C{&T, win, rbits, (const lds_u32 *)s_ascii, w0, text, N, off, R};
+    const Ctx C{&T, win, rbits, w0, text, N, off, R};
 #if defined(SDL_ABLATE) && SDL_ABLATE >= 3
     // diagnostic: load only; every record gets 0 ids (so later stages stay in bounds)
     if (tid == 0) chunk_cnt[blockIdx.x] = s_win[HALO_L + (blockIdx.x & 1023)] & 0u;
@@ -519,25 +596,83 @@ __global__ __launch_bounds__(TOK_THREADS) void k_wordpiece_chunks(
         cls &= nown ? ((1ull << (4 * nown)) - 1ull) : 0ull;
         leads &= (1u << nown) - 1u;
     }
-    while (leads) {  // non-ASCII lead bytes: decode + Unicode table
-        const int i = __builtin_ctz(leads);
-        leads &= leads - 1;
-        const uint32_t c = vclass_general(C, s0 + i);
-        cls = (cls & ~(0xFull << (4 * i))) | ((uint64_t)c << (4 * i));
-    }
-    if (T.n_special) {  // added tokens: an opener byte in [s0 - 24, s0 + 16)?
-        const uint32_t ob = T.opener * 0x01010101u;
-        auto has = [&](uint32_t x) { x ^= ob; return ((x - 0x01010101u) & ~x & 0x80808080u) != 0u; };
-        const lds_u32 *w32 = (const lds_u32 *)s_win;
-        const int d0 = (rel0 - 24) >> 2;
-        bool near = has(v.x) || has(v.y) || has(v.z) || has(v.w);
+    // Rare bytes are classified block-parallel, one per thread, and returned as
+    // per-byte class overrides in LDS (s_cnt doubles as the override array and
+    // s_pieces as the work list until the pieces are found):
+    //   (a) non-ASCII lead bytes: decode + two-level Unicode table;
+    //   (b) added tokens: every opener byte that starts a match marks its bytes
+    //       (SPEC at the start, invisible after); applied after (a).
+    uint8_t *s_ovr = s_cnt;
+    *reinterpret_cast<uint4 *>(s_ovr + 16 * tid) = make_uint4(~0u, ~0u, ~0u, ~0u);
+    uint32_t opens = 0;
+    if (T.n_special) {
 #pragma unroll
-        for (int k = 0; k < 6; ++k) near |= has(w32[d0 + k]);
-        if (near) {
-            for (int i = 0; i < nown; ++i) {
-                const uint32_t c = vclass_general(C, s0 + i);
-                cls = (cls & ~(0xFull << (4 * i))) | ((uint64_t)c << (4 * i));
+        for (int i = 0; i < 16; ++i) {
+            const uint32_t b = (wv[i >> 2] >> (8 * (i & 3))) & 0xFFu;
+            opens |= (b == T.opener ? 1u : 0u) << i;
+        }
+        opens &= nown == 16 ? 0xFFFFu : ((1u << nown) - 1u);
+    }
+    // tid 0 also owns openers in [c0 - max_special_len + 1, c0): a token starting
+    // there may cover this chunk's first bytes
+    uint32_t opens_left = 0;
+    if (T.n_special && tid == 0) {
+        for (int d = 1; d < T.max_special_len; ++d)
+            if (c0 - d >= 0 && C.byte(c0 - d) == T.opener) opens_left |= 1u << (d - 1);
+    }
+    uint32_t nrare;
+    const uint32_t rare_n = (uint32_t)__builtin_popcount(leads) |
+                            ((uint32_t)(__builtin_popcount(opens) + __builtin_popcount(opens_left)) << 16);
+    const uint32_t rbase = block_excl_sum<TOK_THREADS>(rare_n, &nrare, s_scratch);
+    const uint32_t n_leads = nrare & 0xFFFFu, n_opens = nrare >> 16;
+    {
+        uint32_t lb = rbase & 0xFFFFu, ob = n_leads + (rbase >> 16);
+        for (uint32_t m = leads; m;) {
+            const int i = __builtin_ctz(m);
+            m &= m - 1;
+            s_pieces[lb++] = (uint16_t)(HALO_L + 16 * tid + i);
+        }
+        for (uint32_t m = opens; m;) {
+            const int i = __builtin_ctz(m);
+            m &= m - 1;
+            s_pieces[ob++] = (uint16_t)(HALO_L + 16 * tid + i);
+        }
+        for (uint32_t m = opens_left; m;) {
+            const int d = __builtin_ctz(m) + 1;
+            m &= m - 1;
+            s_pieces[ob++] = (uint16_t)(HALO_L - d);
+        }
+    }
+    __syncthreads();
+    SDL_STAMP(2);
+    for (uint32_t k = tid; k < n_leads; k += TOK_THREADS) {
+        const int wi = s_pieces[k];
+        int len;
+        s_ovr[wi - HALO_L] = (uint8_t)vclass_of_entry(uentry(T, decode(C, w0 + wi, win[wi], &len)));
+    }
+    if (n_opens) {  // block-uniform
+        __syncthreads();
+        for (uint32_t k = n_leads + tid; k < n_leads + n_opens; k += TOK_THREADS) {
+            const int wi = s_pieces[k];
+            const int64_t x = w0 + wi;
+            const int m = special_match(C, x);
+            if (m < 0) continue;
+            const int l = T.special_len[m];
+            for (int j = 0; j < l; ++j) {
+                const int64_t y = x + j;
+                if (y >= c0 && y < c1) s_ovr[y - c0] = (uint8_t)(j == 0 ? V_SPEC : V_NONE);
             }
+        }
+    }
+    __syncthreads();
+    SDL_STAMP(3);
+    {
+        const uint4 o = *reinterpret_cast<const uint4 *>(s_ovr + 16 * tid);
+        const uint32_t ov[4] = {o.x, o.y, o.z, o.w};
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const uint32_t c = (ov[i >> 2] >> (8 * (i & 3))) & 0xFFu;
+            if (c != 0xFFu) cls = (cls & ~(0xFull << (4 * i))) | ((uint64_t)c << (4 * i));
         }
     }
     // lane summary for the carry scan: 0 = pass-through, 0x100 | v = state after
@@ -565,6 +700,7 @@ __global__ __launch_bounds__(TOK_THREADS) void k_wordpiece_chunks(
     __syncthreads();
     const uint32_t chunk_state = s_scratch[TOK_THREADS / 64];
     __syncthreads();
+    SDL_STAMP(4);
     const uint32_t st_in = block_excl_last_scan<TOK_THREADS>(summ, s_scratch);
 
     // ---- 3. piece starts -------------------------------------------------------
@@ -590,36 +726,139 @@ __global__ __launch_bounds__(TOK_THREADS) void k_wordpiece_chunks(
         s_pieces[pbase++] = (uint16_t)((16 * tid + i) | (c << 12));
     }
     __syncthreads();
+    SDL_STAMP(5);
     const int np = (int)np_total;
 
-    // ---- 4. tokenize pieces: one probe per lane per iteration -------------------
-    // Lanes pull pieces from a block-wide LDS queue; an ASCII word of <= 16
-    // bytes becomes a WordPiece state (word, start, end, slot) advanced by one
-    // vocab probe per iteration, so no lane idles behind a long word.  Other
-    // pieces are finished in the pull step (added tokens, one-byte punctuation)
-    // or by the general path.
-    if (tid == 0) s_scratch[TOK_THREADS / 64 + 1] = 0;
-    __syncthreads();
-#if defined(SDL_ABLATE) && SDL_ABLATE >= 1
-    for (int i = tid; i < np; i += TOK_THREADS) {
-        s_stage[s_pieces[i] & 0xFFF] = (uint16_t)i;
-        s_cnt[i] = 1;
+    // ---- 4. tokenize pieces ---------------------------------------------------------
+    // (a) every lane sets up TOK_UNROLL pieces at a time and issues their
+    //     full-word probes back to back, so most words (in-vocabulary, <= 16 B)
+    //     finish with one latency and TOK_UNROLL loads in flight per lane;
+    //     added tokens and one-byte punctuation finish without a probe;
+    // (b) the rest (misses, collisions, longer or non-ASCII words) go to a
+    //     pending list that a per-lane state machine drains: lanes pull work
+    //     from a block-wide LDS queue and advance one vocab probe per iteration,
+    //     so no lane idles behind a long word.
+    lds_u16 *stage = (lds_u16 *)s_stage;
+    uint16_t *s_pend = s_poff;  // pending piece indices (s_poff is free until step 5)
+    if (tid == 0) {
+        s_scratch[TOK_THREADS / 64 + 1] = 0;  // pending count
     }
-    if (false)
-#endif
-    {
-        const lds_u32 *w32 = (const lds_u32 *)s_win;
-        lds_u16 *stage = (lds_u16 *)s_stage;
-        const int lane = tid & 63;
+    __syncthreads();
+    SDL_STAMP(10);
+    const int lane = tid & 63;
+    const lds_u32 *w32 = (const lds_u32 *)s_win;
+    // word setup shared by (a) and (b): returns false if the general path is needed
+    auto word_setup = [&](int prel, W16 &lw, int &Lout) -> bool {
+        const int wr = prel + HALO_L;
+        const int a = wr >> 2;
+        const uint32_t sh = (uint32_t)(wr & 3);
+        const uint32_t x0 = w32[a], x1 = w32[a + 1], x2 = w32[a + 2], x3 = w32[a + 3], x4 = w32[a + 4];
+        const W16 raw{__builtin_amdgcn_alignbyte(x1, x0, sh), __builtin_amdgcn_alignbyte(x2, x1, sh),
+                      __builtin_amdgcn_alignbyte(x3, x2, sh), __builtin_amdgcn_alignbyte(x4, x3, sh)};
+        const uint32_t b16 = (x4 >> (8 * sh)) & 0xFFu;  // byte at p + 16
+        const uint32_t om = msb4(swar_alnum(raw.x)) | (msb4(swar_alnum(raw.y)) << 4) |
+                            (msb4(swar_alnum(raw.z)) << 8) | (msb4(swar_alnum(raw.w)) << 12);
+        int Lw = __builtin_ctz(~om);  // leading ASCII letters/digits, <= 16
+        const int rb0 = wr + 1;     // a record start at p+1 .. p+16 ends the word
+        const uint64_t rw = ((uint64_t)rbits[(rb0 >> 5) + 1] << 32) | rbits[rb0 >> 5];
+        const uint32_t rbm = (uint32_t)(rw >> (rb0 & 31)) & 0xFFFFu;
+        const int Lr = rbm ? __builtin_ctz(rbm) + 1 : 17;
+        bool fast;
+        if (Lr <= Lw) {
+            Lw = Lr;
+            fast = true;
+        } else {
+            const uint32_t t =
+                Lw < 16 ? (((Lw < 4 ? raw.x : Lw < 8 ? raw.y : Lw < 12 ? raw.z : raw.w) >> (8 * (Lw & 3))) & 0xFFu) : b16;
+            const uint32_t tc = t < 0x80u ? ascii_vclass(t) : V_NONE;
+            fast = tc == V_WS || tc == V_ISO || c0 + prel + Lw >= N;
+        }
+        lw = keep_bytes(W16{swar_lower(raw.x), swar_lower(raw.y), swar_lower(raw.z), swar_lower(raw.w)}, Lw);
+        Lout = Lw;
+        return fast;
+    };
+    // (a) batched first probes
+    for (int r0 = 0; r0 < np; r0 += TOK_THREADS * TOK_UNROLL) {
+        uint32_t hsh[TOK_UNROLL], key[TOK_UNROLL];
+        W16 cand[TOK_UNROLL];
+        int prel_u[TOK_UNROLL], L_u[TOK_UNROLL];
+        bool probe[TOK_UNROLL], pend[TOK_UNROLL];
+#pragma unroll
+        for (int u = 0; u < TOK_UNROLL; ++u) {
+            const int pi = r0 + u * TOK_THREADS + tid;
+            probe[u] = pend[u] = false;
+            hsh[u] = key[u] = 0;
+            L_u[u] = 0;
+            cand[u] = W16{0, 0, 0, 0};
+            prel_u[u] = 0;
+            if (pi >= np) continue;
+            const uint32_t pc = s_pieces[pi];
+            const int prel = (int)(pc & 0xFFFu);
+            const uint32_t kind = pc >> 12;
+            prel_u[u] = prel;
+            if (kind == V_SPEC) {
+                const int m = special_match(C, c0 + prel);
+                stage[prel] = (uint16_t)T.special_id[m < 0 ? 0 : m];
+                s_cnt[pi] = 1;
+            } else if (kind == V_ISO) {
+                const uint32_t b = win[prel + HALO_L];
+                if (b < 0x80u) {
+                    stage[prel] = (uint16_t)s_ascii_id[b];
+                    s_cnt[pi] = 1;
+                } else {
+                    pend[u] = true;
+                }
+            } else {
+                W16 lw;
+                int Lw;
+                if (word_setup(prel, lw, Lw) && Lw <= T.maxlen_first) {
+                    cand[u] = lw;
+                    L_u[u] = Lw;
+                    key[u] = (uint32_t)Lw;
+                    hsh[u] = hash16(lw, (uint32_t)Lw, 0u);
+                    probe[u] = true;
+                } else {
+                    pend[u] = true;
+                }
+            }
+        }
+        Probe pr[TOK_UNROLL];
+#pragma unroll
+        for (int u = 0; u < TOK_UNROLL; ++u) pr[u] = probe_load(T, hsh[u]);
+#pragma unroll
+        for (int u = 0; u < TOK_UNROLL; ++u) {
+            const int pi = r0 + u * TOK_THREADS + tid;
+            if (probe[u]) {
+                const int id = probe_result(pr[u], key[u], cand[u]);
+                if (id >= 0) {
+                    stage[prel_u[u]] = (uint16_t)id;
+                    s_cnt[pi] = 1;
+                } else {
+                    pend[u] = true;
+                }
+            }
+            const uint64_t pm = __ballot(pend[u]);
+            if (pm) {
+                const int leader = __builtin_ctzll(pm);
+                uint32_t base = 0;
+                if (lane == leader) base = atomicAdd(&s_scratch[TOK_THREADS / 64 + 1], (uint32_t)__popcll(pm));
+                base = __shfl(base, leader, 64);
+                if (pend[u]) s_pend[base + __popcll(pm & ((1ull << lane) - 1ull))] = (uint16_t)pi;
+            }
+        }
+    }
+    __syncthreads();
+    SDL_STAMP(11);
+    const int npend = (int)s_scratch[TOK_THREADS / 64 + 1];
+    if (tid == 0) s_scratch[TOK_THREADS / 64 + 1] = 0;  // becomes the queue head
+    __syncthreads();
+    // (b) state machine over the pending pieces
+    if (npend) {
         bool exhausted = false;
         bool active = false;  // a fast WordPiece state is live
         int pi = 0, prel = 0, L = 0, start = 0, end = 0, nout = 0;
-        uint32_t slot = 0;
-        bool fresh = true;
-        W16 w{0, 0, 0, 0}, cand{0, 0, 0, 0};
-        uint32_t key = 0;
+        W16 w{0, 0, 0, 0};
         for (;;) {
-            // (a) pull: idle lanes take the next pieces of the queue
             const bool need = !active && !exhausted;
             const uint64_t nm = __ballot(need);
             if (nm) {
@@ -628,125 +867,85 @@ __global__ __launch_bounds__(TOK_THREADS) void k_wordpiece_chunks(
                 if (lane == leader) base = atomicAdd(&s_scratch[TOK_THREADS / 64 + 1], (uint32_t)__popcll(nm));
                 base = __shfl(base, leader, 64);
                 if (need) {
-                    const int idx = (int)base + __popcll(nm & ((1ull << lane) - 1ull));
-                    if (idx >= np) {
+                    const int q = (int)base + __popcll(nm & ((1ull << lane) - 1ull));
+                    if (q >= npend) {
                         exhausted = true;
                     } else {
-                        pi = idx;
-                        const uint32_t pc = s_pieces[idx];
+                        pi = s_pend[q];
+                        const uint32_t pc = s_pieces[pi];
                         prel = (int)(pc & 0xFFFu);
                         const uint32_t kind = pc >> 12;
                         const int64_t p = c0 + prel;
                         lds_u16 *out = stage + prel;
-                        if (kind == V_SPEC) {
-                            const int m = special_match(C, p);
-                            out[0] = (uint16_t)T.special_id[m < 0 ? 0 : m];
-                            s_cnt[idx] = 1;
-                        } else if (kind == V_ISO) {
-                            const uint32_t b = win[prel + HALO_L];
-                            if (b < 0x80u) {
-                                out[0] = (uint16_t)s_ascii_id[b];
-                                s_cnt[idx] = 1;
-                            } else {
-                                int len;
-                                const uint32_t e = uentry(T, decode(C, p, b, &len));
-                                uint8_t buf[16];
-                                const int nb = append_norm(C, e, p, len, buf, 0);
-                                s_cnt[idx] = (uint8_t)wordpiece_general(T, buf, nb, out);
-                            }
+                        bool fits;
+                        if (kind == V_OTHER && word_setup(prel, w, L)) {
+                            fits = true;
                         } else {
-                            const int wr = prel + HALO_L;
-                            const int a = wr >> 2;
-                            const uint32_t sh = (uint32_t)(wr & 3);
-                            const uint32_t x0 = w32[a], x1 = w32[a + 1], x2 = w32[a + 2], x3 = w32[a + 3], x4 = w32[a + 4];
-                            const W16 raw{__builtin_amdgcn_alignbyte(x1, x0, sh), __builtin_amdgcn_alignbyte(x2, x1, sh),
-                                          __builtin_amdgcn_alignbyte(x3, x2, sh), __builtin_amdgcn_alignbyte(x4, x3, sh)};
-                            const uint32_t b16 = (x4 >> (8 * sh)) & 0xFFu;  // byte at p + 16
-                            const uint32_t om = msb4(swar_alnum(raw.x)) | (msb4(swar_alnum(raw.y)) << 4) |
-                                                (msb4(swar_alnum(raw.z)) << 8) | (msb4(swar_alnum(raw.w)) << 12);
-                            int Lw = __builtin_ctz(~om);  // leading ASCII letters/digits, <= 16
-                            const int rb0 = wr + 1;     // a record start at p+1 .. p+16 ends the word
-                            const uint64_t rw = ((uint64_t)rbits[(rb0 >> 5) + 1] << 32) | rbits[rb0 >> 5];
-                            const uint32_t rbm = (uint32_t)(rw >> (rb0 & 31)) & 0xFFFFu;
-                            const int Lr = rbm ? __builtin_ctz(rbm) + 1 : 17;
-                            bool fast;
-                            if (Lr <= Lw) {
-                                Lw = Lr;
-                                fast = true;
-                            } else {
-                                const uint32_t t =
-                                    Lw < 16 ? (((Lw < 4 ? raw.x : Lw < 8 ? raw.y : Lw < 12 ? raw.z : raw.w) >> (8 * (Lw & 3))) & 0xFFu)
-                                            : b16;
-                                const uint32_t tc = t < 0x80u ? ascii_vclass(t) : V_NONE;
-                                fast = tc == V_WS || tc == V_ISO || p + Lw >= N;
+                            fits = normalize_w16(C, p, rec_end_of(C, (const lds_u16 *)s_rb, nrb, rb_ok, rb_next, p),
+                                                 kind == V_ISO, w, L);
+                        }
+                        if (fits) {
+                            start = 0;
+                            end = L < T.maxlen_first ? L : T.maxlen_first;
+                            while (end < L && end > 0 && (w16_byte(w, end) & 0xC0u) == 0x80u) --end;
+                            nout = 0;
+                            active = end > 0;
+                            if (!active) {  // no piece can match: the word is [UNK]
+                                out[0] = (uint16_t)T.unk_id;
+                                s_cnt[pi] = 1;
                             }
-                            if (fast) {
-                                w = keep_bytes(W16{swar_lower(raw.x), swar_lower(raw.y), swar_lower(raw.z), swar_lower(raw.w)}, Lw);
-                                L = Lw;
-                                start = 0;
-                                end = L < T.maxlen_first ? L : T.maxlen_first;
-                                nout = 0;
-                                fresh = true;
-                                active = end > 0;
-                                if (!active) {  // no piece can match: the word is [UNK]
-                                    out[0] = (uint16_t)T.unk_id;
-                                    s_cnt[idx] = 1;
-                                }
-                            } else {
-                                s_cnt[idx] = (uint8_t)word_general(
-                                    C, p, rec_end_of(C, (const lds_u16 *)s_rb, nrb, rb_ok, rb_next, p), out);
-                            }
+                        } else if (kind == V_ISO) {
+                            int len;
+                            const uint32_t e = uentry(T, decode(C, p, win[prel + HALO_L], &len));
+                            uint8_t buf[16];
+                            const int nb = append_norm(C, e, p, len, buf, 0);
+                            s_cnt[pi] = (uint8_t)wordpiece_general(T, buf, nb, out);
+                        } else {
+                            s_cnt[pi] = (uint8_t)word_general(
+                                C, p, rec_end_of(C, (const lds_u16 *)s_rb, nrb, rb_ok, rb_next, p), out);
                         }
                     }
                 }
             }
             if (!__any(active || !exhausted)) break;
-            // (b) one vocab probe for every live WordPiece state
-            if (active) {
-                if (fresh) {
-                    cand = keep_bytes(start ? shift_right_bytes(w, start) : w, end - start);
-                    const uint32_t cont = start > 0 ? 1u : 0u;
-                    uint32_t h = hinit((uint32_t)(end - start), cont);
-                    h = hmix(h, cand.x);
-                    h = hmix(h, cand.y);
-                    h = hmix(h, cand.z);
-                    h = hmix(h, cand.w);
-                    slot = hfinal(h) & T.slot_mask;
-                    key = (uint32_t)(end - start) | (cont << 8);
-                    fresh = false;
+            if (active) {  // probe the candidates ending at `end` and one char earlier together
+                const W16 sh = start ? shift_right_bytes(w, start) : w;
+                const uint32_t cont = start > 0 ? 1u : 0u;
+                const int e1 = w16_prev_char(w, end, start);
+                const int n0 = end - start, n1 = e1 - start;
+                const W16 c0w = keep_bytes(sh, n0), c1w = keep_bytes(sh, n1);
+                const Probe P0 = probe_load(T, hash16(c0w, (uint32_t)n0, cont));
+                const Probe P1 = probe_load(T, hash16(c1w, (uint32_t)n1, cont));
+                int id = probe_result(P0, (uint32_t)n0 | (cont << 8), c0w);
+                int got = n0;
+                if (id < 0 && n1 > 0) {
+                    id = probe_result(P1, (uint32_t)n1 | (cont << 8), c1w);
+                    got = n1;
                 }
-                const uint4 *e = reinterpret_cast<const uint4 *>(T.slots + slot);
-                const uint4 ea = e[0];
-                const uint4 eb = e[1];
-                const bool empty = (int32_t)ea.y < 0;
-                const bool hit = !empty && ea.x == key && eb.x == cand.x && eb.y == cand.y && eb.z == cand.z &&
-                                 eb.w == cand.w;
                 lds_u16 *out = stage + prel;
-                if (hit) {
-                    out[nout++] = (uint16_t)ea.y;
-                    start = end;
+                if (id >= 0) {
+                    out[nout++] = (uint16_t)id;
+                    start += got;
                     if (start >= L) {
                         s_cnt[pi] = (uint8_t)nout;
                         active = false;
                     } else {
                         end = L < start + T.maxlen_cont ? L : start + T.maxlen_cont;
-                        fresh = true;
+                        while (end < L && end > start && (w16_byte(w, end) & 0xC0u) == 0x80u) --end;
                     }
-                } else if (empty) {
-                    if (--end <= start) {  // no piece matches here: the whole word is [UNK]
+                } else {
+                    end = n1 > 0 ? w16_prev_char(w, e1, start) : start;
+                    if (end <= start) {  // no piece matches here: the whole word is [UNK]
                         out[0] = (uint16_t)T.unk_id;
                         s_cnt[pi] = 1;
                         active = false;
-                    } else {
-                        fresh = true;
                     }
-                } else {
-                    slot = (slot + 1) & T.slot_mask;  // linear probing: same candidate, next slot
                 }
             }
         }
     }
     __syncthreads();
+    SDL_STAMP(7);
 
     // ---- 5. compact ids into this chunk's tokc slice ------------------------------
     const int per = (np + TOK_THREADS - 1) / TOK_THREADS;
@@ -765,9 +964,20 @@ __global__ __launch_bounds__(TOK_THREADS) void k_wordpiece_chunks(
         base += k;
     }
     __syncthreads();
+    SDL_STAMP(8);
     if (tid == 0) chunk_cnt[blockIdx.x] = total;
-    for (int64_t r = r_lo + tid; r <= R; r += TOK_THREADS) {
-        const int64_t pos = (int64_t)off[r];
+    // record boundaries owned by this chunk: local id offset of the first piece
+    // at or after the boundary (positions come from the LDS record list)
+    const int k_lo = (int)(r_lo - ra);
+    for (int k = k_lo + tid;; k += TOK_THREADS) {
+        int64_t pos;
+        if (rb_ok) {
+            if (k >= nrb) break;
+            pos = w0 + s_rb[k];
+        } else {
+            if (ra + k > R) break;
+            pos = (int64_t)off[ra + k];
+        }
         if (pos >= c1) break;
         const int rel = (int)(pos - c0);
         int lo = 0, hi = np;
@@ -775,9 +985,25 @@ __global__ __launch_bounds__(TOK_THREADS) void k_wordpiece_chunks(
             const int m = (lo + hi) >> 1;
             if ((int)(s_pieces[m] & 0xFFF) < rel) lo = m + 1; else hi = m;
         }
-        rec_local[r] = lo < np ? (uint32_t)s_poff[lo] : total;
+        rec_local[ra + k] = lo < np ? (uint32_t)s_poff[lo] : total;
     }
+    SDL_STAMP(9);
 }
+
+#ifdef SDL_STAMPS
+void print_phase_cycles() {
+    unsigned long long h[16];
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(sdl_phase_cycles), sizeof(h)) != hipSuccess) return;
+    static const char *names[] = {"", "load+rbits", "classify+lists", "rare-passes", "merge+lookback", "scan+pieces",
+                                  "-", "wp-pending", "compact", "rec_local", "wp-init", "wp-first-probes"};
+    unsigned long long tot = 0;
+    for (int k = 1; k <= 11; ++k) tot += h[k];
+    fprintf(stderr, "[stamps] block-cycles by phase (wave 0, all blocks, all calls):");
+    for (int k = 1; k <= 11; ++k)
+        if (k != 6) fprintf(stderr, " %s=%.1f%%", names[k], 100.0 * h[k] / (tot ? tot : 1));
+    fprintf(stderr, " total=%llu\n", tot);
+}
+#endif
 
 hipError_t launch_wordpiece_chunks(const DevTok &T, const uint8_t *text, int64_t N, const uint64_t *off, int64_t R,
                                    uint32_t *ranges, uint32_t *tokc, uint32_t *chunk_cnt, uint32_t *rec_local,
