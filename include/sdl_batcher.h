@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define SDL_ABI_VERSION 1
+#define SDL_ABI_VERSION 2
 
 enum {
     SDL_OK = 0,
@@ -112,7 +112,9 @@ int sdl_batcher_push(sdl_batcher *h, const uint8_t *utf8, size_t len, const uint
 /* Bulk create_sync_batch over n_records records laid out back to back in
  * `arena` (record r = arena[offsets[r] .. offsets[r+1]), offsets[0] = 0,
  * n_records+1 offsets).  Exactly the batches the reference would emit over the
- * same sequence of calls are queued, in order, for sdl_batcher_next(). */
+ * same sequence of calls are queued, in order, for sdl_batcher_next().  For the
+ * multi-label task record r's Label::Multi indices are
+ * labels[label_offsets[r] .. label_offsets[r+1]) (NULL label_offsets = none). */
 int sdl_batcher_push_many(sdl_batcher *h, const uint8_t *arena, const uint64_t *offsets,
                           size_t n_records, const uint32_t *labels, const uint64_t *label_offsets,
                           size_t *n_emitted);
@@ -142,11 +144,22 @@ typedef struct sdl_device_rows {
     uint32_t *d_tokens;      /* device scalar: tokenizer ids produced (before framing) */
     uint64_t rows_capacity;
     int32_t label_width;
+    uint32_t *d_label_errors; /* device scalar (multi-label): Label::Multi indices >= number_labels
+                                 that were skipped (the reference panics on them) */
 } sdl_device_rows;
 
 int sdl_process_device(sdl_batcher *h, const uint8_t *d_text, uint64_t text_len,
                        const uint64_t *d_offsets, uint64_t n_records, uint64_t first_record,
                        void *stream, sdl_device_rows *out);
+
+/* sdl_process_device for the multi-label task with Label::Multi indices per
+ * record: record r's indices are d_labels[d_label_offsets[r] .. d_label_offsets[r+1])
+ * (device memory, n_records+1 offsets).  SimpleBatcher::create_sync_batch
+ * (simple_batcher.rs:35-43) + BertData MultiLabel (bert_data.rs:66-78). */
+int sdl_process_device_labels(sdl_batcher *h, const uint8_t *d_text, uint64_t text_len,
+                              const uint64_t *d_offsets, uint64_t n_records, const uint32_t *d_labels,
+                              const uint64_t *d_label_offsets, uint64_t first_record, void *stream,
+                              sdl_device_rows *out);
 
 /* Copies `bytes` from device memory (e.g. sdl_device_rows planes) to host
  * memory with the handle's HIP runtime, ordered after the handle's work on

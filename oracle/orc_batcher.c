@@ -1,0 +1,313 @@
+/*
+ * orc_batcher.c -- CPU restatement of the reference Batcher stage (TEST
+ * INFRASTRUCTURE ONLY: the checker for the HIP path and bench.py's CPU
+ * baseline, never the product).
+ *
+ *   GenTokenizer           rust/src/tasks/gen_batcher.rs:44-98   (mlm, clm, span)
+ *   SimpleBatcher          rust/src/models/simple_batcher.rs:35-53 (multi-label)
+ *   BertData               rust/src/models/bert_data.rs:40-89    (Mask, MultiLabel)
+ *   GptData                rust/src/models/gpt_data.rs:29-45
+ *   encode_mask framing    rust/src/tokenizer/tokenizer_wrapper.rs:107-134
+ *   RNG contract           DESIGN.md §3 (replaces the unseedable thread_rng)
+ */
+#include <stdio.h>
+#include <string.h>
+
+#include "orc_internal.h"
+
+/* ------------------------------------------------------------------------- */
+/* RNG contract: Philox4x32-10 (Salmon et al., SC'11 / Random123)             */
+/* ------------------------------------------------------------------------- */
+static void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) {
+    for (int r = 0; r < 10; ++r) {
+        uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
+        uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];
+        uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+        uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+        uint32_t n0 = hi1 ^ c[1] ^ k0, n2 = hi0 ^ c[3] ^ k1;
+        c[0] = n0;
+        c[1] = lo1;
+        c[2] = n2;
+        c[3] = lo0;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+}
+
+/* key(pos) = Philox(counter = (pos/4, chunk, rec_lo, rec_hi), key = seed)[pos%4] */
+uint32_t orc_mlm_key(uint64_t seed, uint64_t record, uint32_t chunk, uint32_t pos) {
+    uint32_t c[4] = {pos >> 2, chunk, (uint32_t)record, (uint32_t)(record >> 32)};
+    philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+    return c[pos & 3];
+}
+
+/* ------------------------------------------------------------------------- */
+/* DataSet                                                                    */
+/* ------------------------------------------------------------------------- */
+typedef struct {
+    int32_t *ids, *am, *tt, *lab; /* [B,S] x3, [B,LW] */
+    float *f32;                   /* [B,NL] (multi-label) */
+    int index;
+} obatch;
+
+struct orc_batcher {
+    orc_encoder enc;
+    orc_cfg c;
+    int LW, NL;
+    uint64_t n_records;
+    obatch **q;
+    int qh, qn, qcap;
+};
+
+/* BertData::new / GptData::new: BatchConfig::create_vector (batcher.rs:17-22):
+ * input_ids 0, attention_mask 1, token_type_ids 0, labels -100 (GptData) --
+ * BertData's labels are pushed per row and have no initial value; the ABI
+ * reports them as -100 past `rows`. */
+static obatch *obatch_new(const orc_batcher *b) {
+    obatch *x = (obatch *)calloc(1, sizeof(obatch));
+    size_t bs = (size_t)b->c.B * b->c.S, bl = (size_t)b->c.B * b->LW;
+    x->ids = (int32_t *)calloc(bs, 4);
+    x->am = (int32_t *)malloc(bs * 4);
+    x->tt = (int32_t *)calloc(bs, 4);
+    x->lab = (int32_t *)malloc((bl ? bl : 1) * 4);
+    x->f32 = (float *)calloc((size_t)b->c.B * (b->NL ? b->NL : 1), 4);
+    for (size_t i = 0; i < bs; ++i) x->am[i] = 1;
+    for (size_t i = 0; i < bl; ++i) x->lab[i] = -100;
+    return x;
+}
+
+static void obatch_free(obatch *x) {
+    free(x->ids);
+    free(x->am);
+    free(x->tt);
+    free(x->lab);
+    free(x->f32);
+    free(x);
+}
+
+static void q_push(orc_batcher *b, obatch *x) {
+    if (b->qh + b->qn == b->qcap) {
+        if (b->qh) {
+            memmove(b->q, b->q + b->qh, sizeof(obatch *) * b->qn);
+            b->qh = 0;
+        } else {
+            b->qcap = b->qcap ? 2 * b->qcap : 8;
+            b->q = (obatch **)realloc(b->q, sizeof(obatch *) * b->qcap);
+        }
+    }
+    b->q[b->qh + b->qn++] = x;
+}
+
+orc_batcher *orc_batcher_create(const orc_encoder *e, const orc_cfg *c) {
+    if (!e || !c || c->B <= 0 || c->S <= 0) return NULL;
+    if (c->task != ORC_MLM && c->task != ORC_CLM && c->task != ORC_MULTI_LABEL) return NULL;
+    if (c->task == ORC_MLM && (c->mask_length < 0 || c->mask_length > c->S)) return NULL;
+    if (c->task == ORC_MULTI_LABEL && c->number_labels <= 0) return NULL;
+    orc_batcher *b = (orc_batcher *)calloc(1, sizeof(orc_batcher));
+    b->enc = *e;
+    b->c = *c;
+    if (c->task == ORC_MULTI_LABEL) { /* SimpleBatcher: no chunking, no filter */
+        b->c.chunk = 0;
+        b->c.min_ids = 0;
+    }
+    b->NL = c->task == ORC_MULTI_LABEL ? c->number_labels : 0;
+    b->LW = c->task == ORC_MULTI_LABEL ? 0 : c->S;
+    q_push(b, obatch_new(b)); /* GenTokenizer::new / SimpleBatcher::new: first DataSet */
+    return b;
+}
+
+typedef struct { uint32_t key, pos; } kp;
+static int kp_cmp(const void *a, const void *b) {
+    const kp *x = (const kp *)a, *y = (const kp *)b;
+    if (x->key != y->key) return x->key < y->key ? -1 : 1;
+    return x->pos < y->pos ? -1 : (x->pos > y->pos);
+}
+
+/* BertData::mask_batch (bert_data.rs:40-53) under the RNG contract: the first
+ * mask_length entries of the shuffled positions are the mask_length smallest
+ * (key, position) pairs. */
+static void mask_row(const orc_batcher *b, int32_t *in, int32_t *lb, uint64_t rec, uint32_t chunk) {
+    const int S = b->c.S;
+    kp *perm = (kp *)malloc(sizeof(kp) * S);
+    for (int p = 0; p < S; ++p) {
+        perm[p].key = orc_mlm_key(b->c.seed, rec, chunk, (uint32_t)p);
+        perm[p].pos = (uint32_t)p;
+    }
+    qsort(perm, (size_t)S, sizeof(kp), kp_cmp);
+    for (int j = 0; j < S; ++j) lb[j] = -100;
+    for (int k = 0; k < b->c.mask_length; ++k) {
+        uint32_t p = perm[k].pos;
+        if (in[p] != 0) {
+            lb[p] = in[p];
+            in[p] = b->c.mask_id;
+        }
+    }
+    free(perm);
+}
+
+/* DataSet::put_full_data for one row (dataset.rs:47-61).  Returns -1 on a
+ * label index >= number_labels (the reference panics: bert_data.rs:70-72). */
+static int put_data(orc_batcher *b, obatch *x, const uint32_t *ids, size_t n, uint64_t rec, uint32_t chunk,
+                    const uint32_t *labels, size_t nl) {
+    const size_t S = (size_t)b->c.S;
+    int32_t *in = x->ids + (size_t)x->index * S;
+    int32_t *am = x->am + (size_t)x->index * S;
+    const size_t l = n < S ? n : S;
+    for (size_t j = 0; j < l; ++j) in[j] = (int32_t)ids[j];
+    switch (b->c.task) {
+    case ORC_MLM:
+    case ORC_MULTI_LABEL: /* BertData::put_data (bert_data.rs:55-89) */
+        if (n < S)
+            for (size_t j = S - n; j < S; ++j) am[j] = 0; /* reversed-range quirk */
+        if (b->c.task == ORC_MLM) {
+            mask_row(b, in, x->lab + (size_t)x->index * S, rec, chunk);
+        } else {
+            float *f = x->f32 + (size_t)x->index * b->NL;
+            for (size_t k = 0; k < nl; ++k) {
+                if (labels[k] >= (uint32_t)b->NL) return -1;
+                f[labels[k]] = 1.0f;
+            }
+        }
+        break;
+    case ORC_CLM: { /* GptData::put_data (gpt_data.rs:29-45): labels = row, no shift */
+        int32_t *lb = x->lab + (size_t)x->index * S;
+        for (size_t j = 0; j < S; ++j) lb[j] = in[j];
+        if (n < S)
+            for (size_t j = S - n; j < S; ++j) {
+                lb[j] = -100;
+                am[j] = 0;
+            }
+        break;
+    }
+    }
+    x->index++;
+    return 0;
+}
+
+static void batch_out(const orc_batcher *b, obatch *x, orc_out *o) {
+    if (o) {
+        size_t bs = (size_t)b->c.B * b->c.S;
+        if (o->ids) memcpy(o->ids, x->ids, bs * 4);
+        if (o->am) memcpy(o->am, x->am, bs * 4);
+        if (o->tt) memcpy(o->tt, x->tt, bs * 4);
+        if (o->lab && b->LW) memcpy(o->lab, x->lab, (size_t)b->c.B * b->LW * 4);
+        if (o->f32 && b->NL) memcpy(o->f32, x->f32, (size_t)b->c.B * b->NL * 4);
+        o->rows = x->index;
+    }
+    obatch_free(x);
+}
+
+static obatch *q_pop(orc_batcher *b) {
+    obatch *x = b->q[b->qh];
+    b->qh++;
+    b->qn--;
+    return x;
+}
+
+int orc_batcher_push_ex(orc_batcher *b, const uint8_t *s, size_t n, const uint32_t *labels, size_t nl,
+                        orc_out *out) {
+    const uint64_t rec = b->n_records++;
+    idvec v = {0};
+    for (int i = 0; i < b->enc.npre; ++i) idpush(&v, b->enc.pre[i]);
+    b->enc.encode(b->enc.impl, s, n, &v);
+    for (int i = 0; i < b->enc.npost; ++i) idpush(&v, b->enc.post[i]);
+    if (v.n < (size_t)b->c.min_ids) { /* gen_batcher.rs:74-76 */
+        free(v.p);
+        return 0;
+    }
+    const size_t step = b->c.chunk ? (size_t)b->c.S : (v.n ? v.n : 1);
+    uint32_t chunk = 0;
+    int rc = 0;
+    for (size_t off = 0; off < v.n || (off == 0 && v.n == 0); off += step, ++chunk) { /* chunks_mut(S) */
+        size_t len = v.n - off < step ? v.n - off : step;
+        obatch *back = b->q[b->qh + b->qn - 1];
+        if (put_data(b, back, v.p + off, len, rec, chunk, labels, nl)) rc = -1; /* handle_internal_batch */
+        if (back->index == b->c.B) q_push(b, obatch_new(b));
+        if (v.n == 0) break;
+    }
+    free(v.p);
+    if (rc) return rc;
+    if (b->q[b->qh]->index == b->c.B) { /* gen_batcher.rs:86-91 / simple_batcher.rs:39-41 */
+        batch_out(b, q_pop(b), out);
+        return 1;
+    }
+    return 0;
+}
+
+int orc_batcher_flush_ex(orc_batcher *b, orc_out *out) {
+    if (b->c.task == ORC_MULTI_LABEL) { /* SimpleBatcher::get_working_batch: swap in a new one */
+        batch_out(b, q_pop(b), out);
+        q_push(b, obatch_new(b));
+        return 1;
+    }
+    if (b->qn == 0) return 0; /* GenTokenizer::get_working_batch = store.pop_front() */
+    batch_out(b, q_pop(b), out);
+    return 1;
+}
+
+void orc_batcher_free(orc_batcher *b) {
+    for (int i = 0; i < b->qn; ++i) obatch_free(b->q[b->qh + i]);
+    free(b->q);
+    free(b);
+}
+
+void orc_batcher_set_next_record(orc_batcher *b, uint64_t record) { b->n_records = record; }
+
+/* ---- round-1 MLM entry points (4 planes [B,S] back to back) ---- */
+orc_batcher *orc_batcher_new(const orc_tok *t, int task, int batch_size, int seq_len, int mask_length, int mask_id,
+                             uint64_t seed) {
+    if (task != ORC_MLM) return NULL;
+    orc_encoder e;
+    orc_encoder_bert(t, &e);
+    orc_cfg c;
+    orc_cfg_default(&c, task);
+    c.B = batch_size;
+    c.S = seq_len;
+    c.mask_length = mask_length;
+    c.mask_id = mask_id;
+    c.seed = seed;
+    return orc_batcher_create(&e, &c);
+}
+
+static void planes_out(const orc_batcher *b, int32_t *out, orc_out *o) {
+    size_t bs = (size_t)b->c.B * b->c.S;
+    memset(o, 0, sizeof(*o));
+    if (out) {
+        o->ids = out;
+        o->am = out + bs;
+        o->tt = out + 2 * bs;
+        o->lab = out + 3 * bs;
+    }
+}
+
+int orc_batcher_push(orc_batcher *b, const uint8_t *s, size_t n, int32_t *out, int *rows) {
+    orc_out o;
+    planes_out(b, out, &o);
+    int r = orc_batcher_push_ex(b, s, n, NULL, 0, &o);
+    if (r == 1 && rows) *rows = o.rows;
+    return r;
+}
+
+int orc_batcher_flush(orc_batcher *b, int32_t *out, int *rows) {
+    orc_out o;
+    planes_out(b, out, &o);
+    int r = orc_batcher_flush_ex(b, &o);
+    if (r == 1 && rows) *rows = o.rows;
+    return r;
+}
+
+void orc_cfg_default(orc_cfg *c, int task) {
+    memset(c, 0, sizeof(*c));
+    c->task = task;
+    c->B = 4096;
+    c->S = 128;
+    c->chunk = task == ORC_MULTI_LABEL ? 0 : 1;
+    c->min_ids = task == ORC_MULTI_LABEL ? 0 : 64;
+    c->mask_length = (int)((float)c->S * 0.15f);
+    c->mask_id = 103;
+    c->number_labels = 9;
+    c->avg_span_gap = 16.0;
+    c->avg_span_size = 2.0;
+}
+
+size_t orc_encoder_size(void) { return sizeof(orc_encoder); }

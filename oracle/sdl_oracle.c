@@ -8,7 +8,7 @@
  * crate `tokenizers` 0.13.1 the reference pins in rust/Cargo.lock) and against
  * masking fixtures produced by tests/golden/make_goldens.py.
  */
-#include "sdl_oracle.h"
+#include "orc_internal.h"
 
 #include <stdio.h>
 #include <stdlib.h>
@@ -188,18 +188,6 @@ orc_tok *orc_tok_load(const char *vocab_txt, const char *unicode_bin) {
 void orc_tok_free(orc_tok *t) { free(t); }
 int orc_tok_vocab_size(const orc_tok *t) { return t->v.n; }
 
-typedef struct {
-    uint32_t *p;
-    size_t n, cap;
-} idvec;
-
-static void idpush(idvec *v, uint32_t x) {
-    if (v->n == v->cap) {
-        v->cap = v->cap ? v->cap * 2 : 256;
-        v->p = (uint32_t *)realloc(v->p, v->cap * sizeof(uint32_t));
-    }
-    v->p[v->n++] = x;
-}
 
 /* WordPiece::tokenize (tokenizers/src/models/wordpiece/mod.rs): greedy
  * longest-match-first; "##" prefix after the first piece; the whole word is
@@ -276,7 +264,7 @@ static void encode_segment(const orc_tok *t, const uint8_t *s, size_t n, idvec *
 /* Tokenizer::encode(text, true): AddedVocabulary split (leftmost-longest match
  * of the special strings on the raw text), each remaining segment normalized +
  * pre-tokenized + WordPiece, then TemplateProcessing "[CLS] $A [SEP]". */
-static void bert_encode_vec(const orc_tok *t, const uint8_t *s, size_t n, idvec *out) {
+void orc_bert_encode_vec(const orc_tok *t, const uint8_t *s, size_t n, idvec *out) {
     idpush(out, (uint32_t)t->cls);
     size_t seg = 0, i = 0;
     while (i < n) {
@@ -306,187 +294,26 @@ static void bert_encode_vec(const orc_tok *t, const uint8_t *s, size_t n, idvec 
 
 long orc_bert_encode(const orc_tok *t, const uint8_t *s, size_t n, uint32_t *out, size_t cap) {
     idvec v = {0};
-    bert_encode_vec(t, s, n, &v);
+    orc_bert_encode_vec(t, s, n, &v);
     size_t m = v.n < cap ? v.n : cap;
     if (out && m) memcpy(out, v.p, m * sizeof(uint32_t));
     free(v.p);
     return (long)v.n;
 }
 
-/* ------------------------------------------------------------------------- */
-/* RNG contract: Philox4x32-10 (Salmon et al., SC'11 / Random123)             */
-/* ------------------------------------------------------------------------- */
-static void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) {
-    for (int r = 0; r < 10; ++r) {
-        uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
-        uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];
-        uint32_t n0 = (uint32_t)(p1 >> 32) ^ c[1] ^ k0;
-        uint32_t n1 = (uint32_t)p1;
-        uint32_t n2 = (uint32_t)(p0 >> 32) ^ c[3] ^ k1;
-        uint32_t n3 = (uint32_t)p0;
-        c[0] = n0; c[1] = n1; c[2] = n2; c[3] = n3;
-        k0 += 0x9E3779B9u;
-        k1 += 0xBB67AE85u;
-    }
+/* Framing of TokenizerWrapper::encode_mask for BERT (tokenizer_wrapper.rs:107-116):
+ * [CLS] + encode(text, true) + [SEP] [SEP]. */
+static void bert_encode_cb(const void *impl, const uint8_t *s, size_t n, idvec *out) {
+    orc_bert_encode_vec((const orc_tok *)impl, s, n, out);
 }
 
-/* key(pos) = Philox(counter = (pos/4, chunk, rec_lo, rec_hi), key = seed)[pos%4] */
-uint32_t orc_mlm_key(uint64_t seed, uint64_t record, uint32_t chunk, uint32_t pos) {
-    uint32_t c[4] = {pos >> 2, chunk, (uint32_t)record, (uint32_t)(record >> 32)};
-    philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
-    return c[pos & 3];
+void orc_encoder_bert(const orc_tok *t, orc_encoder *e) {
+    memset(e, 0, sizeof(*e));
+    e->encode = bert_encode_cb;
+    e->impl = t;
+    e->npre = 1;
+    e->pre[0] = (uint32_t)t->cls;
+    e->npost = 2;
+    e->post[0] = (uint32_t)t->sep;
+    e->post[1] = (uint32_t)t->sep;
 }
-
-/* ------------------------------------------------------------------------- */
-/* Batcher: GenTokenizer(chunk=true) + BertData(Mask)                         */
-/* ------------------------------------------------------------------------- */
-typedef struct {
-    int32_t *d; /* 4 planes of [B,S]: input_ids, attention_mask, token_type_ids, labels */
-    int index;
-} obatch;
-
-struct orc_batcher {
-    const orc_tok *t;
-    int task, B, S, mask_length, mask_id;
-    uint64_t seed, n_records;
-    obatch **q;
-    int qh, qn, qcap;
-};
-
-/* BertData::new (bert_data.rs:27-38); labels plane starts at -100 */
-static obatch *obatch_new(int B, int S) {
-    obatch *b = (obatch *)malloc(sizeof(obatch));
-    size_t bs = (size_t)B * S;
-    b->d = (int32_t *)malloc(4 * bs * sizeof(int32_t));
-    for (size_t i = 0; i < bs; ++i) {
-        b->d[i] = 0;
-        b->d[bs + i] = 1;
-        b->d[2 * bs + i] = 0;
-        b->d[3 * bs + i] = -100;
-    }
-    b->index = 0;
-    return b;
-}
-
-static void q_push(orc_batcher *b, obatch *x) {
-    if (b->qh + b->qn == b->qcap) {
-        if (b->qh) {
-            memmove(b->q, b->q + b->qh, sizeof(obatch *) * b->qn);
-            b->qh = 0;
-        } else {
-            b->qcap = b->qcap ? 2 * b->qcap : 8;
-            b->q = (obatch **)realloc(b->q, sizeof(obatch *) * b->qcap);
-        }
-    }
-    b->q[b->qh + b->qn++] = x;
-}
-
-orc_batcher *orc_batcher_new(const orc_tok *t, int task, int batch_size, int seq_len,
-                             int mask_length, int mask_id, uint64_t seed) {
-    if (task != 0 || batch_size <= 0 || seq_len <= 0 || mask_length < 0 || mask_length > seq_len) return NULL;
-    orc_batcher *b = (orc_batcher *)calloc(1, sizeof(orc_batcher));
-    b->t = t;
-    b->task = task;
-    b->B = batch_size;
-    b->S = seq_len;
-    b->mask_length = mask_length;
-    b->mask_id = mask_id;
-    b->seed = seed;
-    q_push(b, obatch_new(b->B, b->S)); /* GenTokenizer::new (gen_batcher.rs:23-41) */
-    return b;
-}
-
-typedef struct { uint32_t key, pos; } kp;
-static int kp_cmp(const void *a, const void *b) {
-    const kp *x = (const kp *)a, *y = (const kp *)b;
-    if (x->key != y->key) return x->key < y->key ? -1 : 1;
-    return x->pos < y->pos ? -1 : (x->pos > y->pos);
-}
-
-/* BertData::put_data (bert_data.rs:55-89) with DataSetConfig::Mask, and
- * mask_batch (bert_data.rs:40-53) under the seeded RNG contract. */
-static void bert_put_data(orc_batcher *b, obatch *x, const uint32_t *ids, size_t n, uint64_t rec, uint32_t chunk) {
-    int S = b->S;
-    size_t bs = (size_t)b->B * S;
-    int32_t *in = x->d + (size_t)x->index * S;
-    int32_t *am = x->d + bs + (size_t)x->index * S;
-    int32_t *lb = x->d + 3 * bs + (size_t)x->index * S;
-    size_t l = n < (size_t)S ? n : (size_t)S;
-    for (size_t j = 0; j < l; ++j) in[j] = (int32_t)ids[j];
-    if (n < (size_t)S)
-        for (size_t j = (size_t)S - n; j < (size_t)S; ++j) am[j] = 0; /* reversed-range quirk */
-    kp *perm = (kp *)malloc(sizeof(kp) * S);
-    for (int p = 0; p < S; ++p) {
-        perm[p].key = orc_mlm_key(b->seed, rec, chunk, (uint32_t)p);
-        perm[p].pos = (uint32_t)p;
-    }
-    qsort(perm, (size_t)S, sizeof(kp), kp_cmp);
-    for (int j = 0; j < S; ++j) lb[j] = -100;
-    for (int k = 0; k < b->mask_length; ++k) {
-        uint32_t p = perm[k].pos;
-        if (in[p] != 0) {
-            lb[p] = in[p];
-            in[p] = b->mask_id;
-        }
-    }
-    free(perm);
-    x->index++;
-}
-
-static void batch_out(orc_batcher *b, obatch *x, int32_t *out, int *rows) {
-    if (out) memcpy(out, x->d, 4 * (size_t)b->B * b->S * sizeof(int32_t));
-    if (rows) *rows = x->index;
-    free(x->d);
-    free(x);
-}
-
-int orc_batcher_push(orc_batcher *b, const uint8_t *s, size_t n, int32_t *out, int *rows) {
-    uint64_t rec = b->n_records++;
-    /* TokenizerWrapper::encode_mask (tokenizer_wrapper.rs:107-116):
-     * [CLS] + encode(text, true) + [SEP] + [SEP] */
-    idvec v = {0};
-    idpush(&v, (uint32_t)b->t->cls);
-    bert_encode_vec(b->t, s, n, &v);
-    idpush(&v, (uint32_t)b->t->sep);
-    idpush(&v, (uint32_t)b->t->sep);
-    if (v.n < 64) { /* gen_batcher.rs:74-76 */
-        free(v.p);
-        return 0;
-    }
-    uint32_t chunk = 0;
-    for (size_t off = 0; off < v.n; off += (size_t)b->S, ++chunk) { /* chunks_mut(S) */
-        size_t len = v.n - off < (size_t)b->S ? v.n - off : (size_t)b->S;
-        obatch *back = b->q[b->qh + b->qn - 1];
-        bert_put_data(b, back, v.p + off, len, rec, chunk); /* handle_internal_batch */
-        if (back->index == b->B) q_push(b, obatch_new(b->B, b->S));
-    }
-    free(v.p);
-    obatch *front = b->q[b->qh];
-    if (front->index == b->B) { /* gen_batcher.rs:86-91: at most one batch per call */
-        b->qh++;
-        b->qn--;
-        batch_out(b, front, out, rows);
-        return 1;
-    }
-    return 0;
-}
-
-int orc_batcher_flush(orc_batcher *b, int32_t *out, int *rows) {
-    if (b->qn == 0) return 0; /* get_working_batch = store.pop_front() */
-    obatch *front = b->q[b->qh];
-    b->qh++;
-    b->qn--;
-    batch_out(b, front, out, rows);
-    return 1;
-}
-
-void orc_batcher_free(orc_batcher *b) {
-    for (int i = 0; i < b->qn; ++i) {
-        free(b->q[b->qh + i]->d);
-        free(b->q[b->qh + i]);
-    }
-    free(b->q);
-    free(b);
-}
-
-void orc_batcher_set_next_record(orc_batcher *b, uint64_t record) { b->n_records = record; }

@@ -40,14 +40,44 @@ long orc_bert_encode(const orc_tok *t, const uint8_t *s, size_t n, uint32_t *out
 /* Philox4x32-10 MLM key of (seed, record, chunk, position) -- RNG contract. */
 uint32_t orc_mlm_key(uint64_t seed, uint64_t record, uint32_t chunk, uint32_t pos);
 
-/* GenTokenizer(chunk) + BertData(Mask). task 0 = mlm (only mode in round 1). */
+/* ---- Batcher ------------------------------------------------------------ */
+enum { ORC_MLM = 0, ORC_CLM = 1, ORC_SPAN = 2, ORC_MULTI_LABEL = 3 }; /* = SDL_TASK_* */
+
+typedef struct orc_encoder orc_encoder; /* a tokenizer + its encode_mask framing */
+
+typedef struct {
+    int32_t task, B, S, chunk, min_ids, mask_length, mask_id, number_labels;
+    double avg_span_gap, avg_span_size;
+    uint64_t seed;
+} orc_cfg;
+
+/* Caller buffers a finished batch is copied into (NULL = skip that plane):
+ * ids/am/tt [B,S], lab [B,LW] (LW = S for mlm/clm), f32 [B,number_labels]. */
+typedef struct {
+    int32_t *ids, *am, *tt, *lab;
+    float *f32;
+    int32_t rows;
+} orc_out;
+
+void orc_cfg_default(orc_cfg *c, int task);
+/* BERT WordPiece encoder with the [CLS] ... [SEP] [SEP] framing.  `e` points
+ * to caller storage of orc_encoder_size() bytes. */
+void orc_encoder_bert(const orc_tok *t, orc_encoder *e);
+size_t orc_encoder_size(void);
+
+orc_batcher *orc_batcher_create(const orc_encoder *e, const orc_cfg *c);
+/* create_sync_batch(record[, Label::Multi indices]): 1 = a batch was emitted
+ * into *out, 0 = none, -1 = label index >= number_labels (reference panics). */
+int orc_batcher_push_ex(orc_batcher *b, const uint8_t *s, size_t n, const uint32_t *labels, size_t nl,
+                        orc_out *out);
+/* get_working_batch(): 1 = *out filled, 0 = none left. */
+int orc_batcher_flush_ex(orc_batcher *b, orc_out *out);
+
+/* Round-1 MLM form: out = 4 planes [B,S] (input_ids, attention_mask,
+ * token_type_ids, labels) back to back.  task must be 0. */
 orc_batcher *orc_batcher_new(const orc_tok *t, int task, int batch_size, int seq_len,
                              int mask_length, int mask_id, uint64_t seed);
-/* create_sync_batch(text).  Returns 1 and fills out (4*B*S int32: input_ids,
- * attention_mask, token_type_ids, labels, each [B,S] row-major) and *rows when a
- * batch is emitted, 0 when not.  Records are numbered 0,1,2,... in push order. */
 int orc_batcher_push(orc_batcher *b, const uint8_t *s, size_t n, int32_t *out, int *rows);
-/* get_working_batch(): pops the front batch (maybe partial). 1 if one existed. */
 int orc_batcher_flush(orc_batcher *b, int32_t *out, int *rows);
 void orc_batcher_free(orc_batcher *b);
 /* Sets the global index the next pushed record gets (sharded streams). */

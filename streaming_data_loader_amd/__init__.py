@@ -5,7 +5,7 @@ MLM mask / CLM labels -> packed [B,S] int32) runs as hand-written gfx950 HIP
 kernels behind the C ABI in include/sdl_batcher.h (libsdl_batcher.so).  This
 package is the Python host mirror of the reference's Batcher interface.
 """
-from .batcher import (Batcher, BatchConfig, DataSet, GenTokenizer, Gpt, Mask, ModelType, MultiLabel,  # noqa: F401
-                      ProviderChannel, Span, TaskType, TokenizerConfig, TrainingConfig, create_batch, get_case,
-                      get_mask_length)
+from .batcher import (Batcher, BatchConfig, DataSet, GenTokenizer, Gpt, Label, Mask, ModelType,  # noqa: F401
+                      MultiLabel, ProviderChannel, SimpleBatcher, SimpleData, SimpleTransport, Span, TaskType,
+                      TokenizerConfig, TrainingConfig, create_batch, get_case, get_mask_length)
 from .native import SDLError  # noqa: F401

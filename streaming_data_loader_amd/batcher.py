@@ -9,6 +9,8 @@ Same names, argument meaning and error behaviour as the reference's Rust:
   ModelType / TaskType   rust/src/config.rs:20-62
   ProviderChannel        rust/src/provider/mod.rs:21-25
   masking cases          rust/src/tasks/masking/masking_cases.rs:34-94
+  SimpleBatcher          rust/src/models/simple_batcher.rs:8-53
+  SimpleTransport/Label  rust/src/models/simple_transport.rs, simple_label.rs
 Every record's tokenize + mask runs in libsdl_batcher.so on the GPU.
 """
 import ctypes
@@ -123,7 +125,8 @@ class ProviderChannel:
 @dataclass
 class DataSet:
     """One batch; `to_dict()` is the reference's Serialize view
-    (bert_data.rs:106-145, gpt_data.rs:53-62)."""
+    (bert_data.rs:106-145, gpt_data.rs:53-62).  `labels` is int32 [B, S] for
+    mlm/clm and float32 [B, number_labels] for multi-label."""
     kind: str
     rows: int
     input_ids: np.ndarray
@@ -133,7 +136,8 @@ class DataSet:
 
     def to_dict(self):
         if self.kind == "bert":
-            # MLM labels: one Vec<i32> per filled row (label list has `index` entries)
+            # BertData.label is pushed per row: the list has `index` entries
+            # (Vec<i32> for Mask, Vec<f32> for MultiLabel)
             return {"input_ids": self.input_ids, "attention_mask": self.attention_mask,
                     "token_type_ids": self.token_type_ids, "labels": self.labels[:self.rows]}
         return {"input_ids": self.input_ids, "attention_mask": self.attention_mask, "labels": self.labels}
@@ -145,11 +149,38 @@ def _dataset_from(b: native.Batch, kind: str) -> DataSet:
     def arr(ptr, n, cols):
         return np.ctypeslib.as_array(ptr, shape=(n * cols,)).reshape(n, cols).copy()
 
+    labels = arr(b.labels_f32, B, LW) if bool(b.labels_f32) else arr(b.labels, B, LW)
     ds = DataSet(kind=kind, rows=b.rows, input_ids=arr(b.input_ids, B, S), attention_mask=arr(b.attention_mask, B, S),
-                 labels=arr(b.labels, B, LW),
-                 token_type_ids=arr(b.token_type_ids, B, S) if bool(b.token_type_ids) else None)
+                 labels=labels, token_type_ids=arr(b.token_type_ids, B, S) if bool(b.token_type_ids) else None)
     native.load().sdl_batch_release(ctypes.byref(b))
     return ds
+
+
+# ---- SimpleTransport (models/simple_transport.rs, simple_label.rs) ----------------
+@dataclass
+class SimpleData:
+    text: str
+    alt_text: Optional[str] = None
+
+
+@dataclass
+class Label:
+    """simple_label::Label; only Multi(Vec<u32>) reaches the GPU Batcher."""
+    multi: Optional[list] = None
+
+
+@dataclass
+class SimpleTransport:
+    data: SimpleData
+    label: Optional[Label] = None
+
+
+def _pack_labels(label_lists):
+    """Label::Multi indices of many records -> (uint32 values, uint64 offsets)."""
+    offs = np.zeros(len(label_lists) + 1, np.uint64)
+    np.cumsum([len(x) for x in label_lists], out=offs[1:])
+    vals = np.fromiter((int(v) for x in label_lists for v in x), np.uint32, count=int(offs[-1]))
+    return vals, offs
 
 
 # ---- Batcher -------------------------------------------------------------------
@@ -163,10 +194,8 @@ class Batcher:
         raise NotImplementedError
 
 
-class GenTokenizer(Batcher):
-    """GenTokenizer (gen_batcher.rs:12-98): S = String, T = DataSet.  Each call
-    tokenizes + masks on the GPU; the emission cadence is the reference's (at
-    most one batch per create_sync_batch, one batch on get_working_batch)."""
+class _NativeBatcher(Batcher):
+    """One sdl_batcher handle (include/sdl_batcher.h)."""
 
     def __init__(self, model_type: ModelType, batch_config: BatchConfig, dataset_config: DataSetConfig,
                  tokenizer: TokenizerConfig, chunk: bool = True, seed: int = 0, device: int = 0,
@@ -209,22 +238,27 @@ class GenTokenizer(Batcher):
 
     __del__ = close
 
-    def create_sync_batch(self, data: str) -> Optional[DataSet]:
+    def _push(self, raw: bytes, labels=None) -> Optional[DataSet]:
         b = native.Batch()
-        raw = data.encode("utf-8") if isinstance(data, str) else bytes(data)
-        got = native.check(native.load().sdl_batcher_push(self._h, raw, len(raw), None, 0, ctypes.byref(b)))
+        lab = None if labels is None else np.ascontiguousarray(labels, np.uint32)
+        got = native.check(native.load().sdl_batcher_push(self._h, raw, len(raw),
+                                                          None if lab is None else lab.ctypes.data,
+                                                          0 if lab is None else lab.size, ctypes.byref(b)))
         return _dataset_from(b, self.kind) if got else None
 
-    def create_sync_batches(self, texts):
-        """create_sync_batch over many records in one device pass; returns the
-        batches the same sequence of calls would have emitted, in order."""
-        blobs = [t.encode("utf-8") if isinstance(t, str) else bytes(t) for t in texts]
-        offs = np.zeros(len(blobs) + 1, np.uint64)
-        np.cumsum([len(x) for x in blobs], out=offs[1:])
-        arena = np.frombuffer(b"".join(blobs) + b"\0" * 16, np.uint8)
+    def push_arena(self, arena, offsets, labels=None, label_offsets=None):
+        """sdl_batcher_push_many over a host arena (uint8) + uint64 offsets
+        (+ uint32 label values / uint64 label offsets); returns the batches
+        the same sequence of create_sync_batch calls would have emitted."""
+        arena = np.ascontiguousarray(arena, np.uint8)
+        offsets = np.ascontiguousarray(offsets, np.uint64)
         n = ctypes.c_size_t()
-        native.check(native.load().sdl_batcher_push_many(self._h, arena.ctypes.data, offs.ctypes.data, len(blobs),
-                                                         None, None, ctypes.byref(n)))
+        lv = None if labels is None else np.ascontiguousarray(labels, np.uint32)
+        lo = None if label_offsets is None else np.ascontiguousarray(label_offsets, np.uint64)
+        native.check(native.load().sdl_batcher_push_many(
+            self._h, arena.ctypes.data, offsets.ctypes.data, offsets.size - 1,
+            None if lv is None or lv.size == 0 else lv.ctypes.data, None if lo is None else lo.ctypes.data,
+            ctypes.byref(n)))
         out = []
         b = native.Batch()
         while native.check(native.load().sdl_batcher_next(self._h, ctypes.byref(b))):
@@ -235,6 +269,66 @@ class GenTokenizer(Batcher):
         b = native.Batch()
         got = native.check(native.load().sdl_batcher_flush(self._h, ctypes.byref(b)))
         return _dataset_from(b, self.kind) if got else None
+
+
+class GenTokenizer(_NativeBatcher):
+    """GenTokenizer (gen_batcher.rs:12-98): S = String, T = DataSet.  Each call
+    tokenizes + masks on the GPU; the emission cadence is the reference's (at
+    most one batch per create_sync_batch, one batch on get_working_batch)."""
+
+    def create_sync_batch(self, data: str) -> Optional[DataSet]:
+        return self._push(data.encode("utf-8") if isinstance(data, str) else bytes(data))
+
+    def create_sync_batches(self, texts):
+        """create_sync_batch over many records in one device pass; returns the
+        batches the same sequence of calls would have emitted, in order."""
+        blobs = [t.encode("utf-8") if isinstance(t, str) else bytes(t) for t in texts]
+        offs = np.zeros(len(blobs) + 1, np.uint64)
+        np.cumsum([len(x) for x in blobs], out=offs[1:])
+        arena = np.frombuffer(b"".join(blobs) + b"\0" * 16, np.uint8)
+        return self.push_arena(arena, offs)
+
+
+class SimpleBatcher(_NativeBatcher):
+    """SimpleBatcher (models/simple_batcher.rs:8-53): S = SimpleTransport,
+    T = DataSet, for DataSetConfig::MultiLabel.  One row per record (encode_mask
+    framing, truncated at S, no <64 filter); the batch is returned by the
+    create_sync_batch call that fills it; get_working_batch always returns the
+    current (possibly empty) batch and starts a new one."""
+
+    def __init__(self, model_type: ModelType, dataset_config: DataSetConfig, batch_config: BatchConfig,
+                 tokenizer: TokenizerConfig, seed: int = 0, device: int = 0):
+        if not isinstance(dataset_config, MultiLabel):
+            raise ValueError("SimpleBatcher on the GPU path supports DataSetConfig::MultiLabel")
+        super().__init__(model_type, batch_config, dataset_config, tokenizer, False, seed, device)
+
+    @classmethod
+    def from_config(cls, cfg: TrainingConfig):
+        """single_class::runner::create_generator (single_class/runner.rs:40-49)."""
+        return cls(cfg.model_config, cfg.dataset_config, cfg.batch, cfg.tokenizer, cfg.seed, cfg.device)
+
+    def create_sync_batch(self, data: SimpleTransport) -> Optional[DataSet]:
+        text = data.data.text
+        raw = text.encode("utf-8") if isinstance(text, str) else bytes(text)
+        if data.label is None or data.label.multi is None:
+            raise ValueError("Label Type Not Supported")  # bert_data.rs:75 panics
+        return self._push(raw, data.label.multi)
+
+    def create_sync_batches(self, items):
+        """create_sync_batch over many SimpleTransport records in one device pass."""
+        blobs = [t.data.text.encode("utf-8") if isinstance(t.data.text, str) else bytes(t.data.text) for t in items]
+        offs = np.zeros(len(blobs) + 1, np.uint64)
+        np.cumsum([len(x) for x in blobs], out=offs[1:])
+        arena = np.frombuffer(b"".join(blobs) + b"\0" * 16, np.uint8)
+        vals, loffs = _pack_labels([t.label.multi for t in items])
+        return self.push_arena(arena, offs, vals, loffs)
+
+    def push_arrow(self, record_batch, text_col="sentence", label_col="labels"):
+        """create_sync_batch for every row of an Arrow record batch with the
+        MultiArrowGenerator schema, fed from the column buffers directly."""
+        from .arrow_io import arena_from_batch
+        a = arena_from_batch(record_batch, text_col, label_col)
+        return self.push_arena(a.arena, a.offsets, a.labels, a.label_offsets)
 
 
 def create_batch(rx, tx, batcher: Batcher):

@@ -46,4 +46,9 @@ hipError_t launch_rows(const RowParams &P, const uint32_t *tok, const uint32_t *
                        const uint32_t *row_off, const uint32_t *row_rec, const uint32_t *d_rows, int64_t rows_cap,
                        RowOut out, hipStream_t st);
 
+// BertData MultiLabel labels_f32 plane (bert_data.rs:66-78)
+hipError_t launch_multi_labels(const uint32_t *labels, const uint64_t *label_off, const uint32_t *row_rec,
+                               const uint32_t *d_rows, int64_t rows_cap, int B, int NL, float *out, uint32_t *err,
+                               hipStream_t st);
+
 }  // namespace sdl

@@ -272,7 +272,7 @@ __global__ __launch_bounds__(256) void k_rows(RowParams P, const uint32_t *__res
         int32_t *ids_o = out.input_ids + g * S;
         int32_t *am_o = out.attention_mask + g * S;
         int32_t *tt_o = out.token_type_ids ? out.token_type_ids + g * S : nullptr;
-        int32_t *lb_o = out.labels + g * (int64_t)P.label_width;
+        int32_t *lb_o = out.labels ? out.labels + g * (int64_t)P.label_width : nullptr;
         if (g >= (int64_t)G) {  // rows of the last batch nobody filled: initial values
 #pragma unroll
             for (int m = 0; m < MR; ++m) {
@@ -280,7 +280,7 @@ __global__ __launch_bounds__(256) void k_rows(RowParams P, const uint32_t *__res
                 store4(ids_o, j0, S, vec, 0, 0, 0, 0);
                 store4(am_o, j0, S, vec, 1, 1, 1, 1);
                 if (tt_o) store4(tt_o, j0, S, vec, 0, 0, 0, 0);
-                store4(lb_o, j0, P.label_width, vec_lb, -100, -100, -100, -100);
+                if (lb_o) store4(lb_o, j0, P.label_width, vec_lb, -100, -100, -100, -100);
             }
             continue;
         }
@@ -344,6 +344,17 @@ __global__ __launch_bounds__(256) void k_rows(RowParams P, const uint32_t *__res
                 if (tt_o) store4(tt_o, j0, S, vec, 0, 0, 0, 0);
                 store4(lb_o, j0, P.label_width, vec_lb, lab[0], lab[1], lab[2], lab[3]);
             }
+        } else if (P.task == 3) {  // MultiLabel: BertData::put_data rows; labels_f32 by k_multi_labels
+#pragma unroll
+            for (int m = 0; m < MR; ++m) {
+                const int j0 = 256 * m + 4 * lane;
+                int32_t am[4];
+#pragma unroll
+                for (int w = 0; w < 4; ++w) am[w] = j0 + w >= tail0 ? 0 : 1;
+                store4(ids_o, j0, S, vec, id[m][0], id[m][1], id[m][2], id[m][3]);
+                store4(am_o, j0, S, vec, am[0], am[1], am[2], am[3]);
+                if (tt_o) store4(tt_o, j0, S, vec, 0, 0, 0, 0);
+            }
         } else {  // CLM: GptData::put_data, labels = row as i32 (no shift)
 #pragma unroll
             for (int m = 0; m < MR; ++m) {
@@ -381,6 +392,42 @@ hipError_t launch_rows(const RowParams &P, const uint32_t *tok, const uint32_t *
     else if (MR <= 8) SDL_ROWS(8);
     else return hipErrorInvalidValue;
 #undef SDL_ROWS
+    return hipGetLastError();
+}
+
+// BertData MultiLabel branch (bert_data.rs:66-78): labels_f32[row] = zeros with
+// 1.0 at each Label::Multi index.  An index >= number_labels (the reference
+// panics) is skipped and counted in *err.  Rows past the last batch: zeros.
+__global__ __launch_bounds__(256) void k_multi_labels(const uint32_t *__restrict__ labels,
+                                                      const uint64_t *__restrict__ label_off,
+                                                      const uint32_t *__restrict__ row_rec,
+                                                      const uint32_t *__restrict__ d_rows, int64_t rows_cap, int B,
+                                                      int NL, float *__restrict__ out, uint32_t *__restrict__ err) {
+    const uint32_t G = *d_rows;
+    int64_t Gpad = ((int64_t)G + B - 1) / B * B;
+    if (Gpad > rows_cap) Gpad = rows_cap;
+    for (int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x; g < Gpad; g += (int64_t)gridDim.x * 256) {
+        float *o = out + g * NL;
+        for (int k = 0; k < NL; ++k) o[k] = 0.f;
+        if (g >= (int64_t)G || !labels) continue;
+        const uint32_t r = row_rec[g];
+        uint32_t bad = 0;
+        for (uint64_t i = label_off[r]; i < label_off[r + 1]; ++i) {
+            const uint32_t x = labels[i];
+            if (x < (uint32_t)NL) o[x] = 1.f;
+            else ++bad;
+        }
+        if (bad) atomicAdd(err, bad);
+    }
+}
+
+hipError_t launch_multi_labels(const uint32_t *labels, const uint64_t *label_off, const uint32_t *row_rec,
+                               const uint32_t *d_rows, int64_t rows_cap, int B, int NL, float *out, uint32_t *err,
+                               hipStream_t st) {
+    if (rows_cap == 0) return hipSuccess;
+    const int64_t want = (rows_cap + 255) / 256;
+    hipLaunchKernelGGL(k_multi_labels, dim3((unsigned)(want < 2048 ? want : 2048)), dim3(256), 0, st, labels,
+                       label_off, row_rec, d_rows, rows_cap, B, NL, out, err);
     return hipGetLastError();
 }
 

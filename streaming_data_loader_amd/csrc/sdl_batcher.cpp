@@ -84,13 +84,15 @@ struct PinBuf {
 // BatchConfig::create_vector (batcher.rs:17-22) and BertData::new (bert_data.rs:27-38).
 struct HostBatch {
     std::vector<int32_t> ids, am, tt, lab;
+    std::vector<float> f32;  // MultiLabel: [B, number_labels]
     int rows = 0;
     int B, S, LW;
-    HostBatch(int B_, int S_, int LW_, bool with_tt) : B(B_), S(S_), LW(LW_) {
+    HostBatch(int B_, int S_, int LW_, bool with_tt, bool multi) : B(B_), S(S_), LW(LW_) {
         ids.assign((size_t)B * S, 0);
         am.assign((size_t)B * S, 1);
         if (with_tt) tt.assign((size_t)B * S, 0);
-        lab.assign((size_t)B * LW, -100);
+        if (multi) f32.assign((size_t)B * LW, 0.f);
+        else lab.assign((size_t)B * LW, -100);
     }
 };
 
@@ -118,8 +120,11 @@ struct sdl_batcher {
     DevBuf<uint32_t> ranges, tokc, chunk_cnt, chunk_off, rec_local, tok_ids, rec_tok, rec_cnt, rec_rows, row_off,
         row_rec, scan_tmp;
     DevBuf<int32_t> o_ids, o_am, o_tt, o_lab;
+    DevBuf<float> o_f32;
+    DevBuf<uint32_t> lab_err;
     DevBuf<uint8_t> h2d_text;
-    DevBuf<uint64_t> h2d_off;
+    DevBuf<uint64_t> h2d_off, h2d_label_off;
+    DevBuf<uint32_t> h2d_labels;
 
     // host streaming path (GenTokenizer.store + emitted batches)
     std::deque<HostBatch *> store;
@@ -128,6 +133,8 @@ struct sdl_batcher {
     PinBuf<uint64_t> pin_off;
     PinBuf<uint32_t> pin_u32;
     PinBuf<int32_t> pin_rows;
+    PinBuf<uint32_t> pin_labels;
+    PinBuf<uint64_t> pin_label_off;
     uint64_t n_records = 0;
 
     bool profiling = false;
@@ -147,9 +154,10 @@ struct sdl_batcher {
         if (stream) (void)hipStreamDestroy(stream);
     }
 
-    HostBatch *new_batch() const {
-        return new HostBatch(P.B, P.S, P.label_width, P.task == SDL_TASK_MLM || P.task == SDL_TASK_MULTI_LABEL);
-    }
+    bool multi() const { return P.task == SDL_TASK_MULTI_LABEL; }
+    bool with_tt() const { return P.task == SDL_TASK_MLM || P.task == SDL_TASK_MULTI_LABEL; }
+
+    HostBatch *new_batch() const { return new HostBatch(P.B, P.S, P.label_width, with_tt(), multi()); }
 
     int64_t rows_capacity(int64_t N, int64_t R) const {
         // rows <= sum_r ceil((ids_r + frame) / S) with ids_r <= bytes_r
@@ -159,7 +167,7 @@ struct sdl_batcher {
     }
 
     void run_device(const uint8_t *d_text, int64_t N, const uint64_t *d_off, int64_t R, uint64_t first_record,
-                    hipStream_t st) {
+                    hipStream_t st, const uint32_t *d_labels = nullptr, const uint64_t *d_label_off = nullptr) {
         const int64_t n_chunks = (N + CHUNK - 1) / CHUNK;
         const int64_t rows_cap = rows_capacity(N, R);
         ranges.ensure((size_t)std::max<int64_t>(n_chunks, 1) * 3);
@@ -176,8 +184,13 @@ struct sdl_batcher {
         const size_t plane = (size_t)std::max<int64_t>(rows_cap, 1) * P.S;
         o_ids.ensure(plane);
         o_am.ensure(plane);
-        if (P.task == SDL_TASK_MLM || P.task == SDL_TASK_MULTI_LABEL) o_tt.ensure(plane);
-        o_lab.ensure((size_t)std::max<int64_t>(rows_cap, 1) * P.label_width);
+        if (with_tt()) o_tt.ensure(plane);
+        if (multi()) {
+            o_f32.ensure((size_t)std::max<int64_t>(rows_cap, 1) * P.label_width);
+            lab_err.ensure(1);
+        } else {
+            o_lab.ensure((size_t)std::max<int64_t>(rows_cap, 1) * P.label_width);
+        }
         row_rec.ensure((size_t)std::max<int64_t>(rows_cap, 1));
 
         RowParams p = P;
@@ -198,9 +211,14 @@ struct sdl_batcher {
         HIP_TRY(launch_exclusive_scan(rec_rows.p, row_off.p, R, scan_tmp.p, st));
         HIP_TRY(launch_row_map(row_off.p, R, row_rec.p, st));
         mark(5);
-        RowOut out{o_ids.p, o_am.p, (P.task == SDL_TASK_MLM || P.task == SDL_TASK_MULTI_LABEL) ? o_tt.p : nullptr,
-                   o_lab.p, nullptr};
+        RowOut out{o_ids.p, o_am.p, with_tt() ? o_tt.p : nullptr, multi() ? nullptr : o_lab.p,
+                   multi() ? o_f32.p : nullptr};
         HIP_TRY(launch_rows(p, tok_ids.p, rec_tok.p, rec_cnt.p, row_off.p, row_rec.p, row_off.p + R, rows_cap, out, st));
+        if (multi()) {
+            HIP_TRY(hipMemsetAsync(lab_err.p, 0, 4, st));
+            HIP_TRY(launch_multi_labels(d_labels, d_label_off, row_rec.p, row_off.p + R, rows_cap, P.B, P.label_width,
+                                        o_f32.p, lab_err.p, st));
+        }
         mark(6);
         last_rows_cap = rows_cap;
         last_R = R;
@@ -209,8 +227,25 @@ struct sdl_batcher {
 
     // H2D a host arena, run the device path, bring back the rows; then play
     // GenTokenizer's queue over the per-record row counts.
-    void process_host(const uint8_t *arena, const uint64_t *offsets, int64_t R, std::vector<int> *emitted_per_record) {
+    void process_host(const uint8_t *arena, const uint64_t *offsets, int64_t R, const uint32_t *labels,
+                      const uint64_t *label_off) {
         const int64_t N = (int64_t)offsets[R];
+        const uint32_t *d_labels = nullptr;
+        const uint64_t *d_label_off = nullptr;
+        if (multi() && labels && label_off) {  // Label::Multi indices, validated by the caller
+            const uint64_t L = label_off[R];
+            pin_labels.ensure((size_t)L + 1);
+            pin_label_off.ensure((size_t)R + 1);
+            std::memcpy(pin_labels.p, labels, sizeof(uint32_t) * (size_t)L);
+            for (int64_t r = 0; r <= R; ++r) pin_label_off.p[r] = label_off[r] - label_off[0];
+            h2d_labels.ensure((size_t)L + 1);
+            h2d_label_off.ensure((size_t)R + 1);
+            if (L) HIP_TRY(hipMemcpyAsync(h2d_labels.p, pin_labels.p, sizeof(uint32_t) * L, hipMemcpyHostToDevice, stream));
+            HIP_TRY(hipMemcpyAsync(h2d_label_off.p, pin_label_off.p, sizeof(uint64_t) * (size_t)(R + 1),
+                                   hipMemcpyHostToDevice, stream));
+            d_labels = h2d_labels.p;
+            d_label_off = h2d_label_off.p;
+        }
         pin_text.ensure((size_t)N + 16);
         pin_off.ensure((size_t)R + 1);
         std::memcpy(pin_text.p, arena, (size_t)N);
@@ -219,13 +254,13 @@ struct sdl_batcher {
         h2d_off.ensure((size_t)R + 1);
         HIP_TRY(hipMemcpyAsync(h2d_text.p, pin_text.p, (size_t)N, hipMemcpyHostToDevice, stream));
         HIP_TRY(hipMemcpyAsync(h2d_off.p, pin_off.p, sizeof(uint64_t) * (size_t)(R + 1), hipMemcpyHostToDevice, stream));
-        run_device(h2d_text.p, N, h2d_off.p, R, cfg.first_record + n_records, stream);
+        run_device(h2d_text.p, N, h2d_off.p, R, cfg.first_record + n_records, stream, d_labels, d_label_off);
         pin_u32.ensure((size_t)R + 1);
         HIP_TRY(hipMemcpyAsync(pin_u32.p, row_off.p, sizeof(uint32_t) * (size_t)(R + 1), hipMemcpyDeviceToHost, stream));
         HIP_TRY(hipStreamSynchronize(stream));
         const uint32_t G = pin_u32.p[R];
         const size_t S = (size_t)P.S, LW = (size_t)P.label_width;
-        const bool with_tt = P.task == SDL_TASK_MLM || P.task == SDL_TASK_MULTI_LABEL;
+        const bool with_tt = this->with_tt();
         const size_t planes = with_tt ? 3 : 2;
         pin_rows.ensure((size_t)G * (planes * S + LW) + 1);
         int32_t *h_ids = pin_rows.p, *h_am = h_ids + (size_t)G * S, *h_tt = h_am + (size_t)G * S;
@@ -234,7 +269,8 @@ struct sdl_batcher {
             HIP_TRY(hipMemcpyAsync(h_ids, o_ids.p, sizeof(int32_t) * G * S, hipMemcpyDeviceToHost, stream));
             HIP_TRY(hipMemcpyAsync(h_am, o_am.p, sizeof(int32_t) * G * S, hipMemcpyDeviceToHost, stream));
             if (with_tt) HIP_TRY(hipMemcpyAsync(h_tt, o_tt.p, sizeof(int32_t) * G * S, hipMemcpyDeviceToHost, stream));
-            HIP_TRY(hipMemcpyAsync(h_lab, o_lab.p, sizeof(int32_t) * G * LW, hipMemcpyDeviceToHost, stream));
+            HIP_TRY(hipMemcpyAsync(h_lab, multi() ? (const void *)o_f32.p : (const void *)o_lab.p, 4 * G * LW,
+                                   hipMemcpyDeviceToHost, stream));
             HIP_TRY(hipStreamSynchronize(stream));
         }
         // GenTokenizer::create_sync_batch per record (gen_batcher.rs:69-94)
@@ -246,7 +282,8 @@ struct sdl_batcher {
                 std::memcpy(&b->ids[dst * S], h_ids + (size_t)g * S, S * 4);
                 std::memcpy(&b->am[dst * S], h_am + (size_t)g * S, S * 4);
                 if (with_tt) std::memcpy(&b->tt[dst * S], h_tt + (size_t)g * S, S * 4);
-                std::memcpy(&b->lab[dst * LW], h_lab + (size_t)g * LW, LW * 4);
+                std::memcpy(multi() ? (void *)&b->f32[dst * LW] : (void *)&b->lab[dst * LW], h_lab + (size_t)g * LW,
+                            LW * 4);
                 b->rows++;
                 if (b->rows == P.B) store.push_back(new_batch());
             }
@@ -256,7 +293,7 @@ struct sdl_batcher {
                 store.pop_front();
                 emitted = 1;
             }
-            if (emitted_per_record) emitted_per_record->push_back(emitted);
+            (void)emitted;
         }
         n_records += (uint64_t)R;
     }
@@ -273,7 +310,8 @@ void fill_batch(const sdl_batcher *h, HostBatch *b, sdl_batch *out) {
     out->input_ids = b->ids.data();
     out->attention_mask = b->am.data();
     out->token_type_ids = b->tt.empty() ? nullptr : b->tt.data();
-    out->labels = b->lab.data();
+    out->labels = b->lab.empty() ? nullptr : b->lab.data();
+    out->labels_f32 = b->f32.empty() ? nullptr : b->f32.data();
     out->owner_ = b;
     (void)h;
 }
@@ -315,8 +353,10 @@ void sdl_config_default(sdl_config *c, int32_t task) {
 int sdl_batcher_create(const sdl_config *cfg, const char *tokenizer_path, const char *data_dir, sdl_batcher **out) {
     if (!cfg || !tokenizer_path || !out) return fail(SDL_ERR_ARG, "null argument");
     *out = nullptr;
-    if (cfg->task != SDL_TASK_MLM && cfg->task != SDL_TASK_CLM)
-        return fail(SDL_ERR_UNSUPPORTED, "task not implemented in this build (mlm, clm)");
+    if (cfg->task != SDL_TASK_MLM && cfg->task != SDL_TASK_CLM && cfg->task != SDL_TASK_MULTI_LABEL)
+        return fail(SDL_ERR_UNSUPPORTED, "task not implemented in this build (mlm, clm, multi-label)");
+    if (cfg->task == SDL_TASK_MULTI_LABEL && (cfg->number_labels <= 0 || cfg->number_labels > 4096))
+        return fail(SDL_ERR_ARG, "number_labels must be in [1, 4096]");
     if (cfg->batch_size <= 0 || cfg->sequence_length <= 0 || cfg->sequence_length > 2048)
         return fail(SDL_ERR_ARG, "batch_size must be > 0 and 0 < sequence_length <= 2048");
     if (cfg->task == SDL_TASK_MLM && (cfg->mask_length < 0 || cfg->mask_length > cfg->sequence_length))
@@ -376,7 +416,11 @@ int sdl_batcher_create(const sdl_config *cfg, const char *tokenizer_path, const 
         P.min_ids = cfg->min_ids;
         P.mask_length = cfg->mask_length;
         P.mask_id = cfg->mask_id;
-        P.label_width = cfg->sequence_length;
+        P.label_width = cfg->task == SDL_TASK_MULTI_LABEL ? cfg->number_labels : cfg->sequence_length;
+        if (cfg->task == SDL_TASK_MULTI_LABEL) {  // SimpleBatcher: one row per record, no filter
+            P.chunk = 0;
+            P.min_ids = 0;
+        }
         P.seed = cfg->seed;
         // encode_mask framing (tokenizer_wrapper.rs:107-116): [CLS] + template([CLS] $A [SEP]) + [SEP] [SEP]
         P.n_pre = 2;
@@ -398,16 +442,28 @@ int sdl_batcher_create(const sdl_config *cfg, const char *tokenizer_path, const 
 
 void sdl_batcher_destroy(sdl_batcher *h) { delete h; }
 
+namespace {
+// BertData::put_data panics on an index >= number_labels (bert_data.rs:70-72)
+int check_labels(const sdl_batcher *h, const uint32_t *labels, size_t n) {
+    for (size_t i = 0; i < n; ++i)
+        if (labels[i] >= (uint32_t)h->P.label_width)
+            return fail(SDL_ERR_ARG, "label index " + std::to_string(labels[i]) + " >= number_labels");
+    return SDL_OK;
+}
+}  // namespace
+
 int sdl_batcher_push(sdl_batcher *h, const uint8_t *utf8, size_t len, const uint32_t *labels, size_t n_labels,
                      sdl_batch *out) {
-    (void)labels;
-    (void)n_labels;
-    if (!h || (!utf8 && len)) return fail(SDL_ERR_ARG, "null argument");
+    if (!h || (!utf8 && len) || (!labels && n_labels)) return fail(SDL_ERR_ARG, "null argument");
+    if (h->multi()) {
+        if (int rc = check_labels(h, labels, n_labels)) return rc;
+    }
     if (len >= (1ull << 32)) return fail(SDL_ERR_CAPACITY, "record too large");
     try {
         uint64_t offs[2] = {0, (uint64_t)len};
+        uint64_t loffs[2] = {0, (uint64_t)n_labels};
         const size_t before = h->outbox.size();
-        h->process_host(utf8 ? utf8 : (const uint8_t *)"", offs, 1, nullptr);
+        h->process_host(utf8 ? utf8 : (const uint8_t *)"", offs, 1, labels, loffs);
         if (h->outbox.size() > before) {
             HostBatch *b = h->outbox.back();
             h->outbox.pop_back();
@@ -425,16 +481,22 @@ int sdl_batcher_push(sdl_batcher *h, const uint8_t *utf8, size_t len, const uint
 
 int sdl_batcher_push_many(sdl_batcher *h, const uint8_t *arena, const uint64_t *offsets, size_t n_records,
                           const uint32_t *labels, const uint64_t *label_offsets, size_t *n_emitted) {
-    (void)labels;
-    (void)label_offsets;
     if (!h || !offsets || (!arena && n_records && offsets[n_records])) return fail(SDL_ERR_ARG, "null argument");
+    if (h->multi() && label_offsets) {
+        if (!labels && label_offsets[n_records] != label_offsets[0]) return fail(SDL_ERR_ARG, "null labels");
+        for (size_t r = 0; r < n_records; ++r)
+            if (label_offsets[r + 1] < label_offsets[r]) return fail(SDL_ERR_ARG, "label_offsets must be non-decreasing");
+        if (int rc = check_labels(h, labels + label_offsets[0], label_offsets[n_records] - label_offsets[0])) return rc;
+    }
     if (offsets[0] != 0) return fail(SDL_ERR_ARG, "offsets[0] must be 0");
     for (size_t r = 0; r < n_records; ++r)
         if (offsets[r + 1] < offsets[r]) return fail(SDL_ERR_ARG, "offsets must be non-decreasing");
     if (offsets[n_records] >= (1ull << 32)) return fail(SDL_ERR_CAPACITY, "arena must be < 4 GiB per call");
     try {
         const size_t before = h->outbox.size();
-        if (n_records) h->process_host(arena, offsets, (int64_t)n_records, nullptr);
+        if (n_records)
+            h->process_host(arena, offsets, (int64_t)n_records, labels ? labels + (label_offsets ? label_offsets[0] : 0) : nullptr,
+                            label_offsets);
         if (n_emitted) *n_emitted = h->outbox.size() - before;
         return SDL_OK;
     } catch (HipError &e) {
@@ -455,9 +517,11 @@ int sdl_batcher_next(sdl_batcher *h, sdl_batch *out) {
 
 int sdl_batcher_flush(sdl_batcher *h, sdl_batch *out) {
     if (!h || !out) return fail(SDL_ERR_ARG, "null argument");
-    if (h->store.empty()) return 0;  // get_working_batch = store.pop_front()
+    if (h->store.empty()) return 0;  // GenTokenizer::get_working_batch = store.pop_front()
     HostBatch *b = h->store.front();
     h->store.pop_front();
+    // SimpleBatcher::get_working_batch swaps in a fresh DataSet (simple_batcher.rs:46-52)
+    if (h->multi() && h->store.empty()) h->store.push_back(h->new_batch());
     fill_batch(h, b, out);
     return 1;
 }
@@ -470,17 +534,28 @@ void sdl_batch_release(sdl_batch *b) {
 
 int sdl_process_device(sdl_batcher *h, const uint8_t *d_text, uint64_t text_len, const uint64_t *d_offsets,
                        uint64_t n_records, uint64_t first_record, void *stream, sdl_device_rows *out) {
+    return sdl_process_device_labels(h, d_text, text_len, d_offsets, n_records, nullptr, nullptr, first_record, stream,
+                                     out);
+}
+
+int sdl_process_device_labels(sdl_batcher *h, const uint8_t *d_text, uint64_t text_len, const uint64_t *d_offsets,
+                              uint64_t n_records, const uint32_t *d_labels, const uint64_t *d_label_offsets,
+                              uint64_t first_record, void *stream, sdl_device_rows *out) {
     if (!h || !out || !d_offsets || (!d_text && text_len)) return fail(SDL_ERR_ARG, "null argument");
+    if ((d_labels == nullptr) != (d_label_offsets == nullptr)) return fail(SDL_ERR_ARG, "labels need label offsets");
     if (text_len >= (1ull << 32)) return fail(SDL_ERR_CAPACITY, "arena must be < 4 GiB per call");
     if (((uintptr_t)d_text & 15u) != 0) return fail(SDL_ERR_ARG, "d_text must be 16-byte aligned");
     try {
         hipStream_t st = stream ? (hipStream_t)stream : h->stream;
-        h->run_device(d_text, (int64_t)text_len, d_offsets, (int64_t)n_records, first_record, st);
+        h->run_device(d_text, (int64_t)text_len, d_offsets, (int64_t)n_records, first_record, st, d_labels,
+                      d_label_offsets);
         std::memset(out, 0, sizeof(*out));
         out->input_ids = h->o_ids.p;
         out->attention_mask = h->o_am.p;
-        out->token_type_ids = (h->P.task == SDL_TASK_MLM || h->P.task == SDL_TASK_MULTI_LABEL) ? h->o_tt.p : nullptr;
-        out->labels = h->o_lab.p;
+        out->token_type_ids = h->with_tt() ? h->o_tt.p : nullptr;
+        out->labels = h->multi() ? nullptr : h->o_lab.p;
+        out->labels_f32 = h->multi() ? h->o_f32.p : nullptr;
+        out->d_label_errors = h->multi() ? h->lab_err.p : nullptr;
         out->d_rows = h->row_off.p + n_records;
         out->d_record_rows = h->rec_rows.p;
         out->d_tokens = h->chunk_off.p + (text_len + CHUNK - 1) / CHUNK;

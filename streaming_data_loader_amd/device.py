@@ -32,32 +32,43 @@ class DeviceResult:
         native.d2h(self.h, v, self.r.d_record_rows, 4 * self.n_records)
         return v
 
+    def label_errors(self):
+        """Multi-label: Label::Multi indices >= number_labels that were skipped."""
+        if not self.r.d_label_errors:
+            return 0
+        v = np.zeros(1, np.uint32)
+        native.d2h(self.h, v, self.r.d_label_errors, 4)
+        return int(v[0])
+
     def planes(self, n_rows=None):
-        """(input_ids, attention_mask, token_type_ids|None, labels) as numpy [n, S]."""
+        """(input_ids, attention_mask, token_type_ids|None, labels) as numpy [n, S]
+        (labels: int32 [n, S] for mlm/clm, float32 [n, number_labels] for multi-label)."""
         n = self.rows() if n_rows is None else n_rows
         S, LW = self.S, self.r.label_width
 
-        def get(ptr, w):
-            a = np.zeros((n, w), np.int32)
+        def get(ptr, w, dt=np.int32):
+            a = np.zeros((n, w), dt)
             if ptr:
                 native.d2h(self.h, a, ptr, a.nbytes)
                 return a
             return None
 
-        return (get(self.r.input_ids, S), get(self.r.attention_mask, S), get(self.r.token_type_ids, S),
-                get(self.r.labels, LW))
+        lab = get(self.r.labels_f32, LW, np.float32) if self.r.labels_f32 else get(self.r.labels, LW)
+        return (get(self.r.input_ids, S), get(self.r.attention_mask, S), get(self.r.token_type_ids, S), lab)
 
 
 class DeviceBatcher:
     """Owns one sdl_batcher handle used through sdl_process_device."""
 
     def __init__(self, task=native.SDL_TASK_MLM, batch_size=256, sequence_length=512, mask_length=None,
-                 mask_id=103, seed=0, device=0, tokenizer=native.BERT_PROXY_TOKENIZER, chunk=True, min_ids=None):
+                 mask_id=103, seed=0, device=0, tokenizer=native.BERT_PROXY_TOKENIZER, chunk=True, min_ids=None,
+                 number_labels=9):
         L = native.load()
         c = native.default_config(task)
         c.batch_size, c.sequence_length = batch_size, sequence_length
         c.mask_length = int(np.float32(sequence_length) * np.float32(0.15)) if mask_length is None else mask_length
         c.mask_id, c.seed, c.device, c.chunk = mask_id, seed, device, 1 if chunk else 0
+        c.number_labels = number_labels
         if min_ids is not None:
             c.min_ids = min_ids
         self.cfg = c
@@ -88,6 +99,16 @@ class DeviceBatcher:
         native.check(native.load().sdl_process_device(self._h, ctypes.c_void_p(text_ptr), text_len,
                                                       ctypes.c_void_p(offsets_ptr), n_records, first_record,
                                                       ctypes.c_void_p(stream or None), ctypes.byref(out)))
+        return DeviceResult(self._h, out, n_records, self.cfg.sequence_length)
+
+    def process_labels(self, text_ptr, text_len, offsets_ptr, n_records, labels_ptr, label_offsets_ptr,
+                       first_record=0, stream=0):
+        """Multi-label task: Label::Multi indices per record in device memory."""
+        out = native.DeviceRows()
+        native.check(native.load().sdl_process_device_labels(
+            self._h, ctypes.c_void_p(text_ptr), text_len, ctypes.c_void_p(offsets_ptr), n_records,
+            ctypes.c_void_p(labels_ptr or None), ctypes.c_void_p(label_offsets_ptr or None), first_record,
+            ctypes.c_void_p(stream or None), ctypes.byref(out)))
         return DeviceResult(self._h, out, n_records, self.cfg.sequence_length)
 
     def process_tensors(self, text, offsets, first_record=0, stream=None):

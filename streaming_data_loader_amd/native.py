@@ -18,7 +18,7 @@ SDL_TASK_MLM, SDL_TASK_CLM, SDL_TASK_SPAN, SDL_TASK_MULTI_LABEL = 0, 1, 2, 3
 EXPORTS = [
     "sdl_config_default", "sdl_batcher_create", "sdl_batcher_destroy", "sdl_batcher_push",
     "sdl_batcher_push_many", "sdl_batcher_next", "sdl_batcher_flush", "sdl_batch_release",
-    "sdl_process_device", "sdl_device_to_host", "sdl_set_profiling", "sdl_stage_times", "sdl_last_error",
+    "sdl_process_device", "sdl_process_device_labels", "sdl_device_to_host", "sdl_set_profiling", "sdl_stage_times", "sdl_last_error",
     "sdl_abi_version",
 ]
 
@@ -56,6 +56,7 @@ class DeviceRows(ctypes.Structure):
         ("labels", ctypes.c_void_p), ("labels_f32", ctypes.c_void_p), ("d_rows", ctypes.c_void_p),
         ("d_record_rows", ctypes.c_void_p), ("d_tokens", ctypes.c_void_p),
         ("rows_capacity", ctypes.c_uint64), ("label_width", ctypes.c_int32),
+        ("d_label_errors", ctypes.c_void_p),
     ]
 
 
@@ -90,6 +91,7 @@ def load(path=LIB_PATH):
     L.sdl_batch_release.argtypes = [ctypes.POINTER(Batch)]
     L.sdl_batch_release.restype = None
     L.sdl_process_device.argtypes = [vp, vp, u64, vp, u64, u64, vp, ctypes.POINTER(DeviceRows)]
+    L.sdl_process_device_labels.argtypes = [vp, vp, u64, vp, u64, vp, vp, u64, vp, ctypes.POINTER(DeviceRows)]
     L.sdl_device_to_host.argtypes = [vp, vp, vp, sz, vp]
     L.sdl_set_profiling.argtypes = [vp, i64]
     L.sdl_stage_times.argtypes = [vp, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_float), i64]
@@ -97,7 +99,7 @@ def load(path=LIB_PATH):
     L.sdl_last_error.argtypes = []
     L.sdl_abi_version.restype = i64
     for name in ("sdl_batcher_create", "sdl_batcher_push", "sdl_batcher_push_many", "sdl_batcher_next",
-                 "sdl_batcher_flush", "sdl_process_device", "sdl_device_to_host", "sdl_set_profiling",
+                 "sdl_batcher_flush", "sdl_process_device", "sdl_process_device_labels", "sdl_device_to_host", "sdl_set_profiling",
                  "sdl_stage_times"):
         getattr(L, name).restype = i64
     _lib = L

@@ -45,8 +45,33 @@ def lib():
         L.orc_batcher_flush.argtypes = [vp, vp, vp]
         L.orc_batcher_free.argtypes = [vp]
         L.orc_batcher_set_next_record.argtypes = [vp, ctypes.c_uint64]
+        L.orc_encoder_size.restype = ctypes.c_size_t
+        L.orc_encoder_bert.argtypes = [vp, vp]
+        L.orc_encoder_bert.restype = None
+        L.orc_cfg_default.argtypes = [ctypes.POINTER(OrcCfg), ctypes.c_int]
+        L.orc_cfg_default.restype = None
+        L.orc_batcher_create.restype = vp
+        L.orc_batcher_create.argtypes = [vp, ctypes.POINTER(OrcCfg)]
+        L.orc_batcher_push_ex.argtypes = [vp, ctypes.c_char_p, ctypes.c_size_t, vp, ctypes.c_size_t,
+                                          ctypes.POINTER(OrcOut)]
+        L.orc_batcher_flush_ex.argtypes = [vp, ctypes.POINTER(OrcOut)]
         _lib = L
     return _lib
+
+
+class OrcCfg(ctypes.Structure):
+    _fields_ = [("task", ctypes.c_int32), ("B", ctypes.c_int32), ("S", ctypes.c_int32), ("chunk", ctypes.c_int32),
+                ("min_ids", ctypes.c_int32), ("mask_length", ctypes.c_int32), ("mask_id", ctypes.c_int32),
+                ("number_labels", ctypes.c_int32), ("avg_span_gap", ctypes.c_double),
+                ("avg_span_size", ctypes.c_double), ("seed", ctypes.c_uint64)]
+
+
+class OrcOut(ctypes.Structure):
+    _fields_ = [("ids", ctypes.c_void_p), ("am", ctypes.c_void_p), ("tt", ctypes.c_void_p),
+                ("lab", ctypes.c_void_p), ("f32", ctypes.c_void_p), ("rows", ctypes.c_int32)]
+
+
+MLM, CLM, SPAN, MULTI_LABEL = 0, 1, 2, 3
 
 
 class Tok:
@@ -82,11 +107,85 @@ class OracleBatcher:
             return self.buf.copy(), rows.value
         return None
 
+    def push_into(self, b):
+        """push() without copying the batch out (the planes stay in self.buf);
+        returns rows of a finished batch or 0."""
+        rows = ctypes.c_int()
+        if lib().orc_batcher_push(self.h, b, len(b), self.buf.ctypes.data, ctypes.byref(rows)):
+            return rows.value
+        return 0
+
     def flush(self):
         rows = ctypes.c_int()
         if lib().orc_batcher_flush(self.h, self.buf.ctypes.data, ctypes.byref(rows)):
             return self.buf.copy(), rows.value
         return None
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().orc_batcher_free(self.h)
+            self.h = None
+
+
+class Encoder:
+    """An orc_encoder (tokenizer + encode_mask framing) in owned storage."""
+
+    def __init__(self, kind="bert", tok=None):
+        self.buf = ctypes.create_string_buffer(lib().orc_encoder_size())
+        self.tok = tok
+        if kind == "bert":
+            lib().orc_encoder_bert(tok.h, self.buf)
+        else:
+            raise ValueError(kind)
+
+
+class OracleBatcherEx:
+    """Generic oracle Batcher (oracle/orc_batcher.c): GenTokenizer for
+    mlm/clm, SimpleBatcher for multi-label.  push/flush return a dict of the
+    batch planes (copies) or None."""
+
+    def __init__(self, encoder, task, B, S, mask_length=None, mask_id=103, number_labels=9, seed=0,
+                 chunk=None, min_ids=None):
+        c = OrcCfg()
+        lib().orc_cfg_default(ctypes.byref(c), task)
+        c.B, c.S, c.mask_id, c.number_labels, c.seed = B, S, mask_id, number_labels, seed
+        c.mask_length = int(np.float32(S) * np.float32(0.15)) if mask_length is None else mask_length
+        if chunk is not None:
+            c.chunk = 1 if chunk else 0
+        if min_ids is not None:
+            c.min_ids = min_ids
+        self.enc, self.task, self.B, self.S, self.NL = encoder, task, B, S, number_labels
+        self.h = lib().orc_batcher_create(encoder.buf, ctypes.byref(c))
+        if not self.h:
+            raise RuntimeError("oracle batcher config rejected")
+        LW = S if task in (MLM, CLM) else 0
+        self.planes = {"input_ids": np.zeros((B, S), np.int32), "attention_mask": np.zeros((B, S), np.int32),
+                       "token_type_ids": np.zeros((B, S), np.int32), "labels": np.zeros((B, max(LW, 1)), np.int32),
+                       "labels_f32": np.zeros((B, number_labels), np.float32)}
+        p = self.planes
+        self.out = OrcOut(p["input_ids"].ctypes.data, p["attention_mask"].ctypes.data,
+                          p["token_type_ids"].ctypes.data, p["labels"].ctypes.data if LW else None,
+                          p["labels_f32"].ctypes.data if task == MULTI_LABEL else None, 0)
+
+    def set_next_record(self, r):
+        lib().orc_batcher_set_next_record(self.h, r)
+
+    def _result(self):
+        d = {k: v.copy() for k, v in self.planes.items()}
+        d["rows"] = self.out.rows
+        return d
+
+    def push(self, text, labels=None):
+        b = text.encode("utf-8") if isinstance(text, str) else bytes(text)
+        lab = None if labels is None else np.ascontiguousarray(labels, np.uint32)
+        rc = lib().orc_batcher_push_ex(self.h, b, len(b), None if lab is None else lab.ctypes.data,
+                                       0 if lab is None else lab.size, ctypes.byref(self.out))
+        if rc < 0:
+            raise ValueError("label index >= number_labels")
+        return self._result() if rc == 1 else None
+
+    def flush(self):
+        return self._result() if lib().orc_batcher_flush_ex(self.h, ctypes.byref(self.out)) == 1 else None
 
     def __del__(self):
         if getattr(self, "h", None):

@@ -26,7 +26,7 @@ def test_header_and_exports_agree(native_lib):
 
 
 def test_abi_version(native_lib):
-    assert native_lib.sdl_abi_version() == 1
+    assert native_lib.sdl_abi_version() == 2
 
 
 def test_config_defaults_mirror_masking_cases(native_lib):
@@ -41,6 +41,32 @@ def test_config_defaults_mirror_masking_cases(native_lib):
 def test_struct_layouts():
     assert ctypes.sizeof(native.Config) == 96  # 8 x i32, 2 x f64, 2 x u64, i32 + 7 reserved
     assert ctypes.sizeof(native.Batch) == 4 * 4 + 8 * 6
+    assert ctypes.sizeof(native.DeviceRows) == 8 * 8 + 8 + 8 + 8
+
+
+def test_struct_layouts_match_header(tmp_path):
+    """The ctypes mirrors agree with what a C compiler makes of include/sdl_batcher.h."""
+    import shutil
+    import subprocess
+    cc = shutil.which("gcc") or shutil.which("cc")
+    if not cc:
+        pytest.skip("no C compiler")
+    src = tmp_path / "layout.c"
+    src.write_text("""#include <stdio.h>
+#include <stddef.h>
+#include "sdl_batcher.h"
+int main(void) {
+  printf("%zu %zu %zu %zu %zu %zu\\n", sizeof(sdl_config), sizeof(sdl_batch), sizeof(sdl_device_rows),
+         offsetof(sdl_config, seed), offsetof(sdl_batch, labels_f32), offsetof(sdl_device_rows, d_label_errors));
+  return 0;
+}
+""")
+    exe = tmp_path / "layout"
+    inc = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include")
+    subprocess.run([cc, "-I", inc, str(src), "-o", str(exe)], check=True)
+    got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
+    assert got == [ctypes.sizeof(native.Config), ctypes.sizeof(native.Batch), ctypes.sizeof(native.DeviceRows),
+                   native.Config.seed.offset, native.Batch.labels_f32.offset, native.DeviceRows.d_label_errors.offset]
 
 
 def test_create_without_gpu_fails_loudly(native_lib):

@@ -103,3 +103,48 @@ def test_unicode_table_probe_sample():
         else:
             mapped = chr(cp) if e & 4 else pool[(e >> 8) + 2:(e >> 8) + 2 + pool[e >> 8]].decode()
             assert mapped == core, (hex(cp), mapped, core)
+
+
+def _multi_label_stream():
+    from streaming_data_loader_amd import arrow_io
+    items = []
+    for b in arrow_io.read_stream(os.path.join(GOLDEN, "multi_label.arrow")):
+        gen = arrow_io.MultiArrowGenerator(b.schema)
+        items += [gen.get_data(b, i) for i in range(b.num_rows)]
+    return items
+
+
+def test_oracle_multi_label_matches_golden(oracle_tok, records):
+    """SimpleBatcher + BertData(MultiLabel) at S=128 B=8 over the Arrow fixture
+    vs the Python restatement (tests/golden/make_multi_label.py)."""
+    g = np.load(os.path.join(GOLDEN, "multi_label_s128_b8.npz"))
+    items = _multi_label_stream()
+    assert [t.data.text for t in items] == records
+    ob = oracle_lib.OracleBatcherEx(oracle_lib.Encoder("bert", oracle_tok), oracle_lib.MULTI_LABEL, 8, 128)
+    got = [r for r in (ob.push(t.data.text, t.label.multi) for t in items) if r is not None]
+    got.append(ob.flush())
+    assert len(got) == int(g["n_batches"])
+    for i, r in enumerate(got):
+        assert r["rows"] == int(g[f"b{i}_rows"])
+        for k in ("input_ids", "attention_mask", "token_type_ids"):
+            np.testing.assert_array_equal(r[k], g[f"b{i}_{k}"], err_msg=f"batch {i} {k}")
+        np.testing.assert_array_equal(r["labels_f32"], g[f"b{i}_labels"], err_msg=f"batch {i} labels")
+
+
+def test_oracle_multi_label_edge_cases(oracle_tok):
+    ob = oracle_lib.OracleBatcherEx(oracle_lib.Encoder("bert", oracle_tok), oracle_lib.MULTI_LABEL, 2, 8)
+    # no <64 filter: an empty record is a row [CLS][CLS][SEP][SEP][SEP]
+    assert ob.push("", []) is None
+    r = ob.push("a b c d e f g h i j", [8, 0, 8])  # truncated at S; duplicate index is fine
+    assert r is not None and r["rows"] == 2
+    assert r["input_ids"][0].tolist()[:5] == [101, 101, 102, 102, 102]
+    assert r["attention_mask"][0].tolist() == [1, 1, 1, 0, 0, 0, 0, 0]  # reversed-range quirk, n=5 < 8
+    assert r["attention_mask"][1].tolist() == [1] * 8
+    assert r["labels_f32"][1].tolist() == [1, 0, 0, 0, 0, 0, 0, 0, 1]
+    with pytest.raises(ValueError):
+        ob.push("x", [9])  # reference: index out of bounds panic
+    # get_working_batch always yields a (possibly empty) batch
+    e = ob.flush()
+    assert e is not None
+    e2 = ob.flush()
+    assert e2 is not None and e2["rows"] == 0
