@@ -40,6 +40,16 @@ long orc_bert_encode(const orc_tok *t, const uint8_t *s, size_t n, uint32_t *out
 /* Philox4x32-10 MLM key of (seed, record, chunk, position) -- RNG contract. */
 uint32_t orc_mlm_key(uint64_t seed, uint64_t record, uint32_t chunk, uint32_t pos);
 
+/* ---- gpt2 (byte-level BPE) tokenizer: oracle/orc_bpe.c ------------------- */
+typedef struct orc_gpt2 orc_gpt2;
+/* Loads a byte-level BPE tokenizer.json and the probed GPT-2 regex class table
+ * (streaming_data_loader_amd/data/gpt2_classes.bin).  NULL on failure. */
+orc_gpt2 *orc_gpt2_load(const char *tokenizer_json, const char *classes_bin);
+void orc_gpt2_free(orc_gpt2 *t);
+/* Tokenizer::encode(text, true).get_ids(); returns the id count, writes <= cap. */
+long orc_gpt2_encode(const orc_gpt2 *t, const uint8_t *s, size_t n, uint32_t *out, size_t cap);
+int orc_gpt2_eos(const orc_gpt2 *t);
+
 /* ---- Batcher ------------------------------------------------------------ */
 enum { ORC_MLM = 0, ORC_CLM = 1, ORC_SPAN = 2, ORC_MULTI_LABEL = 3 }; /* = SDL_TASK_* */
 
@@ -64,6 +74,8 @@ void orc_cfg_default(orc_cfg *c, int task);
  * to caller storage of orc_encoder_size() bytes. */
 void orc_encoder_bert(const orc_tok *t, orc_encoder *e);
 size_t orc_encoder_size(void);
+/* gpt2 encoder with the [eos] ... [eos] framing. */
+void orc_encoder_gpt2(const orc_gpt2 *t, orc_encoder *e);
 
 orc_batcher *orc_batcher_create(const orc_encoder *e, const orc_cfg *c);
 /* create_sync_batch(record[, Label::Multi indices]): 1 = a batch was emitted

@@ -3,7 +3,10 @@
 // tokenizer.json format is read from disk) and packs it for the device.
 #include "assets.hpp"
 
+#include <algorithm>
+#include <array>
 #include <cstdio>
+#include <queue>
 #include <cstring>
 #include <fstream>
 #include <sstream>
@@ -191,14 +194,293 @@ static void to_device_entries(HostTokenizer &t) {
     for (uint32_t cp = 0; cp < 0x10000; ++cp) t.ubmp[cp] = t.uentry[(size_t)t.upage[cp >> 7] * 128 + (cp & 127)];
 }
 
+// ---------------------------------------------------------------------------
+// Byte-level BPE (gpt2): tokenizers' ByteLevel pre-tokenizer + BPE model.
+// ---------------------------------------------------------------------------
+
+// GPT-2 bytes_to_unicode(): byte -> code point of its printable stand-in
+static std::vector<uint32_t> byte_to_cp() {
+    std::vector<uint32_t> m(256, 0);
+    std::vector<bool> direct(256, false);
+    for (uint32_t b = '!'; b <= '~'; ++b) direct[b] = true;
+    for (uint32_t b = 0xA1; b <= 0xAC; ++b) direct[b] = true;
+    for (uint32_t b = 0xAE; b <= 0xFF; ++b) direct[b] = true;
+    uint32_t n = 0;
+    for (uint32_t b = 0; b < 256; ++b) m[b] = direct[b] ? b : 256 + n++;
+    return m;
+}
+
+static void utf8_append(std::string &o, uint32_t cp) {
+    if (cp < 0x80) o += (char)cp;
+    else if (cp < 0x800) { o += (char)(0xC0 | (cp >> 6)); o += (char)(0x80 | (cp & 63)); }
+    else if (cp < 0x10000) {
+        o += (char)(0xE0 | (cp >> 12)); o += (char)(0x80 | ((cp >> 6) & 63)); o += (char)(0x80 | (cp & 63));
+    } else {
+        o += (char)(0xF0 | (cp >> 18)); o += (char)(0x80 | ((cp >> 12) & 63));
+        o += (char)(0x80 | ((cp >> 6) & 63)); o += (char)(0x80 | (cp & 63));
+    }
+}
+
+// byte-level token string -> raw bytes (false if a char is not a byte stand-in)
+static bool token_bytes(const std::string &tok, const std::unordered_map<uint32_t, uint8_t> &rev, std::string &out) {
+    out.clear();
+    size_t i = 0;
+    while (i < tok.size()) {
+        const uint8_t b = (uint8_t)tok[i];
+        uint32_t cp;
+        int n;
+        if (b < 0x80) { cp = b; n = 1; }
+        else if ((b & 0xE0) == 0xC0) { cp = b & 0x1F; n = 2; }
+        else if ((b & 0xF0) == 0xE0) { cp = b & 0x0F; n = 3; }
+        else { cp = b & 0x07; n = 4; }
+        if (i + n > tok.size()) return false;
+        for (int k = 1; k < n; ++k) cp = (cp << 6) | ((uint8_t)tok[i + k] & 0x3F);
+        auto it = rev.find(cp);
+        if (it == rev.end()) return false;
+        out += (char)it->second;
+        i += n;
+    }
+    return true;
+}
+
+static uint32_t merge_lookup(const HostTokenizer &t, uint32_t a, uint32_t b) {
+    const uint32_t key = a << 16 | b, h = merge_hash(key);
+    const MSlot &s1 = t.mslots[cuckoo_slot1(h, t.mslot_mask)];
+    if (s1.key == key) return s1.val;
+    const MSlot &s2 = t.mslots[cuckoo_slot2(h, t.mslot_mask)];
+    if (s2.key == key) return s2.val;
+    return 0xFFFFFFFFu;
+}
+
+// tokenizers' Word::merge_all: a min-heap of (rank, position) over live pairs,
+// stale entries skipped (models/bpe/word.rs).
+std::vector<int> bpe_encode_bytes(const HostTokenizer &t, const uint8_t *s, size_t n) {
+    struct Sym { int id, prev, next; bool live; };
+    std::vector<Sym> sym(n);
+    for (size_t i = 0; i < n; ++i) sym[i] = {t.byte_id[s[i]], (int)i - 1, i + 1 < n ? (int)i + 1 : -1, true};
+    typedef std::pair<uint64_t, uint32_t> Ent;  // (rank << 32 | pos, merged id)
+    std::priority_queue<Ent, std::vector<Ent>, std::greater<Ent>> q;
+    auto push = [&](int pos) {
+        if (pos < 0 || sym[pos].next < 0) return;
+        const uint32_t v = merge_lookup(t, (uint32_t)sym[pos].id, (uint32_t)sym[sym[pos].next].id);
+        if (v != 0xFFFFFFFFu) q.push({(uint64_t)(v >> 16) << 32 | (uint32_t)pos, v & 0xFFFFu});
+    };
+    for (size_t i = 0; i + 1 < n; ++i) push((int)i);
+    while (!q.empty()) {
+        const Ent e = q.top();
+        q.pop();
+        const int pos = (int)(uint32_t)e.first;
+        if (!sym[pos].live || sym[pos].next < 0) continue;
+        const int nx = sym[pos].next;
+        const uint32_t v = merge_lookup(t, (uint32_t)sym[pos].id, (uint32_t)sym[nx].id);
+        if (v == 0xFFFFFFFFu || (v & 0xFFFFu) != e.second) continue;  // expired entry
+        sym[pos].id = (int)e.second;
+        sym[nx].live = false;
+        sym[pos].next = sym[nx].next;
+        if (sym[pos].next >= 0) sym[sym[pos].next].prev = pos;
+        push(sym[pos].prev);
+        push(pos);
+    }
+    std::vector<int> out;
+    for (size_t i = 0; i < n; ++i)
+        if (sym[i].live) out.push_back(sym[i].id);
+    return out;
+}
+
+static void load_gpt2_classes(const std::string &path, HostTokenizer &t) {
+    const std::string b = read_file(path);
+    if (b.size() < 16 || b.compare(0, 4, "SDLG") != 0) throw std::runtime_error("bad class table " + path);
+    uint32_t ver, np, nb;
+    std::memcpy(&ver, &b[4], 4);
+    std::memcpy(&np, &b[8], 4);
+    std::memcpy(&nb, &b[12], 4);
+    if (ver != 1 || np != 0x110000 / 256 || b.size() != 16 + 2 * (size_t)np + 64 * (size_t)nb)
+        throw std::runtime_error("bad class table " + path);
+    t.gpage.resize(np);
+    std::memcpy(t.gpage.data(), &b[16], 2 * (size_t)np);
+    t.gblock.assign(b.begin() + 16 + 2 * np, b.end());
+    // the kernels classify ASCII arithmetically: check it is the table's
+    for (uint32_t c = 0; c < 128; ++c) {
+        const uint32_t k = (t.gblock[(size_t)t.gpage[0] * 64 + (c >> 2)] >> (2 * (c & 3))) & 3u;
+        uint32_t want = GC_O;
+        if ((c | 0x20u) - 'a' < 26u) want = GC_L;
+        else if (c - '0' < 10u) want = GC_N;
+        else if (c == ' ' || (c >= 9 && c <= 13)) want = GC_W;
+        if (k != want) throw std::runtime_error("gpt2 class table: ASCII classes differ from the kernels' classifier");
+    }
+}
+
+static void load_byte_bpe(const JValue &root, const std::string &data_dir, HostTokenizer &t) {
+    const JValue *model = root.get("model");
+    auto is_null_or = [](const JValue *v, const char *s) { return !v || v->kind == JValue::NUL || v->is_str(s); };
+    auto is_true = [](const JValue *v) { return v && v->kind == JValue::BOOL && v->b; };
+    if (model->get("dropout") && model->get("dropout")->kind == JValue::NUM)
+        throw std::runtime_error("BPE dropout unsupported (non-deterministic)");
+    if (!is_null_or(model->get("continuing_subword_prefix"), "") || !is_null_or(model->get("end_of_word_suffix"), ""))
+        throw std::runtime_error("byte-level BPE with subword prefix/suffix unsupported");
+    if (is_true(model->get("byte_fallback")) || is_true(model->get("ignore_merges")))
+        throw std::runtime_error("BPE byte_fallback/ignore_merges unsupported");
+    const JValue *norm = root.get("normalizer");
+    if (norm && norm->kind != JValue::NUL) throw std::runtime_error("byte-level BPE: normalizer must be null (gpt2)");
+    const JValue *pre = root.get("pre_tokenizer");
+    if (!pre || !pre->get("type") || !pre->get("type")->is_str("ByteLevel") || is_true(pre->get("add_prefix_space")) ||
+        (pre->get("use_regex") && !is_true(pre->get("use_regex"))))
+        throw std::runtime_error("pre_tokenizer must be ByteLevel(add_prefix_space=false, use_regex=true)");
+    const JValue *pp = root.get("post_processor");
+    if (pp && pp->kind != JValue::NUL && !(pp->get("type") && pp->get("type")->is_str("ByteLevel")))
+        throw std::runtime_error("post_processor must be ByteLevel or null (no ids added)");
+    t.kind = TOK_BYTE_BPE;
+    const JValue *vocab = model->get("vocab");
+    if (!vocab || vocab->kind != JValue::OBJ) throw std::runtime_error("model.vocab missing");
+    int max_id = -1;
+    for (auto &kv : vocab->obj) max_id = std::max(max_id, (int)kv.second.num);
+    t.pieces.assign((size_t)max_id + 1, std::string());
+    std::unordered_map<std::string, int> id_of;
+    for (auto &kv : vocab->obj) {
+        t.pieces[(size_t)kv.second.num] = kv.first;
+        id_of[kv.first] = (int)kv.second.num;
+    }
+    const JValue *added = root.get("added_tokens");
+    if (added && added->kind == JValue::ARR) {
+        for (auto &a : added->arr) {
+            const JValue *c = a.get("content"), *id = a.get("id");
+            if (!c || !id) continue;
+            // no normalizer: a normalized added token matches the raw text too
+            if (is_true(a.get("lstrip")) || is_true(a.get("rstrip")) || is_true(a.get("single_word")))
+                throw std::runtime_error("added token options (lstrip/rstrip/single_word) unsupported");
+            t.added.emplace_back(c->str, (int)id->num);
+            if ((size_t)id->num >= t.pieces.size()) t.pieces.resize((size_t)id->num + 1);
+            if (t.pieces[(size_t)id->num].empty()) t.pieces[(size_t)id->num] = c->str;
+            id_of.emplace(c->str, (int)id->num);
+        }
+    }
+    if (t.pieces.size() > 65535) throw std::runtime_error("vocabulary larger than 65535 ids is not supported");
+    auto eos = id_of.find("<|endoftext|>");
+    if (eos == id_of.end()) throw std::runtime_error("gpt2 tokenizer lacks <|endoftext|>");
+    t.eos_id = eos->second;
+    // byte symbols
+    const std::vector<uint32_t> b2c = byte_to_cp();
+    std::unordered_map<uint32_t, uint8_t> rev;
+    t.byte_id.assign(256, 0);
+    for (uint32_t b = 0; b < 256; ++b) {
+        rev[b2c[b]] = (uint8_t)b;
+        std::string u;
+        utf8_append(u, b2c[b]);
+        auto it = id_of.find(u);
+        if (it == id_of.end()) throw std::runtime_error("byte-level vocab lacks a byte symbol");
+        t.byte_id[b] = (uint16_t)it->second;
+    }
+    // merges: rank = position; (left, right) -> merged
+    const JValue *merges = model->get("merges");
+    if (!merges || merges->kind != JValue::ARR) throw std::runtime_error("model.merges missing");
+    const size_t nm = merges->arr.size();
+    if (nm >= MERGE_NONE) throw std::runtime_error("too many merges (rank must fit 16 bits)");
+    std::vector<std::array<uint32_t, 3>> ms;
+    ms.reserve(nm);
+    std::vector<int64_t> max_creator(t.pieces.size(), -1);
+    for (size_t r = 0; r < nm; ++r) {
+        const JValue &m = merges->arr[r];
+        std::string a, b;
+        if (m.kind == JValue::STR) {
+            const size_t sp = m.str.find(' ', 1);
+            if (sp == std::string::npos) throw std::runtime_error("bad merge entry");
+            a = m.str.substr(0, sp);
+            b = m.str.substr(sp + 1);
+        } else if (m.kind == JValue::ARR && m.arr.size() == 2) {
+            a = m.arr[0].str;
+            b = m.arr[1].str;
+        } else {
+            throw std::runtime_error("bad merge entry");
+        }
+        auto ia = id_of.find(a), ib = id_of.find(b), ic = id_of.find(a + b);
+        if (ia == id_of.end() || ib == id_of.end() || ic == id_of.end())
+            throw std::runtime_error("merge references a token missing from the vocab");
+        ms.push_back({(uint32_t)ia->second, (uint32_t)ib->second, (uint32_t)ic->second});
+        max_creator[(size_t)ic->second] = std::max<int64_t>(max_creator[(size_t)ic->second], (int64_t)r);
+    }
+    // The device merges every occurrence of the lowest-rank pair per step; that
+    // equals tokenizers' heap order when a merge's parts are only created by
+    // lower-ranked merges (true of any trained BPE).
+    for (size_t r = 0; r < nm; ++r)
+        if (max_creator[ms[r][0]] >= (int64_t)r || max_creator[ms[r][1]] >= (int64_t)r)
+            throw std::runtime_error("merges are not rank-monotone (a part is created by a later merge)");
+    uint32_t slots = 1;
+    while (slots < 4 * std::max<size_t>(nm, 1)) slots <<= 1;
+    for (;; slots <<= 1) {
+        t.mslot_mask = slots - 1;
+        t.mslots.assign(slots, MSlot{0xFFFFFFFFu, 0});
+        bool ok = true;
+        for (size_t r = 0; r < nm && ok; ++r) {
+            MSlot v{ms[r][0] << 16 | ms[r][1], (uint32_t)r << 16 | ms[r][2]};
+            if (merge_lookup(t, ms[r][0], ms[r][1]) != 0xFFFFFFFFu) continue;  // duplicate pair keeps the first rank
+            uint32_t pos = cuckoo_slot1(merge_hash(v.key), t.mslot_mask);
+            bool placed = false;
+            for (int kick = 0; kick < 2000; ++kick) {
+                if (t.mslots[pos].key == 0xFFFFFFFFu) { t.mslots[pos] = v; placed = true; break; }
+                std::swap(v, t.mslots[pos]);
+                const uint32_t h = merge_hash(v.key);
+                const uint32_t a = cuckoo_slot1(h, t.mslot_mask), b = cuckoo_slot2(h, t.mslot_mask);
+                pos = pos == a ? b : a;
+            }
+            ok = placed;
+        }
+        if (ok) break;
+        if (slots >= (1u << 24)) throw std::runtime_error("merge table build failed");
+    }
+    // word table: vocab strings whose own BPE is exactly themselves
+    std::vector<bool> is_added(t.pieces.size(), false);
+    for (auto &a : t.added) is_added[(size_t)a.second] = true;
+    std::vector<VSlot> entries;
+    t.vpool.clear();
+    t.maxlen_first = t.maxlen_cont = 0;
+    std::string bytes;
+    for (auto &kv : vocab->obj) {
+        const int id = (int)kv.second.num;
+        if (is_added[(size_t)id] || id_of[kv.first] != id || !token_bytes(kv.first, rev, bytes)) continue;
+        if (bytes.empty() || bytes.size() > 255) continue;
+        const std::vector<int> enc = bpe_encode_bytes(t, (const uint8_t *)bytes.data(), bytes.size());
+        if (enc.size() != 1 || enc[0] != id) continue;
+        t.maxlen_first = std::max(t.maxlen_first, (int)bytes.size());
+        VSlot v{};
+        v.key = (uint32_t)bytes.size();
+        v.id = (int32_t)id;
+        v.pool_off = (uint32_t)t.vpool.size();
+        v.hash = piece_hash((const uint8_t *)bytes.data(), bytes.size(), 0u);
+        std::memcpy(v.inl, bytes.data(), std::min<size_t>(16, bytes.size()));
+        t.vpool.insert(t.vpool.end(), bytes.begin(), bytes.end());
+        entries.push_back(v);
+    }
+    t.word_table_entries = entries.size();
+    t.vpool.resize(t.vpool.size() + 64, 0);
+    slots = 1;
+    while (slots < 4 * entries.size()) slots <<= 1;
+    for (;; slots <<= 1) {
+        t.slot_mask = slots - 1;
+        t.slots.assign(slots, VSlot{0, -1, 0, 0, {0}});
+        bool ok = true;
+        for (const VSlot &v : entries)
+            if (!cuckoo_insert(t.slots, t.slot_mask, v)) { ok = false; break; }
+        if (ok) break;
+        if (slots >= (1u << 24)) throw std::runtime_error("cuckoo table build failed");
+    }
+    set_added(t);
+    if (t.opener && (t.opener >= 0x80 || (t.opener | 0x20u) - 'a' < 26u || t.opener - '0' < 10u))
+        throw std::runtime_error("added tokens must start with an ASCII non-alphanumeric byte");
+    load_gpt2_classes(data_dir + "/gpt2_classes.bin", t);
+}
+
 void load_tokenizer(const std::string &path, const std::string &data_dir, HostTokenizer &t) {
     const std::string body = read_file(path);
     const bool is_json = path.size() >= 5 && path.compare(path.size() - 5, 5, ".json") == 0;
     if (is_json) {
         JValue root = JParser(body).parse();
         const JValue *model = root.get("model");
+        if (model && model->get("type") && model->get("type")->is_str("BPE")) {
+            load_byte_bpe(root, data_dir, t);
+            return;
+        }
         if (!model || !model->get("type") || !model->get("type")->is_str("WordPiece"))
-            throw std::runtime_error("only WordPiece tokenizer.json models are supported by this build");
+            throw std::runtime_error("only WordPiece and byte-level BPE tokenizer.json models are supported");
         const JValue *pfx = model->get("continuing_subword_prefix");
         if (pfx && !pfx->is_str("##")) throw std::runtime_error("continuing_subword_prefix must be ##");
         const JValue *mx = model->get("max_input_chars_per_word");

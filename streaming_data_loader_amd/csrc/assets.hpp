@@ -11,6 +11,7 @@
 namespace sdl {
 
 struct HostTokenizer {
+    int kind = TOK_WORDPIECE;  // TOK_*
     // ---- what get_tokenizer(cfg) yields (tokenizer_wrapper.rs:162-189) -----
     std::vector<std::string> pieces;                   // id -> piece
     std::vector<std::pair<std::string, int>> added;    // added tokens matched on raw text
@@ -32,7 +33,20 @@ struct HostTokenizer {
     int maxlen_first = 0, maxlen_cont = 0;
     uint32_t opener = 0;
     int max_special_len = 0;
+
+    // ---- byte-level BPE (gpt2) ---------------------------------------------
+    int eos_id = -1;                       // <|endoftext|> (TokenizerInfo.eos)
+    std::vector<uint16_t> byte_id;         // byte -> id of its byte-level symbol
+    std::vector<MSlot> mslots;             // (left, right) -> (rank, merged)
+    uint32_t mslot_mask = 0;
+    std::vector<uint16_t> gpage;           // data/gpt2_classes.bin
+    std::vector<uint8_t> gblock;
+    size_t word_table_entries = 0;
 };
+
+// HF BPE::merge_word over raw bytes (byte-level symbols), host side: used to
+// precompute the word table; same semantics as the device merge loop.
+std::vector<int> bpe_encode_bytes(const HostTokenizer &t, const uint8_t *s, size_t n);
 
 // Loads a HF tokenizer.json (WordPiece model with BertNormalizer +
 // BertPreTokenizer, as bert-base-uncased) or a WordPiece vocab.txt, plus the

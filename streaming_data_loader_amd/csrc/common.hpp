@@ -73,8 +73,23 @@ __host__ __device__ inline uint32_t cuckoo_slot2(uint32_t h, uint32_t mask) {
 }
 static_assert(sizeof(VSlot) == 32, "VSlot must be 32 bytes");
 
+// Byte-level BPE merge table (cuckoo, 2 slots of 8 B): key = left id << 16 |
+// right id, val = rank << 16 | merged id; empty slot key = 0xFFFFFFFF.
+struct MSlot {
+    uint32_t key;
+    uint32_t val;
+};
+__host__ __device__ inline uint32_t merge_hash(uint32_t key) { return ph_final(key * 0x9E3779B1u + 0x632BE5ABu); }
+constexpr uint32_t MERGE_NONE = 0xFFFFu;  // rank of a pair with no merge
+
+// GPT-2 regex classes of a code point (tools/make_gpt2_tables.py)
+enum : uint32_t { GC_O = 0, GC_L = 1, GC_N = 2, GC_W = 3 };
+
+enum : int32_t { TOK_WORDPIECE = 0, TOK_BYTE_BPE = 1 };
+
 // Everything a tokenize kernel needs, passed by value as a kernel argument.
 struct DevTok {
+    int32_t kind;            // TOK_*
     const uint32_t *ubmp;    // device Unicode entries of U+0000..U+FFFF (flat)
     const uint16_t *upage;   // Unicode page table  [0x110000/128]
     const uint32_t *uentry;  // Unicode blocks      [n_blocks*128]
@@ -92,6 +107,13 @@ struct DevTok {
     int32_t special_id[MAX_SPECIAL];
     uint8_t special_len[MAX_SPECIAL];
     uint8_t special_bytes[MAX_SPECIAL][MAX_SPECIAL_LEN];
+    // byte-level BPE (kind == TOK_BYTE_BPE); slots/vpool then hold the word
+    // table: every vocab string whose own BPE is itself, keyed by its raw bytes
+    const uint16_t *gpage;   // code point page (256) -> class block
+    const uint8_t *gblock;   // 64-byte blocks of 2-bit GC_* classes
+    const MSlot *mslots;     // merge table
+    const uint16_t *byte_id; // id of each single byte symbol
+    uint32_t mslot_mask;
 };
 
 // Row assembly parameters (GenTokenizer + BertData/GptData/T5Data framing).

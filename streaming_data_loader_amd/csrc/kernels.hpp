@@ -9,8 +9,11 @@
 
 namespace sdl {
 
+// pipeline.hip: per chunk, the record ranges touching its window (3 words per chunk)
+hipError_t launch_chunk_ranges(const uint64_t *off, int64_t R, int64_t N, uint32_t *ranges, hipStream_t st);
+
 // tokenize_wordpiece.hip: text arena -> per-chunk token lists + boundary offsets
-// `ranges` needs 3 words per 4096-byte chunk.
+// (after launch_chunk_ranges).
 hipError_t launch_wordpiece_chunks(const DevTok &T, const uint8_t *text, int64_t N, const uint64_t *off, int64_t R,
                                    uint32_t *ranges, uint32_t *tokc, uint32_t *chunk_cnt, uint32_t *rec_local,
                                    hipStream_t st);

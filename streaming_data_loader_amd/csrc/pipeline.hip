@@ -92,6 +92,35 @@ hipError_t launch_exclusive_scan(const uint32_t *in, uint32_t *out, int64_t n, u
 }
 
 // ---------------------------------------------------------------------------
+// Per chunk: record ranges touching its window (so the tokenize kernel never
+// binary-searches the offsets serially).
+__global__ __launch_bounds__(256) void k_chunk_ranges(const uint64_t *__restrict__ off, int64_t R, int64_t n_chunks,
+                                                      uint32_t *__restrict__ ranges) {
+    const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (c >= n_chunks) return;
+    auto lower = [&](int64_t x) {  // first r in [0, R] with off[r] >= x (R+1 if none)
+        int64_t lo = 0, hi = R + 1;
+        while (lo < hi) {
+            const int64_t m = (lo + hi) >> 1;
+            if ((int64_t)off[m] < x) lo = m + 1; else hi = m;
+        }
+        return lo;
+    };
+    const int64_t c0 = c * CHUNK;
+    ranges[3 * c + 0] = (uint32_t)lower(c0 - HALO_L);
+    ranges[3 * c + 1] = (uint32_t)lower(c0 - HALO_L + WIN);
+    ranges[3 * c + 2] = (uint32_t)lower(c0);
+}
+
+hipError_t launch_chunk_ranges(const uint64_t *off, int64_t R, int64_t N, uint32_t *ranges, hipStream_t st) {
+    const int64_t n_chunks = (N + CHUNK - 1) / CHUNK;
+    if (n_chunks == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_chunk_ranges, dim3((unsigned)((n_chunks + 255) / 256)), dim3(256), 0, st, off, R, n_chunks,
+                       ranges);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
 // Per-chunk token lists -> one dense token array in arena order.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_compact_tokens(const uint32_t *__restrict__ tokc,

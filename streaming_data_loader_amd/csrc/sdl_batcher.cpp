@@ -199,6 +199,7 @@ struct sdl_batcher {
             if (profiling) HIP_TRY(hipEventRecord(ev[i], st));
         };
         mark(0);
+        HIP_TRY(launch_chunk_ranges(d_off, R, N, ranges.p, st));
         HIP_TRY(launch_wordpiece_chunks(dt, d_text, N, d_off, R, ranges.p, tokc.p, chunk_cnt.p, rec_local.p, st));
         mark(1);
         HIP_TRY(launch_exclusive_scan(chunk_cnt.p, chunk_off.p, n_chunks, scan_tmp.p, st));

@@ -37,3 +37,15 @@ def native_lib():
     from streaming_data_loader_amd import build, native
     build.build()
     return native.load()
+
+
+@pytest.fixture(scope="session")
+def gpt2_goldens():
+    with open(os.path.join(GOLDEN, "gpt2_ids.json"), encoding="utf-8") as f:
+        return json.load(f)
+
+
+@pytest.fixture(scope="session")
+def oracle_gpt2():
+    import oracle_lib
+    return oracle_lib.Gpt2Tok()

@@ -14,13 +14,15 @@ ORACLE_DIR = os.path.join(REPO, "oracle")
 ORACLE_SO = os.path.join(ORACLE_DIR, "build", "liboracle.so")
 VOCAB_TXT = os.path.join(REPO, "streaming_data_loader_amd", "assets", "bert_proxy", "vocab.txt")
 UNICODE_BIN = os.path.join(REPO, "streaming_data_loader_amd", "data", "bert_uncased_unicode.bin")
+GPT2_JSON = os.path.join(REPO, "streaming_data_loader_amd", "assets", "gpt2_proxy", "tokenizer.json")
+GPT2_CLASSES = os.path.join(REPO, "streaming_data_loader_amd", "data", "gpt2_classes.bin")
 
 _lib = None
 
 
 def build():
-    src = os.path.join(ORACLE_DIR, "sdl_oracle.c")
-    if not os.path.exists(ORACLE_SO) or os.path.getmtime(ORACLE_SO) < os.path.getmtime(src):
+    srcs = [os.path.join(ORACLE_DIR, f) for f in os.listdir(ORACLE_DIR) if f.endswith((".c", ".h"))]
+    if not os.path.exists(ORACLE_SO) or os.path.getmtime(ORACLE_SO) < max(os.path.getmtime(f) for f in srcs):
         subprocess.run(["make", "-s", "-C", ORACLE_DIR], check=True)
     return ORACLE_SO
 
@@ -55,6 +57,14 @@ def lib():
         L.orc_batcher_push_ex.argtypes = [vp, ctypes.c_char_p, ctypes.c_size_t, vp, ctypes.c_size_t,
                                           ctypes.POINTER(OrcOut)]
         L.orc_batcher_flush_ex.argtypes = [vp, ctypes.POINTER(OrcOut)]
+        L.orc_gpt2_load.restype = vp
+        L.orc_gpt2_load.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+        L.orc_gpt2_free.argtypes = [vp]
+        L.orc_gpt2_encode.restype = ctypes.c_long
+        L.orc_gpt2_encode.argtypes = [vp, ctypes.c_char_p, ctypes.c_size_t, vp, ctypes.c_size_t]
+        L.orc_gpt2_eos.argtypes = [vp]
+        L.orc_encoder_gpt2.argtypes = [vp, vp]
+        L.orc_encoder_gpt2.restype = None
         _lib = L
     return _lib
 
@@ -127,6 +137,22 @@ class OracleBatcher:
             self.h = None
 
 
+class Gpt2Tok:
+    """The gpt2 byte-level BPE restatement (oracle/orc_bpe.c)."""
+
+    def __init__(self, path=GPT2_JSON, classes=GPT2_CLASSES):
+        self.h = lib().orc_gpt2_load(path.encode(), classes.encode())
+        if not self.h:
+            raise RuntimeError("oracle gpt2 tokenizer load failed")
+        self.eos = lib().orc_gpt2_eos(self.h)
+
+    def encode(self, text):
+        b = text.encode("utf-8") if isinstance(text, str) else bytes(text)
+        out = np.zeros(len(b) + 8, np.uint32)
+        n = lib().orc_gpt2_encode(self.h, b, len(b), out.ctypes.data, out.size)
+        return out[:n].tolist()
+
+
 class Encoder:
     """An orc_encoder (tokenizer + encode_mask framing) in owned storage."""
 
@@ -135,6 +161,8 @@ class Encoder:
         self.tok = tok
         if kind == "bert":
             lib().orc_encoder_bert(tok.h, self.buf)
+        elif kind == "gpt2":
+            lib().orc_encoder_gpt2(tok.h, self.buf)
         else:
             raise ValueError(kind)
 

@@ -148,3 +148,22 @@ def test_oracle_multi_label_edge_cases(oracle_tok):
     assert e is not None
     e2 = ob.flush()
     assert e2 is not None and e2["rows"] == 0
+
+
+# ---- gpt2 (byte-level BPE) ------------------------------------------------------
+def test_gpt2_oracle_matches_tokenizers_goldens(oracle_gpt2, gpt2_goldens):
+    assert gpt2_goldens["n_fixture_records"] == 50 and len(gpt2_goldens["cases"]) > 400
+    bad = [c["text"][:60] for c in gpt2_goldens["cases"] if oracle_gpt2.encode(c["text"]) != c["ids"]]
+    assert not bad, f"{len(bad)} mismatches, e.g. {bad[:3]}"
+
+
+def test_gpt2_oracle_clm_batches_match_golden(oracle_gpt2, records):
+    g = np.load(os.path.join(GOLDEN, "clm_s128_b8.npz"))
+    ob = oracle_lib.OracleBatcherEx(oracle_lib.Encoder("gpt2", oracle_gpt2), oracle_lib.CLM, 8, 128)
+    got = [r for r in (ob.push(t) for t in records) if r is not None]
+    got.append(ob.flush())
+    assert len(got) == int(g["n_batches"])
+    for i, r in enumerate(got):
+        assert r["rows"] == int(g[f"b{i}_rows"])
+        for k in ("input_ids", "attention_mask", "labels"):
+            np.testing.assert_array_equal(r[k], g[f"b{i}_{k}"], err_msg=f"batch {i} {k}")
