@@ -18,8 +18,8 @@
  * (tokenizer_wrapper.rs:118-124).
  *
  * Input bytes that are not valid UTF-8 cannot reach the reference (a Rust
- * String); here a byte 10xxxxxx never starts a char unless it begins a
- * segment, and a malformed or truncated sequence is one char of class O.
+ * String); here every char is either a complete lead + continuation sequence
+ * (overlong forms decoded as is) or a single byte of class O.
  */
 #include <stdio.h>
 #include <string.h>
@@ -300,18 +300,20 @@ typedef struct { size_t start, len; int cls; } gch;
 
 static int cls_of(const orc_gpt2 *t, const uint8_t *s, size_t n, size_t i, size_t *len) {
     const uint8_t b = s[i];
-    if (b < 0x80) { *len = 1; return t->cls[b]; }
-    size_t k = 1;
-    while (i + k < n && (s[i + k] & 0xC0) == 0x80) ++k; /* the char spans its continuation bytes */
-    *len = k;
+    *len = 1;
+    if (b < 0x80) return t->cls[b];
     int need;
     uint32_t cp;
     if ((b & 0xE0) == 0xC0) { need = 2; cp = b & 0x1F; }
     else if ((b & 0xF0) == 0xE0) { need = 3; cp = b & 0x0F; }
     else if ((b & 0xF8) == 0xF0) { need = 4; cp = b & 0x07; }
-    else return GO; /* stray continuation byte or invalid lead */
-    if ((int)k < need) return GO;
-    for (int j = 1; j < need; ++j) cp = (cp << 6) | (s[i + j] & 0x3F);
+    else return GO; /* continuation byte or invalid lead: one O byte */
+    if (i + (size_t)need > n) return GO;
+    for (int j = 1; j < need; ++j) {
+        if ((s[i + j] & 0xC0) != 0x80) return GO;
+        cp = (cp << 6) | (s[i + j] & 0x3F);
+    }
+    *len = (size_t)need;
     return cp < 0x110000 ? t->cls[cp] : GO;
 }
 

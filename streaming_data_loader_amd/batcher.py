@@ -99,8 +99,8 @@ def get_case(task: TaskType, test: bool, sequence_length: int = 128, batch_size:
     if task == TaskType.Mlm:
         return TrainingConfig(ModelType.Bert, TokenizerConfig(), batch, Mask(get_mask_length(sequence_length), 103),
                               seed)
-    if task == TaskType.Clm:
-        return TrainingConfig(ModelType.Gpt2, TokenizerConfig(), batch, Gpt(), seed)
+    if task == TaskType.Clm:  # masking_cases.rs:66: gpt2
+        return TrainingConfig(ModelType.Gpt2, TokenizerConfig(native.GPT2_PROXY_TOKENIZER), batch, Gpt(), seed)
     if task == TaskType.Span:
         return TrainingConfig(ModelType.T5, TokenizerConfig(), batch, Span(16.0, 2.0), seed)
     return TrainingConfig(ModelType.Bert, TokenizerConfig(), BatchConfig(2048 if batch_size is None else b,

@@ -466,6 +466,9 @@ static void load_byte_bpe(const JValue &root, const std::string &data_dir, HostT
     set_added(t);
     if (t.opener && (t.opener >= 0x80 || (t.opener | 0x20u) - 'a' < 26u || t.opener - '0' < 10u))
         throw std::runtime_error("added tokens must start with an ASCII non-alphanumeric byte");
+    for (auto &a : t.added)
+        for (unsigned char ch : a.first)
+            if (ch >= 0x80) throw std::runtime_error("byte-level BPE: added tokens must be ASCII");
     load_gpt2_classes(data_dir + "/gpt2_classes.bin", t);
 }
 

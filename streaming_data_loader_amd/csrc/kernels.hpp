@@ -18,6 +18,22 @@ hipError_t launch_wordpiece_chunks(const DevTok &T, const uint8_t *text, int64_t
                                    uint32_t *ranges, uint32_t *tokc, uint32_t *chunk_cnt, uint32_t *rec_local,
                                    hipStream_t st);
 
+// tokenize_bpe.hip: same outputs for a byte-level BPE (gpt2) tokenizer.  Pieces
+// longer than 64 bytes go through `long_list` (capacity long_cap) and are
+// merged by a second kernel in `scratch` (u16 per text byte); their chunk
+// entry is LONG_MARK | list index (k_compact_tokens expands it).
+struct BpeLong {
+    uint64_t pos;   // first byte
+    uint32_t len;   // bytes (0 until known)
+    uint32_t chunk; // owning chunk
+    uint32_t k;     // ids after merging
+    uint32_t pad;
+};
+hipError_t launch_bpe_chunks(const DevTok &T, const uint8_t *text, int64_t N, const uint64_t *off, int64_t R,
+                             const uint32_t *ranges, uint32_t *tokc, uint32_t *chunk_cnt, uint32_t *chunk_ent,
+                             uint32_t *rec_local, uint32_t *long_count, BpeLong *long_list, uint32_t long_cap,
+                             uint16_t *scratch, uint32_t *err, hipStream_t st);
+
 #ifdef SDL_STAMPS
 void print_phase_cycles();  // diagnostic builds only
 #endif
@@ -28,8 +44,12 @@ void print_phase_cycles();  // diagnostic builds only
 int64_t scan_tmp_words(int64_t n);
 hipError_t launch_exclusive_scan(const uint32_t *in, uint32_t *out, int64_t n, uint32_t *tmp, hipStream_t st);
 
+// long_count == null: no long-piece markers (WordPiece).  Else chunk_ent holds
+// each chunk's entry count (markers count 1; chunk_cnt counts ids).
 hipError_t launch_compact_tokens(const uint32_t *tokc, const uint32_t *chunk_cnt, const uint32_t *chunk_off,
-                                 int64_t n_chunks, uint32_t *tok, hipStream_t st);
+                                 int64_t n_chunks, uint32_t *tok, const uint32_t *long_count,
+                                 const uint32_t *chunk_ent, const BpeLong *long_list, const uint16_t *long_scratch,
+                                 hipStream_t st);
 
 // per record: token offset, token count, rows it yields (gen_batcher.rs:69-94)
 hipError_t launch_records(const RowParams &P, const uint64_t *off, int64_t R, int64_t N, const uint32_t *chunk_off,

@@ -126,20 +126,50 @@ hipError_t launch_chunk_ranges(const uint64_t *off, int64_t R, int64_t N, uint32
 __global__ __launch_bounds__(256) void k_compact_tokens(const uint32_t *__restrict__ tokc,
                                                         const uint32_t *__restrict__ chunk_cnt,
                                                         const uint32_t *__restrict__ chunk_off, int64_t n_chunks,
-                                                        uint32_t *__restrict__ tok) {
+                                                        uint32_t *__restrict__ tok, const uint32_t *long_count,
+                                                        const uint32_t *__restrict__ chunk_ent,
+                                                        const BpeLong *__restrict__ long_list,
+                                                        const uint16_t *__restrict__ long_scratch) {
     const int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);  // one wave per chunk
     if (c >= n_chunks) return;
     const uint32_t n = chunk_cnt[c];
     const uint32_t *src = tokc + c * STAGE;
     uint32_t *dst = tok + chunk_off[c];
-    for (uint32_t i = threadIdx.x & 63; i < n; i += 64) dst[i] = src[i];
+    const int lane = threadIdx.x & 63;
+    if (!long_count || *long_count == 0) {
+        for (uint32_t i = lane; i < n; i += 64) dst[i] = src[i];
+        return;
+    }
+    // byte-level BPE with long pieces: an entry LONG_MARK | i stands for the
+    // k ids of long piece i (in long_scratch at its byte position)
+    const uint32_t ne = chunk_ent[c];  // entries written by the chunk kernel
+    uint32_t written = 0;
+    for (uint32_t e0 = 0; e0 < ne; e0 += 64) {
+        const uint32_t e = e0 + lane;
+        const uint32_t x = e < ne ? src[e] : 0u;
+        const bool mark = (x & 0x80000000u) != 0u;
+        const uint32_t w = e >= ne ? 0u : mark ? long_list[x & 0x7FFFFFFFu].k : 1u;
+        const uint32_t incl = wave_incl_sum(w);
+        const uint32_t at = written + incl - w;
+        if (e < ne && at < n) {
+            if (!mark) {
+                dst[at] = x;
+            } else {
+                const BpeLong L = long_list[x & 0x7FFFFFFFu];
+                for (uint32_t j = 0; j < L.k; ++j) dst[at + j] = long_scratch[L.pos + j];
+            }
+        }
+        written += (uint32_t)__shfl((int)incl, 63, 64);
+    }
 }
 
 hipError_t launch_compact_tokens(const uint32_t *tokc, const uint32_t *chunk_cnt, const uint32_t *chunk_off,
-                                 int64_t n_chunks, uint32_t *tok, hipStream_t st) {
+                                 int64_t n_chunks, uint32_t *tok, const uint32_t *long_count,
+                                 const uint32_t *chunk_ent, const BpeLong *long_list, const uint16_t *long_scratch,
+                                 hipStream_t st) {
     if (n_chunks == 0) return hipSuccess;
     hipLaunchKernelGGL(k_compact_tokens, dim3((unsigned)((n_chunks + 3) / 4)), dim3(256), 0, st, tokc, chunk_cnt,
-                       chunk_off, n_chunks, tok);
+                       chunk_off, n_chunks, tok, long_count, chunk_ent, long_list, long_scratch);
     return hipGetLastError();
 }
 

@@ -115,6 +115,9 @@ struct sdl_batcher {
     DevBuf<uint8_t> d_upool, d_vpool;
     DevBuf<VSlot> d_slots;
     DevBuf<int32_t> d_ascii_id;
+    DevBuf<uint16_t> d_gpage, d_byte_id;
+    DevBuf<uint8_t> d_gblock;
+    DevBuf<MSlot> d_mslots;
 
     // per-call workspace
     DevBuf<uint32_t> ranges, tokc, chunk_cnt, chunk_off, rec_local, tok_ids, rec_tok, rec_cnt, rec_rows, row_off,
@@ -122,6 +125,10 @@ struct sdl_batcher {
     DevBuf<int32_t> o_ids, o_am, o_tt, o_lab;
     DevBuf<float> o_f32;
     DevBuf<uint32_t> lab_err;
+    // byte-level BPE long pieces
+    DevBuf<uint32_t> long_count, bpe_err, chunk_ent;
+    DevBuf<BpeLong> long_list;
+    DevBuf<uint16_t> long_scratch;
     DevBuf<uint8_t> h2d_text;
     DevBuf<uint64_t> h2d_off, h2d_label_off;
     DevBuf<uint32_t> h2d_labels;
@@ -200,11 +207,26 @@ struct sdl_batcher {
         };
         mark(0);
         HIP_TRY(launch_chunk_ranges(d_off, R, N, ranges.p, st));
-        HIP_TRY(launch_wordpiece_chunks(dt, d_text, N, d_off, R, ranges.p, tokc.p, chunk_cnt.p, rec_local.p, st));
+        const bool bpe = dt.kind == TOK_BYTE_BPE;
+        if (bpe) {
+            // long pieces are > 64 bytes or run past their chunk's window (<= 1 per chunk)
+            const uint32_t cap = (uint32_t)(N / 64 + n_chunks + 1);
+            long_count.ensure(1);
+            bpe_err.ensure(1);
+            long_list.ensure(cap);
+            long_scratch.ensure((size_t)N + 64);
+            chunk_ent.ensure((size_t)n_chunks + 1);
+            HIP_TRY(launch_bpe_chunks(dt, d_text, N, d_off, R, ranges.p, tokc.p, chunk_cnt.p, chunk_ent.p,
+                                      rec_local.p, long_count.p, long_list.p, cap, long_scratch.p, bpe_err.p, st));
+        } else {
+            HIP_TRY(launch_wordpiece_chunks(dt, d_text, N, d_off, R, ranges.p, tokc.p, chunk_cnt.p, rec_local.p, st));
+        }
         mark(1);
         HIP_TRY(launch_exclusive_scan(chunk_cnt.p, chunk_off.p, n_chunks, scan_tmp.p, st));
         mark(2);
-        HIP_TRY(launch_compact_tokens(tokc.p, chunk_cnt.p, chunk_off.p, n_chunks, tok_ids.p, st));
+        HIP_TRY(launch_compact_tokens(tokc.p, chunk_cnt.p, chunk_off.p, n_chunks, tok_ids.p,
+                                      bpe ? long_count.p : nullptr, bpe ? chunk_ent.p : nullptr,
+                                      bpe ? long_list.p : nullptr, bpe ? long_scratch.p : nullptr, st));
         mark(3);
         HIP_TRY(launch_records(p, d_off, R, N, chunk_off.p, n_chunks, rec_local.p, rec_tok.p, rec_cnt.p, rec_rows.p,
                                st));
@@ -383,13 +405,30 @@ int sdl_batcher_create(const sdl_config *cfg, const char *tokenizer_path, const 
         h->d_slots.ensure(t.slots.size());
         h->d_vpool.ensure(t.vpool.size());
         h->d_ascii_id.ensure(128);
-        HIP_TRY(hipMemcpy(h->d_ascii_id.p, t.ascii_id.data(), 128 * 4, hipMemcpyHostToDevice));
+        if (t.ascii_id.size() == 128)
+            HIP_TRY(hipMemcpy(h->d_ascii_id.p, t.ascii_id.data(), 128 * 4, hipMemcpyHostToDevice));
         HIP_TRY(hipMemcpy(h->d_upage.p, t.upage.data(), t.upage.size() * 2, hipMemcpyHostToDevice));
         HIP_TRY(hipMemcpy(h->d_uentry.p, t.uentry.data(), t.uentry.size() * 4, hipMemcpyHostToDevice));
         HIP_TRY(hipMemcpy(h->d_upool.p, t.upool.data(), t.upool.size(), hipMemcpyHostToDevice));
         HIP_TRY(hipMemcpy(h->d_slots.p, t.slots.data(), t.slots.size() * sizeof(VSlot), hipMemcpyHostToDevice));
         HIP_TRY(hipMemcpy(h->d_vpool.p, t.vpool.data(), t.vpool.size(), hipMemcpyHostToDevice));
         DevTok &d = h->dt;
+        d.kind = t.kind;
+        if (t.kind == TOK_BYTE_BPE) {
+            h->d_gpage.ensure(t.gpage.size());
+            h->d_gblock.ensure(t.gblock.size());
+            h->d_mslots.ensure(t.mslots.size());
+            h->d_byte_id.ensure(256);
+            HIP_TRY(hipMemcpy(h->d_gpage.p, t.gpage.data(), t.gpage.size() * 2, hipMemcpyHostToDevice));
+            HIP_TRY(hipMemcpy(h->d_gblock.p, t.gblock.data(), t.gblock.size(), hipMemcpyHostToDevice));
+            HIP_TRY(hipMemcpy(h->d_mslots.p, t.mslots.data(), t.mslots.size() * sizeof(MSlot), hipMemcpyHostToDevice));
+            HIP_TRY(hipMemcpy(h->d_byte_id.p, t.byte_id.data(), 256 * 2, hipMemcpyHostToDevice));
+            d.gpage = h->d_gpage.p;
+            d.gblock = h->d_gblock.p;
+            d.mslots = h->d_mslots.p;
+            d.byte_id = h->d_byte_id.p;
+            d.mslot_mask = t.mslot_mask;
+        }
         d.ubmp = h->d_ubmp.p;
         d.upage = h->d_upage.p;
         d.uentry = h->d_uentry.p;
@@ -423,14 +462,22 @@ int sdl_batcher_create(const sdl_config *cfg, const char *tokenizer_path, const 
             P.min_ids = 0;
         }
         P.seed = cfg->seed;
-        // encode_mask framing (tokenizer_wrapper.rs:107-116): [CLS] + template([CLS] $A [SEP]) + [SEP] [SEP]
-        P.n_pre = 2;
-        P.pre[0] = t.cls_id;
-        P.pre[1] = t.tpl_cls;
-        P.n_post = 3;
-        P.post[0] = t.tpl_sep;
-        P.post[1] = t.sep_id;
-        P.post[2] = t.sep_id;
+        if (t.kind == TOK_BYTE_BPE) {
+            // encode_mask framing for Gpt (tokenizer_wrapper.rs:118-124): [eos] + ids + [eos]
+            P.n_pre = 1;
+            P.pre[0] = t.eos_id;
+            P.n_post = 1;
+            P.post[0] = t.eos_id;
+        } else {
+            // encode_mask framing (tokenizer_wrapper.rs:107-116): [CLS] + template([CLS] $A [SEP]) + [SEP] [SEP]
+            P.n_pre = 2;
+            P.pre[0] = t.cls_id;
+            P.pre[1] = t.tpl_cls;
+            P.n_post = 3;
+            P.post[0] = t.tpl_sep;
+            P.post[1] = t.sep_id;
+            P.post[2] = t.sep_id;
+        }
         h->store.push_back(h->new_batch());  // GenTokenizer::new: first DataSet
     } catch (HipError &e) {
         return fail(SDL_ERR_HIP, e.what());

@@ -1,0 +1,648 @@
+// tokenize_bpe.hip -- GPT-2 byte-level BPE tokenization of a text arena on gfx950.
+//
+// Restates, for a whole arena of records at once, what the reference does one
+// record at a time for task=clm (TokenizerHolder::get_ids ->
+// tokenizers::Tokenizer::encode, rust/src/tokenizer/tokenizer_holder.rs:19-28;
+// crate tokenizers 0.13.1) with the gpt2 tokenizer.json:
+//   AddedVocabulary split (<|endoftext|> on the raw text)
+//   -> ByteLevel pre-tokenizer, GPT-2 regex
+//        's|'t|'re|'ve|'m|'ll|'d| ?\p{L}+| ?\p{N}+| ?[^\s\p{L}\p{N}]+|\s+(?!\S)|\s+
+//   -> BPE by merge rank on the byte-level symbols of every pre-token.
+// The wrapper's [eos] ... [eos] framing is added at row assembly (pipeline.hip).
+//
+// The regex is evaluated byte-parallel: whether a pre-token starts at a char
+// depends only on a few neighbouring chars (previous char class, contraction
+// letters, whether a whitespace char ends its run), so every lane flags the
+// starts among its 16 bytes from the chunk's LDS window and class array.
+//
+// One wave64 per workgroup owns CHUNK bytes (16 per lane), as the WordPiece
+// kernel, and produces the same outputs (per-chunk id list in `tokc`, count,
+// per-record local offsets), so scans, compaction and rows are shared:
+//   1. load the window; classify every byte (ASCII arithmetically; lead bytes
+//      block-parallel through the probed class table; added tokens);
+//   2. pre-token starts -> LDS piece list;
+//   3. each piece: one probe of the word table (every vocab string whose BPE
+//      is itself, keyed by raw bytes) -- nearly every pre-token ends here;
+//   4. misses of <= 64 bytes: wave-cooperative BPE, one lane per symbol: each
+//      step merges every occurrence of the lowest-ranked adjacent pair (left
+//      to right within overlapping runs), the order tokenizers' heap yields
+//      for rank-monotone merges (checked on the host);
+//   5. longer pieces (or pieces running past the window) are appended to a
+//      global list and finished by k_bpe_long; the chunk list holds a marker.
+#include "common.hpp"
+#include "device_util.hpp"
+#include "kernels.hpp"
+#include "tok_device.hpp"
+
+namespace sdl {
+
+namespace {
+
+// per-byte class in LDS
+enum : uint8_t { K_CONT = 0, K_L = 1, K_N = 2, K_W = 3, K_O = 4, K_SP = 5, K_AP = 6, K_SPEC = 7, K_SPX = 8 };
+constexpr int K_BND = 15;  // "no char" (record start / added-token edge / text end)
+constexpr int BPE_MAX_WAVE = 64;  // pieces up to this many bytes are merged in the chunk kernel
+constexpr uint32_t LONG_MARK = 0x80000000u;
+
+__device__ __forceinline__ uint32_t ascii_k(uint32_t b) {
+    if ((b | 0x20u) - 'a' < 26u) return K_L;
+    if (b - '0' < 10u) return K_N;
+    if (b == ' ') return K_SP;
+    if (b - 9u < 5u) return K_W;
+    if (b == '\'') return K_AP;
+    return K_O;
+}
+
+__device__ __forceinline__ uint32_t gclass(const DevTok &T, uint32_t cp) {
+    if (cp >= 0x110000u) return GC_O;
+    return (T.gblock[(uint32_t)T.gpage[cp >> 8] * 64u + ((cp & 255u) >> 2)] >> (2 * (cp & 3u))) & 3u;
+}
+
+__device__ __forceinline__ uint32_t k_of_gc(uint32_t g) {
+    return g == GC_L ? K_L : g == GC_N ? K_N : g == GC_W ? K_W : K_O;
+}
+
+__device__ __forceinline__ bool is_w(int k) { return k == K_W || k == K_SP; }
+
+// rank/merged id of the pair (a, b): one cuckoo probe (two 8-B loads)
+__device__ __forceinline__ uint32_t merge_val(const DevTok &T, uint32_t a, uint32_t b) {
+    const uint32_t key = a << 16 | b, h = merge_hash(key);
+    const MSlot s1 = T.mslots[cuckoo_slot1(h, T.mslot_mask)];
+    const MSlot s2 = T.mslots[cuckoo_slot2(h, T.mslot_mask)];
+    if (s1.key == key) return s1.val;
+    if (s2.key == key) return s2.val;
+    return 0xFFFFFFFFu;
+}
+
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t x) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        const uint32_t y = (uint32_t)__shfl_xor((int)x, d, 64);
+        x = y < x ? y : x;
+    }
+    return x;
+}
+
+// Of the candidate pairs in m (bit j = pair (j, j+1)), those merged left to
+// right: the first of every run of adjacent candidates, then every other one.
+__device__ __forceinline__ uint64_t leftmost_alternating(uint64_t m, bool blocked0) {
+    uint64_t sel = 0;
+    if (blocked0) m &= ~1ull;  // its left symbol was merged into the previous pair
+    while (m) {
+        const uint64_t s = m & ~(m << 1);
+        sel |= s;
+        m &= ~(s | (s << 1));
+    }
+    return sel;
+}
+
+// ---- the GPT-2 regex as local rules --------------------------------------------
+// A pre-token starts at the char at q iff (pc = class of the previous char,
+// BND at a record start or next to an added token):
+//   added token                       -> start
+//   pc == BND                         -> start
+//   whitespace c: pc not whitespace   -> start
+//                 else start iff the next char is neither whitespace nor BND
+//                 (\s+(?!\S) leaves the last whitespace of a run to the next
+//                 pre-token)
+//   pc == ' '                         -> no  (" ?" prefix of L/N/O runs)
+//   pc other whitespace               -> start
+//   ' (apostrophe): start iff pc is a letter or digit
+//   O: start iff pc is not O/'
+//   N: start iff pc is not N
+//   L: after an apostrophe: start iff that apostrophe does not begin a
+//      contraction; after L: start iff a contraction ends right before q;
+//      else start.
+// A contraction ('s 't 're 've 'm 'll 'd, case-sensitive) begins at an
+// apostrophe that itself begins a pre-token: pc is BND, L, N or non-space
+// whitespace.  Every char is a valid UTF-8 sequence or one O byte.
+
+// Accessor over the chunk's LDS window (positions are window indices).
+struct LdsAcc {
+    const lds_u8 *win;
+    const lds_u8 *cls;
+    const lds_u32 *rbits;
+    int64_t w0, N;
+    __device__ __forceinline__ int k(int q) const { return cls[q]; }
+    __device__ __forceinline__ uint32_t b(int q) const { return win[q]; }
+    __device__ __forceinline__ bool rs(int q) const { return (rbits[q >> 5] >> (q & 31)) & 1u; }
+    __device__ __forceinline__ bool past(int q) const { return q >= WIN || w0 + q >= N; }
+};
+
+// Class of the byte at absolute position q computed from global memory (the
+// long-piece path).  Added tokens are ASCII (checked on the host), so no
+// UTF-8 sequence overlaps one.
+__device__ int gk_of(const Ctx &C, int64_t q) {
+    const DevTok &T = *C.T;
+    if (q < 0 || q >= C.N) return K_O;
+    if (T.n_special) {
+        for (int d = 0; d < T.max_special_len && q - d >= 0; ++d) {
+            const int64_t x = q - d;
+            if (C.byte(x) == T.opener) {
+                const int m = special_match(C, x);
+                if (m >= 0 && T.special_len[m] > d) return d == 0 ? K_SPEC : K_SPX;
+            }
+            if (C.rstart(x)) break;
+        }
+    }
+    const uint32_t b = C.byte(q);
+    if (b < 0x80u) return (int)ascii_k(b);
+    int len;
+    if (b >= 0xC0u) {
+        const uint32_t cp = decode(C, q, b, &len);
+        return len == 1 ? K_O : (int)k_of_gc(gclass(T, cp));
+    }
+    for (int d = 1; d <= 3 && q - d >= 0; ++d) {  // covered by a lead within 3 bytes?
+        if (C.rstart(q - d + 1)) break;
+        const uint32_t x = C.byte(q - d);
+        if ((x & 0xC0u) == 0x80u) continue;
+        if (x < 0xC0u) break;
+        decode(C, q - d, x, &len);
+        return len > d ? K_CONT : K_O;
+    }
+    return K_O;
+}
+
+struct GlobAcc {
+    const Ctx *C;
+    __device__ __forceinline__ int k(int64_t q) const { return gk_of(*C, q); }
+    __device__ __forceinline__ uint32_t b(int64_t q) const { return C->byte(q); }
+    __device__ __forceinline__ bool rs(int64_t q) const { return C->rstart(q); }
+    __device__ __forceinline__ bool past(int64_t q) const { return q >= C->N; }
+};
+
+// class of the char before the one at q; *pq = its position
+template <class A, class P>
+__device__ __forceinline__ int prev_k(const A &a, P q, P *pq) {
+    if (a.rs(q)) return K_BND;
+    P x = q - 1;
+    int k = a.k(x);
+    for (int s = 0; s < 3 && k == K_CONT; ++s) k = a.k(--x);
+    *pq = x;
+    return (k == K_SPEC || k == K_SPX) ? K_BND : k;
+}
+// class of the char after the one at q
+template <class A, class P>
+__device__ __forceinline__ int next_k(const A &a, P q) {
+    P x = q + 1;
+    for (int s = 0; s < 3 && !a.past(x) && a.k(x) == K_CONT; ++s) ++x;
+    if (a.past(x) || a.rs(x)) return K_BND;
+    const int k = a.k(x);
+    return k == K_SPEC ? K_BND : k;
+}
+// length (2 or 3) of the contraction beginning at the apostrophe q, else 0
+template <class A, class P>
+__device__ __forceinline__ int contraction(const A &a, P q) {
+    P pq;
+    const int pk = prev_k(a, q, &pq);
+    if (!(pk == K_BND || pk == K_L || pk == K_N || pk == K_W)) return 0;
+    if (a.past(q + 1) || a.rs(q + 1) || a.k(q + 1) != K_L) return 0;
+    const uint32_t b1 = a.b(q + 1);
+    if (b1 == 's' || b1 == 't' || b1 == 'm' || b1 == 'd') return 2;
+    if (a.past(q + 2) || a.rs(q + 2) || a.k(q + 2) != K_L) return 0;
+    const uint32_t b2 = a.b(q + 2);
+    if ((b1 == 'r' && b2 == 'e') || (b1 == 'v' && b2 == 'e') || (b1 == 'l' && b2 == 'l')) return 3;
+    return 0;
+}
+template <class A, class P>
+__device__ bool is_start(const A &a, P q) {
+    const int c = a.k(q);
+    if (c == K_CONT || c == K_SPX) return false;
+    if (c == K_SPEC) return true;
+    P pq = q - 1;
+    const int pc = prev_k(a, q, &pq);
+    if (pc == K_BND) return true;
+    if (is_w(c)) {
+        if (!is_w(pc)) return true;
+        const int nk = next_k(a, q);
+        return !(is_w(nk) || nk == K_BND);
+    }
+    if (pc == K_SP) return false;
+    if (pc == K_W) return true;
+    switch (c) {
+        case K_AP: return pc == K_L || pc == K_N;
+        case K_O: return !(pc == K_O || pc == K_AP);
+        case K_N: return pc != K_N;
+        default: break;  // K_L
+    }
+    if (pc == K_AP) return contraction(a, pq) == 0;
+    if (pc != K_L) return true;
+    if (a.k(q - 2) == K_AP && !a.rs(q - 1) && contraction(a, q - 2) == 2) return true;
+    if (a.k(q - 3) == K_AP && !a.rs(q - 2) && !a.rs(q - 1) && contraction(a, q - 3) == 3) return true;
+    return false;
+}
+
+// End of the piece starting at p when it runs past its chunk's window: the
+// next pre-token start, record start or the text end (wave-parallel scan).
+__device__ int64_t bpe_piece_end(const Ctx &C, int64_t p) {
+    const GlobAcc a{&C};
+    const int lane = lane_id();
+    for (int64_t q0 = p + 1;; q0 += 64) {
+        const int64_t q = q0 + lane;
+        const bool hit = q >= C.N || C.rstart(q) || is_start(a, q);
+        const uint64_t m = __ballot(hit);
+        if (m) return q0 + __builtin_ctzll(m);
+    }
+}
+
+// Wave-cooperative BPE of n <= 64 byte symbols held one per lane (sym valid on
+// lanes < n).  Returns the final symbol count; lane j < count holds id j.
+__device__ int bpe_wave(const DevTok &T, uint32_t &sym, int n, lds_u16 *tmp) {
+    const int lane = lane_id();
+    const uint64_t lt = (1ull << lane) - 1ull;
+    while (n > 1) {
+        const uint32_t nxt = (uint32_t)__shfl_down((int)sym, 1, 64);
+        const uint32_t v = lane < n - 1 ? merge_val(T, sym, nxt) : 0xFFFFFFFFu;
+        const uint32_t rank = v >> 16;
+        const uint32_t rmin = wave_min_u32(rank);
+        if (rmin == 0xFFFFu) break;
+        const uint64_t cand = __ballot(rank == rmin && lane < n - 1);
+        const uint64_t sel = leftmost_alternating(cand, false);
+        const bool me_sel = (sel >> lane) & 1ull;
+        if (me_sel) sym = v & 0xFFFFu;
+        const uint64_t live = (n == 64 ? ~0ull : ((1ull << n) - 1ull)) & ~(sel << 1);
+        if ((live >> lane) & 1ull) tmp[__popcll(live & lt)] = (uint16_t)sym;
+        __builtin_amdgcn_wave_barrier();
+        n = __popcll(live);
+        sym = lane < n ? tmp[lane] : 0u;
+        __builtin_amdgcn_wave_barrier();
+    }
+    return n;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(TOK_THREADS) void k_bpe_chunks(
+    DevTok T, const uint8_t *__restrict__ text, int64_t N, const uint64_t *__restrict__ off, int64_t R,
+    const uint32_t *__restrict__ ranges, uint32_t *__restrict__ tokc, uint32_t *__restrict__ chunk_cnt,
+    uint32_t *__restrict__ chunk_ent, uint32_t *__restrict__ rec_local, uint32_t *__restrict__ long_count,
+    BpeLong *__restrict__ long_list, uint32_t long_cap) {
+    __shared__ __attribute__((aligned(16))) uint8_t s_win[WIN];
+    __shared__ __attribute__((aligned(16))) uint8_t s_cls[WIN];
+    __shared__ uint32_t s_rbits[RBITS_WORDS + 1];
+    __shared__ uint16_t s_pieces[CHUNK + 1];  // prel | SPEC << 12 | LONG << 13
+    __shared__ uint16_t s_stage[STAGE];       // ids staged at their piece's byte position
+    __shared__ uint16_t s_cnt[CHUNK];         // ids per piece
+    __shared__ uint16_t s_poff[CHUNK];        // id offset of each piece in the chunk
+    __shared__ uint16_t s_rb[RB_CAP];
+    __shared__ uint16_t s_byte_id[256];
+    __shared__ uint16_t s_tmp[64];
+    __shared__ uint32_t s_scratch[8];
+
+    const int tid = threadIdx.x;
+    const int lane = tid;
+    const int64_t c0 = (int64_t)blockIdx.x * CHUNK;
+    const int64_t c1 = c0 + CHUNK < N ? c0 + CHUNK : N;
+    const int64_t w0 = c0 - HALO_L;
+    const lds_u8 *win = (const lds_u8 *)s_win;
+    lds_u8 *cls = (lds_u8 *)s_cls;
+    const lds_u32 *rbits = (const lds_u32 *)s_rbits;
+
+    // ---- 1. load + classify --------------------------------------------------
+    const uint4 v = load16(text, c0 + 16 * tid, N);
+    *reinterpret_cast<uint4 *>(s_win + HALO_L + 16 * tid) = v;
+    uint4 hv = make_uint4(0, 0, 0, 0);
+    int64_t hp = 0;
+    if (tid < (WIN - CHUNK) / 16) {
+        hp = tid < HALO_L / 16 ? w0 + 16 * tid : c0 + CHUNK + 16 * (tid - HALO_L / 16);
+        hv = load16(text, hp, N);
+        *reinterpret_cast<uint4 *>(s_win + (hp - w0)) = hv;
+    }
+    if (tid <= RBITS_WORDS) s_rbits[tid] = 0;
+    for (int i = tid; i < 256; i += TOK_THREADS) s_byte_id[i] = T.byte_id[i];
+    const int64_t ra = ranges[3 * blockIdx.x], rz = ranges[3 * blockIdx.x + 1], r_lo = ranges[3 * blockIdx.x + 2];
+    const int nrb = (int)(rz - ra);
+    const bool rb_ok = nrb <= RB_CAP;
+    if (tid == 0) s_scratch[0] = s_scratch[1] = 0;
+    __syncthreads();
+    for (int k = tid; k < nrb; k += TOK_THREADS) {
+        const int rel = (int)((int64_t)off[ra + k] - w0);
+        atomicOr(&s_rbits[rel >> 5], 1u << (rel & 31));
+        if (rb_ok) s_rb[k] = (uint16_t)rel;
+    }
+    // ASCII classes (bytes >= 0x80 provisionally O; text past N is O too)
+    auto classify16 = [&](const uint4 &x, int wi0, int64_t p0) {
+        const uint32_t wv[4] = {x.x, x.y, x.z, x.w};
+        uint32_t o[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const uint32_t b = (wv[i >> 2] >> (8 * (i & 3))) & 0xFFu;
+            const uint32_t k = b < 0x80u ? ascii_k(b) : (uint32_t)K_O;
+            o[i >> 2] |= k << (8 * (i & 3));
+        }
+        (void)p0;
+        *reinterpret_cast<uint4 *>(s_cls + wi0) = make_uint4(o[0], o[1], o[2], o[3]);
+    };
+    classify16(v, HALO_L + 16 * tid, c0 + 16 * tid);
+    if (tid < (WIN - CHUNK) / 16) classify16(hv, (int)(hp - w0), hp);
+    __syncthreads();
+
+    const Ctx C{&T, win, rbits, w0, text, N, off, R};
+    // rare bytes, block-parallel: lead bytes (decode: class, and the
+    // continuation bytes they cover), then added tokens (override)
+    for (int wi = tid; wi < WIN; wi += TOK_THREADS) {
+        const uint32_t b = win[wi];
+        const int64_t p = w0 + wi;
+        if (b < 0xC0u || p < 0 || p >= N) continue;
+        int len;
+        const uint32_t cp = decode(C, p, b, &len);
+        if (len == 1) continue;  // malformed: a one-byte O char
+        cls[wi] = (uint8_t)k_of_gc(gclass(T, cp));
+        for (int k = 1; k < len && wi + k < WIN; ++k) cls[wi + k] = K_CONT;
+    }
+    __syncthreads();
+    if (T.n_special) {
+        for (int wi = tid; wi < WIN; wi += TOK_THREADS) {
+            const int64_t p = w0 + wi;
+            if (win[wi] != T.opener || p < 0 || p >= N) continue;
+            const int m = special_match(C, p);
+            if (m < 0) continue;
+            const int l = T.special_len[m];
+            cls[wi] = K_SPEC;
+            for (int j = 1; j < l && wi + j < WIN; ++j) cls[wi + j] = K_SPX;
+        }
+        __syncthreads();
+    }
+
+    // ---- 2. pre-token starts -------------------------------------------------
+    const LdsAcc A{win, cls, rbits, w0, N};
+    const int64_t s0 = c0 + 16 * tid;
+    const int nown = s0 >= c1 ? 0 : (int)(c1 - s0 < 16 ? c1 - s0 : 16);
+    uint32_t pmask = 0;
+    for (int i = 0; i < nown; ++i)
+        if (is_start(A, HALO_L + 16 * tid + i)) pmask |= 1u << i;
+    uint32_t np_total;
+    uint32_t pbase = block_excl_sum<TOK_THREADS>((uint32_t)__builtin_popcount(pmask), &np_total, s_scratch + 2);
+    for (uint32_t m = pmask; m;) {
+        const int i = __builtin_ctz(m);
+        m &= m - 1;
+        const int wi = HALO_L + 16 * tid + i;
+        s_pieces[pbase++] = (uint16_t)((16 * tid + i) | (cls[wi] == K_SPEC ? 1u << 12 : 0u));
+    }
+    // end of the last piece: the first start at or after c1 within the window
+    // (lookahead of a char needs 4 more bytes), else it runs on (long piece)
+    if (tid == 0) {
+        int e = -1;
+        if (c1 >= N) e = (int)(c1 - c0);
+        else {
+            for (int wi = (int)(c1 - w0); wi < WIN - 8; ++wi) {
+                if (w0 + wi >= N) { e = (int)(N - c0); break; }
+                if (rbits[wi >> 5] >> (wi & 31) & 1u || is_start(A, wi)) { e = wi - HALO_L; break; }
+            }
+        }
+        s_scratch[0] = (uint32_t)e;
+    }
+    __syncthreads();
+    const int np = (int)np_total;
+    const int e_last = (int)s_scratch[0];
+    s_pieces[np] = (uint16_t)(e_last < 0 ? 0xFFFFu : (uint32_t)e_last);
+
+    // ---- 3. word-table probe per piece ----------------------------------------
+    lds_u16 *stage = (lds_u16 *)s_stage;
+    lds_u16 *cnt = (lds_u16 *)s_cnt;
+    uint16_t *s_pend = s_poff;  // pieces for the wave BPE (s_poff is free until step 5)
+    const lds_u32 *w32 = (const lds_u32 *)s_win;
+    if (tid == 0) s_scratch[1] = 0;
+    __syncthreads();
+    for (int pi = tid; pi < np; pi += TOK_THREADS) {
+        const uint32_t pc = s_pieces[pi];
+        const int prel = (int)(pc & 0xFFFu);
+        const int nxt = pi + 1 < np ? (int)(s_pieces[pi + 1] & 0xFFFu) : e_last;
+        bool pend = false;
+        if (pc & (1u << 12)) {
+            const int m = special_match(C, c0 + prel);
+            stage[prel] = (uint16_t)T.special_id[m < 0 ? 0 : m];
+            cnt[pi] = 1;
+        } else if (nxt < 0 || nxt - prel > BPE_MAX_WAVE) {
+            // long piece: finished by k_bpe_long
+            const uint32_t li = atomicAdd(long_count, 1u);
+            if (li < long_cap) {
+                long_list[li].pos = (uint64_t)(c0 + prel);
+                long_list[li].len = nxt < 0 ? 0u : (uint32_t)(nxt - prel);  // 0: find the end
+                long_list[li].chunk = (uint32_t)blockIdx.x;
+                long_list[li].k = 0;
+            }
+            stage[prel] = (uint16_t)(li & 0xFFFFu);
+            stage[prel + 1] = (uint16_t)(li >> 16);
+            cnt[pi] = 0xFFFFu;  // marker
+        } else {
+            const int n = nxt - prel;
+            if (n <= 16) {
+                const int wr = prel + HALO_L;
+                const int a = wr >> 2;
+                const uint32_t sh = (uint32_t)(wr & 3);
+                const uint32_t x0 = w32[a], x1 = w32[a + 1], x2 = w32[a + 2], x3 = w32[a + 3], x4 = w32[a + 4];
+                const W16 raw{__builtin_amdgcn_alignbyte(x1, x0, sh), __builtin_amdgcn_alignbyte(x2, x1, sh),
+                              __builtin_amdgcn_alignbyte(x3, x2, sh), __builtin_amdgcn_alignbyte(x4, x3, sh)};
+                const W16 w = keep_bytes(raw, n);
+                const int id = probe_result(probe_load(T, hash16(w, (uint32_t)n, 0u)), (uint32_t)n, w);
+                if (id >= 0) {
+                    stage[prel] = (uint16_t)id;
+                    cnt[pi] = 1;
+                } else {
+                    pend = true;
+                }
+            } else {
+                // 17..64 bytes: hash the LDS bytes, compare the payload beyond 16 from the pool
+                const uint32_t un = (uint32_t)n;
+                uint32_t h = hinit(un, 0u);
+                W16 first{0, 0, 0, 0};
+                for (uint32_t b0 = 0; b0 < un; b0 += 16) {
+                    uint32_t c[4] = {0, 0, 0, 0};
+                    for (uint32_t k = 0; k < 16 && b0 + k < un; ++k)
+                        c[k >> 2] |= (uint32_t)win[prel + HALO_L + b0 + k] << (8 * (k & 3));
+                    if (b0 == 0) first = W16{c[0], c[1], c[2], c[3]};
+                    h = hmix(hmix(hmix(hmix(h, c[0]), c[1]), c[2]), c[3]);
+                }
+                const Probe P = probe_load(T, hfinal(h));
+                int id = -1;
+                for (int which = 0; which < 2 && id < 0; ++which) {
+                    const uint4 sa = which ? P.a2 : P.a1, sb = which ? P.b2 : P.b1;
+                    if (!slot_match(sa, sb, un, first)) continue;
+                    bool ok = true;
+                    for (uint32_t k = 16; k < un && ok; ++k) ok = T.vpool[sa.z + k] == win[prel + HALO_L + k];
+                    if (ok) id = (int32_t)sa.y;
+                }
+                if (id >= 0) {
+                    stage[prel] = (uint16_t)id;
+                    cnt[pi] = 1;
+                } else {
+                    pend = true;
+                }
+            }
+        }
+        const uint64_t pm = __ballot(pend);
+        if (pm) {
+            const int leader = __builtin_ctzll(pm);
+            uint32_t base = 0;
+            if (lane == leader) base = atomicAdd(&s_scratch[1], (uint32_t)__popcll(pm));
+            base = __shfl(base, leader, 64);
+            if (pend) s_pend[base + __popcll(pm & ((1ull << lane) - 1ull))] = (uint16_t)pi;
+        }
+    }
+    __syncthreads();
+
+    // ---- 4. wave BPE of the misses ---------------------------------------------
+    const int npend = (int)s_scratch[1];
+    for (int q = 0; q < npend; ++q) {
+        const int pi = s_pend[q];
+        const int prel = (int)(s_pieces[pi] & 0xFFFu);
+        const int nxt = pi + 1 < np ? (int)(s_pieces[pi + 1] & 0xFFFu) : e_last;
+        const int n = nxt - prel;
+        uint32_t sym = lane < n ? (uint32_t)s_byte_id[win[prel + HALO_L + lane]] : 0u;
+        const int k = bpe_wave(T, sym, n, (lds_u16 *)s_tmp);
+        if (lane < k) stage[prel + lane] = (uint16_t)sym;
+        if (lane == 0) cnt[pi] = (uint16_t)k;
+        __syncthreads();
+    }
+
+    // ---- 5. compact ids into this chunk's tokc slice ------------------------------
+    const int per = (np + TOK_THREADS - 1) / TOK_THREADS;
+    const int a0 = tid * per < np ? tid * per : np;
+    const int a1 = a0 + per < np ? a0 + per : np;
+    uint32_t mine = 0;
+    for (int i = a0; i < a1; ++i) mine += s_cnt[i] == 0xFFFFu ? 1u : s_cnt[i];
+    uint32_t total;
+    uint32_t base = block_excl_sum<TOK_THREADS>(mine, &total, s_scratch + 2);
+    uint32_t *dst = tokc + (int64_t)blockIdx.x * STAGE;
+    for (int i = a0; i < a1; ++i) {
+        s_poff[i] = (uint16_t)base;
+        const int prel = s_pieces[i] & 0xFFF;
+        const int k = s_cnt[i];
+        if (k == 0xFFFF) {
+            dst[base++] = LONG_MARK | (uint32_t)s_stage[prel] | ((uint32_t)s_stage[prel + 1] << 16);
+            continue;
+        }
+        for (int j = 0; j < k; ++j) dst[base + j] = s_stage[prel + j];
+        base += k;
+    }
+    __syncthreads();
+    if (tid == 0) chunk_cnt[blockIdx.x] = chunk_ent[blockIdx.x] = total;
+    // record boundaries owned by this chunk: local entry offset of the first
+    // piece at or after the boundary (k_bpe_long adds long pieces' extra ids)
+    const int k_lo = (int)(r_lo - ra);
+    for (int k = k_lo + tid;; k += TOK_THREADS) {
+        int64_t pos;
+        if (rb_ok) {
+            if (k >= nrb) break;
+            pos = w0 + s_rb[k];
+        } else {
+            if (ra + k > R) break;
+            pos = (int64_t)off[ra + k];
+        }
+        if (pos >= c1) break;
+        const int rel = (int)(pos - c0);
+        int lo = 0, hi = np;
+        while (lo < hi) {
+            const int m = (lo + hi) >> 1;
+            if ((int)(s_pieces[m] & 0xFFF) < rel) lo = m + 1; else hi = m;
+        }
+        rec_local[ra + k] = lo < np ? (uint32_t)s_poff[lo] : total;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Long pieces (> 64 bytes, or running past their chunk's window): one wave
+// each, symbols in `scratch` at the piece's own byte positions (u16), the same
+// merge steps as bpe_wave in 64-symbol tiles.  The ids stay in `scratch`;
+// the chunk's count and the local offsets of its later records grow by k - 1.
+__global__ __launch_bounds__(64) void k_bpe_long(DevTok T, const uint8_t *__restrict__ text, int64_t N,
+                                                 const uint64_t *__restrict__ off, int64_t R,
+                                                 const uint32_t *__restrict__ long_count, BpeLong *__restrict__ list,
+                                                 uint32_t long_cap, uint16_t *__restrict__ scratch,
+                                                 uint32_t *__restrict__ chunk_cnt, uint32_t *__restrict__ rec_local,
+                                                 uint32_t *__restrict__ err) {
+    __shared__ uint16_t s_byte_id[256];
+    for (int i = threadIdx.x; i < 256; i += 64) s_byte_id[i] = T.byte_id[i];
+    __syncthreads();
+    const Ctx C{&T, nullptr, nullptr, INT64_MIN / 4, text, N, off, R};  // no window: global reads
+    const int lane = lane_id();
+    const uint64_t lt = (1ull << lane) - 1ull;
+    uint32_t n_long = *long_count;
+    if (n_long > long_cap) {
+        if (blockIdx.x == 0 && lane == 0) atomicOr(err, 1u);
+        n_long = long_cap;
+    }
+    for (uint32_t li = blockIdx.x; li < n_long; li += gridDim.x) {
+        const int64_t p = (int64_t)list[li].pos;
+        int64_t n = list[li].len;
+        // record containing p (its end bounds the piece)
+        int64_t lo = 0, hi = R;
+        while (lo < hi) {
+            const int64_t mid = (lo + hi) >> 1;
+            if ((int64_t)off[mid + 1] <= p) lo = mid + 1; else hi = mid;
+        }
+        const int64_t rec = lo;
+        if (n == 0) n = bpe_piece_end(C, p) - p;  // ran past its chunk's window
+        // initial symbols
+        for (int64_t j = lane; j < n; j += 64) scratch[p + j] = s_byte_id[text[p + j]];
+        __syncthreads();
+        int64_t m = n;
+        for (;;) {
+            // pass 1: lowest rank over all adjacent pairs
+            uint32_t rmin = 0xFFFFu;
+            for (int64_t j = lane; j + 1 < m; j += 64) {
+                const uint32_t v = merge_val(T, scratch[p + j], scratch[p + j + 1]);
+                const uint32_t r = v >> 16;
+                rmin = r < rmin ? r : rmin;
+            }
+            rmin = wave_min_u32(rmin);
+            if (rmin == 0xFFFFu) break;
+            // pass 2: merge its occurrences left to right, compact in place
+            bool blocked = false;  // the last pair of the previous tile merged
+            int64_t outp = 0;
+            for (int64_t t0 = 0; t0 < m; t0 += 64) {
+                const int64_t j = t0 + lane;
+                const uint32_t sym = j < m ? scratch[p + j] : 0u;
+                const uint32_t nx = j + 1 < m ? scratch[p + j + 1] : 0u;
+                const uint32_t v = j + 1 < m ? merge_val(T, sym, nx) : 0xFFFFFFFFu;
+                const uint64_t cand = __ballot(j + 1 < m && (v >> 16) == rmin);
+                const uint64_t sel = leftmost_alternating(cand, blocked);
+                const uint64_t tile = (m - t0 >= 64) ? ~0ull : ((1ull << (m - t0)) - 1ull);
+                uint64_t live = tile & ~(sel << 1);
+                if (blocked) live &= ~1ull;  // removed by the previous tile's last merge
+                const bool me = (sel >> lane) & 1ull;
+                const uint32_t out = me ? (v & 0xFFFFu) : sym;
+                __syncthreads();  // every lane has read its tile before any lane writes
+                if ((live >> lane) & 1ull) scratch[p + outp + __popcll(live & lt)] = (uint16_t)out;
+                __syncthreads();
+                outp += __popcll(live);
+                blocked = (sel >> 63) & 1ull;
+            }
+            m = outp;
+            __syncthreads();
+        }
+        if (lane == 0) {
+            list[li].k = (uint32_t)m;
+            list[li].len = (uint32_t)n;
+            const uint32_t extra = (uint32_t)m - 1u;
+            if (extra) {
+                atomicAdd(&chunk_cnt[list[li].chunk], extra);
+                // later record starts in the same chunk
+                const int64_t cend = ((int64_t)list[li].chunk + 1) * CHUNK;
+                for (int64_t r = rec + 1; r < R && (int64_t)off[r] < cend; ++r) {
+                    if ((int64_t)off[r] > p) atomicAdd(&rec_local[r], extra);
+                }
+            }
+        }
+        __syncthreads();
+    }
+}
+
+hipError_t launch_bpe_chunks(const DevTok &T, const uint8_t *text, int64_t N, const uint64_t *off, int64_t R,
+                             const uint32_t *ranges, uint32_t *tokc, uint32_t *chunk_cnt, uint32_t *chunk_ent,
+                             uint32_t *rec_local, uint32_t *long_count, BpeLong *long_list, uint32_t long_cap,
+                             uint16_t *scratch, uint32_t *err, hipStream_t st) {
+    const int64_t n_chunks = (N + CHUNK - 1) / CHUNK;
+    if (n_chunks == 0) return hipSuccess;
+    hipError_t e = hipMemsetAsync(long_count, 0, sizeof(uint32_t), st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_bpe_chunks, dim3((unsigned)n_chunks), dim3(TOK_THREADS), 0, st, T, text, N, off, R, ranges,
+                       tokc, chunk_cnt, chunk_ent, rec_local, long_count, long_list, long_cap);
+    hipLaunchKernelGGL(k_bpe_long, dim3(1024), dim3(64), 0, st, T, text, N, off, R, long_count, long_list, long_cap,
+                       scratch, chunk_cnt, rec_local, err);
+    return hipGetLastError();
+}
+
+}  // namespace sdl

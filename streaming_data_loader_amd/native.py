@@ -11,6 +11,7 @@ LIB_PATH = os.environ.get("SDL_LIB") or os.path.join(PKG, "libsdl_batcher.so")
 DATA_DIR = os.path.join(PKG, "data")
 ASSETS = os.path.join(PKG, "assets")
 BERT_PROXY_TOKENIZER = os.path.join(ASSETS, "bert_proxy", "tokenizer.json")
+GPT2_PROXY_TOKENIZER = os.path.join(ASSETS, "gpt2_proxy", "tokenizer.json")
 
 SDL_TASK_MLM, SDL_TASK_CLM, SDL_TASK_SPAN, SDL_TASK_MULTI_LABEL = 0, 1, 2, 3
 
