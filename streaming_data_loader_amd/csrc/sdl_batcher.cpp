@@ -96,8 +96,8 @@ struct HostBatch {
     }
 };
 
-const char *kStageNames[] = {"wordpiece_chunks", "scan_chunks", "compact_tokens", "records", "scan_rows", "rows"};
-constexpr int kStages = 6;
+const char *kStageNames[] = {"chunk_ranges", "tokenize", "scan_chunks", "compact_tokens", "records", "scan_rows", "rows"};
+constexpr int kStages = 7;
 
 }  // namespace
 
@@ -207,6 +207,7 @@ struct sdl_batcher {
         };
         mark(0);
         HIP_TRY(launch_chunk_ranges(d_off, R, N, ranges.p, st));
+        mark(1);
         const bool bpe = dt.kind == TOK_BYTE_BPE;
         if (bpe) {
             // long pieces are > 64 bytes or run past their chunk's window (<= 1 per chunk)
@@ -221,19 +222,19 @@ struct sdl_batcher {
         } else {
             HIP_TRY(launch_wordpiece_chunks(dt, d_text, N, d_off, R, ranges.p, tokc.p, chunk_cnt.p, rec_local.p, st));
         }
-        mark(1);
-        HIP_TRY(launch_exclusive_scan(chunk_cnt.p, chunk_off.p, n_chunks, scan_tmp.p, st));
         mark(2);
+        HIP_TRY(launch_exclusive_scan(chunk_cnt.p, chunk_off.p, n_chunks, scan_tmp.p, st));
+        mark(3);
         HIP_TRY(launch_compact_tokens(tokc.p, chunk_cnt.p, chunk_off.p, n_chunks, tok_ids.p,
                                       bpe ? long_count.p : nullptr, bpe ? chunk_ent.p : nullptr,
                                       bpe ? long_list.p : nullptr, bpe ? long_scratch.p : nullptr, st));
-        mark(3);
+        mark(4);
         HIP_TRY(launch_records(p, d_off, R, N, chunk_off.p, n_chunks, rec_local.p, rec_tok.p, rec_cnt.p, rec_rows.p,
                                st));
-        mark(4);
+        mark(5);
         HIP_TRY(launch_exclusive_scan(rec_rows.p, row_off.p, R, scan_tmp.p, st));
         HIP_TRY(launch_row_map(row_off.p, R, row_rec.p, st));
-        mark(5);
+        mark(6);
         RowOut out{o_ids.p, o_am.p, with_tt() ? o_tt.p : nullptr, multi() ? nullptr : o_lab.p,
                    multi() ? o_f32.p : nullptr};
         HIP_TRY(launch_rows(p, tok_ids.p, rec_tok.p, rec_cnt.p, row_off.p, row_rec.p, row_off.p + R, rows_cap, out, st));
@@ -242,7 +243,7 @@ struct sdl_batcher {
             HIP_TRY(launch_multi_labels(d_labels, d_label_off, row_rec.p, row_off.p + R, rows_cap, P.B, P.label_width,
                                         o_f32.p, lab_err.p, st));
         }
-        mark(6);
+        mark(7);
         last_rows_cap = rows_cap;
         last_R = R;
     }

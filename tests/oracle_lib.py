@@ -212,6 +212,12 @@ class OracleBatcherEx:
             raise ValueError("label index >= number_labels")
         return self._result() if rc == 1 else None
 
+    def push_raw(self, b, labels=None):
+        """push() of bytes without copying a finished batch out (timing)."""
+        lab = None if labels is None else np.ascontiguousarray(labels, np.uint32)
+        return lib().orc_batcher_push_ex(self.h, b, len(b), None if lab is None else lab.ctypes.data,
+                                         0 if lab is None else lab.size, ctypes.byref(self.out))
+
     def flush(self):
         return self._result() if lib().orc_batcher_flush_ex(self.h, ctypes.byref(self.out)) == 1 else None
 
