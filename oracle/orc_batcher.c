@@ -7,9 +7,11 @@
  *   SimpleBatcher          rust/src/models/simple_batcher.rs:35-53 (multi-label)
  *   BertData               rust/src/models/bert_data.rs:40-89    (Mask, MultiLabel)
  *   GptData                rust/src/models/gpt_data.rs:29-45
+ *   T5Data (Span)          rust/src/models/t5_data.rs:162-226
  *   encode_mask framing    rust/src/tokenizer/tokenizer_wrapper.rs:107-134
  *   RNG contract           DESIGN.md §3 (replaces the unseedable thread_rng)
  */
+#include <math.h>
 #include <stdio.h>
 #include <string.h>
 
@@ -41,6 +43,41 @@ uint32_t orc_mlm_key(uint64_t seed, uint64_t record, uint32_t chunk, uint32_t po
     return c[pos & 3];
 }
 
+/* Span draws: the reference's trunc(avg - z) with z ~ StandardNormal
+ * (t5_data.rs:165-176, `as usize` saturating at 0) is sampled exactly in
+ * distribution by inverting its CDF on a 32-bit uniform:
+ *   P(v <= k) = P(z > avg - k - 1) = erfc((avg - k - 1) / sqrt 2) / 2,
+ *   thr[j] = floor(2^32 P(v <= kmin + j)),  v = kmin + #{j : thr[j] <= x}.
+ * `lo` is the smallest value v can take (0 for the gap; 1 for the size, whose
+ * max(.., 1) folds everything below into 1). */
+void orc_span_table(double avg, int lo, int32_t *kmin, int32_t *n, uint32_t *thr, int cap) {
+    double k0 = floor(avg - 10.0);
+    if (k0 < lo) k0 = lo;
+    if (k0 > 1e9) k0 = 1e9;
+    *kmin = (int32_t)k0;
+    int m = 0;
+    for (int j = 0; j < cap; ++j) {
+        const double cdf = 0.5 * erfc((avg - (k0 + j) - 1.0) / sqrt(2.0));
+        const double t = floor(cdf * 4294967296.0);
+        if (t >= 4294967296.0) break;
+        thr[m++] = (uint32_t)t;
+    }
+    *n = m;
+}
+
+/* The two uniforms of span pass `pass` of row (record, chunk). */
+static void span_draws(uint64_t seed, uint64_t rec, uint32_t chunk, uint32_t pass, uint32_t *xg, uint32_t *xs) {
+    uint32_t c[4] = {pass, chunk | 0x40000000u, (uint32_t)rec, (uint32_t)(rec >> 32)};
+    philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+    *xg = c[0];
+    *xs = c[1];
+}
+static uint32_t span_pick(const int32_t kmin, const int32_t n, const uint32_t *thr, uint32_t x) {
+    int32_t v = kmin;
+    for (int j = 0; j < n; ++j) v += thr[j] <= x;
+    return (uint32_t)v;
+}
+
 /* ------------------------------------------------------------------------- */
 /* DataSet                                                                    */
 /* ------------------------------------------------------------------------- */
@@ -50,10 +87,14 @@ typedef struct {
     int index;
 } obatch;
 
+#define SPAN_TAB 32
 struct orc_batcher {
     orc_encoder enc;
     orc_cfg c;
     int LW, NL;
+    int32_t gap_kmin, gap_n, size_kmin, size_n;
+    uint32_t gap_thr[SPAN_TAB], size_thr[SPAN_TAB];
+    uint64_t span_errors; /* label/sentinel writes the reference would panic on */
     uint64_t n_records;
     obatch **q;
     int qh, qn, qcap;
@@ -100,7 +141,8 @@ static void q_push(orc_batcher *b, obatch *x) {
 
 orc_batcher *orc_batcher_create(const orc_encoder *e, const orc_cfg *c) {
     if (!e || !c || c->B <= 0 || c->S <= 0) return NULL;
-    if (c->task != ORC_MLM && c->task != ORC_CLM && c->task != ORC_MULTI_LABEL) return NULL;
+    if (c->task != ORC_MLM && c->task != ORC_CLM && c->task != ORC_MULTI_LABEL && c->task != ORC_SPAN) return NULL;
+    if (c->task == ORC_SPAN && c->S < 4) return NULL;
     if (c->task == ORC_MLM && (c->mask_length < 0 || c->mask_length > c->S)) return NULL;
     if (c->task == ORC_MULTI_LABEL && c->number_labels <= 0) return NULL;
     orc_batcher *b = (orc_batcher *)calloc(1, sizeof(orc_batcher));
@@ -111,7 +153,11 @@ orc_batcher *orc_batcher_create(const orc_encoder *e, const orc_cfg *c) {
         b->c.min_ids = 0;
     }
     b->NL = c->task == ORC_MULTI_LABEL ? c->number_labels : 0;
-    b->LW = c->task == ORC_MULTI_LABEL ? 0 : c->S;
+    b->LW = c->task == ORC_MULTI_LABEL ? 0 : c->task == ORC_SPAN ? c->S / 4 : c->S; /* t5_data.rs:44 */
+    if (c->task == ORC_SPAN) {
+        orc_span_table(c->avg_span_gap, 0, &b->gap_kmin, &b->gap_n, b->gap_thr, SPAN_TAB);
+        orc_span_table(c->avg_span_size, 1, &b->size_kmin, &b->size_n, b->size_thr, SPAN_TAB);
+    }
     q_push(b, obatch_new(b)); /* GenTokenizer::new / SimpleBatcher::new: first DataSet */
     return b;
 }
@@ -169,6 +215,45 @@ static int put_data(orc_batcher *b, obatch *x, const uint32_t *ids, size_t n, ui
             }
         }
         break;
+    case ORC_SPAN: { /* T5Data::put_data (t5_data.rs:162-226), one chunk = one row */
+        int32_t *lb = x->lab + (size_t)x->index * b->LW;
+        const size_t LW = (size_t)b->LW;
+        for (size_t j = 0; j < l; ++j) in[j] = 0; /* rewritten below */
+        size_t ip = 0, lp = 0, ap = 0;
+        uint32_t pass = 0;
+#define EXTRA(k) ((k) < 100 ? (int32_t)b->enc.extra[k] : (b->span_errors++, (int32_t)b->enc.extra[99]))
+#define LAB(i, v) do { if ((i) < LW) lb[i] = (v); else b->span_errors++; } while (0)
+        while (lp < S) {
+            uint32_t xg, xs;
+            span_draws(b->c.seed, rec, chunk, pass, &xg, &xs);
+            size_t g = span_pick(b->gap_kmin, b->gap_n, b->gap_thr, xg);
+            if (g > S - lp) g = S - lp;
+            if (g > n - ip) g = n - ip;
+            for (size_t j = 0; j < g; ++j) in[lp + j] = (int32_t)ids[ip + j];
+            lp += g;
+            ip += g;
+            size_t sz = span_pick(b->size_kmin, b->size_n, b->size_thr, xs);
+            if (sz > S - lp) sz = S - lp;
+            if (sz > n - ip) sz = n - ip;
+            if (sz > 0) {
+                const int32_t e = EXTRA(pass);
+                in[lp] = e;
+                LAB(ap, e);
+                for (size_t j = 0; j < sz; ++j) LAB(ap + j + 1, (int32_t)ids[ip + j]);
+                lp += 1;
+                ip += sz;
+                ap += sz + 1;
+            }
+            if (n <= ip) { /* attention_mask untouched: the loop 0..ip-n is empty */
+                LAB(ap, EXTRA(pass + 1));
+                break;
+            }
+            pass++;
+        }
+#undef EXTRA
+#undef LAB
+        break;
+    }
     case ORC_CLM: { /* GptData::put_data (gpt_data.rs:29-45): labels = row, no shift */
         int32_t *lb = x->lab + (size_t)x->index * S;
         for (size_t j = 0; j < S; ++j) lb[j] = in[j];
@@ -252,6 +337,7 @@ void orc_batcher_free(orc_batcher *b) {
 }
 
 void orc_batcher_set_next_record(orc_batcher *b, uint64_t record) { b->n_records = record; }
+uint64_t orc_batcher_span_errors(const orc_batcher *b) { return b->span_errors; }
 
 /* ---- round-1 MLM entry points (4 planes [B,S] back to back) ---- */
 orc_batcher *orc_batcher_new(const orc_tok *t, int task, int batch_size, int seq_len, int mask_length, int mask_id,

@@ -24,6 +24,7 @@ struct orc_encoder {
     const void *impl;
     int npre, npost;
     uint32_t pre[4], post[4];
+    uint32_t extra[100]; /* T5 <extra_id_k> ids (TokenizerInfo.extra, tokenizer_wrapper.rs:77-80) */
 };
 
 void orc_bert_encode_vec(const orc_tok *t, const uint8_t *s, size_t n, idvec *out);

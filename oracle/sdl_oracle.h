@@ -50,6 +50,21 @@ void orc_gpt2_free(orc_gpt2 *t);
 long orc_gpt2_encode(const orc_gpt2 *t, const uint8_t *s, size_t n, uint32_t *out, size_t cap);
 int orc_gpt2_eos(const orc_gpt2 *t);
 
+/* ---- t5-small (Precompiled + Unigram) tokenizer: oracle/orc_unigram.c ---- */
+typedef struct orc_t5 orc_t5;
+/* Loads a t5 tokenizer.json (Precompiled charsmap, Unigram vocab, added
+ * tokens) and the grapheme property table (data/t5_graphemes.bin). */
+orc_t5 *orc_t5_load(const char *tokenizer_json, const char *graphemes_bin);
+void orc_t5_free(orc_t5 *t);
+/* Tokenizer::encode(text, true).get_ids(); returns the id count, writes <= cap. */
+long orc_t5_encode(const orc_t5 *t, const uint8_t *s, size_t n, uint32_t *out, size_t cap);
+/* The Precompiled normalizer alone; returns the output length. */
+long orc_t5_normalize(const orc_t5 *t, const uint8_t *s, size_t n, uint8_t *out, size_t cap);
+/* Byte offsets of the extended grapheme cluster starts; returns their count. */
+long orc_t5_graphemes(const orc_t5 *t, const uint8_t *s, size_t n, uint32_t *starts, size_t cap);
+int orc_t5_eos(const orc_t5 *t);
+int orc_t5_special_id(const orc_t5 *t, const char *s);
+
 /* ---- Batcher ------------------------------------------------------------ */
 enum { ORC_MLM = 0, ORC_CLM = 1, ORC_SPAN = 2, ORC_MULTI_LABEL = 3 }; /* = SDL_TASK_* */
 
@@ -76,6 +91,10 @@ void orc_encoder_bert(const orc_tok *t, orc_encoder *e);
 size_t orc_encoder_size(void);
 /* gpt2 encoder with the [eos] ... [eos] framing. */
 void orc_encoder_gpt2(const orc_gpt2 *t, orc_encoder *e);
+/* t5 encoder with the </s> ... </s> framing and the 100 sentinel ids. */
+void orc_encoder_t5(const orc_t5 *t, orc_encoder *e);
+/* Span draw table (RNG contract): v = kmin + #{j < n : thr[j] <= x}. */
+void orc_span_table(double avg, int lo, int32_t *kmin, int32_t *n, uint32_t *thr, int cap);
 
 orc_batcher *orc_batcher_create(const orc_encoder *e, const orc_cfg *c);
 /* create_sync_batch(record[, Label::Multi indices]): 1 = a batch was emitted
@@ -94,6 +113,8 @@ int orc_batcher_flush(orc_batcher *b, int32_t *out, int *rows);
 void orc_batcher_free(orc_batcher *b);
 /* Sets the global index the next pushed record gets (sharded streams). */
 void orc_batcher_set_next_record(orc_batcher *b, uint64_t record);
+/* span: label / sentinel writes past their bounds (the reference panics) */
+uint64_t orc_batcher_span_errors(const orc_batcher *b);
 
 #ifdef __cplusplus
 }

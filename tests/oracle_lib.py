@@ -16,6 +16,8 @@ VOCAB_TXT = os.path.join(REPO, "streaming_data_loader_amd", "assets", "bert_prox
 UNICODE_BIN = os.path.join(REPO, "streaming_data_loader_amd", "data", "bert_uncased_unicode.bin")
 GPT2_JSON = os.path.join(REPO, "streaming_data_loader_amd", "assets", "gpt2_proxy", "tokenizer.json")
 GPT2_CLASSES = os.path.join(REPO, "streaming_data_loader_amd", "data", "gpt2_classes.bin")
+T5_JSON = os.path.join(REPO, "streaming_data_loader_amd", "assets", "t5_proxy", "tokenizer.json")
+T5_GRAPHEMES = os.path.join(REPO, "streaming_data_loader_amd", "data", "t5_graphemes.bin")
 
 _lib = None
 
@@ -65,6 +67,20 @@ def lib():
         L.orc_gpt2_eos.argtypes = [vp]
         L.orc_encoder_gpt2.argtypes = [vp, vp]
         L.orc_encoder_gpt2.restype = None
+        L.orc_t5_load.restype = vp
+        L.orc_t5_load.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+        L.orc_t5_free.argtypes = [vp]
+        for f in ("orc_t5_encode", "orc_t5_normalize", "orc_t5_graphemes"):
+            getattr(L, f).restype = ctypes.c_long
+            getattr(L, f).argtypes = [vp, ctypes.c_char_p, ctypes.c_size_t, vp, ctypes.c_size_t]
+        L.orc_t5_eos.argtypes = [vp]
+        L.orc_t5_special_id.argtypes = [vp, ctypes.c_char_p]
+        L.orc_encoder_t5.argtypes = [vp, vp]
+        L.orc_encoder_t5.restype = None
+        L.orc_span_table.argtypes = [ctypes.c_double, ctypes.c_int, vp, vp, vp, ctypes.c_int]
+        L.orc_span_table.restype = None
+        L.orc_batcher_span_errors.argtypes = [vp]
+        L.orc_batcher_span_errors.restype = ctypes.c_uint64
         _lib = L
     return _lib
 
@@ -153,6 +169,46 @@ class Gpt2Tok:
         return out[:n].tolist()
 
 
+class T5Tok:
+    """The t5 Precompiled + Unigram restatement (oracle/orc_unigram.c)."""
+
+    def __init__(self, path=T5_JSON, graphemes=T5_GRAPHEMES):
+        self.h = lib().orc_t5_load(path.encode(), graphemes.encode())
+        if not self.h:
+            raise RuntimeError("oracle t5 tokenizer load failed")
+        self.eos = lib().orc_t5_eos(self.h)
+
+    def _call(self, fn, text, cap_per_byte, dtype):
+        b = text.encode("utf-8") if isinstance(text, str) else bytes(text)
+        cap = cap_per_byte * len(b) + 8
+        while True:
+            out = np.zeros(cap, dtype)
+            n = fn(self.h, b, len(b), out.ctypes.data, out.size)
+            if n <= cap:
+                return out[:n]
+            cap = n
+
+    def encode(self, text):
+        return self._call(lib().orc_t5_encode, text, 2, np.uint32).tolist()
+
+    def normalize(self, text):
+        return self._call(lib().orc_t5_normalize, text, 4, np.uint8).tobytes().decode("utf-8")
+
+    def grapheme_starts(self, text):
+        return self._call(lib().orc_t5_graphemes, text, 1, np.uint32).tolist()
+
+    def special_id(self, s):
+        return lib().orc_t5_special_id(self.h, s.encode())
+
+
+def span_table(avg, lo, cap=32):
+    kmin = ctypes.c_int32()
+    n = ctypes.c_int32()
+    thr = np.zeros(cap, np.uint32)
+    lib().orc_span_table(avg, lo, ctypes.byref(kmin), ctypes.byref(n), thr.ctypes.data, cap)
+    return kmin.value, thr[:n.value].tolist()
+
+
 class Encoder:
     """An orc_encoder (tokenizer + encode_mask framing) in owned storage."""
 
@@ -163,6 +219,8 @@ class Encoder:
             lib().orc_encoder_bert(tok.h, self.buf)
         elif kind == "gpt2":
             lib().orc_encoder_gpt2(tok.h, self.buf)
+        elif kind == "t5":
+            lib().orc_encoder_t5(tok.h, self.buf)
         else:
             raise ValueError(kind)
 
@@ -173,10 +231,11 @@ class OracleBatcherEx:
     batch planes (copies) or None."""
 
     def __init__(self, encoder, task, B, S, mask_length=None, mask_id=103, number_labels=9, seed=0,
-                 chunk=None, min_ids=None):
+                 chunk=None, min_ids=None, avg_span_gap=16.0, avg_span_size=2.0):
         c = OrcCfg()
         lib().orc_cfg_default(ctypes.byref(c), task)
         c.B, c.S, c.mask_id, c.number_labels, c.seed = B, S, mask_id, number_labels, seed
+        c.avg_span_gap, c.avg_span_size = avg_span_gap, avg_span_size
         c.mask_length = int(np.float32(S) * np.float32(0.15)) if mask_length is None else mask_length
         if chunk is not None:
             c.chunk = 1 if chunk else 0
@@ -186,7 +245,7 @@ class OracleBatcherEx:
         self.h = lib().orc_batcher_create(encoder.buf, ctypes.byref(c))
         if not self.h:
             raise RuntimeError("oracle batcher config rejected")
-        LW = S if task in (MLM, CLM) else 0
+        LW = S if task in (MLM, CLM) else S // 4 if task == SPAN else 0
         self.planes = {"input_ids": np.zeros((B, S), np.int32), "attention_mask": np.zeros((B, S), np.int32),
                        "token_type_ids": np.zeros((B, S), np.int32), "labels": np.zeros((B, max(LW, 1)), np.int32),
                        "labels_f32": np.zeros((B, number_labels), np.float32)}
@@ -220,6 +279,9 @@ class OracleBatcherEx:
 
     def flush(self):
         return self._result() if lib().orc_batcher_flush_ex(self.h, ctypes.byref(self.out)) == 1 else None
+
+    def span_errors(self):
+        return int(lib().orc_batcher_span_errors(self.h))
 
     def __del__(self):
         if getattr(self, "h", None):
