@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define SDL_ABI_VERSION 2
+#define SDL_ABI_VERSION 3
 
 enum {
     SDL_OK = 0,
@@ -144,8 +144,13 @@ typedef struct sdl_device_rows {
     uint32_t *d_tokens;      /* device scalar: tokenizer ids produced (before framing) */
     uint64_t rows_capacity;
     int32_t label_width;
-    uint32_t *d_label_errors; /* device scalar (multi-label): Label::Multi indices >= number_labels
-                                 that were skipped (the reference panics on them) */
+    uint32_t *d_label_errors; /* device scalar: multi-label -- Label::Multi indices >= number_labels
+                                 that were skipped; span -- label writes past the S/4 label width or
+                                 sentinel indices >= 100 that were clamped (the reference panics on
+                                 both: bert_data.rs:70-72, t5_data.rs:205-216) */
+    uint32_t *d_tokenize_errors; /* device scalar (t5 tokenizer), 0 = ok; else bit 1: an item's ids
+                                    exceeded their scratch, 2: id pool full, 3: long-item list full,
+                                    4: a whitespace-free run longer than 256 KiB normalized (dropped) */
 } sdl_device_rows;
 
 int sdl_process_device(sdl_batcher *h, const uint8_t *d_text, uint64_t text_len,
@@ -170,6 +175,21 @@ int sdl_device_to_host(sdl_batcher *h, void *dst, const void *src, size_t bytes,
  * hipEvents on the stream the kernels ran on, when enabled. */
 int sdl_set_profiling(sdl_batcher *h, int enable);
 int sdl_stage_times(sdl_batcher *h, const char **names, float *ms, int cap);
+
+/* Loads and checks a tokenizer on the host only (no GPU needed): what
+ * sdl_batcher_create would accept.  kind: 0 WordPiece, 1 byte-level BPE,
+ * 2 Unigram (t5). */
+typedef struct sdl_tokenizer_info {
+    int32_t kind;
+    int32_t vocab_size;
+    int32_t n_added;            /* added tokens matched on the raw text */
+    int32_t unk_id;
+    int32_t eos_id;             /* </s> / <|endoftext|> (TokenizerInfo.eos), -1 if none */
+    int32_t max_piece_bytes;
+    uint64_t word_table_entries; /* device word-table / hash entries */
+    int32_t reserved[6];
+} sdl_tokenizer_info;
+int sdl_tokenizer_info_get(const char *tokenizer_path, const char *data_dir, sdl_tokenizer_info *out);
 
 /* Last error message of the calling thread. */
 const char *sdl_last_error(void);

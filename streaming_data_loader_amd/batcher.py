@@ -101,8 +101,8 @@ def get_case(task: TaskType, test: bool, sequence_length: int = 128, batch_size:
                               seed)
     if task == TaskType.Clm:  # masking_cases.rs:66: gpt2
         return TrainingConfig(ModelType.Gpt2, TokenizerConfig(native.GPT2_PROXY_TOKENIZER), batch, Gpt(), seed)
-    if task == TaskType.Span:
-        return TrainingConfig(ModelType.T5, TokenizerConfig(), batch, Span(16.0, 2.0), seed)
+    if task == TaskType.Span:  # masking_cases.rs:78-90: t5-small, Span{16.0, 2.0}
+        return TrainingConfig(ModelType.T5, TokenizerConfig(native.T5_PROXY_TOKENIZER), batch, Span(16.0, 2.0), seed)
     return TrainingConfig(ModelType.Bert, TokenizerConfig(), BatchConfig(2048 if batch_size is None else b,
                                                                         sequence_length), MultiLabel(9), seed)
 
@@ -125,8 +125,9 @@ class ProviderChannel:
 @dataclass
 class DataSet:
     """One batch; `to_dict()` is the reference's Serialize view
-    (bert_data.rs:106-145, gpt_data.rs:53-62).  `labels` is int32 [B, S] for
-    mlm/clm and float32 [B, number_labels] for multi-label."""
+    (bert_data.rs:106-145, gpt_data.rs:53-62, t5_data.rs:235-249).  `labels` is
+    int32 [B, S] for mlm/clm, int32 [B, S/4] for span and float32
+    [B, number_labels] for multi-label."""
     kind: str
     rows: int
     input_ids: np.ndarray

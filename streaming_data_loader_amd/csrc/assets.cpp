@@ -4,6 +4,7 @@
 #include "assets.hpp"
 
 #include <algorithm>
+#include <cmath>
 #include <array>
 #include <cstdio>
 #include <queue>
@@ -14,6 +15,7 @@
 #include <unordered_map>
 
 #include "json.hpp"
+#include "unigram.hpp"
 
 namespace sdl {
 
@@ -472,6 +474,304 @@ static void load_byte_bpe(const JValue &root, const std::string &data_dir, HostT
     load_gpt2_classes(data_dir + "/gpt2_classes.bin", t);
 }
 
+// ---------------------------------------------------------------------------
+// Unigram (t5-small): Precompiled normalizer + WhitespaceSplit + Metaspace +
+// Unigram model + "$A </s>" (hub tokenizer.json layout).
+// ---------------------------------------------------------------------------
+static std::vector<uint8_t> b64decode(const std::string &s) {
+    std::vector<uint8_t> o;
+    uint32_t acc = 0;
+    int bits = 0;
+    for (unsigned char c : s) {
+        int v = c >= 'A' && c <= 'Z' ? c - 'A' : c >= 'a' && c <= 'z' ? c - 'a' + 26 : c >= '0' && c <= '9' ? c - '0' + 52
+              : c == '+' ? 62 : c == '/' ? 63 : -1;
+        if (v < 0) continue;
+        acc = acc << 6 | (uint32_t)v;
+        bits += 6;
+        if (bits >= 8) {
+            bits -= 8;
+            o.push_back((uint8_t)(acc >> bits));
+        }
+    }
+    return o;
+}
+
+static VSlot make_slot(const std::string &pay, uint32_t cont, int32_t id, std::vector<uint8_t> &pool) {
+    VSlot v{};
+    v.key = (uint32_t)pay.size() | (cont << 8);
+    v.id = id;
+    v.pool_off = (uint32_t)pool.size();
+    v.hash = piece_hash((const uint8_t *)pay.data(), pay.size(), cont);
+    std::memcpy(v.inl, pay.data(), std::min<size_t>(16, pay.size()));
+    pool.insert(pool.end(), pay.begin(), pay.end());
+    return v;
+}
+
+static void build_cuckoo(HostTokenizer &t, const std::vector<VSlot> &entries) {
+    uint32_t slots = 1;
+    while (slots < 4 * entries.size()) slots <<= 1;
+    for (;; slots <<= 1) {
+        t.slot_mask = slots - 1;
+        t.slots.assign(slots, VSlot{0, -1, 0, 0, {0}});
+        bool ok = true;
+        for (const VSlot &v : entries)
+            if (!cuckoo_insert(t.slots, t.slot_mask, v)) { ok = false; break; }
+        if (ok) break;
+        if (slots >= (1u << 24)) throw std::runtime_error("cuckoo table build failed");
+    }
+}
+
+// host probe of the vocab table (same slots the kernels read)
+static int host_probe(const HostTokenizer &t, const uint8_t *pay, size_t n, uint32_t cont) {
+    const uint32_t h = piece_hash(pay, n, cont);
+    const uint32_t key = (uint32_t)n | (cont << 8);
+    for (uint32_t s : {cuckoo_slot1(h, t.slot_mask), cuckoo_slot2(h, t.slot_mask)}) {
+        const VSlot &v = t.slots[s];
+        if (v.id >= 0 && v.key == key && std::memcmp(&t.vpool[v.pool_off], pay, n) == 0) return v.id;
+    }
+    return -1;
+}
+
+static const uint8_t kMeta[3] = {0xE2, 0x96, 0x81};  // U+2581
+
+std::vector<int> unigram_encode_word(const HostTokenizer &t, const uint8_t *w, size_t n) {
+    std::vector<uint8_t> b(kMeta, kMeta + 3);
+    b.insert(b.end(), w, w + n);
+    auto acc = [&](int i) -> uint32_t { return b[(size_t)i]; };
+    auto probe = [&](int s, int e) -> int {
+        if (s == 0) return e >= 3 ? host_probe(t, b.data() + 3, (size_t)(e - 3), UC_META) : -1;
+        return host_probe(t, b.data() + s, (size_t)(e - s), UC_PIECE);
+    };
+    struct Nodes {
+        std::vector<UniNode> v;
+        void set(int i, double s, int st, int id) { v[(size_t)i] = UniNode{s, st, id}; }
+        double score(int i) const { return v[(size_t)i].score; }
+        int start(int i) const { return v[(size_t)i].start; }
+        int id(int i) const { return v[(size_t)i].id; }
+    } nodes{std::vector<UniNode>(b.size() + 1)};
+    std::vector<int> out;
+    const int k = unigram_viterbi(acc, (int)b.size(), probe, nodes, t.uscore.data(), t.unk_score, t.unk_id,
+                                  t.maxlen_piece, [&](int i, int id) {
+                                      if ((int)out.size() <= i) out.resize((size_t)i + 1);
+                                      out[(size_t)i] = id;
+                                  });
+    out.resize((size_t)k);
+    return out;
+}
+
+static void load_t5_props(const std::string &path, HostTokenizer &t) {
+    const std::string b = read_file(path);
+    if (b.size() < 16 || b.compare(0, 4, "SDLU") != 0) throw std::runtime_error("bad grapheme table " + path);
+    uint32_t ver, np, nb;
+    std::memcpy(&ver, &b[4], 4);
+    std::memcpy(&np, &b[8], 4);
+    std::memcpy(&nb, &b[12], 4);
+    if (ver != 1 || np != 0x110000 / 256 || b.size() != 16 + 2 * (size_t)np + 256 * (size_t)nb)
+        throw std::runtime_error("bad grapheme table " + path);
+    t.tpage.resize(np);
+    std::memcpy(t.tpage.data(), &b[16], 2 * (size_t)np);
+    t.tblock.assign(b.begin() + 16 + 2 * np, b.end());
+}
+
+static void load_unigram(const JValue &root, const std::string &data_dir, HostTokenizer &t) {
+    auto is_true = [](const JValue *v) { return v && v->kind == JValue::BOOL && v->b; };
+    const JValue *model = root.get("model");
+    if (is_true(model->get("byte_fallback"))) throw std::runtime_error("Unigram byte_fallback unsupported");
+    // normalizer: Precompiled (the hub t5 layout)
+    const JValue *norm = root.get("normalizer");
+    if (!norm || !norm->get("type") || !norm->get("type")->is_str("Precompiled") || !norm->get("precompiled_charsmap"))
+        throw std::runtime_error("Unigram: normalizer must be Precompiled (t5-small layout)");
+    // pre_tokenizer: Sequence[WhitespaceSplit, Metaspace("▁", prefix)]
+    const JValue *pre = root.get("pre_tokenizer");
+    const JValue *seq = pre ? pre->get("pretokenizers") : nullptr;
+    bool pre_ok = pre && pre->get("type") && pre->get("type")->is_str("Sequence") && seq && seq->kind == JValue::ARR &&
+                  seq->arr.size() == 2 && seq->arr[0].get("type") && seq->arr[0].get("type")->is_str("WhitespaceSplit") &&
+                  seq->arr[1].get("type") && seq->arr[1].get("type")->is_str("Metaspace");
+    if (pre_ok) {
+        const JValue &ms = seq->arr[1];
+        const JValue *rep = ms.get("replacement"), *aps = ms.get("add_prefix_space"), *ps = ms.get("prepend_scheme");
+        const JValue *split = ms.get("split");
+        pre_ok = rep && rep->is_str("\xe2\x96\x81") && (is_true(aps) || (ps && ps->is_str("always"))) &&
+                 (!split || is_true(split));
+    }
+    if (!pre_ok)
+        throw std::runtime_error("Unigram: pre_tokenizer must be Sequence[WhitespaceSplit, Metaspace(U+2581, prefix)]");
+    const JValue *vocab = model->get("vocab"), *unk = model->get("unk_id");
+    if (!vocab || vocab->kind != JValue::ARR || !unk || unk->kind != JValue::NUM)
+        throw std::runtime_error("Unigram: model.vocab / unk_id missing");
+    t.kind = TOK_UNIGRAM;
+    const size_t nv = vocab->arr.size();
+    if (nv > 65535) throw std::runtime_error("vocabulary larger than 65535 ids is not supported");
+    t.pieces.resize(nv);
+    t.uscore.resize(nv);
+    double min_score = INFINITY;
+    for (size_t i = 0; i < nv; ++i) {
+        const JValue &e = vocab->arr[i];
+        if (e.kind != JValue::ARR || e.arr.size() != 2 || e.arr[0].kind != JValue::STR || e.arr[1].kind != JValue::NUM)
+            throw std::runtime_error("Unigram: bad vocab entry");
+        t.pieces[i] = e.arr[0].str;
+        t.uscore[i] = e.arr[1].num;
+        min_score = std::min(min_score, t.uscore[i]);
+        t.maxlen_piece = std::max(t.maxlen_piece, (int)t.pieces[i].size());
+    }
+    t.unk_id = (int)unk->num;
+    if (t.unk_id < 0 || (size_t)t.unk_id >= nv) throw std::runtime_error("Unigram: unk_id out of range");
+    t.unk_score = min_score - 10.0;  // K_UNK_PENALTY
+    // added tokens: "<...>" with no other '<' / '>' inside (so a match ends at the first '>')
+    std::unordered_map<std::string, int> id_of;
+    for (size_t i = 0; i < nv; ++i) id_of[t.pieces[i]] = (int)i;  // HashMap: a duplicate keeps the last id
+    const JValue *added = root.get("added_tokens");
+    if (added && added->kind == JValue::ARR) {
+        for (auto &a : added->arr) {
+            const JValue *c = a.get("content"), *id = a.get("id");
+            if (!c || !id) continue;
+            if (is_true(a.get("lstrip")) || is_true(a.get("rstrip")) || is_true(a.get("single_word")) ||
+                is_true(a.get("normalized")))
+                throw std::runtime_error("added token options (normalized/lstrip/rstrip/single_word) unsupported");
+            const std::string &s = c->str;
+            if (s.size() < 2 || (int)s.size() > MAX_SPECIAL_LEN || s.front() != '<' || s.back() != '>' ||
+                s.find('<', 1) != std::string::npos || s.find('>') != s.size() - 1)
+                throw std::runtime_error("Unigram: added tokens must look like <...>");
+            t.added.emplace_back(s, (int)id->num);
+        }
+    }
+    // post_processor "$A </s>"
+    const JValue *pp = root.get("post_processor");
+    const JValue *single = pp ? pp->get("single") : nullptr;
+    if (!pp || !pp->get("type") || !pp->get("type")->is_str("TemplateProcessing") || !single ||
+        single->kind != JValue::ARR || single->arr.size() != 2 || !single->arr[0].get("Sequence") ||
+        !single->arr[1].get("SpecialToken"))
+        throw std::runtime_error("Unigram: post_processor must be TemplateProcessing \"$A </s>\"");
+    {
+        const std::string eos = single->arr[1].get("SpecialToken")->get("id")->str;
+        const JValue *spt = pp->get("special_tokens");
+        const JValue *ent = spt ? spt->get(eos) : nullptr;
+        const JValue *ids = ent ? ent->get("ids") : nullptr;
+        if (!ids || ids->kind != JValue::ARR || ids->arr.size() != 1)
+            throw std::runtime_error("Unigram: template special token must have one id");
+        t.tpl_eos = (int)ids->arr[0].num;
+    }
+    auto find_added = [&](const std::string &s) {
+        for (auto &a : t.added)
+            if (a.first == s) return a.second;
+        auto it = id_of.find(s);
+        return it == id_of.end() ? -1 : it->second;
+    };
+    t.eos_id = find_added("</s>");  // TokenizerInfo.eos (tokenizer_wrapper.rs:81-88)
+    t.pad_id = find_added("<pad>");
+    if (t.eos_id < 0) throw std::runtime_error("t5 tokenizer lacks </s>");
+    t.extra_ids.resize(100);
+    for (int k = 0; k < 100; ++k) {
+        t.extra_ids[(size_t)k] = find_added("<extra_id_" + std::to_string(k) + ">");
+        if (t.extra_ids[(size_t)k] < 0) throw std::runtime_error("t5 tokenizer lacks <extra_id_" + std::to_string(k) + ">");
+    }
+    // charsmap
+    const std::vector<uint8_t> cm = b64decode(norm->get("precompiled_charsmap")->str);
+    uint32_t tsize = 0;
+    if (cm.size() < 4) throw std::runtime_error("bad precompiled_charsmap");
+    std::memcpy(&tsize, cm.data(), 4);
+    if (tsize % 4 || 4 + (size_t)tsize > cm.size()) throw std::runtime_error("bad precompiled_charsmap");
+    t.trie.resize(tsize / 4);
+    std::memcpy(t.trie.data(), cm.data() + 4, tsize);
+    t.tnorm.assign(cm.begin() + 4 + tsize, cm.end());
+    t.tnorm.push_back(0);
+    load_t5_props(data_dir + "/t5_graphemes.bin", t);
+    // What the kernels assume of the charsmap (checked, else refused):
+    //  - printable ASCII bytes are not changed (a simple ASCII word is its own
+    //    normalization: each of its clusters is one ASCII char);
+    //  - \t \n \f \r map to non-empty whitespace and ' ' to itself (they separate words);
+    //  - no key starts with ' ' or with a Prepend char (a cluster across a word
+    //    edge then falls back to per-char lookups, so words normalize apart).
+    auto lookup = [&](const uint8_t *s, int n) {
+        return trie_shortest(t.trie.data(), (uint32_t)t.trie.size(), [&](int i) -> uint32_t { return s[i]; }, n);
+    };
+    auto norm_at = [&](int32_t off) { return std::string((const char *)&t.tnorm[(size_t)off]); };
+    for (uint32_t b = 0x21; b < 0x7F; ++b) {
+        const uint8_t c = (uint8_t)b;
+        const int32_t r = lookup(&c, 1);
+        if (r >= 0 && norm_at(r) != std::string(1, (char)b))
+            throw std::runtime_error("charsmap changes printable ASCII (unsupported by the kernels)");
+    }
+    for (uint8_t c : {(uint8_t)9, (uint8_t)10, (uint8_t)12, (uint8_t)13, (uint8_t)32}) {
+        const int32_t r = lookup(&c, 1);
+        std::string m = r >= 0 ? norm_at(r) : std::string(1, (char)c);
+        bool ws = !m.empty();
+        for (unsigned char x : m) ws = ws && (x == ' ' || (x >= 9 && x <= 13));
+        if (!ws) throw std::runtime_error("charsmap must keep ASCII whitespace whitespace");
+    }
+    {
+        // first bytes of every key: walk the root's children
+        const uint32_t root_pos = du_offset(t.trie[0]);
+        for (uint32_t c = 1; c < 256; ++c) {
+            const uint32_t p = root_pos ^ c;
+            if (p >= t.trie.size() || (t.trie[p] & ((1u << 31) | 0xFFu)) != c) continue;
+            if (c == 0x20) throw std::runtime_error("charsmap has a key starting with ' '");
+        }
+        // keys starting with a Prepend char: probe every Prepend code point's bytes as a key prefix
+        for (uint32_t cp = 0x80; cp < 0x110000; ++cp) {
+            if ((cp >= 0xD800 && cp < 0xE000) || (gprop(t.tpage.data(), t.tblock.data(), cp) & 15u) != GB_PREPEND) continue;
+            std::string u;
+            utf8_append(u, cp);
+            uint32_t pos = root_pos;
+            bool path = true;
+            for (unsigned char c : u) {
+                pos ^= c;
+                if (pos >= t.trie.size() || (t.trie[pos] & ((1u << 31) | 0xFFu)) != c) { path = false; break; }
+                pos ^= du_offset(t.trie[pos]);
+            }
+            if (path) throw std::runtime_error("charsmap has a key starting with a Prepend char");
+        }
+    }
+    // vocab table: pieces (UC_META "▁"+payload / UC_PIECE), added tokens, word table
+    std::vector<VSlot> entries;
+    t.vpool.clear();
+    t.maxlen_first = t.maxlen_cont = 0;
+    const std::string meta((const char *)kMeta, 3);
+    for (size_t i = 0; i < nv; ++i) {
+        const std::string &s = t.pieces[i];
+        if (s.empty() || id_of[s] != (int)i) continue;
+        const bool m = s.compare(0, 3, meta) == 0;
+        const std::string pay = m ? s.substr(3) : s;
+        if (pay.size() > 255) throw std::runtime_error("vocabulary piece longer than 255 bytes");
+        if (m) t.maxlen_cont = std::max(t.maxlen_cont, (int)pay.size());
+        else t.maxlen_first = std::max(t.maxlen_first, (int)pay.size());
+        entries.push_back(make_slot(pay, m ? UC_META : UC_PIECE, (int32_t)i, t.vpool));
+    }
+    for (auto &a : t.added) entries.push_back(make_slot(a.first, UC_ADDED, a.second, t.vpool));
+    t.max_special_len = 0;
+    for (auto &a : t.added) t.max_special_len = std::max(t.max_special_len, (int)a.first.size());
+    t.opener = t.added.empty() ? 0u : (uint32_t)'<';
+    build_cuckoo(t, entries);  // pieces first: the word table's Viterbi probes them
+    // word table: "▁w" vocab pieces with w printable ASCII -> Viterbi("▁w") ids
+    t.wres.clear();
+    int maxw = 0;
+    for (size_t i = 0; i < nv; ++i) {
+        const std::string &s = t.pieces[i];
+        if (s.size() <= 3 || s.compare(0, 3, meta) != 0 || id_of[s] != (int)i) continue;
+        const std::string w = s.substr(3);
+        bool ascii = w.size() <= 255;
+        for (unsigned char c : w) ascii = ascii && c >= 0x21 && c <= 0x7E;
+        if (!ascii) continue;
+        const std::vector<int> ids = unigram_encode_word(t, (const uint8_t *)w.data(), w.size());
+        if (ids.empty() || ids.size() > 127) continue;
+        int32_t packed;
+        if (ids.size() == 1) {
+            packed = (int32_t)((1u << 24) | (uint32_t)ids[0]);
+        } else {
+            packed = (int32_t)(((uint32_t)ids.size() << 24) | (uint32_t)t.wres.size());
+            for (int x : ids) t.wres.push_back((uint16_t)x);
+        }
+        entries.push_back(make_slot(w, UC_WORD, packed, t.vpool));
+        maxw = std::max(maxw, (int)w.size());
+    }
+    if (t.wres.size() >= (1u << 24)) throw std::runtime_error("word table too large");
+    t.wres.push_back(0);
+    t.word_table_entries = entries.size();
+    t.vpool.resize(t.vpool.size() + 64, 0);
+    build_cuckoo(t, entries);
+    t.max_word = maxw;
+}
+
 void load_tokenizer(const std::string &path, const std::string &data_dir, HostTokenizer &t) {
     const std::string body = read_file(path);
     const bool is_json = path.size() >= 5 && path.compare(path.size() - 5, 5, ".json") == 0;
@@ -480,6 +780,10 @@ void load_tokenizer(const std::string &path, const std::string &data_dir, HostTo
         const JValue *model = root.get("model");
         if (model && model->get("type") && model->get("type")->is_str("BPE")) {
             load_byte_bpe(root, data_dir, t);
+            return;
+        }
+        if (model && model->get("type") && model->get("type")->is_str("Unigram")) {
+            load_unigram(root, data_dir, t);
             return;
         }
         if (!model || !model->get("type") || !model->get("type")->is_str("WordPiece"))

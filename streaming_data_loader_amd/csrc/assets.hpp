@@ -42,7 +42,24 @@ struct HostTokenizer {
     std::vector<uint16_t> gpage;           // data/gpt2_classes.bin
     std::vector<uint8_t> gblock;
     size_t word_table_entries = 0;
+
+    // ---- Unigram (t5) ------------------------------------------------------
+    std::vector<double> uscore;            // id -> score
+    std::vector<uint16_t> wres;            // word-table results of > 1 id
+    std::vector<uint16_t> tpage;           // data/t5_graphemes.bin
+    std::vector<uint8_t> tblock;
+    std::vector<uint32_t> trie;            // Precompiled charsmap double array
+    std::vector<uint8_t> tnorm;            // ... normalized strings
+    double unk_score = 0.0;
+    int maxlen_piece = 0;                  // longest vocab piece (bytes)
+    int max_word = 0;                      // longest word-table word (bytes)
+    int tpl_eos = -1;                      // TemplateProcessing "$A </s>" id
+    std::vector<int> extra_ids;            // <extra_id_0..99>
 };
+
+// Unigram: ids of Viterbi("▁" + word) for an ASCII word, host side (same code
+// as the kernels, unigram.hpp); used to precompute the word table.
+std::vector<int> unigram_encode_word(const HostTokenizer &t, const uint8_t *w, size_t n);
 
 // HF BPE::merge_word over raw bytes (byte-level symbols), host side: used to
 // precompute the word table; same semantics as the device merge loop.

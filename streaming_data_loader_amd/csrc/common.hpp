@@ -85,7 +85,23 @@ constexpr uint32_t MERGE_NONE = 0xFFFFu;  // rank of a pair with no merge
 // GPT-2 regex classes of a code point (tools/make_gpt2_tables.py)
 enum : uint32_t { GC_O = 0, GC_L = 1, GC_N = 2, GC_W = 3 };
 
-enum : int32_t { TOK_WORDPIECE = 0, TOK_BYTE_BPE = 1 };
+enum : int32_t { TOK_WORDPIECE = 0, TOK_BYTE_BPE = 1, TOK_UNIGRAM = 2 };
+
+// ---- Unigram (t5) ------------------------------------------------------------
+// Vocab slot key cont values: 0 piece without "▁", 1 piece "▁"+payload,
+// 2 word-table entry (payload = an ASCII word, id field = packed Viterbi
+// result of "▁"+word: (k << 24) | x, x = the id when k == 1, else the offset
+// of its k ids in DevTok.wres), 3 added token (payload = its raw bytes).
+enum : uint32_t { UC_PIECE = 0, UC_META = 1, UC_WORD = 2, UC_ADDED = 3 };
+constexpr int UNI_STAGE = 2 * CHUNK + 128; // tokc entries per chunk (a 1-byte word can yield 2 ids)
+constexpr int UNI_WMAX = 24;        // longest word (bytes) the chunk kernel's Viterbi takes
+constexpr int UNI_NODES = UNI_WMAX + 4;
+constexpr int UNI_LANE_NORM = 1024; // normalized bytes per lane of the long-item kernel
+constexpr int UNI_HUGE_NORM = 1 << 18;  // ... per wave of the huge-item kernel
+// grapheme / whitespace properties (tools/make_t5_tables.py)
+enum : uint32_t { GB_OTHER = 0, GB_CR, GB_LF, GB_CONTROL, GB_EXTEND, GB_ZWJ, GB_RI, GB_PREPEND, GB_SPACING,
+                  GB_L, GB_V, GB_T, GB_LV, GB_LVT };
+constexpr uint32_t GP_EXTPICT = 0x10u, GP_WS = 0x80u;
 
 // Everything a tokenize kernel needs, passed by value as a kernel argument.
 struct DevTok {
@@ -114,6 +130,19 @@ struct DevTok {
     const MSlot *mslots;     // merge table
     const uint16_t *byte_id; // id of each single byte symbol
     uint32_t mslot_mask;
+    // Unigram (kind == TOK_UNIGRAM): slots/vpool hold pieces, word table and
+    // added tokens (UC_* cont values); specials are matched "<...>" by hash
+    const double *uscore;    // score of each id
+    const uint16_t *wres;    // word-table results with more than one id
+    const uint16_t *tpage;   // grapheme/whitespace property pages (0x110000/256)
+    const uint8_t *tblock;   // property blocks of 256 bytes
+    const uint32_t *trie;    // Precompiled charsmap: double-array units
+    const uint8_t *tnorm;    // ... and its NUL-separated normalized strings
+    uint32_t trie_units, tnorm_len;
+    double unk_score;        // min score - 10 (models/unigram/model.rs)
+    int32_t maxlen_meta;     // longest "▁"-piece payload (bytes)
+    int32_t maxlen_word;     // longest word-table payload
+    int32_t maxlen_piece;    // longest piece, "▁" included (bytes)
 };
 
 // Row assembly parameters (GenTokenizer + BertData/GptData/T5Data framing).
@@ -129,6 +158,11 @@ struct RowParams {
     int32_t post[MAX_FRAME];
     uint64_t seed;
     uint64_t first_record;
+    // span (T5Data): trunc(avg - z) draws as CDF tables (RNG contract) and
+    // the <extra_id_k> ids (device pointer, 100 entries)
+    int32_t gap_kmin, gap_n, size_kmin, size_n;
+    uint32_t gap_thr[32], size_thr[32];
+    const int32_t *extra_ids;
 };
 
 __host__ __device__ inline uint32_t ceil_div_u32(uint32_t a, uint32_t b) { return (a + b - 1) / b; }

@@ -34,6 +34,26 @@ hipError_t launch_bpe_chunks(const DevTok &T, const uint8_t *text, int64_t N, co
                              uint32_t *rec_local, uint32_t *long_count, BpeLong *long_list, uint32_t long_cap,
                              uint16_t *scratch, uint32_t *err, hipStream_t st);
 
+// tokenize_unigram.hip: t5 (Precompiled + Unigram).  Same chunk outputs as the
+// other tokenizers; long items (non-ASCII / long words) are finished by two
+// follow-up kernels into `pool` ([k, ids...] per item), their chunk entry
+// LONG_MARK | pool offset (k_compact_tokens expands it).
+struct UniWork {
+    uint32_t *counters;   // [0] long items [1] lchunks [2] pool words used [3] huge items
+    uint32_t *lchunks;    // chunks holding long items (n_chunks)
+    uint32_t *pool;
+    uint32_t pool_cap;
+    uint4 *huge;          // (chunk, entry, prel, len) of items past a lane's scratch
+    uint32_t huge_cap;
+    uint8_t *scratch;     // unigram_scratch_bytes(lane_blocks, huge_blocks)
+    int lane_blocks, huge_blocks;
+    uint32_t *err;        // bit 1 ids overflow, 2 pool, 3 huge list, 4 item too large
+};
+size_t unigram_scratch_bytes(int lane_blocks, int huge_blocks);
+hipError_t launch_unigram_chunks(const DevTok &T, const uint8_t *text, int64_t N, const uint64_t *off, int64_t R,
+                                 const uint32_t *ranges, uint32_t *tokc, uint32_t *chunk_cnt, uint32_t *chunk_ent,
+                                 uint32_t *rec_local, const UniWork &W, hipStream_t st);
+
 #ifdef SDL_STAMPS
 void print_phase_cycles();  // diagnostic builds only
 #endif
@@ -46,10 +66,12 @@ hipError_t launch_exclusive_scan(const uint32_t *in, uint32_t *out, int64_t n, u
 
 // long_count == null: no long-piece markers (WordPiece).  Else chunk_ent holds
 // each chunk's entry count (markers count 1; chunk_cnt counts ids).
+// long_pool != null (unigram): a marker's ids are long_pool[off + 1 ..], count long_pool[off].
 hipError_t launch_compact_tokens(const uint32_t *tokc, const uint32_t *chunk_cnt, const uint32_t *chunk_off,
                                  int64_t n_chunks, uint32_t *tok, const uint32_t *long_count,
                                  const uint32_t *chunk_ent, const BpeLong *long_list, const uint16_t *long_scratch,
-                                 hipStream_t st);
+                                 hipStream_t st, const uint32_t *long_pool = nullptr, int64_t stride = STAGE);
+
 
 // per record: token offset, token count, rows it yields (gen_batcher.rs:69-94)
 hipError_t launch_records(const RowParams &P, const uint64_t *off, int64_t R, int64_t N, const uint32_t *chunk_off,
@@ -73,5 +95,10 @@ hipError_t launch_rows(const RowParams &P, const uint32_t *tok, const uint32_t *
 hipError_t launch_multi_labels(const uint32_t *labels, const uint64_t *label_off, const uint32_t *row_rec,
                                const uint32_t *d_rows, int64_t rows_cap, int B, int NL, float *out, uint32_t *err,
                                hipStream_t st);
+
+// T5Data::put_data rows for task=span (models/t5_data.rs:162-226)
+hipError_t launch_rows_span(const RowParams &P, const uint32_t *tok, const uint32_t *rec_tok, const uint32_t *rec_cnt,
+                            const uint32_t *row_off, const uint32_t *row_rec, const uint32_t *d_rows, int64_t rows_cap,
+                            RowOut out, uint32_t *err, hipStream_t st);
 
 }  // namespace sdl

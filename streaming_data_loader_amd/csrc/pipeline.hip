@@ -129,11 +129,12 @@ __global__ __launch_bounds__(256) void k_compact_tokens(const uint32_t *__restri
                                                         uint32_t *__restrict__ tok, const uint32_t *long_count,
                                                         const uint32_t *__restrict__ chunk_ent,
                                                         const BpeLong *__restrict__ long_list,
-                                                        const uint16_t *__restrict__ long_scratch) {
+                                                        const uint16_t *__restrict__ long_scratch,
+                                                        const uint32_t *__restrict__ long_pool, int64_t stride) {
     const int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);  // one wave per chunk
     if (c >= n_chunks) return;
     const uint32_t n = chunk_cnt[c];
-    const uint32_t *src = tokc + c * STAGE;
+    const uint32_t *src = tokc + c * stride;
     uint32_t *dst = tok + chunk_off[c];
     const int lane = threadIdx.x & 63;
     if (!long_count || *long_count == 0) {
@@ -148,12 +149,15 @@ __global__ __launch_bounds__(256) void k_compact_tokens(const uint32_t *__restri
         const uint32_t e = e0 + lane;
         const uint32_t x = e < ne ? src[e] : 0u;
         const bool mark = (x & 0x80000000u) != 0u;
-        const uint32_t w = e >= ne ? 0u : mark ? long_list[x & 0x7FFFFFFFu].k : 1u;
+        const uint32_t w = e >= ne ? 0u : !mark ? 1u : long_pool ? long_pool[x & 0x7FFFFFFFu] : long_list[x & 0x7FFFFFFFu].k;
         const uint32_t incl = wave_incl_sum(w);
         const uint32_t at = written + incl - w;
         if (e < ne && at < n) {
             if (!mark) {
                 dst[at] = x;
+            } else if (long_pool) {  // unigram long item: [k, ids...] in the pool
+                const uint32_t o = x & 0x7FFFFFFFu;
+                for (uint32_t j = 0; j < w; ++j) dst[at + j] = long_pool[o + 1 + j];
             } else {
                 const BpeLong L = long_list[x & 0x7FFFFFFFu];
                 for (uint32_t j = 0; j < L.k; ++j) dst[at + j] = long_scratch[L.pos + j];
@@ -166,10 +170,10 @@ __global__ __launch_bounds__(256) void k_compact_tokens(const uint32_t *__restri
 hipError_t launch_compact_tokens(const uint32_t *tokc, const uint32_t *chunk_cnt, const uint32_t *chunk_off,
                                  int64_t n_chunks, uint32_t *tok, const uint32_t *long_count,
                                  const uint32_t *chunk_ent, const BpeLong *long_list, const uint16_t *long_scratch,
-                                 hipStream_t st) {
+                                 hipStream_t st, const uint32_t *long_pool, int64_t stride) {
     if (n_chunks == 0) return hipSuccess;
     hipLaunchKernelGGL(k_compact_tokens, dim3((unsigned)((n_chunks + 3) / 4)), dim3(256), 0, st, tokc, chunk_cnt,
-                       chunk_off, n_chunks, tok, long_count, chunk_ent, long_list, long_scratch);
+                       chunk_off, n_chunks, tok, long_count, chunk_ent, long_list, long_scratch, long_pool, stride);
     return hipGetLastError();
 }
 
@@ -451,6 +455,136 @@ hipError_t launch_rows(const RowParams &P, const uint32_t *tok, const uint32_t *
     else if (MR <= 8) SDL_ROWS(8);
     else return hipErrorInvalidValue;
 #undef SDL_ROWS
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// T5Data::put_data (models/t5_data.rs:162-226) for every row, task=span.
+// A row is one chunk of n <= S framed ids.  Pass p draws gap g_p and span size
+// s_p (RNG contract: Philox(p, chunk | 1 << 30, record; seed) words 0/1 through
+// the CDF tables).  Because the input cursor never passes the id cursor
+// (lp <= ip <= n <= S), the only clamp that binds is n - ip, and only in the
+// last pass P (the first whose g + s reaches n).  So lanes take passes: a wave
+// prefix sum gives every pass's id cursor I_p, input cursor lp_p = I_p - A_p + p
+// (A_p = ids spanned before p) and label cursor ap_p = A_p + p, and each lane
+// writes its pass's gap ids, sentinel and label run; rounds of 64 passes carry.
+// Labels past the S/4 label width (the reference panics) are skipped and
+// counted in *err; so is a sentinel index >= 100 (extra[99] is written).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t span_pick(int32_t kmin, int32_t n, const uint32_t (&thr)[32], uint32_t x) {
+    int32_t v = kmin;
+#pragma unroll
+    for (int j = 0; j < 32; ++j) v += (j < n && thr[j] <= x) ? 1 : 0;
+    return (uint32_t)v;
+}
+
+__global__ __launch_bounds__(256) void k_rows_span(RowParams P, const uint32_t *__restrict__ tok,
+                                                   const uint32_t *__restrict__ rec_tok,
+                                                   const uint32_t *__restrict__ rec_cnt,
+                                                   const uint32_t *__restrict__ row_off,
+                                                   const uint32_t *__restrict__ row_rec,
+                                                   const uint32_t *__restrict__ d_rows, int64_t rows_cap, RowOut out,
+                                                   uint32_t *__restrict__ err) {
+    const int lane = lane_id();
+    const int wid = (int)(threadIdx.x >> 6);
+    const int S = P.S, LW = P.label_width;
+    const uint32_t G = *d_rows;
+    int64_t Gpad = ((int64_t)G + P.B - 1) / P.B * P.B;
+    if (Gpad > rows_cap) Gpad = rows_cap;
+    for (int64_t g = (int64_t)blockIdx.x * 4 + wid; g < Gpad; g += (int64_t)gridDim.x * 4) {
+        int32_t *ids_o = out.input_ids + g * S;
+        int32_t *am_o = out.attention_mask + g * S;
+        int32_t *lb_o = out.labels + g * (int64_t)LW;
+        for (int j = lane; j < S; j += 64) am_o[j] = 1;  // attention stays 1 (the zeroing loop is empty)
+        if (g >= (int64_t)G) {
+            for (int j = lane; j < S; j += 64) ids_o[j] = 0;
+            for (int j = lane; j < LW; j += 64) lb_o[j] = -100;
+            continue;
+        }
+        const int64_t r = row_rec[g];
+        const uint32_t k = (uint32_t)(g - row_off[r]);
+        const uint32_t cnt = rec_cnt[r];
+        const uint32_t t0 = rec_tok[r];
+        const int64_t nf = (int64_t)cnt + P.n_pre + P.n_post;
+        const int64_t base = P.chunk ? (int64_t)k * S : 0;
+        const int n = (int)((nf - base) < S ? (nf - base) : S);
+        if (n <= 0) continue;  // (a row always holds >= 1 id)
+        auto fid = [&](int j) -> int32_t {  // framed id j of this chunk
+            const int64_t f = base + j;
+            if (f < P.n_pre) return frame_id(P.pre, (int)f);
+            if (f < P.n_pre + (int64_t)cnt) return (int32_t)tok[t0 + (f - P.n_pre)];
+            return frame_id(P.post, (int)(f - P.n_pre - cnt));
+        };
+        const uint64_t rec = P.first_record + (uint64_t)r;
+        uint32_t bad = 0;
+        auto extra = [&](uint32_t q) -> int32_t {
+            if (q >= 100u) { ++bad; q = 99u; }
+            return P.extra_ids[q];
+        };
+        auto setlab = [&](int64_t i, int32_t v) {
+            if (i < LW) lb_o[i] = v;
+            else ++bad;
+        };
+        int I0 = 0, A0 = 0;  // ids consumed / ids spanned before this round
+        int lp_end = 0, ap_end = 0;
+        for (uint32_t p0 = 0;; p0 += 64) {
+            const uint32_t p = p0 + (uint32_t)lane;
+            const uint4 c = philox4x32_10(make_uint4(p, k | 0x40000000u, (uint32_t)rec, (uint32_t)(rec >> 32)),
+                                          (uint32_t)P.seed, (uint32_t)(P.seed >> 32));
+            const uint32_t gr = span_pick(P.gap_kmin, P.gap_n, P.gap_thr, c.x);
+            const uint32_t sr = span_pick(P.size_kmin, P.size_n, P.size_thr, c.y);
+            // saturate so the prefix sums cannot wrap (any value >= n ends the row)
+            const uint32_t gs = gr > (uint32_t)n ? (uint32_t)n : gr, ss = sr > (uint32_t)n ? (uint32_t)n : sr;
+            const uint32_t step = gs + ss;
+            const uint32_t incl = wave_incl_sum(step), incl_s = wave_incl_sum(ss);
+            const int Ip = I0 + (int)(incl - step);            // id cursor at the start of pass p
+            const int Ap = A0 + (int)(incl_s - ss);            // ids spanned before p
+            const bool last = Ip + (int)step >= n && Ip < n;   // the pass where ip reaches n
+            const uint64_t lm = __ballot(last);
+            const int Pl = lm ? __builtin_ctzll(lm) : 64;      // lane of the last pass (64: none this round)
+            if (lane <= Pl) {  // passes up to and including the last one write
+                const int lp = Ip - Ap + (int)p;  // input cursor
+                const int ap = Ap + (int)p;       // label cursor
+                const int gg = lane == Pl ? ((int)gs < n - Ip ? (int)gs : n - Ip) : (int)gs;
+                for (int j = 0; j < gg; ++j) ids_o[lp + j] = fid(Ip + j);
+                const int ip1 = Ip + gg;
+                const int sz = lane == Pl ? ((int)ss < n - ip1 ? (int)ss : n - ip1) : (int)ss;
+                if (sz > 0) {
+                    const int32_t e = extra(p);
+                    ids_o[lp + gg] = e;
+                    setlab(ap, e);
+                    for (int j = 0; j < sz; ++j) setlab(ap + 1 + j, fid(ip1 + j));
+                }
+                if (lane == Pl) {
+                    lp_end = lp + gg + (sz > 0 ? 1 : 0);
+                    ap_end = ap + (sz > 0 ? sz + 1 : 0);
+                    setlab(ap_end, extra(p + 1));
+                }
+            }
+            if (Pl < 64) {
+                lp_end = __shfl(lp_end, Pl, 64);
+                ap_end = __shfl(ap_end, Pl, 64);
+                break;
+            }
+            I0 += (int)__shfl((int)incl, 63, 64);
+            A0 += (int)__shfl((int)incl_s, 63, 64);
+        }
+        for (int j = lp_end + lane; j < S; j += 64) ids_o[j] = 0;
+        for (int j = ap_end + 1 + lane; j < LW; j += 64) lb_o[j] = -100;
+        if (bad) atomicAdd(err, bad);
+    }
+}
+
+hipError_t launch_rows_span(const RowParams &P, const uint32_t *tok, const uint32_t *rec_tok, const uint32_t *rec_cnt,
+                            const uint32_t *row_off, const uint32_t *row_rec, const uint32_t *d_rows, int64_t rows_cap,
+                            RowOut out, uint32_t *err, hipStream_t st) {
+    if (rows_cap == 0) return hipSuccess;
+    const int64_t want = (rows_cap + 3) / 4;
+    const unsigned grid = (unsigned)(want < 4096 ? want : 4096);
+    hipError_t e = hipMemsetAsync(err, 0, sizeof(uint32_t), st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_rows_span, dim3(grid), dim3(256), 0, st, P, tok, rec_tok, rec_cnt, row_off, row_rec, d_rows,
+                       rows_cap, out, err);
     return hipGetLastError();
 }
 

@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <deque>
@@ -118,6 +119,12 @@ struct sdl_batcher {
     DevBuf<uint16_t> d_gpage, d_byte_id;
     DevBuf<uint8_t> d_gblock;
     DevBuf<MSlot> d_mslots;
+    // unigram (t5)
+    DevBuf<double> d_uscore;
+    DevBuf<uint16_t> d_wres, d_tpage;
+    DevBuf<uint8_t> d_tblock, d_tnorm;
+    DevBuf<uint32_t> d_trie;
+    DevBuf<int32_t> d_extra;
 
     // per-call workspace
     DevBuf<uint32_t> ranges, tokc, chunk_cnt, chunk_off, rec_local, tok_ids, rec_tok, rec_cnt, rec_rows, row_off,
@@ -129,6 +136,10 @@ struct sdl_batcher {
     DevBuf<uint32_t> long_count, bpe_err, chunk_ent;
     DevBuf<BpeLong> long_list;
     DevBuf<uint16_t> long_scratch;
+    // unigram long items
+    DevBuf<uint32_t> uni_counters, uni_lchunks, uni_pool, uni_err, span_err;
+    DevBuf<uint4> uni_huge;
+    DevBuf<uint8_t> uni_scratch;
     DevBuf<uint8_t> h2d_text;
     DevBuf<uint64_t> h2d_off, h2d_label_off;
     DevBuf<uint32_t> h2d_labels;
@@ -162,6 +173,7 @@ struct sdl_batcher {
     }
 
     bool multi() const { return P.task == SDL_TASK_MULTI_LABEL; }
+    bool span() const { return P.task == SDL_TASK_SPAN; }
     bool with_tt() const { return P.task == SDL_TASK_MLM || P.task == SDL_TASK_MULTI_LABEL; }
 
     HostBatch *new_batch() const { return new HostBatch(P.B, P.S, P.label_width, with_tt(), multi()); }
@@ -169,7 +181,9 @@ struct sdl_batcher {
     int64_t rows_capacity(int64_t N, int64_t R) const {
         // rows <= sum_r ceil((ids_r + frame) / S) with ids_r <= bytes_r
         const int64_t F = P.n_pre + P.n_post;
-        int64_t cap = P.chunk ? (N + R * (F + P.S - 1)) / P.S + 1 : R;
+        // ids <= bytes (WordPiece, BPE); Unigram: <= 2 * bytes + the pool slack
+        const int64_t ids = dt.kind == TOK_UNIGRAM ? 2 * N + 1024 * 1024 : N;
+        int64_t cap = P.chunk ? (ids + R * (F + P.S - 1)) / P.S + 1 : R;
         return (cap + P.B - 1) / P.B * P.B;
     }
 
@@ -178,11 +192,13 @@ struct sdl_batcher {
         const int64_t n_chunks = (N + CHUNK - 1) / CHUNK;
         const int64_t rows_cap = rows_capacity(N, R);
         ranges.ensure((size_t)std::max<int64_t>(n_chunks, 1) * 3);
-        tokc.ensure((size_t)std::max<int64_t>(n_chunks, 1) * STAGE);
+        tokc.ensure((size_t)std::max<int64_t>(n_chunks, 1) * (dt.kind == TOK_UNIGRAM ? UNI_STAGE : STAGE));
         chunk_cnt.ensure((size_t)n_chunks + 1);
         chunk_off.ensure((size_t)n_chunks + 1);
         rec_local.ensure((size_t)R + 1);
-        tok_ids.ensure((size_t)N + 1);
+        // ids <= text bytes for WordPiece/BPE; Unigram adds a "▁" piece per word
+        // and expanding normalizations: bound by the chunk entries + the pool
+        tok_ids.ensure(dt.kind == TOK_UNIGRAM ? (size_t)2 * N + 1024 * 1024 + 1 : (size_t)N + 1);
         rec_tok.ensure((size_t)R + 1);
         rec_cnt.ensure((size_t)R + 1);
         rec_rows.ensure((size_t)R + 1);
@@ -209,7 +225,23 @@ struct sdl_batcher {
         HIP_TRY(launch_chunk_ranges(d_off, R, N, ranges.p, st));
         mark(1);
         const bool bpe = dt.kind == TOK_BYTE_BPE;
-        if (bpe) {
+        const bool uni = dt.kind == TOK_UNIGRAM;
+        if (uni) {
+            // long items: at most one per raw word, words are >= 1 byte and
+            // separated, so <= (N + R) / 2 of them; their ids go to the pool
+            const int lane_blocks = 64, huge_blocks = 16;
+            uni_counters.ensure(4);
+            uni_err.ensure(1);
+            uni_lchunks.ensure((size_t)n_chunks + 1);
+            uni_huge.ensure((size_t)(N / 256 + 64));
+            uni_pool.ensure((size_t)N + 1024 * 1024);
+            uni_scratch.ensure(unigram_scratch_bytes(lane_blocks, huge_blocks));
+            chunk_ent.ensure((size_t)n_chunks + 1);
+            UniWork W{uni_counters.p, uni_lchunks.p, uni_pool.p, (uint32_t)std::min<size_t>(uni_pool.cap, 0x3FFFFFFF),
+                      uni_huge.p, (uint32_t)uni_huge.cap, uni_scratch.p, lane_blocks, huge_blocks, uni_err.p};
+            HIP_TRY(launch_unigram_chunks(dt, d_text, N, d_off, R, ranges.p, tokc.p, chunk_cnt.p, chunk_ent.p,
+                                          rec_local.p, W, st));
+        } else if (bpe) {
             // long pieces are > 64 bytes or run past their chunk's window (<= 1 per chunk)
             const uint32_t cap = (uint32_t)(N / 64 + n_chunks + 1);
             long_count.ensure(1);
@@ -225,9 +257,13 @@ struct sdl_batcher {
         mark(2);
         HIP_TRY(launch_exclusive_scan(chunk_cnt.p, chunk_off.p, n_chunks, scan_tmp.p, st));
         mark(3);
-        HIP_TRY(launch_compact_tokens(tokc.p, chunk_cnt.p, chunk_off.p, n_chunks, tok_ids.p,
-                                      bpe ? long_count.p : nullptr, bpe ? chunk_ent.p : nullptr,
-                                      bpe ? long_list.p : nullptr, bpe ? long_scratch.p : nullptr, st));
+        if (uni)
+            HIP_TRY(launch_compact_tokens(tokc.p, chunk_cnt.p, chunk_off.p, n_chunks, tok_ids.p, uni_counters.p,
+                                          chunk_ent.p, nullptr, nullptr, st, uni_pool.p, UNI_STAGE));
+        else
+            HIP_TRY(launch_compact_tokens(tokc.p, chunk_cnt.p, chunk_off.p, n_chunks, tok_ids.p,
+                                          bpe ? long_count.p : nullptr, bpe ? chunk_ent.p : nullptr,
+                                          bpe ? long_list.p : nullptr, bpe ? long_scratch.p : nullptr, st));
         mark(4);
         HIP_TRY(launch_records(p, d_off, R, N, chunk_off.p, n_chunks, rec_local.p, rec_tok.p, rec_cnt.p, rec_rows.p,
                                st));
@@ -237,7 +273,14 @@ struct sdl_batcher {
         mark(6);
         RowOut out{o_ids.p, o_am.p, with_tt() ? o_tt.p : nullptr, multi() ? nullptr : o_lab.p,
                    multi() ? o_f32.p : nullptr};
-        HIP_TRY(launch_rows(p, tok_ids.p, rec_tok.p, rec_cnt.p, row_off.p, row_rec.p, row_off.p + R, rows_cap, out, st));
+        if (span()) {
+            span_err.ensure(1);
+            HIP_TRY(launch_rows_span(p, tok_ids.p, rec_tok.p, rec_cnt.p, row_off.p, row_rec.p, row_off.p + R, rows_cap,
+                                     out, span_err.p, st));
+        } else {
+            HIP_TRY(launch_rows(p, tok_ids.p, rec_tok.p, rec_cnt.p, row_off.p, row_rec.p, row_off.p + R, rows_cap, out,
+                                st));
+        }
         if (multi()) {
             HIP_TRY(hipMemsetAsync(lab_err.p, 0, 4, st));
             HIP_TRY(launch_multi_labels(d_labels, d_label_off, row_rec.p, row_off.p + R, rows_cap, P.B, P.label_width,
@@ -340,6 +383,26 @@ void fill_batch(const sdl_batcher *h, HostBatch *b, sdl_batch *out) {
     (void)h;
 }
 
+// Span draws (RNG contract): v = trunc_sat(avg - z), z ~ N(0,1),
+// by CDF inversion on a 32-bit uniform -- thr[j] = floor(2^32 P(v <= kmin + j)),
+// P(v <= k) = erfc((avg - k - 1) / sqrt 2) / 2; `lo` folds smaller values in
+// (size: max(.., 1)).  oracle/orc_batcher.c:orc_span_table computes the same.
+void span_table(double avg, int lo, int32_t *kmin, int32_t *n, uint32_t *thr) {
+    double k0 = std::floor(avg - 10.0);
+    if (k0 < lo) k0 = lo;
+    if (k0 > 1e9) k0 = 1e9;
+    *kmin = (int32_t)k0;
+    int m = 0;
+    for (int j = 0; j < 32; ++j) {
+        const double cdf = 0.5 * std::erfc((avg - (k0 + j) - 1.0) / std::sqrt(2.0));
+        const double t = std::floor(cdf * 4294967296.0);
+        if (t >= 4294967296.0) break;
+        thr[m++] = (uint32_t)t;
+    }
+    *n = m;
+    for (int j = m; j < 32; ++j) thr[j] = 0xFFFFFFFFu;
+}
+
 std::string default_data_dir() {
     Dl_info info;
     if (dladdr((void *)&default_data_dir, &info) && info.dli_fname) {
@@ -377,8 +440,12 @@ void sdl_config_default(sdl_config *c, int32_t task) {
 int sdl_batcher_create(const sdl_config *cfg, const char *tokenizer_path, const char *data_dir, sdl_batcher **out) {
     if (!cfg || !tokenizer_path || !out) return fail(SDL_ERR_ARG, "null argument");
     *out = nullptr;
-    if (cfg->task != SDL_TASK_MLM && cfg->task != SDL_TASK_CLM && cfg->task != SDL_TASK_MULTI_LABEL)
-        return fail(SDL_ERR_UNSUPPORTED, "task not implemented in this build (mlm, clm, multi-label)");
+    if (cfg->task != SDL_TASK_MLM && cfg->task != SDL_TASK_CLM && cfg->task != SDL_TASK_MULTI_LABEL &&
+        cfg->task != SDL_TASK_SPAN)
+        return fail(SDL_ERR_UNSUPPORTED, "unknown task");
+    if (cfg->task == SDL_TASK_SPAN && (cfg->sequence_length < 4 || !(cfg->avg_span_gap == cfg->avg_span_gap) ||
+                                       !(cfg->avg_span_size == cfg->avg_span_size)))
+        return fail(SDL_ERR_ARG, "span needs sequence_length >= 4 and finite avg_span_gap / avg_span_size");
     if (cfg->task == SDL_TASK_MULTI_LABEL && (cfg->number_labels <= 0 || cfg->number_labels > 4096))
         return fail(SDL_ERR_ARG, "number_labels must be in [1, 4096]");
     if (cfg->batch_size <= 0 || cfg->sequence_length <= 0 || cfg->sequence_length > 2048)
@@ -430,6 +497,36 @@ int sdl_batcher_create(const sdl_config *cfg, const char *tokenizer_path, const 
             d.byte_id = h->d_byte_id.p;
             d.mslot_mask = t.mslot_mask;
         }
+        if (t.kind == TOK_UNIGRAM) {
+            h->d_uscore.ensure(t.uscore.size());
+            h->d_wres.ensure(t.wres.size());
+            h->d_tpage.ensure(t.tpage.size());
+            h->d_tblock.ensure(t.tblock.size());
+            h->d_trie.ensure(t.trie.size());
+            h->d_tnorm.ensure(t.tnorm.size());
+            h->d_extra.ensure(100);
+            HIP_TRY(hipMemcpy(h->d_uscore.p, t.uscore.data(), t.uscore.size() * 8, hipMemcpyHostToDevice));
+            HIP_TRY(hipMemcpy(h->d_wres.p, t.wres.data(), t.wres.size() * 2, hipMemcpyHostToDevice));
+            HIP_TRY(hipMemcpy(h->d_tpage.p, t.tpage.data(), t.tpage.size() * 2, hipMemcpyHostToDevice));
+            HIP_TRY(hipMemcpy(h->d_tblock.p, t.tblock.data(), t.tblock.size(), hipMemcpyHostToDevice));
+            HIP_TRY(hipMemcpy(h->d_trie.p, t.trie.data(), t.trie.size() * 4, hipMemcpyHostToDevice));
+            HIP_TRY(hipMemcpy(h->d_tnorm.p, t.tnorm.data(), t.tnorm.size(), hipMemcpyHostToDevice));
+            HIP_TRY(hipMemcpy(h->d_extra.p, t.extra_ids.data(), 100 * 4, hipMemcpyHostToDevice));
+            d.uscore = h->d_uscore.p;
+            d.wres = h->d_wres.p;
+            d.tpage = h->d_tpage.p;
+            d.tblock = h->d_tblock.p;
+            d.trie = h->d_trie.p;
+            d.tnorm = h->d_tnorm.p;
+            d.trie_units = (uint32_t)t.trie.size();
+            d.tnorm_len = (uint32_t)t.tnorm.size();
+            d.unk_score = t.unk_score;
+            d.maxlen_meta = t.maxlen_cont;
+            d.maxlen_word = t.max_word;
+            d.maxlen_piece = t.maxlen_piece;
+        }
+        if (cfg->task == SDL_TASK_SPAN && t.kind != TOK_UNIGRAM)
+            throw std::runtime_error("task span needs the t5 (Unigram) tokenizer: TokenizerInfo.extra (tokenizer_wrapper.rs:77-80)");
         d.ubmp = h->d_ubmp.p;
         d.upage = h->d_upage.p;
         d.uentry = h->d_uentry.p;
@@ -444,7 +541,7 @@ int sdl_batcher_create(const sdl_config *cfg, const char *tokenizer_path, const 
         d.n_special = (int)t.added.size();
         d.max_special_len = t.max_special_len;
         d.opener = t.opener;
-        for (size_t i = 0; i < t.added.size(); ++i) {
+        for (size_t i = 0; i < t.added.size() && t.kind != TOK_UNIGRAM; ++i) {
             d.special_id[i] = t.added[i].second;
             d.special_len[i] = (uint8_t)t.added[i].first.size();
             std::memcpy(d.special_bytes[i], t.added[i].first.data(), t.added[i].first.size());
@@ -457,13 +554,27 @@ int sdl_batcher_create(const sdl_config *cfg, const char *tokenizer_path, const 
         P.min_ids = cfg->min_ids;
         P.mask_length = cfg->mask_length;
         P.mask_id = cfg->mask_id;
-        P.label_width = cfg->task == SDL_TASK_MULTI_LABEL ? cfg->number_labels : cfg->sequence_length;
+        P.label_width = cfg->task == SDL_TASK_MULTI_LABEL ? cfg->number_labels
+                        : cfg->task == SDL_TASK_SPAN          ? cfg->sequence_length / 4  // t5_data.rs:44
+                                                              : cfg->sequence_length;
+        if (cfg->task == SDL_TASK_SPAN) {
+            span_table(cfg->avg_span_gap, 0, &P.gap_kmin, &P.gap_n, P.gap_thr);
+            span_table(cfg->avg_span_size, 1, &P.size_kmin, &P.size_n, P.size_thr);
+            P.extra_ids = h->d_extra.p;
+        }
         if (cfg->task == SDL_TASK_MULTI_LABEL) {  // SimpleBatcher: one row per record, no filter
             P.chunk = 0;
             P.min_ids = 0;
         }
         P.seed = cfg->seed;
-        if (t.kind == TOK_BYTE_BPE) {
+        if (t.kind == TOK_UNIGRAM) {
+            // encode_mask framing for T5 (tokenizer_wrapper.rs:125-131): [eos] + template($A </s>) + [eos]
+            P.n_pre = 1;
+            P.pre[0] = t.eos_id;
+            P.n_post = 2;
+            P.post[0] = t.tpl_eos;
+            P.post[1] = t.eos_id;
+        } else if (t.kind == TOK_BYTE_BPE) {
             // encode_mask framing for Gpt (tokenizer_wrapper.rs:118-124): [eos] + ids + [eos]
             P.n_pre = 1;
             P.pre[0] = t.eos_id;
@@ -604,7 +715,8 @@ int sdl_process_device_labels(sdl_batcher *h, const uint8_t *d_text, uint64_t te
         out->token_type_ids = h->with_tt() ? h->o_tt.p : nullptr;
         out->labels = h->multi() ? nullptr : h->o_lab.p;
         out->labels_f32 = h->multi() ? h->o_f32.p : nullptr;
-        out->d_label_errors = h->multi() ? h->lab_err.p : nullptr;
+        out->d_label_errors = h->multi() ? h->lab_err.p : h->span() ? h->span_err.p : nullptr;
+        out->d_tokenize_errors = h->dt.kind == TOK_UNIGRAM ? h->uni_err.p : nullptr;
         out->d_rows = h->row_off.p + n_records;
         out->d_record_rows = h->rec_rows.p;
         out->d_tokens = h->chunk_off.p + (text_len + CHUNK - 1) / CHUNK;
@@ -626,6 +738,27 @@ int sdl_device_to_host(sdl_batcher *h, void *dst, const void *src, size_t bytes,
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     if (e != hipSuccess) return fail(SDL_ERR_HIP, std::string("sdl_device_to_host: ") + hipGetErrorString(e));
     return SDL_OK;
+}
+
+int sdl_tokenizer_info_get(const char *tokenizer_path, const char *data_dir, sdl_tokenizer_info *out) {
+    if (!tokenizer_path || !out) return fail(SDL_ERR_ARG, "null argument");
+    try {
+        HostTokenizer t;
+        load_tokenizer(tokenizer_path, data_dir ? std::string(data_dir) : default_data_dir(), t);
+        std::memset(out, 0, sizeof(*out));
+        out->kind = t.kind;
+        out->vocab_size = (int32_t)t.pieces.size();
+        out->n_added = (int32_t)t.added.size();
+        out->unk_id = t.unk_id;
+        out->eos_id = t.eos_id;
+        int mx = 0;
+        for (auto &p : t.pieces) mx = std::max(mx, (int)p.size());
+        out->max_piece_bytes = mx;
+        out->word_table_entries = t.kind == TOK_WORDPIECE ? 0 : t.word_table_entries;
+        return SDL_OK;
+    } catch (std::exception &e) {
+        return fail(SDL_ERR_IO, e.what());
+    }
 }
 
 int sdl_set_profiling(sdl_batcher *h, int enable) {

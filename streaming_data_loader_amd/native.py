@@ -12,6 +12,7 @@ DATA_DIR = os.path.join(PKG, "data")
 ASSETS = os.path.join(PKG, "assets")
 BERT_PROXY_TOKENIZER = os.path.join(ASSETS, "bert_proxy", "tokenizer.json")
 GPT2_PROXY_TOKENIZER = os.path.join(ASSETS, "gpt2_proxy", "tokenizer.json")
+T5_PROXY_TOKENIZER = os.path.join(ASSETS, "t5_proxy", "tokenizer.json")
 
 SDL_TASK_MLM, SDL_TASK_CLM, SDL_TASK_SPAN, SDL_TASK_MULTI_LABEL = 0, 1, 2, 3
 
@@ -19,8 +20,8 @@ SDL_TASK_MLM, SDL_TASK_CLM, SDL_TASK_SPAN, SDL_TASK_MULTI_LABEL = 0, 1, 2, 3
 EXPORTS = [
     "sdl_config_default", "sdl_batcher_create", "sdl_batcher_destroy", "sdl_batcher_push",
     "sdl_batcher_push_many", "sdl_batcher_next", "sdl_batcher_flush", "sdl_batch_release",
-    "sdl_process_device", "sdl_process_device_labels", "sdl_device_to_host", "sdl_set_profiling", "sdl_stage_times", "sdl_last_error",
-    "sdl_abi_version",
+    "sdl_process_device", "sdl_process_device_labels", "sdl_device_to_host", "sdl_set_profiling", "sdl_stage_times",
+    "sdl_tokenizer_info_get", "sdl_last_error", "sdl_abi_version",
 ]
 
 
@@ -57,7 +58,15 @@ class DeviceRows(ctypes.Structure):
         ("labels", ctypes.c_void_p), ("labels_f32", ctypes.c_void_p), ("d_rows", ctypes.c_void_p),
         ("d_record_rows", ctypes.c_void_p), ("d_tokens", ctypes.c_void_p),
         ("rows_capacity", ctypes.c_uint64), ("label_width", ctypes.c_int32),
-        ("d_label_errors", ctypes.c_void_p),
+        ("d_label_errors", ctypes.c_void_p), ("d_tokenize_errors", ctypes.c_void_p),
+    ]
+
+
+class TokenizerInfo(ctypes.Structure):
+    _fields_ = [
+        ("kind", ctypes.c_int32), ("vocab_size", ctypes.c_int32), ("n_added", ctypes.c_int32),
+        ("unk_id", ctypes.c_int32), ("eos_id", ctypes.c_int32), ("max_piece_bytes", ctypes.c_int32),
+        ("word_table_entries", ctypes.c_uint64), ("reserved", ctypes.c_int32 * 6),
     ]
 
 
@@ -99,6 +108,8 @@ def load(path=LIB_PATH):
     L.sdl_last_error.restype = ctypes.c_char_p
     L.sdl_last_error.argtypes = []
     L.sdl_abi_version.restype = i64
+    L.sdl_tokenizer_info_get.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(TokenizerInfo)]
+    L.sdl_tokenizer_info_get.restype = i64
     for name in ("sdl_batcher_create", "sdl_batcher_push", "sdl_batcher_push_many", "sdl_batcher_next",
                  "sdl_batcher_flush", "sdl_process_device", "sdl_process_device_labels", "sdl_device_to_host", "sdl_set_profiling",
                  "sdl_stage_times"):
@@ -111,6 +122,13 @@ def check(rc):
     if rc < 0:
         raise SDLError(rc, load().sdl_last_error().decode(errors="replace"))
     return rc
+
+
+def tokenizer_info(path, data_dir=DATA_DIR):
+    """sdl_tokenizer_info_get: host-side load + checks of a tokenizer (no GPU)."""
+    info = TokenizerInfo()
+    check(load().sdl_tokenizer_info_get(path.encode(), data_dir.encode(), ctypes.byref(info)))
+    return info
 
 
 def default_config(task):

@@ -26,7 +26,7 @@ def test_header_and_exports_agree(native_lib):
 
 
 def test_abi_version(native_lib):
-    assert native_lib.sdl_abi_version() == 2
+    assert native_lib.sdl_abi_version() == 3
 
 
 def test_config_defaults_mirror_masking_cases(native_lib):
@@ -41,7 +41,8 @@ def test_config_defaults_mirror_masking_cases(native_lib):
 def test_struct_layouts():
     assert ctypes.sizeof(native.Config) == 96  # 8 x i32, 2 x f64, 2 x u64, i32 + 7 reserved
     assert ctypes.sizeof(native.Batch) == 4 * 4 + 8 * 6
-    assert ctypes.sizeof(native.DeviceRows) == 8 * 8 + 8 + 8 + 8
+    assert ctypes.sizeof(native.DeviceRows) == 8 * 8 + 8 + 8 + 8 + 8
+    assert ctypes.sizeof(native.TokenizerInfo) == 6 * 4 + 8 + 6 * 4
 
 
 def test_struct_layouts_match_header(tmp_path):
@@ -56,8 +57,9 @@ def test_struct_layouts_match_header(tmp_path):
 #include <stddef.h>
 #include "sdl_batcher.h"
 int main(void) {
-  printf("%zu %zu %zu %zu %zu %zu\\n", sizeof(sdl_config), sizeof(sdl_batch), sizeof(sdl_device_rows),
-         offsetof(sdl_config, seed), offsetof(sdl_batch, labels_f32), offsetof(sdl_device_rows, d_label_errors));
+  printf("%zu %zu %zu %zu %zu %zu %zu %zu\\n", sizeof(sdl_config), sizeof(sdl_batch), sizeof(sdl_device_rows),
+         offsetof(sdl_config, seed), offsetof(sdl_batch, labels_f32), offsetof(sdl_device_rows, d_label_errors),
+         offsetof(sdl_device_rows, d_tokenize_errors), sizeof(sdl_tokenizer_info));
   return 0;
 }
 """)
@@ -66,7 +68,8 @@ int main(void) {
     subprocess.run([cc, "-I", inc, str(src), "-o", str(exe)], check=True)
     got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
     assert got == [ctypes.sizeof(native.Config), ctypes.sizeof(native.Batch), ctypes.sizeof(native.DeviceRows),
-                   native.Config.seed.offset, native.Batch.labels_f32.offset, native.DeviceRows.d_label_errors.offset]
+                   native.Config.seed.offset, native.Batch.labels_f32.offset, native.DeviceRows.d_label_errors.offset,
+                   native.DeviceRows.d_tokenize_errors.offset, ctypes.sizeof(native.TokenizerInfo)]
 
 
 def test_create_without_gpu_fails_loudly(native_lib):
@@ -85,3 +88,25 @@ def test_create_without_gpu_fails_loudly(native_lib):
 def test_kernels_are_gfx950_code_objects(native_lib):
     data = open(native.LIB_PATH, "rb").read()
     assert b"gfx950" in data
+
+
+@pytest.mark.parametrize("path,kind", [(native.BERT_PROXY_TOKENIZER, 0), (native.GPT2_PROXY_TOKENIZER, 1),
+                                       (native.T5_PROXY_TOKENIZER, 2)])
+def test_tokenizer_info_host_only(native_lib, path, kind):
+    """The host loader accepts the three tokenizer layouts without a GPU."""
+    info = native.tokenizer_info(path)
+    assert info.kind == kind
+    if kind == 2:
+        assert info.vocab_size == 32100 and info.unk_id == 2 and info.eos_id == 1 and info.n_added == 103
+        assert info.word_table_entries > 32100
+
+
+def test_tokenizer_info_rejects_unsupported(native_lib, tmp_path):
+    import json
+    with open(native.T5_PROXY_TOKENIZER, encoding="utf-8") as f:
+        tj = json.load(f)
+    tj["pre_tokenizer"] = {"type": "Metaspace", "replacement": "\u2581", "add_prefix_space": True}
+    p = tmp_path / "t.json"
+    p.write_text(json.dumps(tj))
+    with pytest.raises(native.SDLError, match="WhitespaceSplit"):
+        native.tokenizer_info(str(p))
