@@ -17,6 +17,8 @@ communication.
   torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU)
 
 --task selects the other BASELINE configs (not the headline line):
+  span         configs[2]: t5 Unigram, seq_len=512, batch=256, T5Data span
+               corruption with the reference's Span{16.0, 2.0}
   clm          configs[3]: gpt2 byte-level BPE, seq_len=1024, batch=128
   multi-label  configs[4]: bert WordPiece, seq_len=128, batch=2048, Label::Multi
                indices per record (<= 4 of 9, seed 42); --e2e adds the Arrow
@@ -40,6 +42,8 @@ HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 TASKS = {
     "mlm": {"S": 512, "B": 256, "tok": "bert", "kernel": "k_wordpiece_chunks", "planes": 4,
             "workload": "mlm seq_len=512 batch=256 (BASELINE configs[1])"},
+    "span": {"S": 512, "B": 256, "tok": "t5", "kernel": "k_unigram_chunks", "planes": 2.25,
+             "workload": "span t5 Unigram seq_len=512 batch=256 (BASELINE configs[2]; reference Span{16.0, 2.0})"},
     "clm": {"S": 1024, "B": 128, "tok": "gpt2", "kernel": "k_bpe_chunks", "planes": 3,
             "workload": "clm gpt2 byte-BPE seq_len=1024 batch=128 (BASELINE configs[3])"},
     "multi-label": {"S": 128, "B": 2048, "tok": "bert", "kernel": "k_wordpiece_chunks", "planes": 3,
@@ -90,9 +94,12 @@ def _oracle_batcher(task, oracle_lib):
     t = TASKS[task]
     if t["tok"] == "gpt2":
         enc = oracle_lib.Encoder("gpt2", oracle_lib.Gpt2Tok())
+    elif t["tok"] == "t5":
+        enc = oracle_lib.Encoder("t5", oracle_lib.T5Tok())
     else:
         enc = oracle_lib.Encoder("bert", oracle_lib.Tok())
-    kind = {"mlm": oracle_lib.MLM, "clm": oracle_lib.CLM, "multi-label": oracle_lib.MULTI_LABEL}[task]
+    kind = {"mlm": oracle_lib.MLM, "clm": oracle_lib.CLM, "span": oracle_lib.SPAN,
+            "multi-label": oracle_lib.MULTI_LABEL}[task]
     return lambda: oracle_lib.OracleBatcherEx(enc, kind, t["B"], t["S"], seed=1234)
 
 
@@ -206,8 +213,10 @@ def main():
     text = torch.from_numpy(arena).to(dev)
     offsets = torch.from_numpy(offs.astype(np.int64)).to(dev)
     stream = torch.cuda.Stream(device=dev)
-    kind = {"mlm": native.SDL_TASK_MLM, "clm": native.SDL_TASK_CLM, "multi-label": native.SDL_TASK_MULTI_LABEL}
-    tok_path = native.GPT2_PROXY_TOKENIZER if task["tok"] == "gpt2" else native.BERT_PROXY_TOKENIZER
+    kind = {"mlm": native.SDL_TASK_MLM, "clm": native.SDL_TASK_CLM, "span": native.SDL_TASK_SPAN,
+            "multi-label": native.SDL_TASK_MULTI_LABEL}
+    tok_path = {"gpt2": native.GPT2_PROXY_TOKENIZER, "t5": native.T5_PROXY_TOKENIZER}.get(task["tok"],
+                                                                                          native.BERT_PROXY_TOKENIZER)
     db = DeviceBatcher(task=kind[args.task], batch_size=B, sequence_length=S, seed=1234, device=local,
                        tokenizer=tok_path)
     first_record = rank * 10_000_000  # disjoint global record indices per shard
@@ -266,7 +275,7 @@ def main():
     tok_bytes = N + 8 * (R + 1) + 4 * toks
     achieved = tok_bytes / (tok_ms * 1e-3) / 1e9
     # whole path, per step: text + offsets + the int32 [rows, S] planes
-    path_bytes = N + 8 * (R + 1) + 4 * task["planes"] * rows * S
+    path_bytes = N + 8 * (R + 1) + int(4 * task["planes"] * rows * S)
     line = {
         "metric": METRIC, "value": round(value, 2), "unit": "MB/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(step_ms, 4), "higher_is_better": True, "scaling": "weak",
@@ -275,8 +284,9 @@ def main():
                                "all packed batches",
                    "task": args.task, "seq_len": S, "batch": B, "arena_bytes_per_gpu": N, "records_per_gpu": R,
                    "rows_per_gpu": rows, "batches_per_gpu": -(-rows // B), "ids_per_gpu": toks,
-                   "tokenizer": ("gpt2 byte-level BPE layout, offline proxy vocab (50,257)" if task["tok"] == "gpt2"
-                                 else "bert-base-uncased layout, offline proxy vocab (30,522)"),
+                   "tokenizer": {"gpt2": "gpt2 byte-level BPE layout, offline proxy vocab (50,257)",
+                                 "t5": "t5-small layout (Precompiled nmt_nfkc + Unigram), offline proxy vocab (32,100)"}
+                                .get(task["tok"], "bert-base-uncased layout, offline proxy vocab (30,522)"),
                    "parallelism": f"record shards x{world}, no collective"},
         "roofline": {"bound": "hbm", "kernel": task["kernel"], "achieved": round(achieved, 2),
                      "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 5),
@@ -325,7 +335,8 @@ def end_to_end(task, records, order, nbytes=64 << 20, reps=2):
         run = lambda: [ds for b in batches for ds in sb.push_arrow(b)]  # noqa: E731
         path = "Arrow record batches -> SimpleBatcher.push_arrow (column buffers, pinned H2D, kernels, D2H)"
     else:
-        cfg = Bt.get_case(Bt.TaskType.Mlm if task == "mlm" else Bt.TaskType.Clm, False, t["S"], t["B"], 1234)
+        tt = {"mlm": Bt.TaskType.Mlm, "clm": Bt.TaskType.Clm, "span": Bt.TaskType.Span}[task]
+        cfg = Bt.get_case(tt, False, t["S"], t["B"], 1234)
         gt = Bt.GenTokenizer.from_config(cfg)
         blobs = [x.encode("utf-8") for x in texts]
         run = lambda: gt.create_sync_batches(blobs)  # noqa: E731

@@ -245,7 +245,8 @@ static int put_data(orc_batcher *b, obatch *x, const uint32_t *ids, size_t n, ui
                 ap += sz + 1;
             }
             if (n <= ip) { /* attention_mask untouched: the loop 0..ip-n is empty */
-                LAB(ap, EXTRA(pass + 1));
+                const int32_t e2 = EXTRA(pass + 1); /* Rust evaluates the right-hand side first */
+                LAB(ap, e2);
                 break;
             }
             pass++;
