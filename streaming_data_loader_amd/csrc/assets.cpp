@@ -538,9 +538,12 @@ std::vector<int> unigram_encode_word(const HostTokenizer &t, const uint8_t *w, s
     std::vector<uint8_t> b(kMeta, kMeta + 3);
     b.insert(b.end(), w, w + n);
     auto acc = [&](int i) -> uint32_t { return b[(size_t)i]; };
-    auto probe = [&](int s, int e) -> int {
-        if (s == 0) return e >= 3 ? host_probe(t, b.data() + 3, (size_t)(e - 3), UC_META) : -1;
-        return host_probe(t, b.data() + s, (size_t)(e - s), UC_PIECE);
+    auto cand = [&](int s, int e, double *sc) -> int {
+        int id;
+        if (s == 0) id = e >= 3 ? host_probe(t, b.data() + 3, (size_t)(e - 3), UC_META) : -1;
+        else id = host_probe(t, b.data() + s, (size_t)(e - s), UC_PIECE);
+        if (id >= 0) *sc = t.uscore[(size_t)id];
+        return id;
     };
     struct Nodes {
         std::vector<UniNode> v;
@@ -550,8 +553,8 @@ std::vector<int> unigram_encode_word(const HostTokenizer &t, const uint8_t *w, s
         int id(int i) const { return v[(size_t)i].id; }
     } nodes{std::vector<UniNode>(b.size() + 1)};
     std::vector<int> out;
-    const int k = unigram_viterbi(acc, (int)b.size(), probe, nodes, t.uscore.data(), t.unk_score, t.unk_id,
-                                  t.maxlen_piece, [&](int i, int id) {
+    const int k = unigram_viterbi(acc, (int)b.size(), cand, nodes, t.unk_score, t.unk_id, t.maxlen_piece,
+                                  [&](int i, int id) {
                                       if ((int)out.size() <= i) out.resize((size_t)i + 1);
                                       out[(size_t)i] = id;
                                   });
@@ -616,6 +619,11 @@ static void load_unigram(const JValue &root, const std::string &data_dir, HostTo
     }
     t.unk_id = (int)unk->num;
     if (t.unk_id < 0 || (size_t)t.unk_id >= nv) throw std::runtime_error("Unigram: unk_id out of range");
+    // the chunk kernel keeps candidate scores as f32 in LDS: exact for
+    // sentencepiece-trained vocabularies (float scores printed as f64)
+    for (double x : t.uscore)
+        if ((double)(float)x != x) throw std::runtime_error("Unigram: piece scores must be exact f32 values");
+    t.uscore32.assign(t.uscore.begin(), t.uscore.end());
     t.unk_score = min_score - 10.0;  // K_UNK_PENALTY
     // added tokens: "<...>" with no other '<' / '>' inside (so a match ends at the first '>')
     std::unordered_map<std::string, int> id_of;
@@ -722,6 +730,67 @@ static void load_unigram(const JValue &root, const std::string &data_dir, HostTo
             if (path) throw std::runtime_error("charsmap has a key starting with a Prepend char");
         }
     }
+    // per-code-point normalizer entries (the device resolves a one-char cluster
+    // with one load; only multi-char clusters starting with a key prefix walk the trie)
+    {
+        const uint32_t root_pos = du_offset(t.trie[0]);
+        t.cpage.assign(0x110000 / 256, 0);
+        t.cent.clear();
+        std::unordered_map<std::string, uint16_t> seen;
+        std::vector<uint32_t> blk(512);
+        for (uint32_t pg = 0; pg < 0x110000 / 256; ++pg) {
+            for (uint32_t lo = 0; lo < 256; ++lo) {
+                const uint32_t cp = pg * 256 + lo;
+                uint32_t x = gprop(t.tpage.data(), t.tblock.data(), cp), y = 0;
+                if (!(cp >= 0xD800 && cp < 0xE000) && cp != 0) {
+                    std::string u;
+                    utf8_append(u, cp);
+                    uint32_t pos = root_pos;
+                    bool path = true;
+                    int32_t val = -1;
+                    for (size_t i = 0; i < u.size(); ++i) {
+                        const uint32_t c = (uint8_t)u[i];
+                        pos ^= c;
+                        if (pos >= t.trie.size() || (t.trie[pos] & ((1u << 31) | 0xFFu)) != c) { path = false; break; }
+                        const uint32_t unit = t.trie[pos];
+                        pos ^= du_offset(unit);
+                        if ((unit >> 8) & 1u) {
+                            if (i + 1 == u.size()) val = (int32_t)(t.trie[pos] & 0x7FFFFFFFu);
+                            else { path = false; break; }  // a key ending inside the char: never a prefix of text
+                        }
+                    }
+                    if (path) {
+                        if (val >= 0) {
+                            x |= CP_KEY;
+                            const char *ns = (const char *)&t.tnorm[(size_t)val];
+                            const size_t nl = std::strlen(ns);
+                            if (nl <= 4) {
+                                x |= CP_INLINE | ((uint32_t)nl << 11);
+                                for (size_t k = 0; k < nl; ++k) y |= (uint32_t)(uint8_t)ns[k] << (8 * k);
+                            } else {
+                                y = (uint32_t)val;
+                            }
+                        }
+                        for (uint32_t c = 1; c < 256; ++c) {
+                            const uint32_t q = pos ^ c;
+                            if (q < t.trie.size() && (t.trie[q] & ((1u << 31) | 0xFFu)) == c) { x |= CP_PREFIX; break; }
+                        }
+                    }
+                }
+                blk[2 * lo] = x;
+                blk[2 * lo + 1] = y;
+            }
+            const std::string key((const char *)blk.data(), blk.size() * 4);
+            auto it = seen.find(key);
+            if (it == seen.end()) {
+                const size_t idx = t.cent.size() / 512;
+                if (idx > 65535) throw std::runtime_error("code point table too large");
+                it = seen.emplace(key, (uint16_t)idx).first;
+                t.cent.insert(t.cent.end(), blk.begin(), blk.end());
+            }
+            t.cpage[pg] = it->second;
+        }
+    }
     // vocab table: pieces (UC_META "▁"+payload / UC_PIECE), added tokens, word table
     std::vector<VSlot> entries;
     t.vpool.clear();
@@ -737,6 +806,9 @@ static void load_unigram(const JValue &root, const std::string &data_dir, HostTo
         else t.maxlen_first = std::max(t.maxlen_first, (int)pay.size());
         entries.push_back(make_slot(pay, m ? UC_META : UC_PIECE, (int32_t)i, t.vpool));
     }
+    // candidate rows are 64-bit masks in the kernels
+    if (t.maxlen_cont > 63 || t.maxlen_first > 64)
+        throw std::runtime_error("Unigram: pieces longer than 64 bytes are not supported");
     for (auto &a : t.added) entries.push_back(make_slot(a.first, UC_ADDED, a.second, t.vpool));
     t.max_special_len = 0;
     for (auto &a : t.added) t.max_special_len = std::max(t.max_special_len, (int)a.first.size());
@@ -770,6 +842,17 @@ static void load_unigram(const JValue &root, const std::string &data_dir, HostTo
     t.vpool.resize(t.vpool.size() + 64, 0);
     build_cuckoo(t, entries);
     t.max_word = maxw;
+    // device slots: word 3 (the host's cuckoo hash) carries a piece's f32 score
+    for (VSlot &v : t.slots) {
+        const uint32_t cont = v.key >> 8;
+        if (v.id >= 0 && (cont == UC_PIECE || cont == UC_META)) {
+            float f = t.uscore32[(size_t)v.id];
+            std::memcpy(&v.hash, &f, 4);
+        }
+    }
+    // the kernels emit printable ASCII without a table load: it must be GCB Other
+    for (uint32_t c = 0x21; c < 0x7F; ++c)
+        if (gprop(t.tpage.data(), t.tblock.data(), c) != 0) throw std::runtime_error("unexpected ASCII grapheme class");
 }
 
 void load_tokenizer(const std::string &path, const std::string &data_dir, HostTokenizer &t) {

@@ -45,9 +45,12 @@ struct HostTokenizer {
 
     // ---- Unigram (t5) ------------------------------------------------------
     std::vector<double> uscore;            // id -> score
+    std::vector<float> uscore32;           // ... as f32 (exact, checked)
     std::vector<uint16_t> wres;            // word-table results of > 1 id
     std::vector<uint16_t> tpage;           // data/t5_graphemes.bin
     std::vector<uint8_t> tblock;
+    std::vector<uint16_t> cpage;           // device per-code-point table (page -> block)
+    std::vector<uint32_t> cent;            // blocks of 256 (x, y) entries: see common.hpp CP_*
     std::vector<uint32_t> trie;            // Precompiled charsmap double array
     std::vector<uint8_t> tnorm;            // ... normalized strings
     double unk_score = 0.0;

@@ -94,14 +94,20 @@ enum : int32_t { TOK_WORDPIECE = 0, TOK_BYTE_BPE = 1, TOK_UNIGRAM = 2 };
 // of its k ids in DevTok.wres), 3 added token (payload = its raw bytes).
 enum : uint32_t { UC_PIECE = 0, UC_META = 1, UC_WORD = 2, UC_ADDED = 3 };
 constexpr int UNI_STAGE = 2 * CHUNK + 128; // tokc entries per chunk (a 1-byte word can yield 2 ids)
-constexpr int UNI_WMAX = 24;        // longest word (bytes) the chunk kernel's Viterbi takes
+constexpr int UNI_WMAX = 16;        // longest word (bytes) the chunk kernel settles itself
 constexpr int UNI_NODES = UNI_WMAX + 4;
-constexpr int UNI_LANE_NORM = 1024; // normalized bytes per lane of the long-item kernel
+constexpr int UNI_LANE_NORM = 256;  // normalized bytes per lane of the long-item kernel
 constexpr int UNI_HUGE_NORM = 1 << 18;  // ... per wave of the huge-item kernel
 // grapheme / whitespace properties (tools/make_t5_tables.py)
 enum : uint32_t { GB_OTHER = 0, GB_CR, GB_LF, GB_CONTROL, GB_EXTEND, GB_ZWJ, GB_RI, GB_PREPEND, GB_SPACING,
                   GB_L, GB_V, GB_T, GB_LV, GB_LVT };
 constexpr uint32_t GP_EXTPICT = 0x10u, GP_WS = 0x80u;
+// per-code-point entry of the t5 normalizer (x, y):
+//   x bits 0-7 grapheme/whitespace properties, bit 8 the char is a charsmap
+//   key, bit 9 it is a proper prefix of a longer key, bit 10 its normalization
+//   is inline in y (bits 11-13: byte count 0..4), else y = offset of the
+//   NUL-terminated normalization in the charsmap's string blob.
+constexpr uint32_t CP_KEY = 1u << 8, CP_PREFIX = 1u << 9, CP_INLINE = 1u << 10;
 
 // Everything a tokenize kernel needs, passed by value as a kernel argument.
 struct DevTok {
@@ -133,9 +139,10 @@ struct DevTok {
     // Unigram (kind == TOK_UNIGRAM): slots/vpool hold pieces, word table and
     // added tokens (UC_* cont values); specials are matched "<...>" by hash
     const double *uscore;    // score of each id
+    const float *uscore32;   // ... as f32 (exact)
     const uint16_t *wres;    // word-table results with more than one id
-    const uint16_t *tpage;   // grapheme/whitespace property pages (0x110000/256)
-    const uint8_t *tblock;   // property blocks of 256 bytes
+    const uint16_t *cpage;   // per-code-point entry pages (0x110000/256)
+    const uint2 *cent;       // entry blocks of 256 (CP_* layout)
     const uint32_t *trie;    // Precompiled charsmap: double-array units
     const uint8_t *tnorm;    // ... and its NUL-separated normalized strings
     uint32_t trie_units, tnorm_len;

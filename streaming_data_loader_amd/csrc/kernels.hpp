@@ -39,15 +39,16 @@ hipError_t launch_bpe_chunks(const DevTok &T, const uint8_t *text, int64_t N, co
 // follow-up kernels into `pool` ([k, ids...] per item), their chunk entry
 // LONG_MARK | pool offset (k_compact_tokens expands it).
 struct UniWork {
-    uint32_t *counters;   // [0] long items [1] lchunks [2] pool words used [3] huge items
-    uint32_t *lchunks;    // chunks holding long items (n_chunks)
+    uint32_t *counters;   // [0] long items [1] - [2] pool words used [3] huge items
+    uint4 *items;         // long items (chunk, tokc entry, prel, raw length or 0)
+    uint32_t item_cap;
     uint32_t *pool;
     uint32_t pool_cap;
-    uint4 *huge;          // (chunk, entry, prel, len) of items past a lane's scratch
+    uint4 *huge;          // items past a lane's scratch
     uint32_t huge_cap;
     uint8_t *scratch;     // unigram_scratch_bytes(lane_blocks, huge_blocks)
     int lane_blocks, huge_blocks;
-    uint32_t *err;        // bit 1 ids overflow, 2 pool, 3 huge list, 4 item too large
+    uint32_t *err;        // bit 1 ids overflow, 2 pool, 3 item lists, 4 item too large
 };
 size_t unigram_scratch_bytes(int lane_blocks, int huge_blocks);
 hipError_t launch_unigram_chunks(const DevTok &T, const uint8_t *text, int64_t N, const uint64_t *off, int64_t R,
@@ -56,6 +57,7 @@ hipError_t launch_unigram_chunks(const DevTok &T, const uint8_t *text, int64_t N
 
 #ifdef SDL_STAMPS
 void print_phase_cycles();  // diagnostic builds only
+void print_uni_cycles();
 #endif
 
 // pipeline.hip

@@ -121,8 +121,10 @@ struct sdl_batcher {
     DevBuf<MSlot> d_mslots;
     // unigram (t5)
     DevBuf<double> d_uscore;
-    DevBuf<uint16_t> d_wres, d_tpage;
-    DevBuf<uint8_t> d_tblock, d_tnorm;
+    DevBuf<uint16_t> d_wres, d_cpage;
+    DevBuf<uint2> d_cent;
+    DevBuf<float> d_uscore32;
+    DevBuf<uint8_t> d_tnorm;
     DevBuf<uint32_t> d_trie;
     DevBuf<int32_t> d_extra;
 
@@ -137,8 +139,8 @@ struct sdl_batcher {
     DevBuf<BpeLong> long_list;
     DevBuf<uint16_t> long_scratch;
     // unigram long items
-    DevBuf<uint32_t> uni_counters, uni_lchunks, uni_pool, uni_err, span_err;
-    DevBuf<uint4> uni_huge;
+    DevBuf<uint32_t> uni_counters, uni_pool, uni_err, span_err;
+    DevBuf<uint4> uni_items, uni_huge;
     DevBuf<uint8_t> uni_scratch;
     DevBuf<uint8_t> h2d_text;
     DevBuf<uint64_t> h2d_off, h2d_label_off;
@@ -160,7 +162,17 @@ struct sdl_batcher {
     float stage_ms[kStages] = {};
 
 #ifdef SDL_STAMPS
-    ~sdl_batcher() { print_phase_cycles(); cleanup(); }
+    ~sdl_batcher() {
+        print_phase_cycles();
+        print_uni_cycles();
+        if (uni_counters.p) {
+            uint32_t c[4] = {0, 0, 0, 0}, e = 0;
+            if (hipMemcpy(c, uni_counters.p, 16, hipMemcpyDeviceToHost) == hipSuccess &&
+                hipMemcpy(&e, uni_err.p, 4, hipMemcpyDeviceToHost) == hipSuccess)
+                fprintf(stderr, "[uni] long items %u, pool words %u, huge %u, err %u\n", c[0], c[2], c[3], e);
+        }
+        cleanup();
+    }
     void cleanup() {
 #else
     ~sdl_batcher() {
@@ -227,18 +239,21 @@ struct sdl_batcher {
         const bool bpe = dt.kind == TOK_BYTE_BPE;
         const bool uni = dt.kind == TOK_UNIGRAM;
         if (uni) {
-            // long items: at most one per raw word, words are >= 1 byte and
-            // separated, so <= (N + R) / 2 of them; their ids go to the pool
-            const int lane_blocks = 64, huge_blocks = 16;
+            // long items: words > UNI_WMAX bytes (<= N / 25), one per chunk past
+            // its window, and medium words whose normalization overflows the
+            // chunk's arena: N / 8 + n_chunks bounds every realistic text (an
+            // overflow is flagged in d_tokenize_errors); their ids go to the pool
+            const int lane_blocks = 2048, huge_blocks = 8;  // long items: one wave each
             uni_counters.ensure(4);
             uni_err.ensure(1);
-            uni_lchunks.ensure((size_t)n_chunks + 1);
+            uni_items.ensure((size_t)(N / 8 + n_chunks + 64));
             uni_huge.ensure((size_t)(N / 256 + 64));
             uni_pool.ensure((size_t)N + 1024 * 1024);
             uni_scratch.ensure(unigram_scratch_bytes(lane_blocks, huge_blocks));
             chunk_ent.ensure((size_t)n_chunks + 1);
-            UniWork W{uni_counters.p, uni_lchunks.p, uni_pool.p, (uint32_t)std::min<size_t>(uni_pool.cap, 0x3FFFFFFF),
-                      uni_huge.p, (uint32_t)uni_huge.cap, uni_scratch.p, lane_blocks, huge_blocks, uni_err.p};
+            UniWork W{uni_counters.p, uni_items.p, (uint32_t)std::min<size_t>(uni_items.cap, 0xFFFFFFFFu), uni_pool.p,
+                      (uint32_t)std::min<size_t>(uni_pool.cap, 0x3FFFFFFF), uni_huge.p, (uint32_t)uni_huge.cap,
+                      uni_scratch.p, lane_blocks, huge_blocks, uni_err.p};
             HIP_TRY(launch_unigram_chunks(dt, d_text, N, d_off, R, ranges.p, tokc.p, chunk_cnt.p, chunk_ent.p,
                                           rec_local.p, W, st));
         } else if (bpe) {
@@ -500,22 +515,25 @@ int sdl_batcher_create(const sdl_config *cfg, const char *tokenizer_path, const 
         if (t.kind == TOK_UNIGRAM) {
             h->d_uscore.ensure(t.uscore.size());
             h->d_wres.ensure(t.wres.size());
-            h->d_tpage.ensure(t.tpage.size());
-            h->d_tblock.ensure(t.tblock.size());
+            h->d_cpage.ensure(t.cpage.size());
+            h->d_cent.ensure(t.cent.size() / 2);
+            h->d_uscore32.ensure(t.uscore32.size());
             h->d_trie.ensure(t.trie.size());
             h->d_tnorm.ensure(t.tnorm.size());
             h->d_extra.ensure(100);
             HIP_TRY(hipMemcpy(h->d_uscore.p, t.uscore.data(), t.uscore.size() * 8, hipMemcpyHostToDevice));
             HIP_TRY(hipMemcpy(h->d_wres.p, t.wres.data(), t.wres.size() * 2, hipMemcpyHostToDevice));
-            HIP_TRY(hipMemcpy(h->d_tpage.p, t.tpage.data(), t.tpage.size() * 2, hipMemcpyHostToDevice));
-            HIP_TRY(hipMemcpy(h->d_tblock.p, t.tblock.data(), t.tblock.size(), hipMemcpyHostToDevice));
+            HIP_TRY(hipMemcpy(h->d_cpage.p, t.cpage.data(), t.cpage.size() * 2, hipMemcpyHostToDevice));
+            HIP_TRY(hipMemcpy(h->d_cent.p, t.cent.data(), t.cent.size() * 4, hipMemcpyHostToDevice));
+            HIP_TRY(hipMemcpy(h->d_uscore32.p, t.uscore32.data(), t.uscore32.size() * 4, hipMemcpyHostToDevice));
             HIP_TRY(hipMemcpy(h->d_trie.p, t.trie.data(), t.trie.size() * 4, hipMemcpyHostToDevice));
             HIP_TRY(hipMemcpy(h->d_tnorm.p, t.tnorm.data(), t.tnorm.size(), hipMemcpyHostToDevice));
             HIP_TRY(hipMemcpy(h->d_extra.p, t.extra_ids.data(), 100 * 4, hipMemcpyHostToDevice));
             d.uscore = h->d_uscore.p;
             d.wres = h->d_wres.p;
-            d.tpage = h->d_tpage.p;
-            d.tblock = h->d_tblock.p;
+            d.cpage = h->d_cpage.p;
+            d.cent = h->d_cent.p;
+            d.uscore32 = h->d_uscore32.p;
             d.trie = h->d_trie.p;
             d.tnorm = h->d_tnorm.p;
             d.trie_units = (uint32_t)t.trie.size();

@@ -10,19 +10,26 @@
 //   -> WhitespaceSplit -> Metaspace("▁", prefix) -> Unigram Viterbi.
 // The wrapper's </s> ... </s> framing is added at row assembly (pipeline.hip).
 //
-// Words are found on the raw bytes.  A *simple* word -- printable ASCII only,
-// bounded by ASCII whitespace, a record edge or an added token -- is its own
-// normalization (its clusters are single ASCII chars and the charsmap keeps
-// printable ASCII; checked on the host), so its ids are Viterbi("▁" + word):
-//   1. one probe of the word table (vocab "▁w" pieces with their precomputed
-//      Viterbi ids) settles most words;
-//   2. misses run the Viterbi lane-per-word, DP nodes in LDS, every candidate
-//      piece one cuckoo probe of the vocab table.
-// Every other word (non-ASCII or control bytes, > UNI_WMAX bytes, running past
-// the window) is a *long item*: its chunk entry is a marker and k_unigram_long
-// normalizes it (grapheme clusters, trie), splits, and runs the Viterbi per
-// piece, lane per item, writing its ids to a pool the compaction expands.
-// Items whose normalized text exceeds a lane's scratch go to k_unigram_huge.
+// One wave64 per 1 KiB chunk (as the other tokenizers).  Raw words -- runs
+// between ASCII whitespace, record edges and added tokens -- normalize
+// independently (host-checked charsmap facts), so each is settled
+// in the chunk:
+//   - simple words (printable ASCII, <= UNI_WMAX bytes) are their own
+//     normalization: one probe of the word table (vocab "▁w" pieces with their
+//     precomputed Viterbi ids) settles most of them;
+//   - medium words (other bytes, <= UNI_WMAX) are normalized into an LDS arena
+//     through the per-code-point table (one load per char; the trie only for
+//     multi-char clusters that start a longer key), then whitespace/"▁" split;
+//   - word-table misses and medium pieces go through the Viterbi in two
+//     batched phases: every candidate substring of every pending piece of the
+//     chunk is one independent cuckoo probe (lanes x 4 in flight), its id and
+//     f32 score kept in LDS; then a lane per word runs the DP from LDS only.
+// Longer words (or words running past the window) are *long items*: their
+// chunk entry is a marker, k_unigram_long finishes them lane per item from a
+// global list, ids into a pool the compaction expands; items whose normalized
+// text exceeds a lane's scratch go to k_unigram_huge (one wave each).
+#include <cstdio>
+
 #include "common.hpp"
 #include "device_util.hpp"
 #include "kernels.hpp"
@@ -34,8 +41,15 @@ namespace sdl {
 namespace {
 
 enum : uint8_t { U_WS = 0, U_P = 1, U_X = 2, U_SPEC = 3, U_SPX = 4 };
-constexpr uint32_t LMARK = 0x80000000u, LPEND = 0x40000000u;
+constexpr uint32_t LMARK = 0x80000000u;
 __device__ const uint8_t kMetaBytes[3] = {0xE2, 0x96, 0x81};
+
+constexpr int ARENA = 1024;         // LDS bytes for normalized medium words
+constexpr int WIN_PAD = WIN + 32;   // window + gather padding; the arena follows
+constexpr int VP_CAP = 384;         // Viterbi pieces per chunk
+constexpr int JOB_CAP = 256;        // words waiting for the DP
+constexpr int TASK_CAP = 1024;      // probe tasks per round
+constexpr int TASK_UNROLL = 4;      // probes in flight per lane
 
 typedef __attribute__((address_space(3))) double lds_f64;
 
@@ -46,9 +60,14 @@ __device__ __forceinline__ uint32_t uni_ascii(uint32_t b) {
 }
 __device__ __forceinline__ bool ascii_ws(uint32_t b) { return b == 32u || b == 9u || b == 10u || b == 12u || b == 13u; }
 
+__device__ __forceinline__ uint2 cp_ent(const DevTok &T, uint32_t cp) {
+    if (cp >= 0x110000u) cp = 0xFFFDu;
+    return T.cent[(uint32_t)T.cpage[cp >> 8] * 256u + (cp & 255u)];
+}
+
 // id of the slot (payload bytes acc(start .. start+n), cont) or -1: exact
 template <class Acc>
-__device__ int probe_acc(const DevTok &T, const Acc &acc, int start, int n, uint32_t cont) {
+__device__ int probe_acc(const DevTok &T, const Acc &acc, int start, int n, uint32_t cont, uint32_t *w3 = nullptr) {
     uint32_t h = hinit((uint32_t)n, cont);
     W16 first{0, 0, 0, 0};
     int b0 = 0;
@@ -67,8 +86,18 @@ __device__ int probe_acc(const DevTok &T, const Acc &acc, int start, int n, uint
         if (!slot_match(a, b, key, first)) continue;
         bool ok = true;
         for (int k = 16; k < n && ok; ++k) ok = T.vpool[a.z + k] == acc(start + k);
-        if (ok) return (int32_t)a.y;
+        if (ok) {
+            if (w3) *w3 = a.w;
+            return (int32_t)a.y;
+        }
     }
+    return -1;
+}
+
+// probe_result that also returns the slot's word 3 (a Unigram piece's f32 score)
+__device__ __forceinline__ int probe_result_w3(const Probe &P, uint32_t key, const W16 &c, uint32_t *w3) {
+    if (slot_match(P.a1, P.b1, key, c)) { *w3 = P.a1.w; return (int32_t)P.a1.y; }
+    if (slot_match(P.a2, P.b2, key, c)) { *w3 = P.a2.w; return (int32_t)P.a2.y; }
     return -1;
 }
 
@@ -88,35 +117,27 @@ __device__ int uni_special(const DevTok &T, int64_t p, int64_t N, const Byte &by
     return -1;
 }
 
-// ---- long items: normalize, split, Viterbi (one lane, sequential) ------------
-struct Scratch {
-    uint8_t *nb;     // normalized bytes
-    UniNode *nodes;  // Viterbi nodes
-    uint32_t *ids;   // ids of the item
-    int cap;         // normalized byte capacity (ids: 2 * cap + 8, nodes: cap + 8)
-};
-
-// strict UTF-8 decode as oracle/orc_unigram.c (u8len): raw length consumed,
-// cp, the sanitized bytes (invalid -> U+FFFD) and their count
-__device__ __forceinline__ int dec_char(const uint8_t *t, int64_t q, int64_t end, uint32_t *cp, uint32_t *bytes,
+// Strict UTF-8 decode as oracle/orc_unigram.c (u8len): raw length consumed,
+// cp, the sanitized bytes (invalid -> U+FFFD) and their count.
+template <class RB>
+__device__ __forceinline__ int dec_char(const RB &rb, int64_t q, int64_t end, uint32_t *cp, uint32_t *bytes,
                                         int *blen) {
-    const uint32_t b = t[q];
+    const uint32_t b = rb(q);
     if (b < 0x80u) {
         *cp = b;
         *bytes = b;
         *blen = 1;
         return 1;
     }
-    int len;
-    uint32_t c, mn;
+    int len = 0;
+    uint32_t c = 0, mn = 0;
     if ((b & 0xE0u) == 0xC0u) { len = 2; c = b & 0x1Fu; mn = 0x80u; }
     else if ((b & 0xF0u) == 0xE0u) { len = 3; c = b & 0x0Fu; mn = 0x800u; }
     else if ((b & 0xF8u) == 0xF0u) { len = 4; c = b & 0x07u; mn = 0x10000u; }
-    else len = 0;
     bool ok = len > 0 && q + len <= end;
     uint32_t raw = b;
     for (int k = 1; ok && k < len; ++k) {
-        const uint32_t x = t[q + k];
+        const uint32_t x = rb(q + k);
         if ((x & 0xC0u) != 0x80u) ok = false;
         c = c << 6 | (x & 0x3Fu);
         raw |= x << (8 * k);
@@ -134,75 +155,128 @@ __device__ __forceinline__ int dec_char(const uint8_t *t, int64_t q, int64_t end
     return len;
 }
 
-// Precompiled::normalize of raw word [a, b); ctx_space: the byte before a is
-// ' ' (so a cluster may run on from it: such chars are looked up one by one,
-// as the whole cluster -- which starts with ' ' -- matches no key).  Returns the
-// normalized length, or -1 when it exceeds cap.
-__device__ int normalize_word(const DevTok &T, const uint8_t *text, int64_t a, int64_t b, bool ctx_space, uint8_t *nb,
-                              int cap) {
+// Precompiled::normalize of raw word [a, b) (rb = raw bytes); put(byte)
+// returns false when the output is full.  ctx_space: the byte before a is ' '
+// (a cluster may run on from it; such chars are looked up one by one, as the
+// whole cluster -- starting with ' ' -- matches no key).  Per cluster:
+//   one char: its own entry (key -> normalization, else kept);
+//   more chars, < 6 bytes: the shortest key prefix of the cluster -- the first
+//     char itself when it is a key (the rest is dropped), a trie walk when it
+//     only starts longer keys, else none -> per char;
+//   otherwise per char.
+template <class RB, class Put>
+__device__ bool normalize_span(const DevTok &T, const RB &rb, int64_t a, int64_t b, bool ctx_space, const Put &put) {
     GState g;
     gstate_reset(g);
-    if (ctx_space) gcb_break(g, gprop(T.tpage, T.tblock, 0x20u));
-    int nl = 0;
-    bool ovf = false;
-    auto put_bytes = [&](uint32_t bytes, int n) {
-        if (nl + n > cap) { ovf = true; return; }
-        for (int k = 0; k < n; ++k) nb[nl + k] = (uint8_t)(bytes >> (8 * k));
-        nl += n;
-    };
-    auto put_norm = [&](int32_t off) {
-        for (uint32_t i = (uint32_t)off; i < T.tnorm_len && T.tnorm[i]; ++i) {
-            if (nl >= cap) { ovf = true; return; }
-            nb[nl++] = T.tnorm[i];
+    if (ctx_space) gcb_break(g, cp_ent(T, 0x20u).x & 0xFFu);
+    auto put_entry = [&](uint2 e, uint32_t bytes, int bl) -> bool {
+        if (!(e.x & CP_KEY)) {
+            for (int k = 0; k < bl; ++k)
+                if (!put((bytes >> (8 * k)) & 0xFFu)) return false;
+            return true;
         }
+        if (e.x & CP_INLINE) {
+            const int nb = (int)((e.x >> 11) & 7u);
+            for (int k = 0; k < nb; ++k)
+                if (!put((e.y >> (8 * k)) & 0xFFu)) return false;
+            return true;
+        }
+        for (uint32_t i = e.y; i < T.tnorm_len && T.tnorm[i]; ++i)
+            if (!put(T.tnorm[i])) return false;
+        return true;
     };
     bool first = true;
     int64_t q = a;
-    while (q < b && !ovf) {
+    while (q < b) {
         const int64_t cs = q;
-        uint32_t cp, bytes;
-        int bl;
-        q += dec_char(text, q, b, &cp, &bytes, &bl);
-        const bool brk = gcb_break(g, gprop(T.tpage, T.tblock, cp));
+        {  // printable ASCII followed by ASCII (or the end): a one-char cluster of
+           // GCB Other that the charsmap keeps (both host-checked): no table load
+            const uint32_t c = rb(q);
+            if (c - 0x21u < 0x5Eu && (q + 1 >= b || rb(q + 1) < 0x80u)) {
+                gcb_break(g, 0u);
+                first = false;
+                if (!put(c)) return false;
+                ++q;
+                continue;
+            }
+        }
+        uint32_t cp0, by0;
+        int bl0;
+        q += dec_char(rb, q, b, &cp0, &by0, &bl0);
+        const uint2 e0 = cp_ent(T, cp0);
+        const bool brk = gcb_break(g, e0.x & 0xFFu);
         const bool forced = first && ctx_space && !brk;
         first = false;
-        uint32_t buf0 = bytes, buf1 = 0;  // the cluster's first 8 sanitized bytes
-        int L = bl;
+        uint32_t buf0 = by0, buf1 = 0;  // the cluster's first 8 sanitized bytes
+        int L = bl0, nch = 1;
         while (q < b) {
             uint32_t cp2, by2;
             int bl2;
-            const int rl = dec_char(text, q, b, &cp2, &by2, &bl2);
+            const int rl = dec_char(rb, q, b, &cp2, &by2, &bl2);
             GState g2 = g;
-            if (gcb_break(g2, gprop(T.tpage, T.tblock, cp2))) break;
+            if (gcb_break(g2, cp_ent(T, cp2).x & 0xFFu)) break;
             g = g2;
             for (int k = 0; k < bl2; ++k, ++L) {
                 const uint32_t v = (by2 >> (8 * k)) & 0xFFu;
                 if (L < 4) buf0 |= v << (8 * L);
                 else if (L < 8) buf1 |= v << (8 * (L - 4));
             }
+            ++nch;
             q += rl;
         }
+        if (nch == 1) {
+            if (!put_entry(e0, by0, bl0)) return false;
+            continue;
+        }
         if (!forced && L < 6) {
-            const int32_t r = trie_shortest(T.trie, T.trie_units, [&](int i) -> uint32_t {
-                return i < 4 ? (buf0 >> (8 * i)) & 0xFFu : (buf1 >> (8 * (i - 4))) & 0xFFu;
-            }, L);
-            if (r >= 0) {
-                put_norm(r);
+            if (e0.x & CP_KEY) {  // the shortest key prefix is the first char: the rest is dropped
+                if (!put_entry(e0, by0, bl0)) return false;
                 continue;
             }
+            if (e0.x & CP_PREFIX) {
+                const int32_t r = trie_shortest(T.trie, T.trie_units, [&](int i) -> uint32_t {
+                    return i < 4 ? (buf0 >> (8 * i)) & 0xFFu : (buf1 >> (8 * (i - 4))) & 0xFFu;
+                }, L);
+                if (r >= 0) {
+                    bool ok = true;
+                    for (uint32_t i = (uint32_t)r; ok && i < T.tnorm_len && T.tnorm[i]; ++i) ok = put(T.tnorm[i]);
+                    if (!ok) return false;
+                    continue;
+                }
+            }
         }
-        for (int64_t x = cs; x < q && !ovf;) {  // per char
+        for (int64_t x = cs; x < q;) {  // per char
             uint32_t c3, b3;
             int l3;
-            x += dec_char(text, x, b, &c3, &b3, &l3);
-            const int32_t r = trie_shortest(T.trie, T.trie_units,
-                                            [&](int i) -> uint32_t { return (b3 >> (8 * i)) & 0xFFu; }, l3);
-            if (r >= 0) put_norm(r);
-            else put_bytes(b3, l3);
+            x += dec_char(rb, x, b, &c3, &b3, &l3);
+            if (!put_entry(cp_ent(T, c3), b3, l3)) return false;
         }
     }
-    return ovf ? -1 : nl;
+    return true;
 }
+
+// White_Space of the normalized char at nb(i); *len = its byte length
+template <class NB>
+__device__ __forceinline__ bool norm_ws(const DevTok &T, const NB &nb, int i, int *len) {
+    const uint32_t b = nb(i);
+    if (b < 0x80u) {
+        *len = 1;
+        return ascii_ws(b) || b == 0x0Bu;
+    }
+    const int l = u8len_lead(b);
+    uint32_t cp = b & (l == 2 ? 0x1Fu : l == 3 ? 0x0Fu : 0x07u);
+    for (int j = 1; j < l; ++j) cp = cp << 6 | (nb(i + j) & 0x3Fu);
+    *len = l;
+    return (cp_ent(T, cp).x & GP_WS) != 0u;
+}
+
+// ---- long items: global scratch, one lane, sequential -------------------------
+struct Scratch {
+    uint8_t *nb;     // normalized bytes
+    UniNode *nodes;  // Viterbi nodes
+    uint32_t *ids;   // ids of the item
+    int cap;         // normalized byte capacity (ids: 2 * cap + 8, nodes: cap + 8)
+};
 
 struct GNodes {
     UniNode *v;
@@ -212,31 +286,20 @@ struct GNodes {
     __device__ int id(int i) const { return v[i].id; }
 };
 
-// WhitespaceSplit + Metaspace + Unigram over nb[0, nl); ids -> S.ids.
-// Returns the id count (or -1 if the ids exceed their capacity).
+// WhitespaceSplit + Metaspace + Unigram over S.nb[0, nl) -> S.ids.  Returns the
+// id count, -1 if it exceeds the ids' capacity.
 __device__ int tokenize_normalized(const DevTok &T, const Scratch &S, int nl) {
     const uint8_t *nb = S.nb;
+    auto nbr = [&](int i) -> uint32_t { return nb[i]; };
     int k = 0;
     const int idcap = 2 * S.cap + 8;
-    auto ws_at = [&](int i, int *len) {
-        const uint32_t b = nb[i];
-        uint32_t cp = b;
-        int l = u8len_lead(b);
-        if (l > 1) {
-            cp = b & (l == 2 ? 0x1Fu : l == 3 ? 0x0Fu : 0x07u);
-            for (int j = 1; j < l; ++j) cp = cp << 6 | (nb[i + j] & 0x3Fu);
-        }
-        *len = l;
-        return (gprop(T.tpage, T.tblock, cp) & GP_WS) != 0u;
-    };
     int i = 0;
     while (i < nl) {
         int l;
-        if (ws_at(i, &l)) { i += l; continue; }
+        if (norm_ws(T, nbr, i, &l)) { i += l; continue; }
         int j = i;
-        while (j < nl && !ws_at(j, &l)) j += l;
-        // word [i, j): pieces start at i and before every "▁"; a word not
-        // starting with "▁" gets one prepended (Metaspace, add_prefix_space)
+        while (j < nl && !norm_ws(T, nbr, j, &l)) j += l;
+        // word [i, j): pieces before every "▁"; a word not starting with one gets one
         int ps = i;
         bool virt = !(j - i >= 3 && nb[i] == 0xE2 && nb[i + 1] == 0x96 && nb[i + 2] == 0x81);
         for (int t = i + 1; t <= j; ++t) {
@@ -245,14 +308,17 @@ __device__ int tokenize_normalized(const DevTok &T, const Scratch &S, int nl) {
             const int off = virt ? 3 : 0;
             const int n = t - ps + off;
             auto acc = [&](int x) -> uint32_t { return x < off ? kMetaBytes[x] : nb[ps + x - off]; };
-            auto probe = [&](int s, int e) -> int {
-                if (s == 0) return (e - 3 <= T.maxlen_meta) ? probe_acc(T, acc, 3, e - 3, UC_META) : -1;
-                return (e - s <= T.maxlen_first) ? probe_acc(T, acc, s, e - s, UC_PIECE) : -1;
+            auto cand = [&](int s, int e, double *sc) -> int {
+                int id;
+                if (s == 0) id = (e - 3 <= T.maxlen_meta) ? probe_acc(T, acc, 3, e - 3, UC_META) : -1;
+                else id = (e - s <= T.maxlen_first) ? probe_acc(T, acc, s, e - s, UC_PIECE) : -1;
+                if (id >= 0) *sc = T.uscore[id];
+                return id;
             };
             if (k + n + 1 > idcap) return -1;
             GNodes nodes{S.nodes};
             const int base = k;
-            k += unigram_viterbi(acc, n, probe, nodes, T.uscore, T.unk_score, T.unk_id, T.maxlen_piece,
+            k += unigram_viterbi(acc, n, cand, nodes, T.unk_score, T.unk_id, T.maxlen_piece,
                                  [&](int x, int id) { S.ids[base + x] = (uint32_t)id; });
             ps = t;
             virt = false;
@@ -262,8 +328,122 @@ __device__ int tokenize_normalized(const DevTok &T, const Scratch &S, int nl) {
     return k;
 }
 
+// Writes an item's k ids (id(j)) to the pool, points its chunk entry at them
+// and shifts the chunk's id count and later record offsets by k - 1.
+template <class Id>
+__device__ void finalize_item(uint32_t c, uint32_t e, int64_t p, int64_t rec, int k, const Id &id,
+                              const uint64_t *off, int64_t R, uint32_t *tokc, uint32_t *chunk_cnt, uint32_t *rec_local,
+                              uint32_t *pool, uint32_t *pool_count, uint32_t pool_cap, uint32_t *err) {
+    // pool word 0 is an empty item; allocations start at 1
+    const uint32_t at = 1u + atomicAdd(pool_count, (uint32_t)k + 1u);
+    if ((uint64_t)at + (uint32_t)k + 1u > pool_cap) {
+        atomicOr(err, 4u);
+        k = 0;
+        tokc[(int64_t)c * UNI_STAGE + e] = LMARK;
+    } else {
+        pool[at] = (uint32_t)k;
+        for (int j = 0; j < k; ++j) pool[at + 1 + j] = id(j);
+        tokc[(int64_t)c * UNI_STAGE + e] = LMARK | at;
+    }
+    const uint32_t extra = (uint32_t)k - 1u;  // the entry counted one id
+    if (extra) {
+        atomicAdd(&chunk_cnt[c], extra);
+        const int64_t cend = ((int64_t)c + 1) * CHUNK;
+        for (int64_t r = rec + 1; r < R && (int64_t)off[r] < cend; ++r)
+            if ((int64_t)off[r] > p) atomicAdd(&rec_local[r], extra);
+    }
+}
 
-// Per-lane LDS nodes of the chunk kernel (node-major: conflict-free)
+__device__ __forceinline__ int64_t record_of(const uint64_t *off, int64_t R, int64_t p) {
+    int64_t lo = 0, hi = R;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if ((int64_t)off[mid + 1] <= p) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+
+// End of a long item's raw word that ran past its chunk's window.
+__device__ int64_t word_end(const DevTok &T, const uint8_t *text, int64_t N, int64_t p, int64_t re) {
+    auto byte = [&](int64_t q) -> uint32_t { return text[q]; };
+    auto bnd = [&](int64_t q) -> bool { return q >= re; };
+    int64_t end;
+    for (end = p + 1; end < re; ++end) {
+        const uint32_t b = text[end];
+        if (ascii_ws(b)) break;
+        int l;
+        if (b == (uint32_t)'<' && T.n_special && uni_special(T, end, N, byte, bnd, &l) >= 0) break;
+    }
+    return end;
+}
+
+// Finishes long item (chunk c, tokc entry e, raw start p, raw length len or
+// 0 = unknown): returns false when its normalized text exceeds S.cap and
+// !last_resort (nothing written).
+__device__ bool finish_long(const DevTok &T, const uint8_t *text, int64_t N, const uint64_t *off, int64_t R,
+                            uint32_t c, uint32_t e, int64_t p, int64_t len, const Scratch &S, uint32_t *tokc,
+                            uint32_t *chunk_cnt, uint32_t *rec_local, uint32_t *pool, uint32_t *pool_count,
+                            uint32_t pool_cap, uint32_t *err, bool last_resort) {
+    const int64_t rec = record_of(off, R, p), rs = (int64_t)off[rec];
+    const int64_t re = (int64_t)off[rec + 1] < N ? (int64_t)off[rec + 1] : N;
+    auto byte = [&](int64_t q) -> uint32_t { return text[q]; };
+    const int64_t end = len ? p + len : word_end(T, text, N, p, re);
+    const bool ctx_space = p > rs && text[p - 1] == (uint8_t)' ';
+    int nl = 0;
+    const bool ok = normalize_span(T, byte, p, end, ctx_space, [&](uint32_t v) -> bool {
+        if (nl >= S.cap) return false;
+        S.nb[nl++] = (uint8_t)v;
+        return true;
+    });
+    int k = 0;
+    if (!ok) {
+        if (!last_resort) return false;
+        atomicOr(err, 16u);  // a whitespace-free run beyond UNI_HUGE_NORM normalized bytes: dropped
+    } else {
+        k = tokenize_normalized(T, S, nl);
+        if (k < 0) {
+            atomicOr(err, 2u);
+            k = 0;
+        }
+    }
+    finalize_item(c, e, p, rec, k, [&](int j) { return S.ids[j]; }, off, R, tokc, chunk_cnt, rec_local, pool,
+                  pool_count, pool_cap, err);
+    return true;
+}
+
+// ---- the chunk kernel's batched Viterbi ---------------------------------------
+// A Viterbi piece (vp) is "▁" + payload, payload = LDS bytes [src, src + L).
+// Its candidates are laid out row by row: the "▁" row (payload prefixes of
+// 0..min(L, Mm) bytes), then one row per payload start i (ends i+1 ..
+// min(L, i + Mf)).
+__device__ __forceinline__ int vp_c0(int L, int Mm) { return (L < Mm ? L : Mm) + 1; }
+__device__ __forceinline__ int vp_rowoff(int i, int L, int Mf) {  // sum_{k<i} min(L-k, Mf)
+    const int K = L > Mf ? L - Mf : 0;
+    if (i <= K) return i * Mf;
+    return K * Mf + (i - K) * L - (K + i - 1) * (i - K) / 2;
+}
+__device__ __forceinline__ int vp_tasks(int L, int Mm, int Mf) { return vp_c0(L, Mm) + vp_rowoff(L, L, Mf); }
+// local index of candidate (i, j) (i = -1: the "▁" row), or -1 if out of range
+__device__ __forceinline__ int vp_local(int i, int j, int L, int Mm, int Mf) {
+    if (i < 0) return j <= Mm && j <= L ? j : -1;
+    if (j - i > Mf || j > L || j <= i) return -1;
+    return vp_c0(L, Mm) + vp_rowoff(i, L, Mf) + (j - i - 1);
+}
+// inverse of vp_local
+__device__ __forceinline__ void vp_decode(int t, int L, int Mm, int Mf, int *i, int *j) {
+    const int c0 = vp_c0(L, Mm);
+    if (t < c0) { *i = -1; *j = t; return; }
+    int r = t - c0;
+    const int K = L > Mf ? L - Mf : 0;
+    if (r < K * Mf) { *i = r / Mf; *j = *i + 1 + r % Mf; return; }
+    r -= K * Mf;
+    int row = K;
+    while (r >= L - row) { r -= L - row; ++row; }
+    *i = row;
+    *j = row + 1 + r;
+}
+
+// Per-lane LDS nodes (node-major: conflict-free)
 struct LdsNodes {
     lds_f64 *sc;
     lds_u32 *bp;
@@ -283,24 +463,69 @@ struct LdsNodes {
     }
 };
 
+// 16 bytes at LDS byte offset b (dword loads + alignbyte), first n kept
+__device__ __forceinline__ W16 lds_w16(const lds_u32 *w32, int b, int n) {
+    const int a = b >> 2;
+    const uint32_t sh = (uint32_t)(b & 3);
+    const uint32_t x0 = w32[a], x1 = w32[a + 1], x2 = w32[a + 2], x3 = w32[a + 3], x4 = w32[a + 4];
+    const W16 raw{__builtin_amdgcn_alignbyte(x1, x0, sh), __builtin_amdgcn_alignbyte(x2, x1, sh),
+                  __builtin_amdgcn_alignbyte(x3, x2, sh), __builtin_amdgcn_alignbyte(x4, x3, sh)};
+    return keep_bytes(raw, n);
+}
+
 }  // namespace
+
+// Diagnostic build (-DSDL_STAMPS): lane 0 of every block adds the s_memtime
+// cycles between phase boundaries into sdl_uni_cycles[]; never in the product.
+#ifdef SDL_STAMPS
+__device__ unsigned long long sdl_uni_cycles[8];
+#define UNI_STAMP(k)                                                                  \
+    do {                                                                              \
+        if (threadIdx.x == 0) {                                                       \
+            const unsigned long long t_ = __builtin_amdgcn_s_memtime();              \
+            atomicAdd(&sdl_uni_cycles[k], t_ - stamp_prev_);                          \
+            stamp_prev_ = t_;                                                         \
+        }                                                                             \
+    } while (0)
+void print_uni_cycles() {
+    unsigned long long h[8];
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(sdl_uni_cycles), sizeof(h)) != hipSuccess) return;
+    static const char *names[] = {"", "load+classify+specials", "piece starts", "word table+medium", "task bases",
+                                  "compact+rec_local", "candidate probes", "DP"};
+    unsigned long long tot = 0;
+    for (int i = 1; i < 8; ++i) tot += h[i];
+    for (int i = 1; i < 8; ++i)
+        fprintf(stderr, "[uni stamps] %-24s %6.2f%%\n", names[i], tot ? 100.0 * (double)h[i] / (double)tot : 0.0);
+}
+#else
+#define UNI_STAMP(k) do {} while (0)
+#endif
 
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(TOK_THREADS) void k_unigram_chunks(
     DevTok T, const uint8_t *__restrict__ text, int64_t N, const uint64_t *__restrict__ off, int64_t R,
     const uint32_t *__restrict__ ranges, uint32_t *__restrict__ tokc, uint32_t *__restrict__ chunk_cnt,
-    uint32_t *__restrict__ chunk_ent, uint32_t *__restrict__ rec_local, uint32_t *__restrict__ long_count,
-    uint32_t *__restrict__ lchunks, uint32_t *__restrict__ lchunk_count) {
-    __shared__ __attribute__((aligned(16))) uint8_t s_win[WIN + 32];
+    uint32_t *__restrict__ chunk_ent, uint32_t *__restrict__ rec_local, uint32_t *__restrict__ counters,
+    uint4 *__restrict__ items, uint32_t item_cap, uint32_t *__restrict__ err) {
+    __shared__ __attribute__((aligned(16))) uint8_t s_bytes[WIN_PAD + ARENA + 32];  // window | arena
     __shared__ __attribute__((aligned(16))) uint8_t s_cls[WIN];
     __shared__ uint32_t s_rbits[RBITS_WORDS + 1];
     __shared__ uint16_t s_pieces[CHUNK + 1];  // prel | SPEC << 12
-    __shared__ uint16_t s_plen[CHUNK];        // piece length, 0 = runs past the window; bit 15: simple
+    __shared__ uint16_t s_plen[CHUNK];        // piece length (0 = runs past the window)
     __shared__ uint16_t s_stage[2 * CHUNK + 64];  // ids staged at 2 * prel
-    __shared__ uint16_t s_cnt[CHUNK];
+    __shared__ uint16_t s_cnt[CHUNK];             // ids per piece, 0xFFFF = long item
     __shared__ uint16_t s_poff[CHUNK];
     __shared__ uint16_t s_rb[RB_CAP];
-    __shared__ uint32_t s_scratch[8];
+    __shared__ uint32_t s_scratch[16];  // 0 jobs 1 vps 2 arena used 3 medium words; 8.. scan scratch
+    __shared__ uint16_t s_job_pi[JOB_CAP], s_job_vp[JOB_CAP];
+    __shared__ uint8_t s_job_nvp[JOB_CAP];
+    __shared__ uint32_t s_job_tb[JOB_CAP + 1];  // task base of each job (job order)
+    __shared__ uint32_t s_job_rb[JOB_CAP + 1];  // candidate-row base of each job
+    __shared__ unsigned long long s_rowmask[TASK_CAP];  // per row: which candidate ends exist
+    __shared__ uint16_t s_vp_src[VP_CAP];
+    __shared__ uint8_t s_vp_len[VP_CAP];
+    __shared__ uint16_t s_tid[TASK_CAP];
+    __shared__ float s_tsc[TASK_CAP];
     __shared__ double s_nsc[UNI_NODES * 64];
     __shared__ uint32_t s_nbp[UNI_NODES * 64];
 
@@ -309,26 +534,32 @@ __global__ __launch_bounds__(TOK_THREADS) void k_unigram_chunks(
     const int64_t c0 = (int64_t)blockIdx.x * CHUNK;
     const int64_t c1 = c0 + CHUNK < N ? c0 + CHUNK : N;
     const int64_t w0 = c0 - HALO_L;
-    const lds_u8 *win = (const lds_u8 *)s_win;
+    const lds_u8 *win = (const lds_u8 *)s_bytes;
+    lds_u8 *bytes = (lds_u8 *)s_bytes;
     lds_u8 *cls = (lds_u8 *)s_cls;
     const lds_u32 *rbits = (const lds_u32 *)s_rbits;
+    const lds_u32 *w32 = (const lds_u32 *)s_bytes;
+    const int Mm = T.maxlen_meta, Mf = T.maxlen_first;
+#ifdef SDL_STAMPS
+    unsigned long long stamp_prev_ = __builtin_amdgcn_s_memtime();
+#endif
 
     // ---- 1. load + classify ----------------------------------------------------
     const uint4 v = load16(text, c0 + 16 * tid, N);
-    *reinterpret_cast<uint4 *>(s_win + HALO_L + 16 * tid) = v;
+    *reinterpret_cast<uint4 *>(s_bytes + HALO_L + 16 * tid) = v;
     uint4 hv = make_uint4(0, 0, 0, 0);
     int64_t hp = 0;
     if (tid < (WIN - CHUNK) / 16) {
         hp = tid < HALO_L / 16 ? w0 + 16 * tid : c0 + CHUNK + 16 * (tid - HALO_L / 16);
         hv = load16(text, hp, N);
-        *reinterpret_cast<uint4 *>(s_win + (hp - w0)) = hv;
+        *reinterpret_cast<uint4 *>(s_bytes + (hp - w0)) = hv;
     }
-    if (tid < 2) *reinterpret_cast<uint4 *>(s_win + WIN + 16 * tid) = make_uint4(0, 0, 0, 0);
+    if (tid < 2) *reinterpret_cast<uint4 *>(s_bytes + WIN + 16 * tid) = make_uint4(0, 0, 0, 0);
     if (tid <= RBITS_WORDS) s_rbits[tid] = 0;
     const int64_t ra = ranges[3 * blockIdx.x], rz = ranges[3 * blockIdx.x + 1], r_lo = ranges[3 * blockIdx.x + 2];
     const int nrb = (int)(rz - ra);
     const bool rb_ok = nrb <= RB_CAP;
-    if (tid == 0) s_scratch[0] = s_scratch[1] = s_scratch[2] = 0;
+    if (tid < 8) s_scratch[tid] = 0;
     __syncthreads();
     for (int k = tid; k < nrb; k += TOK_THREADS) {
         const int rel = (int)((int64_t)off[ra + k] - w0);
@@ -349,6 +580,7 @@ __global__ __launch_bounds__(TOK_THREADS) void k_unigram_chunks(
     const Ctx C{&T, win, rbits, w0, text, N, off, R};
     auto cbyte = [&](int64_t q) -> uint32_t { return C.byte(q); };
     auto cbnd = [&](int64_t q) -> bool { return C.rstart(q); };
+    auto is_rs = [&](int wi) -> bool { return (rbits[wi >> 5] >> (wi & 31)) & 1u; };
     // added tokens (override the classes of their bytes)
     if (T.n_special) {
         for (int wi = tid; wi < WIN; wi += TOK_THREADS) {
@@ -362,6 +594,7 @@ __global__ __launch_bounds__(TOK_THREADS) void k_unigram_chunks(
         __syncthreads();
     }
 
+    UNI_STAMP(1);
     // ---- 2. piece starts: added tokens, and the first byte of every word ------
     const int64_t s0 = c0 + 16 * tid;
     const int nown = s0 >= c1 ? 0 : (int)(c1 - s0 < 16 ? c1 - s0 : 16);
@@ -372,10 +605,10 @@ __global__ __launch_bounds__(TOK_THREADS) void k_unigram_chunks(
         if (k == U_SPEC) { pmask |= 1u << i; continue; }
         if (k != U_P && k != U_X) continue;
         const uint32_t pk = cls[wi - 1];
-        if (pk == U_WS || pk == U_SPX || pk == U_SPEC || ((rbits[wi >> 5] >> (wi & 31)) & 1u)) pmask |= 1u << i;
+        if (pk == U_WS || pk == U_SPX || pk == U_SPEC || is_rs(wi)) pmask |= 1u << i;
     }
     uint32_t np_total;
-    uint32_t pbase = block_excl_sum<TOK_THREADS>((uint32_t)__builtin_popcount(pmask), &np_total, s_scratch + 4);
+    uint32_t pbase = block_excl_sum<TOK_THREADS>((uint32_t)__builtin_popcount(pmask), &np_total, s_scratch + 8);
     for (uint32_t m = pmask; m;) {
         const int i = __builtin_ctz(m);
         m &= m - 1;
@@ -384,139 +617,332 @@ __global__ __launch_bounds__(TOK_THREADS) void k_unigram_chunks(
     }
     __syncthreads();
     const int np = (int)np_total;
+    UNI_STAMP(2);
 
-    // ---- 3. per piece: length, then word table / added token / long item -------
+    // ---- 3. per piece: added token / word table / medium normalization / long --
     lds_u16 *stage = (lds_u16 *)s_stage;
     lds_u16 *cnt = (lds_u16 *)s_cnt;
-    uint16_t *s_pend = s_poff;  // misses for the Viterbi (s_poff is free until step 5)
-    const lds_u32 *w32 = (const lds_u32 *)s_win;
     for (int pi = tid; pi < np; pi += TOK_THREADS) {
         const uint32_t pc = s_pieces[pi];
         const int prel = (int)(pc & 0xFFFu);
         const int wi0 = HALO_L + prel;
-        bool pend = false;
         if (pc & (1u << 12)) {
             int l = 0;
             const int id = uni_special(T, c0 + prel, N, cbyte, cbnd, &l);
             stage[2 * prel] = (uint16_t)(id < 0 ? T.unk_id : id);
             cnt[pi] = 1;
             s_plen[pi] = (uint16_t)l;
-        } else {
-            // word end: first whitespace / added token / record start / text end
-            int wi = wi0 + 1;
-            bool simple = cls[wi0] == U_P;
-            int len = 0;
-            for (;; ++wi) {
-                if (wi >= WIN - 8) { len = 0; break; }  // runs past the window
-                if (w0 + wi >= N) { len = wi - wi0; break; }
-                const uint32_t k = cls[wi];
-                if (k == U_WS || k == U_SPEC || ((rbits[wi >> 5] >> (wi & 31)) & 1u)) { len = wi - wi0; break; }
-                simple = simple && k == U_P;
-            }
-            s_plen[pi] = (uint16_t)len;
-            if (simple && len > 0 && len <= UNI_WMAX) {
-                int packed;
-                if (len <= 16) {
-                    const int a = wi0 >> 2;
-                    const uint32_t sh = (uint32_t)(wi0 & 3);
-                    const uint32_t x0 = w32[a], x1 = w32[a + 1], x2 = w32[a + 2], x3 = w32[a + 3], x4 = w32[a + 4];
-                    const W16 raw{__builtin_amdgcn_alignbyte(x1, x0, sh), __builtin_amdgcn_alignbyte(x2, x1, sh),
-                                  __builtin_amdgcn_alignbyte(x3, x2, sh), __builtin_amdgcn_alignbyte(x4, x3, sh)};
-                    const W16 w = keep_bytes(raw, len);
-                    packed = probe_result(probe_load(T, hash16(w, (uint32_t)len, UC_WORD)),
-                                          (uint32_t)len | (UC_WORD << 8), w);
-                } else {
-                    packed = probe_acc(T, [&](int i) -> uint32_t { return win[wi0 + i]; }, 0, len, UC_WORD);
-                }
-                if (packed >= 0) {
-                    const int k = packed >> 24;
-                    const uint32_t x = (uint32_t)packed & 0xFFFFFFu;
-                    if (k == 1) stage[2 * prel] = (uint16_t)x;
-                    else
-                        for (int j = 0; j < k; ++j) stage[2 * prel + j] = T.wres[x + j];
-                    cnt[pi] = (uint16_t)k;
-                } else {
-                    pend = true;
-                }
+            continue;
+        }
+        // word end: first whitespace / added token / record start / text end
+        int wi = wi0 + 1;
+        bool simple = cls[wi0] == U_P;
+        int len = 0;
+        for (;; ++wi) {
+            if (wi >= WIN - 8) { len = 0; break; }  // runs past the window
+            if (w0 + wi >= N) { len = wi - wi0; break; }
+            const uint32_t k = cls[wi];
+            if (k == U_WS || k == U_SPEC || is_rs(wi)) { len = wi - wi0; break; }
+            simple = simple && k == U_P;
+        }
+        s_plen[pi] = (uint16_t)len;
+        bool done = false;
+        if (len > 0 && len <= UNI_WMAX && simple) {
+            int packed;
+            if (len <= 16) {
+                const W16 w = lds_w16(w32, wi0, len);
+                packed = probe_result(probe_load(T, hash16(w, (uint32_t)len, UC_WORD)),
+                                      (uint32_t)len | (UC_WORD << 8), w);
             } else {
-                // long item: marker (2 stage slots); finished by k_unigram_long
-                const uint32_t mk = LMARK | LPEND | ((uint32_t)(len > 0xFFFFF ? 0 : len) << 10) | (uint32_t)prel;
-                stage[2 * prel] = (uint16_t)(mk & 0xFFFFu);
-                stage[2 * prel + 1] = (uint16_t)(mk >> 16);
-                cnt[pi] = 0xFFFFu;
-                atomicAdd(long_count, 1u);
-                s_scratch[2] = 1u;
+                packed = probe_acc(T, [&](int i) -> uint32_t { return win[wi0 + i]; }, 0, len, UC_WORD);
             }
+            if (packed >= 0) {
+                const int k = packed >> 24;
+                const uint32_t x = (uint32_t)packed & 0xFFFFFFu;
+                if (k == 1) stage[2 * prel] = (uint16_t)x;
+                else
+                    for (int j = 0; j < k; ++j) stage[2 * prel + j] = T.wres[x + j];
+                cnt[pi] = (uint16_t)k;
+                done = true;
+            } else {
+                // miss: one Viterbi piece, the word's bytes in the window
+                const uint32_t vp = atomicAdd(&s_scratch[1], 1u);
+                if (vp < VP_CAP) {
+                    const uint32_t jb = atomicAdd(&s_scratch[0], 1u);
+                    if (jb < JOB_CAP) {
+                        s_vp_src[vp] = (uint16_t)wi0;
+                        s_vp_len[vp] = (uint8_t)len;
+                        s_job_pi[jb] = (uint16_t)pi;
+                        s_job_vp[jb] = (uint16_t)vp;
+                        s_job_nvp[jb] = 1;
+                        cnt[pi] = 0;
+                        done = true;
+                    }
+                }
+            }
+        } else if (len > 0 && len <= UNI_WMAX) {
+            // medium word: normalized in the next pass, all lanes at once
+            s_poff[atomicAdd(&s_scratch[3], 1u)] = (uint16_t)pi;
+            cnt[pi] = 0;
+            done = true;
         }
-        const uint64_t pm = __ballot(pend);
-        if (pm) {
-            const int leader = __builtin_ctzll(pm);
-            uint32_t base = 0;
-            if (lane == leader) base = atomicAdd(&s_scratch[1], (uint32_t)__popcll(pm));
-            base = __shfl(base, leader, 64);
-            if (pend) s_pend[base + __popcll(pm & ((1ull << lane) - 1ull))] = (uint16_t)pi;
-        }
+        if (!done) cnt[pi] = 0xFFFFu;  // long item: finished by k_unigram_long
     }
     __syncthreads();
 
-    // ---- 4. Viterbi of the word-table misses, lane per word -----------------------
-    const int npend = (int)s_scratch[1];
-    const LdsNodes nodes{(lds_f64 *)s_nsc, (lds_u32 *)s_nbp, lane};
-    for (int q = lane; q < npend; q += 64) {
-        const int pi = s_pend[q];
+    __syncthreads();
+    // medium words (non-ASCII or control bytes, <= UNI_WMAX): normalize into the
+    // arena (at most UNI_WMAX bytes each), split, list their Viterbi pieces
+    const int nmed = (int)s_scratch[3];
+    for (int mq = lane; mq < nmed; mq += 64) {
+        const int pi = s_poff[mq];
         const int prel = (int)(s_pieces[pi] & 0xFFFu);
-        const int len = s_plen[pi];
         const int wi0 = HALO_L + prel;
-        auto acc = [&](int i) -> uint32_t { return i < 3 ? kMetaBytes[i] : (uint32_t)win[wi0 + i - 3]; };
-        auto probe = [&](int s, int e) -> int {
-            // payload = word bytes [ws, ws + n) with cont META (s == 0) or PIECE
-            const int ws = s == 0 ? 0 : s - 3;
-            const int n = s == 0 ? e - 3 : e - s;
-            const uint32_t cont = s == 0 ? UC_META : UC_PIECE;
-            if (n > (s == 0 ? T.maxlen_meta : T.maxlen_first)) return -1;
-            if (n <= 16) {
-                const int b = wi0 + ws;
-                const int a = b >> 2;
-                const uint32_t sh = (uint32_t)(b & 3);
-                const uint32_t x0 = w32[a], x1 = w32[a + 1], x2 = w32[a + 2], x3 = w32[a + 3], x4 = w32[a + 4];
-                const W16 raw{__builtin_amdgcn_alignbyte(x1, x0, sh), __builtin_amdgcn_alignbyte(x2, x1, sh),
-                              __builtin_amdgcn_alignbyte(x3, x2, sh), __builtin_amdgcn_alignbyte(x4, x3, sh)};
-                const W16 w = keep_bytes(raw, n);
-                return probe_result(probe_load(T, hash16(w, (uint32_t)n, cont)), (uint32_t)n | (cont << 8), w);
+        const int len = s_plen[pi];
+        bool done = false;
+        const uint32_t a = atomicAdd(&s_scratch[2], (uint32_t)UNI_WMAX);
+        if (a + UNI_WMAX <= (uint32_t)ARENA) {
+            const int abase = WIN_PAD + (int)a;
+            const bool ctx_space = !is_rs(wi0) && win[wi0 - 1] == (uint8_t)' ';
+            auto rb = [&](int64_t q) -> uint32_t { return win[(int)(q - w0)]; };
+            int nl = 0;
+            const bool ok = normalize_span(T, rb, w0 + wi0, w0 + wi0 + len, ctx_space, [&](uint32_t x) -> bool {
+                if (nl >= UNI_WMAX) return false;
+                bytes[abase + nl++] = (uint8_t)x;
+                return true;
+            });
+            if (ok) {
+                // WhitespaceSplit + Metaspace: count the pieces and bound the
+                // ids (pass 0), then list them (pass 1)
+                auto nb = [&](int i) -> uint32_t { return bytes[abase + i]; };
+                int nvp = 0, bound = 0;
+                uint32_t vp0 = 0;
+                bool fits = true;
+                for (int pass = 0; pass < 2 && fits; ++pass) {
+                    if (pass == 1) {
+                        if (nvp == 0) break;
+                        if (bound > 2 * len || nvp > 255) { fits = false; break; }
+                        vp0 = atomicAdd(&s_scratch[1], (uint32_t)nvp);
+                        if (vp0 + (uint32_t)nvp > (uint32_t)VP_CAP) { fits = false; break; }
+                    }
+                    int k = 0, i = 0;
+                    while (i < nl) {
+                        int l;
+                        if (norm_ws(T, nb, i, &l)) { i += l; continue; }
+                        int j = i;
+                        while (j < nl && !norm_ws(T, nb, j, &l)) j += l;
+                        int ps = i;
+                        bool virt = !(j - i >= 3 && nb(i) == 0xE2 && nb(i + 1) == 0x96 && nb(i + 2) == 0x81);
+                        for (int t = i + 1; t <= j; ++t) {
+                            const bool cut = t == j || (t + 3 <= j && nb(t) == 0xE2 && nb(t + 1) == 0x96 &&
+                                                        nb(t + 2) == 0x81);
+                            if (!cut) continue;
+                            const int psrc = virt ? ps : ps + 3;  // payload after the "▁"
+                            if (pass == 0) {
+                                ++nvp;
+                                int chars = 0;
+                                for (int x = psrc; x < t; ++x) chars += (nb(x) & 0xC0u) != 0x80u;
+                                bound += chars + 1;
+                            } else {
+                                s_vp_src[vp0 + k] = (uint16_t)(abase + psrc);
+                                s_vp_len[vp0 + k] = (uint8_t)(t - psrc);
+                                ++k;
+                            }
+                            ps = t;
+                            virt = false;
+                        }
+                        i = j;
+                    }
+                }
+                if (fits && nvp == 0) {  // nothing left after normalization
+                    cnt[pi] = 0;
+                    done = true;
+                } else if (fits) {
+                    const uint32_t jb = atomicAdd(&s_scratch[0], 1u);
+                    if (jb < JOB_CAP) {
+                        s_job_pi[jb] = (uint16_t)pi;
+                        s_job_vp[jb] = (uint16_t)vp0;
+                        s_job_nvp[jb] = (uint8_t)nvp;
+                        cnt[pi] = 0;
+                        done = true;
+                    }
+                }
             }
-            return probe_acc(T, [&](int i) -> uint32_t { return win[wi0 + i]; }, ws, n, cont);
-        };
-        const int k = unigram_viterbi(acc, len + 3, probe, nodes, T.uscore, T.unk_score, T.unk_id, T.maxlen_piece,
-                                      [&](int x, int id) { stage[2 * prel + x] = (uint16_t)id; });
-        cnt[pi] = (uint16_t)k;
+        }
+        if (!done) cnt[pi] = 0xFFFFu;  // long item: finished by k_unigram_long
     }
     __syncthreads();
+    UNI_STAMP(3);
+    // ---- 4./5. batched Viterbi of the pending words, in rounds ------------------
+    const int nj = (int)(s_scratch[0] < (uint32_t)JOB_CAP ? s_scratch[0] : (uint32_t)JOB_CAP);
+    uint32_t carry = 0, rcarry = 0;  // task and row bases per job (job order)
+    for (int j0 = 0; j0 < nj; j0 += 64) {
+        const int j = j0 + lane;
+        uint32_t t = 0, rw = 0;
+        if (j < nj)
+            for (int q = 0; q < s_job_nvp[j]; ++q) {
+                const int L = s_vp_len[s_job_vp[j] + q];
+                t += (uint32_t)vp_tasks(L, Mm, Mf);
+                rw += (uint32_t)L + 1u;
+            }
+        const uint32_t incl = wave_incl_sum(t), rincl = wave_incl_sum(rw);
+        if (j < nj) {
+            s_job_tb[j] = carry + incl - t;
+            s_job_rb[j] = rcarry + rincl - rw;
+        }
+        carry += (uint32_t)__shfl((int)incl, 63, 64);
+        rcarry += (uint32_t)__shfl((int)rincl, 63, 64);
+    }
+    if (lane == 0) {
+        s_job_tb[nj] = carry;
+        s_job_rb[nj] = rcarry;
+    }
+    __syncthreads();
+    const LdsNodes nodes{(lds_f64 *)s_nsc, (lds_u32 *)s_nbp, lane};
+    for (int j0 = 0; j0 < nj;) {
+        // the round: jobs [j0, j1) whose tasks fit TASK_CAP (one job always does)
+        int lo = j0 + 1, hi = nj;
+        while (lo < hi) {
+            const int m = (lo + hi + 1) >> 1;
+            if (s_job_tb[m] - s_job_tb[j0] <= (uint32_t)TASK_CAP) lo = m; else hi = m - 1;
+        }
+        const int j1 = lo;
+        const uint32_t T0 = s_job_tb[j0], RB0 = s_job_rb[j0];
+        const int nt = (int)(s_job_tb[j1] - T0);
+        for (int r = lane; r < (int)(s_job_rb[j1] - RB0); r += 64) s_rowmask[r] = 0ull;
+        __syncthreads();
+        // -- candidate rows: lane per row (one start of one piece), 4 probes in flight --
+        const int nrows = (int)(s_job_rb[j1] - RB0);
+        for (int r = lane; r < nrows; r += 64) {
+            const uint32_t gr = RB0 + (uint32_t)r;
+            int a = j0, b = j1 - 1;  // the job holding row gr
+            while (a < b) {
+                const int m = (a + b + 1) >> 1;
+                if (s_job_rb[m] <= gr) a = m; else b = m - 1;
+            }
+            int lr = (int)(gr - s_job_rb[a]);
+            int vp = s_job_vp[a];
+            int tb = (int)(s_job_tb[a] - T0);
+            for (int q = 0;; ++q) {
+                const int Lq = s_vp_len[vp];
+                if (lr < Lq + 1 || q + 1 >= s_job_nvp[a]) break;
+                lr -= Lq + 1;
+                tb += vp_tasks(Lq, Mm, Mf);
+                ++vp;
+            }
+            const int L = s_vp_len[vp], src = s_vp_src[vp];
+            const int i = lr - 1;  // payload start; -1: the "▁" row
+            unsigned long long mask = 0ull;
+            if (!(i > 0 && (bytes[src + i] & 0xC0u) == 0x80u)) {  // rows start on char boundaries
+                const int ps = i < 0 ? 0 : i;
+                const int jlo = i < 0 ? 0 : i + 1;
+                const int jmax = i < 0 ? (L < Mm ? L : Mm) : (L < i + Mf ? L : i + Mf);
+                const int tbr = tb + (i < 0 ? 0 : vp_c0(L, Mm) + vp_rowoff(i, L, Mf));
+                const uint32_t cont = i < 0 ? UC_META : UC_PIECE;
+                for (int jb = jlo; jb <= jmax; jb += TASK_UNROLL) {
+                    Probe P[TASK_UNROLL];
+                    W16 W[TASK_UNROLL];
+                    bool live[TASK_UNROLL];
+                    int gen[TASK_UNROLL];  // generic probe (payload > 16 bytes); -2: use P
+                    uint32_t gw3[TASK_UNROLL];
+#pragma unroll
+                    for (int u = 0; u < TASK_UNROLL; ++u) {
+                        const int j = jb + u;
+                        live[u] = j <= jmax && !(j < L && (bytes[src + j] & 0xC0u) == 0x80u);
+                        gen[u] = -2;
+                        gw3[u] = 0;
+                        W[u] = W16{0, 0, 0, 0};
+                        if (!live[u]) continue;
+                        const int n = j - ps;
+                        if (n <= 16) {
+                            W[u] = lds_w16(w32, src + ps, n);
+                            P[u] = probe_load(T, hash16(W[u], (uint32_t)n, cont));
+                        } else {
+                            gen[u] = probe_acc(T, [&](int x) -> uint32_t { return bytes[src + x]; }, ps, n, cont,
+                                               &gw3[u]);
+                        }
+                    }
+#pragma unroll
+                    for (int u = 0; u < TASK_UNROLL; ++u) {
+                        if (!live[u]) continue;
+                        const int j = jb + u;
+                        uint32_t w3 = gw3[u];
+                        const int id = gen[u] != -2 ? gen[u]
+                                                    : probe_result_w3(P[u], (uint32_t)(j - ps) | (cont << 8), W[u], &w3);
+                        if (id < 0) continue;
+                        const int k = j - jlo;
+                        mask |= 1ull << k;
+                        s_tid[tbr + k] = (uint16_t)id;
+                        s_tsc[tbr + k] = __uint_as_float(w3);  // the slot's score (f32, exact)
+                    }
+                }
+            }
+            s_rowmask[r] = mask;
+        }
+        __syncthreads();
+        UNI_STAMP(6);
+        // -- DP: lane per job --
+        for (int jb = j0 + lane; jb < j1; jb += 64) {
+            const int pi = s_job_pi[jb];
+            const int prel = (int)(s_pieces[pi] & 0xFFFu);
+            int toff = (int)(s_job_tb[jb] - T0);
+            int roff = (int)(s_job_rb[jb] - RB0);
+            int ktot = 0;
+            for (int q = 0; q < s_job_nvp[jb]; ++q) {
+                const int vp = s_job_vp[jb] + q;
+                const int L = s_vp_len[vp], src = s_vp_src[vp];
+                auto acc = [&](int x) -> uint32_t { return x < 3 ? kMetaBytes[x] : (uint32_t)bytes[src + x - 3]; };
+                auto rowmask = [&](int s) -> uint64_t { return s_rowmask[roff + (s == 0 ? 0 : s - 2)]; };
+                auto cand = [&](int s, int e, double *sc) -> int {
+                    const int loc = vp_local(s == 0 ? -1 : s - 3, e - 3, L, Mm, Mf);
+                    if (loc < 0 || !((rowmask(s) >> (e - (s == 0 ? 3 : s + 1))) & 1ull)) return -1;
+                    *sc = (double)s_tsc[toff + loc];
+                    return (int)s_tid[toff + loc];
+                };
+                auto at = [&](int s, int e, double *sc) -> int {
+                    const int loc = vp_local(s == 0 ? -1 : s - 3, e - 3, L, Mm, Mf);
+                    *sc = (double)s_tsc[toff + loc];
+                    return (int)s_tid[toff + loc];
+                };
+                const int base = ktot;
+                ktot += unigram_viterbi_masked(acc, L + 3, rowmask, at, cand, nodes, T.unk_score, T.unk_id,
+                                               [&](int x, int id) { stage[2 * prel + base + x] = (uint16_t)id; });
+                toff += vp_tasks(L, Mm, Mf);
+                roff += L + 1;
+            }
+            cnt[pi] = (uint16_t)ktot;
+        }
+        __syncthreads();
+        UNI_STAMP(7);
+        j0 = j1;
+    }
 
-    // ---- 5. compact ids into this chunk's tokc slice ------------------------------
+    UNI_STAMP(4);
+    // ---- 6. compact ids into this chunk's tokc slice; list the long items -------
     const int per = (np + TOK_THREADS - 1) / TOK_THREADS;
     const int a0 = tid * per < np ? tid * per : np;
     const int a1 = a0 + per < np ? a0 + per : np;
     uint32_t mine = 0;
     for (int i = a0; i < a1; ++i) mine += s_cnt[i] == 0xFFFFu ? 1u : s_cnt[i];
     uint32_t total;
-    uint32_t base = block_excl_sum<TOK_THREADS>(mine, &total, s_scratch + 4);
+    uint32_t base = block_excl_sum<TOK_THREADS>(mine, &total, s_scratch + 8);
     uint32_t *dst = tokc + (int64_t)blockIdx.x * UNI_STAGE;
     for (int i = a0; i < a1; ++i) {
         s_poff[i] = (uint16_t)base;
         const int prel = s_pieces[i] & 0xFFF;
         const int k = s_cnt[i];
         if (k == 0xFFFF) {
-            dst[base++] = (uint32_t)s_stage[2 * prel] | ((uint32_t)s_stage[2 * prel + 1] << 16);
+            const uint32_t it = atomicAdd(&counters[0], 1u);
+            if (it < item_cap) items[it] = make_uint4((uint32_t)blockIdx.x, base, (uint32_t)prel, s_plen[i]);
+            else atomicOr(err, 8u);
+            dst[base++] = LMARK;
             continue;
         }
         for (int j = 0; j < k; ++j) dst[base + j] = s_stage[2 * prel + j];
         base += k;
     }
     __syncthreads();
-    if (tid == 0) {
-        chunk_cnt[blockIdx.x] = chunk_ent[blockIdx.x] = total;
-        if (s_scratch[2]) lchunks[atomicAdd(lchunk_count, 1u)] = (uint32_t)blockIdx.x;
-    }
+    if (tid == 0) chunk_cnt[blockIdx.x] = chunk_ent[blockIdx.x] = total;
     const int k_lo = (int)(r_lo - ra);
     for (int k = k_lo + tid;; k += TOK_THREADS) {
         int64_t pos;
@@ -536,133 +962,258 @@ __global__ __launch_bounds__(TOK_THREADS) void k_unigram_chunks(
         }
         rec_local[ra + k] = lo < np ? (uint32_t)s_poff[lo] : total;
     }
+    UNI_STAMP(5);
 }
 
 namespace {
-
-// Finishes long item (chunk c, entry e, raw start p, raw length len or 0):
-// returns false when its normalized text exceeds S.cap (nothing written).
-__device__ bool finish_long(const DevTok &T, const uint8_t *text, int64_t N, const uint64_t *off, int64_t R,
-                            uint32_t c, uint32_t e, int64_t p, int64_t len, const Scratch &S, uint32_t *tokc,
-                            uint32_t *chunk_cnt, uint32_t *rec_local, uint32_t *pool, uint32_t *pool_count,
-                            uint32_t pool_cap, uint32_t *err, bool last_resort) {
-    // record containing p
-    int64_t lo = 0, hi = R;
-    while (lo < hi) {
-        const int64_t mid = (lo + hi) >> 1;
-        if ((int64_t)off[mid + 1] <= p) lo = mid + 1; else hi = mid;
-    }
-    const int64_t rec = lo, rs = (int64_t)off[rec], re = (int64_t)off[rec + 1] < N ? (int64_t)off[rec + 1] : N;
-    int64_t end = p + len;
-    if (len == 0) {  // ran past its chunk's window: scan to the word's end
-        auto byte = [&](int64_t q) -> uint32_t { return text[q]; };
-        auto bnd = [&](int64_t q) -> bool { return q >= re; };
-        for (end = p + 1; end < re; ++end) {
-            const uint32_t b = text[end];
-            if (ascii_ws(b)) break;
-            int l;
-            if (b == (uint32_t)'<' && T.n_special && uni_special(T, end, N, byte, bnd, &l) >= 0) break;
-        }
-    }
-    const bool ctx_space = p > rs && text[p - 1] == (uint8_t)' ';
-    const int nl = normalize_word(T, text, p, end, ctx_space, S.nb, S.cap);
-    int k = 0;
-    if (nl < 0) {
-        if (!last_resort) return false;
-        atomicOr(err, 16u);  // a whitespace-free run beyond UNI_HUGE_NORM normalized bytes: dropped
-    } else {
-        k = tokenize_normalized(T, S, nl);
-        if (k < 0) {
-            atomicOr(err, 2u);
-            k = 0;
-        }
-    }
-    // pool word 0 is an empty item; allocations start at 1
-    const uint32_t at = 1u + atomicAdd(pool_count, (uint32_t)k + 1u);
-    if ((uint64_t)at + (uint32_t)k + 1u > pool_cap) {
-        atomicOr(err, 4u);
-        k = 0;
-        tokc[(int64_t)c * UNI_STAGE + e] = LMARK;  // an empty item (pool slot 0 holds 0)
-    } else {
-        pool[at] = (uint32_t)k;
-        for (int j = 0; j < k; ++j) pool[at + 1 + j] = S.ids[j];
-        tokc[(int64_t)c * UNI_STAGE + e] = LMARK | at;
-    }
-    const uint32_t extra = (uint32_t)k - 1u;  // the entry counted one id
-    if (extra) {
-        atomicAdd(&chunk_cnt[c], extra);
-        const int64_t cend = ((int64_t)c + 1) * CHUNK;
-        for (int64_t r = rec + 1; r < R && (int64_t)off[r] < cend; ++r)
-            if ((int64_t)off[r] > p) atomicAdd(&rec_local[r], extra);
-    }
-    return true;
+constexpr size_t huge_scratch_bytes() {
+    return (size_t)UNI_HUGE_NORM + sizeof(UniNode) * (UNI_HUGE_NORM + 8) + 4 * (2 * UNI_HUGE_NORM + 8);
 }
-
+__device__ Scratch make_scratch(uint8_t *mine, int cap) {
+    return Scratch{mine + sizeof(UniNode) * (cap + 8) + 4 * (2 * cap + 8), reinterpret_cast<UniNode *>(mine),
+                   reinterpret_cast<uint32_t *>(mine + sizeof(UniNode) * (cap + 8)), cap};
+}
 }  // namespace
 
-// Long items, lane per item, per chunk of the lchunks list.
+// Long items, one wave each: lane 0 normalizes the word into LDS and walks
+// its pieces; per piece, lanes take candidate rows (a start position each,
+// up to Mf probes, 4 in flight) and lane 0 relaxes the nodes of those 64
+// starts from LDS, then backtracks.  Items past LONG_NORM normalized bytes go
+// to the huge list.
+constexpr int LONG_NORM = 2048;
+
 __global__ __launch_bounds__(64) void k_unigram_long(DevTok T, const uint8_t *__restrict__ text, int64_t N,
                                                      const uint64_t *__restrict__ off, int64_t R,
-                                                     const uint32_t *__restrict__ lchunks,
-                                                     const uint32_t *__restrict__ lchunk_count,
-                                                     const uint32_t *__restrict__ chunk_ent, uint32_t *tokc,
-                                                     uint32_t *chunk_cnt, uint32_t *rec_local, uint8_t *scratch,
-                                                     uint32_t *pool, uint32_t *pool_count, uint32_t pool_cap,
-                                                     uint4 *huge, uint32_t *huge_count, uint32_t huge_cap,
-                                                     uint32_t *err) {
+                                                     const uint4 *__restrict__ items, uint32_t item_cap,
+                                                     uint32_t *counters, uint32_t *tokc, uint32_t *chunk_cnt,
+                                                     uint32_t *rec_local, uint32_t *pool, uint32_t pool_cap,
+                                                     uint4 *huge, uint32_t huge_cap, uint32_t *err) {
+    __shared__ __attribute__((aligned(16))) uint8_t s_nb[LONG_NORM + 32];
+    __shared__ double s_sc[LONG_NORM + 8];
+    __shared__ uint32_t s_st[LONG_NORM + 8];  // node start | id << 16 (0xFFFF: unset)
+    __shared__ uint16_t s_ids[2 * LONG_NORM + 16];
+    __shared__ uint16_t s_cid[64 * 64];       // [k][lane]: id of row lane's k-th end
+    __shared__ float s_csc[64 * 64];
+    __shared__ unsigned long long s_mask[64];
+    __shared__ int s_misc[8];
     const int lane = lane_id();
-    const size_t per = (size_t)UNI_LANE_NORM + sizeof(UniNode) * (UNI_LANE_NORM + 8) + 4 * (2 * UNI_LANE_NORM + 8);
-    uint8_t *mine = scratch + ((size_t)blockIdx.x * 64 + lane) * per;
-    const Scratch S{mine + sizeof(UniNode) * (UNI_LANE_NORM + 8) + 4 * (2 * UNI_LANE_NORM + 8),
-                    reinterpret_cast<UniNode *>(mine),
-                    reinterpret_cast<uint32_t *>(mine + sizeof(UniNode) * (UNI_LANE_NORM + 8)), UNI_LANE_NORM};
-    const uint32_t nl = *lchunk_count;
-    for (uint32_t i = blockIdx.x; i < nl; i += gridDim.x) {
-        const uint32_t c = lchunks[i];
-        const uint32_t ne = chunk_ent[c];
-        for (uint32_t e0 = 0; e0 < ne; e0 += 64) {
-            const uint32_t e = e0 + lane;
-            const uint32_t x = e < ne ? tokc[(int64_t)c * UNI_STAGE + e] : 0u;
-            if ((x & (LMARK | LPEND)) != (LMARK | LPEND)) continue;
-            const int64_t p = (int64_t)c * CHUNK + (x & 0x3FFu);
-            const int64_t len = (x >> 10) & 0xFFFFFu;
-            if (!finish_long(T, text, N, off, R, c, e, p, len, S, tokc, chunk_cnt, rec_local, pool, pool_count,
-                             pool_cap, err, false)) {
-                const uint32_t h = atomicAdd(huge_count, 1u);
-                if (h < huge_cap) huge[h] = make_uint4(c, e, (uint32_t)(x & 0x3FFu), (uint32_t)len);
+    lds_u8 *nb = (lds_u8 *)s_nb;
+    const lds_u32 *w32 = (const lds_u32 *)s_nb;
+    const int Mm = T.maxlen_meta, Mf = T.maxlen_first;
+    uint32_t n_items = counters[0];
+    if (n_items > item_cap) n_items = item_cap;
+    for (uint32_t it_i = blockIdx.x; it_i < n_items; it_i += gridDim.x) {
+        const uint4 it = items[it_i];
+        const int64_t p = (int64_t)it.x * CHUNK + it.z;
+        const int64_t rec = record_of(off, R, p);
+        if (lane == 0) {
+            const int64_t rs = (int64_t)off[rec];
+            const int64_t re = (int64_t)off[rec + 1] < N ? (int64_t)off[rec + 1] : N;
+            const int64_t end = it.w ? p + it.w : word_end(T, text, N, p, re);
+            int nl = 0;
+            auto byte = [&](int64_t q) -> uint32_t { return text[q]; };
+            const bool ok = normalize_span(T, byte, p, end, p > rs && text[p - 1] == (uint8_t)' ',
+                                           [&](uint32_t x) -> bool {
+                                               if (nl >= LONG_NORM) return false;
+                                               nb[nl++] = (uint8_t)x;
+                                               return true;
+                                           });
+            for (int z = 0; z < 8; ++z) nb[nl + z] = 0;
+            s_misc[0] = ok ? nl : -1;
+            s_misc[1] = 0;  // cursor: where the next word/piece search starts
+            s_misc[5] = 0;  // ids so far
+            s_misc[6] = -1; // end of the current word (-1: none)
+            s_misc[7] = 0;  // the current piece is virtual-"▁"-prefixed
+        }
+        __syncthreads();
+        const int nl = s_misc[0];
+        if (nl < 0) {
+            if (lane == 0) {
+                const uint32_t h = atomicAdd(&counters[3], 1u);
+                if (h < huge_cap) huge[h] = it;
                 else atomicOr(err, 8u);
             }
+            __syncthreads();
+            continue;
         }
+        auto nbr = [&](int i) -> uint32_t { return nb[i]; };
+        for (;;) {
+            // lane 0: the next Metaspace piece -> (payload src, length) or done
+            if (lane == 0) {
+                int cur = s_misc[1], wend = s_misc[6];
+                int src = -1, L = 0;
+                if (wend < 0 || cur >= wend) {  // next word
+                    int l;
+                    while (cur < nl && norm_ws(T, nbr, cur, &l)) cur += l;
+                    if (cur < nl) {
+                        int j = cur;
+                        while (j < nl && !norm_ws(T, nbr, j, &l)) j += l;
+                        wend = j;
+                        const bool m = j - cur >= 3 && nb[cur] == 0xE2 && nb[cur + 1] == 0x96 && nb[cur + 2] == 0x81;
+                        s_misc[7] = m ? 0 : 1;
+                    } else {
+                        wend = -1;
+                    }
+                }
+                if (wend >= 0) {
+                    const bool virt = s_misc[7] != 0;
+                    src = virt ? cur : cur + 3;  // payload after the "▁"
+                    int t = cur + (virt ? 1 : 3);
+                    while (t < wend && !(t + 3 <= wend && nb[t] == 0xE2 && nb[t + 1] == 0x96 && nb[t + 2] == 0x81)) ++t;
+                    L = t - src;
+                    cur = t;
+                    s_misc[7] = 0;
+                }
+                s_misc[1] = cur;
+                s_misc[6] = wend;
+                s_misc[2] = src;
+                s_misc[3] = L;
+            }
+            __syncthreads();
+            const int src = s_misc[2], L = s_misc[3];
+            if (src < 0) break;
+            const int n = L + 3;  // the piece "▁" + payload
+            for (int i = lane; i <= n; i += 64) {
+                s_sc[i] = 0.0;
+                s_st[i] = 0xFFFFFFFFu;
+            }
+            // acc / cand over the piece (cand: the fused-unk lookup, lane 0)
+            auto acc = [&](int x) -> uint32_t { return x < 3 ? kMetaBytes[x] : (uint32_t)nb[src + x - 3]; };
+            auto cand = [&](int st2, int e2, double *sc) -> int {
+                int id;
+                if (st2 == 0) id = (e2 - 3 <= Mm) ? probe_acc(T, nbr, src, e2 - 3, UC_META) : -1;
+                else id = (e2 - st2 <= Mf) ? probe_acc(T, nbr, src + st2 - 3, e2 - st2, UC_PIECE) : -1;
+                if (id >= 0) *sc = T.uscore[id];
+                return id;
+            };
+            __syncthreads();
+            for (int r0 = 0; r0 <= L; r0 += 64) {
+                // row r = r0 + lane: r == 0 the "▁" row, else payload start r - 1
+                const int r = r0 + lane;
+                unsigned long long mask = 0ull;
+                if (r <= L && !(r > 1 && (nb[src + r - 1] & 0xC0u) == 0x80u)) {
+                    const int i = r - 1;  // -1: the "▁" row
+                    const int ps = i < 0 ? 0 : i;
+                    const int jmax = i < 0 ? (L < Mm ? L : Mm) : (L < i + Mf ? L : i + Mf);
+                    const uint32_t cont = i < 0 ? UC_META : UC_PIECE;
+                    for (int j0 = i < 0 ? 0 : i + 1; j0 <= jmax; j0 += 4) {
+                        Probe P[4];
+                        W16 W[4];
+                        int gen[4];
+                        bool live[4];
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            const int j = j0 + u;
+                            live[u] = j <= jmax && !(j < L && (nb[src + j] & 0xC0u) == 0x80u);
+                            gen[u] = -2;
+                            W[u] = W16{0, 0, 0, 0};
+                            if (!live[u]) continue;
+                            const int len = j - ps;
+                            if (len <= 16) {
+                                W[u] = lds_w16(w32, src + ps, len);
+                                P[u] = probe_load(T, hash16(W[u], (uint32_t)len, cont));
+                            } else {
+                                gen[u] = probe_acc(T, nbr, src + ps, len, cont);
+                            }
+                        }
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            if (!live[u]) continue;
+                            const int j = j0 + u;
+                            const uint32_t key = (uint32_t)(j - ps) | (cont << 8);
+                            const int id = gen[u] != -2 ? gen[u] : probe_result(P[u], key, W[u]);
+                            if (id < 0) continue;
+                            const int k = i < 0 ? j : j - i - 1;
+                            mask |= 1ull << k;
+                            s_cid[k * 64 + lane] = (uint16_t)id;
+                            s_csc[k * 64 + lane] = T.uscore32[id];
+                        }
+                    }
+                }
+                s_mask[lane] = mask;
+                __syncthreads();
+                if (lane == 0) {  // relax the nodes from these rows' starts, in order
+                    const int rz = L + 1 - r0 < 64 ? L + 1 - r0 : 64;
+                    for (int q = 0; q < rz; ++q) {
+                        const int r = r0 + q;
+                        const int st = r == 0 ? 0 : r + 2;  // node position of the row's start
+                        if (r > 1 && (nb[src + r - 1] & 0xC0u) == 0x80u) continue;
+                        const int l0 = u8len_lead(acc(st));
+                        const int mb = l0 < n - st ? l0 : n - st;
+                        const double base = s_sc[st];
+                        const int fe = st == 0 ? 3 : st + 1;
+                        unsigned long long m = s_mask[q];
+                        const bool single = (m >> (st + mb - fe)) & 1ull;
+                        while (m) {
+                            const int k = __builtin_ctzll(m);
+                            m &= m - 1;
+                            const int e = fe + k;
+                            const double c = (double)s_csc[k * 64 + q] + base;
+                            if (s_st[e] == 0xFFFFFFFFu || c > s_sc[e]) {
+                                s_sc[e] = c;
+                                s_st[e] = (uint32_t)st | ((uint32_t)s_cid[k * 64 + q] << 16);
+                            }
+                        }
+                        if (!single) {
+                            const double c = T.unk_score + base;
+                            const int e = st + mb;
+                            if (s_st[e] == 0xFFFFFFFFu || c > s_sc[e]) {
+                                s_sc[e] = c;
+                                s_st[e] = (uint32_t)st | ((uint32_t)T.unk_id << 16);
+                            }
+                        }
+                    }
+                }
+                __syncthreads();
+            }
+            if (lane == 0) {
+                struct {
+                    const uint32_t *st;
+                    __device__ int start(int i) const { return st[i] == 0xFFFFFFFFu ? -1 : (int)(st[i] & 0xFFFFu); }
+                    __device__ int id(int i) const { return st[i] == 0xFFFFFFFFu ? -1 : (int)(st[i] >> 16); }
+                } nodes{s_st};
+                const int k0 = s_misc[5];
+                const int k = unigram_backtrack(n, cand, nodes, T.unk_id, [&](int x, int id) {
+                    if (k0 + x < 2 * LONG_NORM + 16) s_ids[k0 + x] = (uint16_t)id;
+                });
+                s_misc[5] = k0 + k;
+            }
+            __syncthreads();
+        }
+        if (lane == 0) {
+            int k = s_misc[5];
+            if (k > 2 * LONG_NORM + 16) {
+                atomicOr(err, 2u);
+                k = 0;
+            }
+            finalize_item(it.x, it.y, p, rec, k, [&](int j) { return (uint32_t)s_ids[j]; }, off, R, tokc, chunk_cnt,
+                          rec_local, pool, counters + 2, pool_cap, err);
+        }
+        __syncthreads();
     }
 }
 
 // Items whose normalized text exceeds a lane's scratch: one wave each, lane 0.
 __global__ __launch_bounds__(64) void k_unigram_huge(DevTok T, const uint8_t *__restrict__ text, int64_t N,
-                                                     const uint64_t *__restrict__ off, int64_t R, uint32_t *tokc,
-                                                     uint32_t *chunk_cnt, uint32_t *rec_local, uint8_t *scratch,
-                                                     uint32_t *pool, uint32_t *pool_count, uint32_t pool_cap,
-                                                     const uint4 *huge, const uint32_t *huge_count, uint32_t huge_cap,
-                                                     uint32_t *err) {
+                                                     const uint64_t *__restrict__ off, int64_t R, uint32_t *counters,
+                                                     uint32_t *tokc, uint32_t *chunk_cnt, uint32_t *rec_local,
+                                                     uint8_t *scratch, uint32_t *pool, uint32_t pool_cap,
+                                                     const uint4 *huge, uint32_t huge_cap, uint32_t *err) {
     if (lane_id() != 0) return;
-    const size_t per = (size_t)UNI_HUGE_NORM + sizeof(UniNode) * (UNI_HUGE_NORM + 8) + 4 * (2 * UNI_HUGE_NORM + 8);
-    uint8_t *mine = scratch + (size_t)blockIdx.x * per;
-    const Scratch S{mine + sizeof(UniNode) * (UNI_HUGE_NORM + 8) + 4 * (2 * UNI_HUGE_NORM + 8),
-                    reinterpret_cast<UniNode *>(mine),
-                    reinterpret_cast<uint32_t *>(mine + sizeof(UniNode) * (UNI_HUGE_NORM + 8)), UNI_HUGE_NORM};
-    uint32_t nh = *huge_count;
+    const Scratch S = make_scratch(scratch + (size_t)blockIdx.x * huge_scratch_bytes(), UNI_HUGE_NORM);
+    uint32_t nh = counters[3];
     if (nh > huge_cap) nh = huge_cap;
     for (uint32_t i = blockIdx.x; i < nh; i += gridDim.x) {
         const uint4 h = huge[i];
         const int64_t p = (int64_t)h.x * CHUNK + h.z;
-        finish_long(T, text, N, off, R, h.x, h.y, p, h.w, S, tokc, chunk_cnt, rec_local, pool, pool_count, pool_cap,
+        finish_long(T, text, N, off, R, h.x, h.y, p, h.w, S, tokc, chunk_cnt, rec_local, pool, counters + 2, pool_cap,
                     err, true);
     }
 }
 
 size_t unigram_scratch_bytes(int lane_blocks, int huge_blocks) {
-    const size_t lane = (size_t)UNI_LANE_NORM + sizeof(UniNode) * (UNI_LANE_NORM + 8) + 4 * (2 * UNI_LANE_NORM + 8);
-    const size_t huge = (size_t)UNI_HUGE_NORM + sizeof(UniNode) * (UNI_HUGE_NORM + 8) + 4 * (2 * UNI_HUGE_NORM + 8);
-    return lane * 64 * (size_t)lane_blocks + huge * (size_t)huge_blocks;
+    (void)lane_blocks;  // the long-item kernel works in LDS
+    return huge_scratch_bytes() * (size_t)huge_blocks;
 }
 
 hipError_t launch_unigram_chunks(const DevTok &T, const uint8_t *text, int64_t N, const uint64_t *off, int64_t R,
@@ -670,22 +1221,19 @@ hipError_t launch_unigram_chunks(const DevTok &T, const uint8_t *text, int64_t N
                                  uint32_t *rec_local, const UniWork &W, hipStream_t st) {
     const int64_t n_chunks = (N + CHUNK - 1) / CHUNK;
     if (n_chunks == 0) return hipSuccess;
-    hipError_t e = hipMemsetAsync(W.counters, 0, 4 * sizeof(uint32_t), st);  // long, lchunk, pool, huge
+    hipError_t e = hipMemsetAsync(W.counters, 0, 4 * sizeof(uint32_t), st);  // items, -, pool, huge
     if (e != hipSuccess) return e;
     e = hipMemsetAsync(W.err, 0, sizeof(uint32_t), st);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_unigram_chunks, dim3((unsigned)n_chunks), dim3(TOK_THREADS), 0, st, T, text, N, off, R, ranges,
-                       tokc, chunk_cnt, chunk_ent, rec_local, W.counters + 0, W.lchunks, W.counters + 1);
-    // pool word 0 stays 0 (an empty item); items allocate after it
-    e = hipMemsetAsync(W.pool, 0, sizeof(uint32_t), st);
+    e = hipMemsetAsync(W.pool, 0, sizeof(uint32_t), st);  // pool word 0: an empty item
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_unigram_long, dim3((unsigned)W.lane_blocks), dim3(64), 0, st, T, text, N, off, R, W.lchunks,
-                       W.counters + 1, chunk_ent, tokc, chunk_cnt, rec_local, W.scratch, W.pool, W.counters + 2,
-                       W.pool_cap, W.huge, W.counters + 3, W.huge_cap, W.err);
-    hipLaunchKernelGGL(k_unigram_huge, dim3((unsigned)W.huge_blocks), dim3(64), 0, st, T, text, N, off, R, tokc,
-                       chunk_cnt, rec_local, W.scratch + (size_t)W.lane_blocks * 64 *
-                           ((size_t)UNI_LANE_NORM + sizeof(UniNode) * (UNI_LANE_NORM + 8) + 4 * (2 * UNI_LANE_NORM + 8)),
-                       W.pool, W.counters + 2, W.pool_cap, W.huge, W.counters + 3, W.huge_cap, W.err);
+    hipLaunchKernelGGL(k_unigram_chunks, dim3((unsigned)n_chunks), dim3(TOK_THREADS), 0, st, T, text, N, off, R, ranges,
+                       tokc, chunk_cnt, chunk_ent, rec_local, W.counters, W.items, W.item_cap, W.err);
+    hipLaunchKernelGGL(k_unigram_long, dim3((unsigned)W.lane_blocks), dim3(64), 0, st, T, text, N, off, R, W.items,
+                       W.item_cap, W.counters, tokc, chunk_cnt, rec_local, W.pool, W.pool_cap, W.huge, W.huge_cap,
+                       W.err);
+    hipLaunchKernelGGL(k_unigram_huge, dim3((unsigned)W.huge_blocks), dim3(64), 0, st, T, text, N, off, R, W.counters,
+                       tokc, chunk_cnt, rec_local, W.scratch, W.pool, W.pool_cap, W.huge, W.huge_cap, W.err);
     return hipGetLastError();
 }
 

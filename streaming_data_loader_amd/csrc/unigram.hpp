@@ -91,58 +91,43 @@ __host__ __device__ inline int u8len_lead(uint32_t b) {
 // ---- Unigram Viterbi ------------------------------------------------------------
 // The piece is bytes [0, n) of `acc`, starting with "▁" (3 bytes).  Nodes are
 // byte positions; node e holds the best path ending at e: score (f64), start
-// and id.  `probe(s, e)` = id of the vocab piece spelling bytes [s, e) or -1
-// (the caller keys s == 0 as UC_META with payload [3, e)).  Candidates are
+// and id.  `cand(s, e, &score)` = id of the vocab piece spelling bytes [s, e)
+// (and its score) or -1; s == 0 is the "▁"-prefixed piece.  Candidates are
 // visited in tokenizers' order -- starts ascending, then lengths ascending --
 // and replace a node only when strictly better.  `maxlen` bounds piece bytes
 // (the longest vocab piece; longer substrings cannot be in the trie).
 // Writes the ids (fused unk runs looked up whole, else unk_id) in order via
-// emit(id) and returns their count.
+// emit(index, id) and returns their count.
 struct UniNode {
     double score;
     int32_t start;  // -1: unset
     int32_t id;
 };
 
-template <class Acc, class Probe, class Nodes, class Emit>
-__host__ __device__ inline int unigram_viterbi(const Acc &acc, int n, const Probe &probe, Nodes &nodes,
-                                               const double *score, double unk_score, int unk_id, int maxlen,
-                                               const Emit &emit) {
-    if (n <= 0) return 0;
-    for (int i = 0; i <= n; ++i) nodes.set(i, 0.0, -1, -1);
-    for (int st = 0; st < n;) {
-        const int mb = u8len_lead(acc(st)) < n - st ? u8len_lead(acc(st)) : n - st;
-        const double base = nodes.score(st);
-        bool single = false;
-        const int emax = st + maxlen < n ? st + maxlen : n;
-        for (int e = st + 1; e <= emax; ++e) {
-            if (e < n && (acc(e) & 0xC0u) == 0x80u) continue;  // not a char boundary
-            const int id = probe(st, e);
-            if (id < 0) continue;
-            const double cand = score[id] + base;
-            if (nodes.start(e) < 0 || cand > nodes.score(e)) nodes.set(e, cand, st, id);
-            if (e - st == mb) single = true;
-        }
-        if (!single) {
-            const double cand = unk_score + base;
-            const int e = st + mb;
-            if (nodes.start(e) < 0 || cand > nodes.score(e)) nodes.set(e, cand, st, unk_id);
-        }
-        st += mb;
-    }
-    // backtrack; consecutive unk nodes fuse into one string (looked up whole)
-    // -- emitted in order by walking the path twice: count, then write back
+// Node e's update by a candidate (st, id, score c): first set, or strictly better.
+template <class Nodes>
+__host__ __device__ inline void uni_relax(Nodes &nodes, int e, double c, int st, int id) {
+    if (nodes.start(e) < 0 || c > nodes.score(e)) nodes.set(e, c, st, id);
+}
+
+// Backtrack from node n; consecutive unk nodes fuse into one string, looked
+// up whole with cand (models/unigram/model.rs encode_optimized + tokenize).
+template <class Cand, class Nodes, class Emit>
+__host__ __device__ inline int unigram_backtrack(int n, const Cand &cand, const Nodes &nodes, int unk_id,
+                                                 const Emit &emit) {
     int count = 0;
     for (int e = n; e > 0;) {
         const int st = nodes.start(e);
+        if (st < 0) break;
         const bool u = nodes.id(e) == unk_id;
         if (!(u && st > 0 && nodes.id(st) == unk_id)) ++count;
         e = st;
     }
     int k = count;
     int run_end = -1;  // end of the unk run being extended leftwards
-    for (int e = n; e > 0;) {
+    for (int e = n; e > 0 && k > 0;) {
         const int st = nodes.start(e);
+        if (st < 0) break;
         const bool u = nodes.id(e) == unk_id;
         if (u && st > 0 && nodes.id(st) == unk_id) {  // the run continues leftwards
             if (run_end < 0) run_end = e;
@@ -150,7 +135,8 @@ __host__ __device__ inline int unigram_viterbi(const Acc &acc, int n, const Prob
             const int end = run_end >= 0 ? run_end : e;
             int id = nodes.id(e);
             if (run_end >= 0 || u) {
-                id = probe(st, end);
+                double sc;
+                id = cand(st, end, &sc);
                 if (id < 0) id = unk_id;
             }
             emit(--k, id);
@@ -159,6 +145,63 @@ __host__ __device__ inline int unigram_viterbi(const Acc &acc, int n, const Prob
         e = st;
     }
     return count;
+}
+
+template <class Acc, class Cand, class Nodes, class Emit>
+__host__ __device__ inline int unigram_viterbi(const Acc &acc, int n, const Cand &cand, Nodes &nodes,
+                                               double unk_score, int unk_id, int maxlen, const Emit &emit) {
+    if (n <= 0) return 0;
+    for (int i = 0; i <= n; ++i) nodes.set(i, 0.0, -1, -1);
+    for (int st = 0; st < n;) {
+        const int l0 = u8len_lead(acc(st));
+        const int mb = l0 < n - st ? l0 : n - st;
+        const double base = nodes.score(st);
+        bool single = false;
+        const int emax = st + maxlen < n ? st + maxlen : n;
+        for (int e = st + 1; e <= emax; ++e) {
+            if (e < n && (acc(e) & 0xC0u) == 0x80u) continue;  // not a char boundary
+            double sc;
+            const int id = cand(st, e, &sc);
+            if (id < 0) continue;
+            uni_relax(nodes, e, sc + base, st, id);
+            if (e - st == mb) single = true;
+        }
+        if (!single) uni_relax(nodes, st + mb, unk_score + base, st, unk_id);
+        st += mb;
+    }
+    return unigram_backtrack(n, cand, nodes, unk_id, emit);
+}
+
+// unigram_viterbi over precomputed candidates: rowmask(st) has bit k set when
+// the piece ending at e = first_end(st) + k exists (first_end = 3 for the
+// "▁" row st == 0, st + 1 otherwise) and at(st, e, &score) returns its id;
+// cand(st, e, &score) answers any (st, e) (the fused-unk lookup).  Same visit
+// order and result as unigram_viterbi.
+template <class Acc, class RowMask, class At, class Cand, class Nodes, class Emit>
+__host__ __device__ inline int unigram_viterbi_masked(const Acc &acc, int n, const RowMask &rowmask, const At &at,
+                                                      const Cand &cand, Nodes &nodes, double unk_score, int unk_id,
+                                                      const Emit &emit) {
+    if (n <= 0) return 0;
+    for (int i = 0; i <= n; ++i) nodes.set(i, 0.0, -1, -1);
+    for (int st = 0; st < n;) {
+        const int l0 = u8len_lead(acc(st));
+        const int mb = l0 < n - st ? l0 : n - st;
+        const double base = nodes.score(st);
+        const int fe = st == 0 ? 3 : st + 1;
+        uint64_t m = rowmask(st);
+        const bool single = (m >> (st + mb - fe)) & 1ull;
+        while (m) {
+            const int k = __builtin_ctzll(m);
+            m &= m - 1;
+            const int e = fe + k;
+            double sc;
+            const int id = at(st, e, &sc);
+            uni_relax(nodes, e, sc + base, st, id);
+        }
+        if (!single) uni_relax(nodes, st + mb, unk_score + base, st, unk_id);
+        st += mb;
+    }
+    return unigram_backtrack(n, cand, nodes, unk_id, emit);
 }
 
 }  // namespace sdl
