@@ -507,9 +507,11 @@ static VSlot make_slot(const std::string &pay, uint32_t cont, int32_t id, std::v
     return v;
 }
 
+// load <= 0.5 (two choices, one slot per bucket): the Unigram table holds
+// pieces, added tokens and the word table, and a smaller table stays in L2
 static void build_cuckoo(HostTokenizer &t, const std::vector<VSlot> &entries) {
     uint32_t slots = 1;
-    while (slots < 4 * entries.size()) slots <<= 1;
+    while (slots < 2 * entries.size()) slots <<= 1;
     for (;; slots <<= 1) {
         t.slot_mask = slots - 1;
         t.slots.assign(slots, VSlot{0, -1, 0, 0, {0}});
