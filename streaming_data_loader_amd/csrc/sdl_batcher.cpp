@@ -46,6 +46,12 @@ int fail(int code, const std::string &msg) {
 struct HipError : std::runtime_error {
     using std::runtime_error::runtime_error;
 };
+struct ArgError : std::runtime_error {
+    using std::runtime_error::runtime_error;
+};
+struct CapacityError : std::runtime_error {
+    using std::runtime_error::runtime_error;
+};
 
 template <class T>
 struct DevBuf {
@@ -337,9 +343,19 @@ struct sdl_batcher {
         HIP_TRY(hipMemcpyAsync(h2d_text.p, pin_text.p, (size_t)N, hipMemcpyHostToDevice, stream));
         HIP_TRY(hipMemcpyAsync(h2d_off.p, pin_off.p, sizeof(uint64_t) * (size_t)(R + 1), hipMemcpyHostToDevice, stream));
         run_device(h2d_text.p, N, h2d_off.p, R, cfg.first_record + n_records, stream, d_labels, d_label_off);
-        pin_u32.ensure((size_t)R + 1);
+        pin_u32.ensure((size_t)R + 3);
         HIP_TRY(hipMemcpyAsync(pin_u32.p, row_off.p, sizeof(uint32_t) * (size_t)(R + 1), hipMemcpyDeviceToHost, stream));
+        pin_u32.p[R + 1] = pin_u32.p[R + 2] = 0;
+        if (span()) HIP_TRY(hipMemcpyAsync(pin_u32.p + R + 1, span_err.p, 4, hipMemcpyDeviceToHost, stream));
+        if (dt.kind == TOK_UNIGRAM) HIP_TRY(hipMemcpyAsync(pin_u32.p + R + 2, uni_err.p, 4, hipMemcpyDeviceToHost, stream));
         HIP_TRY(hipStreamSynchronize(stream));
+        // where the reference panics (t5_data.rs:205-216: a label past S/4 or a
+        // 101st sentinel) the host path fails the call before any batch is queued
+        if (pin_u32.p[R + 1])
+            throw ArgError("span: " + std::to_string(pin_u32.p[R + 1]) +
+                           " label/sentinel writes out of range (the reference panics)");
+        if (pin_u32.p[R + 2])
+            throw CapacityError("t5 tokenizer capacity exceeded (flags " + std::to_string(pin_u32.p[R + 2]) + ")");
         const uint32_t G = pin_u32.p[R];
         const size_t S = (size_t)P.S, LW = (size_t)P.label_width;
         const bool with_tt = this->with_tt();
@@ -652,6 +668,8 @@ int sdl_batcher_push(sdl_batcher *h, const uint8_t *utf8, size_t len, const uint
         return 0;
     } catch (HipError &e) {
         return fail(SDL_ERR_HIP, e.what());
+    } catch (CapacityError &e) {
+        return fail(SDL_ERR_CAPACITY, e.what());
     } catch (std::exception &e) {
         return fail(SDL_ERR_ARG, e.what());
     }
@@ -679,6 +697,8 @@ int sdl_batcher_push_many(sdl_batcher *h, const uint8_t *arena, const uint64_t *
         return SDL_OK;
     } catch (HipError &e) {
         return fail(SDL_ERR_HIP, e.what());
+    } catch (CapacityError &e) {
+        return fail(SDL_ERR_CAPACITY, e.what());
     } catch (std::exception &e) {
         return fail(SDL_ERR_ARG, e.what());
     }

@@ -173,3 +173,13 @@ def test_span_rows_match_oracle(torch, native_lib, t5tok, records, S, B_, gap, s
     assert res.label_errors() == errs
     # rows of the last batch nobody filled keep T5Data::new's values
     assert (ids[G:] == 0).all() and (am[G:] == 1).all() and (lab[G:] == -100).all()
+
+
+def test_host_path_fails_where_the_reference_panics(native_lib, records):
+    """S=64 with tiny gaps overflows the S/4 label width: the reference panics
+    (t5_data.rs:205-216); the host path fails the call instead of emitting."""
+    gt = B.GenTokenizer(B.ModelType.T5, B.BatchConfig(4, 64), B.Span(1.0, 1.0),
+                        B.TokenizerConfig(native.T5_PROXY_TOKENIZER), chunk=True)
+    with pytest.raises(native.SDLError, match="reference panics"):
+        for t in records:
+            gt.create_sync_batch(t)
