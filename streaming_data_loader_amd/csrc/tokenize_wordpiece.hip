@@ -10,17 +10,17 @@
 // The template's [CLS]/[SEP] and the wrapper's framing are added at row
 // assembly (pipeline.hip).
 //
-// One 256-thread workgroup owns CHUNK = 4096 bytes of the arena; lane t owns
+// One wave64 workgroup owns CHUNK = 1024 bytes of the arena; lane t owns
 // bytes [c0 + 16t, c0 + 16t + 16):
 //   1. each lane loads its 16 bytes with one 16-B non-temporal load (they stay
-//      in VGPRs) and stores them into an LDS window [c0-16, c0+4096+240);
+//      in VGPRs) and stores them into an LDS window [c0-32, c0+1024+32);
 //      record starts in the window become an LDS bitmap;
 //   2. classification is register-resident: an arithmetic ASCII classifier
 //      packs 16 four-bit visible classes into one u64; only lead bytes >= 0xC0
 //      (two-level Unicode table in L2) and added-token openers take a loop;
-//   3. a block scan carries the last visible class across lanes; piece starts
+//   3. a wave scan carries the last visible class across lanes; piece starts
 //      (words, isolated chars, added tokens) are compacted into an LDS list;
-//   4. each lane WordPiece-tokenizes pieces i, i+256, ...: an ASCII word of
+//   4. each lane WordPiece-tokenizes pieces i, i+64, ...: an ASCII word of
 //      <= 16 bytes is read from LDS as 5 aligned dwords + v_alignbyte,
 //      lower-cased and classified with SWAR, and every candidate piece is one
 //      hash of 4 dwords + one 32-B probe of the L2-resident vocab table whose
