@@ -80,9 +80,9 @@ def build_stamps():
     return build(defines=("SDL_STAMPS=1",), lib=os.path.join(d, "libsdl_batcher.so"), build_dir=os.path.join(d, "obj"))
 
 
-def build_ablations(levels=(1, 3)):
+def build_ablations(levels=(1, 2, 3)):
     """Diagnostic builds with phases of the tokenize kernel compiled out
-    (SDL_ABLATE=1: no WordPiece; 3: load only) -> build/abl<N>/libsdl_batcher.so."""
+    (SDL_ABLATE=1: first probes only; 2: no WordPiece; 3: load only) -> build/abl<N>/libsdl_batcher.so."""
     out = []
     for n in levels:
         d = os.path.join(REPO, "build", f"abl{n}")

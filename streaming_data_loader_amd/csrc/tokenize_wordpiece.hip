@@ -505,6 +505,15 @@ __global__ __launch_bounds__(TOK_THREADS) void k_wordpiece_chunks(
     //     so no lane idles behind a long word.
     lds_u16 *stage = (lds_u16 *)s_stage;
     uint16_t *s_pend = s_poff;  // pending piece indices (s_poff is free until step 5)
+#if defined(SDL_ABLATE) && SDL_ABLATE == 2
+    // diagnostic: no WordPiece at all, every piece yields one id 0
+    for (int pi = tid; pi < np; pi += TOK_THREADS) {
+        stage[s_pieces[pi] & 0xFFFu] = 0;
+        s_cnt[pi] = 1;
+    }
+    __syncthreads();
+    if (np < 0) {  // never: keeps the code below compiled in
+#endif
     if (tid == 0) {
         s_scratch[TOK_THREADS / 64 + 1] = 0;  // pending count
     }
@@ -614,9 +623,17 @@ __global__ __launch_bounds__(TOK_THREADS) void k_wordpiece_chunks(
     }
     __syncthreads();
     SDL_STAMP(11);
-    const int npend = (int)s_scratch[TOK_THREADS / 64 + 1];
+    int npend = (int)s_scratch[TOK_THREADS / 64 + 1];
     if (tid == 0) s_scratch[TOK_THREADS / 64 + 1] = 0;  // becomes the queue head
     __syncthreads();
+#if defined(SDL_ABLATE) && SDL_ABLATE == 1
+    // diagnostic: first probes only; every pending piece yields one [UNK]
+    for (int q = tid; q < npend; q += TOK_THREADS) {
+        stage[s_pieces[s_pend[q]] & 0xFFFu] = (uint16_t)T.unk_id;
+        s_cnt[s_pend[q]] = 1;
+    }
+    npend = 0;
+#endif
     // (b) state machine over the pending pieces
     if (npend) {
         bool exhausted = false;
@@ -711,6 +728,9 @@ __global__ __launch_bounds__(TOK_THREADS) void k_wordpiece_chunks(
     }
     __syncthreads();
     SDL_STAMP(7);
+#if defined(SDL_ABLATE) && SDL_ABLATE == 2
+    }
+#endif
 
     // ---- 5. compact ids into this chunk's tokc slice ------------------------------
     const int per = (np + TOK_THREADS - 1) / TOK_THREADS;
