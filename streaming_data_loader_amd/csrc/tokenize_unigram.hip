@@ -44,11 +44,13 @@ enum : uint8_t { U_WS = 0, U_P = 1, U_X = 2, U_SPEC = 3, U_SPX = 4 };
 constexpr uint32_t LMARK = 0x80000000u;
 __device__ const uint8_t kMetaBytes[3] = {0xE2, 0x96, 0x81};
 
-constexpr int ARENA = 1024;         // LDS bytes for normalized medium words
+constexpr int ARENA = 768;          // LDS bytes for normalized medium words
 constexpr int WIN_PAD = WIN + 32;   // window + gather padding; the arena follows
-constexpr int VP_CAP = 384;         // Viterbi pieces per chunk
-constexpr int JOB_CAP = 256;        // words waiting for the DP
-constexpr int TASK_CAP = 1024;      // probe tasks per round
+constexpr int VP_CAP = 256;         // Viterbi pieces per chunk
+constexpr int JOB_CAP = 128;        // words waiting for the DP (more: long items)
+constexpr int TASK_CAP = 320;       // probe tasks per round (>= one job's: L <= UNI_WMAX)
+constexpr int DP_LANES = 16;
+constexpr uint8_t CNT_LONG = 0xFF;   // s_cnt of a long item        // lanes running the DP (a round holds few jobs)
 constexpr int TASK_UNROLL = 4;      // probes in flight per lane
 
 typedef __attribute__((address_space(3))) double lds_f64;
@@ -443,22 +445,22 @@ __device__ __forceinline__ void vp_decode(int t, int L, int Mm, int Mf, int *i, 
     *j = row + 1 + r;
 }
 
-// Per-lane LDS nodes (node-major: conflict-free)
+// Per-lane LDS nodes of the DP lanes (node-major: conflict-free)
 struct LdsNodes {
     lds_f64 *sc;
     lds_u32 *bp;
     int lane;
     __device__ void set(int i, double s, int st, int id) const {
-        sc[i * 64 + lane] = s;
-        bp[i * 64 + lane] = (uint32_t)(st & 0xFFFF) | ((uint32_t)(id & 0xFFFF) << 16);
+        sc[i * DP_LANES + lane] = s;
+        bp[i * DP_LANES + lane] = (uint32_t)(st & 0xFFFF) | ((uint32_t)(id & 0xFFFF) << 16);
     }
-    __device__ double score(int i) const { return sc[i * 64 + lane]; }
+    __device__ double score(int i) const { return sc[i * DP_LANES + lane]; }
     __device__ int start(int i) const {
-        const uint32_t v = bp[i * 64 + lane] & 0xFFFFu;
+        const uint32_t v = bp[i * DP_LANES + lane] & 0xFFFFu;
         return v == 0xFFFFu ? -1 : (int)v;
     }
     __device__ int id(int i) const {
-        const uint32_t v = bp[i * 64 + lane] >> 16;
+        const uint32_t v = bp[i * DP_LANES + lane] >> 16;
         return v == 0xFFFFu ? -1 : (int)v;
     }
 };
@@ -508,26 +510,30 @@ __global__ __launch_bounds__(TOK_THREADS) void k_unigram_chunks(
     uint32_t *__restrict__ chunk_ent, uint32_t *__restrict__ rec_local, uint32_t *__restrict__ counters,
     uint4 *__restrict__ items, uint32_t item_cap, uint32_t *__restrict__ err) {
     __shared__ __attribute__((aligned(16))) uint8_t s_bytes[WIN_PAD + ARENA + 32];  // window | arena
-    __shared__ __attribute__((aligned(16))) uint8_t s_cls[WIN];
+    // s_cls / s_plen / s_poff are dead during the Viterbi rounds (long-item
+    // lengths move to their stage slot), which reuse them for the DP nodes:
+    // LDS per one-wave block decides how many chunks a CU keeps in flight.
+    constexpr int U_CLS = 0, U_PLEN = (WIN + 15) & ~15, U_POFF = U_PLEN + 2 * CHUNK, U_END = U_POFF + 2 * CHUNK;
+    static_assert(DP_LANES * UNI_NODES * 12 <= U_END, "DP nodes must fit the dead arrays");
+    __shared__ __attribute__((aligned(16))) uint8_t s_u[U_END];
+    uint8_t *const s_cls = s_u + U_CLS;
     __shared__ uint32_t s_rbits[RBITS_WORDS + 1];
     __shared__ uint16_t s_pieces[CHUNK + 1];  // prel | SPEC << 12
-    __shared__ uint16_t s_plen[CHUNK];        // piece length (0 = runs past the window)
+    uint16_t *const s_plen = (uint16_t *)(s_u + U_PLEN);  // piece length (0 = runs past the window)
     __shared__ uint16_t s_stage[2 * CHUNK + 64];  // ids staged at 2 * prel
-    __shared__ uint16_t s_cnt[CHUNK];             // ids per piece, 0xFFFF = long item
-    __shared__ uint16_t s_poff[CHUNK];
+    __shared__ uint8_t s_cnt[CHUNK];              // ids per piece (<= 2 UNI_WMAX), CNT_LONG = long item
+    uint16_t *const s_poff = (uint16_t *)(s_u + U_POFF);
     __shared__ uint16_t s_rb[RB_CAP];
     __shared__ uint32_t s_scratch[16];  // 0 jobs 1 vps 2 arena used 3 medium words; 8.. scan scratch
     __shared__ uint16_t s_job_pi[JOB_CAP], s_job_vp[JOB_CAP];
     __shared__ uint8_t s_job_nvp[JOB_CAP];
-    __shared__ uint32_t s_job_tb[JOB_CAP + 1];  // task base of each job (job order)
-    __shared__ uint32_t s_job_rb[JOB_CAP + 1];  // candidate-row base of each job
-    __shared__ unsigned long long s_rowmask[TASK_CAP];  // per row: which candidate ends exist
+    __shared__ uint16_t s_job_tb[JOB_CAP + 1];  // task base of each job (job order; < 2^16)
+    __shared__ uint16_t s_job_rb[JOB_CAP + 1];  // candidate-row base of each job
+    __shared__ uint32_t s_rowmask[TASK_CAP];    // per row: which candidate ends exist (<= UNI_WMAX + 1)
     __shared__ uint16_t s_vp_src[VP_CAP];
     __shared__ uint8_t s_vp_len[VP_CAP];
     __shared__ uint16_t s_tid[TASK_CAP];
     __shared__ float s_tsc[TASK_CAP];
-    __shared__ double s_nsc[UNI_NODES * 64];
-    __shared__ uint32_t s_nbp[UNI_NODES * 64];
 
     const int tid = threadIdx.x;
     const int lane = tid;
@@ -621,7 +627,7 @@ __global__ __launch_bounds__(TOK_THREADS) void k_unigram_chunks(
 
     // ---- 3. per piece: added token / word table / medium normalization / long --
     lds_u16 *stage = (lds_u16 *)s_stage;
-    lds_u16 *cnt = (lds_u16 *)s_cnt;
+    lds_u8 *cnt = (lds_u8 *)s_cnt;
     for (int pi = tid; pi < np; pi += TOK_THREADS) {
         const uint32_t pc = s_pieces[pi];
         const int prel = (int)(pc & 0xFFFu);
@@ -662,7 +668,7 @@ __global__ __launch_bounds__(TOK_THREADS) void k_unigram_chunks(
                 if (k == 1) stage[2 * prel] = (uint16_t)x;
                 else
                     for (int j = 0; j < k; ++j) stage[2 * prel + j] = T.wres[x + j];
-                cnt[pi] = (uint16_t)k;
+                cnt[pi] = (uint8_t)k;
                 done = true;
             } else {
                 // miss: one Viterbi piece, the word's bytes in the window
@@ -686,7 +692,10 @@ __global__ __launch_bounds__(TOK_THREADS) void k_unigram_chunks(
             cnt[pi] = 0;
             done = true;
         }
-        if (!done) cnt[pi] = 0xFFFFu;  // long item: finished by k_unigram_long
+        if (!done) {  // long item: finished by k_unigram_long; its length in its stage slot
+            cnt[pi] = CNT_LONG;
+            stage[2 * prel] = (uint16_t)len;
+        }
     }
     __syncthreads();
 
@@ -769,7 +778,10 @@ __global__ __launch_bounds__(TOK_THREADS) void k_unigram_chunks(
                 }
             }
         }
-        if (!done) cnt[pi] = 0xFFFFu;  // long item: finished by k_unigram_long
+        if (!done) {  // long item: finished by k_unigram_long
+            cnt[pi] = CNT_LONG;
+            stage[2 * prel] = (uint16_t)len;
+        }
     }
     __syncthreads();
     UNI_STAMP(3);
@@ -787,18 +799,18 @@ __global__ __launch_bounds__(TOK_THREADS) void k_unigram_chunks(
             }
         const uint32_t incl = wave_incl_sum(t), rincl = wave_incl_sum(rw);
         if (j < nj) {
-            s_job_tb[j] = carry + incl - t;
-            s_job_rb[j] = rcarry + rincl - rw;
+            s_job_tb[j] = (uint16_t)(carry + incl - t);
+            s_job_rb[j] = (uint16_t)(rcarry + rincl - rw);
         }
         carry += (uint32_t)__shfl((int)incl, 63, 64);
         rcarry += (uint32_t)__shfl((int)rincl, 63, 64);
     }
     if (lane == 0) {
-        s_job_tb[nj] = carry;
-        s_job_rb[nj] = rcarry;
+        s_job_tb[nj] = (uint16_t)carry;
+        s_job_rb[nj] = (uint16_t)rcarry;
     }
     __syncthreads();
-    const LdsNodes nodes{(lds_f64 *)s_nsc, (lds_u32 *)s_nbp, lane};
+    const LdsNodes nodes{(lds_f64 *)s_u, (lds_u32 *)(s_u + DP_LANES * UNI_NODES * 8), lane};
     for (int j0 = 0; j0 < nj;) {
         // the round: jobs [j0, j1) whose tasks fit TASK_CAP (one job always does)
         int lo = j0 + 1, hi = nj;
@@ -809,7 +821,7 @@ __global__ __launch_bounds__(TOK_THREADS) void k_unigram_chunks(
         const int j1 = lo;
         const uint32_t T0 = s_job_tb[j0], RB0 = s_job_rb[j0];
         const int nt = (int)(s_job_tb[j1] - T0);
-        for (int r = lane; r < (int)(s_job_rb[j1] - RB0); r += 64) s_rowmask[r] = 0ull;
+        for (int r = lane; r < (int)(s_job_rb[j1] - RB0); r += 64) s_rowmask[r] = 0u;
         __syncthreads();
         // -- candidate rows: lane per row (one start of one piece), 4 probes in flight --
         const int nrows = (int)(s_job_rb[j1] - RB0);
@@ -832,7 +844,7 @@ __global__ __launch_bounds__(TOK_THREADS) void k_unigram_chunks(
             }
             const int L = s_vp_len[vp], src = s_vp_src[vp];
             const int i = lr - 1;  // payload start; -1: the "▁" row
-            unsigned long long mask = 0ull;
+            uint32_t mask = 0u;
             if (!(i > 0 && (bytes[src + i] & 0xC0u) == 0x80u)) {  // rows start on char boundaries
                 const int ps = i < 0 ? 0 : i;
                 const int jlo = i < 0 ? 0 : i + 1;
@@ -871,7 +883,7 @@ __global__ __launch_bounds__(TOK_THREADS) void k_unigram_chunks(
                                                     : probe_result_w3(P[u], (uint32_t)(j - ps) | (cont << 8), W[u], &w3);
                         if (id < 0) continue;
                         const int k = j - jlo;
-                        mask |= 1ull << k;
+                        mask |= 1u << k;
                         s_tid[tbr + k] = (uint16_t)id;
                         s_tsc[tbr + k] = __uint_as_float(w3);  // the slot's score (f32, exact)
                     }
@@ -882,7 +894,7 @@ __global__ __launch_bounds__(TOK_THREADS) void k_unigram_chunks(
         __syncthreads();
         UNI_STAMP(6);
         // -- DP: lane per job --
-        for (int jb = j0 + lane; jb < j1; jb += 64) {
+        for (int jb = j0 + lane; lane < DP_LANES && jb < j1; jb += DP_LANES) {
             const int pi = s_job_pi[jb];
             const int prel = (int)(s_pieces[pi] & 0xFFFu);
             int toff = (int)(s_job_tb[jb] - T0);
@@ -892,7 +904,7 @@ __global__ __launch_bounds__(TOK_THREADS) void k_unigram_chunks(
                 const int vp = s_job_vp[jb] + q;
                 const int L = s_vp_len[vp], src = s_vp_src[vp];
                 auto acc = [&](int x) -> uint32_t { return x < 3 ? kMetaBytes[x] : (uint32_t)bytes[src + x - 3]; };
-                auto rowmask = [&](int s) -> uint64_t { return s_rowmask[roff + (s == 0 ? 0 : s - 2)]; };
+                auto rowmask = [&](int s) -> uint32_t { return s_rowmask[roff + (s == 0 ? 0 : s - 2)]; };
                 auto cand = [&](int s, int e, double *sc) -> int {
                     const int loc = vp_local(s == 0 ? -1 : s - 3, e - 3, L, Mm, Mf);
                     if (loc < 0 || !((rowmask(s) >> (e - (s == 0 ? 3 : s + 1))) & 1ull)) return -1;
@@ -910,7 +922,7 @@ __global__ __launch_bounds__(TOK_THREADS) void k_unigram_chunks(
                 toff += vp_tasks(L, Mm, Mf);
                 roff += L + 1;
             }
-            cnt[pi] = (uint16_t)ktot;
+            cnt[pi] = (uint8_t)ktot;
         }
         __syncthreads();
         UNI_STAMP(7);
@@ -923,7 +935,7 @@ __global__ __launch_bounds__(TOK_THREADS) void k_unigram_chunks(
     const int a0 = tid * per < np ? tid * per : np;
     const int a1 = a0 + per < np ? a0 + per : np;
     uint32_t mine = 0;
-    for (int i = a0; i < a1; ++i) mine += s_cnt[i] == 0xFFFFu ? 1u : s_cnt[i];
+    for (int i = a0; i < a1; ++i) mine += s_cnt[i] == CNT_LONG ? 1u : s_cnt[i];
     uint32_t total;
     uint32_t base = block_excl_sum<TOK_THREADS>(mine, &total, s_scratch + 8);
     uint32_t *dst = tokc + (int64_t)blockIdx.x * UNI_STAGE;
@@ -931,9 +943,9 @@ __global__ __launch_bounds__(TOK_THREADS) void k_unigram_chunks(
         s_poff[i] = (uint16_t)base;
         const int prel = s_pieces[i] & 0xFFF;
         const int k = s_cnt[i];
-        if (k == 0xFFFF) {
+        if (k == CNT_LONG) {
             const uint32_t it = atomicAdd(&counters[0], 1u);
-            if (it < item_cap) items[it] = make_uint4((uint32_t)blockIdx.x, base, (uint32_t)prel, s_plen[i]);
+            if (it < item_cap) items[it] = make_uint4((uint32_t)blockIdx.x, base, (uint32_t)prel, s_stage[2 * prel]);
             else atomicOr(err, 8u);
             dst[base++] = LMARK;
             continue;
