@@ -12,7 +12,9 @@
 #include <fstream>
 #include <sstream>
 #include <stdexcept>
+#include <unordered_set>
 #include <unordered_map>
+#include <unordered_set>
 
 #include "json.hpp"
 #include "unigram.hpp"
@@ -816,18 +818,17 @@ static void load_unigram(const JValue &root, const std::string &data_dir, HostTo
     for (auto &a : t.added) t.max_special_len = std::max(t.max_special_len, (int)a.first.size());
     t.opener = t.added.empty() ? 0u : (uint32_t)'<';
     build_cuckoo(t, entries);  // pieces first: the word table's Viterbi probes them
-    // word table: "▁w" vocab pieces with w printable ASCII -> Viterbi("▁w") ids
+    // word table: printable-ASCII words w -> Viterbi("▁w") ids, for w = every
+    // "▁w" vocab piece and, up to UNI_WMAX bytes, w + "," and w + "." (a word
+    // is its own normalization, so any entry is exact; comma/period-ended
+    // words are the commonest word-table misses in running text)
     t.wres.clear();
     int maxw = 0;
-    for (size_t i = 0; i < nv; ++i) {
-        const std::string &s = t.pieces[i];
-        if (s.size() <= 3 || s.compare(0, 3, meta) != 0 || id_of[s] != (int)i) continue;
-        const std::string w = s.substr(3);
-        bool ascii = w.size() <= 255;
-        for (unsigned char c : w) ascii = ascii && c >= 0x21 && c <= 0x7E;
-        if (!ascii) continue;
+    std::unordered_set<std::string> in_table;
+    auto add_word = [&](const std::string &w) {
+        if (!in_table.insert(w).second) return;
         const std::vector<int> ids = unigram_encode_word(t, (const uint8_t *)w.data(), w.size());
-        if (ids.empty() || ids.size() > 127) continue;
+        if (ids.empty() || ids.size() > 127) return;
         int32_t packed;
         if (ids.size() == 1) {
             packed = (int32_t)((1u << 24) | (uint32_t)ids[0]);
@@ -837,6 +838,21 @@ static void load_unigram(const JValue &root, const std::string &data_dir, HostTo
         }
         entries.push_back(make_slot(w, UC_WORD, packed, t.vpool));
         maxw = std::max(maxw, (int)w.size());
+    };
+    std::vector<std::string> base_words;
+    for (size_t i = 0; i < nv; ++i) {
+        const std::string &s = t.pieces[i];
+        if (s.size() <= 3 || s.compare(0, 3, meta) != 0 || id_of[s] != (int)i) continue;
+        const std::string w = s.substr(3);
+        bool ascii = w.size() <= 255;
+        for (unsigned char c : w) ascii = ascii && c >= 0x21 && c <= 0x7E;
+        if (!ascii) continue;
+        add_word(w);
+        if ((int)w.size() < UNI_WMAX) base_words.push_back(w);
+    }
+    for (const std::string &w : base_words) {
+        add_word(w + ",");
+        add_word(w + ".");
     }
     if (t.wres.size() >= (1u << 24)) throw std::runtime_error("word table too large");
     t.wres.push_back(0);
