@@ -366,17 +366,20 @@ __device__ __forceinline__ int64_t record_of(const uint64_t *off, int64_t R, int
 }
 
 // End of a long item's raw word that ran past its chunk's window.
-__device__ int64_t word_end(const DevTok &T, const uint8_t *text, int64_t N, int64_t p, int64_t re) {
-    auto byte = [&](int64_t q) -> uint32_t { return text[q]; };
+template <class Byte>
+__device__ int64_t word_end_b(const DevTok &T, const Byte &byte, int64_t N, int64_t p, int64_t re) {
     auto bnd = [&](int64_t q) -> bool { return q >= re; };
     int64_t end;
     for (end = p + 1; end < re; ++end) {
-        const uint32_t b = text[end];
+        const uint32_t b = byte(end);
         if (ascii_ws(b)) break;
         int l;
         if (b == (uint32_t)'<' && T.n_special && uni_special(T, end, N, byte, bnd, &l) >= 0) break;
     }
     return end;
+}
+__device__ int64_t word_end(const DevTok &T, const uint8_t *text, int64_t N, int64_t p, int64_t re) {
+    return word_end_b(T, [&](int64_t q) -> uint32_t { return text[q]; }, N, p, re);
 }
 
 // Finishes long item (chunk c, tokc entry e, raw start p, raw length len or
@@ -987,13 +990,17 @@ __device__ Scratch make_scratch(uint8_t *mine, int cap) {
 }
 }  // namespace
 
-// Long items, one wave each: lane 0 normalizes the word into LDS and walks
-// its pieces; per piece, lanes take candidate rows (a start position each,
-// up to Mf probes, 4 in flight) and lane 0 relaxes the nodes of those 64
+// Long items, one wave each: the lanes stage the item's raw bytes (LONG_RAW
+// from just before it) in LDS, lane 0 normalizes the word from there into LDS
+// and walks its pieces; per piece, lanes take candidate rows (a start position
+// each, up to Mf probes, 4 in flight) and lane 0 relaxes the nodes of those 64
 // starts from LDS, then backtracks.  Items past LONG_NORM normalized bytes go
-// to the huge list.
-constexpr int LONG_NORM = 2048;
+// to the huge list.  KMAX bounds a row's candidate ends (max(Mm + 1, Mf));
+// the LDS footprint (~20 KB at KMAX 32) sets how many items a CU keeps in flight.
+constexpr int LONG_NORM = 512;
+constexpr int LONG_RAW = 1024;
 
+template <int KMAX>
 __global__ __launch_bounds__(64) void k_unigram_long(DevTok T, const uint8_t *__restrict__ text, int64_t N,
                                                      const uint64_t *__restrict__ off, int64_t R,
                                                      const uint4 *__restrict__ items, uint32_t item_cap,
@@ -1004,8 +1011,9 @@ __global__ __launch_bounds__(64) void k_unigram_long(DevTok T, const uint8_t *__
     __shared__ double s_sc[LONG_NORM + 8];
     __shared__ uint32_t s_st[LONG_NORM + 8];  // node start | id << 16 (0xFFFF: unset)
     __shared__ uint16_t s_ids[2 * LONG_NORM + 16];
-    __shared__ uint16_t s_cid[64 * 64];       // [k][lane]: id of row lane's k-th end
-    __shared__ float s_csc[64 * 64];
+    __shared__ uint16_t s_cid[KMAX * 64];     // [k][lane]: id of row lane's k-th end
+    __shared__ float s_csc[KMAX * 64];
+    __shared__ __attribute__((aligned(16))) uint8_t s_raw[LONG_RAW];
     __shared__ unsigned long long s_mask[64];
     __shared__ int s_misc[8];
     const int lane = lane_id();
@@ -1018,13 +1026,19 @@ __global__ __launch_bounds__(64) void k_unigram_long(DevTok T, const uint8_t *__
         const uint4 it = items[it_i];
         const int64_t p = (int64_t)it.x * CHUNK + it.z;
         const int64_t rec = record_of(off, R, p);
+        const int64_t pa = (p - 1) & ~(int64_t)15;  // staged raw bytes: [pa, pa + LONG_RAW)
+        *reinterpret_cast<uint4 *>(s_raw + 16 * lane) = load16(text, pa + 16 * lane, N);
+        __syncthreads();
         if (lane == 0) {
             const int64_t rs = (int64_t)off[rec];
             const int64_t re = (int64_t)off[rec + 1] < N ? (int64_t)off[rec + 1] : N;
-            const int64_t end = it.w ? p + it.w : word_end(T, text, N, p, re);
+            const lds_u8 *raw = (const lds_u8 *)s_raw;
+            auto byte = [&](int64_t q) -> uint32_t {
+                return (uint64_t)(q - pa) < (uint64_t)LONG_RAW ? (uint32_t)raw[q - pa] : (uint32_t)text[q];
+            };
+            const int64_t end = it.w ? p + it.w : word_end_b(T, byte, N, p, re);
             int nl = 0;
-            auto byte = [&](int64_t q) -> uint32_t { return text[q]; };
-            const bool ok = normalize_span(T, byte, p, end, p > rs && text[p - 1] == (uint8_t)' ',
+            const bool ok = normalize_span(T, byte, p, end, p > rs && byte(p - 1) == (uint32_t)' ',
                                            [&](uint32_t x) -> bool {
                                                if (nl >= LONG_NORM) return false;
                                                nb[nl++] = (uint8_t)x;
@@ -1138,7 +1152,7 @@ __global__ __launch_bounds__(64) void k_unigram_long(DevTok T, const uint8_t *__
                             const int k = i < 0 ? j : j - i - 1;
                             mask |= 1ull << k;
                             s_cid[k * 64 + lane] = (uint16_t)id;
-                            s_csc[k * 64 + lane] = T.uscore32[id];
+                            s_csc[k * 64 + lane] = T.uscore32[id];  // k < KMAX (host-checked)
                         }
                     }
                 }
@@ -1241,9 +1255,15 @@ hipError_t launch_unigram_chunks(const DevTok &T, const uint8_t *text, int64_t N
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_unigram_chunks, dim3((unsigned)n_chunks), dim3(TOK_THREADS), 0, st, T, text, N, off, R, ranges,
                        tokc, chunk_cnt, chunk_ent, rec_local, W.counters, W.items, W.item_cap, W.err);
-    hipLaunchKernelGGL(k_unigram_long, dim3((unsigned)W.lane_blocks), dim3(64), 0, st, T, text, N, off, R, W.items,
-                       W.item_cap, W.counters, tokc, chunk_cnt, rec_local, W.pool, W.pool_cap, W.huge, W.huge_cap,
-                       W.err);
+    // a row's candidate ends: <= Mm + 1 ("▁" row) or <= Mf
+    if (T.maxlen_meta + 1 <= 32 && T.maxlen_first <= 32)
+        hipLaunchKernelGGL(k_unigram_long<32>, dim3((unsigned)W.lane_blocks), dim3(64), 0, st, T, text, N, off, R,
+                           W.items, W.item_cap, W.counters, tokc, chunk_cnt, rec_local, W.pool, W.pool_cap, W.huge,
+                           W.huge_cap, W.err);
+    else
+        hipLaunchKernelGGL(k_unigram_long<64>, dim3((unsigned)W.lane_blocks), dim3(64), 0, st, T, text, N, off, R,
+                           W.items, W.item_cap, W.counters, tokc, chunk_cnt, rec_local, W.pool, W.pool_cap, W.huge,
+                           W.huge_cap, W.err);
     hipLaunchKernelGGL(k_unigram_huge, dim3((unsigned)W.huge_blocks), dim3(64), 0, st, T, text, N, off, R, W.counters,
                        tokc, chunk_cnt, rec_local, W.scratch, W.pool, W.pool_cap, W.huge, W.huge_cap, W.err);
     return hipGetLastError();
