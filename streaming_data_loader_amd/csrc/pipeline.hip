@@ -256,8 +256,10 @@ __device__ __forceinline__ int32_t frame_id(const int32_t (&a)[MAX_FRAME], int k
 // plane store is one 16-byte write per lane.
 //
 // Marks the k smallest (key, position) pairs of a row held as key[m][w]: a
-// 32-step radix select of the k-th smallest key with wave ballots, then a
-// position-ordered tie-break among keys equal to it.
+// radix select of the k-th smallest key with wave ballots, then a
+// position-ordered tie-break among keys equal to it.  The descent stops as soon
+// as exactly k keys lie below the candidate (after ~log2(S) + 2 of the 32
+// steps for distinct keys), which selects the same set.
 template <int MR>
 __device__ __forceinline__ void select_k_smallest(const uint32_t (&key)[MR][4], int k, bool (&sel)[MR][4]) {
     if (k <= 0) {
@@ -275,6 +277,13 @@ __device__ __forceinline__ void select_k_smallest(const uint32_t (&key)[MR][4], 
         for (int m = 0; m < MR; ++m)
 #pragma unroll
             for (int w = 0; w < 4; ++w) c += __popcll(__ballot(key[m][w] < cand));
+        if (c == k) {  // exactly the k smallest keys lie below cand: no tie to break
+#pragma unroll
+            for (int m = 0; m < MR; ++m)
+#pragma unroll
+                for (int w = 0; w < 4; ++w) sel[m][w] = key[m][w] < cand;
+            return;
+        }
         if (c < k) prefix = cand;
     }
     int c_lt = 0;
