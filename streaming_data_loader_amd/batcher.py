@@ -144,17 +144,39 @@ class DataSet:
         return {"input_ids": self.input_ids, "attention_mask": self.attention_mask, "labels": self.labels}
 
 
+class _BatchOwner:
+    """Keeps a finished sdl_batch alive while numpy views of its planes exist;
+    the batch's pinned block returns to the handle's pool when the last view
+    goes (sdl_batch_release)."""
+    __slots__ = ("b",)
+
+    def __init__(self, b):
+        self.b = b
+
+    def __del__(self):
+        try:
+            native.load().sdl_batch_release(ctypes.byref(self.b))
+        except Exception:  # interpreter shutdown
+            pass
+
+
 def _dataset_from(b: native.Batch, kind: str) -> DataSet:
+    """Zero-copy: the DataSet's arrays are views of the batch's pinned planes
+    (the D2H wrote them there directly)."""
+    b = native.Batch.from_buffer_copy(b)  # callers reuse their sdl_batch struct
     B, S, LW = b.batch_size, b.sequence_length, b.label_width
+    owner = _BatchOwner(b)
 
-    def arr(ptr, n, cols):
-        return np.ctypeslib.as_array(ptr, shape=(n * cols,)).reshape(n, cols).copy()
+    def arr(ptr, n, cols, ctype, dtype):
+        buf = (ctype * (n * cols)).from_address(ctypes.cast(ptr, ctypes.c_void_p).value)
+        buf._owner = owner
+        return np.frombuffer(buf, dtype=dtype).reshape(n, cols)
 
-    labels = arr(b.labels_f32, B, LW) if bool(b.labels_f32) else arr(b.labels, B, LW)
-    ds = DataSet(kind=kind, rows=b.rows, input_ids=arr(b.input_ids, B, S), attention_mask=arr(b.attention_mask, B, S),
-                 labels=labels, token_type_ids=arr(b.token_type_ids, B, S) if bool(b.token_type_ids) else None)
-    native.load().sdl_batch_release(ctypes.byref(b))
-    return ds
+    i32 = (ctypes.c_int32, np.int32)
+    labels = arr(b.labels_f32, B, LW, ctypes.c_float, np.float32) if bool(b.labels_f32) else arr(b.labels, B, LW, *i32)
+    return DataSet(kind=kind, rows=b.rows, input_ids=arr(b.input_ids, B, S, *i32),
+                   attention_mask=arr(b.attention_mask, B, S, *i32), labels=labels,
+                   token_type_ids=arr(b.token_type_ids, B, S, *i32) if bool(b.token_type_ids) else None)
 
 
 # ---- SimpleTransport (models/simple_transport.rs, simple_label.rs) ----------------
@@ -283,10 +305,10 @@ class GenTokenizer(_NativeBatcher):
     def create_sync_batches(self, texts):
         """create_sync_batch over many records in one device pass; returns the
         batches the same sequence of calls would have emitted, in order."""
-        blobs = [t.encode("utf-8") if isinstance(t, str) else bytes(t) for t in texts]
+        blobs = [t.encode("utf-8") if isinstance(t, str) else t for t in texts]
         offs = np.zeros(len(blobs) + 1, np.uint64)
-        np.cumsum([len(x) for x in blobs], out=offs[1:])
-        arena = np.frombuffer(b"".join(blobs) + b"\0" * 16, np.uint8)
+        np.cumsum(np.fromiter(map(len, blobs), np.uint64, len(blobs)), out=offs[1:])
+        arena = np.frombuffer(b"".join(blobs), np.uint8)  # the C side stages (and pads) it
         return self.push_arena(arena, offs)
 
 

@@ -89,6 +89,17 @@ struct RowOut {
 hipError_t launch_row_map(const uint32_t *row_off, int64_t R, uint32_t *row_rec, hipStream_t st);
 
 // BertData::put_data + mask_batch for every row (models/bert_data.rs:40-89)
+// pipeline.hip: device rows -> finished batches in pinned host memory (the
+// host path's D2H).  Segment i copies rows [g0, g0 + n) of every plane to row
+// dst of its batch's planes (device-visible host pointers; unused planes null).
+struct RowSeg {
+    int32_t *ids, *am, *tt, *lab;  // batch planes (host memory, device-mapped)
+    uint32_t g0, n, dst, pad;
+};
+hipError_t launch_rows_to_host(const RowSeg *segs, int n_segs, uint32_t rows_per_seg_max, const int32_t *ids,
+                               const int32_t *am, const int32_t *tt, const int32_t *lab, int S, int LW,
+                               hipStream_t st);
+
 hipError_t launch_rows(const RowParams &P, const uint32_t *tok, const uint32_t *rec_tok, const uint32_t *rec_cnt,
                        const uint32_t *row_off, const uint32_t *row_rec, const uint32_t *d_rows, int64_t rows_cap,
                        RowOut out, hipStream_t st);

@@ -447,6 +447,44 @@ __global__ __launch_bounds__(256) void k_rows(RowParams P, const uint32_t *__res
     }
 }
 
+// ---------------------------------------------------------------------------
+// The host path's D2H: one launch copies every segment's rows of all planes
+// straight into the batches' pinned blocks (device-mapped host memory), 16-B
+// stores per lane, instead of one hipMemcpyAsync per plane per batch segment.
+// Block (seg, y) copies rows y, y + gridDim.y, ... of segment seg; its four
+// waves take the four planes.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_rows_to_host(const RowSeg *__restrict__ segs, const int32_t *__restrict__ ids,
+                                                      const int32_t *__restrict__ am, const int32_t *__restrict__ tt,
+                                                      const int32_t *__restrict__ lab, int S, int LW) {
+    const RowSeg sg = segs[blockIdx.x];
+    const int plane = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63);
+    const int32_t *src = plane == 0 ? ids : plane == 1 ? am : plane == 2 ? tt : lab;
+    int32_t *dst = plane == 0 ? sg.ids : plane == 1 ? sg.am : plane == 2 ? sg.tt : sg.lab;
+    if (!src || !dst) return;
+    const int W = plane == 3 ? LW : S;  // ints per row
+    const bool vec = (W & 3) == 0;
+    for (uint32_t r = blockIdx.y; r < sg.n; r += gridDim.y) {
+        const int32_t *s = src + (size_t)(sg.g0 + r) * W;
+        int32_t *d = dst + (size_t)(sg.dst + r) * W;
+        if (vec) {
+            for (int j = 4 * lane; j < W; j += 256)
+                *reinterpret_cast<int4 *>(d + j) = *reinterpret_cast<const int4 *>(s + j);
+        } else {
+            for (int j = lane; j < W; j += 64) d[j] = s[j];
+        }
+    }
+}
+
+hipError_t launch_rows_to_host(const RowSeg *segs, int n_segs, uint32_t rows_per_seg_max, const int32_t *ids,
+                               const int32_t *am, const int32_t *tt, const int32_t *lab, int S, int LW,
+                               hipStream_t st) {
+    if (n_segs <= 0) return hipSuccess;
+    const unsigned gy = rows_per_seg_max < 64u ? (rows_per_seg_max ? rows_per_seg_max : 1u) : 64u;
+    hipLaunchKernelGGL(k_rows_to_host, dim3((unsigned)n_segs, gy), dim3(256), 0, st, segs, ids, am, tt, lab, S, LW);
+    return hipGetLastError();
+}
+
 hipError_t launch_rows(const RowParams &P, const uint32_t *tok, const uint32_t *rec_tok, const uint32_t *rec_cnt,
                        const uint32_t *row_off, const uint32_t *row_rec, const uint32_t *d_rows, int64_t rows_cap,
                        RowOut out, hipStream_t st) {

@@ -13,13 +13,17 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdlib>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <deque>
 #include <memory>
+#include <mutex>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/sdl_batcher.h"
@@ -87,21 +91,137 @@ struct PinBuf {
     }
 };
 
-// One DataSet being filled (BertData / GptData): initial values from
-// BatchConfig::create_vector (batcher.rs:17-22) and BertData::new (bert_data.rs:27-38).
-struct HostBatch {
-    std::vector<int32_t> ids, am, tt, lab;
-    std::vector<float> f32;  // MultiLabel: [B, number_labels]
-    int rows = 0;
-    int B, S, LW;
-    HostBatch(int B_, int S_, int LW_, bool with_tt, bool multi) : B(B_), S(S_), LW(LW_) {
-        ids.assign((size_t)B * S, 0);
-        am.assign((size_t)B * S, 1);
-        if (with_tt) tt.assign((size_t)B * S, 0);
-        if (multi) f32.assign((size_t)B * LW, 0.f);
-        else lab.assign((size_t)B * LW, -100);
+// Pinned blocks holding finished batches, recycled: the device rows are copied
+// straight into them (one D2H per plane per batch segment, no host re-copy),
+// and a block returns here when its batch is released -- possibly after the
+// handle is gone, so batches share ownership of the pool.
+struct BatchPool {
+    struct Block {
+        void *host, *dev;  // dev: the device-mapped address (k_rows_to_host writes there)
+    };
+    std::mutex mu;
+    std::vector<Block> free_;
+    size_t bytes;
+    size_t fresh = 0;  // blocks allocated so far
+    explicit BatchPool(size_t b) : bytes(b) {}
+    Block get() {
+        {
+            std::lock_guard<std::mutex> g(mu);
+            if (!free_.empty()) {
+                const Block b = free_.back();
+                free_.pop_back();
+                return b;
+            }
+        }
+        Block b{nullptr, nullptr};
+        HIP_TRY(hipHostMalloc(&b.host, bytes, hipHostMallocDefault));
+        if (hipHostGetDevicePointer(&b.dev, b.host, 0) != hipSuccess) {
+            (void)hipHostFree(b.host);
+            throw HipError("hipHostGetDevicePointer failed");
+        }
+        std::lock_guard<std::mutex> g(mu);
+        ++fresh;
+        return b;
+    }
+    void put(const Block &b) {
+        std::lock_guard<std::mutex> g(mu);
+        free_.push_back(b);
+    }
+    ~BatchPool() {
+        for (const Block &b : free_) (void)hipHostFree(b.host);
     }
 };
+
+// One DataSet being filled (BertData / GptData), planes in one pinned block.
+// Rows [rows, B) get the initial values of BatchConfig::create_vector
+// (batcher.rs:17-22) and BertData::new (bert_data.rs:27-38) when the batch is
+// handed out (init_tail): filled rows are written once, by the D2H.
+struct HostBatch {
+    std::shared_ptr<BatchPool> pool;
+    void *block = nullptr;
+    char *dev = nullptr;  // the block's device-mapped address (k_rows_to_host writes there)
+    int32_t *ids = nullptr, *am = nullptr, *tt = nullptr, *lab = nullptr;
+    float *f32 = nullptr;  // MultiLabel: [B, number_labels]
+    int rows = 0;
+    int B, S, LW;
+    static size_t block_bytes(int B, int S, int LW, bool with_tt) {
+        return 4 * (size_t)B * ((size_t)S * (with_tt ? 3 : 2) + (size_t)LW);
+    }
+    HostBatch(std::shared_ptr<BatchPool> pl, int B_, int S_, int LW_, bool with_tt, bool multi)
+        : pool(std::move(pl)), B(B_), S(S_), LW(LW_) {
+        const BatchPool::Block bl = pool->get();
+        block = bl.host;
+        dev = static_cast<char *>(bl.dev);
+        int32_t *q = static_cast<int32_t *>(block);
+        const size_t BS = (size_t)B * S;
+        ids = q;
+        am = q + BS;
+        q += 2 * BS;
+        if (with_tt) {
+            tt = q;
+            q += BS;
+        }
+        if (multi) f32 = reinterpret_cast<float *>(q);
+        else lab = q;
+    }
+    template <class T>
+    int32_t *on_dev(T *host_plane) const {
+        return host_plane ? reinterpret_cast<int32_t *>(dev + ((char *)host_plane - (char *)block)) : nullptr;
+    }
+    HostBatch(const HostBatch &) = delete;
+    HostBatch &operator=(const HostBatch &) = delete;
+    void init_tail() {
+        const size_t r0 = (size_t)rows, r1 = (size_t)B;
+        if (r0 >= r1) return;
+        std::fill(ids + r0 * S, ids + r1 * S, 0);
+        std::fill(am + r0 * S, am + r1 * S, 1);
+        if (tt) std::fill(tt + r0 * S, tt + r1 * S, 0);
+        if (lab) std::fill(lab + r0 * LW, lab + r1 * LW, -100);
+        if (f32) std::fill(f32 + r0 * LW, f32 + r1 * LW, 0.f);
+    }
+    ~HostBatch() { pool->put(BatchPool::Block{block, dev}); }
+};
+
+// SDL_HOST_TIMING=1: wall-clock split of the host path on stderr (diagnostic)
+struct HostClock {
+    bool on;
+    std::chrono::steady_clock::time_point t;
+    std::string s;
+    HostClock() : on(std::getenv("SDL_HOST_TIMING") != nullptr), t(std::chrono::steady_clock::now()) {}
+    void lap(const char *name) {
+        if (!on) return;
+        const auto n = std::chrono::steady_clock::now();
+        s += std::string(" ") + name + "=" +
+             std::to_string(std::chrono::duration<double, std::milli>(n - t).count()) + "ms";
+        t = n;
+    }
+    void report(int64_t N, size_t segs, size_t fresh) const {
+        if (on)
+            fprintf(stderr, "[host] %lld B, %zu segments, %zu pinned blocks so far:%s\n", (long long)N, segs, fresh,
+                    s.c_str());
+    }
+};
+
+// memcpy of a large host buffer on several threads (pageable -> pinned staging)
+void par_copy(void *dst, const void *src, size_t n) {
+    const size_t kMin = (size_t)8 << 20;
+    unsigned T = std::thread::hardware_concurrency();
+    T = T < 1 ? 1 : T > 8 ? 8 : T;
+    if (n < kMin || T == 1) {
+        std::memcpy(dst, src, n);
+        return;
+    }
+    const size_t per = (n / T + 4095) & ~(size_t)4095;
+    std::vector<std::thread> th;
+    for (unsigned t = 1; t < T; ++t) {
+        const size_t a = per * t;
+        if (a >= n) break;
+        const size_t b = std::min(n, a + per);
+        th.emplace_back([=] { std::memcpy((char *)dst + a, (const char *)src + a, b - a); });
+    }
+    std::memcpy(dst, src, std::min(n, per));
+    for (auto &x : th) x.join();
+}
 
 const char *kStageNames[] = {"chunk_ranges", "tokenize", "scan_chunks", "compact_tokens", "records", "scan_rows", "rows"};
 constexpr int kStages = 7;
@@ -158,8 +278,9 @@ struct sdl_batcher {
     PinBuf<uint8_t> pin_text;
     PinBuf<uint64_t> pin_off;
     PinBuf<uint32_t> pin_u32;
-    PinBuf<int32_t> pin_rows;
     PinBuf<uint32_t> pin_labels;
+    PinBuf<RowSeg> seg_pin;
+    DevBuf<RowSeg> seg_dev;
     PinBuf<uint64_t> pin_label_off;
     uint64_t n_records = 0;
 
@@ -194,7 +315,11 @@ struct sdl_batcher {
     bool span() const { return P.task == SDL_TASK_SPAN; }
     bool with_tt() const { return P.task == SDL_TASK_MLM || P.task == SDL_TASK_MULTI_LABEL; }
 
-    HostBatch *new_batch() const { return new HostBatch(P.B, P.S, P.label_width, with_tt(), multi()); }
+    std::shared_ptr<BatchPool> pool;
+    HostBatch *new_batch() {
+        if (!pool) pool = std::make_shared<BatchPool>(HostBatch::block_bytes(P.B, P.S, P.label_width, with_tt()));
+        return new HostBatch(pool, P.B, P.S, P.label_width, with_tt(), multi());
+    }
 
     int64_t rows_capacity(int64_t N, int64_t R) const {
         // rows <= sum_r ceil((ids_r + frame) / S) with ids_r <= bytes_r
@@ -336,19 +461,23 @@ struct sdl_batcher {
         }
         pin_text.ensure((size_t)N + 16);
         pin_off.ensure((size_t)R + 1);
-        std::memcpy(pin_text.p, arena, (size_t)N);
+        HostClock hc;
+        par_copy(pin_text.p, arena, (size_t)N);
+        hc.lap("stage");
         std::memcpy(pin_off.p, offsets, sizeof(uint64_t) * (size_t)(R + 1));
         h2d_text.ensure((size_t)N + 16);
         h2d_off.ensure((size_t)R + 1);
         HIP_TRY(hipMemcpyAsync(h2d_text.p, pin_text.p, (size_t)N, hipMemcpyHostToDevice, stream));
         HIP_TRY(hipMemcpyAsync(h2d_off.p, pin_off.p, sizeof(uint64_t) * (size_t)(R + 1), hipMemcpyHostToDevice, stream));
         run_device(h2d_text.p, N, h2d_off.p, R, cfg.first_record + n_records, stream, d_labels, d_label_off);
+        hc.lap("enqueue");
         pin_u32.ensure((size_t)R + 3);
         HIP_TRY(hipMemcpyAsync(pin_u32.p, row_off.p, sizeof(uint32_t) * (size_t)(R + 1), hipMemcpyDeviceToHost, stream));
         pin_u32.p[R + 1] = pin_u32.p[R + 2] = 0;
         if (span()) HIP_TRY(hipMemcpyAsync(pin_u32.p + R + 1, span_err.p, 4, hipMemcpyDeviceToHost, stream));
         if (dt.kind == TOK_UNIGRAM) HIP_TRY(hipMemcpyAsync(pin_u32.p + R + 2, uni_err.p, 4, hipMemcpyDeviceToHost, stream));
         HIP_TRY(hipStreamSynchronize(stream));
+        hc.lap("h2d+kernels");
         // where the reference panics (t5_data.rs:205-216: a label past S/4 or a
         // 101st sentinel) the host path fails the call before any batch is queued
         if (pin_u32.p[R + 1])
@@ -356,43 +485,52 @@ struct sdl_batcher {
                            " label/sentinel writes out of range (the reference panics)");
         if (pin_u32.p[R + 2])
             throw CapacityError("t5 tokenizer capacity exceeded (flags " + std::to_string(pin_u32.p[R + 2]) + ")");
-        const uint32_t G = pin_u32.p[R];
         const size_t S = (size_t)P.S, LW = (size_t)P.label_width;
-        const bool with_tt = this->with_tt();
-        const size_t planes = with_tt ? 3 : 2;
-        pin_rows.ensure((size_t)G * (planes * S + LW) + 1);
-        int32_t *h_ids = pin_rows.p, *h_am = h_ids + (size_t)G * S, *h_tt = h_am + (size_t)G * S;
-        int32_t *h_lab = h_am + (size_t)G * S * (planes - 1);
-        if (G) {
-            HIP_TRY(hipMemcpyAsync(h_ids, o_ids.p, sizeof(int32_t) * G * S, hipMemcpyDeviceToHost, stream));
-            HIP_TRY(hipMemcpyAsync(h_am, o_am.p, sizeof(int32_t) * G * S, hipMemcpyDeviceToHost, stream));
-            if (with_tt) HIP_TRY(hipMemcpyAsync(h_tt, o_tt.p, sizeof(int32_t) * G * S, hipMemcpyDeviceToHost, stream));
-            HIP_TRY(hipMemcpyAsync(h_lab, multi() ? (const void *)o_f32.p : (const void *)o_lab.p, 4 * G * LW,
-                                   hipMemcpyDeviceToHost, stream));
-            HIP_TRY(hipStreamSynchronize(stream));
-        }
-        // GenTokenizer::create_sync_batch per record (gen_batcher.rs:69-94)
+        // GenTokenizer::create_sync_batch per record (gen_batcher.rs:69-94):
+        // rows fill the back batch (handle_internal_batch per chunk), at most
+        // one finished batch is emitted per record.  Each run of rows landing
+        // contiguously in one batch is one segment, copied D2H below.
+        struct Seg {
+            HostBatch *b;
+            uint32_t dst, g0, n;
+        };
+        std::vector<Seg> segs;
         for (int64_t r = 0; r < R; ++r) {
             const uint32_t g0 = pin_u32.p[r], g1 = pin_u32.p[r + 1];
-            for (uint32_t g = g0; g < g1; ++g) {  // handle_internal_batch per chunk
+            for (uint32_t g = g0; g < g1; ++g) {
                 HostBatch *b = store.back();
-                const size_t dst = (size_t)b->rows;
-                std::memcpy(&b->ids[dst * S], h_ids + (size_t)g * S, S * 4);
-                std::memcpy(&b->am[dst * S], h_am + (size_t)g * S, S * 4);
-                if (with_tt) std::memcpy(&b->tt[dst * S], h_tt + (size_t)g * S, S * 4);
-                std::memcpy(multi() ? (void *)&b->f32[dst * LW] : (void *)&b->lab[dst * LW], h_lab + (size_t)g * LW,
-                            LW * 4);
+                if (!segs.empty() && segs.back().b == b && segs.back().g0 + segs.back().n == g) ++segs.back().n;
+                else segs.push_back(Seg{b, (uint32_t)b->rows, g, 1u});
                 b->rows++;
                 if (b->rows == P.B) store.push_back(new_batch());
             }
-            int emitted = 0;
             if (!store.empty() && store.front()->rows == P.B) {  // at most one batch per call
                 outbox.push_back(store.front());
                 store.pop_front();
-                emitted = 1;
             }
-            (void)emitted;
         }
+        hc.lap("cadence");
+        if (!segs.empty()) {
+            seg_pin.ensure(segs.size());
+            uint32_t nmax = 0;
+            for (size_t i = 0; i < segs.size(); ++i) {
+                const Seg &q = segs[i];
+                HostBatch *b = q.b;
+                seg_pin.p[i] = RowSeg{b->on_dev(b->ids), b->on_dev(b->am), b->on_dev(b->tt),
+                                      b->on_dev(multi() ? (int32_t *)b->f32 : b->lab), q.g0, q.n, q.dst, 0u};
+                nmax = std::max(nmax, q.n);
+            }
+            seg_dev.ensure(segs.size());
+            HIP_TRY(hipMemcpyAsync(seg_dev.p, seg_pin.p, sizeof(RowSeg) * segs.size(), hipMemcpyHostToDevice, stream));
+            HIP_TRY(launch_rows_to_host(seg_dev.p, (int)segs.size(), nmax, o_ids.p, o_am.p,
+                                        with_tt() ? o_tt.p : nullptr,
+                                        multi() ? reinterpret_cast<const int32_t *>(o_f32.p) : o_lab.p, P.S,
+                                        P.label_width, stream));
+        }
+        hc.lap("d2h enqueue");
+        if (!segs.empty()) HIP_TRY(hipStreamSynchronize(stream));
+        hc.lap("d2h");
+        hc.report(N, segs.size(), pool ? pool->fresh : 0);
         n_records += (uint64_t)R;
     }
 };
@@ -405,11 +543,12 @@ void fill_batch(const sdl_batcher *h, HostBatch *b, sdl_batch *out) {
     out->batch_size = b->B;
     out->sequence_length = b->S;
     out->label_width = b->LW;
-    out->input_ids = b->ids.data();
-    out->attention_mask = b->am.data();
-    out->token_type_ids = b->tt.empty() ? nullptr : b->tt.data();
-    out->labels = b->lab.empty() ? nullptr : b->lab.data();
-    out->labels_f32 = b->f32.empty() ? nullptr : b->f32.data();
+    b->init_tail();
+    out->input_ids = b->ids;
+    out->attention_mask = b->am;
+    out->token_type_ids = b->tt;
+    out->labels = b->lab;
+    out->labels_f32 = b->f32;
     out->owner_ = b;
     (void)h;
 }

@@ -78,6 +78,27 @@ def test_push_many_matches_per_record(native_lib, records):
     np.testing.assert_array_equal(fa.labels, fb.labels)
 
 
+def test_batch_views_survive_block_recycling(native_lib, records):
+    """DataSet arrays are zero-copy views of pinned batch blocks the handle
+    recycles once a batch is released: live batches must never be reused."""
+    g = B.GenTokenizer(B.ModelType.Bert, B.BatchConfig(4, 128), B.Mask(19, 103), B.TokenizerConfig(), seed=9)
+    first = g.create_sync_batches(records)
+    assert len(first) > 4
+    ptrs = {ds.input_ids.ctypes.data for ds in first}
+    assert len(ptrs) == len(first)  # one block per live batch
+    keep = first[::2]
+    snap = [(ds.input_ids.copy(), ds.attention_mask.copy(), ds.token_type_ids.copy(), ds.labels.copy()) for ds in keep]
+    del first
+    for _ in range(3):  # released blocks get reused by these calls
+        more = g.create_sync_batches(records)
+        del more
+    for ds, (i, a, t, l) in zip(keep, snap):
+        np.testing.assert_array_equal(ds.input_ids, i)
+        np.testing.assert_array_equal(ds.attention_mask, a)
+        np.testing.assert_array_equal(ds.token_type_ids, t)
+        np.testing.assert_array_equal(ds.labels, l)
+
+
 def test_b1_cadence_drops_like_reference(native_lib, records, oracle_tok):
     """B=1 (the reference's test config): a record yielding k rows queues k
     batches, only one is emitted per call and one on flush (gen_batcher.rs:86-91)."""
