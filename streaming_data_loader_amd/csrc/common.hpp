@@ -23,6 +23,7 @@ constexpr int HALO_R = 32;                        // look-ahead bytes staged in 
 constexpr int WIN = HALO_L + CHUNK + HALO_R;      // 1088 bytes of text in LDS
 constexpr int STAGE = CHUNK + 128;                // token slots per chunk (>= tokens owned)
 constexpr int TOK_UNROLL = 4;                     // first probes in flight per lane
+constexpr int PEND_CAP = 512;                     // WordPiece pieces pending the state machine (LDS)
 constexpr int RB_CAP = 256;                       // record starts listed in LDS per window
 constexpr int MAX_WORD_CHARS = 100;               // WordPiece max_input_chars_per_word
 constexpr int MAX_WORD_BYTES = 4 * MAX_WORD_CHARS + 8;

@@ -244,24 +244,17 @@ __device__ bool normalize_w16(const Ctx &C, int64_t p, int64_t rec_end, bool iso
     return true;
 }
 
-// Record end (first record start > p) for the general paths.
-__device__ int64_t rec_end_of(const Ctx &C, const lds_u16 *rb, int nrb, bool rb_ok, int64_t rb_next, int64_t p) {
-    if (rb_ok) {
-        const int rel = (int)(p - C.w0);
-        int lo = 0, hi = nrb;
-        while (lo < hi) {
-            const int mid = (lo + hi) >> 1;
-            if ((int)rb[mid] <= rel) lo = mid + 1; else hi = mid;
-        }
-        return lo < nrb ? C.w0 + rb[lo] : rb_next;
+// Record end (first record start > p, p in the window) for the general paths:
+// the next bit of the window's record-start bitmap, else the first start past
+// the window (rb_next).
+__device__ int64_t rec_end_of(const Ctx &C, int64_t rb_next, int64_t p) {
+    const int b = (int)(p - C.w0) + 1;
+    for (int wd = b >> 5; wd < RBITS_WORDS; ++wd) {
+        uint32_t m = C.rbits[wd];
+        if (wd == (b >> 5)) m &= ~0u << (b & 31);
+        if (m) return C.w0 + 32 * wd + __builtin_ctz(m);
     }
-    int64_t lo = 0, hi = C.R;
-    while (lo < hi) {
-        const int64_t mid = (lo + hi) >> 1;
-        if ((int64_t)C.off[mid] <= p) lo = mid + 1; else hi = mid;
-    }
-    const int64_t e = (int64_t)C.off[lo];
-    return e < C.N ? e : C.N;
+    return rb_next;
 }
 
 }  // namespace
@@ -285,7 +278,12 @@ __device__ unsigned long long sdl_phase_cycles[16];
     } while (0)
 #endif
 
-__global__ __launch_bounds__(TOK_THREADS) void k_wordpiece_chunks(
+// Waves per SIMD the register budget is cut to (LDS admits 5 at 7.6 KB per
+// one-wave block; measured: tools/variants.sh).
+#ifndef SDL_WP_WAVES
+#define SDL_WP_WAVES 5
+#endif
+__global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL_WP_WAVES, 8))) void k_wordpiece_chunks(
     DevTok T, const uint8_t *__restrict__ text, int64_t N, const uint64_t *__restrict__ off, int64_t R,
     const uint32_t *__restrict__ ranges, uint32_t *__restrict__ tokc, uint32_t *__restrict__ chunk_cnt,
     uint32_t *__restrict__ rec_local) {
@@ -294,10 +292,15 @@ __global__ __launch_bounds__(TOK_THREADS) void k_wordpiece_chunks(
     __shared__ uint16_t s_pieces[CHUNK];   // (pos - c0) | kind << 12
     __shared__ uint16_t s_stage[STAGE];    // ids staged at their piece's byte position
     __shared__ uint8_t s_cnt[CHUNK];       // ids per piece
-    __shared__ uint16_t s_poff[CHUNK];     // id offset of each piece in the chunk
-    __shared__ int32_t s_ascii_id[128];
-    __shared__ uint16_t s_rb[RB_CAP];
+    __shared__ uint16_t s_pend[PEND_CAP];  // pending piece indices (step 4b)
     __shared__ uint32_t s_scratch[TOK_THREADS / 64 + 2];
+#ifdef SDL_LDS_PAD  // diagnostic: occupancy sensitivity
+    __shared__ uint8_t s_pad[SDL_LDS_PAD];
+    if (N < 0) {
+        s_pad[(blockIdx.x * 7 + threadIdx.x) % SDL_LDS_PAD] = (uint8_t)threadIdx.x;
+        chunk_cnt[threadIdx.x] = ((volatile uint8_t *)s_pad)[(blockIdx.x + 3 * threadIdx.x) % SDL_LDS_PAD];
+    }
+#endif
 
     const int tid = threadIdx.x;
 #ifdef SDL_STAMPS
@@ -317,19 +320,14 @@ __global__ __launch_bounds__(TOK_THREADS) void k_wordpiece_chunks(
         *reinterpret_cast<uint4 *>(s_win + (p - w0)) = load16(text, p, N);
     }
     if (tid <= RBITS_WORDS) s_rbits[tid] = 0;
-    for (int i = tid; i < 128; i += TOK_THREADS) {
-        s_ascii_id[i] = T.ascii_id[i];
-    }
     const int64_t ra = ranges[3 * blockIdx.x], rz = ranges[3 * blockIdx.x + 1], r_lo = ranges[3 * blockIdx.x + 2];
     const int nrb = (int)(rz - ra);
-    const bool rb_ok = nrb <= RB_CAP;
     int64_t rb_next = rz <= R ? (int64_t)off[rz] : N;
     if (rb_next > N) rb_next = N;
     __syncthreads();
     for (int k = tid; k < nrb; k += TOK_THREADS) {
         const int rel = (int)((int64_t)off[ra + k] - w0);
         atomicOr(&s_rbits[rel >> 5], 1u << (rel & 31));
-        if (rb_ok) s_rb[k] = (uint16_t)rel;
     }
     __syncthreads();
     SDL_STAMP(1);
@@ -503,8 +501,9 @@ __global__ __launch_bounds__(TOK_THREADS) void k_wordpiece_chunks(
     //     pending list that a per-lane state machine drains: lanes pull work
     //     from a block-wide LDS queue and advance one vocab probe per iteration,
     //     so no lane idles behind a long word.
+    // (a) and (b) alternate in rounds so the pending list stays within
+    // PEND_CAP (a round of (a) adds at most TOK_THREADS * TOK_UNROLL).
     lds_u16 *stage = (lds_u16 *)s_stage;
-    uint16_t *s_pend = s_poff;  // pending piece indices (s_poff is free until step 5)
 #if defined(SDL_ABLATE) && SDL_ABLATE == 2
     // diagnostic: no WordPiece at all, every piece yields one id 0
     for (int pi = tid; pi < np; pi += TOK_THREADS) {
@@ -551,8 +550,10 @@ __global__ __launch_bounds__(TOK_THREADS) void k_wordpiece_chunks(
         Lout = Lw;
         return fast;
     };
+    for (int r0 = 0; r0 < np;) {
     // (a) batched first probes
-    for (int r0 = 0; r0 < np; r0 += TOK_THREADS * TOK_UNROLL) {
+    for (; r0 < np && (int)s_scratch[TOK_THREADS / 64 + 1] <= PEND_CAP - TOK_THREADS * TOK_UNROLL;
+         r0 += TOK_THREADS * TOK_UNROLL) {
         uint32_t hsh[TOK_UNROLL], key[TOK_UNROLL];
         W16 cand[TOK_UNROLL];
         int prel_u[TOK_UNROLL], L_u[TOK_UNROLL];
@@ -577,7 +578,7 @@ __global__ __launch_bounds__(TOK_THREADS) void k_wordpiece_chunks(
             } else if (kind == V_ISO) {
                 const uint32_t b = win[prel + HALO_L];
                 if (b < 0x80u) {
-                    stage[prel] = (uint16_t)s_ascii_id[b];
+                    stage[prel] = (uint16_t)T.ascii_id[b];
                     s_cnt[pi] = 1;
                 } else {
                     pend[u] = true;
@@ -620,8 +621,8 @@ __global__ __launch_bounds__(TOK_THREADS) void k_wordpiece_chunks(
                 if (pend[u]) s_pend[base + __popcll(pm & ((1ull << lane) - 1ull))] = (uint16_t)pi;
             }
         }
+        __syncthreads();  // the pending count is read by the loop test
     }
-    __syncthreads();
     SDL_STAMP(11);
     int npend = (int)s_scratch[TOK_THREADS / 64 + 1];
     if (tid == 0) s_scratch[TOK_THREADS / 64 + 1] = 0;  // becomes the queue head
@@ -663,7 +664,7 @@ __global__ __launch_bounds__(TOK_THREADS) void k_wordpiece_chunks(
                         if (kind == V_OTHER && word_setup(prel, w, L)) {
                             fits = true;
                         } else {
-                            fits = normalize_w16(C, p, rec_end_of(C, (const lds_u16 *)s_rb, nrb, rb_ok, rb_next, p),
+                            fits = normalize_w16(C, p, rec_end_of(C, rb_next, p),
                                                  kind == V_ISO, w, L);
                         }
                         if (fits) {
@@ -684,7 +685,7 @@ __global__ __launch_bounds__(TOK_THREADS) void k_wordpiece_chunks(
                             s_cnt[pi] = (uint8_t)wordpiece_general(T, buf, nb, out);
                         } else {
                             s_cnt[pi] = (uint8_t)word_general(
-                                C, p, rec_end_of(C, (const lds_u16 *)s_rb, nrb, rb_ok, rb_next, p), out);
+                                C, p, rec_end_of(C, rb_next, p), out);
                         }
                     }
                 }
@@ -727,6 +728,9 @@ __global__ __launch_bounds__(TOK_THREADS) void k_wordpiece_chunks(
         }
     }
     __syncthreads();
+    if (tid == 0) s_scratch[TOK_THREADS / 64 + 1] = 0;  // the next round's pending count
+    __syncthreads();
+    }
     SDL_STAMP(7);
 #if defined(SDL_ABLATE) && SDL_ABLATE == 2
     }
@@ -739,30 +743,31 @@ __global__ __launch_bounds__(TOK_THREADS) void k_wordpiece_chunks(
     uint32_t mine = 0;
     for (int i = a0; i < a1; ++i) mine += s_cnt[i];
     uint32_t total;
-    uint32_t base = block_excl_sum<TOK_THREADS>(mine, &total, s_scratch);
+    const uint32_t base0 = block_excl_sum<TOK_THREADS>(mine, &total, s_scratch);
     uint32_t *dst = tokc + (int64_t)blockIdx.x * STAGE;
+    uint32_t base = base0;
     for (int i = a0; i < a1; ++i) {
-        s_poff[i] = (uint16_t)base;
         const int prel = s_pieces[i] & 0xFFF;
         const int k = s_cnt[i];
         for (int j = 0; j < k; ++j) dst[base + j] = s_stage[prel + j];
         base += k;
     }
     __syncthreads();
+    // the stage is free now: it holds each piece's id offset in the chunk
+    uint16_t *s_poff = s_stage;
+    base = base0;
+    for (int i = a0; i < a1; ++i) {
+        s_poff[i] = (uint16_t)base;
+        base += s_cnt[i];
+    }
+    __syncthreads();
     SDL_STAMP(8);
     if (tid == 0) chunk_cnt[blockIdx.x] = total;
     // record boundaries owned by this chunk: local id offset of the first piece
-    // at or after the boundary (positions come from the LDS record list)
+    // at or after the boundary
     const int k_lo = (int)(r_lo - ra);
-    for (int k = k_lo + tid;; k += TOK_THREADS) {
-        int64_t pos;
-        if (rb_ok) {
-            if (k >= nrb) break;
-            pos = w0 + s_rb[k];
-        } else {
-            if (ra + k > R) break;
-            pos = (int64_t)off[ra + k];
-        }
+    for (int k = k_lo + tid; k < nrb; k += TOK_THREADS) {
+        const int64_t pos = (int64_t)off[ra + k];
         if (pos >= c1) break;
         const int rel = (int)(pos - c0);
         int lo = 0, hi = np;
