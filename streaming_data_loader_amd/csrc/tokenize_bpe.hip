@@ -42,6 +42,7 @@ namespace {
 enum : uint8_t { K_CONT = 0, K_L = 1, K_N = 2, K_W = 3, K_O = 4, K_SP = 5, K_AP = 6, K_SPEC = 7, K_SPX = 8 };
 constexpr int K_BND = 15;  // "no char" (record start / added-token edge / text end)
 constexpr int BPE_MAX_WAVE = 64;  // pieces up to this many bytes are merged in the chunk kernel
+constexpr uint8_t CNT_LONG = 0xFF;  // s_cnt of a long piece (k_bpe_long)
 constexpr uint32_t LONG_MARK = 0x80000000u;
 
 __device__ __forceinline__ uint32_t ascii_k(uint32_t b) {
@@ -273,7 +274,11 @@ __device__ int bpe_wave(const DevTok &T, uint32_t &sym, int n, lds_u16 *tmp) {
 }  // namespace
 
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(TOK_THREADS) void k_bpe_chunks(
+// Register budget for 5 waves/SIMD (the 7.9 KB of LDS per one-wave block admits 5).
+#ifndef SDL_BPE_WAVES
+#define SDL_BPE_WAVES 5
+#endif
+__global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL_BPE_WAVES, 8))) void k_bpe_chunks(
     DevTok T, const uint8_t *__restrict__ text, int64_t N, const uint64_t *__restrict__ off, int64_t R,
     const uint32_t *__restrict__ ranges, uint32_t *__restrict__ tokc, uint32_t *__restrict__ chunk_cnt,
     uint32_t *__restrict__ chunk_ent, uint32_t *__restrict__ rec_local, uint32_t *__restrict__ long_count,
@@ -283,10 +288,7 @@ __global__ __launch_bounds__(TOK_THREADS) void k_bpe_chunks(
     __shared__ uint32_t s_rbits[RBITS_WORDS + 1];
     __shared__ uint16_t s_pieces[CHUNK + 1];  // prel | SPEC << 12 | LONG << 13
     __shared__ uint16_t s_stage[STAGE];       // ids staged at their piece's byte position
-    __shared__ uint16_t s_cnt[CHUNK];         // ids per piece
-    __shared__ uint16_t s_poff[CHUNK];        // id offset of each piece in the chunk
-    __shared__ uint16_t s_rb[RB_CAP];
-    __shared__ uint16_t s_byte_id[256];
+    __shared__ uint8_t s_cnt[CHUNK];          // ids per piece (<= BPE_MAX_WAVE), CNT_LONG = long piece
     __shared__ uint16_t s_tmp[64];
     __shared__ uint32_t s_scratch[8];
 
@@ -310,16 +312,13 @@ __global__ __launch_bounds__(TOK_THREADS) void k_bpe_chunks(
         *reinterpret_cast<uint4 *>(s_win + (hp - w0)) = hv;
     }
     if (tid <= RBITS_WORDS) s_rbits[tid] = 0;
-    for (int i = tid; i < 256; i += TOK_THREADS) s_byte_id[i] = T.byte_id[i];
     const int64_t ra = ranges[3 * blockIdx.x], rz = ranges[3 * blockIdx.x + 1], r_lo = ranges[3 * blockIdx.x + 2];
     const int nrb = (int)(rz - ra);
-    const bool rb_ok = nrb <= RB_CAP;
     if (tid == 0) s_scratch[0] = s_scratch[1] = 0;
     __syncthreads();
     for (int k = tid; k < nrb; k += TOK_THREADS) {
         const int rel = (int)((int64_t)off[ra + k] - w0);
         atomicOr(&s_rbits[rel >> 5], 1u << (rel & 31));
-        if (rb_ok) s_rb[k] = (uint16_t)rel;
     }
     // ASCII classes (bytes >= 0x80 provisionally O; text past N is O too)
     auto classify16 = [&](const uint4 &x, int wi0, int64_t p0) {
@@ -400,8 +399,10 @@ __global__ __launch_bounds__(TOK_THREADS) void k_bpe_chunks(
 
     // ---- 3. word-table probe per piece ----------------------------------------
     lds_u16 *stage = (lds_u16 *)s_stage;
-    lds_u16 *cnt = (lds_u16 *)s_cnt;
-    uint16_t *s_pend = s_poff;  // pieces for the wave BPE (s_poff is free until step 5)
+    lds_u8 *cnt = (lds_u8 *)s_cnt;
+    // pieces for the wave BPE: the byte classes are dead now; a miss spans >= 2
+    // bytes, so a chunk has at most CHUNK / 2 <= WIN / 2 of them
+    uint16_t *s_pend = reinterpret_cast<uint16_t *>(s_cls);
     const lds_u32 *w32 = (const lds_u32 *)s_win;
     if (tid == 0) s_scratch[1] = 0;
     __syncthreads();
@@ -425,7 +426,7 @@ __global__ __launch_bounds__(TOK_THREADS) void k_bpe_chunks(
             }
             stage[prel] = (uint16_t)(li & 0xFFFFu);
             stage[prel + 1] = (uint16_t)(li >> 16);
-            cnt[pi] = 0xFFFFu;  // marker
+            cnt[pi] = CNT_LONG;  // marker
         } else {
             const int n = nxt - prel;
             if (n <= 16) {
@@ -490,10 +491,10 @@ __global__ __launch_bounds__(TOK_THREADS) void k_bpe_chunks(
         const int prel = (int)(s_pieces[pi] & 0xFFFu);
         const int nxt = pi + 1 < np ? (int)(s_pieces[pi + 1] & 0xFFFu) : e_last;
         const int n = nxt - prel;
-        uint32_t sym = lane < n ? (uint32_t)s_byte_id[win[prel + HALO_L + lane]] : 0u;
+        uint32_t sym = lane < n ? (uint32_t)T.byte_id[win[prel + HALO_L + lane]] : 0u;
         const int k = bpe_wave(T, sym, n, (lds_u16 *)s_tmp);
         if (lane < k) stage[prel + lane] = (uint16_t)sym;
-        if (lane == 0) cnt[pi] = (uint16_t)k;
+        if (lane == 0) cnt[pi] = (uint8_t)k;
         __syncthreads();
     }
 
@@ -502,15 +503,15 @@ __global__ __launch_bounds__(TOK_THREADS) void k_bpe_chunks(
     const int a0 = tid * per < np ? tid * per : np;
     const int a1 = a0 + per < np ? a0 + per : np;
     uint32_t mine = 0;
-    for (int i = a0; i < a1; ++i) mine += s_cnt[i] == 0xFFFFu ? 1u : s_cnt[i];
+    for (int i = a0; i < a1; ++i) mine += s_cnt[i] == CNT_LONG ? 1u : s_cnt[i];
     uint32_t total;
-    uint32_t base = block_excl_sum<TOK_THREADS>(mine, &total, s_scratch + 2);
+    const uint32_t base0 = block_excl_sum<TOK_THREADS>(mine, &total, s_scratch + 2);
     uint32_t *dst = tokc + (int64_t)blockIdx.x * STAGE;
+    uint32_t base = base0;
     for (int i = a0; i < a1; ++i) {
-        s_poff[i] = (uint16_t)base;
         const int prel = s_pieces[i] & 0xFFF;
         const int k = s_cnt[i];
-        if (k == 0xFFFF) {
+        if (k == CNT_LONG) {
             dst[base++] = LONG_MARK | (uint32_t)s_stage[prel] | ((uint32_t)s_stage[prel + 1] << 16);
             continue;
         }
@@ -518,19 +519,20 @@ __global__ __launch_bounds__(TOK_THREADS) void k_bpe_chunks(
         base += k;
     }
     __syncthreads();
+    // the stage is free now: it holds each piece's entry offset in the chunk
+    uint16_t *s_poff = s_stage;
+    base = base0;
+    for (int i = a0; i < a1; ++i) {
+        s_poff[i] = (uint16_t)base;
+        base += s_cnt[i] == CNT_LONG ? 1u : s_cnt[i];
+    }
+    __syncthreads();
     if (tid == 0) chunk_cnt[blockIdx.x] = chunk_ent[blockIdx.x] = total;
     // record boundaries owned by this chunk: local entry offset of the first
     // piece at or after the boundary (k_bpe_long adds long pieces' extra ids)
     const int k_lo = (int)(r_lo - ra);
-    for (int k = k_lo + tid;; k += TOK_THREADS) {
-        int64_t pos;
-        if (rb_ok) {
-            if (k >= nrb) break;
-            pos = w0 + s_rb[k];
-        } else {
-            if (ra + k > R) break;
-            pos = (int64_t)off[ra + k];
-        }
+    for (int k = k_lo + tid; k < nrb; k += TOK_THREADS) {
+        const int64_t pos = (int64_t)off[ra + k];
         if (pos >= c1) break;
         const int rel = (int)(pos - c0);
         int lo = 0, hi = np;
