@@ -22,7 +22,10 @@ constexpr int HALO_L = 32;                        // look-back bytes staged in L
 constexpr int HALO_R = 32;                        // look-ahead bytes staged in LDS
 constexpr int WIN = HALO_L + CHUNK + HALO_R;      // 1088 bytes of text in LDS
 constexpr int STAGE = CHUNK + 128;                // token slots per chunk (>= tokens owned)
-constexpr int TOK_UNROLL = 4;                     // first probes in flight per lane
+#ifndef SDL_TOK_UNROLL
+#define SDL_TOK_UNROLL 2
+#endif
+constexpr int TOK_UNROLL = SDL_TOK_UNROLL;        // first probes in flight per lane (2: no spills at 5 waves/SIMD)
 constexpr int PEND_CAP = 512;                     // WordPiece pieces pending the state machine (LDS)
 constexpr int RB_CAP = 256;                       // record starts listed in LDS per window
 constexpr int MAX_WORD_CHARS = 100;               // WordPiece max_input_chars_per_word
