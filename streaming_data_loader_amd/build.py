@@ -48,6 +48,10 @@ def build(verbose=False, force=False, jobs=4, defines=(), lib=None, build_dir=No
     os.makedirs(bdir, exist_ok=True)
     hipcc = _hipcc()
     hdrs = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(REPO, "include", "sdl_batcher.h")]
+    # a prebuilt library newer than every source is used as is (the GPU box
+    # gets the library but not the objects: nothing is recompiled there)
+    if not force and _newer(lib, [os.path.join(CSRC, s) for s in SOURCES] + hdrs):
+        return lib
     objs, todo = [], []
     for s in SOURCES:
         src = os.path.join(CSRC, s)
