@@ -509,17 +509,18 @@ static VSlot make_slot(const std::string &pay, uint32_t cont, int32_t id, std::v
     return v;
 }
 
-// load <= 0.5 (two choices, one slot per bucket): the Unigram table holds
-// pieces, added tokens and the word table, and a smaller table stays in L2
-static void build_cuckoo(HostTokenizer &t, const std::vector<VSlot> &entries) {
+// load <= 0.5 (two choices, one slot per bucket); the Unigram pieces table
+// (probed by every Viterbi candidate) is kept apart from the word table so it
+// stays small enough to live in L2
+static void build_cuckoo(std::vector<VSlot> &tab, uint32_t &mask, const std::vector<VSlot> &entries) {
     uint32_t slots = 1;
     while (slots < 2 * entries.size()) slots <<= 1;
     for (;; slots <<= 1) {
-        t.slot_mask = slots - 1;
-        t.slots.assign(slots, VSlot{0, -1, 0, 0, {0}});
+        mask = slots - 1;
+        tab.assign(slots, VSlot{0, -1, 0, 0, {0}});
         bool ok = true;
         for (const VSlot &v : entries)
-            if (!cuckoo_insert(t.slots, t.slot_mask, v)) { ok = false; break; }
+            if (!cuckoo_insert(tab, mask, v)) { ok = false; break; }
         if (ok) break;
         if (slots >= (1u << 24)) throw std::runtime_error("cuckoo table build failed");
     }
@@ -817,7 +818,7 @@ static void load_unigram(const JValue &root, const std::string &data_dir, HostTo
     t.max_special_len = 0;
     for (auto &a : t.added) t.max_special_len = std::max(t.max_special_len, (int)a.first.size());
     t.opener = t.added.empty() ? 0u : (uint32_t)'<';
-    build_cuckoo(t, entries);  // pieces first: the word table's Viterbi probes them
+    build_cuckoo(t.slots, t.slot_mask, entries);  // pieces first: the word table's Viterbi probes them
     // word table: printable-ASCII words w -> Viterbi("▁w") ids, for w = every
     // "▁w" vocab piece and, up to UNI_WMAX bytes, w + "," and w + "." (a word
     // is its own normalization, so any entry is exact; comma/period-ended
@@ -825,6 +826,7 @@ static void load_unigram(const JValue &root, const std::string &data_dir, HostTo
     t.wres.clear();
     int maxw = 0;
     std::unordered_set<std::string> in_table;
+    std::vector<VSlot> wentries;
     auto add_word = [&](const std::string &w) {
         if (!in_table.insert(w).second) return;
         const std::vector<int> ids = unigram_encode_word(t, (const uint8_t *)w.data(), w.size());
@@ -836,7 +838,7 @@ static void load_unigram(const JValue &root, const std::string &data_dir, HostTo
             packed = (int32_t)(((uint32_t)ids.size() << 24) | (uint32_t)t.wres.size());
             for (int x : ids) t.wres.push_back((uint16_t)x);
         }
-        entries.push_back(make_slot(w, UC_WORD, packed, t.vpool));
+        wentries.push_back(make_slot(w, UC_WORD, packed, t.vpool));
         maxw = std::max(maxw, (int)w.size());
     };
     std::vector<std::string> base_words;
@@ -856,9 +858,9 @@ static void load_unigram(const JValue &root, const std::string &data_dir, HostTo
     }
     if (t.wres.size() >= (1u << 24)) throw std::runtime_error("word table too large");
     t.wres.push_back(0);
-    t.word_table_entries = entries.size();
+    t.word_table_entries = entries.size() + wentries.size();
     t.vpool.resize(t.vpool.size() + 64, 0);
-    build_cuckoo(t, entries);
+    build_cuckoo(t.wslots, t.wslot_mask, wentries);
     t.max_word = maxw;
     // device slots: word 3 (the host's cuckoo hash) carries a piece's f32 score
     for (VSlot &v : t.slots) {

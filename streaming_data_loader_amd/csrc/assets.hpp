@@ -47,6 +47,8 @@ struct HostTokenizer {
     std::vector<double> uscore;            // id -> score
     std::vector<float> uscore32;           // ... as f32 (exact, checked)
     std::vector<uint16_t> wres;            // word-table results of > 1 id
+    std::vector<VSlot> wslots;             // word table (UC_WORD), apart from the pieces in `slots`
+    uint32_t wslot_mask = 0;
     std::vector<uint16_t> tpage;           // data/t5_graphemes.bin
     std::vector<uint8_t> tblock;
     std::vector<uint16_t> cpage;           // device per-code-point table (page -> block)

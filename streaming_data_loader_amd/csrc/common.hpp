@@ -140,11 +140,14 @@ struct DevTok {
     const MSlot *mslots;     // merge table
     const uint16_t *byte_id; // id of each single byte symbol
     uint32_t mslot_mask;
-    // Unigram (kind == TOK_UNIGRAM): slots/vpool hold pieces, word table and
-    // added tokens (UC_* cont values); specials are matched "<...>" by hash
+    // Unigram (kind == TOK_UNIGRAM): slots hold pieces and added tokens, wslots
+    // the word table (UC_* cont values, payloads in vpool); specials are
+    // matched "<...>" by hash
     const double *uscore;    // score of each id
     const float *uscore32;   // ... as f32 (exact)
     const uint16_t *wres;    // word-table results with more than one id
+    const VSlot *wslots;     // word table (UC_WORD entries; `slots` holds pieces + added tokens)
+    uint32_t wslot_mask;
     const uint16_t *cpage;   // per-code-point entry pages (0x110000/256)
     const uint2 *cent;       // entry blocks of 256 (CP_* layout)
     const uint32_t *trie;    // Precompiled charsmap: double-array units

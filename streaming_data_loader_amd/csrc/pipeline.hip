@@ -317,8 +317,13 @@ __device__ __forceinline__ void select_k_smallest(const uint32_t (&key)[MR][4], 
 
 __device__ __forceinline__ void store4(int32_t *p, int j0, int S, bool vec, int32_t a, int32_t b, int32_t c,
                                        int32_t d) {
-    if (vec) {
+    if (vec) {  // the planes stream out: non-temporal, they are not re-read by this pass
+#ifdef SDL_ROWS_TEMPORAL
         if (j0 < S) *reinterpret_cast<int4 *>(p + j0) = make_int4(a, b, c, d);
+#else
+        typedef int32_t v4i __attribute__((ext_vector_type(4)));
+        if (j0 < S) __builtin_nontemporal_store(v4i{a, b, c, d}, reinterpret_cast<v4i *>(p + j0));
+#endif
     } else {
         if (j0 < S) p[j0] = a;
         if (j0 + 1 < S) p[j0 + 1] = b;

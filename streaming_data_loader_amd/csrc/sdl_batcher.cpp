@@ -240,7 +240,7 @@ struct sdl_batcher {
     DevBuf<uint16_t> d_upage;
     DevBuf<uint32_t> d_uentry, d_ubmp;
     DevBuf<uint8_t> d_upool, d_vpool;
-    DevBuf<VSlot> d_slots;
+    DevBuf<VSlot> d_slots, d_wslots;
     DevBuf<int32_t> d_ascii_id;
     DevBuf<uint16_t> d_gpage, d_byte_id;
     DevBuf<uint8_t> d_gblock;
@@ -684,6 +684,10 @@ int sdl_batcher_create(const sdl_config *cfg, const char *tokenizer_path, const 
             HIP_TRY(hipMemcpy(h->d_trie.p, t.trie.data(), t.trie.size() * 4, hipMemcpyHostToDevice));
             HIP_TRY(hipMemcpy(h->d_tnorm.p, t.tnorm.data(), t.tnorm.size(), hipMemcpyHostToDevice));
             HIP_TRY(hipMemcpy(h->d_extra.p, t.extra_ids.data(), 100 * 4, hipMemcpyHostToDevice));
+            h->d_wslots.ensure(t.wslots.size());
+            HIP_TRY(hipMemcpy(h->d_wslots.p, t.wslots.data(), t.wslots.size() * sizeof(VSlot), hipMemcpyHostToDevice));
+            d.wslots = h->d_wslots.p;
+            d.wslot_mask = t.wslot_mask;
             d.uscore = h->d_uscore.p;
             d.wres = h->d_wres.p;
             d.cpage = h->d_cpage.p;

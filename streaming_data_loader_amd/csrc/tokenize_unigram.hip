@@ -44,12 +44,21 @@ enum : uint8_t { U_WS = 0, U_P = 1, U_X = 2, U_SPEC = 3, U_SPX = 4 };
 constexpr uint32_t LMARK = 0x80000000u;
 __device__ const uint8_t kMetaBytes[3] = {0xE2, 0x96, 0x81};
 
+// LDS budget: 3 one-wave blocks per SIMD (<= 13.3 KB each) -- the kernel waits
+// on probe latency, so resident waves are what it runs on
 constexpr int ARENA = 768;          // LDS bytes for normalized medium words
 constexpr int WIN_PAD = WIN + 32;   // window + gather padding; the arena follows
-constexpr int VP_CAP = 256;         // Viterbi pieces per chunk
-constexpr int JOB_CAP = 128;        // words waiting for the DP (more: long items)
-constexpr int TASK_CAP = 320;       // probe tasks per round (>= one job's: L <= UNI_WMAX)
-constexpr int DP_LANES = 16;
+constexpr int VP_CAP = 128;         // Viterbi pieces per chunk
+constexpr int JOB_CAP = 80;         // words waiting for the DP (more: long items)
+constexpr int MED_CAP = 128;        // medium words per chunk (more: long items)
+#ifndef SDL_UNI_TASK_CAP
+#define SDL_UNI_TASK_CAP 256
+#endif
+constexpr int TASK_CAP = SDL_UNI_TASK_CAP;  // probe tasks per round (>= one job's: L <= UNI_WMAX)
+#ifndef SDL_UNI_DP_LANES
+#define SDL_UNI_DP_LANES 8
+#endif
+constexpr int DP_LANES = SDL_UNI_DP_LANES;
 constexpr uint8_t CNT_LONG = 0xFF;   // s_cnt of a long item        // lanes running the DP (a round holds few jobs)
 constexpr int TASK_UNROLL = 4;      // probes in flight per lane
 
@@ -67,6 +76,13 @@ __device__ __forceinline__ uint2 cp_ent(const DevTok &T, uint32_t cp) {
     return T.cent[(uint32_t)T.cpage[cp >> 8] * 256u + (cp & 255u)];
 }
 
+// both cuckoo slots of hash h in the word table (UC_WORD keys)
+__device__ __forceinline__ Probe probe_load_words(const DevTok &T, uint32_t h) {
+    const uint4 *e1 = reinterpret_cast<const uint4 *>(T.wslots + cuckoo_slot1(h, T.wslot_mask));
+    const uint4 *e2 = reinterpret_cast<const uint4 *>(T.wslots + cuckoo_slot2(h, T.wslot_mask));
+    return Probe{e1[0], e1[1], e2[0], e2[1]};
+}
+
 // id of the slot (payload bytes acc(start .. start+n), cont) or -1: exact
 template <class Acc>
 __device__ int probe_acc(const DevTok &T, const Acc &acc, int start, int n, uint32_t cont, uint32_t *w3 = nullptr) {
@@ -82,7 +98,7 @@ __device__ int probe_acc(const DevTok &T, const Acc &acc, int start, int n, uint
     } while (b0 < n);
     h = hfinal(h);
     const uint32_t key = (uint32_t)n | (cont << 8);
-    const Probe P = probe_load(T, h);
+    const Probe P = cont == UC_WORD ? probe_load_words(T, h) : probe_load(T, h);
     for (int which = 0; which < 2; ++which) {
         const uint4 a = which ? P.a2 : P.a1, b = which ? P.b2 : P.b1;
         if (!slot_match(a, b, key, first)) continue;
@@ -513,20 +529,21 @@ __global__ __launch_bounds__(TOK_THREADS) void k_unigram_chunks(
     uint32_t *__restrict__ chunk_ent, uint32_t *__restrict__ rec_local, uint32_t *__restrict__ counters,
     uint4 *__restrict__ items, uint32_t item_cap, uint32_t *__restrict__ err) {
     __shared__ __attribute__((aligned(16))) uint8_t s_bytes[WIN_PAD + ARENA + 32];  // window | arena
-    // s_cls / s_plen / s_poff are dead during the Viterbi rounds (long-item
+    // s_cls / s_plen / s_med are dead during the Viterbi rounds (long-item
     // lengths move to their stage slot), which reuse them for the DP nodes:
     // LDS per one-wave block decides how many chunks a CU keeps in flight.
-    constexpr int U_CLS = 0, U_PLEN = (WIN + 15) & ~15, U_POFF = U_PLEN + 2 * CHUNK, U_END = U_POFF + 2 * CHUNK;
-    static_assert(DP_LANES * UNI_NODES * 12 <= U_END, "DP nodes must fit the dead arrays");
+    constexpr int U_CLS = 0, U_PLEN = (WIN + 15) & ~15, U_MED = U_PLEN + CHUNK, U_MED_END = U_MED + 2 * MED_CAP;
+    constexpr int U_END = U_MED_END > DP_LANES * UNI_NODES * 12 ? U_MED_END : DP_LANES * UNI_NODES * 12;
     __shared__ __attribute__((aligned(16))) uint8_t s_u[U_END];
     uint8_t *const s_cls = s_u + U_CLS;
     __shared__ uint32_t s_rbits[RBITS_WORDS + 1];
     __shared__ uint16_t s_pieces[CHUNK + 1];  // prel | SPEC << 12
-    uint16_t *const s_plen = (uint16_t *)(s_u + U_PLEN);  // piece length (0 = runs past the window)
-    __shared__ uint16_t s_stage[2 * CHUNK + 64];  // ids staged at 2 * prel
+    uint8_t *const s_plen = s_u + U_PLEN;  // piece length, settled pieces only (0 = runs past the window)
+    // ids staged at their piece's byte offset: a piece may use the bytes up to
+    // the next piece (stage_room); one that needs more becomes a long item
+    __shared__ uint16_t s_stage[STAGE];
     __shared__ uint8_t s_cnt[CHUNK];              // ids per piece (<= 2 UNI_WMAX), CNT_LONG = long item
-    uint16_t *const s_poff = (uint16_t *)(s_u + U_POFF);
-    __shared__ uint16_t s_rb[RB_CAP];
+    uint16_t *const s_med = (uint16_t *)(s_u + U_MED);  // medium words (piece indices)
     __shared__ uint32_t s_scratch[16];  // 0 jobs 1 vps 2 arena used 3 medium words; 8.. scan scratch
     __shared__ uint16_t s_job_pi[JOB_CAP], s_job_vp[JOB_CAP];
     __shared__ uint8_t s_job_nvp[JOB_CAP];
@@ -567,13 +584,11 @@ __global__ __launch_bounds__(TOK_THREADS) void k_unigram_chunks(
     if (tid <= RBITS_WORDS) s_rbits[tid] = 0;
     const int64_t ra = ranges[3 * blockIdx.x], rz = ranges[3 * blockIdx.x + 1], r_lo = ranges[3 * blockIdx.x + 2];
     const int nrb = (int)(rz - ra);
-    const bool rb_ok = nrb <= RB_CAP;
     if (tid < 8) s_scratch[tid] = 0;
     __syncthreads();
     for (int k = tid; k < nrb; k += TOK_THREADS) {
         const int rel = (int)((int64_t)off[ra + k] - w0);
         atomicOr(&s_rbits[rel >> 5], 1u << (rel & 31));
-        if (rb_ok) s_rb[k] = (uint16_t)rel;
     }
     auto classify16 = [&](const uint4 &x, int wi0) {
         const uint32_t wv[4] = {x.x, x.y, x.z, x.w};
@@ -631,6 +646,11 @@ __global__ __launch_bounds__(TOK_THREADS) void k_unigram_chunks(
     // ---- 3. per piece: added token / word table / medium normalization / long --
     lds_u16 *stage = (lds_u16 *)s_stage;
     lds_u8 *cnt = (lds_u8 *)s_cnt;
+    // stage slots of piece pi: up to the next piece's (the last one: the stage's end)
+    auto stage_room = [&](int pi) -> int {
+        const int prel = (int)(s_pieces[pi] & 0xFFFu);
+        return (pi + 1 < np ? (int)(s_pieces[pi + 1] & 0xFFFu) : STAGE) - prel;
+    };
     for (int pi = tid; pi < np; pi += TOK_THREADS) {
         const uint32_t pc = s_pieces[pi];
         const int prel = (int)(pc & 0xFFFu);
@@ -638,11 +658,11 @@ __global__ __launch_bounds__(TOK_THREADS) void k_unigram_chunks(
         if (pc & (1u << 12)) {
             int l = 0;
             const int id = uni_special(T, c0 + prel, N, cbyte, cbnd, &l);
-            stage[2 * prel] = (uint16_t)(id < 0 ? T.unk_id : id);
+            stage[prel] = (uint16_t)(id < 0 ? T.unk_id : id);
             cnt[pi] = 1;
-            s_plen[pi] = (uint16_t)l;
             continue;
         }
+        const int room = stage_room(pi);
         // word end: first whitespace / added token / record start / text end
         int wi = wi0 + 1;
         bool simple = cls[wi0] == U_P;
@@ -654,26 +674,26 @@ __global__ __launch_bounds__(TOK_THREADS) void k_unigram_chunks(
             if (k == U_WS || k == U_SPEC || is_rs(wi)) { len = wi - wi0; break; }
             simple = simple && k == U_P;
         }
-        s_plen[pi] = (uint16_t)len;
+        s_plen[pi] = (uint8_t)(len <= UNI_WMAX ? len : 0);
         bool done = false;
         if (len > 0 && len <= UNI_WMAX && simple) {
             int packed;
             if (len <= 16) {
                 const W16 w = lds_w16(w32, wi0, len);
-                packed = probe_result(probe_load(T, hash16(w, (uint32_t)len, UC_WORD)),
+                packed = probe_result(probe_load_words(T, hash16(w, (uint32_t)len, UC_WORD)),
                                       (uint32_t)len | (UC_WORD << 8), w);
             } else {
                 packed = probe_acc(T, [&](int i) -> uint32_t { return win[wi0 + i]; }, 0, len, UC_WORD);
             }
-            if (packed >= 0) {
+            if (packed >= 0 && (packed >> 24) <= room) {
                 const int k = packed >> 24;
                 const uint32_t x = (uint32_t)packed & 0xFFFFFFu;
-                if (k == 1) stage[2 * prel] = (uint16_t)x;
+                if (k == 1) stage[prel] = (uint16_t)x;
                 else
-                    for (int j = 0; j < k; ++j) stage[2 * prel + j] = T.wres[x + j];
+                    for (int j = 0; j < k; ++j) stage[prel + j] = T.wres[x + j];
                 cnt[pi] = (uint8_t)k;
                 done = true;
-            } else {
+            } else if (packed < 0 && len + 1 <= room) {  // Viterbi yields <= len + 1 ids
                 // miss: one Viterbi piece, the word's bytes in the window
                 const uint32_t vp = atomicAdd(&s_scratch[1], 1u);
                 if (vp < VP_CAP) {
@@ -691,13 +711,16 @@ __global__ __launch_bounds__(TOK_THREADS) void k_unigram_chunks(
             }
         } else if (len > 0 && len <= UNI_WMAX) {
             // medium word: normalized in the next pass, all lanes at once
-            s_poff[atomicAdd(&s_scratch[3], 1u)] = (uint16_t)pi;
-            cnt[pi] = 0;
-            done = true;
+            const uint32_t mq = atomicAdd(&s_scratch[3], 1u);
+            if (mq < (uint32_t)MED_CAP) {
+                s_med[mq] = (uint16_t)pi;
+                cnt[pi] = 0;
+                done = true;
+            }
         }
         if (!done) {  // long item: finished by k_unigram_long; its length in its stage slot
             cnt[pi] = CNT_LONG;
-            stage[2 * prel] = (uint16_t)len;
+            stage[prel] = (uint16_t)len;
         }
     }
     __syncthreads();
@@ -705,9 +728,9 @@ __global__ __launch_bounds__(TOK_THREADS) void k_unigram_chunks(
     __syncthreads();
     // medium words (non-ASCII or control bytes, <= UNI_WMAX): normalize into the
     // arena (at most UNI_WMAX bytes each), split, list their Viterbi pieces
-    const int nmed = (int)s_scratch[3];
+    const int nmed = (int)(s_scratch[3] < (uint32_t)MED_CAP ? s_scratch[3] : (uint32_t)MED_CAP);
     for (int mq = lane; mq < nmed; mq += 64) {
-        const int pi = s_poff[mq];
+        const int pi = s_med[mq];
         const int prel = (int)(s_pieces[pi] & 0xFFFu);
         const int wi0 = HALO_L + prel;
         const int len = s_plen[pi];
@@ -733,7 +756,7 @@ __global__ __launch_bounds__(TOK_THREADS) void k_unigram_chunks(
                 for (int pass = 0; pass < 2 && fits; ++pass) {
                     if (pass == 1) {
                         if (nvp == 0) break;
-                        if (bound > 2 * len || nvp > 255) { fits = false; break; }
+                        if (bound > stage_room(pi) || nvp > 255) { fits = false; break; }
                         vp0 = atomicAdd(&s_scratch[1], (uint32_t)nvp);
                         if (vp0 + (uint32_t)nvp > (uint32_t)VP_CAP) { fits = false; break; }
                     }
@@ -783,7 +806,7 @@ __global__ __launch_bounds__(TOK_THREADS) void k_unigram_chunks(
         }
         if (!done) {  // long item: finished by k_unigram_long
             cnt[pi] = CNT_LONG;
-            stage[2 * prel] = (uint16_t)len;
+            stage[prel] = (uint16_t)len;
         }
     }
     __syncthreads();
@@ -826,6 +849,73 @@ __global__ __launch_bounds__(TOK_THREADS) void k_unigram_chunks(
         const int nt = (int)(s_job_tb[j1] - T0);
         for (int r = lane; r < (int)(s_job_rb[j1] - RB0); r += 64) s_rowmask[r] = 0u;
         __syncthreads();
+#ifndef SDL_UNI_LANE_ROWS
+        // -- candidate probes: the round's tasks (one candidate (start, end) of
+        //    one piece each) dealt to all 64 lanes, TASK_UNROLL in flight per lane,
+        //    so a round costs ceil(tasks / 256) probe latencies whatever its rows' lengths --
+        for (int tq = 0; tq < nt; tq += 64 * TASK_UNROLL) {
+            Probe P[TASK_UNROLL];
+            W16 W[TASK_UNROLL];
+            uint32_t meta[TASK_UNROLL];  // row | k << 16 | n << 22 | cont << 29; ~0u: no probe
+            int gen[TASK_UNROLL];        // generic probe (payload > 16 bytes); -2: use P
+            uint32_t gw3[TASK_UNROLL];
+#pragma unroll
+            for (int u = 0; u < TASK_UNROLL; ++u) {
+                const int t = tq + 64 * u + lane;
+                meta[u] = ~0u;
+                gen[u] = -2;
+                gw3[u] = 0;
+                W[u] = W16{0, 0, 0, 0};
+                if (t >= nt) continue;
+                const uint32_t gt = T0 + (uint32_t)t;
+                int a = j0, b = j1 - 1;  // the job holding task gt
+                while (a < b) {
+                    const int m = (a + b + 1) >> 1;
+                    if (s_job_tb[m] <= gt) a = m; else b = m - 1;
+                }
+                int lt = (int)(gt - s_job_tb[a]);
+                int row = (int)(s_job_rb[a] - RB0);
+                int vp = s_job_vp[a];
+                for (int q = 0; q + 1 < s_job_nvp[a]; ++q) {
+                    const int Lq = s_vp_len[vp];
+                    const int tk = vp_tasks(Lq, Mm, Mf);
+                    if (lt < tk) break;
+                    lt -= tk;
+                    row += Lq + 1;
+                    ++vp;
+                }
+                const int L = s_vp_len[vp], src = s_vp_src[vp];
+                int i, j;  // payload start (-1: the "▁" row) and end
+                vp_decode(lt, L, Mm, Mf, &i, &j);
+                // candidates start and end on char boundaries
+                if ((i > 0 && (bytes[src + i] & 0xC0u) == 0x80u) || (j < L && (bytes[src + j] & 0xC0u) == 0x80u))
+                    continue;
+                const int ps = i < 0 ? 0 : i;
+                const int n = j - ps;
+                const uint32_t cont = i < 0 ? UC_META : UC_PIECE;
+                meta[u] = (uint32_t)(row + i + 1) | (uint32_t)(j - (i < 0 ? 0 : i + 1)) << 16 | (uint32_t)n << 22 |
+                          cont << 29;
+                if (n <= 16) {
+                    W[u] = lds_w16(w32, src + ps, n);
+                    P[u] = probe_load(T, hash16(W[u], (uint32_t)n, cont));
+                } else {
+                    gen[u] = probe_acc(T, [&](int x) -> uint32_t { return bytes[src + x]; }, ps, n, cont, &gw3[u]);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < TASK_UNROLL; ++u) {
+                if (meta[u] == ~0u) continue;
+                uint32_t w3 = gw3[u];
+                const uint32_t key = ((meta[u] >> 22) & 0x7Fu) | ((meta[u] >> 29) << 8);
+                const int id = gen[u] != -2 ? gen[u] : probe_result_w3(P[u], key, W[u], &w3);
+                if (id < 0) continue;
+                const int t = tq + 64 * u + lane;
+                s_tid[t] = (uint16_t)id;
+                s_tsc[t] = __uint_as_float(w3);  // the slot's score (f32, exact)
+                atomicOr(&s_rowmask[meta[u] & 0xFFFFu], 1u << ((meta[u] >> 16) & 0x3Fu));
+            }
+        }
+#else
         // -- candidate rows: lane per row (one start of one piece), 4 probes in flight --
         const int nrows = (int)(s_job_rb[j1] - RB0);
         for (int r = lane; r < nrows; r += 64) {
@@ -894,6 +984,7 @@ __global__ __launch_bounds__(TOK_THREADS) void k_unigram_chunks(
             }
             s_rowmask[r] = mask;
         }
+#endif
         __syncthreads();
         UNI_STAMP(6);
         // -- DP: lane per job --
@@ -921,7 +1012,7 @@ __global__ __launch_bounds__(TOK_THREADS) void k_unigram_chunks(
                 };
                 const int base = ktot;
                 ktot += unigram_viterbi_masked(acc, L + 3, rowmask, at, cand, nodes, T.unk_score, T.unk_id,
-                                               [&](int x, int id) { stage[2 * prel + base + x] = (uint16_t)id; });
+                                               [&](int x, int id) { stage[prel + base + x] = (uint16_t)id; });
                 toff += vp_tasks(L, Mm, Mf);
                 roff += L + 1;
             }
@@ -942,32 +1033,35 @@ __global__ __launch_bounds__(TOK_THREADS) void k_unigram_chunks(
     uint32_t total;
     uint32_t base = block_excl_sum<TOK_THREADS>(mine, &total, s_scratch + 8);
     uint32_t *dst = tokc + (int64_t)blockIdx.x * UNI_STAGE;
+    const uint32_t base0 = base;
     for (int i = a0; i < a1; ++i) {
-        s_poff[i] = (uint16_t)base;
         const int prel = s_pieces[i] & 0xFFF;
         const int k = s_cnt[i];
         if (k == CNT_LONG) {
             const uint32_t it = atomicAdd(&counters[0], 1u);
-            if (it < item_cap) items[it] = make_uint4((uint32_t)blockIdx.x, base, (uint32_t)prel, s_stage[2 * prel]);
+            if (it < item_cap) items[it] = make_uint4((uint32_t)blockIdx.x, base, (uint32_t)prel, s_stage[prel]);
             else atomicOr(err, 8u);
             dst[base++] = LMARK;
             continue;
         }
-        for (int j = 0; j < k; ++j) dst[base + j] = s_stage[2 * prel + j];
+        for (int j = 0; j < k; ++j) dst[base + j] = s_stage[prel + j];
         base += k;
     }
     __syncthreads();
+    // the stage is free now: it holds each piece's entry offset in the chunk
+    uint16_t *const s_poff = s_stage;
+    base = base0;
+    for (int i = a0; i < a1; ++i) {
+        s_poff[i] = (uint16_t)base;
+        base += s_cnt[i] == CNT_LONG ? 1u : s_cnt[i];
+    }
+    __syncthreads();
     if (tid == 0) chunk_cnt[blockIdx.x] = chunk_ent[blockIdx.x] = total;
+    // record boundaries owned by this chunk: entry offset of the first piece at
+    // or after the boundary (k_unigram_long adds long items' extra ids)
     const int k_lo = (int)(r_lo - ra);
-    for (int k = k_lo + tid;; k += TOK_THREADS) {
-        int64_t pos;
-        if (rb_ok) {
-            if (k >= nrb) break;
-            pos = w0 + s_rb[k];
-        } else {
-            if (ra + k > R) break;
-            pos = (int64_t)off[ra + k];
-        }
+    for (int k = k_lo + tid; ra + k <= R; k += TOK_THREADS) {
+        const int64_t pos = (int64_t)off[ra + k];
         if (pos >= c1) break;
         const int rel = (int)(pos - c0);
         int lo = 0, hi = np;
