@@ -164,6 +164,36 @@ def cpu_baseline(task, records, order, seconds=12.0, mt_seconds=6.0):
                                     f"{mt_bytes / 1e6:.1f} MB in {mt_dt:.1f} s"}}
 
 
+def reference_engine_rate(task, records, order, seconds=6.0):
+    """The reference's own tokenizer engine -- HF `tokenizers` (Rust core; the
+    reference pins crate 0.13.1, tokenizer_holder.rs:19-28), here its Python
+    binding -- encoding the same record stream one record at a time on one
+    thread with the same tokenizer.json, as the reference Batcher's single task
+    does.  Tokenization only (no masking/batching): an upper bound on the
+    reference CPU Batcher's rate.  None when the binding is absent."""
+    os.environ.setdefault("RAYON_NUM_THREADS", "1")
+    try:
+        from tokenizers import Tokenizer
+    except Exception:
+        return None
+    from streaming_data_loader_amd import native
+    path = {"gpt2": native.GPT2_PROXY_TOKENIZER, "t5": native.T5_PROXY_TOKENIZER}.get(TASKS[task]["tok"],
+                                                                                     native.BERT_PROXY_TOKENIZER)
+    tok = Tokenizer.from_file(path)
+    done = n = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        r = records[order[n % len(order)]]
+        tok.encode(r, add_special_tokens=True)
+        done += len(r.encode("utf-8"))
+        n += 1
+    dt = time.perf_counter() - t0
+    return {"value": round(done / dt / 1e6, 3), "unit": "MB/s", "cores": 1, "kind": "reference engine",
+            "sample": f"{n} records ({done / 1e6:.1f} MB) of rank 0's arena stream, tokenizers "
+                      f"{getattr(__import__('tokenizers'), '__version__', '?')} Tokenizer.encode, one thread, "
+                      f"{dt:.1f} s (tokenization only)"}
+
+
 def load_traffic(kernel):
     """HBM bytes per tokenize launch from the committed rocprofv3 PMC summary
     (2 x FETCH_SIZE gfx950 correction + WRITE_SIZE, MI355X_MICROARCH.md §HBM)."""
@@ -301,6 +331,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("cpu baseline ...")
         line["cpu_baseline"] = cpu_baseline(args.task, records, order)
+        line["cpu_baseline"]["reference_engine"] = reference_engine_rate(args.task, records, order)
     elif rank == 0:
         line["cpu_baseline"] = None
     if rank == 0:

@@ -48,9 +48,16 @@ __device__ const uint8_t kMetaBytes[3] = {0xE2, 0x96, 0x81};
 // on probe latency, so resident waves are what it runs on
 constexpr int ARENA = 768;          // LDS bytes for normalized medium words
 constexpr int WIN_PAD = WIN + 32;   // window + gather padding; the arena follows
-constexpr int VP_CAP = 128;         // Viterbi pieces per chunk
-constexpr int JOB_CAP = 80;         // words waiting for the DP (more: long items)
+#ifndef SDL_UNI_JOB_CAP
+#define SDL_UNI_JOB_CAP 112
+#endif
+constexpr int JOB_CAP = SDL_UNI_JOB_CAP;  // words waiting for the DP (more: long items)
+constexpr int VP_CAP = JOB_CAP + JOB_CAP / 2;  // Viterbi pieces per chunk
 constexpr int MED_CAP = 128;        // medium words per chunk (more: long items)
+#ifndef SDL_UNI_WT_UNROLL
+#define SDL_UNI_WT_UNROLL 2
+#endif
+constexpr int UNI_WT_UNROLL = SDL_UNI_WT_UNROLL;  // word-table probes in flight per lane
 #ifndef SDL_UNI_TASK_CAP
 #define SDL_UNI_TASK_CAP 256
 #endif
@@ -58,7 +65,11 @@ constexpr int TASK_CAP = SDL_UNI_TASK_CAP;  // probe tasks per round (>= one job
 #ifndef SDL_UNI_DP_LANES
 #define SDL_UNI_DP_LANES 8
 #endif
-constexpr int DP_LANES = SDL_UNI_DP_LANES;
+constexpr int DP_LANES = SDL_UNI_DP_LANES;  // (SDL_UNI_DP_SERIAL: lanes running a whole DP each)
+#ifndef SDL_UNI_DPG
+#define SDL_UNI_DPG 8
+#endif
+constexpr int DPG = SDL_UNI_DPG;  // lanes relaxing one job's candidates together
 constexpr uint8_t CNT_LONG = 0xFF;   // s_cnt of a long item        // lanes running the DP (a round holds few jobs)
 constexpr int TASK_UNROLL = 4;      // probes in flight per lane
 
@@ -372,8 +383,9 @@ __device__ void finalize_item(uint32_t c, uint32_t e, int64_t p, int64_t rec, in
     }
 }
 
-__device__ __forceinline__ int64_t record_of(const uint64_t *off, int64_t R, int64_t p) {
-    int64_t lo = 0, hi = R;
+__device__ __forceinline__ int64_t record_of(const uint64_t *off, int64_t R, int64_t p, int64_t lo = 0,
+                                             int64_t hi = -1) {
+    if (hi < 0) hi = R;
     while (lo < hi) {
         const int64_t mid = (lo + hi) >> 1;
         if ((int64_t)off[mid + 1] <= p) lo = mid + 1; else hi = mid;
@@ -533,7 +545,8 @@ __global__ __launch_bounds__(TOK_THREADS) void k_unigram_chunks(
     // lengths move to their stage slot), which reuse them for the DP nodes:
     // LDS per one-wave block decides how many chunks a CU keeps in flight.
     constexpr int U_CLS = 0, U_PLEN = (WIN + 15) & ~15, U_MED = U_PLEN + CHUNK, U_MED_END = U_MED + 2 * MED_CAP;
-    constexpr int U_END = U_MED_END > DP_LANES * UNI_NODES * 12 ? U_MED_END : DP_LANES * UNI_NODES * 12;
+    constexpr int DP_BYTES = (DP_LANES > 64 / DPG ? DP_LANES : 64 / DPG) * UNI_NODES * 12;
+    constexpr int U_END = U_MED_END > DP_BYTES ? U_MED_END : DP_BYTES;
     __shared__ __attribute__((aligned(16))) uint8_t s_u[U_END];
     uint8_t *const s_cls = s_u + U_CLS;
     __shared__ uint32_t s_rbits[RBITS_WORDS + 1];
@@ -651,76 +664,125 @@ __global__ __launch_bounds__(TOK_THREADS) void k_unigram_chunks(
         const int prel = (int)(s_pieces[pi] & 0xFFFu);
         return (pi + 1 < np ? (int)(s_pieces[pi + 1] & 0xFFFu) : STAGE) - prel;
     };
-    for (int pi = tid; pi < np; pi += TOK_THREADS) {
-        const uint32_t pc = s_pieces[pi];
-        const int prel = (int)(pc & 0xFFFu);
-        const int wi0 = HALO_L + prel;
-        if (pc & (1u << 12)) {
-            int l = 0;
-            const int id = uni_special(T, c0 + prel, N, cbyte, cbnd, &l);
-            stage[prel] = (uint16_t)(id < 0 ? T.unk_id : id);
-            cnt[pi] = 1;
-            continue;
-        }
-        const int room = stage_room(pi);
-        // word end: first whitespace / added token / record start / text end
-        int wi = wi0 + 1;
-        bool simple = cls[wi0] == U_P;
-        int len = 0;
-        for (;; ++wi) {
-            if (wi >= WIN - 8) { len = 0; break; }  // runs past the window
-            if (w0 + wi >= N) { len = wi - wi0; break; }
-            const uint32_t k = cls[wi];
-            if (k == U_WS || k == U_SPEC || is_rs(wi)) { len = wi - wi0; break; }
-            simple = simple && k == U_P;
-        }
-        s_plen[pi] = (uint8_t)(len <= UNI_WMAX ? len : 0);
-        bool done = false;
-        if (len > 0 && len <= UNI_WMAX && simple) {
-            int packed;
-            if (len <= 16) {
-                const W16 w = lds_w16(w32, wi0, len);
-                packed = probe_result(probe_load_words(T, hash16(w, (uint32_t)len, UC_WORD)),
-                                      (uint32_t)len | (UC_WORD << 8), w);
-            } else {
-                packed = probe_acc(T, [&](int i) -> uint32_t { return win[wi0 + i]; }, 0, len, UC_WORD);
+    const lds_u32 *cls32 = (const lds_u32 *)s_cls;
+    // Length of the raw word starting at window index wi0: 1..UNI_WMAX, 0 when it
+    // runs past the window, UNI_WMAX + 1 when longer (its end is found by the
+    // long-item kernel); *simple = printable ASCII only.  Its first 20 classes
+    // come in 6 independent dword loads, the end is a bit scan.
+    auto word_len = [&](int wi0, bool *simple) -> int {
+        const int a = wi0 >> 2;
+        const uint32_t sh = (uint32_t)(wi0 & 3);
+        uint32_t d[6];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) d[k] = cls32[a + k];
+        uint32_t bnd = 0, nonp = 0;  // bit q: class at offset q is a word boundary / not U_P
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            const uint32_t c = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                const uint32_t v = (c >> (8 * b)) & 0xFFu;
+                bnd |= (v == U_WS || v == U_SPEC ? 1u : 0u) << (4 * k + b);
+                nonp |= (v != U_P ? 1u : 0u) << (4 * k + b);
             }
-            if (packed >= 0 && (packed >> 24) <= room) {
-                const int k = packed >> 24;
-                const uint32_t x = (uint32_t)packed & 0xFFFFFFu;
-                if (k == 1) stage[prel] = (uint16_t)x;
-                else
-                    for (int j = 0; j < k; ++j) stage[prel + j] = T.wres[x + j];
-                cnt[pi] = (uint8_t)k;
-                done = true;
-            } else if (packed < 0 && len + 1 <= room) {  // Viterbi yields <= len + 1 ids
-                // miss: one Viterbi piece, the word's bytes in the window
-                const uint32_t vp = atomicAdd(&s_scratch[1], 1u);
-                if (vp < VP_CAP) {
-                    const uint32_t jb = atomicAdd(&s_scratch[0], 1u);
-                    if (jb < JOB_CAP) {
-                        s_vp_src[vp] = (uint16_t)wi0;
-                        s_vp_len[vp] = (uint8_t)len;
-                        s_job_pi[jb] = (uint16_t)pi;
-                        s_job_vp[jb] = (uint16_t)vp;
-                        s_job_nvp[jb] = 1;
-                        cnt[pi] = 0;
-                        done = true;
+        }
+        const uint64_t rw = ((uint64_t)rbits[(wi0 >> 5) + 1] << 32) | rbits[wi0 >> 5];
+        bnd |= (uint32_t)(rw >> (wi0 & 31));            // record starts
+        const int64_t lim_n = N - (w0 + wi0);           // offsets >= lim_n: past the text
+        if (lim_n <= (int64_t)UNI_WMAX) bnd |= ~0u << (int)lim_n;
+        bnd &= ((2u << UNI_WMAX) - 1u) & ~1u;           // offsets 1 .. UNI_WMAX
+        const int qb = bnd ? __builtin_ctz(bnd) : UNI_WMAX + 1;
+        const int qp = WIN - 8 - wi0;                   // first offset past the window
+        if (qp <= qb) return 0;
+        *simple = qb <= UNI_WMAX && (nonp & ((1u << qb) - 1u)) == 0u;
+        return qb;
+    };
+    for (int p0 = 0; p0 < np; p0 += TOK_THREADS * UNI_WT_UNROLL) {
+        // word-table probes of this lane's next UNI_WT_UNROLL pieces, in flight together
+        Probe P[UNI_WT_UNROLL];
+        W16 W[UNI_WT_UNROLL];
+        int len_u[UNI_WT_UNROLL];
+        uint32_t kind[UNI_WT_UNROLL];  // 0 none, 1 probe, 2 medium, 3 long
+#pragma unroll
+        for (int u = 0; u < UNI_WT_UNROLL; ++u) {
+            const int pi = p0 + u * TOK_THREADS + tid;
+            kind[u] = 0;
+            len_u[u] = 0;
+            W[u] = W16{0, 0, 0, 0};
+            if (pi >= np) continue;
+            const uint32_t pc = s_pieces[pi];
+            const int prel = (int)(pc & 0xFFFu);
+            const int wi0 = HALO_L + prel;
+            if (pc & (1u << 12)) {
+                int l = 0;
+                const int id = uni_special(T, c0 + prel, N, cbyte, cbnd, &l);
+                stage[prel] = (uint16_t)(id < 0 ? T.unk_id : id);
+                cnt[pi] = 1;
+                continue;
+            }
+            bool simple = false;
+            const int len = word_len(wi0, &simple);
+            len_u[u] = len;
+            s_plen[pi] = (uint8_t)(len <= UNI_WMAX ? len : 0);
+            if (len > 0 && len <= UNI_WMAX && simple) {
+                W[u] = lds_w16(w32, wi0, len);
+                P[u] = probe_load_words(T, hash16(W[u], (uint32_t)len, UC_WORD));
+                kind[u] = 1;
+            } else {
+                kind[u] = len > 0 && len <= UNI_WMAX ? 2u : 3u;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < UNI_WT_UNROLL; ++u) {
+            if (kind[u] == 0) continue;
+            const int pi = p0 + u * TOK_THREADS + tid;
+            const int prel = (int)(s_pieces[pi] & 0xFFFu);
+            const int wi0 = HALO_L + prel;
+            const int len = len_u[u];
+            const int room = stage_room(pi);
+            bool done = false;
+            if (kind[u] == 1) {
+                const int packed = probe_result(P[u], (uint32_t)len | (UC_WORD << 8), W[u]);
+                if (packed >= 0 && (packed >> 24) <= room) {
+                    const int k = packed >> 24;
+                    const uint32_t x = (uint32_t)packed & 0xFFFFFFu;
+                    if (k == 1) stage[prel] = (uint16_t)x;
+                    else
+                        for (int j = 0; j < k; ++j) stage[prel + j] = T.wres[x + j];
+                    cnt[pi] = (uint8_t)k;
+                    done = true;
+                } else if (packed < 0 && len + 1 <= room) {  // Viterbi yields <= len + 1 ids
+                    // miss: one Viterbi piece, the word's bytes in the window
+                    const uint32_t vp = atomicAdd(&s_scratch[1], 1u);
+                    if (vp < VP_CAP) {
+                        const uint32_t jb = atomicAdd(&s_scratch[0], 1u);
+                        if (jb < JOB_CAP) {
+                            s_vp_src[vp] = (uint16_t)wi0;
+                            s_vp_len[vp] = (uint8_t)len;
+                            s_job_pi[jb] = (uint16_t)pi;
+                            s_job_vp[jb] = (uint16_t)vp;
+                            s_job_nvp[jb] = 1;
+                            cnt[pi] = 0;
+                            done = true;
+                        }
                     }
                 }
+            } else if (kind[u] == 2) {
+#ifdef SDL_UNI_MEDIUM_LONG  // diagnostic: medium words go to the long-item kernel
+                if (len > 0) { cnt[pi] = CNT_LONG; stage[prel] = (uint16_t)len; continue; }
+#endif
+                // medium word: normalized in the next pass, all lanes at once
+                const uint32_t mq = atomicAdd(&s_scratch[3], 1u);
+                if (mq < (uint32_t)MED_CAP) {
+                    s_med[mq] = (uint16_t)pi;
+                    cnt[pi] = 0;
+                    done = true;
+                }
             }
-        } else if (len > 0 && len <= UNI_WMAX) {
-            // medium word: normalized in the next pass, all lanes at once
-            const uint32_t mq = atomicAdd(&s_scratch[3], 1u);
-            if (mq < (uint32_t)MED_CAP) {
-                s_med[mq] = (uint16_t)pi;
-                cnt[pi] = 0;
-                done = true;
+            if (!done) {  // long item: finished by k_unigram_long; its length (0: unknown) in its stage slot
+                cnt[pi] = CNT_LONG;
+                stage[prel] = (uint16_t)(len <= UNI_WMAX ? len : 0);
             }
-        }
-        if (!done) {  // long item: finished by k_unigram_long; its length in its stage slot
-            cnt[pi] = CNT_LONG;
-            stage[prel] = (uint16_t)len;
         }
     }
     __syncthreads();
@@ -836,7 +898,9 @@ __global__ __launch_bounds__(TOK_THREADS) void k_unigram_chunks(
         s_job_rb[nj] = (uint16_t)rcarry;
     }
     __syncthreads();
+#ifdef SDL_UNI_DP_SERIAL
     const LdsNodes nodes{(lds_f64 *)s_u, (lds_u32 *)(s_u + DP_LANES * UNI_NODES * 8), lane};
+#endif
     for (int j0 = 0; j0 < nj;) {
         // the round: jobs [j0, j1) whose tasks fit TASK_CAP (one job always does)
         int lo = j0 + 1, hi = nj;
@@ -987,6 +1051,91 @@ __global__ __launch_bounds__(TOK_THREADS) void k_unigram_chunks(
 #endif
         __syncthreads();
         UNI_STAMP(6);
+#ifndef SDL_UNI_DP_SERIAL
+        // -- DP: a group of DPG lanes per job.  Starts are visited in order; the
+        //    candidates of one start end at distinct nodes, so the group's lanes
+        //    relax them together (same visit order and strict-> replacement as
+        //    unigram_viterbi_masked), then lane 0 of the group backtracks.  The
+        //    groups' loops diverge; lanes of a group meet through LDS in program
+        //    order (wave_sync: one wave per block) --
+        {
+            const int grp = lane / DPG, gl = lane % DPG;
+            lds_f64 *gsc = (lds_f64 *)s_u + grp * UNI_NODES;
+            lds_u32 *gbp = (lds_u32 *)(s_u + (64 / DPG) * UNI_NODES * 8) + grp * UNI_NODES;
+            auto wave_sync = [] {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            };
+            for (int jb = j0 + grp; jb < j1; jb += 64 / DPG) {
+                const int pi = s_job_pi[jb];
+                const int prel = (int)(s_pieces[pi] & 0xFFFu);
+                int toff = (int)(s_job_tb[jb] - T0);
+                int roff = (int)(s_job_rb[jb] - RB0);
+                int ktot = 0;
+                for (int q = 0; q < s_job_nvp[jb]; ++q) {
+                    const int vp = s_job_vp[jb] + q;
+                    const int L = s_vp_len[vp], src = s_vp_src[vp];
+                    const int n = L + 3;  // "▁" + payload
+                    auto acc = [&](int x) -> uint32_t { return x < 3 ? kMetaBytes[x] : (uint32_t)bytes[src + x - 3]; };
+                    auto rowmask = [&](int st) -> uint32_t { return s_rowmask[roff + (st == 0 ? 0 : st - 2)]; };
+                    for (int x = gl; x <= n; x += DPG) {
+                        gsc[x] = 0.0;
+                        gbp[x] = 0xFFFFFFFFu;
+                    }
+                    wave_sync();
+                    for (int st = 0; st < n;) {
+                        const int l0 = u8len_lead(acc(st));
+                        const int mb = l0 < n - st ? l0 : n - st;
+                        const double base = gsc[st];
+                        const int fe = st == 0 ? 3 : st + 1;
+                        const uint32_t m = rowmask(st);
+                        const bool single = (m >> (st + mb - fe)) & 1u;
+                        for (int k = gl; k < 32 && (m >> k); k += DPG) {
+                            if (!((m >> k) & 1u)) continue;
+                            const int e = fe + k;
+                            const int loc = toff + vp_local(st == 0 ? -1 : st - 3, e - 3, L, Mm, Mf);
+                            const double c = (double)s_tsc[loc] + base;
+                            if (gbp[e] == 0xFFFFFFFFu || c > gsc[e]) {
+                                gsc[e] = c;
+                                gbp[e] = (uint32_t)st | ((uint32_t)s_tid[loc] << 16);
+                            }
+                        }
+                        if (!single && gl == DPG - 1) {  // unk: ends where no piece candidate does
+                            const double c = T.unk_score + base;
+                            const int e = st + mb;
+                            if (gbp[e] == 0xFFFFFFFFu || c > gsc[e]) {
+                                gsc[e] = c;
+                                gbp[e] = (uint32_t)st | ((uint32_t)T.unk_id << 16);
+                            }
+                        }
+                        wave_sync();
+                        st += mb;
+                    }
+                    if (gl == 0) {
+                        struct {
+                            lds_u32 *bp;
+                            __device__ int start(int x) const { return bp[x] == 0xFFFFFFFFu ? -1 : (int)(bp[x] & 0xFFFFu); }
+                            __device__ int id(int x) const { return bp[x] == 0xFFFFFFFFu ? -1 : (int)(bp[x] >> 16); }
+                        } gnodes{gbp};
+                        auto cand = [&](int st, int e, double *sc) -> int {  // the fused-unk lookup
+                            const int loc = vp_local(st == 0 ? -1 : st - 3, e - 3, L, Mm, Mf);
+                            if (loc < 0 || !((rowmask(st) >> (e - (st == 0 ? 3 : st + 1))) & 1u)) return -1;
+                            *sc = (double)s_tsc[toff + loc];
+                            return (int)s_tid[toff + loc];
+                        };
+                        const int base = ktot;
+                        ktot += unigram_backtrack(n, cand, gnodes, T.unk_id,
+                                                  [&](int x, int id) { stage[prel + base + x] = (uint16_t)id; });
+                    }
+                    wave_sync();  // the nodes are re-initialised for the next piece
+                    toff += vp_tasks(L, Mm, Mf);
+                    roff += L + 1;
+                }
+                if (gl == 0) cnt[pi] = (uint8_t)ktot;
+            }
+        }
+#else
         // -- DP: lane per job --
         for (int jb = j0 + lane; lane < DP_LANES && jb < j1; jb += DP_LANES) {
             const int pi = s_job_pi[jb];
@@ -1018,6 +1167,7 @@ __global__ __launch_bounds__(TOK_THREADS) void k_unigram_chunks(
             }
             cnt[pi] = (uint8_t)ktot;
         }
+#endif
         __syncthreads();
         UNI_STAMP(7);
         j0 = j1;
@@ -1097,6 +1247,7 @@ constexpr int LONG_RAW = 1024;
 template <int KMAX>
 __global__ __launch_bounds__(64) void k_unigram_long(DevTok T, const uint8_t *__restrict__ text, int64_t N,
                                                      const uint64_t *__restrict__ off, int64_t R,
+                                                     const uint32_t *__restrict__ ranges,
                                                      const uint4 *__restrict__ items, uint32_t item_cap,
                                                      uint32_t *counters, uint32_t *tokc, uint32_t *chunk_cnt,
                                                      uint32_t *rec_local, uint32_t *pool, uint32_t pool_cap,
@@ -1119,7 +1270,10 @@ __global__ __launch_bounds__(64) void k_unigram_long(DevTok T, const uint8_t *__
     for (uint32_t it_i = blockIdx.x; it_i < n_items; it_i += gridDim.x) {
         const uint4 it = items[it_i];
         const int64_t p = (int64_t)it.x * CHUNK + it.z;
-        const int64_t rec = record_of(off, R, p);
+        // the record holding p: between the last one starting before its chunk
+        // and the first one starting past its window (k_chunk_ranges)
+        const int64_t r_lo = ranges[3 * (int64_t)it.x + 2], r_hi = ranges[3 * (int64_t)it.x + 1];
+        const int64_t rec = record_of(off, R, p, r_lo > 0 ? r_lo - 1 : 0, (r_hi < R ? r_hi : R) - 1);
         const int64_t pa = (p - 1) & ~(int64_t)15;  // staged raw bytes: [pa, pa + LONG_RAW)
         *reinterpret_cast<uint4 *>(s_raw + 16 * lane) = load16(text, pa + 16 * lane, N);
         __syncthreads();
@@ -1252,37 +1406,36 @@ __global__ __launch_bounds__(64) void k_unigram_long(DevTok T, const uint8_t *__
                 }
                 s_mask[lane] = mask;
                 __syncthreads();
-                if (lane == 0) {  // relax the nodes from these rows' starts, in order
-                    const int rz = L + 1 - r0 < 64 ? L + 1 - r0 : 64;
-                    for (int q = 0; q < rz; ++q) {
-                        const int r = r0 + q;
-                        const int st = r == 0 ? 0 : r + 2;  // node position of the row's start
-                        if (r > 1 && (nb[src + r - 1] & 0xC0u) == 0x80u) continue;
-                        const int l0 = u8len_lead(acc(st));
-                        const int mb = l0 < n - st ? l0 : n - st;
-                        const double base = s_sc[st];
-                        const int fe = st == 0 ? 3 : st + 1;
-                        unsigned long long m = s_mask[q];
-                        const bool single = (m >> (st + mb - fe)) & 1ull;
-                        while (m) {
-                            const int k = __builtin_ctzll(m);
-                            m &= m - 1;
-                            const int e = fe + k;
-                            const double c = (double)s_csc[k * 64 + q] + base;
-                            if (s_st[e] == 0xFFFFFFFFu || c > s_sc[e]) {
-                                s_sc[e] = c;
-                                s_st[e] = (uint32_t)st | ((uint32_t)s_cid[k * 64 + q] << 16);
-                            }
-                        }
-                        if (!single) {
-                            const double c = T.unk_score + base;
-                            const int e = st + mb;
-                            if (s_st[e] == 0xFFFFFFFFu || c > s_sc[e]) {
-                                s_sc[e] = c;
-                                s_st[e] = (uint32_t)st | ((uint32_t)T.unk_id << 16);
-                            }
+                // relax the nodes from these rows' starts, in order; a row's candidates
+                // end at distinct nodes, so lane k relaxes the row's k-th end
+                const int rz = L + 1 - r0 < 64 ? L + 1 - r0 : 64;
+                for (int q = 0; q < rz; ++q) {
+                    const int r = r0 + q;
+                    const int st = r == 0 ? 0 : r + 2;  // node position of the row's start
+                    if (r > 1 && (nb[src + r - 1] & 0xC0u) == 0x80u) continue;
+                    const int l0 = u8len_lead(acc(st));
+                    const int mb = l0 < n - st ? l0 : n - st;
+                    const double base = s_sc[st];
+                    const int fe = st == 0 ? 3 : st + 1;
+                    const unsigned long long m = s_mask[q];
+                    const bool single = (m >> (st + mb - fe)) & 1ull;
+                    if (lane < KMAX && ((m >> lane) & 1ull)) {
+                        const int e = fe + lane;
+                        const double c = (double)s_csc[lane * 64 + q] + base;
+                        if (s_st[e] == 0xFFFFFFFFu || c > s_sc[e]) {
+                            s_sc[e] = c;
+                            s_st[e] = (uint32_t)st | ((uint32_t)s_cid[lane * 64 + q] << 16);
                         }
                     }
+                    if (!single && lane == 63) {  // the unk candidate ends where no piece candidate does
+                        const double c = T.unk_score + base;
+                        const int e = st + mb;
+                        if (s_st[e] == 0xFFFFFFFFu || c > s_sc[e]) {
+                            s_sc[e] = c;
+                            s_st[e] = (uint32_t)st | ((uint32_t)T.unk_id << 16);
+                        }
+                    }
+                    __syncthreads();
                 }
                 __syncthreads();
             }
@@ -1352,11 +1505,11 @@ hipError_t launch_unigram_chunks(const DevTok &T, const uint8_t *text, int64_t N
     // a row's candidate ends: <= Mm + 1 ("▁" row) or <= Mf
     if (T.maxlen_meta + 1 <= 32 && T.maxlen_first <= 32)
         hipLaunchKernelGGL(k_unigram_long<32>, dim3((unsigned)W.lane_blocks), dim3(64), 0, st, T, text, N, off, R,
-                           W.items, W.item_cap, W.counters, tokc, chunk_cnt, rec_local, W.pool, W.pool_cap, W.huge,
+                           ranges, W.items, W.item_cap, W.counters, tokc, chunk_cnt, rec_local, W.pool, W.pool_cap, W.huge,
                            W.huge_cap, W.err);
     else
         hipLaunchKernelGGL(k_unigram_long<64>, dim3((unsigned)W.lane_blocks), dim3(64), 0, st, T, text, N, off, R,
-                           W.items, W.item_cap, W.counters, tokc, chunk_cnt, rec_local, W.pool, W.pool_cap, W.huge,
+                           ranges, W.items, W.item_cap, W.counters, tokc, chunk_cnt, rec_local, W.pool, W.pool_cap, W.huge,
                            W.huge_cap, W.err);
     hipLaunchKernelGGL(k_unigram_huge, dim3((unsigned)W.huge_blocks), dim3(64), 0, st, T, text, N, off, R, W.counters,
                        tokc, chunk_cnt, rec_local, W.scratch, W.pool, W.pool_cap, W.huge, W.huge_cap, W.err);
