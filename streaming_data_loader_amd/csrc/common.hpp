@@ -150,6 +150,7 @@ struct DevTok {
     uint32_t wslot_mask;
     const uint16_t *cpage;   // per-code-point entry pages (0x110000/256)
     const uint2 *cent;       // entry blocks of 256 (CP_* layout)
+    const uint2 *cbmp;       // ... flattened for U+0000..U+FFFF (one load per BMP char)
     const uint32_t *trie;    // Precompiled charsmap: double-array units
     const uint8_t *tnorm;    // ... and its NUL-separated normalized strings
     uint32_t trie_units, tnorm_len;

@@ -248,7 +248,7 @@ struct sdl_batcher {
     // unigram (t5)
     DevBuf<double> d_uscore;
     DevBuf<uint16_t> d_wres, d_cpage;
-    DevBuf<uint2> d_cent;
+    DevBuf<uint2> d_cent, d_cbmp;
     DevBuf<float> d_uscore32;
     DevBuf<uint8_t> d_tnorm;
     DevBuf<uint32_t> d_trie;
@@ -692,6 +692,17 @@ int sdl_batcher_create(const sdl_config *cfg, const char *tokenizer_path, const 
             d.wres = h->d_wres.p;
             d.cpage = h->d_cpage.p;
             d.cent = h->d_cent.p;
+            {  // the BMP entries flattened: one dependent load per char instead of two
+                std::vector<uint32_t> flat(2 * 0x10000);
+                for (uint32_t cp = 0; cp < 0x10000; ++cp) {
+                    const size_t at = 2 * ((size_t)t.cpage[cp >> 8] * 256 + (cp & 255));
+                    flat[2 * cp] = t.cent[at];
+                    flat[2 * cp + 1] = t.cent[at + 1];
+                }
+                h->d_cbmp.ensure(0x10000);
+                HIP_TRY(hipMemcpy(h->d_cbmp.p, flat.data(), flat.size() * 4, hipMemcpyHostToDevice));
+                d.cbmp = h->d_cbmp.p;
+            }
             d.uscore32 = h->d_uscore32.p;
             d.trie = h->d_trie.p;
             d.tnorm = h->d_tnorm.p;

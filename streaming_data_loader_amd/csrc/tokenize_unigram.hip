@@ -83,6 +83,7 @@ __device__ __forceinline__ uint32_t uni_ascii(uint32_t b) {
 __device__ __forceinline__ bool ascii_ws(uint32_t b) { return b == 32u || b == 9u || b == 10u || b == 12u || b == 13u; }
 
 __device__ __forceinline__ uint2 cp_ent(const DevTok &T, uint32_t cp) {
+    if (cp < 0x10000u) return T.cbmp[cp];
     if (cp >= 0x110000u) cp = 0xFFFDu;
     return T.cent[(uint32_t)T.cpage[cp >> 8] * 256u + (cp & 255u)];
 }
