@@ -62,10 +62,6 @@ constexpr int UNI_WT_UNROLL = SDL_UNI_WT_UNROLL;  // word-table probes in flight
 #define SDL_UNI_TASK_CAP 256
 #endif
 constexpr int TASK_CAP = SDL_UNI_TASK_CAP;  // probe tasks per round (>= one job's: L <= UNI_WMAX)
-#ifndef SDL_UNI_DP_LANES
-#define SDL_UNI_DP_LANES 8
-#endif
-constexpr int DP_LANES = SDL_UNI_DP_LANES;  // (SDL_UNI_DP_SERIAL: lanes running a whole DP each)
 #ifndef SDL_UNI_DPG
 #define SDL_UNI_DPG 8
 #endif
@@ -477,26 +473,6 @@ __device__ __forceinline__ void vp_decode(int t, int L, int Mm, int Mf, int *i, 
     *j = row + 1 + r;
 }
 
-// Per-lane LDS nodes of the DP lanes (node-major: conflict-free)
-struct LdsNodes {
-    lds_f64 *sc;
-    lds_u32 *bp;
-    int lane;
-    __device__ void set(int i, double s, int st, int id) const {
-        sc[i * DP_LANES + lane] = s;
-        bp[i * DP_LANES + lane] = (uint32_t)(st & 0xFFFF) | ((uint32_t)(id & 0xFFFF) << 16);
-    }
-    __device__ double score(int i) const { return sc[i * DP_LANES + lane]; }
-    __device__ int start(int i) const {
-        const uint32_t v = bp[i * DP_LANES + lane] & 0xFFFFu;
-        return v == 0xFFFFu ? -1 : (int)v;
-    }
-    __device__ int id(int i) const {
-        const uint32_t v = bp[i * DP_LANES + lane] >> 16;
-        return v == 0xFFFFu ? -1 : (int)v;
-    }
-};
-
 // 16 bytes at LDS byte offset b (dword loads + alignbyte), first n kept
 __device__ __forceinline__ W16 lds_w16(const lds_u32 *w32, int b, int n) {
     const int a = b >> 2;
@@ -546,7 +522,7 @@ __global__ __launch_bounds__(TOK_THREADS) void k_unigram_chunks(
     // lengths move to their stage slot), which reuse them for the DP nodes:
     // LDS per one-wave block decides how many chunks a CU keeps in flight.
     constexpr int U_CLS = 0, U_PLEN = (WIN + 15) & ~15, U_MED = U_PLEN + CHUNK, U_MED_END = U_MED + 2 * MED_CAP;
-    constexpr int DP_BYTES = (DP_LANES > 64 / DPG ? DP_LANES : 64 / DPG) * UNI_NODES * 12;
+    constexpr int DP_BYTES = (64 / DPG) * UNI_NODES * 12;
     constexpr int U_END = U_MED_END > DP_BYTES ? U_MED_END : DP_BYTES;
     __shared__ __attribute__((aligned(16))) uint8_t s_u[U_END];
     uint8_t *const s_cls = s_u + U_CLS;
@@ -899,160 +875,94 @@ __global__ __launch_bounds__(TOK_THREADS) void k_unigram_chunks(
         s_job_rb[nj] = (uint16_t)rcarry;
     }
     __syncthreads();
-#ifdef SDL_UNI_DP_SERIAL
-    const LdsNodes nodes{(lds_f64 *)s_u, (lds_u32 *)(s_u + DP_LANES * UNI_NODES * 8), lane};
-#endif
-    for (int j0 = 0; j0 < nj;) {
-        // the round: jobs [j0, j1) whose tasks fit TASK_CAP (one job always does)
-        int lo = j0 + 1, hi = nj;
+    // Rounds are software-pipelined: round r + 1's probes are issued right after
+    // round r's results land in LDS, and are in flight while round r's DP runs.
+    static_assert(TASK_CAP <= 64 * TASK_UNROLL, "a round's tasks are one probe batch");
+    auto round_end = [&](int a) -> int {  // jobs [a, end) whose tasks fit TASK_CAP (one job always does)
+        int lo = a + 1, hi = nj;
         while (lo < hi) {
             const int m = (lo + hi + 1) >> 1;
-            if (s_job_tb[m] - s_job_tb[j0] <= (uint32_t)TASK_CAP) lo = m; else hi = m - 1;
+            if (s_job_tb[m] - s_job_tb[a] <= (uint32_t)TASK_CAP) lo = m; else hi = m - 1;
         }
-        const int j1 = lo;
-        const uint32_t T0 = s_job_tb[j0], RB0 = s_job_rb[j0];
-        const int nt = (int)(s_job_tb[j1] - T0);
-        for (int r = lane; r < (int)(s_job_rb[j1] - RB0); r += 64) s_rowmask[r] = 0u;
-        __syncthreads();
-#ifndef SDL_UNI_LANE_ROWS
-        // -- candidate probes: the round's tasks (one candidate (start, end) of
-        //    one piece each) dealt to all 64 lanes, TASK_UNROLL in flight per lane,
-        //    so a round costs ceil(tasks / 256) probe latencies whatever its rows' lengths --
-        for (int tq = 0; tq < nt; tq += 64 * TASK_UNROLL) {
-            Probe P[TASK_UNROLL];
-            W16 W[TASK_UNROLL];
-            uint32_t meta[TASK_UNROLL];  // row | k << 16 | n << 22 | cont << 29; ~0u: no probe
-            int gen[TASK_UNROLL];        // generic probe (payload > 16 bytes); -2: use P
-            uint32_t gw3[TASK_UNROLL];
+        return lo;
+    };
+    // candidate probes: task t = 64 u + lane of the round (one candidate (start,
+    // end) of one piece), TASK_UNROLL in flight per lane
+    Probe P[TASK_UNROLL];
+    W16 W[TASK_UNROLL];
+    uint32_t meta[TASK_UNROLL];  // row | k << 16 | n << 22 | cont << 29; ~0u: no probe
+    int gen[TASK_UNROLL];        // generic probe result (payload > 16 bytes); -2: use P
+    uint32_t gw3[TASK_UNROLL];
+    auto issue = [&](int ja, int jz) {
+        const uint32_t T0 = s_job_tb[ja], RB0 = s_job_rb[ja];
+        const int nt = (int)(s_job_tb[jz] - T0);
 #pragma unroll
-            for (int u = 0; u < TASK_UNROLL; ++u) {
-                const int t = tq + 64 * u + lane;
-                meta[u] = ~0u;
-                gen[u] = -2;
-                gw3[u] = 0;
-                W[u] = W16{0, 0, 0, 0};
-                if (t >= nt) continue;
-                const uint32_t gt = T0 + (uint32_t)t;
-                int a = j0, b = j1 - 1;  // the job holding task gt
-                while (a < b) {
-                    const int m = (a + b + 1) >> 1;
-                    if (s_job_tb[m] <= gt) a = m; else b = m - 1;
-                }
-                int lt = (int)(gt - s_job_tb[a]);
-                int row = (int)(s_job_rb[a] - RB0);
-                int vp = s_job_vp[a];
-                for (int q = 0; q + 1 < s_job_nvp[a]; ++q) {
-                    const int Lq = s_vp_len[vp];
-                    const int tk = vp_tasks(Lq, Mm, Mf);
-                    if (lt < tk) break;
-                    lt -= tk;
-                    row += Lq + 1;
-                    ++vp;
-                }
-                const int L = s_vp_len[vp], src = s_vp_src[vp];
-                int i, j;  // payload start (-1: the "▁" row) and end
-                vp_decode(lt, L, Mm, Mf, &i, &j);
-                // candidates start and end on char boundaries
-                if ((i > 0 && (bytes[src + i] & 0xC0u) == 0x80u) || (j < L && (bytes[src + j] & 0xC0u) == 0x80u))
-                    continue;
-                const int ps = i < 0 ? 0 : i;
-                const int n = j - ps;
-                const uint32_t cont = i < 0 ? UC_META : UC_PIECE;
-                meta[u] = (uint32_t)(row + i + 1) | (uint32_t)(j - (i < 0 ? 0 : i + 1)) << 16 | (uint32_t)n << 22 |
-                          cont << 29;
-                if (n <= 16) {
-                    W[u] = lds_w16(w32, src + ps, n);
-                    P[u] = probe_load(T, hash16(W[u], (uint32_t)n, cont));
-                } else {
-                    gen[u] = probe_acc(T, [&](int x) -> uint32_t { return bytes[src + x]; }, ps, n, cont, &gw3[u]);
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < TASK_UNROLL; ++u) {
-                if (meta[u] == ~0u) continue;
-                uint32_t w3 = gw3[u];
-                const uint32_t key = ((meta[u] >> 22) & 0x7Fu) | ((meta[u] >> 29) << 8);
-                const int id = gen[u] != -2 ? gen[u] : probe_result_w3(P[u], key, W[u], &w3);
-                if (id < 0) continue;
-                const int t = tq + 64 * u + lane;
-                s_tid[t] = (uint16_t)id;
-                s_tsc[t] = __uint_as_float(w3);  // the slot's score (f32, exact)
-                atomicOr(&s_rowmask[meta[u] & 0xFFFFu], 1u << ((meta[u] >> 16) & 0x3Fu));
-            }
-        }
-#else
-        // -- candidate rows: lane per row (one start of one piece), 4 probes in flight --
-        const int nrows = (int)(s_job_rb[j1] - RB0);
-        for (int r = lane; r < nrows; r += 64) {
-            const uint32_t gr = RB0 + (uint32_t)r;
-            int a = j0, b = j1 - 1;  // the job holding row gr
+        for (int u = 0; u < TASK_UNROLL; ++u) {
+            const int t = 64 * u + lane;
+            meta[u] = ~0u;
+            gen[u] = -2;
+            gw3[u] = 0;
+            W[u] = W16{0, 0, 0, 0};
+            if (t >= nt) continue;
+            const uint32_t gt = T0 + (uint32_t)t;
+            int a = ja, b = jz - 1;  // the job holding task gt
             while (a < b) {
                 const int m = (a + b + 1) >> 1;
-                if (s_job_rb[m] <= gr) a = m; else b = m - 1;
+                if (s_job_tb[m] <= gt) a = m; else b = m - 1;
             }
-            int lr = (int)(gr - s_job_rb[a]);
+            int lt = (int)(gt - s_job_tb[a]);
+            int row = (int)(s_job_rb[a] - RB0);
             int vp = s_job_vp[a];
-            int tb = (int)(s_job_tb[a] - T0);
-            for (int q = 0;; ++q) {
+            for (int q = 0; q + 1 < s_job_nvp[a]; ++q) {
                 const int Lq = s_vp_len[vp];
-                if (lr < Lq + 1 || q + 1 >= s_job_nvp[a]) break;
-                lr -= Lq + 1;
-                tb += vp_tasks(Lq, Mm, Mf);
+                const int tk = vp_tasks(Lq, Mm, Mf);
+                if (lt < tk) break;
+                lt -= tk;
+                row += Lq + 1;
                 ++vp;
             }
             const int L = s_vp_len[vp], src = s_vp_src[vp];
-            const int i = lr - 1;  // payload start; -1: the "▁" row
-            uint32_t mask = 0u;
-            if (!(i > 0 && (bytes[src + i] & 0xC0u) == 0x80u)) {  // rows start on char boundaries
-                const int ps = i < 0 ? 0 : i;
-                const int jlo = i < 0 ? 0 : i + 1;
-                const int jmax = i < 0 ? (L < Mm ? L : Mm) : (L < i + Mf ? L : i + Mf);
-                const int tbr = tb + (i < 0 ? 0 : vp_c0(L, Mm) + vp_rowoff(i, L, Mf));
-                const uint32_t cont = i < 0 ? UC_META : UC_PIECE;
-                for (int jb = jlo; jb <= jmax; jb += TASK_UNROLL) {
-                    Probe P[TASK_UNROLL];
-                    W16 W[TASK_UNROLL];
-                    bool live[TASK_UNROLL];
-                    int gen[TASK_UNROLL];  // generic probe (payload > 16 bytes); -2: use P
-                    uint32_t gw3[TASK_UNROLL];
-#pragma unroll
-                    for (int u = 0; u < TASK_UNROLL; ++u) {
-                        const int j = jb + u;
-                        live[u] = j <= jmax && !(j < L && (bytes[src + j] & 0xC0u) == 0x80u);
-                        gen[u] = -2;
-                        gw3[u] = 0;
-                        W[u] = W16{0, 0, 0, 0};
-                        if (!live[u]) continue;
-                        const int n = j - ps;
-                        if (n <= 16) {
-                            W[u] = lds_w16(w32, src + ps, n);
-                            P[u] = probe_load(T, hash16(W[u], (uint32_t)n, cont));
-                        } else {
-                            gen[u] = probe_acc(T, [&](int x) -> uint32_t { return bytes[src + x]; }, ps, n, cont,
-                                               &gw3[u]);
-                        }
-                    }
-#pragma unroll
-                    for (int u = 0; u < TASK_UNROLL; ++u) {
-                        if (!live[u]) continue;
-                        const int j = jb + u;
-                        uint32_t w3 = gw3[u];
-                        const int id = gen[u] != -2 ? gen[u]
-                                                    : probe_result_w3(P[u], (uint32_t)(j - ps) | (cont << 8), W[u], &w3);
-                        if (id < 0) continue;
-                        const int k = j - jlo;
-                        mask |= 1u << k;
-                        s_tid[tbr + k] = (uint16_t)id;
-                        s_tsc[tbr + k] = __uint_as_float(w3);  // the slot's score (f32, exact)
-                    }
-                }
+            int i, j;  // payload start (-1: the "▁" row) and end
+            vp_decode(lt, L, Mm, Mf, &i, &j);
+            // candidates start and end on char boundaries
+            if ((i > 0 && (bytes[src + i] & 0xC0u) == 0x80u) || (j < L && (bytes[src + j] & 0xC0u) == 0x80u))
+                continue;
+            const int ps = i < 0 ? 0 : i;
+            const int n = j - ps;
+            const uint32_t cont = i < 0 ? UC_META : UC_PIECE;
+            meta[u] = (uint32_t)(row + i + 1) | (uint32_t)(j - (i < 0 ? 0 : i + 1)) << 16 | (uint32_t)n << 22 |
+                      cont << 29;
+            if (n <= 16) {
+                W[u] = lds_w16(w32, src + ps, n);
+                P[u] = probe_load(T, hash16(W[u], (uint32_t)n, cont));
+            } else {
+                gen[u] = probe_acc(T, [&](int x) -> uint32_t { return bytes[src + x]; }, ps, n, cont, &gw3[u]);
             }
-            s_rowmask[r] = mask;
         }
-#endif
+    };
+    int j0 = 0, j1 = nj > 0 ? round_end(0) : 0;
+    if (nj > 0) issue(j0, j1);
+    while (j0 < nj) {
+        const uint32_t T0 = s_job_tb[j0], RB0 = s_job_rb[j0];
+        for (int r = lane; r < (int)(s_job_rb[j1] - RB0); r += 64) s_rowmask[r] = 0u;
+        __syncthreads();
+        // -- this round's probe results -> LDS --
+#pragma unroll
+        for (int u = 0; u < TASK_UNROLL; ++u) {
+            if (meta[u] == ~0u) continue;
+            uint32_t w3 = gw3[u];
+            const uint32_t key = ((meta[u] >> 22) & 0x7Fu) | ((meta[u] >> 29) << 8);
+            const int id = gen[u] != -2 ? gen[u] : probe_result_w3(P[u], key, W[u], &w3);
+            if (id < 0) continue;
+            const int t = 64 * u + lane;
+            s_tid[t] = (uint16_t)id;
+            s_tsc[t] = __uint_as_float(w3);  // the slot's score (f32, exact)
+            atomicOr(&s_rowmask[meta[u] & 0xFFFFu], 1u << ((meta[u] >> 16) & 0x3Fu));
+        }
         __syncthreads();
         UNI_STAMP(6);
-#ifndef SDL_UNI_DP_SERIAL
+        const int n0 = j1, n1 = n0 < nj ? round_end(n0) : n0;
+        if (n0 < nj) issue(n0, n1);  // the next round's probes fly during this DP
         // -- DP: a group of DPG lanes per job.  Starts are visited in order; the
         //    candidates of one start end at distinct nodes, so the group's lanes
         //    relax them together (same visit order and strict-> replacement as
@@ -1136,42 +1046,10 @@ __global__ __launch_bounds__(TOK_THREADS) void k_unigram_chunks(
                 if (gl == 0) cnt[pi] = (uint8_t)ktot;
             }
         }
-#else
-        // -- DP: lane per job --
-        for (int jb = j0 + lane; lane < DP_LANES && jb < j1; jb += DP_LANES) {
-            const int pi = s_job_pi[jb];
-            const int prel = (int)(s_pieces[pi] & 0xFFFu);
-            int toff = (int)(s_job_tb[jb] - T0);
-            int roff = (int)(s_job_rb[jb] - RB0);
-            int ktot = 0;
-            for (int q = 0; q < s_job_nvp[jb]; ++q) {
-                const int vp = s_job_vp[jb] + q;
-                const int L = s_vp_len[vp], src = s_vp_src[vp];
-                auto acc = [&](int x) -> uint32_t { return x < 3 ? kMetaBytes[x] : (uint32_t)bytes[src + x - 3]; };
-                auto rowmask = [&](int s) -> uint32_t { return s_rowmask[roff + (s == 0 ? 0 : s - 2)]; };
-                auto cand = [&](int s, int e, double *sc) -> int {
-                    const int loc = vp_local(s == 0 ? -1 : s - 3, e - 3, L, Mm, Mf);
-                    if (loc < 0 || !((rowmask(s) >> (e - (s == 0 ? 3 : s + 1))) & 1ull)) return -1;
-                    *sc = (double)s_tsc[toff + loc];
-                    return (int)s_tid[toff + loc];
-                };
-                auto at = [&](int s, int e, double *sc) -> int {
-                    const int loc = vp_local(s == 0 ? -1 : s - 3, e - 3, L, Mm, Mf);
-                    *sc = (double)s_tsc[toff + loc];
-                    return (int)s_tid[toff + loc];
-                };
-                const int base = ktot;
-                ktot += unigram_viterbi_masked(acc, L + 3, rowmask, at, cand, nodes, T.unk_score, T.unk_id,
-                                               [&](int x, int id) { stage[prel + base + x] = (uint16_t)id; });
-                toff += vp_tasks(L, Mm, Mf);
-                roff += L + 1;
-            }
-            cnt[pi] = (uint8_t)ktot;
-        }
-#endif
         __syncthreads();
         UNI_STAMP(7);
-        j0 = j1;
+        j0 = n0;
+        j1 = n1;
     }
 
     UNI_STAMP(4);
