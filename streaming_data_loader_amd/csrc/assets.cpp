@@ -855,6 +855,16 @@ static void load_unigram(const JValue &root, const std::string &data_dir, HostTo
     for (const std::string &w : base_words) {
         add_word(w + ",");
         add_word(w + ".");
+#ifndef SDL_T5_SHORT_WORD_TABLE
+        // the next commonest word-table misses in running text: quoted,
+        // parenthesised and colon/question/exclamation-ended words, possessives
+        if ((int)w.size() + 2 <= UNI_WMAX) {
+            for (const char *suf : {":", ";", "?", "!", ")", "\"", "'s", "),", ").", ".\"", ",\""})
+                if ((int)(w.size() + std::strlen(suf)) <= UNI_WMAX) add_word(w + suf);
+            add_word("\"" + w);
+            add_word("(" + w);
+        }
+#endif
     }
     if (t.wres.size() >= (1u << 24)) throw std::runtime_error("word table too large");
     t.wres.push_back(0);
