@@ -1241,49 +1241,55 @@ __global__ __launch_bounds__(64) void k_unigram_long(DevTok T, const uint8_t *__
             };
             __syncthreads();
             for (int r0 = 0; r0 <= L; r0 += 64) {
-                // row r = r0 + lane: r == 0 the "▁" row, else payload start r - 1
-                const int r = r0 + lane;
-                unsigned long long mask = 0ull;
-                if (r <= L && !(r > 1 && (nb[src + r - 1] & 0xC0u) == 0x80u)) {
-                    const int i = r - 1;  // -1: the "▁" row
-                    const int ps = i < 0 ? 0 : i;
-                    const int jmax = i < 0 ? (L < Mm ? L : Mm) : (L < i + Mf ? L : i + Mf);
-                    const uint32_t cont = i < 0 ? UC_META : UC_PIECE;
-                    for (int j0 = i < 0 ? 0 : i + 1; j0 <= jmax; j0 += 4) {
-                        Probe P[4];
-                        W16 W[4];
-                        int gen[4];
-                        bool live[4];
+                // the candidates of rows r0 .. r0 + 63 (row r: payload start r - 1, r == 0
+                // the "▁" row) dealt to all lanes, 4 probes in flight each
+                const int nrow = L + 1 - r0 < 64 ? L + 1 - r0 : 64;
+                const int ta = r0 == 0 ? 0 : vp_c0(L, Mm) + vp_rowoff(r0 - 1, L, Mf);
+                const int tz = r0 + nrow > L ? vp_tasks(L, Mm, Mf) : vp_c0(L, Mm) + vp_rowoff(r0 + nrow - 1, L, Mf);
+                s_mask[lane] = 0ull;
+                __syncthreads();
+                for (int tq = ta; tq < tz; tq += 256) {
+                    Probe P[4];
+                    W16 Wd[4];
+                    int gen[4];
+                    uint32_t gw3[4], meta[4];  // row | k << 8 | len << 16 | cont << 24; ~0u: none
 #pragma unroll
-                        for (int u = 0; u < 4; ++u) {
-                            const int j = j0 + u;
-                            live[u] = j <= jmax && !(j < L && (nb[src + j] & 0xC0u) == 0x80u);
-                            gen[u] = -2;
-                            W[u] = W16{0, 0, 0, 0};
-                            if (!live[u]) continue;
-                            const int len = j - ps;
-                            if (len <= 16) {
-                                W[u] = lds_w16(w32, src + ps, len);
-                                P[u] = probe_load(T, hash16(W[u], (uint32_t)len, cont));
-                            } else {
-                                gen[u] = probe_acc(T, nbr, src + ps, len, cont);
-                            }
-                        }
-#pragma unroll
-                        for (int u = 0; u < 4; ++u) {
-                            if (!live[u]) continue;
-                            const int j = j0 + u;
-                            const uint32_t key = (uint32_t)(j - ps) | (cont << 8);
-                            const int id = gen[u] != -2 ? gen[u] : probe_result(P[u], key, W[u]);
-                            if (id < 0) continue;
-                            const int k = i < 0 ? j : j - i - 1;
-                            mask |= 1ull << k;
-                            s_cid[k * 64 + lane] = (uint16_t)id;
-                            s_csc[k * 64 + lane] = T.uscore32[id];  // k < KMAX (host-checked)
+                    for (int u = 0; u < 4; ++u) {
+                        const int t = tq + 64 * u + lane;
+                        meta[u] = ~0u;
+                        gen[u] = -2;
+                        gw3[u] = 0;
+                        Wd[u] = W16{0, 0, 0, 0};
+                        if (t >= tz) continue;
+                        int i, j;
+                        vp_decode(t, L, Mm, Mf, &i, &j);
+                        if ((i > 0 && (nb[src + i] & 0xC0u) == 0x80u) || (j < L && (nb[src + j] & 0xC0u) == 0x80u))
+                            continue;  // candidates start and end on char boundaries
+                        const int ps = i < 0 ? 0 : i;
+                        const int len = j - ps;
+                        const uint32_t cont = i < 0 ? UC_META : UC_PIECE;
+                        meta[u] = (uint32_t)(i + 1 - r0) | (uint32_t)(i < 0 ? j : j - i - 1) << 8 | (uint32_t)len << 16 |
+                                  cont << 24;
+                        if (len <= 16) {
+                            Wd[u] = lds_w16(w32, src + ps, len);
+                            P[u] = probe_load(T, hash16(Wd[u], (uint32_t)len, cont));
+                        } else {
+                            gen[u] = probe_acc(T, nbr, src + ps, len, cont, &gw3[u]);
                         }
                     }
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        if (meta[u] == ~0u) continue;
+                        uint32_t w3 = gw3[u];
+                        const uint32_t key = ((meta[u] >> 16) & 0xFFu) | ((meta[u] >> 24) << 8);
+                        const int id = gen[u] != -2 ? gen[u] : probe_result_w3(P[u], key, Wd[u], &w3);
+                        if (id < 0) continue;
+                        const int q = (int)(meta[u] & 0xFFu), k = (int)((meta[u] >> 8) & 0xFFu);
+                        s_cid[k * 64 + q] = (uint16_t)id;
+                        s_csc[k * 64 + q] = __uint_as_float(w3);  // the slot's score (f32, exact; k < KMAX host-checked)
+                        atomicOr(&s_mask[q], 1ull << k);
+                    }
                 }
-                s_mask[lane] = mask;
                 __syncthreads();
                 // relax the nodes from these rows' starts, in order; a row's candidates
                 // end at distinct nodes, so lane k relaxes the row's k-th end
