@@ -138,7 +138,14 @@ __global__ __launch_bounds__(256) void k_compact_tokens(const uint32_t *__restri
     uint32_t *dst = tok + chunk_off[c];
     const int lane = threadIdx.x & 63;
     if (!long_count || *long_count == 0) {
-        for (uint32_t i = lane; i < n; i += 64) dst[i] = src[i];
+        // 16-B loads of the (16-B aligned) chunk list, 4 dword stores per lane
+        for (uint32_t i = 4 * lane; i < n; i += 256) {
+            const uint4 v = *reinterpret_cast<const uint4 *>(src + i);
+            dst[i] = v.x;
+            if (i + 1 < n) dst[i + 1] = v.y;
+            if (i + 2 < n) dst[i + 2] = v.z;
+            if (i + 3 < n) dst[i + 3] = v.w;
+        }
         return;
     }
     // byte-level BPE with long pieces: an entry LONG_MARK | i stands for the
