@@ -339,8 +339,11 @@ __device__ __forceinline__ void store4(int32_t *p, int j0, int S, bool vec, int3
     }
 }
 
+#ifndef SDL_ROWS_WAVES
+#define SDL_ROWS_WAVES 1
+#endif
 template <int MR>
-__global__ __launch_bounds__(256) void k_rows(RowParams P, const uint32_t *__restrict__ tok,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SDL_ROWS_WAVES, 8))) void k_rows(RowParams P, const uint32_t *__restrict__ tok,
                                               const uint32_t *__restrict__ rec_tok, const uint32_t *__restrict__ rec_cnt,
                                               const uint32_t *__restrict__ row_off, const uint32_t *__restrict__ row_rec,
                                               const uint32_t *__restrict__ d_rows, int64_t rows_cap, RowOut out) {
@@ -501,8 +504,11 @@ hipError_t launch_rows(const RowParams &P, const uint32_t *tok, const uint32_t *
                        const uint32_t *row_off, const uint32_t *row_rec, const uint32_t *d_rows, int64_t rows_cap,
                        RowOut out, hipStream_t st) {
     if (rows_cap == 0) return hipSuccess;
+#ifndef SDL_ROWS_GRID_CAP
+#define SDL_ROWS_GRID_CAP 16384
+#endif
     const int64_t want = (rows_cap + 3) / 4;
-    const unsigned grid = (unsigned)(want < 4096 ? want : 4096);
+    const unsigned grid = (unsigned)(want < SDL_ROWS_GRID_CAP ? want : SDL_ROWS_GRID_CAP);
     const int MR = (P.S + 255) / 256;
     if (P.label_width > 256 * MR) return hipErrorInvalidValue;
 #define SDL_ROWS(MM)                                                                                                 \
