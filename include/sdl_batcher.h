@@ -166,6 +166,27 @@ int sdl_process_device_labels(sdl_batcher *h, const uint8_t *d_text, uint64_t te
                               const uint64_t *d_label_offsets, uint64_t first_record, void *stream,
                               sdl_device_rows *out);
 
+/* ---- Provider step: the JsonText filter on the device ----------------------
+ * SourceFilter::JsonText over inflated JSON lines (gzip_file_provider.rs:30-50
+ * -> provider_util.rs:60-64: serde_json::from_str(line).unwrap(),
+ * v["text"].as_str()): every '\n'-separated line whose value is an object with
+ * a string member "text" (the last one if repeated) becomes one record, that
+ * string unescaped to UTF-8, in a device text arena ready for
+ * sdl_process_device.  Lines the reference's unwrap() panics on are skipped and
+ * counted.  `d_jsonl` is device memory, 16-byte aligned and readable up to the
+ * next multiple of 16 bytes past `len` (< 4 GiB).  The arena and offsets are
+ * owned by the handle until the next call; the counts are copied to the host
+ * (the call synchronises `stream`). */
+typedef struct sdl_json_text {
+    uint8_t *d_text;       /* device, 16-byte aligned: records back to back, 16 zero bytes after */
+    uint64_t *d_offsets;   /* device [n_records + 1] */
+    uint64_t n_records;
+    uint64_t text_bytes;   /* = offsets[n_records] */
+    uint64_t n_lines;      /* lines seen */
+    uint64_t n_invalid;    /* lines the reference would panic on (skipped) */
+} sdl_json_text;
+int sdl_json_text_device(sdl_batcher *h, const uint8_t *d_jsonl, uint64_t len, void *stream, sdl_json_text *out);
+
 /* Copies `bytes` from device memory (e.g. sdl_device_rows planes) to host
  * memory with the handle's HIP runtime, ordered after the handle's work on
  * `stream` (NULL = the handle's stream); returns when the copy is complete. */

@@ -266,6 +266,11 @@ struct sdl_batcher {
     DevBuf<uint16_t> long_scratch;
     // unigram long items
     DevBuf<uint32_t> uni_counters, uni_pool, uni_err, span_err;
+    // JsonText provider step (sdl_json_text_device)
+    DevBuf<uint32_t> j_cnt, j_base, j_nl, j_len, j_rec, j_toff, j_ridx, j_inv;
+    DevBuf<uint2> j_span;
+    DevBuf<uint8_t> j_text;
+    DevBuf<uint64_t> j_off;
     DevBuf<uint4> uni_items, uni_huge;
     DevBuf<uint8_t> uni_scratch;
     DevBuf<uint8_t> h2d_text;
@@ -914,6 +919,73 @@ int sdl_process_device_labels(sdl_batcher *h, const uint8_t *d_text, uint64_t te
         out->d_tokens = h->chunk_off.p + (text_len + CHUNK - 1) / CHUNK;
         out->rows_capacity = (uint64_t)h->last_rows_cap;
         out->label_width = h->P.label_width;
+        return SDL_OK;
+    } catch (HipError &e) {
+        return fail(SDL_ERR_HIP, e.what());
+    } catch (std::exception &e) {
+        return fail(SDL_ERR_ARG, e.what());
+    }
+}
+
+int sdl_json_text_device(sdl_batcher *h, const uint8_t *d_jsonl, uint64_t len, void *stream, sdl_json_text *out) {
+    if (!h || !out || (!d_jsonl && len)) return fail(SDL_ERR_ARG, "null argument");
+    if (len >= (1ull << 32)) return fail(SDL_ERR_CAPACITY, "JSON buffer must be < 4 GiB per call");
+    if (((uintptr_t)d_jsonl & 15u) != 0) return fail(SDL_ERR_ARG, "d_jsonl must be 16-byte aligned");
+    try {
+        hipStream_t st = stream ? (hipStream_t)stream : h->stream;
+        const int64_t N = (int64_t)len, nb = (N + CHUNK - 1) / CHUNK;
+        h->j_cnt.ensure((size_t)nb + 1);
+        h->j_base.ensure((size_t)nb + 1);
+        h->scan_tmp.ensure((size_t)scan_tmp_words(std::max<int64_t>(nb, 1)) + 1);
+        uint32_t n_nl = 0;
+        if (nb) {
+            HIP_TRY(launch_json_nl_count(d_jsonl, N, h->j_cnt.p, h->j_base.p, h->scan_tmp.p, st));
+            HIP_TRY(hipMemcpyAsync(&n_nl, h->j_base.p + nb, 4, hipMemcpyDeviceToHost, st));
+            HIP_TRY(hipStreamSynchronize(st));
+        }
+        h->j_nl.ensure((size_t)n_nl + 1);
+        if (nb) HIP_TRY(launch_json_nl_write(d_jsonl, N, h->j_base.p, h->j_nl.p, st));
+        uint32_t last_nl = 0;
+        if (n_nl) {
+            HIP_TRY(hipMemcpyAsync(&last_nl, h->j_nl.p + n_nl - 1, 4, hipMemcpyDeviceToHost, st));
+            HIP_TRY(hipStreamSynchronize(st));
+        }
+        // tokio lines(): a last line without '\n' counts, an empty tail does not
+        const int64_t tail0 = n_nl ? (int64_t)last_nl + 1 : 0;
+        const int64_t n_lines = (int64_t)n_nl + (N > tail0 ? 1 : 0);
+        const size_t L1 = (size_t)n_lines + 1;
+        h->j_len.ensure(L1);
+        h->j_rec.ensure(L1);
+        h->j_toff.ensure(L1);
+        h->j_ridx.ensure(L1);
+        h->j_span.ensure(L1);
+        h->j_off.ensure(L1);
+        h->j_inv.ensure(1);
+        h->j_text.ensure((size_t)N + 32);
+        h->scan_tmp.ensure((size_t)scan_tmp_words(std::max<int64_t>(std::max<int64_t>(nb, n_lines), 1)) + 1);
+        HIP_TRY(hipMemsetAsync(h->j_inv.p, 0, 4, st));
+        HIP_TRY(hipMemsetAsync(h->j_off.p, 0, 8, st));
+        HIP_TRY(launch_json_parse(d_jsonl, N, h->j_nl.p, n_nl, n_lines, h->j_len.p, h->j_rec.p, h->j_span.p,
+                                  h->j_inv.p, st));
+        uint32_t counts[3] = {0, 0, 0};  // records, text bytes, invalid lines
+        if (n_lines) {
+            HIP_TRY(launch_exclusive_scan(h->j_len.p, h->j_toff.p, n_lines, h->scan_tmp.p, st));
+            HIP_TRY(launch_exclusive_scan(h->j_rec.p, h->j_ridx.p, n_lines, h->scan_tmp.p, st));
+            HIP_TRY(launch_json_write(d_jsonl, n_lines, h->j_rec.p, h->j_span.p, h->j_toff.p, h->j_ridx.p, h->j_text.p,
+                                      h->j_off.p, st));
+            HIP_TRY(hipMemcpyAsync(&counts[0], h->j_ridx.p + n_lines, 4, hipMemcpyDeviceToHost, st));
+            HIP_TRY(hipMemcpyAsync(&counts[1], h->j_toff.p + n_lines, 4, hipMemcpyDeviceToHost, st));
+        }
+        HIP_TRY(hipMemcpyAsync(&counts[2], h->j_inv.p, 4, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        HIP_TRY(hipMemsetAsync(h->j_text.p + counts[1], 0, 16, st));  // zero tail for 16-B readers
+        std::memset(out, 0, sizeof(*out));
+        out->d_text = h->j_text.p;
+        out->d_offsets = h->j_off.p;
+        out->n_records = counts[0];
+        out->text_bytes = counts[1];
+        out->n_lines = (uint64_t)n_lines;
+        out->n_invalid = counts[2];
         return SDL_OK;
     } catch (HipError &e) {
         return fail(SDL_ERR_HIP, e.what());

@@ -121,6 +121,15 @@ class DeviceBatcher:
             ctypes.c_void_p(stream or None), ctypes.byref(out)))
         return DeviceResult(self._h, out, n_records, self.cfg.sequence_length)
 
+    def json_text(self, jsonl_ptr, jsonl_len, stream=0):
+        """The provider's JsonText filter on the device (sdl_json_text_device):
+        a 16-B aligned device buffer of JSON lines -> the `text` records as a
+        device arena + offsets owned by this handle (native.JsonText)."""
+        out = native.JsonText()
+        native.check(native.load().sdl_json_text_device(self._h, ctypes.c_void_p(jsonl_ptr), jsonl_len,
+                                                        ctypes.c_void_p(stream or None), ctypes.byref(out)))
+        return out
+
     def process_tensors(self, text, offsets, first_record=0, stream=None):
         """text: uint8 cuda tensor; offsets: int64 cuda tensor of n_records+1 entries."""
         s = stream.cuda_stream if stream is not None else 0

@@ -20,7 +20,7 @@ SDL_TASK_MLM, SDL_TASK_CLM, SDL_TASK_SPAN, SDL_TASK_MULTI_LABEL = 0, 1, 2, 3
 EXPORTS = [
     "sdl_config_default", "sdl_batcher_create", "sdl_batcher_destroy", "sdl_batcher_push",
     "sdl_batcher_push_many", "sdl_batcher_next", "sdl_batcher_flush", "sdl_batch_release",
-    "sdl_process_device", "sdl_process_device_labels", "sdl_device_to_host", "sdl_set_profiling", "sdl_stage_times",
+    "sdl_process_device", "sdl_process_device_labels", "sdl_json_text_device", "sdl_device_to_host", "sdl_set_profiling", "sdl_stage_times",
     "sdl_tokenizer_info_get", "sdl_last_error", "sdl_abi_version",
 ]
 
@@ -59,6 +59,13 @@ class DeviceRows(ctypes.Structure):
         ("d_record_rows", ctypes.c_void_p), ("d_tokens", ctypes.c_void_p),
         ("rows_capacity", ctypes.c_uint64), ("label_width", ctypes.c_int32),
         ("d_label_errors", ctypes.c_void_p), ("d_tokenize_errors", ctypes.c_void_p),
+    ]
+
+
+class JsonText(ctypes.Structure):
+    _fields_ = [
+        ("d_text", ctypes.c_void_p), ("d_offsets", ctypes.c_void_p), ("n_records", ctypes.c_uint64),
+        ("text_bytes", ctypes.c_uint64), ("n_lines", ctypes.c_uint64), ("n_invalid", ctypes.c_uint64),
     ]
 
 
@@ -103,6 +110,7 @@ def load(path=LIB_PATH):
     L.sdl_process_device.argtypes = [vp, vp, u64, vp, u64, u64, vp, ctypes.POINTER(DeviceRows)]
     L.sdl_process_device_labels.argtypes = [vp, vp, u64, vp, u64, vp, vp, u64, vp, ctypes.POINTER(DeviceRows)]
     L.sdl_device_to_host.argtypes = [vp, vp, vp, sz, vp]
+    L.sdl_json_text_device.argtypes = [vp, vp, u64, vp, ctypes.POINTER(JsonText)]
     L.sdl_set_profiling.argtypes = [vp, i64]
     L.sdl_stage_times.argtypes = [vp, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_float), i64]
     L.sdl_last_error.restype = ctypes.c_char_p
