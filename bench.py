@@ -216,6 +216,8 @@ def main():
     ap.add_argument("--arena-mib", type=int, default=256)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--e2e", action="store_true", help="also time the host record path (H2D + kernels + D2H)")
+    ap.add_argument("--json", action="store_true",
+                    help="also time the provider's JsonText filter on the device (JSON lines -> text arena)")
     args = ap.parse_args()
     task = TASKS[args.task]
     S, B = task["S"], task["B"]
@@ -328,6 +330,8 @@ def main():
     log(f"stages {stage_ms}")
     if args.e2e and rank == 0:
         line["end_to_end"] = end_to_end(args.task, records, order)
+    if args.json and rank == 0:
+        line["provider_json"] = provider_json(db, records, order, dev, args.steps, args.warmup, step_ms)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("cpu baseline ...")
         line["cpu_baseline"] = cpu_baseline(args.task, records, order)
@@ -338,6 +342,33 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def provider_json(db, records, order, dev, steps, warmup, step_ms):
+    """SourceFilter::JsonText on the device (sdl_json_text_device): this rank's
+    record stream as JSON lines ({"id", "title", "text"}, json.dumps) already in
+    HBM -> the text arena + offsets the Batcher consumes.  Reports JSON MB/s and
+    the JSON-lines -> batches rate with the step time measured above."""
+    import torch
+    lines = [json.dumps({"id": i, "title": f"t{i}", "text": records[k]}).encode("utf-8") for i, k in enumerate(order)]
+    buf = b"\n".join(lines) + b"\n"
+    a = np.zeros(len(buf) + 32, np.uint8)
+    a[:len(buf)] = np.frombuffer(buf, np.uint8)
+    d = torch.from_numpy(a).to(dev)
+    for _ in range(warmup):
+        out = db.json_text(d.data_ptr(), len(buf))
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        out = db.json_text(d.data_ptr(), len(buf))
+    torch.cuda.synchronize(dev)
+    ms = (time.perf_counter() - t0) / steps * 1e3
+    text = sum(len(records[k].encode("utf-8")) for k in order)
+    return {"json_MBps": round(len(buf) / ms / 1e3, 2), "ms": round(ms, 4), "json_bytes": len(buf),
+            "records": int(out.n_records), "text_bytes": int(out.text_bytes), "text_bytes_expected": text,
+            "invalid_lines": int(out.n_invalid),
+            "json_to_batches_MBps": round(len(buf) / (ms + step_ms) / 1e3, 2),
+            "note": "host-timed (the call synchronises twice to size its outputs); JSON bytes / time"}
 
 
 def end_to_end(task, records, order, nbytes=64 << 20, reps=2):
