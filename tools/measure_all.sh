@@ -25,6 +25,7 @@ if [[ $STEPS == *tasks* ]]; then
     step bench_$t 600 python bench.py --task $t > $O/bench_$t.json 2> $O/bench_$t.err
   done
 fi
+[[ $STEPS == *json* ]] && step bench_json 300 python bench.py --steps 5 --warmup 2 --arena-mib 64 --no-cpu-baseline --json > $O/bench_json.json 2> $O/bench_json.err
 if [[ $STEPS == *e2e* ]]; then
   for t in mlm span clm multi-label; do
     step e2e_$t 300 python bench.py --task $t --steps 3 --warmup 1 --arena-mib 64 --no-cpu-baseline --e2e > $O/e2e_$t.json 2> $O/e2e_$t.err
