@@ -218,6 +218,8 @@ def main():
     ap.add_argument("--e2e", action="store_true", help="also time the host record path (H2D + kernels + D2H)")
     ap.add_argument("--json", action="store_true",
                     help="also time the provider's JsonText filter on the device (JSON lines -> text arena)")
+    ap.add_argument("--frames", action="store_true",
+                    help="also time the Transport step on the device: every batch -> its serde_pickle frame")
     args = ap.parse_args()
     task = TASKS[args.task]
     S, B = task["S"], task["B"]
@@ -332,6 +334,9 @@ def main():
         line["end_to_end"] = end_to_end(args.task, records, order)
     if args.json and rank == 0:
         line["provider_json"] = provider_json(db, records, order, dev, args.steps, args.warmup, step_ms)
+    if args.frames and rank == 0:
+        line["transport_frames"] = transport_frames(db, res, args.task, stream, dev, args.steps, args.warmup,
+                                                    not args.no_cpu_baseline)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("cpu baseline ...")
         line["cpu_baseline"] = cpu_baseline(args.task, records, order)
@@ -342,6 +347,60 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def transport_frames(db, res, task_name, stream, dev, steps, warmup, with_cpu):
+    """Transport step on the device (sdl_pickle_frames_device): every batch of
+    this step (full batches + the flushed partial one) -> the serde_pickle
+    frame the reference's Transport sends (zmq_transmit.rs:71).  Timed with HIP
+    events on the stream the kernels run on.  Algorithmic bytes per launch:
+    the int32/f32 plane elements read (4 B) + the frame bytes written."""
+    import torch
+    rows = res.rows()
+    fr = None
+    for _ in range(warmup):
+        fr = db.pickle_frames(res, rows, True, stream.cuda_stream)
+    torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(steps):
+        fr = db.pickle_frames(res, rows, True, stream.cuda_stream)
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    ms = e0.elapsed_time(e1) / steps
+    t = TASKS[task_name]
+    B, S = t["B"], t["S"]
+    nb = len(fr)
+    LW = {"span": S // 4, "multi-label": 9}.get(task_name, S)
+    n_planes = {"mlm": 3, "multi-label": 3}.get(task_name, 2)
+    rows_full = nb * B
+    lab_rows = rows if task_name in ("mlm", "multi-label") else rows_full
+    elems = n_planes * rows_full * S + lab_rows * LW
+    alg = 4 * elems + int(fr.f.total_bytes)
+    achieved = alg / (ms * 1e-3) / 1e9
+    out = {"frames": nb, "frame_bytes": int(fr.f.frame_bytes), "total_bytes": int(fr.f.total_bytes),
+           "ms": round(ms, 4), "frame_MBps": round(fr.f.total_bytes / ms / 1e3, 2),
+           "roofline": {"bound": "hbm", "kernel": "k_frame_rows", "achieved": round(achieved, 2),
+                        "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 5),
+                        "algorithmic_bytes_per_launch": alg, "avg_launch_ms": round(ms, 4)}}
+    if with_cpu:
+        # the C restatement of serde_pickle (single thread) on a bounded sample of the same batches
+        sys.path.insert(0, os.path.join(REPO, "tests"))
+        import oracle_lib
+        k = min(nb, 24 if S * B >= 65536 else 96)
+        ids, am, tt, lab = res.planes(k * B)
+        t0, done, nfr = time.perf_counter(), 0, 0
+        while time.perf_counter() - t0 < 5.0:
+            for b in range(k):
+                sl = slice(b * B, (b + 1) * B)
+                done += len(oracle_lib.pickle_dataset(task_name, B, S, LW, B, ids[sl], am[sl],
+                                                      None if tt is None else tt[sl], lab[sl]))
+                nfr += 1
+        dt = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": round(done / dt / 1e6, 2), "unit": "MB/s of frames", "cores": 1,
+                               "kind": "port", "sample": f"{nfr} frames ({k} distinct batches of this step), "
+                                                         f"oracle/orc_pickle.c single-threaded, {dt:.1f} s"}
+    return out
 
 
 def provider_json(db, records, order, dev, steps, warmup, step_ms):

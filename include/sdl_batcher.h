@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define SDL_ABI_VERSION 3
+#define SDL_ABI_VERSION 4
 
 enum {
     SDL_OK = 0,
@@ -186,6 +186,29 @@ typedef struct sdl_json_text {
     uint64_t n_invalid;    /* lines the reference would panic on (skipped) */
 } sdl_json_text;
 int sdl_json_text_device(sdl_batcher *h, const uint8_t *d_jsonl, uint64_t len, void *stream, sdl_json_text *out);
+
+/* ---- Transport step: batches as serde_pickle frames on the device ----------
+ * Replaces serde_pickle::to_vec(&dataset, Default::default()) of each finished
+ * DataSet (transport/zmq_transmit.rs:71, serde-pickle 1.1.1) that the Python
+ * consumer reads with pickle.loads (python/external_dataset.py:52): the planes
+ * of `rows` (from the last sdl_process_device[_labels] call of `h`) become one
+ * frame per batch -- PROTO 3, the DataSet's fields in Serialize order
+ * (bert_data.rs:106-145, gpt_data.rs:53-62, t5_data.rs:235-249), rows as lists
+ * of BININT / BINFLOAT, STOP -- back to back in device memory.  Batches are the
+ * n_rows / B full ones plus, when flush_partial and n_rows % B != 0, the
+ * partial batch get_working_batch() would flush (its BertData `labels` list
+ * holds the filled rows only).  `n_rows` is the value of *rows->d_rows (or
+ * fewer rows).  The frames are owned by the handle until the next call; no
+ * host synchronisation. */
+typedef struct sdl_frames {
+    uint8_t *d_frames;         /* device: frame f at f * frame_bytes */
+    uint64_t n_frames;
+    uint64_t frame_bytes;      /* bytes of every frame but the last */
+    uint64_t last_frame_bytes; /* bytes of the last frame */
+    uint64_t total_bytes;
+} sdl_frames;
+int sdl_pickle_frames_device(sdl_batcher *h, const sdl_device_rows *rows, uint64_t n_rows, int flush_partial,
+                             void *stream, sdl_frames *out);
 
 /* Copies `bytes` from device memory (e.g. sdl_device_rows planes) to host
  * memory with the handle's HIP runtime, ordered after the handle's work on

@@ -116,6 +116,15 @@ void orc_batcher_set_next_record(orc_batcher *b, uint64_t record);
 /* span: label / sentinel writes past their bounds (the reference panics) */
 uint64_t orc_batcher_span_errors(const orc_batcher *b);
 
+/* Transport frame of one DataSet (orc_pickle.c): serde_pickle::to_vec bytes
+ * (zmq_transmit.rs:71).  task: 0 mlm, 1 clm, 2 span, 3 multi-label.  Planes are
+ * row-major [batch_size, seq_len] (labels [.., label_width]); `rows` = filled
+ * rows (the BertData label list length).  Returns the frame size; writes it
+ * when cap suffices. */
+size_t orc_pickle_dataset(int task, int batch_size, int seq_len, int label_width, int rows, const int32_t *input_ids,
+                          const int32_t *attention_mask, const int32_t *token_type_ids, const int32_t *labels,
+                          const float *labels_f32, uint8_t *out, size_t cap);
+
 #ifdef __cplusplus
 }
 #endif

@@ -125,4 +125,29 @@ hipError_t launch_rows_span(const RowParams &P, const uint32_t *tok, const uint3
                             const uint32_t *row_off, const uint32_t *row_rec, const uint32_t *d_rows, int64_t rows_cap,
                             RowOut out, uint32_t *err, hipStream_t st);
 
+// transport_frame.hip: the Transport's serde_pickle frames of finished batches
+// (zmq_transmit.rs:71) written straight from the device row planes.
+struct FramePlane {
+    const void *src;     // device plane [rows, width] (int32, or f32 when is_f32)
+    uint32_t width;      // elements per row
+    uint32_t is_f32;
+    uint32_t rows_full;  // rows of this plane in a full frame
+    uint32_t rows_last;  // rows in the last frame
+    uint32_t row_bytes;  // encoded bytes per row list
+    uint32_t key_len;    // bytes of the key segment: 'X' + u32 len + name + "]("
+    uint64_t off_full;   // frame offset of row 0 (just past the key segment), full frames
+    uint64_t off_last;   // the same in the last frame
+    uint8_t key[24];
+};
+struct FrameParams {
+    FramePlane plane[4];
+    uint8_t *out;
+    uint64_t frame_bytes;       // every frame but the last
+    uint64_t last_frame_bytes;
+    uint64_t n_frames;
+    uint32_t B;                 // rows per batch in the source planes
+    int n_planes;
+};
+hipError_t launch_frames(const FrameParams &fp, hipStream_t st);
+
 }  // namespace sdl

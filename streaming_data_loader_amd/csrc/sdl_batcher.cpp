@@ -271,6 +271,8 @@ struct sdl_batcher {
     DevBuf<uint2> j_span;
     DevBuf<uint8_t> j_text;
     DevBuf<uint64_t> j_off;
+    // Transport frames (sdl_pickle_frames_device)
+    DevBuf<uint8_t> f_out;
     DevBuf<uint4> uni_items, uni_huge;
     DevBuf<uint8_t> uni_scratch;
     DevBuf<uint8_t> h2d_text;
@@ -986,6 +988,98 @@ int sdl_json_text_device(sdl_batcher *h, const uint8_t *d_jsonl, uint64_t len, v
         out->text_bytes = counts[1];
         out->n_lines = (uint64_t)n_lines;
         out->n_invalid = counts[2];
+        return SDL_OK;
+    } catch (HipError &e) {
+        return fail(SDL_ERR_HIP, e.what());
+    } catch (std::exception &e) {
+        return fail(SDL_ERR_ARG, e.what());
+    }
+}
+
+namespace {
+
+struct FramePlaneDesc {
+    const char *name;
+    const void *src;
+    uint32_t width;
+    bool f32;
+    bool filled_rows_only;  // BertData.label: one entry per filled row
+};
+
+// list of `n` items of `item` bytes each: "](" items ["e(" per 1000] "e", or "]" when empty
+uint64_t list_bytes(uint64_t n, uint64_t item) { return n ? 3 + n * item + 2 * (n / 1000) : 1; }
+
+// lays out one frame (the plane_rows rows of each plane); returns its size
+uint64_t frame_layout(FrameParams &fp, const FramePlaneDesc *d, int np, const uint32_t *plane_rows, bool last) {
+    uint64_t pos = 4;  // PROTO 3, EMPTY_DICT, MARK
+    for (int p = 0; p < np; ++p) {
+        FramePlane &P = fp.plane[p];
+        const uint32_t n = (uint32_t)std::strlen(d[p].name);
+        P.key_len = 5 + n + 2;
+        P.key[0] = 'X';
+        for (int i = 0; i < 4; ++i) P.key[1 + i] = (uint8_t)(n >> (8 * i));
+        std::memcpy(P.key + 5, d[p].name, n);
+        P.key[5 + n] = ']';
+        P.key[6 + n] = '(';
+        (last ? P.off_last : P.off_full) = pos + P.key_len;
+        pos += 5 + n + list_bytes(plane_rows[p], P.row_bytes);
+    }
+    return pos + 2;  // SETITEMS, STOP
+}
+
+}  // namespace
+
+int sdl_pickle_frames_device(sdl_batcher *h, const sdl_device_rows *rows, uint64_t n_rows, int flush_partial,
+                             void *stream, sdl_frames *out) {
+    if (!h || !rows || !out) return fail(SDL_ERR_ARG, "null argument");
+    const int task = h->cfg.task;
+    const uint64_t B = (uint64_t)h->cfg.batch_size, S = (uint64_t)h->cfg.sequence_length;
+    const uint64_t LW = (uint64_t)rows->label_width;
+    if (B == 0 || S == 0) return fail(SDL_ERR_ARG, "batch_size and sequence_length must be > 0");
+    const uint64_t rem = n_rows % B, n_frames = n_rows / B + (flush_partial && rem ? 1 : 0);
+    if (n_frames * B > rows->rows_capacity)
+        return fail(SDL_ERR_ARG, "n_rows exceeds the rows the device planes hold");
+    const bool bert = task == SDL_TASK_MLM || task == SDL_TASK_MULTI_LABEL;
+    FramePlaneDesc d[4];
+    int np = 0;
+    d[np++] = {"input_ids", rows->input_ids, (uint32_t)S, false, false};
+    d[np++] = {"attention_mask", rows->attention_mask, (uint32_t)S, false, false};
+    if (bert) d[np++] = {"token_type_ids", rows->token_type_ids, (uint32_t)S, false, false};
+    if (task == SDL_TASK_MULTI_LABEL)
+        d[np++] = {"labels", rows->labels_f32, (uint32_t)LW, true, true};
+    else
+        d[np++] = {"labels", rows->labels, (uint32_t)LW, false, bert};
+    for (int p = 0; p < np; ++p)
+        if (!d[p].src && n_frames) return fail(SDL_ERR_ARG, std::string("device plane missing: ") + d[p].name);
+    try {
+        FrameParams fp{};
+        fp.n_planes = np;
+        fp.B = (uint32_t)B;
+        fp.n_frames = n_frames;
+        uint32_t full_rows[4], last_rows[4];
+        const bool partial = n_frames && n_frames * B > n_rows;
+        for (int p = 0; p < np; ++p) {
+            FramePlane &P = fp.plane[p];
+            P.src = d[p].src;
+            P.width = d[p].width;
+            P.is_f32 = d[p].f32;
+            P.row_bytes = (uint32_t)list_bytes(P.width, d[p].f32 ? 9 : 5);
+            full_rows[p] = P.rows_full = (uint32_t)B;
+            last_rows[p] = P.rows_last = (uint32_t)(partial && d[p].filled_rows_only ? rem : B);
+        }
+        fp.frame_bytes = frame_layout(fp, d, np, full_rows, false);
+        fp.last_frame_bytes = frame_layout(fp, d, np, last_rows, true);
+        const uint64_t total = n_frames ? (n_frames - 1) * fp.frame_bytes + fp.last_frame_bytes : 0;
+        h->f_out.ensure((size_t)total + 16);
+        fp.out = h->f_out.p;
+        hipStream_t st = stream ? (hipStream_t)stream : h->stream;
+        HIP_TRY(launch_frames(fp, st));
+        std::memset(out, 0, sizeof(*out));
+        out->d_frames = h->f_out.p;
+        out->n_frames = n_frames;
+        out->frame_bytes = fp.frame_bytes;
+        out->last_frame_bytes = n_frames ? fp.last_frame_bytes : 0;
+        out->total_bytes = total;
         return SDL_OK;
     } catch (HipError &e) {
         return fail(SDL_ERR_HIP, e.what());

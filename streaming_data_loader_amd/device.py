@@ -66,6 +66,30 @@ class DeviceResult:
         return (get(self.r.input_ids, S), get(self.r.attention_mask, S), get(self.r.token_type_ids, S), lab)
 
 
+class DeviceFrames:
+    """Transport frames on the device (sdl_pickle_frames_device): frame f is
+    d_frames[f*frame_bytes : f*frame_bytes + size(f)], the bytes
+    serde_pickle::to_vec(&DataSet) gives the socket (zmq_transmit.rs:71)."""
+
+    def __init__(self, handle, fr):
+        self.h = handle
+        self.f = fr
+
+    def __len__(self):
+        return int(self.f.n_frames)
+
+    def to_host(self):
+        """All frames as one uint8 array (D2H copy)."""
+        a = np.zeros(int(self.f.total_bytes), np.uint8)
+        return native.d2h(self.h, a, self.f.d_frames, a.nbytes)
+
+    def frames(self):
+        """List of bytes objects, one per batch."""
+        a = self.to_host().tobytes()
+        n, F = len(self), int(self.f.frame_bytes)
+        return [a[i * F:(i * F + (F if i < n - 1 else int(self.f.last_frame_bytes)))] for i in range(n)]
+
+
 class DeviceBatcher:
     """Owns one sdl_batcher handle used through sdl_process_device."""
 
@@ -129,6 +153,16 @@ class DeviceBatcher:
         native.check(native.load().sdl_json_text_device(self._h, ctypes.c_void_p(jsonl_ptr), jsonl_len,
                                                         ctypes.c_void_p(stream or None), ctypes.byref(out)))
         return out
+
+    def pickle_frames(self, result, n_rows=None, flush_partial=True, stream=0):
+        """Transport step on the device: the batches of `result` (the last
+        process*() call) as serde_pickle frames (DeviceFrames)."""
+        n = result.rows() if n_rows is None else n_rows
+        out = native.Frames()
+        native.check(native.load().sdl_pickle_frames_device(self._h, ctypes.byref(result.r), n,
+                                                            1 if flush_partial else 0,
+                                                            ctypes.c_void_p(stream or None), ctypes.byref(out)))
+        return DeviceFrames(self._h, out)
 
     def process_tensors(self, text, offsets, first_record=0, stream=None):
         """text: uint8 cuda tensor; offsets: int64 cuda tensor of n_records+1 entries."""

@@ -20,7 +20,7 @@ SDL_TASK_MLM, SDL_TASK_CLM, SDL_TASK_SPAN, SDL_TASK_MULTI_LABEL = 0, 1, 2, 3
 EXPORTS = [
     "sdl_config_default", "sdl_batcher_create", "sdl_batcher_destroy", "sdl_batcher_push",
     "sdl_batcher_push_many", "sdl_batcher_next", "sdl_batcher_flush", "sdl_batch_release",
-    "sdl_process_device", "sdl_process_device_labels", "sdl_json_text_device", "sdl_device_to_host", "sdl_set_profiling", "sdl_stage_times",
+    "sdl_process_device", "sdl_process_device_labels", "sdl_json_text_device", "sdl_pickle_frames_device", "sdl_device_to_host", "sdl_set_profiling", "sdl_stage_times",
     "sdl_tokenizer_info_get", "sdl_last_error", "sdl_abi_version",
 ]
 
@@ -69,6 +69,13 @@ class JsonText(ctypes.Structure):
     ]
 
 
+class Frames(ctypes.Structure):
+    _fields_ = [
+        ("d_frames", ctypes.c_void_p), ("n_frames", ctypes.c_uint64), ("frame_bytes", ctypes.c_uint64),
+        ("last_frame_bytes", ctypes.c_uint64), ("total_bytes", ctypes.c_uint64),
+    ]
+
+
 class TokenizerInfo(ctypes.Structure):
     _fields_ = [
         ("kind", ctypes.c_int32), ("vocab_size", ctypes.c_int32), ("n_added", ctypes.c_int32),
@@ -111,6 +118,7 @@ def load(path=LIB_PATH):
     L.sdl_process_device_labels.argtypes = [vp, vp, u64, vp, u64, vp, vp, u64, vp, ctypes.POINTER(DeviceRows)]
     L.sdl_device_to_host.argtypes = [vp, vp, vp, sz, vp]
     L.sdl_json_text_device.argtypes = [vp, vp, u64, vp, ctypes.POINTER(JsonText)]
+    L.sdl_pickle_frames_device.argtypes = [vp, ctypes.POINTER(DeviceRows), u64, i64, vp, ctypes.POINTER(Frames)]
     L.sdl_set_profiling.argtypes = [vp, i64]
     L.sdl_stage_times.argtypes = [vp, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_float), i64]
     L.sdl_last_error.restype = ctypes.c_char_p
@@ -119,7 +127,8 @@ def load(path=LIB_PATH):
     L.sdl_tokenizer_info_get.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(TokenizerInfo)]
     L.sdl_tokenizer_info_get.restype = i64
     for name in ("sdl_batcher_create", "sdl_batcher_push", "sdl_batcher_push_many", "sdl_batcher_next",
-                 "sdl_batcher_flush", "sdl_process_device", "sdl_process_device_labels", "sdl_device_to_host", "sdl_set_profiling",
+                 "sdl_batcher_flush", "sdl_process_device", "sdl_process_device_labels", "sdl_json_text_device",
+                 "sdl_pickle_frames_device", "sdl_device_to_host", "sdl_set_profiling",
                  "sdl_stage_times"):
         getattr(L, name).restype = i64
     _lib = L

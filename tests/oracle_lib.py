@@ -80,6 +80,8 @@ def lib():
         L.orc_span_table.argtypes = [ctypes.c_double, ctypes.c_int, vp, vp, vp, ctypes.c_int]
         L.orc_span_table.restype = None
         L.orc_batcher_span_errors.argtypes = [vp]
+        L.orc_pickle_dataset.restype = ctypes.c_size_t
+        L.orc_pickle_dataset.argtypes = [ctypes.c_int] * 5 + [vp] * 5 + [vp, ctypes.c_size_t]
         L.orc_batcher_span_errors.restype = ctypes.c_uint64
         _lib = L
     return _lib
@@ -307,3 +309,21 @@ def oracle_rows(tok, texts, S, mask_length, mask_id=103, seed=0, B=64, first_rec
     if not planes:
         return np.zeros((4, 0, S), np.int32)
     return np.concatenate(planes, axis=1)
+
+
+TASK_IDS = {"mlm": 0, "clm": 1, "span": 2, "multi-label": 3}
+
+
+def pickle_dataset(task, B, S, LW, rows, input_ids, attention_mask, token_type_ids, labels):
+    """serde_pickle::to_vec(&DataSet) bytes (oracle/orc_pickle.c).  Planes are
+    numpy [B, S] int32 (labels [B, LW] int32, or float32 for multi-label)."""
+    L = lib()
+    arrs = [np.ascontiguousarray(a) if a is not None else None
+            for a in (input_ids, attention_mask, token_type_ids, labels)]
+    ptr = [a.ctypes.data if a is not None else None for a in arrs]
+    f32 = task == "multi-label"
+    args = [TASK_IDS[task], B, S, LW, rows, ptr[0], ptr[1], ptr[2], None if f32 else ptr[3], ptr[3] if f32 else None]
+    n = L.orc_pickle_dataset(*args, None, 0)
+    out = np.zeros(n, np.uint8)
+    assert L.orc_pickle_dataset(*args, out.ctypes.data, n) == n
+    return out.tobytes()
