@@ -48,6 +48,8 @@ TASKS = {
             "workload": "clm gpt2 byte-BPE seq_len=1024 batch=128 (BASELINE configs[3])"},
     "multi-label": {"S": 128, "B": 2048, "tok": "bert", "kernel": "k_wordpiece_chunks", "planes": 3,
                     "workload": "multi-label seq_len=128 batch=2048 (BASELINE configs[4], B from multi_cases.rs:22)"},
+    "single-class": {"S": 128, "B": 2048, "tok": "bert", "kernel": "k_wordpiece_chunks", "planes": 3.0078125,
+                     "workload": "single-class seq_len=128 batch=2048 (single_cases.rs Imdb; SURVEY 8(f) row 4)"},
 }
 
 _T0 = time.perf_counter()
@@ -99,7 +101,7 @@ def _oracle_batcher(task, oracle_lib):
     else:
         enc = oracle_lib.Encoder("bert", oracle_lib.Tok())
     kind = {"mlm": oracle_lib.MLM, "clm": oracle_lib.CLM, "span": oracle_lib.SPAN,
-            "multi-label": oracle_lib.MULTI_LABEL}[task]
+            "multi-label": oracle_lib.MULTI_LABEL, "single-class": oracle_lib.SINGLE_CLASS}[task]
     return lambda: oracle_lib.OracleBatcherEx(enc, kind, t["B"], t["S"], seed=1234)
 
 
@@ -135,6 +137,8 @@ def cpu_baseline(task, records, order, seconds=12.0, mt_seconds=6.0):
     if task == "multi-label":
         vals, offs = record_labels(len(blobs))
         labels = [vals[int(offs[i]):int(offs[i + 1])] for i in range(len(blobs))]
+    elif task == "single-class":
+        labels = [np.array([i & 1], np.uint32) for i in range(len(blobs))]
     done, n, dt = _oracle_stream(make(), blobs, order, labels, 0, seconds)
     try:
         ncpu = len(os.sched_getaffinity(0))
@@ -248,13 +252,20 @@ def main():
     offsets = torch.from_numpy(offs.astype(np.int64)).to(dev)
     stream = torch.cuda.Stream(device=dev)
     kind = {"mlm": native.SDL_TASK_MLM, "clm": native.SDL_TASK_CLM, "span": native.SDL_TASK_SPAN,
-            "multi-label": native.SDL_TASK_MULTI_LABEL}
+            "multi-label": native.SDL_TASK_MULTI_LABEL, "single-class": native.SDL_TASK_SINGLE_CLASS}
     tok_path = {"gpt2": native.GPT2_PROXY_TOKENIZER, "t5": native.T5_PROXY_TOKENIZER}.get(task["tok"],
                                                                                           native.BERT_PROXY_TOKENIZER)
     db = DeviceBatcher(task=kind[args.task], batch_size=B, sequence_length=S, seed=1234, device=local,
                        tokenizer=tok_path)
     first_record = rank * 10_000_000  # disjoint global record indices per shard
-    if args.task == "multi-label":
+    if args.task == "single-class":  # Label::Single: record i's label is i & 1 (imdb: 2 classes)
+        t_lab = torch.from_numpy((np.asarray(order, np.int64) & 1).astype(np.int32)).to(dev)
+        t_loff = torch.arange(R + 1, dtype=torch.int64, device=dev)
+
+        def step():
+            return db.process_labels(text.data_ptr(), N, offsets.data_ptr(), R, t_lab.data_ptr(), t_loff.data_ptr(),
+                                     first_record, stream.cuda_stream)
+    elif args.task == "multi-label":
         lv, lo = record_labels(len(records))
         per = [lv[int(lo[i]):int(lo[i + 1])] for i in range(len(records))]
         vals = np.concatenate([per[i] for i in order]).astype(np.int32)
@@ -371,10 +382,10 @@ def transport_frames(db, res, task_name, stream, dev, steps, warmup, with_cpu):
     t = TASKS[task_name]
     B, S = t["B"], t["S"]
     nb = len(fr)
-    LW = {"span": S // 4, "multi-label": 9}.get(task_name, S)
-    n_planes = {"mlm": 3, "multi-label": 3}.get(task_name, 2)
+    LW = {"span": S // 4, "multi-label": 9, "single-class": 1}.get(task_name, S)
+    n_planes = {"mlm": 3, "multi-label": 3, "single-class": 3}.get(task_name, 2)
     rows_full = nb * B
-    lab_rows = rows if task_name in ("mlm", "multi-label") else rows_full
+    lab_rows = rows if task_name in ("mlm", "multi-label", "single-class") else rows_full
     elems = n_planes * rows_full * S + lab_rows * LW
     alg = 4 * elems + int(fr.f.total_bytes)
     achieved = alg / (ms * 1e-3) / 1e9
@@ -445,7 +456,16 @@ def end_to_end(task, records, order, nbytes=64 << 20, reps=2):
         done += len(records[i].encode("utf-8"))
         if done >= nbytes:
             break
-    if task == "multi-label":
+    if task == "single-class":
+        import pyarrow as pa
+        table = pa.table({"text": pa.array(texts, pa.utf8()),
+                          "label": pa.array([i & 1 for i in order[:len(texts)]], pa.int64())})
+        batches = table.to_batches(max_chunksize=65536)
+        sb = Bt.SimpleBatcher(Bt.ModelType.Bert, Bt.SingleClass(), Bt.BatchConfig(t["B"], t["S"]),
+                              Bt.TokenizerConfig())
+        run = lambda: [ds for b in batches for ds in sb.push_arrow(b)]  # noqa: E731
+        path = "Arrow record batches (text, label) -> SimpleBatcher.push_arrow (column buffers, pinned H2D, kernels, D2H)"
+    elif task == "multi-label":
         import pyarrow as pa
         lv, lo = record_labels(len(records))
         labs = [lv[int(lo[i]):int(lo[i + 1])].astype(np.int64) for i in range(len(records))]

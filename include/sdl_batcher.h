@@ -50,7 +50,9 @@ enum {
     SDL_TASK_MLM = 0,        /* BertData, DataSetConfig::Mask   (models/bert_data.rs) */
     SDL_TASK_CLM = 1,        /* GptData,  DataSetConfig::Gpt    (models/gpt_data.rs) */
     SDL_TASK_SPAN = 2,       /* T5Data,   DataSetConfig::Span   (models/t5_data.rs) */
-    SDL_TASK_MULTI_LABEL = 3 /* BertData, DataSetConfig::MultiLabel via SimpleBatcher */
+    SDL_TASK_MULTI_LABEL = 3, /* BertData, DataSetConfig::MultiLabel via SimpleBatcher */
+    SDL_TASK_SINGLE_CLASS = 4 /* BertData, DataSetConfig::SingleClass via SimpleBatcher
+                                 (tasks/single_class/runner.rs:40-49): one Label::Single per record */
 };
 
 /* Mirrors TrainingConfig.batch + .dataset_config (rust/src/config.rs:64-72,
@@ -79,11 +81,12 @@ typedef struct sdl_batch {
     int32_t rows;            /* rows filled (BertData.index); the MLM `labels` list has this length */
     int32_t batch_size;
     int32_t sequence_length;
-    int32_t label_width;     /* S (mlm/clm), S/4 (span), number_labels (multi-label) */
+    int32_t label_width;     /* S (mlm/clm), S/4 (span), number_labels (multi-label), 1 (single-class) */
     const int32_t *input_ids;      /* [batch_size, sequence_length] */
     const int32_t *attention_mask; /* [batch_size, sequence_length] */
     const int32_t *token_type_ids; /* [batch_size, sequence_length] or NULL (clm/span) */
-    const int32_t *labels;         /* [batch_size, label_width] or NULL (multi-label) */
+    const int32_t *labels;         /* [batch_size, label_width] or NULL (multi-label); single-class:
+                                      [batch_size, 1], the BertData `label` list = the first `rows` */
     const float *labels_f32;       /* [batch_size, number_labels] (multi-label) or NULL */
     void *owner_;                  /* opaque, for sdl_batch_release */
 } sdl_batch;

@@ -141,19 +141,22 @@ static void q_push(orc_batcher *b, obatch *x) {
 
 orc_batcher *orc_batcher_create(const orc_encoder *e, const orc_cfg *c) {
     if (!e || !c || c->B <= 0 || c->S <= 0) return NULL;
-    if (c->task != ORC_MLM && c->task != ORC_CLM && c->task != ORC_MULTI_LABEL && c->task != ORC_SPAN) return NULL;
+    if (c->task != ORC_MLM && c->task != ORC_CLM && c->task != ORC_MULTI_LABEL && c->task != ORC_SPAN &&
+        c->task != ORC_SINGLE_CLASS)
+        return NULL;
     if (c->task == ORC_SPAN && c->S < 4) return NULL;
     if (c->task == ORC_MLM && (c->mask_length < 0 || c->mask_length > c->S)) return NULL;
     if (c->task == ORC_MULTI_LABEL && c->number_labels <= 0) return NULL;
     orc_batcher *b = (orc_batcher *)calloc(1, sizeof(orc_batcher));
     b->enc = *e;
     b->c = *c;
-    if (c->task == ORC_MULTI_LABEL) { /* SimpleBatcher: no chunking, no filter */
+    if (c->task == ORC_MULTI_LABEL || c->task == ORC_SINGLE_CLASS) { /* SimpleBatcher: no chunking, no filter */
         b->c.chunk = 0;
         b->c.min_ids = 0;
     }
     b->NL = c->task == ORC_MULTI_LABEL ? c->number_labels : 0;
-    b->LW = c->task == ORC_MULTI_LABEL ? 0 : c->task == ORC_SPAN ? c->S / 4 : c->S; /* t5_data.rs:44 */
+    b->LW = c->task == ORC_MULTI_LABEL ? 0 : c->task == ORC_SINGLE_CLASS ? 1 : c->task == ORC_SPAN ? c->S / 4 : c->S;
+    /* t5_data.rs:44 for span; SingleClass: one u32 per row */
     if (c->task == ORC_SPAN) {
         orc_span_table(c->avg_span_gap, 0, &b->gap_kmin, &b->gap_n, b->gap_thr, SPAN_TAB);
         orc_span_table(c->avg_span_size, 1, &b->size_kmin, &b->size_n, b->size_thr, SPAN_TAB);
@@ -202,11 +205,17 @@ static int put_data(orc_batcher *b, obatch *x, const uint32_t *ids, size_t n, ui
     for (size_t j = 0; j < l; ++j) in[j] = (int32_t)ids[j];
     switch (b->c.task) {
     case ORC_MLM:
+    case ORC_SINGLE_CLASS:
     case ORC_MULTI_LABEL: /* BertData::put_data (bert_data.rs:55-89) */
         if (n < S)
             for (size_t j = S - n; j < S; ++j) am[j] = 0; /* reversed-range quirk */
         if (b->c.task == ORC_MLM) {
             mask_row(b, in, x->lab + (size_t)x->index * S, rec, chunk);
+        } else if (b->c.task == ORC_SINGLE_CLASS) {
+            /* label.map(|s| self.label.push(s)) (bert_data.rs:79-81); SingleClassArrowGenerator
+             * always yields Some(Label::Single) (single_arrow.rs:16-26): exactly one label */
+            if (nl != 1) return -1;
+            x->lab[x->index] = (int32_t)labels[0];
         } else {
             float *f = x->f32 + (size_t)x->index * b->NL;
             for (size_t k = 0; k < nl; ++k) {
@@ -321,7 +330,7 @@ int orc_batcher_push_ex(orc_batcher *b, const uint8_t *s, size_t n, const uint32
 }
 
 int orc_batcher_flush_ex(orc_batcher *b, orc_out *out) {
-    if (b->c.task == ORC_MULTI_LABEL) { /* SimpleBatcher::get_working_batch: swap in a new one */
+    if (b->c.task == ORC_MULTI_LABEL || b->c.task == ORC_SINGLE_CLASS) { /* SimpleBatcher::get_working_batch */
         batch_out(b, q_pop(b), out);
         q_push(b, obatch_new(b));
         return 1;
@@ -388,8 +397,8 @@ void orc_cfg_default(orc_cfg *c, int task) {
     c->task = task;
     c->B = 4096;
     c->S = 128;
-    c->chunk = task == ORC_MULTI_LABEL ? 0 : 1;
-    c->min_ids = task == ORC_MULTI_LABEL ? 0 : 64;
+    c->chunk = task == ORC_MULTI_LABEL || task == ORC_SINGLE_CLASS ? 0 : 1;
+    c->min_ids = task == ORC_MULTI_LABEL || task == ORC_SINGLE_CLASS ? 0 : 64;
     c->mask_length = (int)((float)c->S * 0.15f);
     c->mask_id = 103;
     c->number_labels = 9;

@@ -19,8 +19,9 @@
  *   f32 (-> f64)   : BINFLOAT "G" + f64 big-endian
  * The field order and names are the reference's Serialize impls:
  *   BertData (models/bert_data.rs:106-145): input_ids, attention_mask, token_type_ids,
- *     labels (Mask: Vec<Vec<i32>>; MultiLabel: Vec<Vec<f32>>), labels having one entry
- *     per filled row (BertData.label is pushed per row, :50/:75);
+ *     labels (Mask: Vec<Vec<i32>>; MultiLabel: Vec<Vec<f32>>) or, for SingleClass,
+ *     label (Vec<u32>), having one entry per filled row (BertData.label is pushed per
+ *     row, :50/:75/:80);
  *   GptData (models/gpt_data.rs:53-62): input_ids, attention_mask, labels;
  *   T5Data  (models/t5_data.rs:235-249): input_ids, attention_mask, labels (S/4 wide).
  * Byte-exactness against the crate itself is unpinned (it cannot run here); the
@@ -117,7 +118,7 @@ size_t orc_pickle_dataset(int task, int batch_size, int seq_len, int label_width
                           const float *labels_f32, uint8_t *out, size_t cap) {
     pw w = {out, 0, out ? cap : 0};
     const size_t B = (size_t)batch_size, S = (size_t)seq_len, LW = (size_t)label_width;
-    const int bert = task == 0 || task == 3; /* SDL_TASK_MLM / SDL_TASK_MULTI_LABEL -> BertData */
+    const int bert = task == 0 || task == 3 || task == 4; /* MLM / MULTI_LABEL / SINGLE_CLASS -> BertData */
     put(&w, "\x80\x03", 2);
     put1(&w, '}');
     put1(&w, '('); /* every DataSet struct has fields */
@@ -128,6 +129,19 @@ size_t orc_pickle_dataset(int task, int batch_size, int seq_len, int label_width
     if (bert) {
         put_key(&w, "token_type_ids");
         put_rows_i32(&w, token_type_ids, B, S);
+    }
+    if (task == 4) { /* SingleClass: "label": Vec<u32>, one per filled row (bert_data.rs:118-121) */
+        size_t c = 0;
+        put_key(&w, "label");
+        seq_open(&w, (size_t)rows);
+        for (int r = 0; r < rows; ++r) {
+            put_i32(&w, labels[r]);
+            seq_elem_done(&w, &c);
+        }
+        seq_close(&w, (size_t)rows);
+        put1(&w, 'u');
+        put1(&w, '.');
+        return w.n;
     }
     put_key(&w, "labels");
     if (task == 3)

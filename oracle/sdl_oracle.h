@@ -66,7 +66,7 @@ int orc_t5_eos(const orc_t5 *t);
 int orc_t5_special_id(const orc_t5 *t, const char *s);
 
 /* ---- Batcher ------------------------------------------------------------ */
-enum { ORC_MLM = 0, ORC_CLM = 1, ORC_SPAN = 2, ORC_MULTI_LABEL = 3 }; /* = SDL_TASK_* */
+enum { ORC_MLM = 0, ORC_CLM = 1, ORC_SPAN = 2, ORC_MULTI_LABEL = 3, ORC_SINGLE_CLASS = 4 }; /* = SDL_TASK_* */
 
 typedef struct orc_encoder orc_encoder; /* a tokenizer + its encode_mask framing */
 

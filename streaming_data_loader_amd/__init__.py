@@ -6,6 +6,7 @@ kernels behind the C ABI in include/sdl_batcher.h (libsdl_batcher.so).  This
 package is the Python host mirror of the reference's Batcher interface.
 """
 from .batcher import (Batcher, BatchConfig, DataSet, GenTokenizer, Gpt, Label, Mask, ModelType,  # noqa: F401
-                      MultiLabel, ProviderChannel, SimpleBatcher, SimpleData, SimpleTransport, Span, TaskType,
+                      MultiLabel, ProviderChannel, SimpleBatcher, SimpleData, SimpleTransport, SingleClass, Span,
+                      TaskType,
                       TokenizerConfig, TrainingConfig, create_batch, get_case, get_mask_length)
 from .native import SDLError  # noqa: F401

@@ -50,6 +50,22 @@ class MultiArrowGenerator:
         return SimpleTransport(SimpleData(text, None), Label(multi=labels))
 
 
+class SingleClassArrowGenerator:
+    """ArrowGenerator for single-class rows (single_class/single_arrow.rs:11-39):
+    `text` utf8 + `label` int64 -> SimpleTransport with Label::Single(label as u32)."""
+
+    def __init__(self, schema):
+        self.t = schema.get_field_index("text")
+        self.l = schema.get_field_index("label")
+        if self.t < 0 or self.l < 0:
+            raise KeyError("schema needs `text` and `label` columns")  # reference: unwrap() panics
+
+    def get_data(self, batch, row: int = 0) -> SimpleTransport:
+        text = batch.column(self.t)[row].as_py()
+        label = int(batch.column(self.l)[row].as_py()) & 0xFFFFFFFF  # `as u32`
+        return SimpleTransport(SimpleData(text, None), Label(single=label))
+
+
 @dataclass
 class ArrowArena:
     arena: np.ndarray          # uint8, the utf8 value bytes (+16 B pad)
@@ -93,6 +109,11 @@ def arena_from_batch(batch, text_col="sentence", label_col="labels") -> ArrowAre
     arena = np.concatenate([body, np.zeros(16, np.uint8)])
 
     lc = batch.column(batch.schema.get_field_index(label_col))
+    if pa.types.is_integer(lc.type):  # SingleClassArrowGenerator: one label per row, `as u32`
+        if lc.null_count:
+            raise ValueError("null label")  # Int64Array::value of a null slot is not a label
+        vals = (np.asarray(lc, np.int64) & 0xFFFFFFFF).astype(np.uint32)
+        return ArrowArena(arena, offs, vals, np.arange(n + 1, dtype=np.uint64))
     if not pa.types.is_list(lc.type) and not pa.types.is_large_list(lc.type):
         raise TypeError(f"{label_col} must be list<int64>, got {lc.type}")
     lo = np.asarray(lc.offsets, dtype=np.int64)

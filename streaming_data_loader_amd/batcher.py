@@ -52,7 +52,12 @@ class MultiLabel:
     number_labels: int = 9
 
 
-DataSetConfig = Union[Mask, Gpt, Span, MultiLabel]
+@dataclass
+class SingleClass:
+    """DataSetConfig::SingleClass (dataset_config.rs; single_cases.rs: Imdb)."""
+
+
+DataSetConfig = Union[Mask, Gpt, Span, MultiLabel, SingleClass]
 
 
 class ModelType(enum.Enum):
@@ -67,6 +72,7 @@ class TaskType(enum.Enum):
     Clm = "clm"
     Span = "span"
     MultiLabel = "multi-label"
+    SingleClass = "single-class"
 
 
 @dataclass
@@ -136,6 +142,10 @@ class DataSet:
     token_type_ids: Optional[np.ndarray] = None
 
     def to_dict(self):
+        if self.kind == "bert-single":
+            # DataSetConfig::SingleClass: "label" is Vec<u32>, one per filled row (bert_data.rs:118-121)
+            return {"input_ids": self.input_ids, "attention_mask": self.attention_mask,
+                    "token_type_ids": self.token_type_ids, "label": self.labels[:self.rows, 0]}
         if self.kind == "bert":
             # BertData.label is pushed per row: the list has `index` entries
             # (Vec<i32> for Mask, Vec<f32> for MultiLabel)
@@ -188,8 +198,9 @@ class SimpleData:
 
 @dataclass
 class Label:
-    """simple_label::Label; only Multi(Vec<u32>) reaches the GPU Batcher."""
+    """simple_label::Label: Multi(Vec<u32>) or Single(u32) reach the GPU Batcher."""
     multi: Optional[list] = None
+    single: Optional[int] = None
 
 
 @dataclass
@@ -230,6 +241,8 @@ class _NativeBatcher(Batcher):
             task, self.kind = native.SDL_TASK_CLM, "gpt2"
         elif isinstance(dataset_config, Span):
             task, self.kind = native.SDL_TASK_SPAN, "t5"
+        elif isinstance(dataset_config, SingleClass):
+            task, self.kind = native.SDL_TASK_SINGLE_CLASS, "bert-single"
         else:
             task, self.kind = native.SDL_TASK_MULTI_LABEL, "bert"
         c = native.default_config(task)
@@ -321,8 +334,8 @@ class SimpleBatcher(_NativeBatcher):
 
     def __init__(self, model_type: ModelType, dataset_config: DataSetConfig, batch_config: BatchConfig,
                  tokenizer: TokenizerConfig, seed: int = 0, device: int = 0):
-        if not isinstance(dataset_config, MultiLabel):
-            raise ValueError("SimpleBatcher on the GPU path supports DataSetConfig::MultiLabel")
+        if not isinstance(dataset_config, (MultiLabel, SingleClass)):
+            raise ValueError("SimpleBatcher on the GPU path supports DataSetConfig::MultiLabel / SingleClass")
         super().__init__(model_type, batch_config, dataset_config, tokenizer, False, seed, device)
 
     @classmethod
@@ -333,6 +346,12 @@ class SimpleBatcher(_NativeBatcher):
     def create_sync_batch(self, data: SimpleTransport) -> Optional[DataSet]:
         text = data.data.text
         raw = text.encode("utf-8") if isinstance(text, str) else bytes(text)
+        if isinstance(self.dataset_config, SingleClass):
+            if data.label is None or data.label.single is None:
+                # the reference's label.map(push) would skip the label and misalign the
+                # label list; SingleClassArrowGenerator always yields Some(Label::Single)
+                raise ValueError("single-class records carry exactly one Label::Single")
+            return self._push(raw, [data.label.single])
         if data.label is None or data.label.multi is None:
             raise ValueError("Label Type Not Supported")  # bert_data.rs:75 panics
         return self._push(raw, data.label.multi)
@@ -343,14 +362,19 @@ class SimpleBatcher(_NativeBatcher):
         offs = np.zeros(len(blobs) + 1, np.uint64)
         np.cumsum([len(x) for x in blobs], out=offs[1:])
         arena = np.frombuffer(b"".join(blobs) + b"\0" * 16, np.uint8)
-        vals, loffs = _pack_labels([t.label.multi for t in items])
+        single = isinstance(self.dataset_config, SingleClass)
+        vals, loffs = _pack_labels([[t.label.single] if single else t.label.multi for t in items])
         return self.push_arena(arena, offs, vals, loffs)
 
-    def push_arrow(self, record_batch, text_col="sentence", label_col="labels"):
+    def push_arrow(self, record_batch, text_col=None, label_col=None):
         """create_sync_batch for every row of an Arrow record batch with the
-        MultiArrowGenerator schema, fed from the column buffers directly."""
+        MultiArrowGenerator schema (sentence, labels: list<int64>) or the
+        SingleClassArrowGenerator one (text, label: int64), fed from the column
+        buffers directly."""
         from .arrow_io import arena_from_batch
-        a = arena_from_batch(record_batch, text_col, label_col)
+        single = isinstance(self.dataset_config, SingleClass)
+        a = arena_from_batch(record_batch, text_col or ("text" if single else "sentence"),
+                             label_col or ("label" if single else "labels"))
         return self.push_arena(a.arena, a.offsets, a.labels, a.label_offsets)
 
 

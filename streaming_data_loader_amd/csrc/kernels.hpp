@@ -125,6 +125,10 @@ hipError_t launch_rows_span(const RowParams &P, const uint32_t *tok, const uint3
                             const uint32_t *row_off, const uint32_t *row_rec, const uint32_t *d_rows, int64_t rows_cap,
                             RowOut out, uint32_t *err, hipStream_t st);
 
+hipError_t launch_single_labels(const uint32_t *labels, const uint64_t *label_off, const uint32_t *row_rec,
+                                const uint32_t *d_rows, int64_t rows_cap, int B, int32_t *out, uint32_t *err,
+                                hipStream_t st);
+
 // transport_frame.hip: the Transport's serde_pickle frames of finished batches
 // (zmq_transmit.rs:71) written straight from the device row planes.
 struct FramePlane {
@@ -134,7 +138,11 @@ struct FramePlane {
     uint32_t rows_full;  // rows of this plane in a full frame
     uint32_t rows_last;  // rows in the last frame
     uint32_t row_bytes;  // encoded bytes per row list
-    uint32_t key_len;    // bytes of the key segment: 'X' + u32 len + name + "]("
+    uint32_t key_len;    // bytes of the key segment: 'X' + u32 len + name (+ "](" unless flat)
+    uint32_t flat;       // the value is one flat list (Vec<u32>): one "row" per frame, no outer list
+    uint32_t width_last;      // row width in the last frame (flat: its filled rows)
+    uint32_t row_bytes_last;
+    uint64_t frame_stride;    // source elements per frame (B * width; flat: B)
     uint64_t off_full;   // frame offset of row 0 (just past the key segment), full frames
     uint64_t off_last;   // the same in the last frame
     uint8_t key[24];

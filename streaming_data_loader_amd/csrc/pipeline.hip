@@ -431,7 +431,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SDL_ROWS_WA
                 if (tt_o) store4(tt_o, j0, S, vec, 0, 0, 0, 0);
                 store4(lb_o, j0, P.label_width, vec_lb, lab[0], lab[1], lab[2], lab[3]);
             }
-        } else if (P.task == 3) {  // MultiLabel: BertData::put_data rows; labels_f32 by k_multi_labels
+        } else if (P.task == 3 || P.task == 4) {  // Multi/SingleClass: BertData::put_data rows; labels by k_*_labels
 #pragma unroll
             for (int m = 0; m < MR; ++m) {
                 const int j0 = 256 * m + 4 * lane;
@@ -686,6 +686,41 @@ hipError_t launch_multi_labels(const uint32_t *labels, const uint64_t *label_off
     const int64_t want = (rows_cap + 255) / 256;
     hipLaunchKernelGGL(k_multi_labels, dim3((unsigned)(want < 2048 ? want : 2048)), dim3(256), 0, st, labels,
                        label_off, row_rec, d_rows, rows_cap, B, NL, out, err);
+    return hipGetLastError();
+}
+
+// BertData SingleClass branch (bert_data.rs:79-81: label.map(|s| self.label.push(s))),
+// fed by SingleClassArrowGenerator (single_arrow.rs:16-26), which always yields
+// Some(Label::Single): labels[row] = the record's one label.  A record with a
+// label count other than one is counted in *err (label 0 written).  Rows past the
+// last batch: 0 (BertData's label list has one entry per filled row).
+__global__ __launch_bounds__(256) void k_single_labels(const uint32_t *__restrict__ labels,
+                                                       const uint64_t *__restrict__ label_off,
+                                                       const uint32_t *__restrict__ row_rec,
+                                                       const uint32_t *__restrict__ d_rows, int64_t rows_cap, int B,
+                                                       int32_t *__restrict__ out, uint32_t *__restrict__ err) {
+    const uint32_t G = *d_rows;
+    int64_t Gpad = ((int64_t)G + B - 1) / B * B;
+    if (Gpad > rows_cap) Gpad = rows_cap;
+    for (int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x; g < Gpad; g += (int64_t)gridDim.x * 256) {
+        int32_t v = 0;
+        if (g < (int64_t)G && labels) {
+            const uint32_t r = row_rec[g];
+            const uint64_t a = label_off[r], e = label_off[r + 1];
+            if (e == a + 1) v = (int32_t)labels[a];
+            else atomicAdd(err, 1u);
+        }
+        out[g] = v;
+    }
+}
+
+hipError_t launch_single_labels(const uint32_t *labels, const uint64_t *label_off, const uint32_t *row_rec,
+                                const uint32_t *d_rows, int64_t rows_cap, int B, int32_t *out, uint32_t *err,
+                                hipStream_t st) {
+    if (rows_cap == 0) return hipSuccess;
+    const int64_t want = (rows_cap + 255) / 256;
+    hipLaunchKernelGGL(k_single_labels, dim3((unsigned)(want < 2048 ? want : 2048)), dim3(256), 0, st, labels,
+                       label_off, row_rec, d_rows, rows_cap, B, out, err);
     return hipGetLastError();
 }
 

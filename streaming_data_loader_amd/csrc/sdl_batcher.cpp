@@ -319,8 +319,10 @@ struct sdl_batcher {
     }
 
     bool multi() const { return P.task == SDL_TASK_MULTI_LABEL; }
+    bool single() const { return P.task == SDL_TASK_SINGLE_CLASS; }
+    bool simple() const { return multi() || single(); }  // SimpleBatcher (simple_batcher.rs)
     bool span() const { return P.task == SDL_TASK_SPAN; }
-    bool with_tt() const { return P.task == SDL_TASK_MLM || P.task == SDL_TASK_MULTI_LABEL; }
+    bool with_tt() const { return P.task == SDL_TASK_MLM || simple(); }
 
     std::shared_ptr<BatchPool> pool;
     HostBatch *new_batch() {
@@ -363,6 +365,7 @@ struct sdl_batcher {
             lab_err.ensure(1);
         } else {
             o_lab.ensure((size_t)std::max<int64_t>(rows_cap, 1) * P.label_width);
+            if (single()) lab_err.ensure(1);
         }
         row_rec.ensure((size_t)std::max<int64_t>(rows_cap, 1));
 
@@ -438,6 +441,10 @@ struct sdl_batcher {
             HIP_TRY(hipMemsetAsync(lab_err.p, 0, 4, st));
             HIP_TRY(launch_multi_labels(d_labels, d_label_off, row_rec.p, row_off.p + R, rows_cap, P.B, P.label_width,
                                         o_f32.p, lab_err.p, st));
+        } else if (single()) {
+            HIP_TRY(hipMemsetAsync(lab_err.p, 0, 4, st));
+            HIP_TRY(launch_single_labels(d_labels, d_label_off, row_rec.p, row_off.p + R, rows_cap, P.B, o_lab.p,
+                                         lab_err.p, st));
         }
         mark(7);
         last_rows_cap = rows_cap;
@@ -452,7 +459,7 @@ struct sdl_batcher {
         const int64_t N = (int64_t)offsets[R];
         const uint32_t *d_labels = nullptr;
         const uint64_t *d_label_off = nullptr;
-        if (multi() && labels && label_off) {  // Label::Multi indices, validated by the caller
+        if (simple() && labels && label_off) {  // Label::Multi indices / Label::Single, validated by the caller
             const uint64_t L = label_off[R];
             pin_labels.ensure((size_t)L + 1);
             pin_label_off.ensure((size_t)R + 1);
@@ -602,8 +609,10 @@ void sdl_config_default(sdl_config *c, int32_t task) {
     c->task = task;
     c->batch_size = 4096;  // masking_cases.rs:43
     c->sequence_length = 128;
-    c->chunk = task == SDL_TASK_MULTI_LABEL ? 0 : 1;
-    c->min_ids = task == SDL_TASK_MULTI_LABEL ? 0 : 64;
+    const bool simple = task == SDL_TASK_MULTI_LABEL || task == SDL_TASK_SINGLE_CLASS;
+    c->chunk = simple ? 0 : 1;
+    c->min_ids = simple ? 0 : 64;
+    if (task == SDL_TASK_SINGLE_CLASS) c->batch_size = 2048;  // single_cases.rs (Imdb)
     c->mask_length = (int32_t)((float)c->sequence_length * 0.15f);  // masking_cases.rs:34-36
     c->mask_id = 103;
     c->number_labels = 9;
@@ -618,7 +627,7 @@ int sdl_batcher_create(const sdl_config *cfg, const char *tokenizer_path, const 
     if (!cfg || !tokenizer_path || !out) return fail(SDL_ERR_ARG, "null argument");
     *out = nullptr;
     if (cfg->task != SDL_TASK_MLM && cfg->task != SDL_TASK_CLM && cfg->task != SDL_TASK_MULTI_LABEL &&
-        cfg->task != SDL_TASK_SPAN)
+        cfg->task != SDL_TASK_SPAN && cfg->task != SDL_TASK_SINGLE_CLASS)
         return fail(SDL_ERR_UNSUPPORTED, "unknown task");
     if (cfg->task == SDL_TASK_SPAN && (cfg->sequence_length < 4 || !(cfg->avg_span_gap == cfg->avg_span_gap) ||
                                        !(cfg->avg_span_size == cfg->avg_span_size)))
@@ -749,7 +758,8 @@ int sdl_batcher_create(const sdl_config *cfg, const char *tokenizer_path, const 
         P.min_ids = cfg->min_ids;
         P.mask_length = cfg->mask_length;
         P.mask_id = cfg->mask_id;
-        P.label_width = cfg->task == SDL_TASK_MULTI_LABEL ? cfg->number_labels
+        P.label_width = cfg->task == SDL_TASK_MULTI_LABEL    ? cfg->number_labels
+                        : cfg->task == SDL_TASK_SINGLE_CLASS ? 1
                         : cfg->task == SDL_TASK_SPAN          ? cfg->sequence_length / 4  // t5_data.rs:44
                                                               : cfg->sequence_length;
         if (cfg->task == SDL_TASK_SPAN) {
@@ -757,7 +767,7 @@ int sdl_batcher_create(const sdl_config *cfg, const char *tokenizer_path, const 
             span_table(cfg->avg_span_size, 1, &P.size_kmin, &P.size_n, P.size_thr);
             P.extra_ids = h->d_extra.p;
         }
-        if (cfg->task == SDL_TASK_MULTI_LABEL) {  // SimpleBatcher: one row per record, no filter
+        if (cfg->task == SDL_TASK_MULTI_LABEL || cfg->task == SDL_TASK_SINGLE_CLASS) {  // SimpleBatcher: one row per record, no filter
             P.chunk = 0;
             P.min_ids = 0;
         }
@@ -813,6 +823,7 @@ int sdl_batcher_push(sdl_batcher *h, const uint8_t *utf8, size_t len, const uint
     if (h->multi()) {
         if (int rc = check_labels(h, labels, n_labels)) return rc;
     }
+    if (h->single() && n_labels != 1) return fail(SDL_ERR_ARG, "single-class records carry exactly one label");
     if (len >= (1ull << 32)) return fail(SDL_ERR_CAPACITY, "record too large");
     try {
         uint64_t offs[2] = {0, (uint64_t)len};
@@ -844,6 +855,12 @@ int sdl_batcher_push_many(sdl_batcher *h, const uint8_t *arena, const uint64_t *
         for (size_t r = 0; r < n_records; ++r)
             if (label_offsets[r + 1] < label_offsets[r]) return fail(SDL_ERR_ARG, "label_offsets must be non-decreasing");
         if (int rc = check_labels(h, labels + label_offsets[0], label_offsets[n_records] - label_offsets[0])) return rc;
+    }
+    if (h->single()) {
+        if (!label_offsets || !labels) return fail(SDL_ERR_ARG, "single-class records need their labels");
+        for (size_t r = 0; r < n_records; ++r)
+            if (label_offsets[r + 1] != label_offsets[r] + 1)
+                return fail(SDL_ERR_ARG, "single-class records carry exactly one label");
     }
     if (offsets[0] != 0) return fail(SDL_ERR_ARG, "offsets[0] must be 0");
     for (size_t r = 0; r < n_records; ++r)
@@ -880,7 +897,7 @@ int sdl_batcher_flush(sdl_batcher *h, sdl_batch *out) {
     HostBatch *b = h->store.front();
     h->store.pop_front();
     // SimpleBatcher::get_working_batch swaps in a fresh DataSet (simple_batcher.rs:46-52)
-    if (h->multi() && h->store.empty()) h->store.push_back(h->new_batch());
+    if (h->simple() && h->store.empty()) h->store.push_back(h->new_batch());
     fill_batch(h, b, out);
     return 1;
 }
@@ -914,7 +931,7 @@ int sdl_process_device_labels(sdl_batcher *h, const uint8_t *d_text, uint64_t te
         out->token_type_ids = h->with_tt() ? h->o_tt.p : nullptr;
         out->labels = h->multi() ? nullptr : h->o_lab.p;
         out->labels_f32 = h->multi() ? h->o_f32.p : nullptr;
-        out->d_label_errors = h->multi() ? h->lab_err.p : h->span() ? h->span_err.p : nullptr;
+        out->d_label_errors = h->simple() ? h->lab_err.p : h->span() ? h->span_err.p : nullptr;
         out->d_tokenize_errors = h->dt.kind == TOK_UNIGRAM ? h->uni_err.p : nullptr;
         out->d_rows = h->row_off.p + n_records;
         out->d_record_rows = h->rec_rows.p;
@@ -1004,6 +1021,7 @@ struct FramePlaneDesc {
     uint32_t width;
     bool f32;
     bool filled_rows_only;  // BertData.label: one entry per filled row
+    bool flat;              // Vec<u32> (SingleClass `label`): one list of B (filled) items
 };
 
 // list of `n` items of `item` bytes each: "](" items ["e(" per 1000] "e", or "]" when empty
@@ -1015,14 +1033,16 @@ uint64_t frame_layout(FrameParams &fp, const FramePlaneDesc *d, int np, const ui
     for (int p = 0; p < np; ++p) {
         FramePlane &P = fp.plane[p];
         const uint32_t n = (uint32_t)std::strlen(d[p].name);
-        P.key_len = 5 + n + 2;
+        P.key_len = 5 + n + (P.flat ? 0 : 2);
         P.key[0] = 'X';
         for (int i = 0; i < 4; ++i) P.key[1 + i] = (uint8_t)(n >> (8 * i));
         std::memcpy(P.key + 5, d[p].name, n);
-        P.key[5 + n] = ']';
-        P.key[6 + n] = '(';
+        if (!P.flat) {
+            P.key[5 + n] = ']';
+            P.key[6 + n] = '(';
+        }
         (last ? P.off_last : P.off_full) = pos + P.key_len;
-        pos += 5 + n + list_bytes(plane_rows[p], P.row_bytes);
+        pos += 5 + n + (P.flat ? (last ? P.row_bytes_last : P.row_bytes) : list_bytes(plane_rows[p], P.row_bytes));
     }
     return pos + 2;  // SETITEMS, STOP
 }
@@ -1039,16 +1059,18 @@ int sdl_pickle_frames_device(sdl_batcher *h, const sdl_device_rows *rows, uint64
     const uint64_t rem = n_rows % B, n_frames = n_rows / B + (flush_partial && rem ? 1 : 0);
     if (n_frames * B > rows->rows_capacity)
         return fail(SDL_ERR_ARG, "n_rows exceeds the rows the device planes hold");
-    const bool bert = task == SDL_TASK_MLM || task == SDL_TASK_MULTI_LABEL;
+    const bool bert = task == SDL_TASK_MLM || task == SDL_TASK_MULTI_LABEL || task == SDL_TASK_SINGLE_CLASS;
     FramePlaneDesc d[4];
     int np = 0;
-    d[np++] = {"input_ids", rows->input_ids, (uint32_t)S, false, false};
-    d[np++] = {"attention_mask", rows->attention_mask, (uint32_t)S, false, false};
-    if (bert) d[np++] = {"token_type_ids", rows->token_type_ids, (uint32_t)S, false, false};
+    d[np++] = {"input_ids", rows->input_ids, (uint32_t)S, false, false, false};
+    d[np++] = {"attention_mask", rows->attention_mask, (uint32_t)S, false, false, false};
+    if (bert) d[np++] = {"token_type_ids", rows->token_type_ids, (uint32_t)S, false, false, false};
     if (task == SDL_TASK_MULTI_LABEL)
-        d[np++] = {"labels", rows->labels_f32, (uint32_t)LW, true, true};
+        d[np++] = {"labels", rows->labels_f32, (uint32_t)LW, true, true, false};
+    else if (task == SDL_TASK_SINGLE_CLASS)  // bert_data.rs:118-121: "label": Vec<u32>
+        d[np++] = {"label", rows->labels, 1, false, true, true};
     else
-        d[np++] = {"labels", rows->labels, (uint32_t)LW, false, bert};
+        d[np++] = {"labels", rows->labels, (uint32_t)LW, false, bert, false};
     for (int p = 0; p < np; ++p)
         if (!d[p].src && n_frames) return fail(SDL_ERR_ARG, std::string("device plane missing: ") + d[p].name);
     try {
@@ -1060,12 +1082,25 @@ int sdl_pickle_frames_device(sdl_batcher *h, const sdl_device_rows *rows, uint64
         const bool partial = n_frames && n_frames * B > n_rows;
         for (int p = 0; p < np; ++p) {
             FramePlane &P = fp.plane[p];
+            const uint32_t ew = d[p].f32 ? 9 : 5;
+            const uint64_t filled_last = partial && d[p].filled_rows_only ? rem : B;
             P.src = d[p].src;
-            P.width = d[p].width;
             P.is_f32 = d[p].f32;
-            P.row_bytes = (uint32_t)list_bytes(P.width, d[p].f32 ? 9 : 5);
-            full_rows[p] = P.rows_full = (uint32_t)B;
-            last_rows[p] = P.rows_last = (uint32_t)(partial && d[p].filled_rows_only ? rem : B);
+            P.flat = d[p].flat;
+            if (P.flat) {  // one list per frame of the B (last: filled) values
+                P.width = (uint32_t)B;
+                P.width_last = (uint32_t)filled_last;
+                P.frame_stride = B;
+                full_rows[p] = P.rows_full = 1;
+                last_rows[p] = P.rows_last = 1;
+            } else {
+                P.width = P.width_last = d[p].width;
+                P.frame_stride = B * d[p].width;
+                full_rows[p] = P.rows_full = (uint32_t)B;
+                last_rows[p] = P.rows_last = (uint32_t)filled_last;
+            }
+            P.row_bytes = (uint32_t)list_bytes(P.width, ew);
+            P.row_bytes_last = (uint32_t)list_bytes(P.width_last, ew);
         }
         fp.frame_bytes = frame_layout(fp, d, np, full_rows, false);
         fp.last_frame_bytes = frame_layout(fp, d, np, last_rows, true);

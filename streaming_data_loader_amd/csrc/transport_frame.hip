@@ -75,9 +75,9 @@ __device__ __forceinline__ void lds_put_f64(uint8_t *L, uint32_t p, float f) {
 
 }  // namespace
 
-__global__ __launch_bounds__(64 * FRAME_WAVES) void k_frame_rows(FrameParams fp, uint32_t lds_stride) {
+__global__ __launch_bounds__(64 * FRAME_WAVES) void k_frame_rows(FrameParams fp, int plane, uint32_t lds_stride) {
     extern __shared__ uint4 lds_raw[];
-    const FramePlane &P = fp.plane[blockIdx.y];
+    const FramePlane &P = fp.plane[plane];
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     uint8_t *L = reinterpret_cast<uint8_t *>(lds_raw) + wv * lds_stride;
     const uint64_t total = fp.n_frames ? (fp.n_frames - 1) * P.rows_full + P.rows_last : 0;
@@ -86,17 +86,18 @@ __global__ __launch_bounds__(64 * FRAME_WAVES) void k_frame_rows(FrameParams fp,
     uint64_t f = 0, r = 0;
     uint8_t *dst = nullptr;
     uint32_t mis = 0;
-    const uint32_t rb = P.row_bytes, W = P.width;
+    uint32_t rb = P.row_bytes, W = P.width;
     if (valid) {
         f = g / P.rows_full;
         r = g - f * P.rows_full;
-        dst = fp.out + f * fp.frame_bytes + (f == fp.n_frames - 1 ? P.off_last : P.off_full) +
-              row_pos((uint32_t)r, rb);
+        const bool last = f == fp.n_frames - 1;
+        if (last) rb = P.row_bytes_last, W = P.width_last;
+        dst = fp.out + f * fp.frame_bytes + (last ? P.off_last : P.off_full) + row_pos((uint32_t)r, P.row_bytes);
         mis = (uint32_t)((uintptr_t)dst & 15u);
-        const uint64_t srow = f * fp.B + r;
+        const uint64_t e0 = f * P.frame_stride + r * P.width;  // first source element of the row
         if (!P.is_f32) {
-            const int32_t *src = static_cast<const int32_t *>(P.src) + srow * W;
-            const bool v16 = (W & 3u) == 0;  // rows start 16-B aligned
+            const int32_t *src = static_cast<const int32_t *>(P.src) + e0;
+            const bool v16 = (e0 & 3u) == 0;  // the row starts 16-B aligned
             for (uint32_t grp = lane; grp * 4u < W; grp += 64u) {
                 const uint32_t k0 = grp * 4u, p = mis + elem_pos(k0, 5u);
                 if (k0 + 4u <= W) {
@@ -117,7 +118,7 @@ __global__ __launch_bounds__(64 * FRAME_WAVES) void k_frame_rows(FrameParams fp,
                 }
             }
         } else {
-            const float *src = static_cast<const float *>(P.src) + srow * W;
+            const float *src = static_cast<const float *>(P.src) + e0;
             for (uint32_t k = lane; k < W; k += 64u) lds_put_f64(L, mis + elem_pos(k, 9u), src[k]);
         }
         if (lane == 0) {
@@ -169,7 +170,7 @@ __global__ __launch_bounds__(64) void k_frame_skeleton(FrameParams fp) {
     const uint32_t rows = last ? P.rows_last : P.rows_full;
     uint8_t *K = F + off - P.key_len;
     for (uint32_t i = 0; i < P.key_len; ++i) K[i] = P.key[i];
-    if (!rows) return;  // key ends "]" (an empty list)
+    if (P.flat) return;  // the value is one list, written whole by k_frame_rows
     for (uint32_t m = 1; m * 1000u <= rows; ++m) {
         uint8_t *q = F + off + (uint64_t)m * 1000u * P.row_bytes + 2ull * (m - 1u);
         q[0] = 'e', q[1] = '(';
@@ -179,18 +180,16 @@ __global__ __launch_bounds__(64) void k_frame_skeleton(FrameParams fp) {
 
 hipError_t launch_frames(const FrameParams &fp, hipStream_t st) {
     if (fp.n_frames == 0) return hipSuccess;
-    uint32_t max_rb = 0;
-    uint64_t max_rows = 0;
-    for (int p = 0; p < fp.n_planes; ++p) {
-        max_rb = fp.plane[p].row_bytes > max_rb ? fp.plane[p].row_bytes : max_rb;
-        const uint64_t n = (fp.n_frames - 1) * fp.plane[p].rows_full + fp.plane[p].rows_last;
-        max_rows = n > max_rows ? n : max_rows;
-    }
-    const uint32_t stride = (max_rb + 15u + 16u) & ~15u;
-    const uint64_t nb = (max_rows + FRAME_WAVES - 1) / FRAME_WAVES;
-    if (nb) {
-        hipLaunchKernelGGL(k_frame_rows, dim3((unsigned)nb, (unsigned)fp.n_planes), dim3(64 * FRAME_WAVES),
-                           (size_t)stride * FRAME_WAVES, st, fp, stride);
+    for (int p = 0; p < fp.n_planes; ++p) {  // one launch per plane: LDS sized to its rows
+        const FramePlane &P = fp.plane[p];
+        const uint32_t rb = P.row_bytes > P.row_bytes_last ? P.row_bytes : P.row_bytes_last;
+        const uint32_t stride = (rb + 15u + 16u) & ~15u;
+        const uint64_t rows = (fp.n_frames - 1) * P.rows_full + P.rows_last;
+        const uint64_t nb = (rows + FRAME_WAVES - 1) / FRAME_WAVES;
+        if (!nb) continue;
+        if ((size_t)stride * FRAME_WAVES > 160u * 1024u) return hipErrorInvalidValue;
+        hipLaunchKernelGGL(k_frame_rows, dim3((unsigned)nb), dim3(64 * FRAME_WAVES), (size_t)stride * FRAME_WAVES, st,
+                           fp, p, stride);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }

@@ -14,7 +14,7 @@ BERT_PROXY_TOKENIZER = os.path.join(ASSETS, "bert_proxy", "tokenizer.json")
 GPT2_PROXY_TOKENIZER = os.path.join(ASSETS, "gpt2_proxy", "tokenizer.json")
 T5_PROXY_TOKENIZER = os.path.join(ASSETS, "t5_proxy", "tokenizer.json")
 
-SDL_TASK_MLM, SDL_TASK_CLM, SDL_TASK_SPAN, SDL_TASK_MULTI_LABEL = 0, 1, 2, 3
+SDL_TASK_MLM, SDL_TASK_CLM, SDL_TASK_SPAN, SDL_TASK_MULTI_LABEL, SDL_TASK_SINGLE_CLASS = 0, 1, 2, 3, 4
 
 # every symbol include/sdl_batcher.h declares
 EXPORTS = [

@@ -100,6 +100,7 @@ class OrcOut(ctypes.Structure):
 
 
 MLM, CLM, SPAN, MULTI_LABEL = 0, 1, 2, 3
+SINGLE_CLASS = 4
 
 
 class Tok:
@@ -247,7 +248,7 @@ class OracleBatcherEx:
         self.h = lib().orc_batcher_create(encoder.buf, ctypes.byref(c))
         if not self.h:
             raise RuntimeError("oracle batcher config rejected")
-        LW = S if task in (MLM, CLM) else S // 4 if task == SPAN else 0
+        LW = S if task in (MLM, CLM) else S // 4 if task == SPAN else 1 if task == SINGLE_CLASS else 0
         self.planes = {"input_ids": np.zeros((B, S), np.int32), "attention_mask": np.zeros((B, S), np.int32),
                        "token_type_ids": np.zeros((B, S), np.int32), "labels": np.zeros((B, max(LW, 1)), np.int32),
                        "labels_f32": np.zeros((B, number_labels), np.float32)}
@@ -311,7 +312,7 @@ def oracle_rows(tok, texts, S, mask_length, mask_id=103, seed=0, B=64, first_rec
     return np.concatenate(planes, axis=1)
 
 
-TASK_IDS = {"mlm": 0, "clm": 1, "span": 2, "multi-label": 3}
+TASK_IDS = {"mlm": 0, "clm": 1, "span": 2, "multi-label": 3, "single-class": 4}
 
 
 def pickle_dataset(task, B, S, LW, rows, input_ids, attention_mask, token_type_ids, labels):
