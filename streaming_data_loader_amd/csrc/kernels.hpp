@@ -142,6 +142,7 @@ struct FramePlane {
     uint32_t flat;       // the value is one flat list (Vec<u32>): one "row" per frame, no outer list
     uint32_t width_last;      // row width in the last frame (flat: its filled rows)
     uint32_t row_bytes_last;
+    uint32_t rpw;             // rows per wave (set by launch_frames)
     uint64_t frame_stride;    // source elements per frame (B * width; flat: B)
     uint64_t off_full;   // frame offset of row 0 (just past the key segment), full frames
     uint64_t off_last;   // the same in the last frame

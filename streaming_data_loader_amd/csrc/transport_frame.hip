@@ -14,8 +14,9 @@
 // host computes, per plane, the key position, the first row's offset and the
 // row size; row r of a plane starts at off + r*row_bytes + 2*(r/1000).
 //
-// k_frame_rows: one wave per row.  The wave reads its row (16-B loads, one
-// group of 4 ids per lane), composes the 5-byte records of 4 ids as 5 dwords in
+// k_frame_rows: one wave per run of rows (rows of <= 1024 ids, as many as fit:
+// S=128 -> 8 rows, S=512 -> 2, the 9-wide f32 labels -> 100).  The wave reads its
+// rows (16-B loads, one group of 4 ids per lane), composes the 5-byte records of 4 ids as 5 dwords in
 // registers, funnel-shifts them to the row's byte alignment and stores them in
 // an LDS image whose alignment matches the destination's; the image then goes
 // to HBM as aligned 16-B stores (byte stores only at the row's two ends).  The
@@ -75,70 +76,80 @@ __device__ __forceinline__ void lds_put_f64(uint8_t *L, uint32_t p, float f) {
 
 }  // namespace
 
-__global__ __launch_bounds__(64 * FRAME_WAVES) void k_frame_rows(FrameParams fp, int plane, uint32_t lds_stride) {
+__global__ __launch_bounds__(64 * FRAME_WAVES) void k_frame_rows(FrameParams fp, uint32_t lds_stride) {
     extern __shared__ uint4 lds_raw[];
-    const FramePlane &P = fp.plane[plane];
+    const FramePlane &P = fp.plane[blockIdx.y];
+    const uint32_t rpw = P.rpw;
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     uint8_t *L = reinterpret_cast<uint8_t *>(lds_raw) + wv * lds_stride;
-    const uint64_t total = fp.n_frames ? (fp.n_frames - 1) * P.rows_full + P.rows_last : 0;
+    // a wave writes a run of up to rpw rows of one frame; rpw divides 1000, so a run
+    // never contains an APPENDS marker (those sit between runs)
+    const uint64_t wpf = (P.rows_full + rpw - 1) / rpw;  // waves per frame
     const uint64_t g = (uint64_t)blockIdx.x * FRAME_WAVES + wv;
-    const bool valid = g < total;
-    uint64_t f = 0, r = 0;
+    const uint64_t f = g / wpf;
+    const uint32_t r0 = (uint32_t)(g - f * wpf) * rpw;
+    const bool last = f == fp.n_frames - 1;
+    const uint32_t rows_f = last ? P.rows_last : P.rows_full;
+    const bool valid = f < fp.n_frames && r0 < rows_f;
+    const uint32_t nr = valid ? min(rpw, rows_f - r0) : 0u;
+    const uint32_t rb = last ? P.row_bytes_last : P.row_bytes, W = last ? P.width_last : P.width;
     uint8_t *dst = nullptr;
     uint32_t mis = 0;
-    uint32_t rb = P.row_bytes, W = P.width;
     if (valid) {
-        f = g / P.rows_full;
-        r = g - f * P.rows_full;
-        const bool last = f == fp.n_frames - 1;
-        if (last) rb = P.row_bytes_last, W = P.width_last;
-        dst = fp.out + f * fp.frame_bytes + (last ? P.off_last : P.off_full) + row_pos((uint32_t)r, P.row_bytes);
+        dst = fp.out + f * fp.frame_bytes + (last ? P.off_last : P.off_full) + row_pos(r0, P.row_bytes);
         mis = (uint32_t)((uintptr_t)dst & 15u);
-        const uint64_t e0 = f * P.frame_stride + r * P.width;  // first source element of the row
+        const uint64_t e0 = f * P.frame_stride + (uint64_t)r0 * P.width;  // first source element of the run
         if (!P.is_f32) {
             const int32_t *src = static_cast<const int32_t *>(P.src) + e0;
-            const bool v16 = (e0 & 3u) == 0;  // the row starts 16-B aligned
-            for (uint32_t grp = lane; grp * 4u < W; grp += 64u) {
-                const uint32_t k0 = grp * 4u, p = mis + elem_pos(k0, 5u);
+            const uint32_t gpr = (W + 3u) >> 2;  // groups of 4 ids per row
+            const bool v16 = ((e0 | W) & 3u) == 0;  // every row of the run starts 16-B aligned
+            for (uint32_t q = lane; q < nr * gpr; q += 64u) {
+                const uint32_t i = q / gpr, k0 = (q - i * gpr) * 4u;
+                const uint32_t p = mis + i * rb + elem_pos(k0, 5u);
+                const int32_t *s = src + (size_t)i * W;
                 if (k0 + 4u <= W) {
                     uint32_t v0, v1, v2, v3;
                     if (v16) {
-                        const uint4 q = *reinterpret_cast<const uint4 *>(src + k0);
-                        v0 = q.x, v1 = q.y, v2 = q.z, v3 = q.w;
+                        const uint4 x = *reinterpret_cast<const uint4 *>(s + k0);
+                        v0 = x.x, v1 = x.y, v2 = x.z, v3 = x.w;
                     } else {
-                        v0 = (uint32_t)src[k0], v1 = (uint32_t)src[k0 + 1], v2 = (uint32_t)src[k0 + 2],
-                        v3 = (uint32_t)src[k0 + 3];
+                        v0 = (uint32_t)s[k0], v1 = (uint32_t)s[k0 + 1], v2 = (uint32_t)s[k0 + 2],
+                        v3 = (uint32_t)s[k0 + 3];
                     }
                     // 'J' v0 'J' v1 'J' v2 'J' v3, little-endian dwords
                     const uint32_t d[5] = {0x4Au | v0 << 8, v0 >> 24 | 0x4Au << 8 | v1 << 16,
                                            v1 >> 16 | 0x4Au << 16 | v2 << 24, v2 >> 8 | 0x4Au << 24, v3};
                     lds_put20(L, p, d);
                 } else {
-                    for (uint32_t k = k0; k < W; ++k) lds_put_i32(L, mis + elem_pos(k, 5u), (uint32_t)src[k]);
+                    for (uint32_t k = k0; k < W; ++k) lds_put_i32(L, mis + i * rb + elem_pos(k, 5u), (uint32_t)s[k]);
                 }
             }
         } else {
             const float *src = static_cast<const float *>(P.src) + e0;
-            for (uint32_t k = lane; k < W; k += 64u) lds_put_f64(L, mis + elem_pos(k, 9u), src[k]);
+            for (uint32_t q = lane; q < nr * W; q += 64u) {
+                const uint32_t i = q / W, k = q - i * W;
+                lds_put_f64(L, mis + i * rb + elem_pos(k, 9u), src[q]);
+            }
         }
-        if (lane == 0) {
-            L[mis] = ']';
+        for (uint32_t i = lane; i < nr; i += 64u) {  // list opener, inner markers, closer of each row
+            uint8_t *R = L + mis + i * rb;
+            R[0] = ']';
             if (W) {
-                L[mis + 1] = '(';
+                R[1] = '(';
                 const uint32_t ew = P.is_f32 ? 9u : 5u;
                 for (uint32_t m = 1; m * 1000u <= W; ++m) {
-                    const uint32_t q = mis + 2u + m * 1000u * ew + 2u * (m - 1u);
-                    L[q] = 'e';
-                    L[q + 1] = '(';
+                    const uint32_t q = 2u + m * 1000u * ew + 2u * (m - 1u);
+                    R[q] = 'e';
+                    R[q + 1] = '(';
                 }
-                L[mis + rb - 1] = 'e';
+                R[rb - 1] = 'e';
             }
         }
     }
     __syncthreads();
     if (valid) {
         uint8_t *A = dst - mis;  // 16-B aligned
-        const uint32_t end = mis + rb, nch = (end + 15u) >> 4;
+        const uint32_t end = mis + nr * rb, nch = (end + 15u) >> 4;
         for (uint32_t c = lane; c < nch; c += 64u) {
             const uint32_t lo = c * 16u, hi = lo + 16u;
             if (lo >= mis && hi <= end) {
@@ -180,16 +191,30 @@ __global__ __launch_bounds__(64) void k_frame_skeleton(FrameParams fp) {
 
 hipError_t launch_frames(const FrameParams &fp, hipStream_t st) {
     if (fp.n_frames == 0) return hipSuccess;
-    for (int p = 0; p < fp.n_planes; ++p) {  // one launch per plane: LDS sized to its rows
-        const FramePlane &P = fp.plane[p];
+    FrameParams q = fp;  // one launch for all planes (blockIdx.y), LDS sized to the widest run
+    uint32_t stride = 16;
+    uint64_t max_waves = 0;
+    for (int p = 0; p < q.n_planes; ++p) {
+        FramePlane &P = q.plane[p];
+        const uint32_t w = P.width > 0 ? P.width : 1u;
+        P.rpw = 1;  // rows per wave: the largest divisor of 1000 with <= 1024 elements
+        for (uint32_t d : {1000u, 500u, 250u, 200u, 125u, 100u, 50u, 40u, 25u, 20u, 10u, 8u, 5u, 4u, 2u})
+            if (d * w <= 1024u) {
+                P.rpw = d;
+                break;
+            }
+        if (P.flat) P.rpw = 1;
         const uint32_t rb = P.row_bytes > P.row_bytes_last ? P.row_bytes : P.row_bytes_last;
-        const uint32_t stride = (rb + 15u + 16u) & ~15u;
-        const uint64_t rows = (fp.n_frames - 1) * P.rows_full + P.rows_last;
-        const uint64_t nb = (rows + FRAME_WAVES - 1) / FRAME_WAVES;
-        if (!nb) continue;
-        if ((size_t)stride * FRAME_WAVES > 160u * 1024u) return hipErrorInvalidValue;
-        hipLaunchKernelGGL(k_frame_rows, dim3((unsigned)nb), dim3(64 * FRAME_WAVES), (size_t)stride * FRAME_WAVES, st,
-                           fp, p, stride);
+        const uint32_t st_p = (P.rpw * rb + 15u + 16u) & ~15u;
+        stride = st_p > stride ? st_p : stride;
+        const uint64_t waves = q.n_frames * ((P.rows_full + P.rpw - 1) / P.rpw);
+        max_waves = waves > max_waves ? waves : max_waves;
+    }
+    const uint64_t nb = (max_waves + FRAME_WAVES - 1) / FRAME_WAVES;
+    if ((size_t)stride * FRAME_WAVES > 160u * 1024u) return hipErrorInvalidValue;
+    if (nb) {
+        hipLaunchKernelGGL(k_frame_rows, dim3((unsigned)nb, (unsigned)q.n_planes), dim3(64 * FRAME_WAVES),
+                           (size_t)stride * FRAME_WAVES, st, q, stride);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
