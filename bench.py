@@ -222,6 +222,9 @@ def main():
     ap.add_argument("--e2e", action="store_true", help="also time the host record path (H2D + kernels + D2H)")
     ap.add_argument("--json", action="store_true",
                     help="also time the provider's JsonText filter on the device (JSON lines -> text arena)")
+    ap.add_argument("--e2e-frames", action="store_true",
+                    help="end to end from host JSON lines to host pickle frames: H2D, JsonText filter, "
+                         "tokenize+mask, transport frames, D2H (the provider -> batcher -> transport path)")
     ap.add_argument("--frames", action="store_true",
                     help="also time the Transport step on the device: every batch -> its serde_pickle frame")
     args = ap.parse_args()
@@ -348,6 +351,9 @@ def main():
     if args.frames and rank == 0:
         line["transport_frames"] = transport_frames(db, res, args.task, stream, dev, args.steps, args.warmup,
                                                     not args.no_cpu_baseline)
+    if args.e2e_frames and rank == 0 and args.task in ("mlm", "clm", "span"):
+        # last: it reuses the handle's workspace (the step's planes are overwritten)
+        line["end_to_end_frames"] = end_to_end_frames(db, records, order, dev, stream, args.task)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("cpu baseline ...")
         line["cpu_baseline"] = cpu_baseline(args.task, records, order)
@@ -412,6 +418,52 @@ def transport_frames(db, res, task_name, stream, dev, steps, warmup, with_cpu):
                                "kind": "port", "sample": f"{nfr} frames ({k} distinct batches of this step), "
                                                          f"oracle/orc_pickle.c single-threaded, {dt:.1f} s"}
     return out
+
+
+def end_to_end_frames(db, records, order, dev, stream, task_name, nbytes=64 << 20, reps=3):
+    """The whole hot path from host memory to host memory, as north_star frames it
+    (a JSON-lines stream in, the bytes the Transport socket sends out): JSON lines
+    in pinned host memory -> H2D -> sdl_json_text_device (the Provider's JsonText
+    filter) -> sdl_process_device (tokenize + mask) -> sdl_pickle_frames_device
+    (serde_pickle frames of every batch, the flushed partial one included) -> D2H
+    into pinned host memory.  Rate = text bytes / wall time; sequential stages on
+    one stream (no copy/compute overlap)."""
+    import torch
+    lines, done = [], 0
+    for i, k in enumerate(order):
+        lines.append(json.dumps({"id": i, "text": records[k]}).encode("utf-8"))
+        done += len(records[k].encode("utf-8"))
+        if done >= nbytes:
+            break
+    buf = b"\n".join(lines) + b"\n"
+    host = torch.zeros(len(buf) + 32, dtype=torch.uint8).pin_memory()
+    host[:len(buf)] = torch.frombuffer(bytearray(buf), dtype=torch.uint8)
+    d_json = torch.empty(len(buf) + 32, dtype=torch.uint8, device=dev)
+    out_host = None
+    best, info = None, {}
+    for r in range(reps + 1):  # first pass warms the workspaces
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        with torch.cuda.stream(stream):
+            d_json.copy_(host, non_blocking=True)
+        jt = db.json_text(d_json.data_ptr(), len(buf), stream.cuda_stream)
+        res = db.process(jt.d_text, jt.text_bytes, jt.d_offsets, jt.n_records, 0, stream.cuda_stream)
+        rows = res.rows()
+        fr = db.pickle_frames(res, rows, True, stream.cuda_stream)
+        total = int(fr.f.total_bytes)
+        if out_host is None or out_host.numel() < total:
+            out_host = torch.empty(total, dtype=torch.uint8).pin_memory()
+        from streaming_data_loader_amd import native
+        native.d2h(db._h, out_host.numpy(), fr.f.d_frames, total, stream.cuda_stream)
+        dt = time.perf_counter() - t0
+        if r:
+            best = dt if best is None else min(best, dt)
+        info = {"records": int(jt.n_records), "rows": rows, "frames": len(fr), "frame_bytes": total}
+    assert info["records"] == len(lines)
+    return {"MBps": round(done / best / 1e6, 2), "ms": round(best * 1e3, 2), "text_bytes": done,
+            "json_bytes": len(buf), **info,
+            "path": "pinned host JSON lines -> H2D -> JsonText filter -> tokenize+mask -> serde_pickle frames -> "
+                    "D2H to pinned host (sequential, one stream)"}
 
 
 def provider_json(db, records, order, dev, steps, warmup, step_ms):
