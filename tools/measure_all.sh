@@ -21,22 +21,23 @@ STEPS="${1:-tests,bench,tasks,e2e,prof,pmc}"
 [[ $STEPS == *tests* ]] && step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
 [[ $STEPS == *bench* ]] && step bench 600 python bench.py > $O/bench_mlm.json 2> $O/bench_mlm.err
 if [[ $STEPS == *tasks* ]]; then
-  for t in span clm multi-label; do
-    step bench_$t 600 python bench.py --task $t > $O/bench_$t.json 2> $O/bench_$t.err
+  for t in span clm multi-label single-class; do
+    step bench_$t 600 python bench.py --task $t --frames > $O/bench_$t.json 2> $O/bench_$t.err
   done
+  step bench_mlm_frames 300 python bench.py --frames --e2e-frames --no-cpu-baseline > $O/bench_mlm_frames.json 2> $O/bench_mlm_frames.err
 fi
 [[ $STEPS == *json* ]] && step bench_json 300 python bench.py --steps 5 --warmup 2 --arena-mib 64 --no-cpu-baseline --json > $O/bench_json.json 2> $O/bench_json.err
 if [[ $STEPS == *e2e* ]]; then
-  for t in mlm span clm multi-label; do
+  for t in mlm span clm multi-label single-class; do
     step e2e_$t 300 python bench.py --task $t --steps 3 --warmup 1 --arena-mib 64 --no-cpu-baseline --e2e > $O/e2e_$t.json 2> $O/e2e_$t.err
   done
 fi
 if [[ $STEPS == *prof* ]]; then
-  for t in mlm span clm multi-label; do
-    step prof_$t 300 rocprofv3 --kernel-trace --stats -d $O/prof_$t -o run --output-format csv -- python3 bench.py --task $t --steps 5 --warmup 2 --no-cpu-baseline > $O/prof_$t.json 2> $O/prof_$t.err
+  for t in mlm span clm multi-label single-class; do
+    step prof_$t 300 rocprofv3 --kernel-trace --stats -d $O/prof_$t -o run --output-format csv -- python3 bench.py --task $t --steps 5 --warmup 2 --no-cpu-baseline --frames > $O/prof_$t.json 2> $O/prof_$t.err
   done
 fi
 if [[ $STEPS == *pmc* ]]; then
-  step pmc 900 tools/pmc.sh
+  PMC_BENCH_ARGS="--steps 2 --warmup 1 --arena-mib 256 --no-cpu-baseline --frames" step pmc 900 tools/pmc.sh
 fi
 echo all done | tee -a $O/steps.log
