@@ -211,6 +211,30 @@ def load_traffic(kernel):
         return None
 
 
+VALU_ISSUE_PEAK = 256 * 4 * 2.4e9 / 2  # wave64 VALU instr/s: 256 CUs x 4 SIMD32, 2 cycles each, 2.4 GHz
+
+
+def load_issue(kernel, launch_ms):
+    """The bound that actually limits the tokenizers: VALU issue.
+    Wave-instructions per launch from the committed PMC summary (SQ_INSTS_VALU /
+    SALU, same arena and config) over this run's HIP-event launch time."""
+    p = os.path.join(REPO, "profiles", "pmc_wordpiece.json")
+    try:
+        with open(p) as f:
+            c = json.load(f)["kernels"]["sdl::" + kernel]["counters"]
+    except Exception:
+        return None
+    valu, salu = c.get("SQ_INSTS_VALU"), c.get("SQ_INSTS_SALU")
+    if not valu:
+        return None
+    rate = valu / (launch_ms * 1e-3)
+    return {"bound": "valu_issue", "valu_wave_instr_per_launch": int(valu), "salu_wave_instr_per_launch": int(salu or 0),
+            "achieved_T_per_s": round(rate / 1e12, 4), "peak_T_per_s": round(VALU_ISSUE_PEAK / 1e12, 4),
+            "frac": round(rate / VALU_ISSUE_PEAK, 4),
+            "wait_frac": round(c["SQ_WAIT_ANY"] / c["SQ_WAVE_CYCLES"], 4) if c.get("SQ_WAVE_CYCLES") else None,
+            "source": "profiles/pmc_wordpiece.json (rocprofv3 --pmc, mlm 256 MiB)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -339,6 +363,7 @@ def main():
         "roofline": {"bound": "hbm", "kernel": task["kernel"], "achieved": round(achieved, 2),
                      "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 5),
                      "traffic": load_traffic(task["kernel"]) if args.task == "mlm" else None,
+                     "issue": load_issue(task["kernel"], tok_ms) if args.task == "mlm" else None,
                      "algorithmic_bytes_per_launch": tok_bytes, "avg_launch_ms": round(tok_ms, 4)},
         "stage_ms": {k: round(v, 4) for k, v in stage_ms.items()},
         "path_GBps": round(path_bytes / (step_ms * 1e-3) / 1e9, 2),
