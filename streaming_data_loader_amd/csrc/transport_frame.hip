@@ -76,9 +76,9 @@ __device__ __forceinline__ void lds_put_f64(uint8_t *L, uint32_t p, float f) {
 
 }  // namespace
 
-__global__ __launch_bounds__(64 * FRAME_WAVES) void k_frame_rows(FrameParams fp, uint32_t lds_stride) {
+__global__ __launch_bounds__(64 * FRAME_WAVES) void k_frame_rows(FrameParams fp, int plane0, uint32_t lds_stride) {
     extern __shared__ uint4 lds_raw[];
-    const FramePlane &P = fp.plane[blockIdx.y];
+    const FramePlane &P = fp.plane[plane0 + (int)blockIdx.y];
     const uint32_t rpw = P.rpw;
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     uint8_t *L = reinterpret_cast<uint8_t *>(lds_raw) + wv * lds_stride;
@@ -191,9 +191,7 @@ __global__ __launch_bounds__(64) void k_frame_skeleton(FrameParams fp) {
 
 hipError_t launch_frames(const FrameParams &fp, hipStream_t st) {
     if (fp.n_frames == 0) return hipSuccess;
-    FrameParams q = fp;  // one launch for all planes (blockIdx.y), LDS sized to the widest run
-    uint32_t stride = 16;
-    uint64_t max_waves = 0;
+    FrameParams q = fp;
     for (int p = 0; p < q.n_planes; ++p) {
         FramePlane &P = q.plane[p];
         const uint32_t w = P.width > 0 ? P.width : 1u;
@@ -204,19 +202,36 @@ hipError_t launch_frames(const FrameParams &fp, hipStream_t st) {
                 break;
             }
         if (P.flat) P.rpw = 1;
-        const uint32_t rb = P.row_bytes > P.row_bytes_last ? P.row_bytes : P.row_bytes_last;
-        const uint32_t st_p = (P.rpw * rb + 15u + 16u) & ~15u;
-        stride = st_p > stride ? st_p : stride;
-        const uint64_t waves = q.n_frames * ((P.rows_full + P.rpw - 1) / P.rpw);
-        max_waves = waves > max_waves ? waves : max_waves;
     }
-    const uint64_t nb = (max_waves + FRAME_WAVES - 1) / FRAME_WAVES;
-    if ((size_t)stride * FRAME_WAVES > 160u * 1024u) return hipErrorInvalidValue;
-    if (nb) {
-        hipLaunchKernelGGL(k_frame_rows, dim3((unsigned)nb, (unsigned)q.n_planes), dim3(64 * FRAME_WAVES),
-                           (size_t)stride * FRAME_WAVES, st, q, stride);
-        hipError_t e = hipGetLastError();
+    // the row-list planes in one launch (blockIdx.y), LDS sized to their widest run; a flat
+    // list (SingleClass `label`, B items in one run) in a launch of its own so its larger
+    // LDS run does not cut the occupancy of the others
+    auto launch = [&](int p0, int p1) -> hipError_t {
+        uint32_t stride = 16;
+        uint64_t max_waves = 0;
+        for (int p = p0; p < p1; ++p) {
+            const FramePlane &P = q.plane[p];
+            const uint32_t rb = P.row_bytes > P.row_bytes_last ? P.row_bytes : P.row_bytes_last;
+            const uint32_t st_p = (P.rpw * rb + 15u + 16u) & ~15u;
+            stride = st_p > stride ? st_p : stride;
+            const uint64_t waves = q.n_frames * ((P.rows_full + P.rpw - 1) / P.rpw);
+            max_waves = waves > max_waves ? waves : max_waves;
+        }
+        const uint64_t nb = (max_waves + FRAME_WAVES - 1) / FRAME_WAVES;
+        if ((size_t)stride * FRAME_WAVES > 160u * 1024u) return hipErrorInvalidValue;
+        if (!nb || p1 <= p0) return hipSuccess;
+        hipLaunchKernelGGL(k_frame_rows, dim3((unsigned)nb, (unsigned)(p1 - p0)), dim3(64 * FRAME_WAVES),
+                           (size_t)stride * FRAME_WAVES, st, q, p0, stride);
+        return hipGetLastError();
+    };
+    int p0 = 0;
+    while (p0 < q.n_planes) {
+        int p1 = p0 + 1;
+        if (!q.plane[p0].flat)
+            while (p1 < q.n_planes && !q.plane[p1].flat) ++p1;
+        hipError_t e = launch(p0, p1);
         if (e != hipSuccess) return e;
+        p0 = p1;
     }
     const uint64_t nt = fp.n_frames * (uint64_t)(fp.n_planes + 1);
     hipLaunchKernelGGL(k_frame_skeleton, dim3((unsigned)((nt + 63) / 64)), dim3(64), 0, st, fp);
