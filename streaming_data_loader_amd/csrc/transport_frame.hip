@@ -153,7 +153,9 @@ __global__ __launch_bounds__(64 * FRAME_WAVES) void k_frame_rows(FrameParams fp,
         for (uint32_t c = lane; c < nch; c += 64u) {
             const uint32_t lo = c * 16u, hi = lo + 16u;
             if (lo >= mis && hi <= end) {
-                *reinterpret_cast<uint4 *>(A + lo) = *reinterpret_cast<const uint4 *>(L + lo);
+                // frames stream out (read next by the D2H copy, not by this pass): non-temporal
+                typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+                __builtin_nontemporal_store(*reinterpret_cast<const v4u *>(L + lo), reinterpret_cast<v4u *>(A + lo));
             } else {
                 const uint32_t b0 = lo > mis ? lo : mis, b1 = hi < end ? hi : end;
                 for (uint32_t b = b0; b < b1; ++b) A[b] = L[b];
