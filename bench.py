@@ -13,8 +13,9 @@ shard of the global record stream (weak scaling, no data-path collective);
 the barrier and the max-over-ranks time reduction are the harness's only
 communication.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--task mlm|clm|multi-label]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--task mlm|span|clm|multi-label|single-class]
   torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU)
+  python bench.py --gpus N ...   (no launcher: starts the N ranks itself, launch_ranks)
 
 --task selects the other BASELINE configs (not the headline line):
   span         configs[2]: t5 Unigram, seq_len=512, batch=256, T5Data span
@@ -61,6 +62,16 @@ def log(msg):
 
 def fixture_records():
     with open(os.path.join(REPO, "tests", "golden", "test_records.jsonl"), encoding="utf-8") as f:
+        return [json.loads(l)["text"] for l in f]
+
+
+def corpus_records(corpus="fixture"):
+    """fixture: the reference's data/test.json.gz records; heldout: English
+    text never used to build or tune any table (tests/golden/heldout_records.jsonl,
+    tools/make_heldout.py)."""
+    if corpus == "fixture":
+        return fixture_records()
+    with open(os.path.join(REPO, "tests", "golden", "heldout_records.jsonl"), encoding="utf-8") as f:
         return [json.loads(l)["text"] for l in f]
 
 
@@ -198,50 +209,71 @@ def reference_engine_rate(task, records, order, seconds=6.0):
                       f"{dt:.1f} s (tokenization only)"}
 
 
-def load_traffic(kernel):
-    """HBM bytes per tokenize launch from the committed rocprofv3 PMC summary
-    (2 x FETCH_SIZE gfx950 correction + WRITE_SIZE, MI355X_MICROARCH.md §HBM)."""
-    p = os.path.join(REPO, "profiles", "pmc_wordpiece.json")
-    if not os.path.exists(p):
-        return None
-    try:
-        with open(p) as f:
-            return json.load(f)["kernels"].get("sdl::" + kernel, {}).get("hbm_bytes_per_launch")
-    except Exception:
-        return None
-
-
+PMC_DIR = os.path.join(REPO, "profiles", "pmc")
 VALU_ISSUE_PEAK = 256 * 4 * 2.4e9 / 2  # wave64 VALU instr/s: 256 CUs x 4 SIMD32, 2 cycles each, 2.4 GHz
 
 
-def load_issue(kernel, launch_ms):
-    """The bound that actually limits the tokenizers: VALU issue.
-    Wave-instructions per launch from the committed PMC summary (SQ_INSTS_VALU /
-    SALU, same arena and config) over this run's HIP-event launch time."""
-    p = os.path.join(REPO, "profiles", "pmc_wordpiece.json")
+def pmc_path(task, arena_mib):
+    return os.path.join(PMC_DIR, f"{task}_{arena_mib}mib.json")
+
+
+def load_pmc(task, arena_mib, kernel):
+    """The committed rocprofv3 --pmc summary of `kernel` (tools/pmc.sh +
+    tools/pmc_summary.py) for THIS task and arena size, or (None, reason).
+    Counters of another task or arena never describe the timed launch, so they
+    are not used."""
+    p = pmc_path(task, arena_mib)
+    if not os.path.exists(p):
+        return None, f"no PMC summary for task={task} arena={arena_mib} MiB ({os.path.relpath(p, REPO)})"
     try:
         with open(p) as f:
-            c = json.load(f)["kernels"]["sdl::" + kernel]["counters"]
-    except Exception:
-        return None
+            d = json.load(f)
+        if d.get("task") != task or int(d.get("arena_mib", -1)) != arena_mib:
+            return None, f"{os.path.relpath(p, REPO)} was collected for task={d.get('task')} arena={d.get('arena_mib')}"
+        k = d["kernels"]["sdl::" + kernel]
+        k["_file"] = os.path.relpath(p, REPO)
+        return k, None
+    except Exception as e:  # a malformed summary is reported, not used
+        return None, f"{os.path.relpath(p, REPO)}: {e}"
+
+
+def pmc_roofline(pmc, launch_ms, alg_bytes):
+    """traffic = HBM bytes per launch (2 x FETCH_SIZE gfx950 correction +
+    WRITE_SIZE, MI355X_MICROARCH.md §HBM); issue = VALU wave-instructions per
+    launch over this run's HIP-event launch time against the issue peak.
+    A figure that cannot describe the timed launch (issue above its peak) is
+    dropped with the reason."""
+    traffic = pmc.get("hbm_bytes_per_launch")
+    c = pmc["counters"]
     valu, salu = c.get("SQ_INSTS_VALU"), c.get("SQ_INSTS_SALU")
-    if not valu:
-        return None
-    rate = valu / (launch_ms * 1e-3)
-    return {"bound": "valu_issue", "valu_wave_instr_per_launch": int(valu), "salu_wave_instr_per_launch": int(salu or 0),
-            "achieved_T_per_s": round(rate / 1e12, 4), "peak_T_per_s": round(VALU_ISSUE_PEAK / 1e12, 4),
-            "frac": round(rate / VALU_ISSUE_PEAK, 4),
-            "wait_frac": round(c["SQ_WAIT_ANY"] / c["SQ_WAVE_CYCLES"], 4) if c.get("SQ_WAVE_CYCLES") else None,
-            "source": "profiles/pmc_wordpiece.json (rocprofv3 --pmc, mlm 256 MiB)"}
+    issue, note = None, None
+    if valu:
+        rate = valu / (launch_ms * 1e-3)
+        frac = rate / VALU_ISSUE_PEAK
+        if frac > 1.0:
+            note = f"PMC VALU count over this launch time gives issue frac {frac:.3f} > 1: not this launch"
+        else:
+            issue = {"bound": "valu_issue", "valu_wave_instr_per_launch": int(valu),
+                     "salu_wave_instr_per_launch": int(salu or 0),
+                     "achieved_T_per_s": round(rate / 1e12, 4), "peak_T_per_s": round(VALU_ISSUE_PEAK / 1e12, 4),
+                     "frac": round(frac, 4),
+                     "wait_frac": round(c["SQ_WAIT_ANY"] / c["SQ_WAVE_CYCLES"], 4) if c.get("SQ_WAVE_CYCLES") else None,
+                     "source": pmc["_file"]}
+    if traffic is not None and traffic < 0.9 * alg_bytes:
+        note = (note + "; " if note else "") + f"PMC traffic {traffic} B < algorithmic {alg_bytes} B"
+    return traffic, issue, note
 
 
-def main():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--task", default="mlm", choices=sorted(TASKS))
     ap.add_argument("--arena-mib", type=int, default=256)
+    ap.add_argument("--corpus", default="fixture", choices=["fixture", "heldout"],
+                    help="fixture: data/test.json.gz records tiled (default); heldout: English text on the image "
+                         "never used to build or tune the tables (tests/golden/heldout_records.jsonl)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--e2e", action="store_true", help="also time the host record path (H2D + kernels + D2H)")
     ap.add_argument("--json", action="store_true",
@@ -251,16 +283,144 @@ def main():
                          "tokenize+mask, transport frames, D2H (the provider -> batcher -> transport path)")
     ap.add_argument("--frames", action="store_true",
                     help="also time the Transport step on the device: every batch -> its serde_pickle frame")
-    args = ap.parse_args()
+    ap.add_argument("--spawn", action="store_true",
+                    help="start the ranks as child processes even for --gpus 1 (tests the launcher)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="harness check without a GPU: ranks, gloo barrier/max reduction and the JSON line, "
+                         "with a CPU checksum of the arena as the 'step' (never a measurement)")
+    return ap.parse_args(argv)
+
+
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n, argv):
+    """`--gpus N` without a launcher: start N ranks of this script as child
+    processes (one per GPU, RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* set), the way
+    torch.distributed.run would.  This parent never touches the GPU and never
+    re-execs; it forwards the children's output (rank 0 prints the JSON line)
+    and exits with the first non-zero child status."""
+    import subprocess
+    port = os.environ.get("MASTER_PORT") or str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR=os.environ.get("MASTER_ADDR", "127.0.0.1"), MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    rc = 0
+    for p in procs:
+        c = p.wait()
+        if c != 0 and rc == 0:
+            rc = c
+    if rc:  # a rank failed: do not leave its peers waiting in a barrier
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    return rc
+
+
+def rank_env():
+    return (int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def shard(rank, nbytes, corpus="fixture"):
+    """This rank's disjoint shard of the global record stream: its own seeded
+    arena of the corpus records and its global record indices (first_record),
+    so mask keys never collide across ranks."""
+    records = corpus_records(corpus)
+    arena, offs, order = build_arena(records, nbytes, seed=0x5D1B + rank)
+    return records, arena, offs, order, rank * 10_000_000
+
+
+def max_over_ranks(dt, world, device=None):
+    """The harness's only communication besides the barrier: the slowest rank's time."""
+    if world == 1:
+        return dt
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([dt], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def base_line(args, world, step_ms, value, task, N, R, rows, toks):
+    S, B = task["S"], task["B"]
+    return {
+        "metric": METRIC, "value": round(value, 2), "unit": "MB/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(step_ms, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "u8->int32",
+        "data": ("synthetic: data/test.json.gz records tiled (seeded)" if args.corpus == "fixture" else
+                 "synthetic: held-out English text on the image (never used for tuning) tiled (seeded)"),
+        "config": {"workload": f"{task['workload']}, one step = one rank's {args.arena_mib} MiB text arena -> "
+                               "all packed batches",
+                   "task": args.task, "seq_len": S, "batch": B, "corpus": args.corpus,
+                   "arena_bytes_per_gpu": N, "records_per_gpu": R,
+                   "rows_per_gpu": rows, "batches_per_gpu": -(-rows // B), "ids_per_gpu": toks,
+                   "tokenizer": {"gpt2": "gpt2 byte-level BPE layout, offline proxy vocab (50,257)",
+                                 "t5": "t5-small layout (Precompiled nmt_nfkc + Unigram), offline proxy vocab (32,100)"}
+                                .get(task["tok"], "bert-base-uncased layout, offline proxy vocab (30,522)"),
+                   "parallelism": f"record shards x{world}, no collective"},
+    }
+
+
+def dry_run(args, world, rank):
+    """--dry-run: the multi-rank harness on the CPU (gloo): shard, barrier,
+    timed 'steps' (a numpy checksum of the arena, NOT the product), max over
+    ranks, rank 0's JSON line.  Exercises launch_ranks in CPU tests."""
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    records, arena, offs, order, first = shard(rank, args.arena_mib << 20, args.corpus)
+    N, R = len(arena) - 16, len(order)
+    sums = []
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        sums.append(int(arena[:N].sum(dtype=np.uint64)))
+    if world > 1:
+        dist.barrier()
+    dt = max_over_ranks(time.perf_counter() - t0, world)
+    meta = [None] * world
+    if world > 1:
+        dist.all_gather_object(meta, (rank, first, R, N, sums[-1]))
+    else:
+        meta = [(rank, first, R, N, sums[-1])]
+    task = TASKS[args.task]
+    if rank == 0:
+        line = base_line(args, world, dt / args.steps * 1e3, N * world * args.steps / dt / 1e6, task, N, R, 0, 0)
+        line["data"] = "DRY RUN: CPU checksum of the arena, no GPU -- not a measurement"
+        line["ranks"] = [{"rank": m[0], "first_record": m[1], "records": m[2], "bytes": m[3], "checksum": m[4]}
+                         for m in meta]
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse_args(argv)
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and (args.gpus > 1 or args.spawn):
+        sys.exit(launch_ranks(args.gpus, [a for a in argv if a != "--spawn"]))
+    if env_world is not None and int(env_world) != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={env_world}: launch one rank per GPU with "
+              f"--nproc-per-node equal to --gpus", file=sys.stderr)
+        sys.exit(2)
+    world, rank, local = rank_env()
+    if args.dry_run:
+        return dry_run(args, world, rank)
     task = TASKS[args.task]
     S, B = task["S"], task["B"]
 
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -271,10 +431,10 @@ def main():
 
     if not os.path.exists(build.LIB):
         build.build()
-    records = fixture_records()
-    arena, offs, order = build_arena(records, args.arena_mib << 20, seed=0x5D1B + rank)
+    records, arena, offs, order, first_record = shard(rank, args.arena_mib << 20, args.corpus)
     N, R = len(arena) - 16, len(order)
-    log(f"rank {rank}: task {args.task}, arena {N} bytes, {R} records")
+    log(f"rank {rank}/{world}: task {args.task}, corpus {args.corpus}, arena {N} bytes, {R} records, "
+        f"first record {first_record}")
     text = torch.from_numpy(arena).to(dev)
     offsets = torch.from_numpy(offs.astype(np.int64)).to(dev)
     stream = torch.cuda.Stream(device=dev)
@@ -284,7 +444,6 @@ def main():
                                                                                           native.BERT_PROXY_TOKENIZER)
     db = DeviceBatcher(task=kind[args.task], batch_size=B, sequence_length=S, seed=1234, device=local,
                        tokenizer=tok_path)
-    first_record = rank * 10_000_000  # disjoint global record indices per shard
     if args.task == "single-class":  # Label::Single: record i's label is i & 1 (imdb: 2 classes)
         t_lab = torch.from_numpy((np.asarray(order, np.int64) & 1).astype(np.int32)).to(dev)
         t_loff = torch.arange(R + 1, dtype=torch.int64, device=dev)
@@ -332,10 +491,14 @@ def main():
     dt = time.perf_counter() - t0
     log(f"timed {args.steps} steps in {dt:.3f} s")
     db.set_profiling(False)
-    if world > 1:
-        t = torch.tensor([dt], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+    dt = max_over_ranks(dt, world, dev)
+
+    # capacity flags: a run that dropped text or clamped labels is not a measurement
+    tok_err, lab_err = res.tokenize_errors(), res.label_errors()
+    if tok_err or lab_err:
+        print(f"bench.py: rank {rank}: tokenize_errors={tok_err:#x} label_errors={lab_err} -- the timed run "
+              "dropped or clamped data (include/sdl_batcher.h d_tokenize_errors / d_label_errors)", file=sys.stderr)
+        sys.exit(3)
 
     rows, toks = res.rows(), res.tokens()
     stage_ms = {k: v / args.steps for k, v in stage_sum.items()}
@@ -348,26 +511,21 @@ def main():
     achieved = tok_bytes / (tok_ms * 1e-3) / 1e9
     # whole path, per step: text + offsets + the int32 [rows, S] planes
     path_bytes = N + 8 * (R + 1) + int(4 * task["planes"] * rows * S)
-    line = {
-        "metric": METRIC, "value": round(value, 2), "unit": "MB/s", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": round(step_ms, 4), "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "u8->int32", "data": "synthetic: data/test.json.gz records tiled (seeded)",
-        "config": {"workload": f"{task['workload']}, one step = one rank's {args.arena_mib} MiB text arena -> "
-                               "all packed batches",
-                   "task": args.task, "seq_len": S, "batch": B, "arena_bytes_per_gpu": N, "records_per_gpu": R,
-                   "rows_per_gpu": rows, "batches_per_gpu": -(-rows // B), "ids_per_gpu": toks,
-                   "tokenizer": {"gpt2": "gpt2 byte-level BPE layout, offline proxy vocab (50,257)",
-                                 "t5": "t5-small layout (Precompiled nmt_nfkc + Unigram), offline proxy vocab (32,100)"}
-                                .get(task["tok"], "bert-base-uncased layout, offline proxy vocab (30,522)"),
-                   "parallelism": f"record shards x{world}, no collective"},
-        "roofline": {"bound": "hbm", "kernel": task["kernel"], "achieved": round(achieved, 2),
-                     "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 5),
-                     "traffic": load_traffic(task["kernel"]) if args.task == "mlm" else None,
-                     "issue": load_issue(task["kernel"], tok_ms) if args.task == "mlm" else None,
-                     "algorithmic_bytes_per_launch": tok_bytes, "avg_launch_ms": round(tok_ms, 4)},
-        "stage_ms": {k: round(v, 4) for k, v in stage_ms.items()},
-        "path_GBps": round(path_bytes / (step_ms * 1e-3) / 1e9, 2),
-    }
+    line = base_line(args, world, step_ms, value, task, N, R, rows, toks)
+    pmc, pmc_note = load_pmc(args.task, args.arena_mib, task["kernel"]) if args.corpus == "fixture" else \
+        (None, "PMC summaries are collected on the fixture corpus")
+    traffic, issue = None, None
+    if pmc is not None:
+        traffic, issue, pmc_note = pmc_roofline(pmc, tok_ms, tok_bytes)
+    line["roofline"] = {"bound": "hbm", "kernel": task["kernel"], "achieved": round(achieved, 2),
+                        "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 5),
+                        "traffic": traffic, "issue": issue,
+                        "algorithmic_bytes_per_launch": tok_bytes, "avg_launch_ms": round(tok_ms, 4)}
+    if pmc_note:
+        line["roofline"]["pmc_note"] = pmc_note
+    line["stage_ms"] = {k: round(v, 4) for k, v in stage_ms.items()}
+    line["path_GBps"] = round(path_bytes / (step_ms * 1e-3) / 1e9, 2)
+    line["errors"] = {"tokenize": tok_err, "label": lab_err}
     log(f"stages {stage_ms}")
     if args.e2e and rank == 0:
         line["end_to_end"] = end_to_end(args.task, records, order)
@@ -586,7 +744,53 @@ def end_to_end(task, records, order, nbytes=64 << 20, reps=2):
         res["from_arena"] = {"MBps": round(done / best_a / 1e6, 2), "ms": round(best_a * 1e3, 2),
                              "path": "host arena + offsets -> sdl_batcher_push_many + sdl_batcher_next "
                                      "(pinned H2D, kernels, D2H of all rows, host batch queue)"}
+        res["channel"] = channel_rates(task, cfg, texts)
     return res
+
+
+def channel_rates(task, cfg, texts, per_record_seconds=3.0):
+    """The reference plug-in point (batcher::create_batch, batcher.rs:33-77) fed
+    a ProviderChannel stream of the same records: (i) the per-record loop --
+    one sdl_batcher_push (a device round trip) per Data message, timed on a
+    bounded sample; (ii) create_batch_drained -- every waiting Data message in
+    one sdl_batcher_push_many.  Both emit the identical Data sequence
+    (tests/test_gpu_drop_in.py)."""
+    import queue
+    from streaming_data_loader_amd import batcher as Bt
+
+    def stream(recs):
+        rx = queue.Queue()
+        rx.put(Bt.ProviderChannel.Info("bench"))
+        for t in recs:
+            rx.put(Bt.ProviderChannel.Data(t))
+        rx.put(Bt.ProviderChannel.Complete())
+        return rx
+
+    # (i) per record, bounded: records until per_record_seconds have passed
+    gt = Bt.GenTokenizer.from_config(cfg)
+    gt.create_sync_batch(texts[0])  # warm
+    n = done = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < per_record_seconds and n < len(texts):
+        gt.create_sync_batch(texts[n])
+        done += len(texts[n].encode("utf-8"))
+        n += 1
+    dt1 = time.perf_counter() - t0
+    # (ii) drained: the whole stream waiting in the channel
+    total = sum(len(t.encode("utf-8")) for t in texts)
+    best = None
+    for _ in range(2):
+        gt2 = Bt.GenTokenizer.from_config(cfg)
+        rx, tx = stream(texts), queue.Queue()
+        t0 = time.perf_counter()
+        Bt.create_batch_drained(rx, tx, gt2)
+        dt = time.perf_counter() - t0
+        best = dt if best is None else min(best, dt)
+        del tx
+    return {"per_record": {"MBps": round(done / dt1 / 1e6, 3), "records": n, "us_per_record": round(dt1 / n * 1e6, 1),
+                           "path": "create_batch: one sdl_batcher_push per ProviderChannel::Data"},
+            "drained": {"MBps": round(total / best / 1e6, 2), "records": len(texts), "ms": round(best * 1e3, 2),
+                        "path": "create_batch_drained: waiting Data messages -> one sdl_batcher_push_many"}}
 
 
 if __name__ == "__main__":

@@ -8,5 +8,6 @@ package is the Python host mirror of the reference's Batcher interface.
 from .batcher import (Batcher, BatchConfig, DataSet, GenTokenizer, Gpt, Label, Mask, ModelType,  # noqa: F401
                       MultiLabel, ProviderChannel, SimpleBatcher, SimpleData, SimpleTransport, SingleClass, Span,
                       TaskType,
-                      TokenizerConfig, TrainingConfig, create_batch, get_case, get_mask_length)
+                      TokenizerConfig, TrainingConfig, create_batch, create_batch_drained, get_case,
+                      get_mask_length)
 from .native import SDLError  # noqa: F401

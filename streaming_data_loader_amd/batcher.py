@@ -398,3 +398,63 @@ def create_batch(rx, tx, batcher: Batcher):
             batch = batcher.create_sync_batch(msg.value)
             if batch is not None:
                 tx.put(ProviderChannel.Data(batch))
+
+
+def _record_bytes(x):
+    if isinstance(x, SimpleTransport):
+        x = x.data.text
+    return len(x) if isinstance(x, (bytes, bytearray)) else len(x) * 4 if isinstance(x, str) else 0
+
+
+_NOTHING = object()
+
+
+def create_batch_drained(rx, tx, batcher: _NativeBatcher, max_bytes: int = 64 << 20, max_records: int = 1 << 20):
+    """batcher::create_batch (batcher.rs:33-77) for the GPU Batcher: every
+    ProviderChannel::Data already waiting in `rx` (up to max_bytes of text /
+    max_records) is drained and handed to the device in ONE
+    sdl_batcher_push_many call, instead of one device round trip per record.
+
+    The Data sequence sent to `tx` is the per-record loop's, message for
+    message: push_many queues exactly the batches the same sequence of
+    create_sync_batch calls would emit (at most one per record, in order, the
+    handle keeping GenTokenizer's/SimpleBatcher's queue across calls), they
+    are sent before the message that ended the drain, Info passes through in
+    stream order, and Complete flushes one get_working_batch() then forwards
+    Complete.  rx needs get() (blocking) and get_nowait() (raising
+    queue.Empty); a None message ends the loop like a closed channel."""
+    import queue
+    pending, size = [], 0
+
+    def flush():
+        nonlocal pending, size
+        if pending:
+            for ds in batcher.create_sync_batches(pending):
+                tx.put(ProviderChannel.Data(ds))
+        pending, size = [], 0
+
+    while True:
+        msg = rx.get()
+        # drain what is already waiting (never block with records pending)
+        while isinstance(msg, ProviderChannel.Data):
+            pending.append(msg.value)
+            size += _record_bytes(msg.value)
+            if size >= max_bytes or len(pending) >= max_records:
+                flush()
+            try:
+                msg = rx.get_nowait()
+            except queue.Empty:
+                msg = _NOTHING
+        flush()
+        if msg is _NOTHING:
+            continue
+        if msg is None:
+            break
+        if isinstance(msg, ProviderChannel.Info):
+            tx.put(msg)
+        elif isinstance(msg, ProviderChannel.Complete) or msg is ProviderChannel.Complete:
+            cur = batcher.get_working_batch()
+            if cur is not None:
+                tx.put(ProviderChannel.Data(cur))
+            tx.put(ProviderChannel.Complete())
+            break

@@ -30,9 +30,8 @@ def shard_rows(rank, nbytes=48 << 10, S=128, B=8):
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import bench
     import oracle_lib
-    recs = bench.fixture_records()
-    arena, offs, order = bench.build_arena(recs, nbytes, seed=0x5D1B + rank)
-    first = rank * 10_000_000
+    # bench.shard is the rank logic bench.py runs: this rank's arena and record indices
+    _, arena, offs, order, first = bench.shard(rank, nbytes)
     texts = [bytes(arena[int(offs[i]):int(offs[i + 1])]) for i in range(len(order))]
     rows = oracle_lib.oracle_rows(oracle_lib.Tok(), texts, S, int(np.float32(S) * np.float32(0.15)), seed=1234, B=B,
                                   first_record=first)
@@ -43,11 +42,11 @@ def _worker(rank, world, port, out):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     import torch
+    import bench
     texts, first, rows = shard_rows(rank)
-    # the harness: barrier, per-rank time, max over ranks
+    # the harness: barrier, per-rank time, bench's max over ranks
     dist.barrier()
-    t = torch.tensor([1.0 + rank], dtype=torch.float64)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    t = torch.tensor([bench.max_over_ranks(1.0 + rank, world)], dtype=torch.float64)
     meta = [None] * world
     dist.all_gather_object(meta, (first, len(texts), int(rows.shape[1]), int(np.int64(rows.sum()))))
     if rank == 0:
@@ -102,3 +101,36 @@ def test_shard_rows_are_the_whole_streams_rows():
     whole = np.concatenate(planes, axis=1)
     n1 = rows1.shape[1]
     np.testing.assert_array_equal(whole[:, -n1:], rows1)
+
+
+def test_bench_gpus_flag_launches_ranks():
+    """`bench.py --gpus 2` without a launcher starts 2 ranks itself (RANK /
+    WORLD_SIZE / MASTER_* set per child, no GPU touched in the parent): the
+    dry run exercises the same launcher, gloo barrier and max reduction, and
+    rank 0's line reports n_gpus == 2 with disjoint shards."""
+    import json
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--dry-run", "--gpus", "2", "--steps", "2",
+                        "--arena-mib", "2"], capture_output=True, text=True, timeout=240, env=env)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1  # only rank 0 prints
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["scaling"] == "weak"
+    r0, r1 = d["ranks"]
+    assert (r0["first_record"], r1["first_record"]) == (0, 10_000_000)
+    assert r0["checksum"] != r1["checksum"]  # different seeded shards
+    total = r0["bytes"] + r1["bytes"]
+    assert abs(d["value"] - d["config"]["arena_bytes_per_gpu"] * 2 / d["ms_per_step"] / 1e3) / d["value"] < 0.01
+    assert total > 0
+
+
+def test_bench_gpus_disagreeing_with_world_size_fails():
+    import subprocess
+    import sys
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--dry-run", "--gpus", "1"],
+                       capture_output=True, text=True, timeout=120, env=env)
+    assert p.returncode == 2 and "WORLD_SIZE" in p.stderr

@@ -3,16 +3,19 @@
 # kernel-trace/stats only -- no sys/runtime trace with --pmc).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-mkdir -p gpurun_out/pmc
+TASK="${1:-mlm}"
+ARENA="${2:-256}"
+D=gpurun_out/pmc_${TASK}_${ARENA}
+mkdir -p $D
 export TMPDIR=/tmp
-ARGS="${PMC_BENCH_ARGS:---steps 2 --warmup 1 --arena-mib 256 --no-cpu-baseline}"
+ARGS="--task $TASK --steps 2 --warmup 1 --arena-mib $ARENA --no-cpu-baseline"
 i=0
 while IFS= read -r group; do
   [[ -z "$group" ]] && continue
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $group --kernel-trace --output-format csv -d gpurun_out/pmc/p$i -o run -- python3 bench.py $ARGS > gpurun_out/pmc/p$i.out 2> gpurun_out/pmc/p$i.err
+  timeout -k 10 240 rocprofv3 --pmc $group --kernel-trace --output-format csv -d $D/p$i -o run -- python3 bench.py $ARGS > $D/p$i.out 2> $D/p$i.err
   rc=$?
-  echo "pass $i [$group] exit $rc" | tee -a gpurun_out/pmc/passes.log
+  echo "pass $i [$group] exit $rc" | tee -a $D/passes.log
   case $rc in 0) ;; *) exit $rc;; esac
 done <<'GROUPS'
 FETCH_SIZE
@@ -21,4 +24,3 @@ SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM
 SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM
 GRBM_GUI_ACTIVE SQ_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_INSTS_FLAT
 GROUPS
-timeout -k 10 120 rocprofv3 -L > gpurun_out/pmc/counters_list.txt 2>&1 || true

@@ -1,11 +1,12 @@
 #!/usr/bin/env python3
-"""Summarise rocprofv3 --pmc passes (tools/pmc.sh) into profiles/pmc_wordpiece.json.
+"""Summarise rocprofv3 --pmc passes (tools/pmc.sh) into profiles/pmc/<task>_<arena>mib.json
+(bench.py reads it only for the same task and arena size).
 
 HBM bytes per launch = 2 x FETCH_SIZE + WRITE_SIZE (KiB units), the gfx950
 FETCH_SIZE correction of MI355X_MICROARCH.md §HBM (FETCH_SIZE reports half the
 bytes of a 16 B/lane streaming read).  Averaged over every launch of a kernel.
 
-    python tools/pmc_summary.py gpurun_out/pmc [profiles/pmc_wordpiece.json]
+    python tools/pmc_summary.py gpurun_out/pmc TASK ARENA_MIB
 """
 import csv
 import glob
@@ -21,7 +22,10 @@ def short(name):
 
 def main():
     src = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
-    dst = sys.argv[2] if len(sys.argv) > 2 else "profiles/pmc_wordpiece.json"
+    task = sys.argv[2] if len(sys.argv) > 2 else "mlm"
+    arena = int(sys.argv[3]) if len(sys.argv) > 3 else 256
+    os.makedirs("profiles/pmc", exist_ok=True)
+    dst = f"profiles/pmc/{task}_{arena}mib.json"
     vals = defaultdict(lambda: defaultdict(list))  # kernel -> counter -> per-dispatch values
     for f in sorted(glob.glob(os.path.join(src, "**", "*counter_collection.csv"), recursive=True)):
         per = defaultdict(float)
@@ -33,16 +37,14 @@ def main():
                 names[row["Dispatch_Id"]] = short(row["Kernel_Name"])
         for (d, c), v in per.items():
             vals[names[d]][c].append(v)
-    out = {"source": "rocprofv3 --pmc passes of bench.py (tools/pmc.sh)", "kernels": {}}
+    out = {"source": f"rocprofv3 --pmc passes of bench.py --task {task} --arena-mib {arena} (tools/pmc.sh)",
+           "task": task, "arena_mib": arena, "kernels": {}}
     for k, cs in vals.items():
         avg = {c: sum(v) / len(v) for c, v in cs.items()}
         ent = {"launches": max(len(v) for v in cs.values()), "counters": avg}
         if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
             ent["hbm_bytes_per_launch"] = int((2 * avg["FETCH_SIZE"] + avg["WRITE_SIZE"]) * 1024)
         out["kernels"][k] = ent
-    wp = out["kernels"].get("sdl::k_wordpiece_chunks", {})
-    out["kernel"] = "sdl::k_wordpiece_chunks"
-    out["hbm_bytes_per_launch"] = wp.get("hbm_bytes_per_launch")
     with open(dst, "w") as fh:
         json.dump(out, fh, indent=1)
     print(json.dumps({k: v.get("hbm_bytes_per_launch") for k, v in out["kernels"].items()}, indent=1))
