@@ -26,7 +26,10 @@ constexpr int STAGE = CHUNK + 128;                // token slots per chunk (>= t
 #define SDL_TOK_UNROLL 2
 #endif
 constexpr int TOK_UNROLL = SDL_TOK_UNROLL;        // first probes in flight per lane (2: no spills at 5 waves/SIMD)
-constexpr int PEND_CAP = 512;                     // WordPiece pieces pending the state machine (LDS)
+#ifndef SDL_PEND_CAP
+#define SDL_PEND_CAP 256
+#endif
+constexpr int PEND_CAP = SDL_PEND_CAP;            // WordPiece pieces pending the state machine (LDS)
 constexpr int RB_CAP = 256;                       // record starts listed in LDS per window
 constexpr int MAX_WORD_CHARS = 100;               // WordPiece max_input_chars_per_word
 constexpr int MAX_WORD_BYTES = 4 * MAX_WORD_CHARS + 8;

@@ -13,10 +13,10 @@ namespace sdl {
 hipError_t launch_chunk_ranges(const uint64_t *off, int64_t R, int64_t N, uint32_t *ranges, hipStream_t st);
 
 // tokenize_wordpiece.hip: text arena -> per-chunk token lists + boundary offsets
-// (after launch_chunk_ranges).
+// (after launch_chunk_ranges), for chunks [c_begin, c_end) (c_end < 0: all).
 hipError_t launch_wordpiece_chunks(const DevTok &T, const uint8_t *text, int64_t N, const uint64_t *off, int64_t R,
                                    uint32_t *ranges, uint32_t *tokc, uint32_t *chunk_cnt, uint32_t *rec_local,
-                                   hipStream_t st);
+                                   hipStream_t st, int64_t c_begin = 0, int64_t c_end = -1);
 
 // tokenize_bpe.hip: same outputs for a byte-level BPE (gpt2) tokenizer.  Pieces
 // longer than 64 bytes go through `long_list` (capacity long_cap) and are
@@ -72,10 +72,25 @@ hipError_t launch_json_write(const uint8_t *buf, int64_t n_lines, const uint32_t
                              hipStream_t st);
 
 // pipeline.hip
-// out[0..n) = exclusive prefix sum of in[0..n), out[n] = total.  tmp needs
-// scan_tmp_words(n) words.
+// out[0..n) = exclusive prefix sum of in[0..n) (+ *carry_in when given),
+// out[n] = total.  tmp needs scan_tmp_words(n) words.  carry_in may alias out[0].
 int64_t scan_tmp_words(int64_t n);
-hipError_t launch_exclusive_scan(const uint32_t *in, uint32_t *out, int64_t n, uint32_t *tmp, hipStream_t st);
+hipError_t launch_exclusive_scan(const uint32_t *in, uint32_t *out, int64_t n, uint32_t *tmp, hipStream_t st,
+                                 const uint32_t *carry_in = nullptr);
+
+// Pipelined segments: the arena's chunks are cut into K host-known ranges
+// [cb[k], cb[k+1]); record range k is [rb[k], rb[k+1]) -- the records whose ids
+// all lie in chunks < cb[k+1] (rb[K] = R) -- computed on the device from the
+// chunk ranges, so nothing syncs with the host.
+constexpr int MAX_SEGMENTS = 16;
+struct SegChunks {
+    int64_t cb[MAX_SEGMENTS + 1];
+    int K;
+};
+hipError_t launch_seg_bounds(const uint32_t *ranges, const SegChunks &sc, int64_t R, uint32_t *rb, hipStream_t st);
+// out[rb[k] .. rb[k+1]] = exclusive scan of in[rb[k] .. rb[k+1]) carried from out[rb[k]]
+// (0 for k == 0); one workgroup.
+hipError_t launch_scan_range(const uint32_t *in, uint32_t *out, const uint32_t *rb, int k, hipStream_t st);
 
 // long_count == null: no long-piece markers (WordPiece).  Else chunk_ent holds
 // each chunk's entry count (markers count 1; chunk_cnt counts ids).
@@ -86,10 +101,19 @@ hipError_t launch_compact_tokens(const uint32_t *tokc, const uint32_t *chunk_cnt
                                  hipStream_t st, const uint32_t *long_pool = nullptr, int64_t stride = STAGE);
 
 
+// Which records / rows a launch covers: records [rb[k], rb[k+1]), rows
+// [row_off[rb[k]], row_off[rb[k+1]]); the last segment (last != 0) also writes
+// the initial values of the rows up to the next multiple of B.
+struct SegSel {
+    const uint32_t *rb;
+    int k;
+    int last;
+};
+
 // per record: token offset, token count, rows it yields (gen_batcher.rs:69-94)
 hipError_t launch_records(const RowParams &P, const uint64_t *off, int64_t R, int64_t N, const uint32_t *chunk_off,
                           int64_t n_chunks, const uint32_t *rec_local, uint32_t *rec_tok, uint32_t *rec_cnt,
-                          uint32_t *rec_rows, hipStream_t st);
+                          uint32_t *rec_rows, SegSel sel, hipStream_t st);
 
 struct RowOut {
     int32_t *input_ids, *attention_mask, *token_type_ids, *labels;
@@ -97,7 +121,7 @@ struct RowOut {
 };
 
 // row -> record map (row_rec needs one word per row)
-hipError_t launch_row_map(const uint32_t *row_off, int64_t R, uint32_t *row_rec, hipStream_t st);
+hipError_t launch_row_map(const uint32_t *row_off, int64_t R, uint32_t *row_rec, SegSel sel, hipStream_t st);
 
 // BertData::put_data + mask_batch for every row (models/bert_data.rs:40-89)
 // pipeline.hip: device rows -> finished batches in pinned host memory (the
@@ -112,22 +136,22 @@ hipError_t launch_rows_to_host(const RowSeg *segs, int n_segs, uint32_t rows_per
                                hipStream_t st);
 
 hipError_t launch_rows(const RowParams &P, const uint32_t *tok, const uint32_t *rec_tok, const uint32_t *rec_cnt,
-                       const uint32_t *row_off, const uint32_t *row_rec, const uint32_t *d_rows, int64_t rows_cap,
-                       RowOut out, hipStream_t st);
+                       const uint32_t *row_off, const uint32_t *row_rec, SegSel sel, int64_t rows_cap, RowOut out,
+                       hipStream_t st);
 
 // BertData MultiLabel labels_f32 plane (bert_data.rs:66-78)
 hipError_t launch_multi_labels(const uint32_t *labels, const uint64_t *label_off, const uint32_t *row_rec,
-                               const uint32_t *d_rows, int64_t rows_cap, int B, int NL, float *out, uint32_t *err,
-                               hipStream_t st);
+                               const uint32_t *row_off, SegSel sel, int64_t rows_cap, int B, int NL, float *out,
+                               uint32_t *err, hipStream_t st);
 
 // T5Data::put_data rows for task=span (models/t5_data.rs:162-226)
 hipError_t launch_rows_span(const RowParams &P, const uint32_t *tok, const uint32_t *rec_tok, const uint32_t *rec_cnt,
-                            const uint32_t *row_off, const uint32_t *row_rec, const uint32_t *d_rows, int64_t rows_cap,
+                            const uint32_t *row_off, const uint32_t *row_rec, SegSel sel, int64_t rows_cap,
                             RowOut out, uint32_t *err, hipStream_t st);
 
 hipError_t launch_single_labels(const uint32_t *labels, const uint64_t *label_off, const uint32_t *row_rec,
-                                const uint32_t *d_rows, int64_t rows_cap, int B, int32_t *out, uint32_t *err,
-                                hipStream_t st);
+                                const uint32_t *row_off, SegSel sel, int64_t rows_cap, int B, int32_t *out,
+                                uint32_t *err, hipStream_t st);
 
 // transport_frame.hip: the Transport's serde_pickle frames of finished batches
 // (zmq_transmit.rs:71) written straight from the device row planes.

@@ -36,9 +36,10 @@ __global__ __launch_bounds__(SCAN_NT) void k_scan_reduce(const uint32_t *__restr
     if (threadIdx.x == 0) sums[blockIdx.x] = tot;
 }
 
-__global__ __launch_bounds__(SCAN_NT) void k_scan_sums(uint32_t *__restrict__ sums, int64_t nb) {
+__global__ __launch_bounds__(SCAN_NT) void k_scan_sums(uint32_t *__restrict__ sums, int64_t nb,
+                                                       const uint32_t *carry_in) {
     __shared__ uint32_t scratch[SCAN_NT / 64];
-    uint32_t carry = 0;
+    uint32_t carry = carry_in ? *carry_in : 0u;
     for (int64_t t0 = 0; t0 < nb; t0 += SCAN_TILE) {
         const int64_t base = t0 + (int64_t)threadIdx.x * SCAN_PER;
         uint32_t v[SCAN_PER], s = 0;
@@ -82,13 +83,90 @@ __global__ __launch_bounds__(SCAN_NT) void k_scan_apply(const uint32_t *__restri
 
 int64_t scan_tmp_words(int64_t n) { return (n + SCAN_TILE - 1) / SCAN_TILE + 1; }
 
-hipError_t launch_exclusive_scan(const uint32_t *in, uint32_t *out, int64_t n, uint32_t *tmp, hipStream_t st) {
-    if (n <= 0) return hipMemsetAsync(out, 0, sizeof(uint32_t), st);
+hipError_t launch_exclusive_scan(const uint32_t *in, uint32_t *out, int64_t n, uint32_t *tmp, hipStream_t st,
+                                 const uint32_t *carry_in) {
+    if (n <= 0) return carry_in ? hipSuccess : hipMemsetAsync(out, 0, sizeof(uint32_t), st);
     const int64_t nb = (n + SCAN_TILE - 1) / SCAN_TILE;
     hipLaunchKernelGGL(k_scan_reduce, dim3((unsigned)nb), dim3(SCAN_NT), 0, st, in, n, tmp);
-    hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(SCAN_NT), 0, st, tmp, nb);
+    hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(SCAN_NT), 0, st, tmp, nb, carry_in);
     hipLaunchKernelGGL(k_scan_apply, dim3((unsigned)nb), dim3(SCAN_NT), 0, st, in, n, tmp, nb, out);
     return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Pipelined segments (kernels.hpp SegChunks): rb[k] = first record whose ids
+// are not all in chunks < cb[k], i.e. (first r with off[r] >= cb[k] * CHUNK) - 1
+// = ranges[3 cb[k] + 2] - 1; rb[0] = 0, rb[K] = R.
+__global__ void k_seg_bounds(const uint32_t *__restrict__ ranges, SegChunks sc, int64_t R, uint32_t *__restrict__ rb) {
+    const int k = (int)threadIdx.x;
+    if (k > sc.K) return;
+    uint32_t v;
+    if (k == 0) v = 0;
+    else if (k == sc.K) v = (uint32_t)R;
+    else {
+        const uint32_t q = ranges[3 * sc.cb[k] + 2];
+        v = q == 0 ? 0u : q - 1u;
+        if (v > (uint32_t)R) v = (uint32_t)R;
+    }
+    rb[k] = v;
+}
+
+hipError_t launch_seg_bounds(const uint32_t *ranges, const SegChunks &sc, int64_t R, uint32_t *rb, hipStream_t st) {
+    hipLaunchKernelGGL(k_seg_bounds, dim3(1), dim3(64), 0, st, ranges, sc, R, rb);
+    return hipGetLastError();
+}
+
+// Exclusive scan of in[a, b) into out[a, b] (out[b] = total), carried from
+// out[a] when k > 0 (the previous segment wrote its total there); one
+// workgroup of 1024 threads, 8 elements per thread per tile.
+constexpr int RSCAN_NT = 1024, RSCAN_PER = 8;
+__global__ __launch_bounds__(RSCAN_NT) void k_scan_range(const uint32_t *__restrict__ in, uint32_t *__restrict__ out,
+                                                         const uint32_t *__restrict__ rb, int k) {
+    __shared__ uint32_t scratch[RSCAN_NT / 64];
+    const int64_t a = rb[k], b = rb[k + 1];
+    uint32_t carry = k > 0 ? out[a] : 0u;
+    __syncthreads();  // every thread has read out[a] before it is rewritten
+    for (int64_t t0 = a; t0 < b; t0 += (int64_t)RSCAN_NT * RSCAN_PER) {
+        const int64_t base = t0 + (int64_t)threadIdx.x * RSCAN_PER;
+        uint32_t v[RSCAN_PER], sum = 0;
+#pragma unroll
+        for (int j = 0; j < RSCAN_PER; ++j) {
+            v[j] = base + j < b ? in[base + j] : 0u;
+            sum += v[j];
+        }
+        uint32_t tot;
+        uint32_t ex = block_excl_sum<RSCAN_NT>(sum, &tot, scratch) + carry;
+#pragma unroll
+        for (int j = 0; j < RSCAN_PER; ++j) {
+            if (base + j < b) out[base + j] = ex;
+            ex += v[j];
+        }
+        carry += tot;
+    }
+    if (threadIdx.x == 0) out[b] = carry;
+}
+
+hipError_t launch_scan_range(const uint32_t *in, uint32_t *out, const uint32_t *rb, int k, hipStream_t st) {
+    hipLaunchKernelGGL(k_scan_range, dim3(1), dim3(RSCAN_NT), 0, st, in, out, rb, k);
+    return hipGetLastError();
+}
+
+// Rows [g_lo, g_end) of a launch; rows >= g_real are the last batch's padding.
+struct RowSpan {
+    int64_t g_lo, g_real, g_end;
+};
+__device__ __forceinline__ RowSpan row_span(const SegSel &s, const uint32_t *row_off, int B, int64_t rows_cap) {
+    const uint32_t r0 = s.rb[s.k], r1 = s.rb[s.k + 1];
+    RowSpan x;
+    x.g_lo = row_off[r0];
+    x.g_real = row_off[r1];
+    x.g_end = x.g_real;
+    if (s.last) {
+        int64_t Gpad = (x.g_real + B - 1) / B * B;
+        if (Gpad > rows_cap) Gpad = rows_cap;
+        x.g_end = Gpad > x.g_real ? Gpad : x.g_real;
+    }
+    return x;
 }
 
 // ---------------------------------------------------------------------------
@@ -140,7 +218,9 @@ __global__ __launch_bounds__(256) void k_compact_tokens(const uint32_t *__restri
     if (!long_count || *long_count == 0) {
         // 16-B loads of the (16-B aligned) chunk list, 4 dword stores per lane
         for (uint32_t i = 4 * lane; i < n; i += 256) {
-            const uint4 v = *reinterpret_cast<const uint4 *>(src + i);
+            typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+            const u4v vv = __builtin_nontemporal_load(reinterpret_cast<const u4v *>(src + i));
+            const uint4 v = make_uint4(vv.x, vv.y, vv.z, vv.w);
             dst[i] = v.x;
             if (i + 1 < n) dst[i + 1] = v.y;
             if (i + 2 < n) dst[i + 2] = v.z;
@@ -154,7 +234,7 @@ __global__ __launch_bounds__(256) void k_compact_tokens(const uint32_t *__restri
     uint32_t written = 0;
     for (uint32_t e0 = 0; e0 < ne; e0 += 64) {
         const uint32_t e = e0 + lane;
-        const uint32_t x = e < ne ? src[e] : 0u;
+        const uint32_t x = e < ne ? __builtin_nontemporal_load(src + e) : 0u;
         const bool mark = (x & 0x80000000u) != 0u;
         const uint32_t w = e >= ne ? 0u : !mark ? 1u : long_pool ? long_pool[x & 0x7FFFFFFFu] : long_list[x & 0x7FFFFFFFu].k;
         const uint32_t incl = wave_incl_sum(w);
@@ -190,44 +270,49 @@ hipError_t launch_compact_tokens(const uint32_t *tokc, const uint32_t *chunk_cnt
 __global__ __launch_bounds__(256) void k_records(RowParams P, const uint64_t *__restrict__ off, int64_t R, int64_t N,
                                                  const uint32_t *__restrict__ chunk_off, int64_t n_chunks,
                                                  const uint32_t *__restrict__ rec_local, uint32_t *__restrict__ rec_tok,
-                                                 uint32_t *__restrict__ rec_cnt, uint32_t *__restrict__ rec_rows) {
-    const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (r >= R) return;
-    const uint32_t total = chunk_off[n_chunks];
-    auto tok_off = [&](int64_t q) -> uint32_t {
-        const int64_t p = (int64_t)off[q];
-        return p >= N ? total : chunk_off[p / CHUNK] + rec_local[q];
-    };
-    const uint32_t a = tok_off(r), b = tok_off(r + 1);
-    const uint32_t cnt = b - a;
-    const uint32_t n = cnt + (uint32_t)(P.n_pre + P.n_post);  // encode_mask framing
-    uint32_t rows = 0;
-    if (n >= (uint32_t)P.min_ids) rows = P.chunk ? ceil_div_u32(n, (uint32_t)P.S) : 1u;  // gen_batcher.rs:74-80
-    rec_tok[r] = a;
-    rec_cnt[r] = cnt;
-    rec_rows[r] = rows;
+                                                 uint32_t *__restrict__ rec_cnt, uint32_t *__restrict__ rec_rows,
+                                                 SegSel sel) {
+    const int64_t r_lo = sel.rb[sel.k], r_hi = sel.rb[sel.k + 1];
+    for (int64_t r = r_lo + (int64_t)blockIdx.x * 256 + threadIdx.x; r < r_hi; r += (int64_t)gridDim.x * 256) {
+        auto tok_off = [&](int64_t q) -> uint32_t {
+            const int64_t p = (int64_t)off[q];
+            // (chunk_off[n_chunks], the total, is final once the last segment is scanned:
+            // only the last segment holds records that end at N)
+            return p >= N ? chunk_off[n_chunks] : chunk_off[p / CHUNK] + rec_local[q];
+        };
+        const uint32_t a = tok_off(r), b = tok_off(r + 1);
+        const uint32_t cnt = b - a;
+        const uint32_t n = cnt + (uint32_t)(P.n_pre + P.n_post);  // encode_mask framing
+        uint32_t rows = 0;
+        if (n >= (uint32_t)P.min_ids) rows = P.chunk ? ceil_div_u32(n, (uint32_t)P.S) : 1u;  // gen_batcher.rs:74-80
+        rec_tok[r] = a;
+        rec_cnt[r] = cnt;
+        rec_rows[r] = rows;
+    }
 }
 
 hipError_t launch_records(const RowParams &P, const uint64_t *off, int64_t R, int64_t N, const uint32_t *chunk_off,
                           int64_t n_chunks, const uint32_t *rec_local, uint32_t *rec_tok, uint32_t *rec_cnt,
-                          uint32_t *rec_rows, hipStream_t st) {
+                          uint32_t *rec_rows, SegSel sel, hipStream_t st) {
     if (R == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_records, dim3((unsigned)((R + 255) / 256)), dim3(256), 0, st, P, off, R, N, chunk_off,
-                       n_chunks, rec_local, rec_tok, rec_cnt, rec_rows);
+    const int64_t want = (R + 255) / 256;
+    hipLaunchKernelGGL(k_records, dim3((unsigned)(want < 1024 ? want : 1024)), dim3(256), 0, st, P, off, R, N,
+                       chunk_off, n_chunks, rec_local, rec_tok, rec_cnt, rec_rows, sel);
     return hipGetLastError();
 }
 
 // Row g -> its record (one thread per record writes its rows' entries).
-__global__ __launch_bounds__(256) void k_row_map(const uint32_t *__restrict__ row_off, int64_t R,
-                                                 uint32_t *__restrict__ row_rec) {
-    const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (r >= R) return;
-    for (uint32_t g = row_off[r]; g < row_off[r + 1]; ++g) row_rec[g] = (uint32_t)r;
+__global__ __launch_bounds__(256) void k_row_map(const uint32_t *__restrict__ row_off, uint32_t *__restrict__ row_rec,
+                                                 SegSel sel) {
+    const int64_t r_lo = sel.rb[sel.k], r_hi = sel.rb[sel.k + 1];
+    for (int64_t r = r_lo + (int64_t)blockIdx.x * 256 + threadIdx.x; r < r_hi; r += (int64_t)gridDim.x * 256)
+        for (uint32_t g = row_off[r]; g < row_off[r + 1]; ++g) row_rec[g] = (uint32_t)r;
 }
 
-hipError_t launch_row_map(const uint32_t *row_off, int64_t R, uint32_t *row_rec, hipStream_t st) {
+hipError_t launch_row_map(const uint32_t *row_off, int64_t R, uint32_t *row_rec, SegSel sel, hipStream_t st) {
     if (R == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_row_map, dim3((unsigned)((R + 255) / 256)), dim3(256), 0, st, row_off, R, row_rec);
+    const int64_t want = (R + 255) / 256;
+    hipLaunchKernelGGL(k_row_map, dim3((unsigned)(want < 1024 ? want : 1024)), dim3(256), 0, st, row_off, row_rec, sel);
     return hipGetLastError();
 }
 
@@ -346,16 +431,15 @@ template <int MR>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SDL_ROWS_WAVES, 8))) void k_rows(RowParams P, const uint32_t *__restrict__ tok,
                                               const uint32_t *__restrict__ rec_tok, const uint32_t *__restrict__ rec_cnt,
                                               const uint32_t *__restrict__ row_off, const uint32_t *__restrict__ row_rec,
-                                              const uint32_t *__restrict__ d_rows, int64_t rows_cap, RowOut out) {
+                                              SegSel sel, int64_t rows_cap, RowOut out) {
     const int lane = lane_id();
     const int wid = (int)(threadIdx.x >> 6);
     const int S = P.S;
     const bool vec = (S & 3) == 0;  // 16-byte aligned rows
     const bool vec_lb = (P.label_width & 3) == 0;
-    const uint32_t G = *d_rows;
-    int64_t Gpad = ((int64_t)G + P.B - 1) / P.B * P.B;
-    if (Gpad > rows_cap) Gpad = rows_cap;
-    for (int64_t g = (int64_t)blockIdx.x * 4 + wid; g < Gpad; g += (int64_t)gridDim.x * 4) {
+    const RowSpan rs = row_span(sel, row_off, P.B, rows_cap);
+    const int64_t G = rs.g_real;
+    for (int64_t g = rs.g_lo + (int64_t)blockIdx.x * 4 + wid; g < rs.g_end; g += (int64_t)gridDim.x * 4) {
         int32_t *ids_o = out.input_ids + g * S;
         int32_t *am_o = out.attention_mask + g * S;
         int32_t *tt_o = out.token_type_ids ? out.token_type_ids + g * S : nullptr;
@@ -501,8 +585,8 @@ hipError_t launch_rows_to_host(const RowSeg *segs, int n_segs, uint32_t rows_per
 }
 
 hipError_t launch_rows(const RowParams &P, const uint32_t *tok, const uint32_t *rec_tok, const uint32_t *rec_cnt,
-                       const uint32_t *row_off, const uint32_t *row_rec, const uint32_t *d_rows, int64_t rows_cap,
-                       RowOut out, hipStream_t st) {
+                       const uint32_t *row_off, const uint32_t *row_rec, SegSel sel, int64_t rows_cap, RowOut out,
+                       hipStream_t st) {
     if (rows_cap == 0) return hipSuccess;
 #ifndef SDL_ROWS_GRID_CAP
 #define SDL_ROWS_GRID_CAP 16384
@@ -512,7 +596,7 @@ hipError_t launch_rows(const RowParams &P, const uint32_t *tok, const uint32_t *
     const int MR = (P.S + 255) / 256;
     if (P.label_width > 256 * MR) return hipErrorInvalidValue;
 #define SDL_ROWS(MM)                                                                                                 \
-    hipLaunchKernelGGL(k_rows<MM>, dim3(grid), dim3(256), 0, st, P, tok, rec_tok, rec_cnt, row_off, row_rec, d_rows, \
+    hipLaunchKernelGGL(k_rows<MM>, dim3(grid), dim3(256), 0, st, P, tok, rec_tok, rec_cnt, row_off, row_rec, sel, \
                        rows_cap, out)
     if (MR <= 1) SDL_ROWS(1);
     else if (MR <= 2) SDL_ROWS(2);
@@ -547,16 +631,14 @@ __global__ __launch_bounds__(256) void k_rows_span(RowParams P, const uint32_t *
                                                    const uint32_t *__restrict__ rec_tok,
                                                    const uint32_t *__restrict__ rec_cnt,
                                                    const uint32_t *__restrict__ row_off,
-                                                   const uint32_t *__restrict__ row_rec,
-                                                   const uint32_t *__restrict__ d_rows, int64_t rows_cap, RowOut out,
-                                                   uint32_t *__restrict__ err) {
+                                                   const uint32_t *__restrict__ row_rec, SegSel sel,
+                                                   int64_t rows_cap, RowOut out, uint32_t *__restrict__ err) {
     const int lane = lane_id();
     const int wid = (int)(threadIdx.x >> 6);
     const int S = P.S, LW = P.label_width;
-    const uint32_t G = *d_rows;
-    int64_t Gpad = ((int64_t)G + P.B - 1) / P.B * P.B;
-    if (Gpad > rows_cap) Gpad = rows_cap;
-    for (int64_t g = (int64_t)blockIdx.x * 4 + wid; g < Gpad; g += (int64_t)gridDim.x * 4) {
+    const RowSpan rs = row_span(sel, row_off, P.B, rows_cap);
+    const int64_t G = rs.g_real;
+    for (int64_t g = rs.g_lo + (int64_t)blockIdx.x * 4 + wid; g < rs.g_end; g += (int64_t)gridDim.x * 4) {
         int32_t *ids_o = out.input_ids + g * S;
         int32_t *am_o = out.attention_mask + g * S;
         int32_t *lb_o = out.labels + g * (int64_t)LW;
@@ -641,14 +723,16 @@ __global__ __launch_bounds__(256) void k_rows_span(RowParams P, const uint32_t *
 }
 
 hipError_t launch_rows_span(const RowParams &P, const uint32_t *tok, const uint32_t *rec_tok, const uint32_t *rec_cnt,
-                            const uint32_t *row_off, const uint32_t *row_rec, const uint32_t *d_rows, int64_t rows_cap,
+                            const uint32_t *row_off, const uint32_t *row_rec, SegSel sel, int64_t rows_cap,
                             RowOut out, uint32_t *err, hipStream_t st) {
     if (rows_cap == 0) return hipSuccess;
     const int64_t want = (rows_cap + 3) / 4;
     const unsigned grid = (unsigned)(want < 4096 ? want : 4096);
-    hipError_t e = hipMemsetAsync(err, 0, sizeof(uint32_t), st);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_rows_span, dim3(grid), dim3(256), 0, st, P, tok, rec_tok, rec_cnt, row_off, row_rec, d_rows,
+    if (sel.k == 0) {  // the error count covers the whole call
+        hipError_t e = hipMemsetAsync(err, 0, sizeof(uint32_t), st);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(k_rows_span, dim3(grid), dim3(256), 0, st, P, tok, rec_tok, rec_cnt, row_off, row_rec, sel,
                        rows_cap, out, err);
     return hipGetLastError();
 }
@@ -659,12 +743,12 @@ hipError_t launch_rows_span(const RowParams &P, const uint32_t *tok, const uint3
 __global__ __launch_bounds__(256) void k_multi_labels(const uint32_t *__restrict__ labels,
                                                       const uint64_t *__restrict__ label_off,
                                                       const uint32_t *__restrict__ row_rec,
-                                                      const uint32_t *__restrict__ d_rows, int64_t rows_cap, int B,
-                                                      int NL, float *__restrict__ out, uint32_t *__restrict__ err) {
-    const uint32_t G = *d_rows;
-    int64_t Gpad = ((int64_t)G + B - 1) / B * B;
-    if (Gpad > rows_cap) Gpad = rows_cap;
-    for (int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x; g < Gpad; g += (int64_t)gridDim.x * 256) {
+                                                      const uint32_t *__restrict__ row_off, SegSel sel,
+                                                      int64_t rows_cap, int B, int NL, float *__restrict__ out,
+                                                      uint32_t *__restrict__ err) {
+    const RowSpan rs = row_span(sel, row_off, B, rows_cap);
+    const int64_t G = rs.g_real;
+    for (int64_t g = rs.g_lo + (int64_t)blockIdx.x * 256 + threadIdx.x; g < rs.g_end; g += (int64_t)gridDim.x * 256) {
         float *o = out + g * NL;
         for (int k = 0; k < NL; ++k) o[k] = 0.f;
         if (g >= (int64_t)G || !labels) continue;
@@ -680,12 +764,12 @@ __global__ __launch_bounds__(256) void k_multi_labels(const uint32_t *__restrict
 }
 
 hipError_t launch_multi_labels(const uint32_t *labels, const uint64_t *label_off, const uint32_t *row_rec,
-                               const uint32_t *d_rows, int64_t rows_cap, int B, int NL, float *out, uint32_t *err,
-                               hipStream_t st) {
+                               const uint32_t *row_off, SegSel sel, int64_t rows_cap, int B, int NL, float *out,
+                               uint32_t *err, hipStream_t st) {
     if (rows_cap == 0) return hipSuccess;
     const int64_t want = (rows_cap + 255) / 256;
     hipLaunchKernelGGL(k_multi_labels, dim3((unsigned)(want < 2048 ? want : 2048)), dim3(256), 0, st, labels,
-                       label_off, row_rec, d_rows, rows_cap, B, NL, out, err);
+                       label_off, row_rec, row_off, sel, rows_cap, B, NL, out, err);
     return hipGetLastError();
 }
 
@@ -697,12 +781,12 @@ hipError_t launch_multi_labels(const uint32_t *labels, const uint64_t *label_off
 __global__ __launch_bounds__(256) void k_single_labels(const uint32_t *__restrict__ labels,
                                                        const uint64_t *__restrict__ label_off,
                                                        const uint32_t *__restrict__ row_rec,
-                                                       const uint32_t *__restrict__ d_rows, int64_t rows_cap, int B,
-                                                       int32_t *__restrict__ out, uint32_t *__restrict__ err) {
-    const uint32_t G = *d_rows;
-    int64_t Gpad = ((int64_t)G + B - 1) / B * B;
-    if (Gpad > rows_cap) Gpad = rows_cap;
-    for (int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x; g < Gpad; g += (int64_t)gridDim.x * 256) {
+                                                       const uint32_t *__restrict__ row_off, SegSel sel,
+                                                       int64_t rows_cap, int B, int32_t *__restrict__ out,
+                                                       uint32_t *__restrict__ err) {
+    const RowSpan rs = row_span(sel, row_off, B, rows_cap);
+    const int64_t G = rs.g_real;
+    for (int64_t g = rs.g_lo + (int64_t)blockIdx.x * 256 + threadIdx.x; g < rs.g_end; g += (int64_t)gridDim.x * 256) {
         int32_t v = 0;
         if (g < (int64_t)G && labels) {
             const uint32_t r = row_rec[g];
@@ -715,12 +799,12 @@ __global__ __launch_bounds__(256) void k_single_labels(const uint32_t *__restric
 }
 
 hipError_t launch_single_labels(const uint32_t *labels, const uint64_t *label_off, const uint32_t *row_rec,
-                                const uint32_t *d_rows, int64_t rows_cap, int B, int32_t *out, uint32_t *err,
-                                hipStream_t st) {
+                                const uint32_t *row_off, SegSel sel, int64_t rows_cap, int B, int32_t *out,
+                                uint32_t *err, hipStream_t st) {
     if (rows_cap == 0) return hipSuccess;
     const int64_t want = (rows_cap + 255) / 256;
     hipLaunchKernelGGL(k_single_labels, dim3((unsigned)(want < 2048 ? want : 2048)), dim3(256), 0, st, labels,
-                       label_off, row_rec, d_rows, rows_cap, B, out, err);
+                       label_off, row_rec, row_off, sel, rows_cap, B, out, err);
     return hipGetLastError();
 }
 

@@ -225,6 +225,15 @@ void par_copy(void *dst, const void *src, size_t n) {
 
 const char *kStageNames[] = {"chunk_ranges", "tokenize", "scan_chunks", "compact_tokens", "records", "scan_rows", "rows"};
 constexpr int kStages = 7;
+// pipelined segments: the tokenize launches, then the downstream work left after the last one
+const char *kPipedStageNames[] = {"chunk_ranges", "tokenize", "downstream_tail"};
+// segments per call (SDL_SEGMENTS) and the fewest 1 KiB chunks a pipelined
+// segment holds (SDL_SEG_MIN_CHUNKS, default 16 MiB of text); read when a
+// handle is created
+int env_int(const char *name, int dflt) {
+    const char *e = std::getenv(name);
+    return e ? std::max(1, std::atoi(e)) : dflt;
+}
 
 }  // namespace
 
@@ -294,6 +303,14 @@ struct sdl_batcher {
     bool profiling = false;
     hipEvent_t ev[kStages + 1] = {};
     float stage_ms[kStages] = {};
+    int n_stages = kStages;
+    const char **stage_names = kStageNames;
+    // pipelined segments: second stream, cross-stream events, record bounds
+    hipStream_t stream2 = nullptr;
+    std::vector<hipEvent_t> pipe_ev;
+    DevBuf<uint32_t> seg_rb;
+    int seg_target = env_int("SDL_SEGMENTS", 1);
+    int64_t seg_min_chunks = env_int("SDL_SEG_MIN_CHUNKS", 16384);
 
 #ifdef SDL_STAMPS
     ~sdl_batcher() {
@@ -315,6 +332,8 @@ struct sdl_batcher {
         for (auto *b : outbox) delete b;
         for (auto &e : ev)
             if (e) (void)hipEventDestroy(e);
+        for (auto &e : pipe_ev) (void)hipEventDestroy(e);
+        if (stream2) (void)hipStreamDestroy(stream2);
         if (stream) (void)hipStreamDestroy(stream);
     }
 
@@ -371,14 +390,74 @@ struct sdl_batcher {
 
         RowParams p = P;
         p.first_record = first_record;
+        const bool bpe = dt.kind == TOK_BYTE_BPE;
+        const bool uni = dt.kind == TOK_UNIGRAM;
+        // Pipelined segments (WordPiece): the tokenize launches of the chunk
+        // ranges run back to back on `st` while a second stream runs each
+        // finished segment's scans, compaction, records and rows -- the
+        // latency-bound tokenizer and the write-bound row assembly overlap.
+        // The other tokenizers finish long items in follow-up kernels over the
+        // whole call, so they run as one segment.
+        SegChunks sc{};
+        sc.K = 1;
+        if (!bpe && !uni && seg_target > 1 && n_chunks >= 2 * seg_min_chunks) {
+            sc.K = (int)std::min<int64_t>(seg_target, n_chunks / seg_min_chunks);
+            sc.K = std::min(sc.K, MAX_SEGMENTS);
+        }
+        for (int k = 0; k <= sc.K; ++k) sc.cb[k] = n_chunks * k / sc.K;
+        seg_rb.ensure(MAX_SEGMENTS + 2);
+        const bool piped = sc.K > 1;
+        n_stages = piped ? 3 : kStages;
+        stage_names = piped ? kPipedStageNames : kStageNames;
         auto mark = [&](int i) {
             if (profiling) HIP_TRY(hipEventRecord(ev[i], st));
         };
         mark(0);
         HIP_TRY(launch_chunk_ranges(d_off, R, N, ranges.p, st));
+        HIP_TRY(launch_seg_bounds(ranges.p, sc, R, seg_rb.p, st));
+        if (multi() || single()) HIP_TRY(hipMemsetAsync(lab_err.p, 0, 4, st));
         mark(1);
-        const bool bpe = dt.kind == TOK_BYTE_BPE;
-        const bool uni = dt.kind == TOK_UNIGRAM;
+        RowOut out{o_ids.p, o_am.p, with_tt() ? o_tt.p : nullptr, multi() ? nullptr : o_lab.p,
+                   multi() ? o_f32.p : nullptr};
+        // everything after the tokenizer, for segment k, on stream s
+        auto downstream = [&](int k, hipStream_t s) {
+            const SegSel sel{seg_rb.p, k, k == sc.K - 1 ? 1 : 0};
+            const int64_t ca = sc.cb[k], cz = sc.cb[k + 1];
+            if (!piped) mark(2);
+            HIP_TRY(launch_exclusive_scan(chunk_cnt.p + ca, chunk_off.p + ca, cz - ca, scan_tmp.p, s,
+                                          k > 0 ? chunk_off.p + ca : nullptr));
+            if (!piped) mark(3);
+            if (uni)
+                HIP_TRY(launch_compact_tokens(tokc.p, chunk_cnt.p, chunk_off.p, n_chunks, tok_ids.p, uni_counters.p,
+                                              chunk_ent.p, nullptr, nullptr, s, uni_pool.p, UNI_STAGE));
+            else if (bpe)
+                HIP_TRY(launch_compact_tokens(tokc.p, chunk_cnt.p, chunk_off.p, n_chunks, tok_ids.p, long_count.p,
+                                              chunk_ent.p, long_list.p, long_scratch.p, s));
+            else
+                HIP_TRY(launch_compact_tokens(tokc.p + ca * STAGE, chunk_cnt.p + ca, chunk_off.p + ca, cz - ca,
+                                              tok_ids.p, nullptr, nullptr, nullptr, nullptr, s));
+            if (!piped) mark(4);
+            HIP_TRY(launch_records(p, d_off, R, N, chunk_off.p, n_chunks, rec_local.p, rec_tok.p, rec_cnt.p, rec_rows.p,
+                                   sel, s));
+            if (!piped) mark(5);
+            if (piped) HIP_TRY(launch_scan_range(rec_rows.p, row_off.p, seg_rb.p, k, s));
+            else HIP_TRY(launch_exclusive_scan(rec_rows.p, row_off.p, R, scan_tmp.p, s));
+            HIP_TRY(launch_row_map(row_off.p, R, row_rec.p, sel, s));
+            if (!piped) mark(6);
+            if (span()) {
+                span_err.ensure(1);
+                HIP_TRY(launch_rows_span(p, tok_ids.p, rec_tok.p, rec_cnt.p, row_off.p, row_rec.p, sel, rows_cap, out,
+                                         span_err.p, s));
+            } else {
+                HIP_TRY(launch_rows(p, tok_ids.p, rec_tok.p, rec_cnt.p, row_off.p, row_rec.p, sel, rows_cap, out, s));
+            }
+            if (multi())
+                HIP_TRY(launch_multi_labels(d_labels, d_label_off, row_rec.p, row_off.p, sel, rows_cap, P.B,
+                                            P.label_width, o_f32.p, lab_err.p, s));
+            else if (single())
+                HIP_TRY(launch_single_labels(d_labels, d_label_off, row_rec.p, row_off.p, sel, rows_cap, P.B, o_lab.p,
+                                             lab_err.p, s));
+        };
         if (uni) {
             // long items: words > UNI_WMAX bytes (<= N / 25), one per chunk past
             // its window, and medium words whose normalization overflows the
@@ -397,6 +476,7 @@ struct sdl_batcher {
                       uni_scratch.p, lane_blocks, huge_blocks, uni_err.p};
             HIP_TRY(launch_unigram_chunks(dt, d_text, N, d_off, R, ranges.p, tokc.p, chunk_cnt.p, chunk_ent.p,
                                           rec_local.p, W, st));
+            downstream(0, st);
         } else if (bpe) {
             // long pieces are > 64 bytes or run past their chunk's window (<= 1 per chunk)
             const uint32_t cap = (uint32_t)(N / 64 + n_chunks + 1);
@@ -407,49 +487,37 @@ struct sdl_batcher {
             chunk_ent.ensure((size_t)n_chunks + 1);
             HIP_TRY(launch_bpe_chunks(dt, d_text, N, d_off, R, ranges.p, tokc.p, chunk_cnt.p, chunk_ent.p,
                                       rec_local.p, long_count.p, long_list.p, cap, long_scratch.p, bpe_err.p, st));
-        } else {
+            downstream(0, st);
+        } else if (!piped) {
             HIP_TRY(launch_wordpiece_chunks(dt, d_text, N, d_off, R, ranges.p, tokc.p, chunk_cnt.p, rec_local.p, st));
-        }
-        mark(2);
-        HIP_TRY(launch_exclusive_scan(chunk_cnt.p, chunk_off.p, n_chunks, scan_tmp.p, st));
-        mark(3);
-        if (uni)
-            HIP_TRY(launch_compact_tokens(tokc.p, chunk_cnt.p, chunk_off.p, n_chunks, tok_ids.p, uni_counters.p,
-                                          chunk_ent.p, nullptr, nullptr, st, uni_pool.p, UNI_STAGE));
-        else
-            HIP_TRY(launch_compact_tokens(tokc.p, chunk_cnt.p, chunk_off.p, n_chunks, tok_ids.p,
-                                          bpe ? long_count.p : nullptr, bpe ? chunk_ent.p : nullptr,
-                                          bpe ? long_list.p : nullptr, bpe ? long_scratch.p : nullptr, st));
-        mark(4);
-        HIP_TRY(launch_records(p, d_off, R, N, chunk_off.p, n_chunks, rec_local.p, rec_tok.p, rec_cnt.p, rec_rows.p,
-                               st));
-        mark(5);
-        HIP_TRY(launch_exclusive_scan(rec_rows.p, row_off.p, R, scan_tmp.p, st));
-        HIP_TRY(launch_row_map(row_off.p, R, row_rec.p, st));
-        mark(6);
-        RowOut out{o_ids.p, o_am.p, with_tt() ? o_tt.p : nullptr, multi() ? nullptr : o_lab.p,
-                   multi() ? o_f32.p : nullptr};
-        if (span()) {
-            span_err.ensure(1);
-            HIP_TRY(launch_rows_span(p, tok_ids.p, rec_tok.p, rec_cnt.p, row_off.p, row_rec.p, row_off.p + R, rows_cap,
-                                     out, span_err.p, st));
+            downstream(0, st);
         } else {
-            HIP_TRY(launch_rows(p, tok_ids.p, rec_tok.p, rec_cnt.p, row_off.p, row_rec.p, row_off.p + R, rows_cap, out,
-                                st));
+            ensure_pipe_events(sc.K);
+            for (int k = 0; k < sc.K; ++k) {
+                HIP_TRY(launch_wordpiece_chunks(dt, d_text, N, d_off, R, ranges.p, tokc.p, chunk_cnt.p, rec_local.p, st,
+                                                sc.cb[k], sc.cb[k + 1]));
+                HIP_TRY(hipEventRecord(pipe_ev[k], st));
+                HIP_TRY(hipStreamWaitEvent(stream2, pipe_ev[k], 0));
+                downstream(k, stream2);
+            }
+            mark(2);
+            HIP_TRY(hipEventRecord(pipe_ev[sc.K], stream2));
+            HIP_TRY(hipStreamWaitEvent(st, pipe_ev[sc.K], 0));  // the caller's stream sees every row
         }
-        if (multi()) {
-            HIP_TRY(hipMemsetAsync(lab_err.p, 0, 4, st));
-            HIP_TRY(launch_multi_labels(d_labels, d_label_off, row_rec.p, row_off.p + R, rows_cap, P.B, P.label_width,
-                                        o_f32.p, lab_err.p, st));
-        } else if (single()) {
-            HIP_TRY(hipMemsetAsync(lab_err.p, 0, 4, st));
-            HIP_TRY(launch_single_labels(d_labels, d_label_off, row_rec.p, row_off.p + R, rows_cap, P.B, o_lab.p,
-                                         lab_err.p, st));
-        }
-        mark(7);
+        mark(piped ? 3 : 7);
         last_rows_cap = rows_cap;
         last_R = R;
+        last_segments = sc.K;
     }
+    void ensure_pipe_events(int K) {
+        while ((int)pipe_ev.size() < K + 1) {
+            hipEvent_t e;
+            HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            pipe_ev.push_back(e);
+        }
+        if (!stream2) HIP_TRY(hipStreamCreateWithFlags(&stream2, hipStreamNonBlocking));
+    }
+    int64_t last_segments = 1;
     int64_t last_rows_cap = 0, last_R = 0;
 
     // H2D a host arena, run the device path, bring back the rows; then play
@@ -1163,12 +1231,12 @@ int sdl_set_profiling(sdl_batcher *h, int enable) {
 int sdl_stage_times(sdl_batcher *h, const char **names, float *ms, int cap) {
     if (!h) return fail(SDL_ERR_ARG, "null argument");
     if (!h->profiling) return fail(SDL_ERR_STATE, "profiling not enabled");
-    if (hipEventSynchronize(h->ev[kStages]) != hipSuccess) return fail(SDL_ERR_HIP, "event sync failed");
-    int n = std::min(cap, kStages);
+    if (hipEventSynchronize(h->ev[h->n_stages]) != hipSuccess) return fail(SDL_ERR_HIP, "event sync failed");
+    int n = std::min(cap, h->n_stages);
     for (int i = 0; i < n; ++i) {
         float t = 0.f;
         if (hipEventElapsedTime(&t, h->ev[i], h->ev[i + 1]) != hipSuccess) return fail(SDL_ERR_HIP, "event time");
-        if (names) names[i] = kStageNames[i];
+        if (names) names[i] = h->stage_names[i];
         if (ms) ms[i] = t;
     }
     return n;

@@ -515,7 +515,7 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
             dst[base++] = LONG_MARK | (uint32_t)s_stage[prel] | ((uint32_t)s_stage[prel + 1] << 16);
             continue;
         }
-        for (int j = 0; j < k; ++j) dst[base + j] = s_stage[prel + j];
+        for (int j = 0; j < k; ++j) __builtin_nontemporal_store((uint32_t)s_stage[prel + j], dst + base + j);
         base += k;
     }
     __syncthreads();

@@ -1073,7 +1073,7 @@ __global__ __launch_bounds__(TOK_THREADS) void k_unigram_chunks(
             dst[base++] = LMARK;
             continue;
         }
-        for (int j = 0; j < k; ++j) dst[base + j] = s_stage[prel + j];
+        for (int j = 0; j < k; ++j) __builtin_nontemporal_store((uint32_t)s_stage[prel + j], dst + base + j);
         base += k;
     }
     __syncthreads();

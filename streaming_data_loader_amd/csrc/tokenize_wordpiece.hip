@@ -278,15 +278,16 @@ __device__ unsigned long long sdl_phase_cycles[16];
     } while (0)
 #endif
 
-// Waves per SIMD the register budget is cut to (LDS admits 5 at 7.6 KB per
-// one-wave block; measured: tools/variants.sh).
+// Waves per SIMD the register budget is cut to: 6 (80 VGPRs) with the 7.1 KB
+// block (PEND_CAP 256) measured 1% faster than 5 (tools/variants.sh).  The
+// LDS step that matters: one more 64-B array (7.7 KB) cost 7%.
 #ifndef SDL_WP_WAVES
-#define SDL_WP_WAVES 5
+#define SDL_WP_WAVES 6
 #endif
 __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL_WP_WAVES, 8))) void k_wordpiece_chunks(
     DevTok T, const uint8_t *__restrict__ text, int64_t N, const uint64_t *__restrict__ off, int64_t R,
     const uint32_t *__restrict__ ranges, uint32_t *__restrict__ tokc, uint32_t *__restrict__ chunk_cnt,
-    uint32_t *__restrict__ rec_local) {
+    uint32_t *__restrict__ rec_local, int64_t c_begin) {
     __shared__ __attribute__((aligned(16))) uint8_t s_win[WIN];
     __shared__ uint32_t s_rbits[RBITS_WORDS + 1];
     __shared__ uint16_t s_pieces[CHUNK];   // (pos - c0) | kind << 12
@@ -306,7 +307,8 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
 #ifdef SDL_STAMPS
     unsigned long long stamp_prev_ = __builtin_amdgcn_s_memtime();
 #endif
-    const int64_t c0 = (int64_t)blockIdx.x * CHUNK;
+    const int64_t ci = c_begin + (int64_t)blockIdx.x;  // this block's chunk
+    const int64_t c0 = ci * CHUNK;
     const int64_t c1 = c0 + CHUNK < N ? c0 + CHUNK : N;
     const int64_t w0 = c0 - HALO_L;
     const lds_u8 *win = (const lds_u8 *)s_win;
@@ -314,13 +316,16 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
 
     // ---- 1. load -------------------------------------------------------------
     const uint4 v = load16(text, c0 + 16 * tid, N);
-    *reinterpret_cast<uint4 *>(s_win + HALO_L + 16 * tid) = v;
+    uint4 hv = make_uint4(0u, 0u, 0u, 0u);
+    int64_t hp = 0;
     if (tid < (WIN - CHUNK) / 16) {  // left and right halo pieces
-        const int64_t p = tid < HALO_L / 16 ? w0 + 16 * tid : c0 + CHUNK + 16 * (tid - HALO_L / 16);
-        *reinterpret_cast<uint4 *>(s_win + (p - w0)) = load16(text, p, N);
+        hp = tid < HALO_L / 16 ? w0 + 16 * tid : c0 + CHUNK + 16 * (tid - HALO_L / 16);
+        hv = load16(text, hp, N);
     }
+    const int64_t ra = ranges[3 * ci], rz = ranges[3 * ci + 1], r_lo = ranges[3 * ci + 2];
+    *reinterpret_cast<uint4 *>(s_win + HALO_L + 16 * tid) = v;
+    if (tid < (WIN - CHUNK) / 16) *reinterpret_cast<uint4 *>(s_win + (hp - w0)) = hv;
     if (tid <= RBITS_WORDS) s_rbits[tid] = 0;
-    const int64_t ra = ranges[3 * blockIdx.x], rz = ranges[3 * blockIdx.x + 1], r_lo = ranges[3 * blockIdx.x + 2];
     const int nrb = (int)(rz - ra);
     int64_t rb_next = rz <= R ? (int64_t)off[rz] : N;
     if (rb_next > N) rb_next = N;
@@ -335,7 +340,7 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
     const Ctx C{&T, win, rbits, w0, text, N, off, R};
 #if defined(SDL_ABLATE) && SDL_ABLATE >= 3
     // diagnostic: load only; every record gets 0 ids (so later stages stay in bounds)
-    if (tid == 0) chunk_cnt[blockIdx.x] = s_win[HALO_L + (blockIdx.x & 1023)] & 0u;
+    if (tid == 0) chunk_cnt[ci] = s_win[HALO_L + (ci & 1023)] & 0u;
     for (int64_t r = r_lo + tid; r <= R && (int64_t)off[r] < c1; r += TOK_THREADS) rec_local[r] = 0;
     return;
 #endif
@@ -359,14 +364,14 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
         cls &= nown ? ((1ull << (4 * nown)) - 1ull) : 0ull;
         leads &= (1u << nown) - 1u;
     }
+    uint8_t *s_ovr = s_cnt;
+    *reinterpret_cast<uint4 *>(s_ovr + 16 * tid) = make_uint4(~0u, ~0u, ~0u, ~0u);
     // Rare bytes are classified block-parallel, one per thread, and returned as
     // per-byte class overrides in LDS (s_cnt doubles as the override array and
     // s_pieces as the work list until the pieces are found):
     //   (a) non-ASCII lead bytes: decode + two-level Unicode table;
     //   (b) added tokens: every opener byte that starts a match marks its bytes
     //       (SPEC at the start, invisible after); applied after (a).
-    uint8_t *s_ovr = s_cnt;
-    *reinterpret_cast<uint4 *>(s_ovr + 16 * tid) = make_uint4(~0u, ~0u, ~0u, ~0u);
     uint32_t opens = 0;
     if (T.n_special) {
 #pragma unroll
@@ -744,12 +749,14 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
     for (int i = a0; i < a1; ++i) mine += s_cnt[i];
     uint32_t total;
     const uint32_t base0 = block_excl_sum<TOK_THREADS>(mine, &total, s_scratch);
-    uint32_t *dst = tokc + (int64_t)blockIdx.x * STAGE;
+    uint32_t *dst = tokc + ci * STAGE;
     uint32_t base = base0;
     for (int i = a0; i < a1; ++i) {
         const int prel = s_pieces[i] & 0xFFF;
         const int k = s_cnt[i];
-        for (int j = 0; j < k; ++j) dst[base + j] = s_stage[prel + j];
+        // non-temporal: the lists are read once, by the compaction, and must not
+        // evict the vocabulary table from L2 (rows 0.39 -> 0.34 ms measured)
+        for (int j = 0; j < k; ++j) __builtin_nontemporal_store((uint32_t)s_stage[prel + j], dst + base + j);
         base += k;
     }
     __syncthreads();
@@ -762,7 +769,7 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
     }
     __syncthreads();
     SDL_STAMP(8);
-    if (tid == 0) chunk_cnt[blockIdx.x] = total;
+    if (tid == 0) chunk_cnt[ci] = total;
     // record boundaries owned by this chunk: local id offset of the first piece
     // at or after the boundary
     const int k_lo = (int)(r_lo - ra);
@@ -797,11 +804,13 @@ void print_phase_cycles() {
 
 hipError_t launch_wordpiece_chunks(const DevTok &T, const uint8_t *text, int64_t N, const uint64_t *off, int64_t R,
                                    uint32_t *ranges, uint32_t *tokc, uint32_t *chunk_cnt, uint32_t *rec_local,
-                                   hipStream_t st) {
+                                   hipStream_t st, int64_t c_begin, int64_t c_end) {
     const int64_t n_chunks = (N + CHUNK - 1) / CHUNK;
-    if (n_chunks == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_wordpiece_chunks, dim3((unsigned)n_chunks), dim3(TOK_THREADS), 0, st, T, text, N, off, R,
-                       ranges, tokc, chunk_cnt, rec_local);
+    if (c_end < 0 || c_end > n_chunks) c_end = n_chunks;
+    if (c_begin < 0) c_begin = 0;
+    if (c_end <= c_begin) return hipSuccess;
+    hipLaunchKernelGGL(k_wordpiece_chunks, dim3((unsigned)(c_end - c_begin)), dim3(TOK_THREADS), 0, st, T, text, N, off,
+                       R, ranges, tokc, chunk_cnt, rec_local, c_begin);
     return hipGetLastError();
 }
 

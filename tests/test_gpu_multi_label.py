@@ -105,9 +105,12 @@ def random_items(n, seed):
     return items
 
 
-@pytest.mark.parametrize("S,Bsz", [(128, 64), (512, 16), (100, 7)])
-def test_device_path_matches_oracle(torch, native_lib, oracle_tok, S, Bsz):
-    """sdl_process_device_labels on ragged random records vs the oracle."""
+@pytest.mark.parametrize("S,Bsz,segments", [(128, 64, 1), (512, 16, 1), (100, 7, 1), (128, 64, 5), (100, 7, 3)])
+def test_device_path_matches_oracle(torch, native_lib, oracle_tok, S, Bsz, segments, monkeypatch):
+    """sdl_process_device_labels on ragged random records vs the oracle
+    (segments > 1: the pipelined two-stream path)."""
+    monkeypatch.setenv("SDL_SEGMENTS", str(segments))
+    monkeypatch.setenv("SDL_SEG_MIN_CHUNKS", "16")
     items = random_items(600, seed=S)
     texts = [t for t, _ in items]
     arena, offs = arena_from_texts(texts)

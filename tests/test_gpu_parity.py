@@ -260,3 +260,30 @@ def test_full_size_properties(torch, native_lib, oracle_tok, records):
         sl = slice(int(row_off[r]), int(row_off[r + 1]))
         for j, got in enumerate((ids, am, tt, lab)):
             np.testing.assert_array_equal(got[sl], want[j])
+
+
+@pytest.mark.parametrize("segments", [2, 3, 7])
+def test_pipelined_segments_match_oracle(torch, native_lib, oracle_tok, records, segments, monkeypatch):
+    """The WordPiece path cut into pipelined segments (tokenize on the caller's
+    stream, scans/compaction/records/rows of finished segments on a second
+    stream): same rows as the oracle, pad rows included, for segment counts
+    whose cuts fall inside records; mlm and multi-label."""
+    monkeypatch.setenv("SDL_SEGMENTS", str(segments))
+    monkeypatch.setenv("SDL_SEG_MIN_CHUNKS", "16")
+    rng = np.random.default_rng(segments)
+    texts = [records[i] for i in rng.integers(0, len(records), 400)] + hard_records(segments)
+    db = DeviceBatcher(batch_size=32, sequence_length=512, seed=99)
+    res = run_device(torch, db, texts, first_record=17)
+    G = res.rows()
+    Gp = -(-G // 32) * 32
+    ids, am, tt, lab = res.planes(Gp)
+    want = oracle_lib.oracle_rows(oracle_tok, texts, 512, 76, 103, seed=99, B=32, first_record=17)
+    assert want.shape[1] == G
+    for j, got in enumerate((ids, am, tt, lab)):
+        np.testing.assert_array_equal(got[:G], want[j])
+    assert (ids[G:] == 0).all() and (am[G:] == 1).all() and (lab[G:] == -100).all()
+    assert int(res.record_rows().sum()) == G
+    # the same arena twice through one handle: buffers reused across calls
+    res2 = run_device(torch, db, texts, first_record=17)
+    assert res2.rows() == G
+    np.testing.assert_array_equal(res2.planes(G)[0], want[0])
