@@ -42,7 +42,9 @@ namespace {
 
 enum : uint8_t { U_WS = 0, U_P = 1, U_X = 2, U_SPEC = 3, U_SPX = 4 };
 constexpr uint32_t LMARK = 0x80000000u;
-__device__ const uint8_t kMetaBytes[3] = {0xE2, 0x96, 0x81};
+// byte x (< 3) of "▁" (U+2581) -- arithmetic, not a global table: a load here
+// would make the DP wait for every probe in flight (vmcnt counts in order)
+__device__ __forceinline__ uint32_t meta_byte(int x) { return x == 0 ? 0xE2u : x == 1 ? 0x96u : 0x81u; }
 
 // LDS budget: 3 one-wave blocks per SIMD (<= 13.3 KB each) -- the kernel waits
 // on probe latency, so resident waves are what it runs on
@@ -333,7 +335,7 @@ __device__ int tokenize_normalized(const DevTok &T, const Scratch &S, int nl) {
             if (!cut) continue;
             const int off = virt ? 3 : 0;
             const int n = t - ps + off;
-            auto acc = [&](int x) -> uint32_t { return x < off ? kMetaBytes[x] : nb[ps + x - off]; };
+            auto acc = [&](int x) -> uint32_t { return x < off ? meta_byte(x) : nb[ps + x - off]; };
             auto cand = [&](int s, int e, double *sc) -> int {
                 int id;
                 if (s == 0) id = (e - 3 <= T.maxlen_meta) ? probe_acc(T, acc, 3, e - 3, UC_META) : -1;
@@ -512,7 +514,10 @@ void print_uni_cycles() {
 #endif
 
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(TOK_THREADS) void k_unigram_chunks(
+#ifndef SDL_UNI_WAVES
+#define SDL_UNI_WAVES 3
+#endif
+__global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL_UNI_WAVES, 8))) void k_unigram_chunks(
     DevTok T, const uint8_t *__restrict__ text, int64_t N, const uint64_t *__restrict__ off, int64_t R,
     const uint32_t *__restrict__ ranges, uint32_t *__restrict__ tokc, uint32_t *__restrict__ chunk_cnt,
     uint32_t *__restrict__ chunk_ent, uint32_t *__restrict__ rec_local, uint32_t *__restrict__ counters,
@@ -886,34 +891,32 @@ __global__ __launch_bounds__(TOK_THREADS) void k_unigram_chunks(
         }
         return lo;
     };
-    // candidate probes: task t = 64 u + lane of the round (one candidate (start,
-    // end) of one piece), TASK_UNROLL in flight per lane
+    // candidate probes: task t of the round is one candidate (start, end) of one
+    // piece, TASK_UNROLL in flight per lane
     Probe P[TASK_UNROLL];
     W16 W[TASK_UNROLL];
     uint32_t meta[TASK_UNROLL];  // row | k << 16 | n << 22 | cont << 29; ~0u: no probe
     int gen[TASK_UNROLL];        // generic probe result (payload > 16 bytes); -2: use P
     uint32_t gw3[TASK_UNROLL];
+    // A lane takes TASK_UNROLL consecutive tasks (4 lane + u): one job/vp search
+    // and one candidate decode per lane, then (i, j) steps along the rows, and
+    // the 16 payload bytes of a row are read from LDS once for its candidates.
     auto issue = [&](int ja, int jz) {
         const uint32_t T0 = s_job_tb[ja], RB0 = s_job_rb[ja];
         const int nt = (int)(s_job_tb[jz] - T0);
-#pragma unroll
-        for (int u = 0; u < TASK_UNROLL; ++u) {
-            const int t = 64 * u + lane;
-            meta[u] = ~0u;
-            gen[u] = -2;
-            gw3[u] = 0;
-            W[u] = W16{0, 0, 0, 0};
-            if (t >= nt) continue;
-            const uint32_t gt = T0 + (uint32_t)t;
-            int a = ja, b = jz - 1;  // the job holding task gt
+        const int t0 = TASK_UNROLL * lane;
+        int a = ja, vp = 0, q = 0, row = 0, L = 0, src = 0, i = -1, j = 0;
+        if (t0 < nt) {
+            const uint32_t gt = T0 + (uint32_t)t0;
+            int b = jz - 1;  // the job holding task gt
             while (a < b) {
                 const int m = (a + b + 1) >> 1;
                 if (s_job_tb[m] <= gt) a = m; else b = m - 1;
             }
             int lt = (int)(gt - s_job_tb[a]);
-            int row = (int)(s_job_rb[a] - RB0);
-            int vp = s_job_vp[a];
-            for (int q = 0; q + 1 < s_job_nvp[a]; ++q) {
+            row = (int)(s_job_rb[a] - RB0);
+            vp = s_job_vp[a];
+            for (; q + 1 < s_job_nvp[a]; ++q) {
                 const int Lq = s_vp_len[vp];
                 const int tk = vp_tasks(Lq, Mm, Mf);
                 if (lt < tk) break;
@@ -921,9 +924,42 @@ __global__ __launch_bounds__(TOK_THREADS) void k_unigram_chunks(
                 row += Lq + 1;
                 ++vp;
             }
-            const int L = s_vp_len[vp], src = s_vp_src[vp];
-            int i, j;  // payload start (-1: the "▁" row) and end
+            L = s_vp_len[vp];
+            src = s_vp_src[vp];
             vp_decode(lt, L, Mm, Mf, &i, &j);
+        }
+        int cur_ps = -1;
+        W16 rowb{0, 0, 0, 0};
+#pragma unroll
+        for (int u = 0; u < TASK_UNROLL; ++u) {
+            meta[u] = ~0u;
+            gen[u] = -2;
+            gw3[u] = 0;
+            W[u] = W16{0, 0, 0, 0};
+            if (t0 + u >= nt) continue;
+            if (u > 0) {  // the next candidate: (i, j + 1), else the next row / vp / job
+                ++j;
+                const int jmax = i < 0 ? (L < Mm ? L : Mm) : (L < i + Mf ? L : i + Mf);
+                if (j > jmax) {
+                    ++i;
+                    j = i + 1;
+                    if (i >= L) {  // past this vp's last row
+                        row += L + 1;
+                        if (q + 1 < s_job_nvp[a]) {
+                            ++q;
+                            ++vp;
+                        } else {
+                            ++a;
+                            q = 0;
+                            vp = s_job_vp[a];
+                        }
+                        L = s_vp_len[vp];
+                        src = s_vp_src[vp];
+                        i = -1;
+                        j = 0;
+                    }
+                }
+            }
             // candidates start and end on char boundaries
             if ((i > 0 && (bytes[src + i] & 0xC0u) == 0x80u) || (j < L && (bytes[src + j] & 0xC0u) == 0x80u))
                 continue;
@@ -933,7 +969,11 @@ __global__ __launch_bounds__(TOK_THREADS) void k_unigram_chunks(
             meta[u] = (uint32_t)(row + i + 1) | (uint32_t)(j - (i < 0 ? 0 : i + 1)) << 16 | (uint32_t)n << 22 |
                       cont << 29;
             if (n <= 16) {
-                W[u] = lds_w16(w32, src + ps, n);
+                if (src + ps != cur_ps) {
+                    cur_ps = src + ps;
+                    rowb = lds_w16(w32, cur_ps, 16);
+                }
+                W[u] = keep_bytes(rowb, n);
                 P[u] = probe_load(T, hash16(W[u], (uint32_t)n, cont));
             } else {
                 gen[u] = probe_acc(T, [&](int x) -> uint32_t { return bytes[src + x]; }, ps, n, cont, &gw3[u]);
@@ -954,7 +994,7 @@ __global__ __launch_bounds__(TOK_THREADS) void k_unigram_chunks(
             const uint32_t key = ((meta[u] >> 22) & 0x7Fu) | ((meta[u] >> 29) << 8);
             const int id = gen[u] != -2 ? gen[u] : probe_result_w3(P[u], key, W[u], &w3);
             if (id < 0) continue;
-            const int t = 64 * u + lane;
+            const int t = TASK_UNROLL * lane + u;
             s_tid[t] = (uint16_t)id;
             s_tsc[t] = __uint_as_float(w3);  // the slot's score (f32, exact)
             atomicOr(&s_rowmask[meta[u] & 0xFFFFu], 1u << ((meta[u] >> 16) & 0x3Fu));
@@ -962,7 +1002,9 @@ __global__ __launch_bounds__(TOK_THREADS) void k_unigram_chunks(
         __syncthreads();
         UNI_STAMP(6);
         const int n0 = j1, n1 = n0 < nj ? round_end(n0) : n0;
+#ifndef SDL_UNI_NO_PIPE
         if (n0 < nj) issue(n0, n1);  // the next round's probes fly during this DP
+#endif
         // -- DP: a group of DPG lanes per job.  Starts are visited in order; the
         //    candidates of one start end at distinct nodes, so the group's lanes
         //    relax them together (same visit order and strict-> replacement as
@@ -973,6 +1015,8 @@ __global__ __launch_bounds__(TOK_THREADS) void k_unigram_chunks(
             const int grp = lane / DPG, gl = lane % DPG;
             lds_f64 *gsc = (lds_f64 *)s_u + grp * UNI_NODES;
             lds_u32 *gbp = (lds_u32 *)(s_u + (64 / DPG) * UNI_NODES * 8) + grp * UNI_NODES;
+            // (A wavefront-scope fence -- enough for one wave's LDS, which executes
+            // in program order -- measured 1% slower than this workgroup fence.)
             auto wave_sync = [] {
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
                 __builtin_amdgcn_wave_barrier();
@@ -988,7 +1032,7 @@ __global__ __launch_bounds__(TOK_THREADS) void k_unigram_chunks(
                     const int vp = s_job_vp[jb] + q;
                     const int L = s_vp_len[vp], src = s_vp_src[vp];
                     const int n = L + 3;  // "▁" + payload
-                    auto acc = [&](int x) -> uint32_t { return x < 3 ? kMetaBytes[x] : (uint32_t)bytes[src + x - 3]; };
+                    auto acc = [&](int x) -> uint32_t { return x < 3 ? meta_byte(x) : (uint32_t)bytes[src + x - 3]; };
                     auto rowmask = [&](int st) -> uint32_t { return s_rowmask[roff + (st == 0 ? 0 : st - 2)]; };
                     for (int x = gl; x <= n; x += DPG) {
                         gsc[x] = 0.0;
@@ -1050,6 +1094,9 @@ __global__ __launch_bounds__(TOK_THREADS) void k_unigram_chunks(
         UNI_STAMP(7);
         j0 = n0;
         j1 = n1;
+#ifdef SDL_UNI_NO_PIPE
+        if (j0 < nj) issue(j0, j1);  // (diagnostic) the next round's probes after this DP
+#endif
     }
 
     UNI_STAMP(4);
@@ -1231,7 +1278,7 @@ __global__ __launch_bounds__(64) void k_unigram_long(DevTok T, const uint8_t *__
                 s_st[i] = 0xFFFFFFFFu;
             }
             // acc / cand over the piece (cand: the fused-unk lookup, lane 0)
-            auto acc = [&](int x) -> uint32_t { return x < 3 ? kMetaBytes[x] : (uint32_t)nb[src + x - 3]; };
+            auto acc = [&](int x) -> uint32_t { return x < 3 ? meta_byte(x) : (uint32_t)nb[src + x - 3]; };
             auto cand = [&](int st2, int e2, double *sc) -> int {
                 int id;
                 if (st2 == 0) id = (e2 - 3 <= Mm) ? probe_acc(T, nbr, src, e2 - 3, UC_META) : -1;

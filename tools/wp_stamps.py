@@ -20,8 +20,8 @@ arena, offs, order = bench.build_arena(bench.fixture_records(), mib << 20, seed=
 N, R = len(arena) - 16, len(order)
 text = torch.from_numpy(arena).cuda()
 off = torch.from_numpy(offs.astype(np.int64)).cuda()
-kind = {"mlm": native.SDL_TASK_MLM, "clm": native.SDL_TASK_CLM, "multi-label": native.SDL_TASK_MULTI_LABEL}[task]
-tok = native.GPT2_PROXY_TOKENIZER if t["tok"] == "gpt2" else native.BERT_PROXY_TOKENIZER
+kind = {"mlm": native.SDL_TASK_MLM, "clm": native.SDL_TASK_CLM, "multi-label": native.SDL_TASK_MULTI_LABEL, "span": native.SDL_TASK_SPAN}[task]
+tok = {"gpt2": native.GPT2_PROXY_TOKENIZER, "t5": native.T5_PROXY_TOKENIZER}.get(t["tok"], native.BERT_PROXY_TOKENIZER)
 db = DeviceBatcher(task=kind, batch_size=t["B"], sequence_length=t["S"], seed=1234, tokenizer=tok)
 db.set_profiling(True)
 db.process(text.data_ptr(), N, off.data_ptr(), R)
