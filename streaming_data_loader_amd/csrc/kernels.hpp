@@ -61,15 +61,15 @@ void print_uni_cycles();
 #endif
 
 // json_text.hip: the provider's JsonText filter (newline count + scan, newline
-// positions, lane-per-line parse, lane-per-line decode)
+// positions, parse and decode: lane per line below JL_MIN bytes, wave per line above)
 hipError_t launch_json_nl_count(const uint8_t *buf, int64_t len, uint32_t *cnt, uint32_t *base, uint32_t *scan_tmp,
                                 hipStream_t st);
 hipError_t launch_json_nl_write(const uint8_t *buf, int64_t len, const uint32_t *base, uint32_t *nl, hipStream_t st);
 hipError_t launch_json_parse(const uint8_t *buf, int64_t len, const uint32_t *nl, uint32_t n_nl, int64_t n_lines,
                              uint32_t *out_len, uint32_t *is_rec, uint2 *span, uint32_t *n_invalid, hipStream_t st);
-hipError_t launch_json_write(const uint8_t *buf, int64_t n_lines, const uint32_t *is_rec, const uint2 *span,
-                             const uint32_t *toff, const uint32_t *ridx, uint8_t *text, uint64_t *offsets,
-                             hipStream_t st);
+hipError_t launch_json_write(const uint8_t *buf, int64_t len, const uint32_t *nl, uint32_t n_nl, int64_t n_lines,
+                             const uint32_t *is_rec, const uint2 *span, const uint32_t *toff, const uint32_t *ridx,
+                             uint8_t *text, uint64_t *offsets, hipStream_t st);
 
 // pipeline.hip
 // out[0..n) = exclusive prefix sum of in[0..n) (+ *carry_in when given),

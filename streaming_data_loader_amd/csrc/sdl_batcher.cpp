@@ -1058,7 +1058,7 @@ int sdl_json_text_device(sdl_batcher *h, const uint8_t *d_jsonl, uint64_t len, v
         if (n_lines) {
             HIP_TRY(launch_exclusive_scan(h->j_len.p, h->j_toff.p, n_lines, h->scan_tmp.p, st));
             HIP_TRY(launch_exclusive_scan(h->j_rec.p, h->j_ridx.p, n_lines, h->scan_tmp.p, st));
-            HIP_TRY(launch_json_write(d_jsonl, n_lines, h->j_rec.p, h->j_span.p, h->j_toff.p, h->j_ridx.p, h->j_text.p,
+            HIP_TRY(launch_json_write(d_jsonl, N, h->j_nl.p, n_nl, n_lines, h->j_rec.p, h->j_span.p, h->j_toff.p, h->j_ridx.p, h->j_text.p,
                                       h->j_off.p, st));
             HIP_TRY(hipMemcpyAsync(&counts[0], h->j_ridx.p + n_lines, 4, hipMemcpyDeviceToHost, st));
             HIP_TRY(hipMemcpyAsync(&counts[1], h->j_toff.p + n_lines, 4, hipMemcpyDeviceToHost, st));

@@ -151,3 +151,65 @@ def test_json_lines_to_batches_on_device(torch, native_lib, records, oracle_tok)
     want = oracle_lib.oracle_rows(oracle_lib.Tok(), [r.decode("utf-8") for r in recs], 128, 19, 103, seed=1234, B=8)
     for j in range(4):
         np.testing.assert_array_equal(got[j], want[j])
+
+
+def long_lines():
+    """Lines >= 512 bytes (the wave-per-line kernels): every hand case padded
+    with JSON whitespace, escape runs crossing 16-byte lanes and 1 KiB steps
+    (chains of \\u escapes, backslash runs, surrogate pairs at every offset),
+    and long invalid lines whose error sits deep inside."""
+    pad = b" " * 600
+    out = [(pad + line + b" \r", want) for line, want in HAND]
+    out.append((b'{"text": "' + b"\\u00e9" * 500 + b'"}', "é".encode() * 500))
+    out.append((b'{"text": "' + b"\\\\" * 700 + b'"}', b"\\" * 700))
+    out.append((b'{"text": "' + b"\\ud83d\\ude00" * 200 + b'"}', "😀".encode() * 200))
+    for k in range(0, 40):
+        body = b"a" * (1000 + k) + b"\\ud83d\\ude00\\n\\\"" + b"b" * 30
+        out.append((b'{"id": 1, "text": "' + body + b'"}', b"a" * (1000 + k) + "😀".encode() + b'\n"' + b"b" * 30))
+    x = b"x" * 2000
+    out += [
+        (b'{"text": "' + x + b'\\q"}', "invalid"),                 # bad escape deep inside
+        (b'{"text": "' + x, "invalid"),                             # unterminated
+        (b'{"text": "' + x + b'\x01"}', "invalid"),                 # raw control character
+        (b'{"text": "' + x + b'\xe2\x82"}', "invalid"),             # truncated UTF-8
+        (b'{"text": "' + x + b'\xed\xa0\x80"}', "invalid"),         # UTF-8 surrogate
+        (b'{"text": "' + x + b'\xc0\xaf"}', "invalid"),             # overlong
+        (b'{"text": "' + x + b'\\udc00"}', "invalid"),              # lone trailing surrogate
+        (b'{"text": "' + x + b'\\ud83d"}', "invalid"),              # lone leading surrogate
+        (b'{"text": "' + x + b'"} x', "invalid"),                   # trailing characters
+        (b'{"a": "' + x + b'", "n": 12}', None),                    # number ends the object
+        (b'{"a": "' + x + b'", "n": 012}', "invalid"),
+        (b'{"a": "' + x + b'", "text": tru}', "invalid"),
+        (b'{"a": "' + x + b'", "text": true}', None),
+        (b'{"a": "' + x + b'", "text": "' + x + b'", "text": "' + b"y" * 700 + b'"}', b"y" * 700),
+        (b'{"te\\u0078t": "' + x + b'"}', x),                       # escaped key
+        (b'{"meta": {"text": "' + x + b'"}}', None),
+        (b'[' * 127 + b'"' + x + b'"' + b']' * 127, None),
+        (b'[' * 128 + b'"' + x + b'"' + b']' * 128, "invalid"),
+        (b'{"text": "' + "é".encode() * 1000 + b'", "n": -1.5e+7}', "é".encode() * 1000),
+    ]
+    return out
+
+
+def test_oracle_long_cases():
+    for line, want in long_lines():
+        got = J.extract_line(line)
+        if want == "invalid":
+            assert got is J.INVALID, line[:80]
+        else:
+            assert got == want, line[:80]
+
+
+@pytest.mark.gpu
+def test_long_lines_on_device(torch, native_lib):
+    """The wave-per-line parse and decode (lines >= 512 bytes) against the
+    oracle, mixed with short lines so both kernels run in one call."""
+    from streaming_data_loader_amd.device import DeviceBatcher
+    db = DeviceBatcher(batch_size=8, sequence_length=128)
+    lines = [line for line, _ in long_lines()] + [line for line, _ in HAND]
+    random.Random(5).shuffle(lines)
+    buf = b"\n".join(lines)
+    recs, out, _ = device_records(torch, db, buf)
+    want, n_lines, n_bad = J.json_text(buf)
+    assert (out.n_lines, out.n_invalid, out.n_records) == (n_lines, n_bad, len(want))
+    assert recs == want
