@@ -643,10 +643,39 @@ def end_to_end_frames(db, records, order, dev, stream, task_name, nbytes=64 << 2
             best = dt if best is None else min(best, dt)
         info = {"records": int(jt.n_records), "rows": rows, "frames": len(fr), "frame_bytes": total}
     assert info["records"] == len(lines)
-    return {"MBps": round(done / best / 1e6, 2), "ms": round(best * 1e3, 2), "text_bytes": done,
-            "json_bytes": len(buf), **info,
-            "path": "pinned host JSON lines -> H2D -> JsonText filter -> tokenize+mask -> serde_pickle frames -> "
-                    "D2H to pinned host (sequential, one stream)"}
+    out = {"MBps": round(done / best / 1e6, 2), "ms": round(best * 1e3, 2), "text_bytes": done,
+           "json_bytes": len(buf), **info,
+           "path": "pinned host JSON lines -> H2D -> JsonText filter -> tokenize+mask -> serde_pickle frames -> "
+                   "D2H to pinned host (sequential, one stream)"}
+    # the same, pipelined in the library (sdl_json_to_frames): chunks cut at line ends,
+    # chunk k's frames copied out while chunk k+1 is copied in and computed
+    # the link's own rate: the frame bytes alone, device -> pinned host (the bound of this path)
+    from streaming_data_loader_amd import native
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(3):
+        native.d2h(db._h, out_host.numpy(), fr.f.d_frames, info["frame_bytes"], stream.cuda_stream)
+    d2h_s = (time.perf_counter() - t0) / 3
+    out["d2h_only"] = {"GBps": round(info["frame_bytes"] / d2h_s / 1e9, 2), "ms": round(d2h_s * 1e3, 2),
+                       "text_MBps_bound": round(done / d2h_s / 1e6, 2),
+                       "note": "hipMemcpyAsync of the frames alone: the PCIe D2H bound of this path"}
+    pinned_json = host[:len(buf)].numpy()  # the pinned copy the sequential path reads
+    for chunk_mib, src, kind in ((8, buf, "pageable"), (8, pinned_json, "pinned"), (16, pinned_json, "pinned"),
+                                 (32, pinned_json, "pinned")):
+        best_p, st = None, None
+        for r in range(reps + 1):
+            _, st = db.json_to_frames(src, chunk_bytes=chunk_mib << 20, collect=False)
+            if r:
+                best_p = st.seconds if best_p is None else min(best_p, st.seconds)
+        assert st.n_records == len(lines) and st.n_frames == info["frames"] and st.frame_bytes == info["frame_bytes"]
+        out.setdefault("pipelined", []).append(
+            {"MBps": round(done / best_p / 1e6, 2), "ms": round(best_p * 1e3, 2), "chunk_MiB": chunk_mib,
+             "input": kind, "chunks": int(st.n_chunks), "frame_GBps_d2h": round(st.frame_bytes / best_p / 1e9, 2),
+             "host_ms": {k: round(v * 1e3, 2) for k, v in zip(("json_text", "tokenize_rows", "frames_issue",
+                                                                "delivery_wait"), st.host_wait)},
+             "path": f"{kind} host JSON lines -> sdl_json_to_frames (H2D | JsonText + tokenize+mask + frames | D2H "
+                     "on three streams) -> host frames"})
+    return out
 
 
 def provider_json(db, records, order, dev, steps, warmup, step_ms):

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define SDL_ABI_VERSION 4
+#define SDL_ABI_VERSION 5
 
 enum {
     SDL_OK = 0,
@@ -212,6 +212,29 @@ typedef struct sdl_frames {
 } sdl_frames;
 int sdl_pickle_frames_device(sdl_batcher *h, const sdl_device_rows *rows, uint64_t n_rows, int flush_partial,
                              void *stream, sdl_frames *out);
+
+/* ---- End to end, host to host: JSON lines in, socket bytes out -------------
+ * The reference's Provider -> Batcher -> Transport path for a buffer of
+ * inflated JSON lines in host memory (gzip_file_provider.rs:30-50 ->
+ * provider_util.rs:60-64 -> create_batch, batcher.rs:33-77 -> zmq_transmit.rs:71):
+ * JsonText, tokenize + mask and serde_pickle frames on the device, in chunks of
+ * about chunk_bytes (cut at line ends; 0 = 8 MiB) on three streams, so one
+ * chunk's frames copy out while the next is copied in and computed.  Every
+ * frame is handed to sink(user, frame, bytes) in order (sink may be NULL: the
+ * frames still reach host memory); a non-zero return stops the call.  The
+ * frames are those of the whole buffer in one sdl_json_text_device +
+ * sdl_process_device + sdl_pickle_frames_device call: every full batch (rows
+ * short of a batch carry into the next chunk), then the partial batch when
+ * flush_partial.  Tasks mlm, clm and span (JSON lines carry no labels). */
+typedef int (*sdl_frame_sink)(void *user, const uint8_t *frame, uint64_t bytes);
+typedef struct sdl_json_frames_stats {
+    uint64_t n_lines, n_invalid, n_records, text_bytes, n_rows, n_frames, frame_bytes, n_chunks;
+    double seconds;  /* wall time of the call */
+    double host_wait[4];  /* host time in: JsonText (its sizing syncs), tokenize + mask to the row count,
+                             frames + copy-out issue, waiting for earlier copies out (delivery) */
+} sdl_json_frames_stats;
+int sdl_json_to_frames(sdl_batcher *h, const uint8_t *jsonl, uint64_t len, uint64_t chunk_bytes, int flush_partial,
+                       sdl_frame_sink sink, void *user, sdl_json_frames_stats *stats);
 
 /* Copies `bytes` from device memory (e.g. sdl_device_rows planes) to host
  * memory with the handle's HIP runtime, ordered after the handle's work on

@@ -281,7 +281,17 @@ struct sdl_batcher {
     DevBuf<uint8_t> j_text;
     DevBuf<uint64_t> j_off;
     // Transport frames (sdl_pickle_frames_device)
-    DevBuf<uint8_t> f_out;
+    DevBuf<uint8_t> f_out, f_out2;
+    DevBuf<uint8_t> *f_target = &f_out;  // where the next frames go
+    uint8_t *f_dest = nullptr;           // ... or here (device-visible, e.g. mapped pinned host memory)
+    size_t f_dest_cap = 0;
+    bool f_dry = false;                  // lay the frames out, launch nothing
+    // sdl_json_to_frames: input slots, the rows carried between chunks, streams/events
+    DevBuf<uint8_t> x_json[2];
+    PinBuf<uint8_t> x_pin_in[2], x_pin_out[2];
+    DevBuf<int32_t> x_ids[2], x_am[2], x_tt[2], x_lab[2];
+    hipStream_t x_in = nullptr, x_out = nullptr;
+    hipEvent_t x_ev[8] = {};
     DevBuf<uint4> uni_items, uni_huge;
     DevBuf<uint8_t> uni_scratch;
     DevBuf<uint8_t> h2d_text;
@@ -298,6 +308,7 @@ struct sdl_batcher {
     PinBuf<RowSeg> seg_pin;
     DevBuf<RowSeg> seg_dev;
     PinBuf<uint64_t> pin_label_off;
+    uint32_t pin_u32_err = 0;
     uint64_t n_records = 0;
 
     bool profiling = false;
@@ -333,6 +344,10 @@ struct sdl_batcher {
         for (auto &e : ev)
             if (e) (void)hipEventDestroy(e);
         for (auto &e : pipe_ev) (void)hipEventDestroy(e);
+        for (auto &e : x_ev)
+            if (e) (void)hipEventDestroy(e);
+        if (x_in) (void)hipStreamDestroy(x_in);
+        if (x_out) (void)hipStreamDestroy(x_out);
         if (stream2) (void)hipStreamDestroy(stream2);
         if (stream) (void)hipStreamDestroy(stream);
     }
@@ -1173,12 +1188,20 @@ int sdl_pickle_frames_device(sdl_batcher *h, const sdl_device_rows *rows, uint64
         fp.frame_bytes = frame_layout(fp, d, np, full_rows, false);
         fp.last_frame_bytes = frame_layout(fp, d, np, last_rows, true);
         const uint64_t total = n_frames ? (n_frames - 1) * fp.frame_bytes + fp.last_frame_bytes : 0;
-        h->f_out.ensure((size_t)total + 16);
-        fp.out = h->f_out.p;
+        uint8_t *dst = nullptr;
+        if (h->f_dest) {
+            if (!h->f_dry && (size_t)total > h->f_dest_cap) return fail(SDL_ERR_CAPACITY, "frames exceed the destination");
+            dst = h->f_dest;
+        } else if (!h->f_dry) {
+            DevBuf<uint8_t> &fo = *h->f_target;
+            fo.ensure((size_t)total + 16);
+            dst = fo.p;
+        }
+        fp.out = dst;
         hipStream_t st = stream ? (hipStream_t)stream : h->stream;
-        HIP_TRY(launch_frames(fp, st));
+        if (!h->f_dry && n_frames) HIP_TRY(launch_frames(fp, st));
         std::memset(out, 0, sizeof(*out));
-        out->d_frames = h->f_out.p;
+        out->d_frames = dst;
         out->n_frames = n_frames;
         out->frame_bytes = fp.frame_bytes;
         out->last_frame_bytes = n_frames ? fp.last_frame_bytes : 0;
@@ -1186,6 +1209,232 @@ int sdl_pickle_frames_device(sdl_batcher *h, const sdl_device_rows *rows, uint64
         return SDL_OK;
     } catch (HipError &e) {
         return fail(SDL_ERR_HIP, e.what());
+    } catch (std::exception &e) {
+        return fail(SDL_ERR_ARG, e.what());
+    }
+}
+
+// ---- End to end, host to host (north_star's path) ------------------------------
+// Host JSON lines -> H2D -> JsonText -> tokenize + mask -> serde_pickle frames ->
+// D2H -> sink, in chunks cut at line ends, on three streams: chunk k's frames
+// copy out (x_out) while chunk k + 1 is copied in (x_in) and computed (the
+// handle's stream).  Rows short of a batch at the end of a chunk are carried
+// (device to device) to the front of the next chunk's rows, so the frames are
+// exactly those of the whole buffer in one call: every full batch, then the
+// flushed partial one when flush_partial.  Record indices (RNG keys) continue
+// across chunks from cfg.first_record.
+int sdl_json_to_frames(sdl_batcher *h, const uint8_t *jsonl, uint64_t len, uint64_t chunk_bytes, int flush_partial,
+                       sdl_frame_sink sink, void *user, sdl_json_frames_stats *stats) {
+    if (!h || (!jsonl && len)) return fail(SDL_ERR_ARG, "null argument");
+    const int task = h->cfg.task;
+    if (task != SDL_TASK_MLM && task != SDL_TASK_CLM && task != SDL_TASK_SPAN)
+        return fail(SDL_ERR_UNSUPPORTED, "sdl_json_to_frames: JSON lines carry text only (mlm, clm, span)");
+    if (chunk_bytes == 0) chunk_bytes = (uint64_t)8 << 20;
+    if (chunk_bytes >= (1ull << 31)) return fail(SDL_ERR_CAPACITY, "chunk_bytes must be < 2 GiB");
+    try {
+        const auto t_start = std::chrono::steady_clock::now();
+        if (!h->x_in) HIP_TRY(hipStreamCreateWithFlags(&h->x_in, hipStreamNonBlocking));
+        if (!h->x_out) HIP_TRY(hipStreamCreateWithFlags(&h->x_out, hipStreamNonBlocking));
+        for (auto &e : h->x_ev)
+            if (!e) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        // per slot (chunk k uses slot k & 1): H2D done, rows of the chunk ready, frames written
+        hipEvent_t *e_h2d = h->x_ev, *e_rows = h->x_ev + 2, *e_frames = h->x_ev + 4;
+        const hipStream_t sc = h->stream;
+        const uint64_t B = (uint64_t)h->cfg.batch_size, S = (uint64_t)h->cfg.sequence_length;
+        const uint64_t LW = (uint64_t)h->P.label_width;
+        const bool tt = h->with_tt();
+        // chunks end at a '\n' (the last one at len)
+        std::vector<uint64_t> cut{0};
+        while (cut.back() < len) {
+            uint64_t e = cut.back() + chunk_bytes;
+            if (e >= len) { cut.push_back(len); break; }
+            const void *nl = std::memchr(jsonl + e, '\n', (size_t)(len - e));
+            cut.push_back(nl ? (uint64_t)((const uint8_t *)nl - jsonl) + 1 : len);
+        }
+        const size_t nch = cut.size() - 1;
+        // pinned input is copied in directly; pageable input is staged through pinned slots
+        bool pinned_in = false;
+        {
+            hipPointerAttribute_t pa;
+            if (len && hipPointerGetAttributes(&pa, jsonl) == hipSuccess && pa.type == hipMemoryTypeHost)
+                pinned_in = true;
+            (void)hipGetLastError();
+        }
+        uint64_t carry = 0, carry_at = 0, records = 0, lines = 0, invalid = 0, frames_total = 0, bytes_total = 0;
+        uint64_t rows_total = 0, text_total = 0;
+        struct Pending {
+            bool live = false;
+            uint64_t n_frames = 0, frame_bytes = 0, last_bytes = 0, total = 0;
+        } pend[2];
+        bool used[2] = {false, false};
+        double hw[4] = {0, 0, 0, 0};
+        auto now = [] { return std::chrono::steady_clock::now(); };
+        auto since = [&](std::chrono::steady_clock::time_point t) {
+            return std::chrono::duration<double>(now() - t).count();
+        };
+        auto deliver = [&](int slot) -> int {  // frames of the chunk in slot, once written to host memory
+            Pending &q = pend[slot];
+            if (!q.live) return 0;
+            const auto t0 = now();
+            HIP_TRY(hipEventSynchronize(e_frames[slot]));
+            hw[3] += since(t0);
+            const uint8_t *f = h->x_pin_out[slot].p;
+            for (uint64_t i = 0; i < q.n_frames; ++i) {
+                const uint64_t nb = i + 1 == q.n_frames ? q.last_bytes : q.frame_bytes;
+                if (sink && sink(user, f, nb) != 0) return fail(SDL_ERR_STATE, "sdl_json_to_frames: sink stopped");
+                f += nb;
+            }
+            q.live = false;
+            return 0;
+        };
+        for (size_t k = 0; k <= nch; ++k) {
+            const bool last = k == nch;  // the final pass only flushes the carried rows
+            const int slot = (int)(k & 1);
+            const uint64_t a = last ? len : cut[k], n = last ? 0 : cut[k + 1] - cut[k];
+            // this slot's previous frames (chunk k - 2) leave first: its buffers are reused
+            if (int rc = deliver(slot)) return rc;
+            uint64_t G = 0;
+            sdl_device_rows rows{};
+            if (n) {
+                h->x_json[slot].ensure((size_t)n + 32);
+                if (pinned_in) {
+                    HIP_TRY(hipMemsetAsync(h->x_json[slot].p + n, 0, 32, h->x_in));
+                    HIP_TRY(hipMemcpyAsync(h->x_json[slot].p, jsonl + a, (size_t)n, hipMemcpyHostToDevice, h->x_in));
+                } else {
+                    if (used[slot]) HIP_TRY(hipEventSynchronize(e_h2d[slot]));
+                    h->x_pin_in[slot].ensure((size_t)n + 32);
+                    par_copy(h->x_pin_in[slot].p, jsonl + a, (size_t)n);
+                    std::memset(h->x_pin_in[slot].p + n, 0, 32);
+                    HIP_TRY(hipMemcpyAsync(h->x_json[slot].p, h->x_pin_in[slot].p, (size_t)n + 32,
+                                           hipMemcpyHostToDevice, h->x_in));
+                }
+                HIP_TRY(hipEventRecord(e_h2d[slot], h->x_in));
+                used[slot] = true;
+                HIP_TRY(hipStreamWaitEvent(sc, e_h2d[slot], 0));
+                sdl_json_text jt;
+                auto t0 = now();
+                if (int rc = sdl_json_text_device(h, h->x_json[slot].p, n, sc, &jt)) return rc;  // syncs sc
+                hw[0] += since(t0);
+                t0 = now();
+                lines += jt.n_lines;
+                invalid += jt.n_invalid;
+                text_total += jt.text_bytes;
+                if (int rc = sdl_process_device(h, jt.d_text, jt.text_bytes, jt.d_offsets, jt.n_records,
+                                                h->cfg.first_record + records, sc, &rows))
+                    return rc;
+                records += jt.n_records;
+                uint32_t g32 = 0;
+                h->pin_u32_err = 0;
+                HIP_TRY(hipMemcpyAsync(&g32, rows.d_rows, 4, hipMemcpyDeviceToHost, sc));
+                if (rows.d_tokenize_errors)
+                    HIP_TRY(hipMemcpyAsync(&h->pin_u32_err, rows.d_tokenize_errors, 4, hipMemcpyDeviceToHost, sc));
+                HIP_TRY(hipStreamSynchronize(sc));
+                hw[1] += since(t0);
+                if (h->pin_u32_err)
+                    throw CapacityError("t5 tokenizer capacity exceeded (flags " + std::to_string(h->pin_u32_err) + ")");
+                G = g32;
+            }
+            // this pass's rows in its slot's planes: the carried rows (from the other slot), then the chunk's
+            const uint64_t have = carry + G;
+            const uint64_t cap = have + B;
+            h->x_ids[slot].ensure((size_t)(cap * S));
+            h->x_am[slot].ensure((size_t)(cap * S));
+            if (tt) h->x_tt[slot].ensure((size_t)(cap * S));
+            h->x_lab[slot].ensure((size_t)(cap * LW));
+            const int o = slot ^ 1;
+            if (carry) {
+                HIP_TRY(hipMemcpyAsync(h->x_ids[slot].p, h->x_ids[o].p + carry_at * S, carry * S * 4,
+                                       hipMemcpyDeviceToDevice, sc));
+                HIP_TRY(hipMemcpyAsync(h->x_am[slot].p, h->x_am[o].p + carry_at * S, carry * S * 4,
+                                       hipMemcpyDeviceToDevice, sc));
+                if (tt)
+                    HIP_TRY(hipMemcpyAsync(h->x_tt[slot].p, h->x_tt[o].p + carry_at * S, carry * S * 4,
+                                           hipMemcpyDeviceToDevice, sc));
+                HIP_TRY(hipMemcpyAsync(h->x_lab[slot].p, h->x_lab[o].p + carry_at * LW, carry * LW * 4,
+                                       hipMemcpyDeviceToDevice, sc));
+            }
+            if (G) {
+                HIP_TRY(hipMemcpyAsync(h->x_ids[slot].p + carry * S, rows.input_ids, G * S * 4, hipMemcpyDeviceToDevice,
+                                       sc));
+                HIP_TRY(hipMemcpyAsync(h->x_am[slot].p + carry * S, rows.attention_mask, G * S * 4,
+                                       hipMemcpyDeviceToDevice, sc));
+                if (tt)
+                    HIP_TRY(hipMemcpyAsync(h->x_tt[slot].p + carry * S, rows.token_type_ids, G * S * 4,
+                                           hipMemcpyDeviceToDevice, sc));
+                HIP_TRY(hipMemcpyAsync(h->x_lab[slot].p + carry * LW, rows.labels, G * LW * 4, hipMemcpyDeviceToDevice,
+                                       sc));
+            }
+            rows_total += G;
+            uint64_t nframe_rows = have / B * B;
+            const bool flush_now = last && flush_partial && have % B;
+            if (flush_now) {  // the partial batch: initial values past its rows
+                const uint64_t r0 = have, r1 = (have / B + 1) * B;
+                HIP_TRY(hipMemsetD32Async(h->x_ids[slot].p + r0 * S, 0, (r1 - r0) * S, sc));
+                HIP_TRY(hipMemsetD32Async(h->x_am[slot].p + r0 * S, 1, (r1 - r0) * S, sc));
+                if (tt) HIP_TRY(hipMemsetD32Async(h->x_tt[slot].p + r0 * S, 0, (r1 - r0) * S, sc));
+                HIP_TRY(hipMemsetD32Async(h->x_lab[slot].p + r0 * LW, -100, (r1 - r0) * LW, sc));
+                nframe_rows = have;
+            }
+            HIP_TRY(hipEventRecord(e_rows[slot], sc));
+            if (nframe_rows) {
+                const auto t2 = now();
+                sdl_device_rows x{};
+                x.input_ids = h->x_ids[slot].p;
+                x.attention_mask = h->x_am[slot].p;
+                x.token_type_ids = tt ? h->x_tt[slot].p : nullptr;
+                x.labels = h->x_lab[slot].p;
+                x.rows_capacity = (have / B + 1) * B;
+                x.label_width = (int32_t)LW;
+                // size the frames, then write them straight into mapped pinned host memory from the
+                // copy-out stream: no D2H copy, and the next chunk's kernels overlap the PCIe writes
+                sdl_frames fr;
+                h->f_dry = true;
+                int rc = sdl_pickle_frames_device(h, &x, nframe_rows, flush_now ? 1 : 0, h->x_out, &fr);
+                h->f_dry = false;
+                if (rc) return rc;
+                h->x_pin_out[slot].ensure((size_t)fr.total_bytes + 16);
+                void *dp = nullptr;
+                HIP_TRY(hipHostGetDevicePointer(&dp, h->x_pin_out[slot].p, 0));
+                h->f_dest = static_cast<uint8_t *>(dp);
+                h->f_dest_cap = h->x_pin_out[slot].cap;
+                HIP_TRY(hipStreamWaitEvent(h->x_out, e_rows[slot], 0));
+                rc = sdl_pickle_frames_device(h, &x, nframe_rows, flush_now ? 1 : 0, h->x_out, &fr);
+                h->f_dest = nullptr;
+                h->f_dest_cap = 0;
+                if (rc) return rc;
+                HIP_TRY(hipEventRecord(e_frames[slot], h->x_out));
+                pend[slot] = Pending{true, fr.n_frames, fr.frame_bytes, fr.last_frame_bytes, fr.total_bytes};
+                frames_total += fr.n_frames;
+                bytes_total += fr.total_bytes;
+                hw[2] += since(t2);
+            }
+            // rows short of a batch are carried into the next pass (copied from this slot)
+            const uint64_t rem = have - have / B * B;
+            carry = last ? 0 : rem;
+            carry_at = have - rem;
+            // hand over the previous chunk's frames while this one's are written
+            if (int rc = deliver(slot ^ 1)) return rc;
+        }
+        for (int sl = 0; sl < 2; ++sl)
+            if (int rc = deliver(sl)) return rc;
+        if (stats) {
+            std::memset(stats, 0, sizeof(*stats));
+            stats->n_lines = lines;
+            stats->n_invalid = invalid;
+            stats->n_records = records;
+            stats->text_bytes = text_total;
+            stats->n_rows = rows_total;
+            stats->n_frames = frames_total;
+            stats->frame_bytes = bytes_total;
+            stats->n_chunks = nch;
+            stats->seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
+            for (int i = 0; i < 4; ++i) stats->host_wait[i] = hw[i];
+        }
+        return SDL_OK;
+    } catch (HipError &e) {
+        return fail(SDL_ERR_HIP, e.what());
+    } catch (CapacityError &e) {
+        return fail(SDL_ERR_CAPACITY, e.what());
     } catch (std::exception &e) {
         return fail(SDL_ERR_ARG, e.what());
     }

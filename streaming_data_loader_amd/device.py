@@ -164,6 +164,23 @@ class DeviceBatcher:
                                                             ctypes.c_void_p(stream or None), ctypes.byref(out)))
         return DeviceFrames(self._h, out)
 
+    def json_to_frames(self, jsonl, chunk_bytes=8 << 20, flush_partial=True, collect=True):
+        """End to end, host to host (sdl_json_to_frames): JSON lines in host
+        memory -> the serde_pickle frames of every batch, pipelined in chunks.
+        Returns (list of frames or None, native.JsonFramesStats)."""
+        buf = np.frombuffer(jsonl, np.uint8) if isinstance(jsonl, (bytes, bytearray)) else np.ascontiguousarray(jsonl)
+        frames = [] if collect else None
+
+        def sink(_user, ptr, n):
+            frames.append(ctypes.string_at(ptr, n))
+            return 0
+        cb = native.FRAME_SINK(sink) if collect else ctypes.cast(None, native.FRAME_SINK)
+        st = native.JsonFramesStats()
+        native.check(native.load().sdl_json_to_frames(self._h, buf.ctypes.data if buf.size else None, buf.size,
+                                                      chunk_bytes, 1 if flush_partial else 0, cb, None,
+                                                      ctypes.byref(st)))
+        return frames, st
+
     def process_tensors(self, text, offsets, first_record=0, stream=None):
         """text: uint8 cuda tensor; offsets: int64 cuda tensor of n_records+1 entries."""
         s = stream.cuda_stream if stream is not None else 0

@@ -21,7 +21,7 @@ EXPORTS = [
     "sdl_config_default", "sdl_batcher_create", "sdl_batcher_destroy", "sdl_batcher_push",
     "sdl_batcher_push_many", "sdl_batcher_next", "sdl_batcher_flush", "sdl_batch_release",
     "sdl_process_device", "sdl_process_device_labels", "sdl_json_text_device", "sdl_pickle_frames_device", "sdl_device_to_host", "sdl_set_profiling", "sdl_stage_times",
-    "sdl_tokenizer_info_get", "sdl_last_error", "sdl_abi_version",
+    "sdl_tokenizer_info_get", "sdl_last_error", "sdl_abi_version", "sdl_json_to_frames",
 ]
 
 
@@ -76,6 +76,18 @@ class Frames(ctypes.Structure):
     ]
 
 
+class JsonFramesStats(ctypes.Structure):
+    _fields_ = [
+        ("n_lines", ctypes.c_uint64), ("n_invalid", ctypes.c_uint64), ("n_records", ctypes.c_uint64),
+        ("text_bytes", ctypes.c_uint64), ("n_rows", ctypes.c_uint64), ("n_frames", ctypes.c_uint64),
+        ("frame_bytes", ctypes.c_uint64), ("n_chunks", ctypes.c_uint64), ("seconds", ctypes.c_double),
+        ("host_wait", ctypes.c_double * 4),
+    ]
+
+
+FRAME_SINK = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint8), ctypes.c_uint64)
+
+
 class TokenizerInfo(ctypes.Structure):
     _fields_ = [
         ("kind", ctypes.c_int32), ("vocab_size", ctypes.c_int32), ("n_added", ctypes.c_int32),
@@ -119,6 +131,8 @@ def load(path=LIB_PATH):
     L.sdl_device_to_host.argtypes = [vp, vp, vp, sz, vp]
     L.sdl_json_text_device.argtypes = [vp, vp, u64, vp, ctypes.POINTER(JsonText)]
     L.sdl_pickle_frames_device.argtypes = [vp, ctypes.POINTER(DeviceRows), u64, i64, vp, ctypes.POINTER(Frames)]
+    L.sdl_json_to_frames.argtypes = [vp, vp, u64, u64, i64, FRAME_SINK, vp, ctypes.POINTER(JsonFramesStats)]
+    L.sdl_json_to_frames.restype = i64
     L.sdl_set_profiling.argtypes = [vp, i64]
     L.sdl_stage_times.argtypes = [vp, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_float), i64]
     L.sdl_last_error.restype = ctypes.c_char_p

@@ -213,3 +213,32 @@ def test_long_lines_on_device(torch, native_lib):
     want, n_lines, n_bad = J.json_text(buf)
     assert (out.n_lines, out.n_invalid, out.n_records) == (n_lines, n_bad, len(want))
     assert recs == want
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("task,S,B,chunk", [("mlm", 128, 8, 20000), ("mlm", 512, 16, 65536), ("clm", 256, 4, 9000),
+                                            ("span", 128, 8, 30000), ("mlm", 128, 8, 1 << 30)])
+def test_json_to_frames_equals_one_call(torch, native_lib, records, task, S, B, chunk):
+    """sdl_json_to_frames (chunks cut at line ends, rows carried across chunks,
+    copies overlapped on three streams) hands the sink exactly the frames of
+    one whole-buffer call: JsonText -> process -> pickle frames (flush)."""
+    from streaming_data_loader_amd import native
+    from streaming_data_loader_amd.device import DeviceBatcher
+    kind = {"mlm": native.SDL_TASK_MLM, "clm": native.SDL_TASK_CLM, "span": native.SDL_TASK_SPAN}[task]
+    tok = {"clm": native.GPT2_PROXY_TOKENIZER, "span": native.T5_PROXY_TOKENIZER}.get(task, native.BERT_PROXY_TOKENIZER)
+    lines = fixture_jsonl(records, 7) * 3 + [line for line, _ in HAND] + [line for line, _ in long_lines()[:20]]
+    random.Random(11).shuffle(lines)
+    buf = b"\n".join(lines) + b"\n"
+    db = DeviceBatcher(task=kind, batch_size=B, sequence_length=S, seed=42, tokenizer=tok)
+    d = to_dev(torch, buf)
+    jt = db.json_text(d.data_ptr(), len(buf))
+    res = db.process(jt.d_text, int(jt.text_bytes), jt.d_offsets, int(jt.n_records))
+    torch.cuda.synchronize()
+    want = db.pickle_frames(res, res.rows(), True).frames()
+    db2 = DeviceBatcher(task=kind, batch_size=B, sequence_length=S, seed=42, tokenizer=tok)
+    got, st = db2.json_to_frames(buf, chunk_bytes=chunk)
+    assert st.n_records == jt.n_records and st.n_invalid == jt.n_invalid and st.n_lines == jt.n_lines
+    assert st.n_chunks >= (2 if chunk < len(buf) else 1)
+    assert len(got) == len(want) and st.n_frames == len(want)
+    for i, (a, b) in enumerate(zip(got, want)):
+        assert a == b, f"frame {i} of {len(want)}"
