@@ -31,7 +31,7 @@ static int utab_load(utab *u, const char *path) {
     if (!f) return -1;
     char magic[4];
     uint32_t hdr[4];
-    if (fread(magic, 1, 4, f) != 4 || memcmp(magic, "SDLU", 4) || fread(hdr, 4, 4, f) != 4 || hdr[0] != 1) {
+    if (fread(magic, 1, 4, f) != 4 || memcmp(magic, "SDLU", 4) || fread(hdr, 4, 4, f) != 4 || hdr[0] != 2) {
         fclose(f);
         return -1;
     }
@@ -220,12 +220,52 @@ static void wordpiece(const orc_tok *t, const uint8_t *w, size_t L, size_t nchar
     }
 }
 
+/* NFD canonical ordering of the combining marks strip_accents keeps
+ * (unicode-normalization's decompose + stable sort by ccc, then the Mn filter):
+ * kept marks (table bit 4 + ccc) wait in a run, which ends -- sorted, stable --
+ * at any char holding a starter (bit 4 on a DEL char: a removed starter). */
+typedef struct {
+    uint8_t bytes[64][4];
+    uint8_t len[64], ccc[64];
+    int n;
+} mark_run;
+
+static void run_flush(mark_run *r, uint8_t *word, size_t *wl, size_t cap, int *overflow) {
+    for (int pass = 1; pass < r->n; ++pass)  /* insertion sort: stable */
+        for (int j = pass; j > 0 && r->ccc[j - 1] > r->ccc[j]; --j) {
+            uint8_t tb[4], tl = r->len[j], tc = r->ccc[j];
+            memcpy(tb, r->bytes[j], 4);
+            memcpy(r->bytes[j], r->bytes[j - 1], 4);
+            r->len[j] = r->len[j - 1];
+            r->ccc[j] = r->ccc[j - 1];
+            memcpy(r->bytes[j - 1], tb, 4);
+            r->len[j - 1] = tl;
+            r->ccc[j - 1] = tc;
+        }
+    for (int k = 0; k < r->n; ++k) {
+        if (*wl + r->len[k] > cap) *overflow = 1;
+        else { memcpy(word + *wl, r->bytes[k], r->len[k]); *wl += r->len[k]; }
+    }
+    r->n = 0;
+}
+
+static void run_push(mark_run *r, const uint8_t *b, int len, int ccc, uint8_t *word, size_t *wl, size_t cap,
+                     int *overflow) {
+    if (r->n == 64) run_flush(r, word, wl, cap, overflow); /* > 64 marks in a row: the word is [UNK] anyway */
+    memcpy(r->bytes[r->n], b, (size_t)len);
+    r->len[r->n] = (uint8_t)len;
+    r->ccc[r->n] = (uint8_t)ccc;
+    r->n++;
+}
+
 /* BertNormalizer + BertPreTokenizer over one non-special segment, feeding each
  * word to WordPiece.  Per-char behaviour comes from the probed table. */
 static void encode_segment(const orc_tok *t, const uint8_t *s, size_t n, idvec *out) {
     uint8_t word[4096];
     size_t wl = 0, wc = 0;
     int overflow = 0;
+    mark_run run;
+    run.n = 0;
     size_t i = 0;
     while (i < n) {
         uint32_t cp;
@@ -241,8 +281,12 @@ static void encode_segment(const orc_tok *t, const uint8_t *s, size_t n, idvec *
             mb = pe + 2;
         }
         i += (size_t)len;
-        if (cls == C_DEL) continue;
+        if (cls == C_DEL) {
+            if (e & 16) run_flush(&run, word, &wl, sizeof(word), &overflow); /* a removed starter */
+            continue;
+        }
         if (cls == C_WS || cls == C_ISO) {
+            run_flush(&run, word, &wl, sizeof(word), &overflow);
             if (wl || overflow) {
                 if (overflow) idpush(out, (uint32_t)t->unk);
                 else wordpiece(t, word, wl, wc, out);
@@ -253,10 +297,33 @@ static void encode_segment(const orc_tok *t, const uint8_t *s, size_t n, idvec *
             continue;
         }
         /* OTHER: extend the current word */
+        wc += mc;
+        if (e & 16) {
+            if (e & 4) { /* a kept mark */
+                run_push(&run, mb, (int)ml, (int)((e >> 8) & 0xFF), word, &wl, sizeof(word), &overflow);
+                continue;
+            }
+            /* precomposed: its starters end the run, its kept marks join it */
+            for (size_t q = 0; q < ml;) {
+                uint32_t c2;
+                int l2 = utf8_decode(mb, ml, q, &c2);
+                uint32_t e2 = utab_get(&t->u, c2);
+                if ((e2 & 16) && (e2 & 4) && (e2 & 3) == C_OTHER) {
+                    run_push(&run, mb + q, l2, (int)((e2 >> 8) & 0xFF), word, &wl, sizeof(word), &overflow);
+                } else {
+                    run_flush(&run, word, &wl, sizeof(word), &overflow);
+                    if (wl + (size_t)l2 > sizeof(word)) overflow = 1;
+                    else { memcpy(word + wl, mb + q, (size_t)l2); wl += (size_t)l2; }
+                }
+                q += (size_t)l2;
+            }
+            continue;
+        }
+        run_flush(&run, word, &wl, sizeof(word), &overflow);
         if (wl + ml > sizeof(word)) overflow = 1; /* > 100 chars for sure */
         else { memcpy(word + wl, mb, ml); wl += ml; }
-        wc += mc;
     }
+    run_flush(&run, word, &wl, sizeof(word), &overflow);
     if (overflow) idpush(out, (uint32_t)t->unk);
     else if (wl) wordpiece(t, word, wl, wc, out);
 }

@@ -46,7 +46,7 @@ static void load_unicode(const std::string &path, HostTokenizer &t) {
     if (d.size() < 20 || std::memcmp(d.data(), "SDLU", 4) != 0) throw std::runtime_error("bad unicode table " + path);
     uint32_t hdr[4];
     std::memcpy(hdr, d.data() + 4, 16);
-    if (hdr[0] != 1) throw std::runtime_error("unicode table version mismatch");
+    if (hdr[0] != 2) throw std::runtime_error("unicode table version mismatch (tools/make_unicode_tables.py)");
     const size_t np = hdr[1], nb = hdr[2], pb = hdr[3];
     if (np != 0x110000 / 128 || d.size() != 20 + 2 * np + 4 * 128 * nb + pb)
         throw std::runtime_error("unicode table size mismatch");
@@ -180,11 +180,15 @@ static void set_added(HostTokenizer &t) {
 // Device entry format: the file's entries with short normalizations (<= 3
 // bytes) moved inline -- bits 0-1 class, bit 2 identity, bit 3 inline,
 // bits 4-5 nbytes-1, 6-7 nchars-1, 8-31 the bytes; longer ones keep the pool
-// offset in bits 8-31.  Plus a flat copy of the BMP so one load resolves it.
+// offset in bits 8-31.  Canonical-ordering entries (file bit 4: kept marks with
+// their ccc in bits 8-15, precomposed chars holding them, removed starters) are
+// never inlined, so on the device (e & 24) == 16 identifies them.  Plus a flat
+// copy of the BMP so one load resolves it.
 static void to_device_entries(HostTokenizer &t) {
     for (uint32_t &e : t.uentry) {
         const uint32_t cls = e & 3u;
-        if ((e & 4u) || cls == UC_WS || cls == UC_DEL) continue;
+        // bit 4 (canonical ordering) entries stay as they are: (e & 24) == 16 marks them
+        if ((e & 4u) || (e & 16u) || cls == UC_WS || cls == UC_DEL) continue;
         const uint32_t off = e >> 8;
         const uint32_t nb = t.upool[off], nc = t.upool[off + 1];
         if (nb >= 1 && nb <= 3 && nc >= 1 && nc <= 4) {

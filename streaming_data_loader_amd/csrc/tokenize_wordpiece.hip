@@ -136,6 +136,10 @@ __device__ __forceinline__ int append_norm(const Ctx &C, uint32_t e, int64_t p, 
     return nb + m;
 }
 
+__device__ __forceinline__ int utf8_len(uint32_t lead) {
+    return lead < 0x80u ? 1 : (lead & 0xE0u) == 0xC0u ? 2 : (lead & 0xF0u) == 0xE0u ? 3 : 4;
+}
+
 // General WORD piece: runs over OTHER and invisible chars until a WS/ISO char,
 // an added token or the record end; materialized in private memory.
 __device__ int word_general(const Ctx &C, int64_t p, int64_t rec_end, lds_u16 *out) {
@@ -169,19 +173,91 @@ __device__ int word_general(const Ctx &C, int64_t p, int64_t rec_end, lds_u16 *o
     }
     uint8_t buf[MAX_WORD_BYTES];
     int nb = 0;
+    // NFD canonical ordering of the kept combining marks: a run of them is
+    // appended to buf as it comes and sorted in place (stable, by ccc) when a
+    // starter -- kept, removed or inside a precomposed char -- ends it
+    int run = -1;
+    auto ccc_at = [&](int x, int l) {
+        uint32_t cp = l == 2 ? buf[x] & 0x1Fu : l == 3 ? buf[x] & 0x0Fu : buf[x] & 0x07u;
+        for (int k = 1; k < l; ++k) cp = (cp << 6) | (buf[x + k] & 0x3Fu);
+        return (uentry(T, cp) >> 8) & 0xFFu;
+    };
+    auto flush = [&]() {
+        if (run < 0) return;
+        for (bool swapped = true; swapped;) {
+            swapped = false;
+            for (int x = run; x < nb;) {
+                const int l1 = utf8_len(buf[x]);
+                if (x + l1 >= nb) break;
+                const int l2 = utf8_len(buf[x + l1]);
+                if (ccc_at(x, l1) > ccc_at(x + l1, l2)) {
+                    uint8_t t[4];
+                    for (int k = 0; k < l1; ++k) t[k] = buf[x + k];
+                    for (int k = 0; k < l2; ++k) buf[x + k] = buf[x + l1 + k];
+                    for (int k = 0; k < l1; ++k) buf[x + l2 + k] = t[k];
+                    swapped = true;
+                    x += l2;
+                } else {
+                    x += l1;
+                }
+            }
+        }
+        run = -1;
+    };
+    auto push = [&](uint32_t bytes, int l) {
+        if (run < 0) run = nb;
+        for (int k = 0; k < l; ++k) buf[nb++] = (uint8_t)(bytes >> (8 * k));
+    };
     for (int64_t q = p; q < i;) {
         const uint32_t b = C.byte(q);
         if (b < 0x80u) {
-            if (ascii_vclass(b) == V_OTHER) buf[nb++] = (uint8_t)((b - 'A' < 26u) ? b + 32u : b);
+            if (ascii_vclass(b) == V_OTHER) {
+                flush();
+                buf[nb++] = (uint8_t)((b - 'A' < 26u) ? b + 32u : b);
+            }
             ++q;
             continue;
         }
         if ((b & 0xC0u) == 0x80u) { ++q; continue; }
         int len;
         const uint32_t e = uentry(T, decode(C, q, b, &len));
-        if ((e & 3u) == UC_OTHER) nb = append_norm(C, e, q, len, buf, nb);
+        const uint32_t cls = e & 3u;
+        if ((e & 24u) == 16u) {  // canonical ordering entry
+            if (cls == UC_DEL) {
+                flush();  // a removed starter ends the run
+            } else if (e & 4u) {  // a kept mark
+                uint32_t bytes = 0;
+                for (int k = 0; k < len; ++k) bytes |= C.byte(q + k) << (8 * k);
+                push(bytes, len);
+            } else {  // precomposed: its starters end the run, its kept marks join it
+                const uint8_t *pe = T.upool + (e >> 8);
+                const int m = pe[0];
+                for (int x = 0; x < m;) {
+                    const uint32_t lead = pe[2 + x];
+                    const int l = utf8_len(lead);
+                    uint32_t cp = l == 1 ? lead : l == 2 ? lead & 0x1Fu : l == 3 ? lead & 0x0Fu : lead & 0x07u;
+                    uint32_t bytes = lead;
+                    for (int k = 1; k < l; ++k) {
+                        cp = (cp << 6) | (pe[2 + x + k] & 0x3Fu);
+                        bytes |= (uint32_t)pe[2 + x + k] << (8 * k);
+                    }
+                    const uint32_t e2 = uentry(T, cp);
+                    if ((e2 & 24u) == 16u && (e2 & 4u) && (e2 & 3u) == UC_OTHER) {
+                        push(bytes, l);
+                    } else {
+                        flush();
+                        for (int k = 0; k < l; ++k) buf[nb++] = (uint8_t)(bytes >> (8 * k));
+                    }
+                    x += l;
+                }
+            }
+        } else if (cls == UC_OTHER) {
+            flush();
+            nb = append_norm(C, e, q, len, buf, nb);
+        }
         q += len;
     }
+    flush();
     return wordpiece_general(T, buf, nb, out);
 }
 
@@ -219,6 +295,7 @@ __device__ bool normalize_w16(const Ctx &C, int64_t p, int64_t rec_end, bool iso
         int len;
         const uint32_t e = uentry(T, decode(C, i, b, &len));
         const uint32_t c = e & 3u;
+        if (c == UC_OTHER && (e & 24u) == 16u) return false;  // canonical ordering: the general path
         if (iso || c == UC_OTHER) {
             if (e & 4u) {
                 if (nb + len > 16) return false;

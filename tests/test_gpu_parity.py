@@ -154,6 +154,38 @@ def test_tokenizer_on_hard_records(torch, native_lib, oracle_tok):
     assert (lab == -100).all()
 
 
+def test_canonical_ordering_on_device(torch, native_lib):
+    """NFD canonical ordering of kept combining marks (tests/golden/
+    bert_marks_ids.json, widened vocab): every golden case as its own record,
+    then the cases joined into long records so mark runs straddle chunk seams
+    (checked against the oracle, pinned by the same goldens)."""
+    import json
+    g = json.load(open(os.path.join(GOLDEN, "bert_marks_ids.json"), encoding="utf-8"))
+    tj = os.path.join(GOLDEN, "bert_marks", "tokenizer.json")
+    tok = oracle_lib.Tok(vocab=os.path.join(GOLDEN, "bert_marks", "vocab.txt"))
+    texts = [c["text"] for c in g["cases"]]
+
+    class Golden:
+        ids = {c["text"]: c["ids"] for c in g["cases"]}
+
+        def encode(self, t):
+            return self.ids[t]
+
+    rng = random.Random(7)
+    long_texts = []
+    for _ in range(24):
+        sel = rng.sample(texts, 120)
+        long_texts.append(rng.choice(["", " ", "x"]).join(sel))
+    for batch, want_tok in ((texts, Golden()), (long_texts, tok)):
+        db = DeviceBatcher(batch_size=16, sequence_length=128, mask_length=0, min_ids=0, tokenizer=tj)
+        ids = run_device(torch, db, batch).planes()[0]
+        want = framed_rows(want_tok, batch, 128)
+        assert ids.shape == want.shape
+        bad = np.nonzero((ids != want).any(axis=1))[0]
+        assert bad.size == 0, f"{bad.size} rows differ, first {bad[:5]}"
+        db.close()
+
+
 @pytest.mark.parametrize("feature", ["[SEP]", "é", "中", "\U0001f600", "\x00", "​", " ", "!", "supercalifragilisticexpialidocious"])
 def test_chunk_boundary_straddle(torch, native_lib, oracle_tok, feature):
     """Put `feature` across every position near the 4096-byte chunk seams,

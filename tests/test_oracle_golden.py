@@ -27,6 +27,18 @@ def test_oracle_matches_tokenizers_goldens(oracle_tok, bert_goldens):
     assert not bad, f"{len(bad)} mismatches, e.g. {bad[:3]}"
 
 
+def test_oracle_canonical_ordering_goldens():
+    """Kept combining marks leave the normalizer in ccc order (NFD canonical
+    ordering); a widened vocab makes that order show in the ids --
+    tests/golden/make_reorder_goldens.py."""
+    import json
+    g = json.load(open(os.path.join(GOLDEN, "bert_marks_ids.json"), encoding="utf-8"))
+    assert g["n_reordered"] > 100
+    tok = oracle_lib.Tok(vocab=os.path.join(GOLDEN, "bert_marks", "vocab.txt"))
+    bad = [c["text"] for c in g["cases"] if tok.encode(c["text"]) != c["ids"]]
+    assert not bad, f"{len(bad)} mismatches, e.g. {[ascii(t) for t in bad[:3]]}"
+
+
 def test_oracle_special_ids_layout(oracle_tok):
     # [CLS] ... [SEP] template; literal added tokens map to their ids
     assert oracle_tok.encode("") == [101, 102]

@@ -4,10 +4,10 @@
 The reference's tokenizer arithmetic lives in the third-party crate
 `tokenizers 0.13.1` (`rust/Cargo.lock`), not vendored.  Its BertNormalizer
 (clean_text, handle_chinese_chars, strip_accents=None->lowercase, lowercase)
-and BertPreTokenizer are context-free per codepoint (NFD canonical re-ordering
-of non-Mn combining marks excepted), so they are captured here
-as tables by probing EVERY codepoint through the same project's Python binding
-(`tokenizers 0.22.2`, the version importable in this container):
+and BertPreTokenizer are context-free per codepoint except for the NFD
+canonical re-ordering of combining marks that strip_accents keeps, so they are
+captured here as tables by probing EVERY codepoint through the same project's
+Python binding (`tokenizers 0.22.2`, the version importable in this container):
 
   N(c)  = BertNormalizer(lowercase=True).normalize_str(chr(c))
   class = how BertPreTokenizer treats N(c):
@@ -18,16 +18,27 @@ as tables by probing EVERY codepoint through the same project's Python binding
           OTHER word character; its normalized bytes are N(c)
 
 Binary layout (little endian), read by oracle/ and by the HIP library:
-  char[4] "SDLU", u32 version=1, u32 n_pages, u32 n_blocks, u32 pool_bytes
+  char[4] "SDLU", u32 version=2, u32 n_pages, u32 n_blocks, u32 pool_bytes
   u16 page[n_pages]                  block index for codepoints [p*128, p*128+128)
   u32 entry[n_blocks*128]            bits 0-1 class (0 OTHER,1 WS,2 ISO,3 DEL)
                                      bit 2   identity (N(c) == chr(c))
+                                     bit 4   canonical ordering (NFD) flag, below
                                      bits 8-31 pool offset of N(c) (if not identity)
   u8  pool[pool_bytes]               at each offset: u8 nbytes, u8 nchars, bytes
+
+Canonical ordering (version 2, bit 4).  NFD sorts every run of combining marks
+(ccc > 0) by ccc before strip_accents drops the Mn ones, so the marks it KEEPS
+come out of a run in ccc order.  Probed the same way (N("x" + M226 + c + M216)):
+  - a kept mark (identity, ccc > 0): bit 4, ccc in bits 8-15;
+  - a char whose N(c) contains a kept mark (a precomposed char): bit 4;
+  - a DEL char that still ends a run (a removed starter, e.g. an Mn with ccc 0):
+    bit 4; other DEL chars (clean_text removals, Mn with ccc > 0) do not.
+Everything else either holds a starter (ends the run) or is removed.
 """
 import os
 import struct
 import sys
+import unicodedata
 
 from tokenizers import normalizers, pre_tokenizers
 
@@ -101,6 +112,40 @@ def main():
     if mixed:
         print("mixed-class codepoints (handled as OTHER):", len(mixed), mixed[:10], file=sys.stderr)
 
+    # canonical ordering flags (bit 4), probed: H (ccc 226) and L (ccc 216) are kept marks
+    H, L = "\U0001D16D", "\U0001D165"
+    kept_ccc = {}
+    for cp in range(0x110000):
+        if 0xD800 <= cp <= 0xDFFF:
+            continue
+        c = chr(cp)
+        n = norm.normalize_str(c)
+        r = norm.normalize_str("x" + H + c + L)
+        if n == "":
+            if r == "x" + H + L:
+                entries[cp] |= 16  # a removed starter: ends the run
+            elif r != "x" + L + H:
+                raise RuntimeError(f"U+{cp:04X}: unexpected ordering {r!r}")
+            continue
+        if r == "x" + H + n + L:
+            continue  # holds a starter
+        ccc = unicodedata.combining(c)
+        if n != c or ccc == 0:
+            raise RuntimeError(f"U+{cp:04X}: reorders but is not a known kept mark")
+        want = "x" + "".join(m for _, m in sorted([(226, H), (ccc, c), (216, L)], key=lambda t: t[0]))
+        if r != want:
+            raise RuntimeError(f"U+{cp:04X}: ccc {ccc} does not explain {r!r}")
+        kept_ccc[cp] = ccc
+        entries[cp] = (entries[cp] & ~0xFFFFFF00) | 16 | (ccc << 8)
+    for cp in range(0x110000):
+        e = entries[cp]
+        if (e & 3) == OTHER and not (e & 4) and any(ord(x) in kept_ccc for x in norm.normalize_str(chr(cp))):
+            entries[cp] |= 16  # precomposed: its decomposition holds kept marks
+    print(f"canonical ordering: {len(kept_ccc)} kept marks, "
+          f"{sum(1 for e in entries if (e & 3) == DEL and e & 16)} removed starters, "
+          f"{sum(1 for cp, e in enumerate(entries) if (e & 3) == OTHER and e & 16 and cp not in kept_ccc)} "
+          f"precomposed", file=sys.stderr)
+
     pages, blocks, block_index = [], [], {}
     for p in range(0x110000 // 128):
         blk = tuple(entries[p * 128:(p + 1) * 128])
@@ -112,7 +157,7 @@ def main():
         pages.append(bi)
     os.makedirs(os.path.dirname(OUT), exist_ok=True)
     with open(OUT, "wb") as f:
-        f.write(b"SDLU" + struct.pack("<IIII", 1, len(pages), len(blocks), len(pool)))
+        f.write(b"SDLU" + struct.pack("<IIII", 2, len(pages), len(blocks), len(pool)))
         f.write(struct.pack(f"<{len(pages)}H", *pages))
         for blk in blocks:
             f.write(struct.pack("<128I", *blk))
