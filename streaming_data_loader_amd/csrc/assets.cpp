@@ -108,6 +108,9 @@ static void build_vocab_table(HostTokenizer &t) {
     std::vector<VSlot> entries;
     t.vpool.clear();
     t.maxlen_first = t.maxlen_cont = 0;
+    t.wp_lens[0].clear();
+    t.wp_lens[1].clear();
+    t.wp_long_pieces = false;
     for (size_t id = 0; id < n; ++id) {
         const std::string &s = t.pieces[id];
         if (s.empty() || last[s] != (int)id) continue;
@@ -116,6 +119,9 @@ static void build_vocab_table(HostTokenizer &t) {
         if (pay.size() > 255) throw std::runtime_error("vocabulary piece longer than 255 bytes");
         if (cont) t.maxlen_cont = std::max(t.maxlen_cont, (int)pay.size());
         else t.maxlen_first = std::max(t.maxlen_first, (int)pay.size());
+        if (pay.size() > (size_t)LW_MAX) t.wp_long_pieces = true;
+        else if (std::find(t.wp_lens[cont].begin(), t.wp_lens[cont].end(), (uint8_t)pay.size()) == t.wp_lens[cont].end())
+            t.wp_lens[cont].push_back((uint8_t)pay.size());
         VSlot v{};
         v.key = (uint32_t)pay.size() | (cont << 8);
         v.id = (int32_t)id;

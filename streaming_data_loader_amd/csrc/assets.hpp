@@ -31,6 +31,8 @@ struct HostTokenizer {
     std::vector<int32_t> ascii_id;  // id of the one-byte word b (ISO ASCII fast path)
     uint32_t slot_mask = 0;
     int maxlen_first = 0, maxlen_cont = 0;
+    std::vector<uint8_t> wp_lens[2];  // WordPiece: distinct payload lengths <= LW_MAX (non-"##", "##")
+    bool wp_long_pieces = false;      // a payload longer than LW_MAX exists
     uint32_t opener = 0;
     int max_special_len = 0;
 

@@ -33,6 +33,8 @@ constexpr int PEND_CAP = SDL_PEND_CAP;            // WordPiece pieces pending th
 constexpr int RB_CAP = 256;                       // record starts listed in LDS per window
 constexpr int MAX_WORD_CHARS = 100;               // WordPiece max_input_chars_per_word
 constexpr int MAX_WORD_BYTES = 4 * MAX_WORD_CHARS + 8;
+constexpr int LW_MAX = 96;   // WordPiece: longest normalized word for the LDS lattice (bytes)
+constexpr int LW_BUF = 128;  // ... its byte buffer (LW_MAX + 20 readable), then u32 best[LW_MAX]
 
 constexpr int MAX_SPECIAL = 8;
 constexpr int MAX_SPECIAL_LEN = 24;
@@ -79,6 +81,7 @@ __host__ __device__ inline uint32_t cuckoo_slot2(uint32_t h, uint32_t mask) {
     return g & mask;
 }
 static_assert(sizeof(VSlot) == 32, "VSlot must be 32 bytes");
+static_assert(PEND_CAP % 64 == 0 && 2 * PEND_CAP >= LW_BUF + 4 * LW_MAX, "the WordPiece lattice buffer reuses the pending list");
 
 // Byte-level BPE merge table (cuckoo, 2 slots of 8 B): key = left id << 16 |
 // right id, val = rank << 16 | merged id; empty slot key = 0xFFFFFFFF.
@@ -130,6 +133,9 @@ struct DevTok {
     int32_t unk_id;
     int32_t maxlen_first;    // longest non-"##" piece (bytes)
     int32_t maxlen_cont;     // longest "##" piece without the prefix (bytes)
+    int32_t wp_nlens[2];     // WordPiece: distinct payload lengths <= LW_MAX of non-"##" / "##" pieces,
+    const uint8_t *wp_lens;  // ... ascending: [0, LW_MAX) non-"##", [LW_MAX, 2 LW_MAX) "##"
+    int32_t wp_long_pieces;  // some piece payload is longer than LW_MAX
     int32_t n_special;       // added tokens matched on the raw text
     int32_t max_special_len;
     uint32_t opener;         // first byte shared by every added token

@@ -251,6 +251,7 @@ struct sdl_batcher {
     DevBuf<uint8_t> d_upool, d_vpool;
     DevBuf<VSlot> d_slots, d_wslots;
     DevBuf<int32_t> d_ascii_id;
+    DevBuf<uint8_t> d_wp_lens;
     DevBuf<uint16_t> d_gpage, d_byte_id;
     DevBuf<uint8_t> d_gblock;
     DevBuf<MSlot> d_mslots;
@@ -824,6 +825,19 @@ int sdl_batcher_create(const sdl_config *cfg, const char *tokenizer_path, const 
         d.unk_id = t.unk_id;
         d.maxlen_first = t.maxlen_first;
         d.maxlen_cont = t.maxlen_cont;
+        {
+            std::vector<uint8_t> all(2 * LW_MAX, 0);
+            for (int c = 0; c < 2; ++c) {
+                std::vector<uint8_t> lens = t.wp_lens[c];
+                std::sort(lens.begin(), lens.end());
+                d.wp_nlens[c] = (int32_t)lens.size();
+                std::copy(lens.begin(), lens.end(), all.begin() + c * LW_MAX);
+            }
+            h->d_wp_lens.ensure(all.size());
+            HIP_TRY(hipMemcpy(h->d_wp_lens.p, all.data(), all.size(), hipMemcpyHostToDevice));
+            d.wp_lens = h->d_wp_lens.p;
+        }
+        d.wp_long_pieces = t.wp_long_pieces ? 1 : 0;
         d.ascii_id = h->d_ascii_id.p;
         d.n_special = (int)t.added.size();
         d.max_special_len = t.max_special_len;

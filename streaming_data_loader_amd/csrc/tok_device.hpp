@@ -33,7 +33,7 @@ struct Ctx {
         return r;
     }
     // true when a record starts at p (0 <= p <= N)
-    __device__ bool rstart(int64_t p) const {
+    __device__ __forceinline__ bool rstart(int64_t p) const {
         if (in_win(p)) {
             const int i = (int)(p - w0);
             return (rbits[i >> 5] >> (i & 31)) & 1u;
@@ -122,7 +122,7 @@ __device__ __forceinline__ uint32_t decode(const Ctx &C, int64_t p, uint32_t b, 
 // Longest added token starting at p that does not cross a record start; -1 if
 // none.  Added tokens never overlap: their first byte occurs nowhere else in
 // them (checked on the host), so leftmost-longest matching is local.
-__device__ int special_match(const Ctx &C, int64_t p) {
+__device__ __forceinline__ int special_match(const Ctx &C, int64_t p) {
     const DevTok &T = *C.T;
     int best = -1, best_len = 0;
     for (int k = 0; k < T.n_special; ++k) {
@@ -163,7 +163,7 @@ __device__ __forceinline__ uint32_t hash16(const W16 &c, uint32_t n, uint32_t co
 }
 
 // General probe: payload = w[start, end) of a byte buffer (any length).
-__device__ int probe_general(const DevTok &T, const uint8_t *w, int start, int end, uint32_t cont) {
+__device__ __forceinline__ int probe_general(const DevTok &T, const uint8_t *w, int start, int end, uint32_t cont) {
     const uint32_t n = (uint32_t)(end - start);
     uint32_t h = hinit(n, cont);
     W16 first{0, 0, 0, 0};

@@ -271,6 +271,53 @@ __device__ int bpe_wave(const DevTok &T, uint32_t &sym, int n, lds_u16 *tmp) {
     return n;
 }
 
+// Segmented form: lanes < n hold the byte symbols of several words, each word
+// a run of lanes starting at a set bit of `heads` (bit 0 set).  Every word
+// runs bpe_wave's steps independently and at once: per word the lowest rank
+// among its adjacent pairs, all its non-overlapping occurrences merged left to
+// right.  Pairs never straddle a word, so the runs of candidate bits do not
+// either and one leftmost_alternating serves every word.  Returns the final
+// symbol count; `heads` then marks where each word's ids start.
+__device__ int bpe_wave_seg(const DevTok &T, uint32_t &sym, int n, uint64_t &heads, lds_u16 *tmp) {
+    const int lane = lane_id();
+    const uint64_t lt = (1ull << lane) - 1ull;
+    for (;;) {
+        const uint32_t nxt = (uint32_t)__shfl_down((int)sym, 1, 64);
+        const bool pair = lane < n - 1 && !((heads >> (lane + 1)) & 1ull);
+        const uint32_t v = pair ? merge_val(T, sym, nxt) : 0xFFFFFFFFu;
+        const uint32_t rank = v >> 16;
+        // segmented inclusive min scan, then each lane takes its word's last value
+        uint32_t x = rank;
+        bool f = (heads >> lane) & 1ull;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)x, d, 64);
+            const bool fy = __shfl_up(f ? 1 : 0, d, 64) != 0;
+            if (lane >= d) {
+                if (!f) x = y < x ? y : x;
+                f = f || fy;
+            }
+        }
+        const uint64_t after = lane == 63 ? 0ull : heads & ~((2ull << lane) - 1ull);
+        const int last = after ? __builtin_ctzll(after) - 1 : n - 1;
+        const uint32_t rmin = (uint32_t)__shfl((int)x, last < 0 ? 0 : last, 64);
+        if (!__any(lane < n && rmin != 0xFFFFu)) break;
+        const uint64_t cand = __ballot(pair && rank == rmin && rank != 0xFFFFu);
+        const uint64_t sel = leftmost_alternating(cand, false);
+        if ((sel >> lane) & 1ull) sym = v & 0xFFFFu;
+        const uint64_t live = (n == 64 ? ~0ull : ((1ull << n) - 1ull)) & ~(sel << 1);
+        if ((live >> lane) & 1ull) tmp[__popcll(live & lt)] = (uint16_t)sym;
+        uint64_t nh = 0;  // heads survive every step: their new positions
+        for (uint64_t m = heads; m; m &= m - 1) nh |= 1ull << __popcll(live & ((1ull << __builtin_ctzll(m)) - 1ull));
+        heads = nh;
+        __builtin_amdgcn_wave_barrier();
+        n = __popcll(live);
+        sym = lane < n ? tmp[lane] : 0u;
+        __builtin_amdgcn_wave_barrier();
+    }
+    return n;
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -484,17 +531,39 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
     }
     __syncthreads();
 
-    // ---- 4. wave BPE of the misses ---------------------------------------------
+    // ---- 4. wave BPE of the misses, packed: consecutive misses share the lanes --
     const int npend = (int)s_scratch[1];
-    for (int q = 0; q < npend; ++q) {
-        const int pi = s_pend[q];
-        const int prel = (int)(s_pieces[pi] & 0xFFFu);
-        const int nxt = pi + 1 < np ? (int)(s_pieces[pi + 1] & 0xFFFu) : e_last;
-        const int n = nxt - prel;
-        uint32_t sym = lane < n ? (uint32_t)T.byte_id[win[prel + HALO_L + lane]] : 0u;
-        const int k = bpe_wave(T, sym, n, (lds_u16 *)s_tmp);
-        if (lane < k) stage[prel + lane] = (uint16_t)sym;
-        if (lane == 0) cnt[pi] = (uint8_t)k;
+    for (int q = 0; q < npend;) {
+        int total = 0, nw = 0, wprel = 0, wpi = 0;
+        uint32_t sym = 0;
+        uint64_t heads = 0;
+        while (q < npend) {  // wave-uniform packing (every miss is 2..64 bytes)
+            const int pi = s_pend[q];
+            const int prel = (int)(s_pieces[pi] & 0xFFFu);
+            const int nxt = pi + 1 < np ? (int)(s_pieces[pi + 1] & 0xFFFu) : e_last;
+            const int n = nxt - prel;
+            if (total + n > 64) break;
+            if (lane >= total && lane < total + n) sym = (uint32_t)T.byte_id[win[prel + HALO_L + lane - total]];
+            if (lane == nw) {
+                wprel = prel;
+                wpi = pi;
+            }
+            heads |= 1ull << total;
+            total += n;
+            ++nw;
+            ++q;
+        }
+        const int k = bpe_wave_seg(T, sym, total, heads, (lds_u16 *)s_tmp);
+        const uint64_t upto = lane == 63 ? heads : heads & ((2ull << lane) - 1ull);
+        const int seg = __popcll(upto) - 1;
+        const int start = upto ? 63 - __builtin_clzll(upto) : 0;
+        const int sprel = __shfl(wprel, seg < 0 ? 0 : seg, 64);
+        const int spi = __shfl(wpi, seg < 0 ? 0 : seg, 64);
+        if (lane < k) {
+            stage[sprel + lane - start] = (uint16_t)sym;
+            const bool lastl = lane == k - 1 || ((heads >> (lane + 1)) & 1ull);
+            if (lastl) cnt[spi] = (uint8_t)(lane - start + 1);
+        }
         __syncthreads();
     }
 

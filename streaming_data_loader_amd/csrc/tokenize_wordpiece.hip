@@ -72,7 +72,7 @@ __device__ __forceinline__ uint32_t vclass_of_entry(uint32_t e) {
 }
 
 // Full visible class of the char at q (general path).
-__device__ uint32_t vclass_general(const Ctx &C, int64_t q) {
+__device__ __forceinline__ uint32_t vclass_general(const Ctx &C, int64_t q) {
     const DevTok &T = *C.T;
     const uint32_t b = C.byte(q);
     if ((b & 0xC0u) == 0x80u) return V_NONE;
@@ -97,7 +97,7 @@ __device__ uint32_t vclass_general(const Ctx &C, int64_t q) {
 // ---- WordPiece ------------------------------------------------------------------
 
 // WordPiece::tokenize over a normalized word held in a byte buffer.
-__device__ int wordpiece_general(const DevTok &T, const uint8_t *w, int L, lds_u16 *out) {
+__device__ __forceinline__ int wordpiece_general(const DevTok &T, const uint8_t *w, int L, lds_u16 *out) {
     int n = 0, start = 0;
     while (start < L) {
         const int lim = start == 0 ? T.maxlen_first : T.maxlen_cont;
@@ -120,7 +120,8 @@ __device__ int wordpiece_general(const DevTok &T, const uint8_t *w, int L, lds_u
 }
 
 // Appends the normalized bytes of a non-ASCII OTHER/ISO char.
-__device__ __forceinline__ int append_norm(const Ctx &C, uint32_t e, int64_t p, int len, uint8_t *buf, int nb) {
+template <typename Buf>
+__device__ __forceinline__ int append_norm(const Ctx &C, uint32_t e, int64_t p, int len, Buf *buf, int nb) {
     if (e & 4u) {
         for (int k = 0; k < len; ++k) buf[nb + k] = (uint8_t)C.byte(p + k);
         return nb + len;
@@ -140,12 +141,13 @@ __device__ __forceinline__ int utf8_len(uint32_t lead) {
     return lead < 0x80u ? 1 : (lead & 0xE0u) == 0xC0u ? 2 : (lead & 0xF0u) == 0xE0u ? 3 : 4;
 }
 
-// General WORD piece: runs over OTHER and invisible chars until a WS/ISO char,
-// an added token or the record end; materialized in private memory.
-__device__ int word_general(const Ctx &C, int64_t p, int64_t rec_end, lds_u16 *out) {
+// Extent of the general WORD piece at p: it runs over OTHER and invisible
+// chars until a WS/ISO char, an added token or the record end.  Counts its
+// normalized chars (stops past MAX_WORD_CHARS) and bytes.
+__device__ __forceinline__ int64_t word_extent(const Ctx &C, int64_t p, int64_t rec_end, int *nchars_out, int *nbytes_out) {
     const DevTok &T = *C.T;
     int64_t i = p;
-    int nchars = 0;
+    int nchars = 0, nbytes = 0;
     while (i < rec_end && nchars <= MAX_WORD_CHARS) {
         const uint32_t b = C.byte(i);
         if (b < 0x80u) {
@@ -153,6 +155,7 @@ __device__ int word_general(const Ctx &C, int64_t p, int64_t rec_end, lds_u16 *o
             if (c == V_OTHER) {
                 if (T.n_special && b == T.opener && special_match(C, i) >= 0) break;
                 ++nchars;
+                ++nbytes;
                 ++i;
                 continue;
             }
@@ -163,19 +166,27 @@ __device__ int word_general(const Ctx &C, int64_t p, int64_t rec_end, lds_u16 *o
         int len;
         const uint32_t e = uentry(T, decode(C, i, b, &len));
         const uint32_t c = e & 3u;
-        if (c == UC_OTHER) nchars += entry_nchars(T, e);
-        else if (c != UC_DEL) break;
+        if (c == UC_OTHER) {
+            nchars += entry_nchars(T, e);
+            nbytes += (e & 4u) ? len : (e & 8u) ? (int)((e >> 4) & 3u) + 1 : (int)T.upool[e >> 8];
+        } else if (c != UC_DEL) {
+            break;
+        }
         i += len;
     }
-    if (nchars > MAX_WORD_CHARS) {
-        out[0] = (uint16_t)T.unk_id;
-        return 1;
-    }
-    uint8_t buf[MAX_WORD_BYTES];
+    *nchars_out = nchars;
+    *nbytes_out = nbytes;
+    return i;
+}
+
+// Normalized bytes of the word [p, i) into buf (private or LDS); returns the
+// count.  NFD canonical ordering of the kept combining marks: a run of them is
+// appended as it comes and sorted in place (stable, by ccc) when a starter --
+// kept, removed or inside a precomposed char -- ends it.
+template <typename Buf>
+__device__ __forceinline__ int word_materialize(const Ctx &C, int64_t p, int64_t i, Buf *buf) {
+    const DevTok &T = *C.T;
     int nb = 0;
-    // NFD canonical ordering of the kept combining marks: a run of them is
-    // appended to buf as it comes and sorted in place (stable, by ccc) when a
-    // starter -- kept, removed or inside a precomposed char -- ends it
     int run = -1;
     auto ccc_at = [&](int x, int l) {
         uint32_t cp = l == 2 ? buf[x] & 0x1Fu : l == 3 ? buf[x] & 0x0Fu : buf[x] & 0x07u;
@@ -258,7 +269,32 @@ __device__ int word_general(const Ctx &C, int64_t p, int64_t rec_end, lds_u16 *o
         q += len;
     }
     flush();
-    return wordpiece_general(T, buf, nb, out);
+    return nb;
+}
+
+// General WORD piece materialized in private memory, WordPiece one probe at a
+// time (words whose normalization exceeds the LDS lattice buffer).
+__device__ __forceinline__ int word_general(const Ctx &C, int64_t p, int64_t rec_end, lds_u16 *out) {
+    int nchars, nbytes;
+    const int64_t i = word_extent(C, p, rec_end, &nchars, &nbytes);
+    if (nchars > MAX_WORD_CHARS) {
+        out[0] = (uint16_t)C.T->unk_id;
+        return 1;
+    }
+    uint8_t buf[MAX_WORD_BYTES];
+    const int nb = word_materialize(C, p, i, buf);
+    return wordpiece_general(*C.T, buf, nb, out);
+}
+
+// Bytes [off, off + 16) of an LDS byte buffer (dword aligned, readable 20
+// bytes past off) in registers, the first n kept.
+__device__ __forceinline__ W16 lds_w16(const lds_u32 *b32, int off, int n) {
+    const int a = off >> 2;
+    const uint32_t sh = (uint32_t)(off & 3);
+    const uint32_t x0 = b32[a], x1 = b32[a + 1], x2 = b32[a + 2], x3 = b32[a + 3], x4 = b32[a + 4];
+    return keep_bytes(W16{__builtin_amdgcn_alignbyte(x1, x0, sh), __builtin_amdgcn_alignbyte(x2, x1, sh),
+                          __builtin_amdgcn_alignbyte(x3, x2, sh), __builtin_amdgcn_alignbyte(x4, x3, sh)},
+                      n < 16 ? n : 16);
 }
 
 // start of the char that ends right before byte `end` (UTF-8 in registers)
@@ -271,7 +307,7 @@ __device__ __forceinline__ int w16_prev_char(const W16 &w, int end, int start) {
 // BertNormalizer output of the WORD piece at p (or of the single ISO char at
 // p if iso) into registers.  Returns false if the normalized word does not fit
 // in 16 bytes (then the scratch path handles it, including the 100-char rule).
-__device__ bool normalize_w16(const Ctx &C, int64_t p, int64_t rec_end, bool iso, W16 &w, int &L) {
+__device__ __forceinline__ bool normalize_w16(const Ctx &C, int64_t p, int64_t rec_end, bool iso, W16 &w, int &L) {
     const DevTok &T = *C.T;
     w = W16{0, 0, 0, 0};
     int nb = 0;
@@ -324,7 +360,7 @@ __device__ bool normalize_w16(const Ctx &C, int64_t p, int64_t rec_end, bool iso
 // Record end (first record start > p, p in the window) for the general paths:
 // the next bit of the window's record-start bitmap, else the first start past
 // the window (rb_next).
-__device__ int64_t rec_end_of(const Ctx &C, int64_t rb_next, int64_t p) {
+__device__ __forceinline__ int64_t rec_end_of(const Ctx &C, int64_t rb_next, int64_t p) {
     const int b = (int)(p - C.w0) + 1;
     for (int wd = b >> 5; wd < RBITS_WORDS; ++wd) {
         uint32_t m = C.rbits[wd];
@@ -371,7 +407,7 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
     __shared__ uint16_t s_stage[STAGE];    // ids staged at their piece's byte position
     __shared__ uint8_t s_cnt[CHUNK];       // ids per piece
     __shared__ uint16_t s_pend[PEND_CAP];  // pending piece indices (step 4b)
-    __shared__ uint32_t s_scratch[TOK_THREADS / 64 + 2];
+    __shared__ uint32_t s_scratch[TOK_THREADS / 64 + 3];
 #ifdef SDL_LDS_PAD  // diagnostic: occupancy sensitivity
     __shared__ uint8_t s_pad[SDL_LDS_PAD];
     if (N < 0) {
@@ -597,6 +633,7 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
 #endif
     if (tid == 0) {
         s_scratch[TOK_THREADS / 64 + 1] = 0;  // pending count
+        s_scratch[TOK_THREADS / 64 + 2] = 0;  // deferred count
     }
     __syncthreads();
     SDL_STAMP(10);
@@ -765,9 +802,9 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
                             uint8_t buf[16];
                             const int nb = append_norm(C, e, p, len, buf, 0);
                             s_cnt[pi] = (uint8_t)wordpiece_general(T, buf, nb, out);
-                        } else {
-                            s_cnt[pi] = (uint8_t)word_general(
-                                C, p, rec_end_of(C, rb_next, p), out);
+                        } else {  // deferred to the cooperative lattice below
+                            const uint32_t d = atomicAdd(&s_scratch[TOK_THREADS / 64 + 2], 1u);
+                            s_pend[d] = (uint16_t)pi;  // d < this round's consumed entries
                         }
                     }
                 }
@@ -808,9 +845,118 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
                 }
             }
         }
+        // (c) deferred words (normalization longer than 16 bytes, DEL runs,
+        //     canonical ordering): one at a time, normalized by lane 0 into LDS
+        //     (the pending list's space, free now), then the WordPiece lattice:
+        //     every (start, length) candidate with a vocab piece of that length
+        //     is one probe task dealt across the wave, and each start keeps its
+        //     longest hit (atomic max of length << 16 | id); lane 0 walks
+        //     greedy longest-match-first over them.  Probe latencies per word
+        //     ~ candidates / 64, where probing one candidate at a time pays one
+        //     per candidate.
+        __syncthreads();
+        const int ndef = (int)s_scratch[TOK_THREADS / 64 + 2];
+        if (ndef) {
+            uint32_t dl[PEND_CAP / 64];
+#pragma unroll
+            for (int j = 0; j < PEND_CAP / 64; ++j) {
+                const int d = 64 * j + lane;
+                dl[j] = d < ndef ? s_pend[d] : 0u;
+            }
+            __syncthreads();
+            lds_u8 *wb = (lds_u8 *)s_pend;
+            const lds_u32 *wb32 = (const lds_u32 *)s_pend;
+            lds_u32 *best = (lds_u32 *)s_pend + LW_BUF / 4;
+            for (int d = 0; d < ndef; ++d) {
+                uint32_t mine = dl[0];
+#pragma unroll
+                for (int j = 1; j < PEND_CAP / 64; ++j)
+                    if ((d >> 6) == j) mine = dl[j];
+                const int dpi = __shfl((int)mine, d & 63, 64);
+                const int dprel = (int)(s_pieces[dpi] & 0xFFFu);
+                const int64_t dp = c0 + dprel;
+                lds_u16 *dout = stage + dprel;
+                int dL = 0;
+                if (lane == 0) {
+                    const int64_t rend = rec_end_of(C, rb_next, dp);
+                    int nch, nby;
+                    const int64_t iend = word_extent(C, dp, rend, &nch, &nby);
+                    if (nch > MAX_WORD_CHARS) {
+                        dout[0] = (uint16_t)T.unk_id;
+                        s_cnt[dpi] = 1;
+                    } else if (nby > LW_MAX || T.wp_long_pieces) {
+                        s_cnt[dpi] = (uint8_t)word_general(C, dp, rend, dout);
+                    } else {
+                        dL = word_materialize(C, dp, iend, wb);
+                        for (int k = dL; k < dL + 20; ++k) wb[k] = 0;
+                    }
+                }
+                dL = __shfl(dL, 0, 64);
+                if (dL == 0) continue;  // wave-uniform
+                for (int k = lane; k < dL; k += 64) best[k] = 0u;
+                __syncthreads();
+                const int nf = T.wp_nlens[0], nc = T.wp_nlens[1];
+                const int ntask = nf + (dL - 1) * nc;
+                for (int k = lane; k < ntask; k += 64) {
+                    int st, n;
+                    if (k < nf) {
+                        st = 0;
+                        n = T.wp_lens[k];
+                    } else {
+                        st = 1 + (k - nf) / nc;
+                        n = T.wp_lens[LW_MAX + (k - nf) % nc];
+                    }
+                    if (st + n > dL || (wb[st] & 0xC0u) == 0x80u || (st + n < dL && (wb[st + n] & 0xC0u) == 0x80u))
+                        continue;
+                    const uint32_t cont = st > 0 ? 1u : 0u;
+                    uint32_t h = hinit((uint32_t)n, cont);
+                    for (int b0 = 0; b0 < n; b0 += 16) {
+                        const W16 blk = lds_w16(wb32, st + b0, n - b0);
+                        h = hmix(hmix(hmix(hmix(h, blk.x), blk.y), blk.z), blk.w);
+                    }
+                    h = hfinal(h);
+                    const W16 first = lds_w16(wb32, st, n);
+                    const Probe P = probe_load(T, h);
+                    const uint32_t key = (uint32_t)n | (cont << 8);
+                    int id = -1;
+                    for (int which = 0; which < 2 && id < 0; ++which) {
+                        const uint4 a = which ? P.a2 : P.a1, b = which ? P.b2 : P.b1;
+                        if (!slot_match(a, b, key, first)) continue;
+                        bool ok = true;
+                        for (int x = 16; x < n && ok; ++x) ok = T.vpool[a.z + x] == wb[st + x];
+                        if (ok) id = (int32_t)a.y;
+                    }
+                    if (id >= 0)
+                        __hip_atomic_fetch_max(best + st, ((uint32_t)n << 16) | (uint32_t)id, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+                __syncthreads();
+                if (lane == 0) {
+                    int nout = 0;
+                    for (int st = 0; st < dL;) {
+                        const uint32_t bv = best[st];
+                        if (!bv) {
+                            nout = -1;
+                            break;
+                        }
+                        dout[nout++] = (uint16_t)(bv & 0xFFFFu);
+                        st += (int)(bv >> 16);
+                    }
+                    if (nout < 0) {
+                        dout[0] = (uint16_t)T.unk_id;
+                        nout = 1;
+                    }
+                    s_cnt[dpi] = (uint8_t)nout;
+                }
+                __syncthreads();
+            }
+        }
     }
     __syncthreads();
-    if (tid == 0) s_scratch[TOK_THREADS / 64 + 1] = 0;  // the next round's pending count
+    if (tid == 0) {
+        s_scratch[TOK_THREADS / 64 + 1] = 0;  // the next round's pending count
+        s_scratch[TOK_THREADS / 64 + 2] = 0;  // ... and deferred count
+    }
     __syncthreads();
     }
     SDL_STAMP(7);
