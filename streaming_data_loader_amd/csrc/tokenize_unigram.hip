@@ -509,8 +509,32 @@ void print_uni_cycles() {
     for (int i = 1; i < 8; ++i)
         fprintf(stderr, "[uni stamps] %-24s %6.2f%%\n", names[i], tot ? 100.0 * (double)h[i] / (double)tot : 0.0);
 }
+__device__ unsigned long long sdl_long_cycles[8], sdl_long_counts[4];
+#define LONG_STAMP(k)                                                                 \
+    do {                                                                              \
+        if (threadIdx.x == 0) {                                                       \
+            const unsigned long long t_ = __builtin_amdgcn_s_memtime();              \
+            atomicAdd(&sdl_long_cycles[k], t_ - lstamp_);                             \
+            lstamp_ = t_;                                                             \
+        }                                                                             \
+    } while (0)
+#define LONG_COUNT(k, v) do { if (threadIdx.x == 0) atomicAdd(&sdl_long_counts[k], (unsigned long long)(v)); } while (0)
+void print_long_cycles() {
+    unsigned long long h[8], c[4];
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(sdl_long_cycles), sizeof(h)) != hipSuccess) return;
+    if (hipMemcpyFromSymbol(c, HIP_SYMBOL(sdl_long_counts), sizeof(c)) != hipSuccess) return;
+    static const char *names[] = {"", "load+normalize", "piece select", "probes", "relax", "backtrack", "finalize", "-"};
+    unsigned long long tot = 0;
+    for (int i = 1; i < 8; ++i) tot += h[i];
+    for (int i = 1; i < 7; ++i)
+        fprintf(stderr, "[long stamps] %-16s %6.2f%%\n", names[i], tot ? 100.0 * (double)h[i] / (double)tot : 0.0);
+    fprintf(stderr, "[long stamps] total cycles %llu items %llu ascii %llu pieces %llu sumL %llu\n", tot, c[0], c[1], c[2],
+            c[3]);
+}
 #else
 #define UNI_STAMP(k) do {} while (0)
+#define LONG_STAMP(k) do {} while (0)
+#define LONG_COUNT(k, v) do {} while (0)
 #endif
 
 // ---------------------------------------------------------------------------
@@ -1193,6 +1217,9 @@ __global__ __launch_bounds__(64) void k_unigram_long(DevTok T, const uint8_t *__
     const int Mm = T.maxlen_meta, Mf = T.maxlen_first;
     uint32_t n_items = counters[0];
     if (n_items > item_cap) n_items = item_cap;
+#ifdef SDL_STAMPS
+    unsigned long long lstamp_ = __builtin_amdgcn_s_memtime();
+#endif
     for (uint32_t it_i = blockIdx.x; it_i < n_items; it_i += gridDim.x) {
         const uint4 it = items[it_i];
         const int64_t p = (int64_t)it.x * CHUNK + it.z;
@@ -1203,14 +1230,45 @@ __global__ __launch_bounds__(64) void k_unigram_long(DevTok T, const uint8_t *__
         const int64_t pa = (p - 1) & ~(int64_t)15;  // staged raw bytes: [pa, pa + LONG_RAW)
         *reinterpret_cast<uint4 *>(s_raw + 16 * lane) = load16(text, pa + 16 * lane, N);
         __syncthreads();
-        if (lane == 0) {
-            const int64_t rs = (int64_t)off[rec];
-            const int64_t re = (int64_t)off[rec + 1] < N ? (int64_t)off[rec + 1] : N;
-            const lds_u8 *raw = (const lds_u8 *)s_raw;
-            auto byte = [&](int64_t q) -> uint32_t {
-                return (uint64_t)(q - pa) < (uint64_t)LONG_RAW ? (uint32_t)raw[q - pa] : (uint32_t)text[q];
-            };
-            const int64_t end = it.w ? p + it.w : word_end_b(T, byte, N, p, re);
+        const int64_t rs = (int64_t)off[rec];
+        const int64_t re = (int64_t)off[rec + 1] < N ? (int64_t)off[rec + 1] : N;
+        const lds_u8 *raw = (const lds_u8 *)s_raw;
+        auto byte = [&](int64_t q) -> uint32_t {
+            return (uint64_t)(q - pa) < (uint64_t)LONG_RAW ? (uint32_t)raw[q - pa] : (uint32_t)text[q];
+        };
+        // the raw word's end (word_end_b), the wave scanning 64 bytes a step
+        int64_t end = it.w ? p + it.w : -1;
+        for (int64_t q0 = p + 1; end < 0; q0 += 64) {
+            const int64_t q = q0 + lane;
+            bool stop = q >= re;
+            if (!stop) {
+                const uint32_t b = byte(q);
+                int l;
+                auto bnd = [&](int64_t x) -> bool { return x >= re; };
+                stop = ascii_ws(b) || (b == (uint32_t)'<' && T.n_special && uni_special(T, q, N, byte, bnd, &l) >= 0);
+            }
+            const uint64_t m = __ballot(stop);
+            if (m) end = q0 + __builtin_ctzll(m);
+        }
+        // a word of printable ASCII is its own normalization (host-checked
+        // charsmap facts, as the chunk kernel's simple words): copied by the wave
+        const int wl = (int)(end - p);
+        bool ascii = wl <= LONG_NORM && p - pa + wl <= LONG_RAW;
+        if (ascii) {
+            bool mine = true;
+            for (int j = lane; j < wl; j += 64) mine = mine && (uint32_t)s_raw[p - pa + j] - 0x21u < 0x5Eu;
+            ascii = !__any(!mine);
+        }
+        if (ascii) {
+            for (int j = lane; j < wl + 8; j += 64) nb[j] = j < wl ? s_raw[p - pa + j] : (uint8_t)0;
+            if (lane == 0) {
+                s_misc[0] = wl;
+                s_misc[1] = 0;
+                s_misc[5] = 0;
+                s_misc[6] = -1;
+                s_misc[7] = 0;
+            }
+        } else if (lane == 0) {
             int nl = 0;
             const bool ok = normalize_span(T, byte, p, end, p > rs && byte(p - 1) == (uint32_t)' ',
                                            [&](uint32_t x) -> bool {
@@ -1227,6 +1285,9 @@ __global__ __launch_bounds__(64) void k_unigram_long(DevTok T, const uint8_t *__
         }
         __syncthreads();
         const int nl = s_misc[0];
+        LONG_COUNT(0, 1);
+        LONG_COUNT(1, ascii ? 1 : 0);
+        LONG_STAMP(1);
         if (nl < 0) {
             if (lane == 0) {
                 const uint32_t h = atomicAdd(&counters[3], 1u);
@@ -1271,7 +1332,10 @@ __global__ __launch_bounds__(64) void k_unigram_long(DevTok T, const uint8_t *__
             }
             __syncthreads();
             const int src = s_misc[2], L = s_misc[3];
+            LONG_STAMP(2);
             if (src < 0) break;
+            LONG_COUNT(2, 1);
+            LONG_COUNT(3, L);
             const int n = L + 3;  // the piece "▁" + payload
             for (int i = lane; i <= n; i += 64) {
                 s_sc[i] = 0.0;
@@ -1317,9 +1381,16 @@ __global__ __launch_bounds__(64) void k_unigram_long(DevTok T, const uint8_t *__
                         const uint32_t cont = i < 0 ? UC_META : UC_PIECE;
                         meta[u] = (uint32_t)(i + 1 - r0) | (uint32_t)(i < 0 ? j : j - i - 1) << 8 | (uint32_t)len << 16 |
                                   cont << 24;
+                        Wd[u] = lds_w16(w32, src + ps, len);
                         if (len <= 16) {
-                            Wd[u] = lds_w16(w32, src + ps, len);
                             P[u] = probe_load(T, hash16(Wd[u], (uint32_t)len, cont));
+                        } else if (len <= 32) {  // two blocks; bytes past 16 checked on a header match
+                            const W16 w2 = lds_w16(w32, src + ps + 16, len - 16);
+                            uint32_t h = hinit((uint32_t)len, cont);
+                            h = hmix(hmix(hmix(hmix(h, Wd[u].x), Wd[u].y), Wd[u].z), Wd[u].w);
+                            h = hmix(hmix(hmix(hmix(h, w2.x), w2.y), w2.z), w2.w);
+                            P[u] = probe_load(T, hfinal(h));
+                            gen[u] = -3;
                         } else {
                             gen[u] = probe_acc(T, nbr, src + ps, len, cont, &gw3[u]);
                         }
@@ -1329,7 +1400,24 @@ __global__ __launch_bounds__(64) void k_unigram_long(DevTok T, const uint8_t *__
                         if (meta[u] == ~0u) continue;
                         uint32_t w3 = gw3[u];
                         const uint32_t key = ((meta[u] >> 16) & 0xFFu) | ((meta[u] >> 24) << 8);
-                        const int id = gen[u] != -2 ? gen[u] : probe_result_w3(P[u], key, Wd[u], &w3);
+                        int id;
+                        if (gen[u] == -3) {  // 17..32 bytes: header + first 16 bytes, then the pool
+                            id = -1;
+                            const int len = (int)((meta[u] >> 16) & 0xFFu);
+                            const int ps = (int)(meta[u] & 0xFFu) + r0 - 1;
+                            for (int which = 0; which < 2 && id < 0; ++which) {
+                                const uint4 sa = which ? P[u].a2 : P[u].a1, sb = which ? P[u].b2 : P[u].b1;
+                                if (!slot_match(sa, sb, key, Wd[u])) continue;
+                                bool ok = true;
+                                for (int x = 16; x < len && ok; ++x) ok = T.vpool[sa.z + x] == nb[src + (ps < 0 ? 0 : ps) + x];
+                                if (ok) {
+                                    id = (int32_t)sa.y;
+                                    w3 = sa.w;
+                                }
+                            }
+                        } else {
+                            id = gen[u] != -2 ? gen[u] : probe_result_w3(P[u], key, Wd[u], &w3);
+                        }
                         if (id < 0) continue;
                         const int q = (int)(meta[u] & 0xFFu), k = (int)((meta[u] >> 8) & 0xFFu);
                         s_cid[k * 64 + q] = (uint16_t)id;
@@ -1338,6 +1426,7 @@ __global__ __launch_bounds__(64) void k_unigram_long(DevTok T, const uint8_t *__
                     }
                 }
                 __syncthreads();
+                LONG_STAMP(3);
                 // relax the nodes from these rows' starts, in order; a row's candidates
                 // end at distinct nodes, so lane k relaxes the row's k-th end
                 const int rz = L + 1 - r0 < 64 ? L + 1 - r0 : 64;
@@ -1370,6 +1459,7 @@ __global__ __launch_bounds__(64) void k_unigram_long(DevTok T, const uint8_t *__
                     __syncthreads();
                 }
                 __syncthreads();
+                LONG_STAMP(4);
             }
             if (lane == 0) {
                 struct {
@@ -1384,6 +1474,7 @@ __global__ __launch_bounds__(64) void k_unigram_long(DevTok T, const uint8_t *__
                 s_misc[5] = k0 + k;
             }
             __syncthreads();
+            LONG_STAMP(5);
         }
         if (lane == 0) {
             int k = s_misc[5];
@@ -1395,6 +1486,7 @@ __global__ __launch_bounds__(64) void k_unigram_long(DevTok T, const uint8_t *__
                           rec_local, pool, counters + 2, pool_cap, err);
         }
         __syncthreads();
+        LONG_STAMP(6);
     }
 }
 

@@ -391,11 +391,13 @@ __device__ unsigned long long sdl_phase_cycles[16];
     } while (0)
 #endif
 
-// Waves per SIMD the register budget is cut to: 6 (80 VGPRs) with the 7.1 KB
-// block (PEND_CAP 256) measured 1% faster than 5 (tools/variants.sh).  The
-// LDS step that matters: one more 64-B array (7.7 KB) cost 7%.
+// Waves per SIMD the register budget is cut to: 5 (96 VGPRs).  6 (80 VGPRs)
+// was 1% faster before the deferred-word lattice; with it, 80 VGPRs spill and
+// 5 measures faster on both corpora (fixture 1.868 -> 1.818 ms, held-out
+// 2.98 -> 2.86 ms).  LDS (7.1 KB per one-wave block) admits ~5.5 anyway; one
+// more 64-B array (7.7 KB) cost 7%.
 #ifndef SDL_WP_WAVES
-#define SDL_WP_WAVES 6
+#define SDL_WP_WAVES 5
 #endif
 __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL_WP_WAVES, 8))) void k_wordpiece_chunks(
     DevTok T, const uint8_t *__restrict__ text, int64_t N, const uint64_t *__restrict__ off, int64_t R,

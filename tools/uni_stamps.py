@@ -15,7 +15,8 @@ from streaming_data_loader_amd import native  # noqa: E402
 from streaming_data_loader_amd.device import DeviceBatcher  # noqa: E402
 
 mib = int(sys.argv[1]) if len(sys.argv) > 1 else 64
-arena, offs, order = bench.build_arena(bench.fixture_records(), mib << 20, seed=0x5D1B)
+corpus = sys.argv[2] if len(sys.argv) > 2 else "fixture"
+arena, offs, order = bench.build_arena(bench.corpus_records(corpus), mib << 20, seed=0x5D1B)
 N, R = len(arena) - 16, len(order)
 text = torch.from_numpy(arena).cuda()
 off = torch.from_numpy(offs.astype(np.int64)).cuda()
