@@ -1134,6 +1134,12 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
     uint32_t base = block_excl_sum<TOK_THREADS>(mine, &total, s_scratch + 8);
     uint32_t *dst = tokc + (int64_t)blockIdx.x * UNI_STAGE;
     const uint32_t base0 = base;
+    // the list is packed in LDS first (window and arena are dead now) and
+    // written as whole 16-B lanes: scattered 4-B non-temporal stores cost ~3x
+    // the list's bytes in HBM writes
+    constexpr uint32_t PK_CAP = (uint32_t)(WIN_PAD + ARENA + 32) / 4 - 3;
+    const bool packed = total <= PK_CAP;
+    lds_u32 *pk = (lds_u32 *)s_bytes;
     for (int i = a0; i < a1; ++i) {
         const int prel = s_pieces[i] & 0xFFF;
         const int k = s_cnt[i];
@@ -1141,13 +1147,29 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
             const uint32_t it = atomicAdd(&counters[0], 1u);
             if (it < item_cap) items[it] = make_uint4((uint32_t)blockIdx.x, base, (uint32_t)prel, s_stage[prel]);
             else atomicOr(err, 8u);
-            dst[base++] = LMARK;
+            if (packed) pk[base] = LMARK;
+            else dst[base] = LMARK;
+            ++base;
             continue;
         }
-        for (int j = 0; j < k; ++j) __builtin_nontemporal_store((uint32_t)s_stage[prel + j], dst + base + j);
+        if (packed) {
+            for (int j = 0; j < k; ++j) pk[base + j] = (uint32_t)s_stage[prel + j];
+        } else {
+            for (int j = 0; j < k; ++j) __builtin_nontemporal_store((uint32_t)s_stage[prel + j], dst + base + j);
+        }
         base += k;
     }
     __syncthreads();
+    if (packed) {
+        for (uint32_t e = 4u * (uint32_t)tid; e < total; e += 4u * TOK_THREADS) {
+            u32x4 v;
+            v.x = pk[e];
+            v.y = pk[e + 1];
+            v.z = pk[e + 2];
+            v.w = pk[e + 3];
+            __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(dst + e));
+        }
+    }
     // the stage is free now: it holds each piece's entry offset in the chunk
     uint16_t *const s_poff = s_stage;
     base = base0;
