@@ -660,7 +660,8 @@ def end_to_end_frames(db, records, order, dev, stream, task_name, nbytes=64 << 2
                        "text_MBps_bound": round(done / d2h_s / 1e6, 2),
                        "note": "hipMemcpyAsync of the frames alone: the PCIe D2H bound of this path"}
     pinned_json = host[:len(buf)].numpy()  # the pinned copy the sequential path reads
-    for chunk_mib, src, kind in ((8, buf, "pageable"), (8, pinned_json, "pinned"), (16, pinned_json, "pinned"),
+    for chunk_mib, src, kind in ((8, buf, "pageable"), (8, pinned_json, "pinned"), (12, pinned_json, "pinned"),
+                                 (16, pinned_json, "pinned"), (24, pinned_json, "pinned"),
                                  (32, pinned_json, "pinned")):
         best_p, st = None, None
         for r in range(reps + 1):

@@ -952,6 +952,20 @@ hipError_t launch_json_nl_write(const uint8_t *buf, int64_t len, const uint32_t 
     return hipGetLastError();
 }
 
+// {newline count, position of the last newline} in one word pair, so the host
+// reads both with one copy and one synchronisation
+__global__ void k_json_nl_tail(const uint32_t *__restrict__ total, const uint32_t *__restrict__ nl,
+                               uint32_t *__restrict__ out) {
+    const uint32_t n = *total;
+    out[0] = n;
+    out[1] = n ? nl[n - 1] : 0u;
+}
+
+hipError_t launch_json_nl_tail(const uint32_t *total, const uint32_t *nl, uint32_t *out, hipStream_t st) {
+    hipLaunchKernelGGL(k_json_nl_tail, dim3(1), dim3(1), 0, st, total, nl, out);
+    return hipGetLastError();
+}
+
 hipError_t launch_json_parse(const uint8_t *buf, int64_t len, const uint32_t *nl, uint32_t n_nl, int64_t n_lines,
                              uint32_t *out_len, uint32_t *is_rec, uint2 *span, uint32_t *n_invalid, hipStream_t st) {
     if (n_lines == 0) return hipSuccess;

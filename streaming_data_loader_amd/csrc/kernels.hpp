@@ -66,6 +66,7 @@ void print_long_cycles();
 hipError_t launch_json_nl_count(const uint8_t *buf, int64_t len, uint32_t *cnt, uint32_t *base, uint32_t *scan_tmp,
                                 hipStream_t st);
 hipError_t launch_json_nl_write(const uint8_t *buf, int64_t len, const uint32_t *base, uint32_t *nl, hipStream_t st);
+hipError_t launch_json_nl_tail(const uint32_t *total, const uint32_t *nl, uint32_t *out, hipStream_t st);
 hipError_t launch_json_parse(const uint8_t *buf, int64_t len, const uint32_t *nl, uint32_t n_nl, int64_t n_lines,
                              uint32_t *out_len, uint32_t *is_rec, uint2 *span, uint32_t *n_invalid, hipStream_t st);
 hipError_t launch_json_write(const uint8_t *buf, int64_t len, const uint32_t *nl, uint32_t n_nl, int64_t n_lines,

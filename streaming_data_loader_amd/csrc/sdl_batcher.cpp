@@ -277,7 +277,7 @@ struct sdl_batcher {
     // unigram long items
     DevBuf<uint32_t> uni_counters, uni_pool, uni_err, span_err;
     // JsonText provider step (sdl_json_text_device)
-    DevBuf<uint32_t> j_cnt, j_base, j_nl, j_len, j_rec, j_toff, j_ridx, j_inv;
+    DevBuf<uint32_t> j_cnt, j_base, j_nl, j_len, j_rec, j_toff, j_ridx, j_inv, j_tail;
     DevBuf<uint2> j_span;
     DevBuf<uint8_t> j_text;
     DevBuf<uint64_t> j_off;
@@ -288,11 +288,13 @@ struct sdl_batcher {
     size_t f_dest_cap = 0;
     bool f_dry = false;                  // lay the frames out, launch nothing
     // sdl_json_to_frames: input slots, the rows carried between chunks, streams/events
-    DevBuf<uint8_t> x_json[2];
+    DevBuf<uint8_t> x_json[2], x_frames[2];
     PinBuf<uint8_t> x_pin_in[2], x_pin_out[2];
     DevBuf<int32_t> x_ids[2], x_am[2], x_tt[2], x_lab[2];
     hipStream_t x_in = nullptr, x_out = nullptr;
     hipEvent_t x_ev[8] = {};
+    std::vector<hipEvent_t> x_in_ev;  // json_to_frames, pinned input: chunk k's H2D done
+    DevBuf<uint8_t> x_json_all;       // ... every chunk, 32 zero bytes after each
     DevBuf<uint4> uni_items, uni_huge;
     DevBuf<uint8_t> uni_scratch;
     DevBuf<uint8_t> h2d_text;
@@ -310,6 +312,7 @@ struct sdl_batcher {
     DevBuf<RowSeg> seg_dev;
     PinBuf<uint64_t> pin_label_off;
     uint32_t pin_u32_err = 0;
+    uint32_t pin_u32_2[2] = {0, 0};
     uint64_t n_records = 0;
 
     bool profiling = false;
@@ -348,6 +351,7 @@ struct sdl_batcher {
         for (auto &e : pipe_ev) (void)hipEventDestroy(e);
         for (auto &e : x_ev)
             if (e) (void)hipEventDestroy(e);
+        for (auto &e : x_in_ev) (void)hipEventDestroy(e);
         if (x_in) (void)hipStreamDestroy(x_in);
         if (x_out) (void)hipStreamDestroy(x_out);
         if (stream2) (void)hipStreamDestroy(stream2);
@@ -1054,18 +1058,19 @@ int sdl_json_text_device(sdl_batcher *h, const uint8_t *d_jsonl, uint64_t len, v
         h->j_cnt.ensure((size_t)nb + 1);
         h->j_base.ensure((size_t)nb + 1);
         h->scan_tmp.ensure((size_t)scan_tmp_words(std::max<int64_t>(nb, 1)) + 1);
-        uint32_t n_nl = 0;
+        // the newline list is sized for the worst case (every byte), so the count and the last
+        // position come back together: one synchronisation instead of two
+        uint32_t n_nl = 0, last_nl = 0;
+        h->j_nl.ensure((size_t)N + 2);
+        h->j_tail.ensure(2);
         if (nb) {
             HIP_TRY(launch_json_nl_count(d_jsonl, N, h->j_cnt.p, h->j_base.p, h->scan_tmp.p, st));
-            HIP_TRY(hipMemcpyAsync(&n_nl, h->j_base.p + nb, 4, hipMemcpyDeviceToHost, st));
+            HIP_TRY(launch_json_nl_write(d_jsonl, N, h->j_base.p, h->j_nl.p, st));
+            HIP_TRY(launch_json_nl_tail(h->j_base.p + nb, h->j_nl.p, h->j_tail.p, st));
+            HIP_TRY(hipMemcpyAsync(h->pin_u32_2, h->j_tail.p, 8, hipMemcpyDeviceToHost, st));
             HIP_TRY(hipStreamSynchronize(st));
-        }
-        h->j_nl.ensure((size_t)n_nl + 1);
-        if (nb) HIP_TRY(launch_json_nl_write(d_jsonl, N, h->j_base.p, h->j_nl.p, st));
-        uint32_t last_nl = 0;
-        if (n_nl) {
-            HIP_TRY(hipMemcpyAsync(&last_nl, h->j_nl.p + n_nl - 1, 4, hipMemcpyDeviceToHost, st));
-            HIP_TRY(hipStreamSynchronize(st));
+            n_nl = h->pin_u32_2[0];
+            last_nl = h->pin_u32_2[1];
         }
         // tokio lines(): a last line without '\n' counts, an empty tail does not
         const int64_t tail0 = n_nl ? (int64_t)last_nl + 1 : 0;
@@ -1258,10 +1263,12 @@ int sdl_json_to_frames(sdl_batcher *h, const uint8_t *jsonl, uint64_t len, uint6
         const uint64_t B = (uint64_t)h->cfg.batch_size, S = (uint64_t)h->cfg.sequence_length;
         const uint64_t LW = (uint64_t)h->P.label_width;
         const bool tt = h->with_tt();
-        // chunks end at a '\n' (the last one at len)
+        // chunks end at a '\n' (the last one at len); the first is chunk_bytes / SDL_J2F_HEAD
+        // (default 4) so the copy-out stream starts early
         std::vector<uint64_t> cut{0};
+        const int64_t head_div = std::max<int64_t>(1, env_int("SDL_J2F_HEAD", 4));
         while (cut.back() < len) {
-            uint64_t e = cut.back() + chunk_bytes;
+            uint64_t e = cut.back() + (cut.size() == 1 ? std::max<uint64_t>(chunk_bytes / head_div, 4096) : chunk_bytes);
             if (e >= len) { cut.push_back(len); break; }
             const void *nl = std::memchr(jsonl + e, '\n', (size_t)(len - e));
             cut.push_back(nl ? (uint64_t)((const uint8_t *)nl - jsonl) + 1 : len);
@@ -1274,6 +1281,24 @@ int sdl_json_to_frames(sdl_batcher *h, const uint8_t *jsonl, uint64_t len, uint6
             if (len && hipPointerGetAttributes(&pa, jsonl) == hipSuccess && pa.type == hipMemoryTypeHost)
                 pinned_in = true;
             (void)hipGetLastError();
+        }
+        // pinned input: every chunk's H2D is queued up front (one copy each, into its own region
+        // followed by 32 zero bytes), so no chunk's input waits behind an earlier chunk's D2H
+        std::vector<uint64_t> region(nch + 1, 0);
+        for (size_t k = 0; k < nch; ++k) region[k + 1] = region[k] + ((cut[k + 1] - cut[k] + 32 + 255) & ~(uint64_t)255);
+        if (pinned_in && nch) {
+            while (h->x_in_ev.size() < nch) {
+                hipEvent_t e;
+                HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+                h->x_in_ev.push_back(e);
+            }
+            h->x_json_all.ensure((size_t)region[nch]);
+            HIP_TRY(hipMemsetAsync(h->x_json_all.p, 0, (size_t)region[nch], h->x_in));
+            for (size_t k = 0; k < nch; ++k) {
+                HIP_TRY(hipMemcpyAsync(h->x_json_all.p + region[k], jsonl + cut[k], (size_t)(cut[k + 1] - cut[k]),
+                                       hipMemcpyHostToDevice, h->x_in));
+                HIP_TRY(hipEventRecord(h->x_in_ev[k], h->x_in));
+            }
         }
         uint64_t carry = 0, carry_at = 0, records = 0, lines = 0, invalid = 0, frames_total = 0, bytes_total = 0;
         uint64_t rows_total = 0, text_total = 0;
@@ -1311,24 +1336,26 @@ int sdl_json_to_frames(sdl_batcher *h, const uint8_t *jsonl, uint64_t len, uint6
             uint64_t G = 0;
             sdl_device_rows rows{};
             if (n) {
-                h->x_json[slot].ensure((size_t)n + 32);
+                const uint8_t *d_json;
                 if (pinned_in) {
-                    HIP_TRY(hipMemsetAsync(h->x_json[slot].p + n, 0, 32, h->x_in));
-                    HIP_TRY(hipMemcpyAsync(h->x_json[slot].p, jsonl + a, (size_t)n, hipMemcpyHostToDevice, h->x_in));
+                    d_json = h->x_json_all.p + region[k];
+                    HIP_TRY(hipStreamWaitEvent(sc, h->x_in_ev[k], 0));
                 } else {
+                    h->x_json[slot].ensure((size_t)n + 32);
                     if (used[slot]) HIP_TRY(hipEventSynchronize(e_h2d[slot]));
                     h->x_pin_in[slot].ensure((size_t)n + 32);
                     par_copy(h->x_pin_in[slot].p, jsonl + a, (size_t)n);
                     std::memset(h->x_pin_in[slot].p + n, 0, 32);
                     HIP_TRY(hipMemcpyAsync(h->x_json[slot].p, h->x_pin_in[slot].p, (size_t)n + 32,
                                            hipMemcpyHostToDevice, h->x_in));
+                    HIP_TRY(hipEventRecord(e_h2d[slot], h->x_in));
+                    used[slot] = true;
+                    HIP_TRY(hipStreamWaitEvent(sc, e_h2d[slot], 0));
+                    d_json = h->x_json[slot].p;
                 }
-                HIP_TRY(hipEventRecord(e_h2d[slot], h->x_in));
-                used[slot] = true;
-                HIP_TRY(hipStreamWaitEvent(sc, e_h2d[slot], 0));
                 sdl_json_text jt;
                 auto t0 = now();
-                if (int rc = sdl_json_text_device(h, h->x_json[slot].p, n, sc, &jt)) return rc;  // syncs sc
+                if (int rc = sdl_json_text_device(h, d_json, n, sc, &jt)) return rc;  // syncs sc
                 hw[0] += since(t0);
                 t0 = now();
                 lines += jt.n_lines;
@@ -1400,23 +1427,42 @@ int sdl_json_to_frames(sdl_batcher *h, const uint8_t *jsonl, uint64_t len, uint6
                 x.labels = h->x_lab[slot].p;
                 x.rows_capacity = (have / B + 1) * B;
                 x.label_width = (int32_t)LW;
-                // size the frames, then write them straight into mapped pinned host memory from the
-                // copy-out stream: no D2H copy, and the next chunk's kernels overlap the PCIe writes
+                // size the frames, write them into this slot's device buffer from the copy-out
+                // stream and copy them to pinned host memory there: the next chunk's kernels
+                // overlap the copy.  (SDL_FRAMES_MAPPED=1: the kernel writes mapped pinned host
+                // memory itself -- shader stores over PCIe measured ~25 GB/s against ~56 GB/s
+                // for the DMA copy.)
+                // The frames kernel runs on the compute stream, so the copy-out stream holds
+                // nothing but the copies and they run back to back.
                 sdl_frames fr;
                 h->f_dry = true;
                 int rc = sdl_pickle_frames_device(h, &x, nframe_rows, flush_now ? 1 : 0, h->x_out, &fr);
                 h->f_dry = false;
                 if (rc) return rc;
                 h->x_pin_out[slot].ensure((size_t)fr.total_bytes + 16);
-                void *dp = nullptr;
-                HIP_TRY(hipHostGetDevicePointer(&dp, h->x_pin_out[slot].p, 0));
-                h->f_dest = static_cast<uint8_t *>(dp);
-                h->f_dest_cap = h->x_pin_out[slot].cap;
-                HIP_TRY(hipStreamWaitEvent(h->x_out, e_rows[slot], 0));
-                rc = sdl_pickle_frames_device(h, &x, nframe_rows, flush_now ? 1 : 0, h->x_out, &fr);
+                const bool mapped = env_int("SDL_FRAMES_MAPPED", 0) != 0;
+                const hipStream_t fs = mapped ? h->x_out : sc;
+                if (mapped) {
+                    void *dp = nullptr;
+                    HIP_TRY(hipHostGetDevicePointer(&dp, h->x_pin_out[slot].p, 0));
+                    h->f_dest = static_cast<uint8_t *>(dp);
+                    h->f_dest_cap = h->x_pin_out[slot].cap;
+                } else {
+                    h->x_frames[slot].ensure((size_t)fr.total_bytes + 16);
+                    h->f_dest = h->x_frames[slot].p;
+                    h->f_dest_cap = h->x_frames[slot].cap;
+                }
+                if (mapped) HIP_TRY(hipStreamWaitEvent(h->x_out, e_rows[slot], 0));
+                rc = sdl_pickle_frames_device(h, &x, nframe_rows, flush_now ? 1 : 0, fs, &fr);
                 h->f_dest = nullptr;
                 h->f_dest_cap = 0;
                 if (rc) return rc;
+                if (!mapped) {
+                    HIP_TRY(hipEventRecord(e_rows[slot], sc));  // frames written
+                    HIP_TRY(hipStreamWaitEvent(h->x_out, e_rows[slot], 0));
+                    HIP_TRY(hipMemcpyAsync(h->x_pin_out[slot].p, h->x_frames[slot].p, (size_t)fr.total_bytes,
+                                           hipMemcpyDeviceToHost, h->x_out));
+                }
                 HIP_TRY(hipEventRecord(e_frames[slot], h->x_out));
                 pend[slot] = Pending{true, fr.n_frames, fr.frame_bytes, fr.last_frame_bytes, fr.total_bytes};
                 frames_total += fr.n_frames;
