@@ -275,6 +275,8 @@ def parse_args(argv=None):
                     help="fixture: data/test.json.gz records tiled (default); heldout: English text on the image "
                          "never used to build or tune the tables (tests/golden/heldout_records.jsonl)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--rng-mode", type=int, default=0, choices=[0, 1],
+                    help="MLM masks: 0 the Philox contract (default), 1 rand 0.8.5 StdRng per row")
     ap.add_argument("--e2e", action="store_true", help="also time the host record path (H2D + kernels + D2H)")
     ap.add_argument("--json", action="store_true",
                     help="also time the provider's JsonText filter on the device (JSON lines -> text arena)")
@@ -364,7 +366,9 @@ def base_line(args, world, step_ms, value, task, N, R, rows, toks):
                    "tokenizer": {"gpt2": "gpt2 byte-level BPE layout, offline proxy vocab (50,257)",
                                  "t5": "t5-small layout (Precompiled nmt_nfkc + Unigram), offline proxy vocab (32,100)"}
                                 .get(task["tok"], "bert-base-uncased layout, offline proxy vocab (30,522)"),
-                   "parallelism": f"record shards x{world}, no collective"},
+                   "parallelism": f"record shards x{world}, no collective",
+                   "mlm_masks": "rand 0.8.5 StdRng per row (rng_mode 1)" if getattr(args, "rng_mode", 0) == 1
+                                else "Philox contract (rng_mode 0)"},
     }
 
 
@@ -443,7 +447,7 @@ def main(argv=None):
     tok_path = {"gpt2": native.GPT2_PROXY_TOKENIZER, "t5": native.T5_PROXY_TOKENIZER}.get(task["tok"],
                                                                                           native.BERT_PROXY_TOKENIZER)
     db = DeviceBatcher(task=kind[args.task], batch_size=B, sequence_length=S, seed=1234, device=local,
-                       tokenizer=tok_path)
+                       tokenizer=tok_path, rng_mode=args.rng_mode)
     if args.task == "single-class":  # Label::Single: record i's label is i & 1 (imdb: 2 classes)
         t_lab = torch.from_numpy((np.asarray(order, np.int64) & 1).astype(np.int32)).to(dev)
         t_loff = torch.arange(R + 1, dtype=torch.int64, device=dev)

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define SDL_ABI_VERSION 5
+#define SDL_ABI_VERSION 6
 
 enum {
     SDL_OK = 0,
@@ -72,7 +72,11 @@ typedef struct sdl_config {
     uint64_t seed;           /* RNG contract seed */
     uint64_t first_record;   /* global index of this handle's first record (sharding) */
     int32_t device;          /* HIP device ordinal */
-    int32_t reserved[7];
+    int32_t rng_mode;        /* MLM masks: 0 = the Philox contract (default);
+                                1 = rand 0.8.5: position_base.shuffle(&mut StdRng::from_seed(
+                                seed | record | chunk, little-endian, zero padded)) per row
+                                (bert_data.rs:40-43 with a seeded StdRng; S <= 2048) */
+    int32_t reserved[6];
 } sdl_config;
 
 /* A finished batch: DataSet's Serialize view (bert_data.rs:106-145,

@@ -43,6 +43,97 @@ uint32_t orc_mlm_key(uint64_t seed, uint64_t record, uint32_t chunk, uint32_t po
     return c[pos & 3];
 }
 
+/* ------------------------------------------------------------------------- */
+/* Optional rand-compatible MLM mode (cfg.rng_mode = 1): BertData::mask_batch's */
+/* `position_base.shuffle(&mut thread_rng())` (bert_data.rs:40-43) with        */
+/* thread_rng replaced by a StdRng per row:                                     */
+/*     StdRng::from_seed(row_seed)   row_seed = seed (u64 LE) | record (u64 LE) */
+/*                                              | chunk (u32 LE) | 12 zero bytes */
+/* restating, from their published sources (not vendored, not buildable here): */
+/*   rand_chacha 0.3.1  StdRng = ChaCha12Rng: key = the 32-byte seed, 64-bit    */
+/*                      block counter in words 12-13 from 0, stream 0 in words  */
+/*                      14-15, output words in block order;                     */
+/*   rand 0.8.5         SliceRandom::shuffle -> gen_index -> gen_range(0..n) ->   */
+/*                      UniformInt<u32>::sample_single_inclusive (widening       */
+/*                      multiply, zone = (range << lz(range)) - 1, rejection).    */
+/* Pinned (tests/test_rand_mode.py) by RFC 7539's ChaCha20 vectors, rand's       */
+/* test_stdrng_construction vectors and rand's value_stability_slice shuffle.   */
+/* ------------------------------------------------------------------------- */
+static inline uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
+#define ORC_QR(a, b, c, d)                                                      \
+    a += b; d ^= a; d = rotl32(d, 16); c += d; b ^= c; b = rotl32(b, 12);       \
+    a += b; d ^= a; d = rotl32(d, 8);  c += d; b ^= c; b = rotl32(b, 7);
+
+void orc_chacha_block(const uint32_t key[8], uint64_t counter, uint64_t stream, int rounds, uint32_t out[16]) {
+    const uint32_t s[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u, key[0], key[1], key[2], key[3],
+                            key[4], key[5], key[6], key[7], (uint32_t)counter, (uint32_t)(counter >> 32),
+                            (uint32_t)stream, (uint32_t)(stream >> 32)};
+    uint32_t x[16];
+    memcpy(x, s, sizeof(x));
+    for (int i = 0; i < rounds; i += 2) {
+        ORC_QR(x[0], x[4], x[8], x[12]) ORC_QR(x[1], x[5], x[9], x[13])
+        ORC_QR(x[2], x[6], x[10], x[14]) ORC_QR(x[3], x[7], x[11], x[15])
+        ORC_QR(x[0], x[5], x[10], x[15]) ORC_QR(x[1], x[6], x[11], x[12])
+        ORC_QR(x[2], x[7], x[8], x[13]) ORC_QR(x[3], x[4], x[9], x[14])
+    }
+    for (int i = 0; i < 16; ++i) out[i] = x[i] + s[i];
+}
+
+typedef struct {
+    uint32_t key[8];
+    uint64_t ctr;
+    uint32_t buf[16];
+    int idx;
+} orc_stdrng;
+
+static void stdrng_from_seed(orc_stdrng *r, const uint8_t seed[32]) {
+    for (int i = 0; i < 8; ++i)
+        r->key[i] = (uint32_t)seed[4 * i] | (uint32_t)seed[4 * i + 1] << 8 | (uint32_t)seed[4 * i + 2] << 16 |
+                    (uint32_t)seed[4 * i + 3] << 24;
+    r->ctr = 0;
+    r->idx = 16;
+}
+static uint32_t stdrng_u32(orc_stdrng *r) {
+    if (r->idx >= 16) {
+        orc_chacha_block(r->key, r->ctr++, 0, 12, r->buf);
+        r->idx = 0;
+    }
+    return r->buf[r->idx++];
+}
+/* first u64 of StdRng::from_seed(seed) (next_u64: low word first) -- for the KAT */
+uint64_t orc_stdrng_first_u64(const uint8_t seed[32]) {
+    orc_stdrng r;
+    stdrng_from_seed(&r, seed);
+    const uint64_t lo = stdrng_u32(&r);
+    return lo | (uint64_t)stdrng_u32(&r) << 32;
+}
+/* gen_index(rng, n) = gen_range(0..n as u32) */
+static uint32_t gen_index(orc_stdrng *r, uint32_t n) {
+    const uint32_t zone = (n << __builtin_clz(n)) - 1u;
+    for (;;) {
+        const uint64_t m = (uint64_t)stdrng_u32(r) * n;
+        if ((uint32_t)m <= zone) return (uint32_t)(m >> 32);
+    }
+}
+/* position_base after `shuffle` with the row's StdRng */
+void orc_rand_positions(uint64_t seed, uint64_t record, uint32_t chunk, int S, uint32_t *pos) {
+    uint8_t sd[32] = {0};
+    for (int b = 0; b < 8; ++b) {
+        sd[b] = (uint8_t)(seed >> (8 * b));
+        sd[8 + b] = (uint8_t)(record >> (8 * b));
+    }
+    for (int b = 0; b < 4; ++b) sd[16 + b] = (uint8_t)(chunk >> (8 * b));
+    orc_stdrng r;
+    stdrng_from_seed(&r, sd);
+    for (int i = 0; i < S; ++i) pos[i] = (uint32_t)i;
+    for (int i = S - 1; i >= 1; --i) {
+        const uint32_t j = gen_index(&r, (uint32_t)i + 1u);
+        const uint32_t t = pos[i];
+        pos[i] = pos[j];
+        pos[j] = t;
+    }
+}
+
 /* Span draws: the reference's trunc(avg - z) with z ~ StandardNormal
  * (t5_data.rs:165-176, `as usize` saturating at 0) is sampled exactly in
  * distribution by inverting its CDF on a 32-bit uniform:
@@ -177,6 +268,20 @@ static int kp_cmp(const void *a, const void *b) {
  * (key, position) pairs. */
 static void mask_row(const orc_batcher *b, int32_t *in, int32_t *lb, uint64_t rec, uint32_t chunk) {
     const int S = b->c.S;
+    if (b->c.rng_mode == 1) { /* rand-compatible mode: the shuffled positions themselves */
+        uint32_t *pos = (uint32_t *)malloc(sizeof(uint32_t) * S);
+        orc_rand_positions(b->c.seed, rec, chunk, S, pos);
+        for (int j = 0; j < S; ++j) lb[j] = -100;
+        for (int k = 0; k < b->c.mask_length; ++k) {
+            const uint32_t p = pos[k];
+            if (in[p] != 0) {
+                lb[p] = in[p];
+                in[p] = b->c.mask_id;
+            }
+        }
+        free(pos);
+        return;
+    }
     kp *perm = (kp *)malloc(sizeof(kp) * S);
     for (int p = 0; p < S; ++p) {
         perm[p].key = orc_mlm_key(b->c.seed, rec, chunk, (uint32_t)p);
@@ -391,6 +496,8 @@ int orc_batcher_flush(orc_batcher *b, int32_t *out, int *rows) {
     if (r == 1 && rows) *rows = o.rows;
     return r;
 }
+
+void orc_batcher_set_rng_mode(orc_batcher *b, int mode) { b->c.rng_mode = mode; }
 
 void orc_cfg_default(orc_cfg *c, int task) {
     memset(c, 0, sizeof(*c));

@@ -40,6 +40,14 @@ long orc_bert_encode(const orc_tok *t, const uint8_t *s, size_t n, uint32_t *out
 /* Philox4x32-10 MLM key of (seed, record, chunk, position) -- RNG contract. */
 uint32_t orc_mlm_key(uint64_t seed, uint64_t record, uint32_t chunk, uint32_t pos);
 
+/* rand-compatible MLM mode: ChaCha block (20 rounds: RFC 7539; 12: StdRng),
+ * StdRng's first u64, and a row's shuffled positions (StdRng::from_seed of
+ * seed | record | chunk, little-endian, zero padded). */
+void orc_chacha_block(const uint32_t key[8], uint64_t counter, uint64_t stream, int rounds, uint32_t out[16]);
+uint64_t orc_stdrng_first_u64(const uint8_t seed[32]);
+void orc_rand_positions(uint64_t seed, uint64_t record, uint32_t chunk, int S, uint32_t *pos);
+void orc_batcher_set_rng_mode(orc_batcher *b, int mode); /* 0 Philox contract, 1 rand 0.8.5 StdRng */
+
 /* ---- gpt2 (byte-level BPE) tokenizer: oracle/orc_bpe.c ------------------- */
 typedef struct orc_gpt2 orc_gpt2;
 /* Loads a byte-level BPE tokenizer.json and the probed GPT-2 regex class table
@@ -74,6 +82,7 @@ typedef struct {
     int32_t task, B, S, chunk, min_ids, mask_length, mask_id, number_labels;
     double avg_span_gap, avg_span_size;
     uint64_t seed;
+    int32_t rng_mode; /* 0: Philox contract; 1: rand 0.8.5 StdRng per row (orc_rand_positions) */
 } orc_cfg;
 
 /* Caller buffers a finished batch is copied into (NULL = skip that plane):

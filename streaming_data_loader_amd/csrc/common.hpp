@@ -33,6 +33,7 @@ constexpr int PEND_CAP = SDL_PEND_CAP;            // WordPiece pieces pending th
 constexpr int RB_CAP = 256;                       // record starts listed in LDS per window
 constexpr int MAX_WORD_CHARS = 100;               // WordPiece max_input_chars_per_word
 constexpr int MAX_WORD_BYTES = 4 * MAX_WORD_CHARS + 8;
+constexpr int RAND_MAX_S = 2048;  // rng_mode 1: longest row the shuffle kernel holds in LDS
 constexpr int LW_MAX = 96;   // WordPiece: longest normalized word for the LDS lattice (bytes)
 constexpr int LW_BUF = 128;  // ... its byte buffer (LW_MAX + 20 readable), then u32 best[LW_MAX]
 
@@ -182,6 +183,8 @@ struct RowParams {
     int32_t post[MAX_FRAME];
     uint64_t seed;
     uint64_t first_record;
+    int32_t rng_mode;              // MLM masks: 0 Philox contract, 1 rand 0.8.5 StdRng (k_mask_rand)
+    const uint32_t *mask_bits;     // rng_mode 1: per row, ceil(S/32) words of mask bits
     // span (T5Data): trunc(avg - z) draws as CDF tables (RNG contract) and
     // the <extra_id_k> ids (device pointer, 100 entries)
     int32_t gap_kmin, gap_n, size_kmin, size_n;

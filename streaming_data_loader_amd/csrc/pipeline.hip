@@ -482,20 +482,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SDL_ROWS_WA
         const int tail0 = l < S ? S - l : S;
         const uint64_t rec = P.first_record + (uint64_t)r;
         if (P.task == 0) {  // MLM: BertData::mask_batch
-            uint32_t key[MR][4];
-#pragma unroll
-            for (int m = 0; m < MR; ++m) {
-                const uint4 c = philox4x32_10(make_uint4((uint32_t)(64 * m + lane), k, (uint32_t)rec,
-                                                         (uint32_t)(rec >> 32)),
-                                              (uint32_t)P.seed, (uint32_t)(P.seed >> 32));
-                const int j0 = 256 * m + 4 * lane;
-                key[m][0] = j0 < S ? c.x : 0xFFFFFFFFu;
-                key[m][1] = j0 + 1 < S ? c.y : 0xFFFFFFFFu;
-                key[m][2] = j0 + 2 < S ? c.z : 0xFFFFFFFFu;
-                key[m][3] = j0 + 3 < S ? c.w : 0xFFFFFFFFu;
-            }
             bool sel[MR][4];
-            select_k_smallest<MR>(key, P.mask_length, sel);
+            if (P.rng_mode == 1) {  // rand-compatible mode: the row's bits from k_mask_rand
+                const uint32_t *mb = P.mask_bits + g * (int64_t)((S + 31) >> 5);
+#pragma unroll
+                for (int m = 0; m < MR; ++m) {
+                    const int j0 = 256 * m + 4 * lane;
+                    const uint32_t wd = j0 < S ? mb[j0 >> 5] : 0u;
+#pragma unroll
+                    for (int w = 0; w < 4; ++w) sel[m][w] = (wd >> ((j0 + w) & 31)) & 1u;
+                }
+            } else {
+                uint32_t key[MR][4];
+#pragma unroll
+                for (int m = 0; m < MR; ++m) {
+                    const uint4 c = philox4x32_10(make_uint4((uint32_t)(64 * m + lane), k, (uint32_t)rec,
+                                                             (uint32_t)(rec >> 32)),
+                                                  (uint32_t)P.seed, (uint32_t)(P.seed >> 32));
+                    const int j0 = 256 * m + 4 * lane;
+                    key[m][0] = j0 < S ? c.x : 0xFFFFFFFFu;
+                    key[m][1] = j0 + 1 < S ? c.y : 0xFFFFFFFFu;
+                    key[m][2] = j0 + 2 < S ? c.z : 0xFFFFFFFFu;
+                    key[m][3] = j0 + 3 < S ? c.w : 0xFFFFFFFFu;
+                }
+                select_k_smallest<MR>(key, P.mask_length, sel);
+            }
 #pragma unroll
             for (int m = 0; m < MR; ++m) {
                 const int j0 = 256 * m + 4 * lane;
@@ -544,6 +555,127 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SDL_ROWS_WA
             }
         }
     }
+}
+
+// ---------------------------------------------------------------------------
+// rand-compatible MLM masks (rng_mode 1, oracle/orc_batcher.c orc_rand_positions):
+// BertData::mask_batch's position_base.shuffle (bert_data.rs:40-43; rand 0.8.5
+// SliceRandom::shuffle -> gen_index -> UniformInt<u32> widening-multiply
+// rejection) driven by StdRng::from_seed(seed | record | chunk) (rand_chacha
+// 0.3.1 ChaCha12: 64-bit block counter, stream 0, words in block order).
+// One wave per row: lanes compute the ChaCha12 blocks of the S-1 draws the
+// shuffle takes when nothing is rejected and every swap's index j_i at once;
+// a rejection anywhere in the row (probability ~S^2 / 2^32) sends lane 0 through
+// the draws in order.  The first mask_length shuffled positions follow each
+// x < mask_length back through the swaps (last applied first): a lane per x,
+// the S-1 swap indices read from LDS.  Output: the row's mask bits.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
+#define CC_QR(a, b, c, d)                                                         \
+    a += b; d ^= a; d = rotl32(d, 16); c += d; b ^= c; b = rotl32(b, 12);         \
+    a += b; d ^= a; d = rotl32(d, 8);  c += d; b ^= c; b = rotl32(b, 7);
+// ChaCha12 block `ctr` of key k (stream 0)
+__device__ __forceinline__ void chacha12_block(const uint32_t (&k)[8], uint32_t ctr, uint32_t (&o)[16]) {
+    uint32_t x0 = 0x61707865u, x1 = 0x3320646eu, x2 = 0x79622d32u, x3 = 0x6b206574u;
+    uint32_t x4 = k[0], x5 = k[1], x6 = k[2], x7 = k[3], x8 = k[4], x9 = k[5], x10 = k[6], x11 = k[7];
+    uint32_t x12 = ctr, x13 = 0u, x14 = 0u, x15 = 0u;
+#pragma unroll
+    for (int r = 0; r < 6; ++r) {
+        CC_QR(x0, x4, x8, x12) CC_QR(x1, x5, x9, x13) CC_QR(x2, x6, x10, x14) CC_QR(x3, x7, x11, x15)
+        CC_QR(x0, x5, x10, x15) CC_QR(x1, x6, x11, x12) CC_QR(x2, x7, x8, x13) CC_QR(x3, x4, x9, x14)
+    }
+    o[0] = x0 + 0x61707865u; o[1] = x1 + 0x3320646eu; o[2] = x2 + 0x79622d32u; o[3] = x3 + 0x6b206574u;
+    o[4] = x4 + k[0]; o[5] = x5 + k[1]; o[6] = x6 + k[2]; o[7] = x7 + k[3];
+    o[8] = x8 + k[4]; o[9] = x9 + k[5]; o[10] = x10 + k[6]; o[11] = x11 + k[7];
+    o[12] = x12 + ctr; o[13] = x13; o[14] = x14; o[15] = x15;
+}
+
+__global__ __launch_bounds__(64) void k_mask_rand(RowParams P, const uint32_t *__restrict__ row_off,
+                                                  const uint32_t *__restrict__ row_rec, SegSel sel, int64_t rows_cap,
+                                                  uint32_t *__restrict__ bits) {
+    __shared__ uint32_t s_draw[RAND_MAX_S + 16];
+    __shared__ uint16_t s_j[RAND_MAX_S];
+    __shared__ uint32_t s_bits[RAND_MAX_S / 32];
+    const int lane = lane_id();
+    const int S = P.S, W = (S + 31) >> 5, kmask = P.mask_length < S ? P.mask_length : S;
+    const int nblk = (S - 1 + 15) >> 4;
+    const RowSpan rs = row_span(sel, row_off, P.B, rows_cap);
+    for (int64_t g = rs.g_lo + blockIdx.x; g < (int64_t)rs.g_real; g += gridDim.x) {
+        const int64_t r = row_rec[g];
+        const uint32_t chunk = (uint32_t)(g - row_off[r]);
+        const uint64_t rec = P.first_record + (uint64_t)r;
+        const uint32_t key[8] = {(uint32_t)P.seed, (uint32_t)(P.seed >> 32), (uint32_t)rec, (uint32_t)(rec >> 32),
+                                 chunk, 0u, 0u, 0u};
+        for (int b = lane; b < nblk; b += 64) {
+            uint32_t o[16];
+            chacha12_block(key, (uint32_t)b, o);
+#pragma unroll
+            for (int q = 0; q < 16; ++q) s_draw[16 * b + q] = o[q];
+        }
+        for (int w = lane; w < W; w += 64) s_bits[w] = 0u;
+        __syncthreads();
+        // draw t feeds swap i = S-1-t when nothing before it was rejected
+        bool rej = false;
+        for (int t = lane; t < S - 1; t += 64) {
+            const uint32_t n = (uint32_t)(S - t), zone = (n << __builtin_clz(n)) - 1u;
+            const uint64_t m = (uint64_t)s_draw[t] * n;
+            rej = rej || (uint32_t)m > zone;
+            s_j[S - 1 - t] = (uint16_t)(m >> 32);
+        }
+        if (__any(rej)) {  // (rare) the draws in order, blocks past the buffer computed on demand
+            __syncthreads();
+            if (lane == 0) {
+                uint32_t blk[16];
+                int have = -1;
+                int t = 0;
+                for (int i = S - 1; i >= 1; --i) {
+                    const uint32_t n = (uint32_t)i + 1u, zone = (n << __builtin_clz(n)) - 1u;
+                    for (;;) {
+                        uint32_t v;
+                        if (t < 16 * nblk) {
+                            v = s_draw[t];
+                        } else {
+                            if ((t >> 4) != have) {
+                                have = t >> 4;
+                                chacha12_block(key, (uint32_t)have, blk);
+                            }
+                            v = blk[t & 15];
+                        }
+                        ++t;
+                        const uint64_t m = (uint64_t)v * n;
+                        if ((uint32_t)m <= zone) {
+                            s_j[i] = (uint16_t)(m >> 32);
+                            break;
+                        }
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        // the first kmask shuffled positions: x traced back through swaps 1 .. S-1
+        for (int x0 = 0; x0 < kmask; x0 += 128) {
+            int p0 = x0 + lane, p1 = x0 + 64 + lane;
+            for (int i = 1; i < S; ++i) {
+                const int ji = s_j[i];
+                p0 = p0 == i ? ji : p0 == ji ? i : p0;
+                p1 = p1 == i ? ji : p1 == ji ? i : p1;
+            }
+            if (x0 + lane < kmask) atomicOr(&s_bits[p0 >> 5], 1u << (p0 & 31));
+            if (x0 + 64 + lane < kmask) atomicOr(&s_bits[p1 >> 5], 1u << (p1 & 31));
+        }
+        __syncthreads();
+        uint32_t *dst = bits + g * (int64_t)W;
+        for (int w = lane; w < W; w += 64) dst[w] = s_bits[w];
+        __syncthreads();
+    }
+}
+
+hipError_t launch_mask_rand(const RowParams &P, const uint32_t *row_off, const uint32_t *row_rec, SegSel sel,
+                            int64_t rows_cap, uint32_t *bits, hipStream_t st) {
+    if (rows_cap <= 0) return hipSuccess;
+    const int64_t grid = rows_cap < 16384 ? rows_cap : 16384;
+    hipLaunchKernelGGL(k_mask_rand, dim3((unsigned)grid), dim3(64), 0, st, P, row_off, row_rec, sel, rows_cap, bits);
+    return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------

@@ -268,6 +268,7 @@ struct sdl_batcher {
     DevBuf<uint32_t> ranges, tokc, chunk_cnt, chunk_off, rec_local, tok_ids, rec_tok, rec_cnt, rec_rows, row_off,
         row_rec, scan_tmp;
     DevBuf<int32_t> o_ids, o_am, o_tt, o_lab;
+    DevBuf<uint32_t> mask_bits;  // rng_mode 1: per-row mask bits (k_mask_rand)
     DevBuf<float> o_f32;
     DevBuf<uint32_t> lab_err;
     // byte-level BPE long pieces
@@ -408,9 +409,12 @@ struct sdl_batcher {
             if (single()) lab_err.ensure(1);
         }
         row_rec.ensure((size_t)std::max<int64_t>(rows_cap, 1));
+        if (P.task == SDL_TASK_MLM && P.rng_mode == 1)
+            mask_bits.ensure((size_t)std::max<int64_t>(rows_cap, 1) * (size_t)((P.S + 31) / 32));
 
         RowParams p = P;
         p.first_record = first_record;
+        p.mask_bits = mask_bits.p;
         const bool bpe = dt.kind == TOK_BYTE_BPE;
         const bool uni = dt.kind == TOK_UNIGRAM;
         // Pipelined segments (WordPiece): the tokenize launches of the chunk
@@ -470,6 +474,8 @@ struct sdl_batcher {
                 HIP_TRY(launch_rows_span(p, tok_ids.p, rec_tok.p, rec_cnt.p, row_off.p, row_rec.p, sel, rows_cap, out,
                                          span_err.p, s));
             } else {
+                if (p.task == SDL_TASK_MLM && p.rng_mode == 1)
+                    HIP_TRY(launch_mask_rand(p, row_off.p, row_rec.p, sel, rows_cap, mask_bits.p, s));
                 HIP_TRY(launch_rows(p, tok_ids.p, rec_tok.p, rec_cnt.p, row_off.p, row_rec.p, sel, rows_cap, out, s));
             }
             if (multi())
@@ -727,6 +733,9 @@ int sdl_batcher_create(const sdl_config *cfg, const char *tokenizer_path, const 
         return fail(SDL_ERR_ARG, "batch_size must be > 0 and 0 < sequence_length <= 2048");
     if (cfg->task == SDL_TASK_MLM && (cfg->mask_length < 0 || cfg->mask_length > cfg->sequence_length))
         return fail(SDL_ERR_ARG, "mask_length must be in [0, sequence_length]");
+    if (cfg->rng_mode != 0 && cfg->rng_mode != 1) return fail(SDL_ERR_ARG, "rng_mode must be 0 or 1");
+    if (cfg->task == SDL_TASK_MLM && cfg->rng_mode == 1 && cfg->sequence_length > RAND_MAX_S)
+        return fail(SDL_ERR_UNSUPPORTED, "rng_mode 1 supports sequence_length <= 2048");
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
         return fail(SDL_ERR_NODEV, "no HIP device visible: the Batcher runs only on the GPU (no CPU fallback)");
@@ -874,6 +883,7 @@ int sdl_batcher_create(const sdl_config *cfg, const char *tokenizer_path, const 
             P.min_ids = 0;
         }
         P.seed = cfg->seed;
+        P.rng_mode = cfg->rng_mode;
         if (t.kind == TOK_UNIGRAM) {
             // encode_mask framing for T5 (tokenizer_wrapper.rs:125-131): [eos] + template($A </s>) + [eos]
             P.n_pre = 1;

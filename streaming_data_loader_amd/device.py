@@ -95,13 +95,14 @@ class DeviceBatcher:
 
     def __init__(self, task=native.SDL_TASK_MLM, batch_size=256, sequence_length=512, mask_length=None,
                  mask_id=103, seed=0, device=0, tokenizer=native.BERT_PROXY_TOKENIZER, chunk=True, min_ids=None,
-                 number_labels=9, avg_span_gap=16.0, avg_span_size=2.0):
+                 number_labels=9, avg_span_gap=16.0, avg_span_size=2.0, rng_mode=0):
         L = native.load()
         c = native.default_config(task)
         c.batch_size, c.sequence_length = batch_size, sequence_length
         c.mask_length = int(np.float32(sequence_length) * np.float32(0.15)) if mask_length is None else mask_length
         c.mask_id, c.seed, c.device, c.chunk = mask_id, seed, device, 1 if chunk else 0
         c.number_labels = number_labels
+        c.rng_mode = rng_mode
         c.avg_span_gap, c.avg_span_size = avg_span_gap, avg_span_size
         if min_ids is not None:
             c.min_ids = min_ids

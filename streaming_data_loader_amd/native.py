@@ -38,7 +38,7 @@ class Config(ctypes.Structure):
         ("mask_id", ctypes.c_int32), ("number_labels", ctypes.c_int32),
         ("avg_span_gap", ctypes.c_double), ("avg_span_size", ctypes.c_double),
         ("seed", ctypes.c_uint64), ("first_record", ctypes.c_uint64),
-        ("device", ctypes.c_int32), ("reserved", ctypes.c_int32 * 7),
+        ("device", ctypes.c_int32), ("rng_mode", ctypes.c_int32), ("reserved", ctypes.c_int32 * 6),
     ]
 
 

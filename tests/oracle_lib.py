@@ -40,6 +40,10 @@ def lib():
         L.orc_tok_free.argtypes = [vp]
         L.orc_bert_encode.restype = ctypes.c_long
         L.orc_bert_encode.argtypes = [vp, ctypes.c_char_p, ctypes.c_size_t, vp, ctypes.c_size_t]
+        L.orc_chacha_block.argtypes = [vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int, vp]
+        L.orc_stdrng_first_u64.restype = ctypes.c_uint64
+        L.orc_stdrng_first_u64.argtypes = [vp]
+        L.orc_rand_positions.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int, vp]
         L.orc_mlm_key.restype = ctypes.c_uint32
         L.orc_mlm_key.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32]
         L.orc_batcher_new.restype = vp
@@ -49,6 +53,7 @@ def lib():
         L.orc_batcher_flush.argtypes = [vp, vp, vp]
         L.orc_batcher_free.argtypes = [vp]
         L.orc_batcher_set_next_record.argtypes = [vp, ctypes.c_uint64]
+        L.orc_batcher_set_rng_mode.argtypes = [vp, ctypes.c_int]
         L.orc_encoder_size.restype = ctypes.c_size_t
         L.orc_encoder_bert.argtypes = [vp, vp]
         L.orc_encoder_bert.restype = None
@@ -91,7 +96,7 @@ class OrcCfg(ctypes.Structure):
     _fields_ = [("task", ctypes.c_int32), ("B", ctypes.c_int32), ("S", ctypes.c_int32), ("chunk", ctypes.c_int32),
                 ("min_ids", ctypes.c_int32), ("mask_length", ctypes.c_int32), ("mask_id", ctypes.c_int32),
                 ("number_labels", ctypes.c_int32), ("avg_span_gap", ctypes.c_double),
-                ("avg_span_size", ctypes.c_double), ("seed", ctypes.c_uint64)]
+                ("avg_span_size", ctypes.c_double), ("seed", ctypes.c_uint64), ("rng_mode", ctypes.c_int32)]
 
 
 class OrcOut(ctypes.Structure):
@@ -234,10 +239,11 @@ class OracleBatcherEx:
     batch planes (copies) or None."""
 
     def __init__(self, encoder, task, B, S, mask_length=None, mask_id=103, number_labels=9, seed=0,
-                 chunk=None, min_ids=None, avg_span_gap=16.0, avg_span_size=2.0):
+                 chunk=None, min_ids=None, avg_span_gap=16.0, avg_span_size=2.0, rng_mode=0):
         c = OrcCfg()
         lib().orc_cfg_default(ctypes.byref(c), task)
         c.B, c.S, c.mask_id, c.number_labels, c.seed = B, S, mask_id, number_labels, seed
+        c.rng_mode = rng_mode
         c.avg_span_gap, c.avg_span_size = avg_span_gap, avg_span_size
         c.mask_length = int(np.float32(S) * np.float32(0.15)) if mask_length is None else mask_length
         if chunk is not None:
@@ -292,11 +298,12 @@ class OracleBatcherEx:
             self.h = None
 
 
-def oracle_rows(tok, texts, S, mask_length, mask_id=103, seed=0, B=64, first_record=0):
+def oracle_rows(tok, texts, S, mask_length, mask_id=103, seed=0, B=64, first_record=0, rng_mode=0):
     """All rows the reference Batcher would produce for `texts`, in order
     (concatenation of every batch, flushing until the queue is empty)."""
     ob = OracleBatcher(tok, B, S, mask_length, mask_id, seed)
     ob.set_next_record(first_record)
+    lib().orc_batcher_set_rng_mode(ob.h, rng_mode)
     planes = []
     for t in texts:
         r = ob.push(t)

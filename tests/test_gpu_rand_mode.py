@@ -1,0 +1,48 @@
+"""GPU parity of the rand-compatible MLM mode (rng_mode 1, k_mask_rand):
+device rows bit-exact against the oracle, whose StdRng / shuffle restatement
+is pinned by rand's and RFC 7539's vectors (tests/test_rand_mode.py)."""
+import numpy as np
+import pytest
+
+import oracle_lib
+from streaming_data_loader_amd.device import DeviceBatcher
+from test_gpu_parity import hard_records, run_device
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch as t
+    assert t.cuda.is_available(), "GPU tests need a HIP device"
+    return t
+
+
+@pytest.mark.parametrize("S,B,first_record,seed", [(128, 8, 0, 5), (512, 256, 1000, 1234), (1024, 16, 7, 2 ** 63 + 3)])
+def test_rand_mode_rows_match_oracle(torch, native_lib, oracle_tok, records, S, B, first_record, seed):
+    rng = np.random.default_rng(S)
+    texts = [records[i] for i in rng.integers(0, len(records), 300)] + hard_records(2)[:40]
+    k = int(np.float32(S) * np.float32(0.15))
+    db = DeviceBatcher(batch_size=B, sequence_length=S, seed=seed, rng_mode=1)
+    res = run_device(torch, db, texts, first_record=first_record)
+    G = res.rows()
+    got = res.planes(G)
+    want = oracle_lib.oracle_rows(oracle_tok, texts, S, k, 103, seed=seed, B=B, first_record=first_record,
+                                  rng_mode=1)
+    assert want.shape[1] == G
+    for j in range(4):
+        np.testing.assert_array_equal(got[j], want[j])
+    # the Philox contract gives other masks on the same rows
+    db0 = DeviceBatcher(batch_size=B, sequence_length=S, seed=seed, rng_mode=0)
+    lab0 = run_device(torch, db0, texts, first_record=first_record).planes(G)[3]
+    assert not np.array_equal(lab0, got[3])
+    masked = (got[3] != -100).sum(axis=1)
+    assert masked.max() <= k and masked.mean() > 0.2 * k  # pad positions (id 0) are never masked
+
+
+def test_rand_mode_rejects_long_rows(native_lib):
+    from streaming_data_loader_amd import native
+    with pytest.raises(native.SDLError):
+        DeviceBatcher(batch_size=8, sequence_length=4096, rng_mode=1)
+    with pytest.raises(native.SDLError):
+        DeviceBatcher(batch_size=8, sequence_length=128, rng_mode=2)
