@@ -410,6 +410,10 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
     __shared__ uint8_t s_cnt[CHUNK];       // ids per piece
     __shared__ uint16_t s_pend[PEND_CAP];  // pending piece indices (step 4b)
     __shared__ uint32_t s_scratch[TOK_THREADS / 64 + 3];
+    // non-ASCII chars found by the rare pass: [0, 32) a WS/ISO char starts at the
+    // chunk position (a word before it ends there), [32, 64) an ISO char whose id
+    // is already in its stage slot
+    __shared__ uint32_t s_nabits[2 * CHUNK / 32];
 #ifdef SDL_LDS_PAD  // diagnostic: occupancy sensitivity
     __shared__ uint8_t s_pad[SDL_LDS_PAD];
     if (N < 0) {
@@ -441,6 +445,7 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
     *reinterpret_cast<uint4 *>(s_win + HALO_L + 16 * tid) = v;
     if (tid < (WIN - CHUNK) / 16) *reinterpret_cast<uint4 *>(s_win + (hp - w0)) = hv;
     if (tid <= RBITS_WORDS) s_rbits[tid] = 0;
+    s_nabits[tid] = 0u;  // 2 * CHUNK / 32 == TOK_THREADS words
     const int nrb = (int)(rz - ra);
     int64_t rb_next = rz <= R ? (int64_t)off[rz] : N;
     if (rb_next > N) rb_next = N;
@@ -530,8 +535,30 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
     SDL_STAMP(2);
     for (uint32_t k = tid; k < n_leads; k += TOK_THREADS) {
         const int wi = s_pieces[k];
+        const int rel = wi - HALO_L;
         int len;
-        s_ovr[wi - HALO_L] = (uint8_t)vclass_of_entry(uentry(T, decode(C, w0 + wi, win[wi], &len)));
+        const uint32_t e = uentry(T, decode(C, w0 + wi, win[wi], &len));
+        const uint32_t vc = vclass_of_entry(e);
+        s_ovr[rel] = (uint8_t)vc;
+        if (vc == V_WS || vc == V_ISO) atomicOr(&s_nabits[rel >> 5], 1u << (rel & 31));
+        // an ISO char is a piece of its own: when it normalizes to one char of <= 16
+        // bytes, its WordPiece is one probe of that char (no "##" piece can start
+        // inside a char), done here so the piece skips the pending pass
+        if (vc == V_ISO && (e & 24u) != 16u && ((e & 4u) || ((e & 8u) && ((e >> 6) & 3u) == 0u))) {
+            W16 w{0, 0, 0, 0};
+            int L;
+            if (e & 4u) {
+                L = len;
+                for (int q = 0; q < len; ++q) w16_put(w, q, win[wi + q]);
+            } else {
+                L = (int)((e >> 4) & 3u) + 1;
+                for (int q = 0; q < L; ++q) w16_put(w, q, (e >> (8 + 8 * q)) & 0xFFu);
+            }
+            const int id = L <= T.maxlen_first ? probe_result(probe_load(T, hash16(w, (uint32_t)L, 0u)), (uint32_t)L, w)
+                                               : -1;
+            s_stage[rel] = (uint16_t)(id >= 0 ? id : T.unk_id);
+            atomicOr(&s_nabits[CHUNK / 32 + (rel >> 5)], 1u << (rel & 31));
+        }
     }
     if (n_opens) {  // block-uniform
         __syncthreads();
@@ -665,7 +692,9 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
             const uint32_t t =
                 Lw < 16 ? (((Lw < 4 ? raw.x : Lw < 8 ? raw.y : Lw < 12 ? raw.z : raw.w) >> (8 * (Lw & 3))) & 0xFFu) : b16;
             const uint32_t tc = t < 0x80u ? ascii_vclass(t) : V_NONE;
-            fast = tc == V_WS || tc == V_ISO || c0 + prel + Lw >= N;
+            const int te = prel + Lw;  // a non-ASCII WS/ISO char there ends the word too
+            fast = tc == V_WS || tc == V_ISO || c0 + prel + Lw >= N ||
+                   (t >= 0xC0u && te < CHUNK && ((s_nabits[te >> 5] >> (te & 31)) & 1u));
         }
         lw = keep_bytes(W16{swar_lower(raw.x), swar_lower(raw.y), swar_lower(raw.z), swar_lower(raw.w)}, Lw);
         Lout = Lw;
@@ -701,6 +730,8 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
                 if (b < 0x80u) {
                     stage[prel] = (uint16_t)T.ascii_id[b];
                     s_cnt[pi] = 1;
+                } else if ((s_nabits[CHUNK / 32 + (prel >> 5)] >> (prel & 31)) & 1u) {
+                    s_cnt[pi] = 1;  // its id is in its stage slot (rare pass)
                 } else {
                     pend[u] = true;
                 }
