@@ -585,13 +585,25 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
             if (c != 0xFFu) cls = (cls & ~(0xFull << (4 * i))) | ((uint64_t)c << (4 * i));
         }
     }
+    // Fast case (nearly every lane): 16 owned bytes, all visible, no record start.
+    // Then the carry summary is the last char's class and the piece starts are
+    // nibble-parallel: start_i = SPEC/ISO, or OTHER after a non-OTHER char.
+    constexpr uint64_t NIB1 = 0x1111111111111111ull;
+    auto nib_zero = [](uint64_t x) -> uint64_t {  // 1 at the base bit of every zero nibble
+        return ~(x | (x >> 1) | (x >> 2) | (x >> 3)) & NIB1;
+    };
+    const bool fast_lane = rmask == 0u && nown == 16 && nib_zero(cls) == 0ull;
     // lane summary for the carry scan: 0 = pass-through, 0x100 | v = state after
     uint32_t summ = 0;
+    if (fast_lane) {
+        summ = 0x100u | (uint32_t)(cls >> 60);
+    } else {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        if ((rmask >> i) & 1u) summ = 0x100u | V_NONE;
-        const uint32_t c = (uint32_t)(cls >> (4 * i)) & 0xFu;
-        if (c != V_NONE) summ = 0x100u | c;
+        for (int i = 0; i < 16; ++i) {
+            if ((rmask >> i) & 1u) summ = 0x100u | V_NONE;
+            const uint32_t c = (uint32_t)(cls >> (4 * i)) & 0xFu;
+            if (c != V_NONE) summ = 0x100u | c;
+        }
     }
     // state before the chunk: last visible char of the same record before c0
     if (tid == 0) {
@@ -617,13 +629,24 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
     uint32_t pmask = 0;
     {
         uint32_t st = (st_in & 0x100u) ? (st_in & 0xFFu) : chunk_state;
+        if (fast_lane) {
+            const uint64_t is_o = nib_zero(cls ^ (NIB1 * V_OTHER));
+            const uint64_t is_si = nib_zero(cls ^ (NIB1 * V_ISO)) | nib_zero(cls ^ (NIB1 * V_SPEC));
+            const uint64_t prev_o = (is_o << 4) | (st == V_OTHER ? 1ull : 0ull);
+            uint64_t m = (is_si | (is_o & ~prev_o)) & NIB1;  // bit 4i: a piece starts at byte i
+            m = (m | (m >> 3)) & 0x0303030303030303ull;
+            m = (m | (m >> 6)) & 0x000F000F000F000Full;
+            m = (m | (m >> 12)) & 0x000000FF000000FFull;
+            pmask = (uint32_t)((m | (m >> 24)) & 0xFFFFull);
+        } else {
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            if ((rmask >> i) & 1u) st = V_NONE;
-            const uint32_t c = (uint32_t)(cls >> (4 * i)) & 0xFu;
-            if (c != V_NONE) {
-                if (c == V_SPEC || c == V_ISO || (c == V_OTHER && st != V_OTHER)) pmask |= 1u << i;
-                st = c;
+            for (int i = 0; i < 16; ++i) {
+                if ((rmask >> i) & 1u) st = V_NONE;
+                const uint32_t c = (uint32_t)(cls >> (4 * i)) & 0xFu;
+                if (c != V_NONE) {
+                    if (c == V_SPEC || c == V_ISO || (c == V_OTHER && st != V_OTHER)) pmask |= 1u << i;
+                    st = c;
+                }
             }
         }
     }
