@@ -1214,6 +1214,10 @@ __device__ Scratch make_scratch(uint8_t *mine, int cap) {
 // to the huge list.  KMAX bounds a row's candidate ends (max(Mm + 1, Mf));
 // the LDS footprint (~20 KB at KMAX 32) sets how many items a CU keeps in flight.
 constexpr int LONG_NORM = 512;
+#ifndef SDL_LONG_UNROLL
+#define SDL_LONG_UNROLL 4
+#endif
+constexpr int LONG_UNROLL = SDL_LONG_UNROLL;  // candidate probes in flight per lane (k_unigram_long)
 constexpr int LONG_RAW = 1024;
 
 template <int KMAX>
@@ -1381,13 +1385,13 @@ __global__ __launch_bounds__(64) void k_unigram_long(DevTok T, const uint8_t *__
                 const int tz = r0 + nrow > L ? vp_tasks(L, Mm, Mf) : vp_c0(L, Mm) + vp_rowoff(r0 + nrow - 1, L, Mf);
                 s_mask[lane] = 0ull;
                 __syncthreads();
-                for (int tq = ta; tq < tz; tq += 256) {
-                    Probe P[4];
-                    W16 Wd[4];
-                    int gen[4];
-                    uint32_t gw3[4], meta[4];  // row | k << 8 | len << 16 | cont << 24; ~0u: none
+                for (int tq = ta; tq < tz; tq += 64 * LONG_UNROLL) {
+                    Probe P[LONG_UNROLL];
+                    W16 Wd[LONG_UNROLL];
+                    int gen[LONG_UNROLL];
+                    uint32_t gw3[LONG_UNROLL], meta[LONG_UNROLL];  // row | k << 8 | len << 16 | cont << 24; ~0u: none
 #pragma unroll
-                    for (int u = 0; u < 4; ++u) {
+                    for (int u = 0; u < LONG_UNROLL; ++u) {
                         const int t = tq + 64 * u + lane;
                         meta[u] = ~0u;
                         gen[u] = -2;
@@ -1418,7 +1422,7 @@ __global__ __launch_bounds__(64) void k_unigram_long(DevTok T, const uint8_t *__
                         }
                     }
 #pragma unroll
-                    for (int u = 0; u < 4; ++u) {
+                    for (int u = 0; u < LONG_UNROLL; ++u) {
                         if (meta[u] == ~0u) continue;
                         uint32_t w3 = gw3[u];
                         const uint32_t key = ((meta[u] >> 16) & 0xFFu) | ((meta[u] >> 24) << 8);
@@ -1549,7 +1553,11 @@ hipError_t launch_unigram_chunks(const DevTok &T, const uint8_t *text, int64_t N
     hipLaunchKernelGGL(k_unigram_chunks, dim3((unsigned)n_chunks), dim3(TOK_THREADS), 0, st, T, text, N, off, R, ranges,
                        tokc, chunk_cnt, chunk_ent, rec_local, W.counters, W.items, W.item_cap, W.err);
     // a row's candidate ends: <= Mm + 1 ("▁" row) or <= Mf
-    if (T.maxlen_meta + 1 <= 32 && T.maxlen_first <= 32)
+    if (T.maxlen_meta + 1 <= 20 && T.maxlen_first <= 20)  // smaller LDS: more items in flight
+        hipLaunchKernelGGL(k_unigram_long<20>, dim3((unsigned)W.lane_blocks), dim3(64), 0, st, T, text, N, off, R,
+                           ranges, W.items, W.item_cap, W.counters, tokc, chunk_cnt, rec_local, W.pool, W.pool_cap, W.huge,
+                           W.huge_cap, W.err);
+    else if (T.maxlen_meta + 1 <= 32 && T.maxlen_first <= 32)
         hipLaunchKernelGGL(k_unigram_long<32>, dim3((unsigned)W.lane_blocks), dim3(64), 0, st, T, text, N, off, R,
                            ranges, W.items, W.item_cap, W.counters, tokc, chunk_cnt, rec_local, W.pool, W.pool_cap, W.huge,
                            W.huge_cap, W.err);
