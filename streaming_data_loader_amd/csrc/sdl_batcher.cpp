@@ -490,8 +490,8 @@ struct sdl_batcher {
             // its window, and medium words whose normalization overflows the
             // chunk's arena: N / 8 + n_chunks bounds every realistic text (an
             // overflow is flagged in d_tokenize_errors); their ids go to the pool
-            // long items: one wave each; 256 CUs x 8 resident (k_unigram_long<20>: 18 KB of LDS)
-            const int lane_blocks = (int)env_int("SDL_UNI_LONG_BLOCKS", 2048), huge_blocks = 8;
+            // long items: one wave each; 256 CUs x 9 resident (k_unigram_long<20>: 17 KB of LDS, 154 VGPRs)
+            const int lane_blocks = (int)env_int("SDL_UNI_LONG_BLOCKS", 2304), huge_blocks = 8;
             uni_counters.ensure(4);
             uni_err.ensure(1);
             uni_items.ensure((size_t)(N / 8 + n_chunks + 64));

@@ -1215,7 +1215,7 @@ __device__ Scratch make_scratch(uint8_t *mine, int cap) {
 // the LDS footprint (~20 KB at KMAX 32) sets how many items a CU keeps in flight.
 constexpr int LONG_NORM = 512;
 #ifndef SDL_LONG_UNROLL
-#define SDL_LONG_UNROLL 4
+#define SDL_LONG_UNROLL 2
 #endif
 constexpr int LONG_UNROLL = SDL_LONG_UNROLL;  // candidate probes in flight per lane (k_unigram_long)
 constexpr int LONG_RAW = 1024;
@@ -1233,8 +1233,11 @@ __global__ __launch_bounds__(64) void k_unigram_long(DevTok T, const uint8_t *__
     __shared__ uint32_t s_st[LONG_NORM + 8];  // node start | id << 16 (0xFFFF: unset)
     __shared__ uint16_t s_ids[2 * LONG_NORM + 16];
     __shared__ uint16_t s_cid[KMAX * 64];     // [k][lane]: id of row lane's k-th end
-    __shared__ float s_csc[KMAX * 64];
-    __shared__ __attribute__((aligned(16))) uint8_t s_raw[LONG_RAW];
+    __shared__ __attribute__((aligned(16))) float s_csc[KMAX * 64];
+    // the item's raw bytes are staged where the candidate scores go later (the
+    // normalization is done before the first probe): 1 KB less LDS per item
+    static_assert(KMAX * 64 * 4 >= LONG_RAW, "raw staging aliases s_csc");
+    uint8_t *const s_raw = reinterpret_cast<uint8_t *>(s_csc);
     __shared__ unsigned long long s_mask[64];
     __shared__ int s_misc[8];
     const int lane = lane_id();
