@@ -39,13 +39,15 @@ hipError_t launch_bpe_chunks(const DevTok &T, const uint8_t *text, int64_t N, co
 // follow-up kernels into `pool` ([k, ids...] per item), their chunk entry
 // LONG_MARK | pool offset (k_compact_tokens expands it).
 struct UniWork {
-    uint32_t *counters;   // [0] long items [1] - [2] pool words used [3] huge items
+    uint32_t *counters;   // [0] long items [1] - [2] pool words used [3] huge items [4] stage-2 items
     uint4 *items;         // long items (chunk, tokc entry, prel, raw length or 0)
     uint32_t item_cap;
     uint32_t *pool;
     uint32_t pool_cap;
     uint4 *huge;          // items past a lane's scratch
     uint32_t huge_cap;
+    uint4 *items2;        // stage-2 long items (normalized past LONG_NORM1)
+    uint32_t items2_cap;
     uint8_t *scratch;     // unigram_scratch_bytes(lane_blocks, huge_blocks)
     int lane_blocks, huge_blocks;
     uint32_t *err;        // bit 1 ids overflow, 2 pool, 3 item lists, 4 item too large

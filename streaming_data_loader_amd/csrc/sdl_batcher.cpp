@@ -296,7 +296,7 @@ struct sdl_batcher {
     hipEvent_t x_ev[8] = {};
     std::vector<hipEvent_t> x_in_ev;  // json_to_frames, pinned input: chunk k's H2D done
     DevBuf<uint8_t> x_json_all;       // ... every chunk, 32 zero bytes after each
-    DevBuf<uint4> uni_items, uni_huge;
+    DevBuf<uint4> uni_items, uni_items2, uni_huge;
     DevBuf<uint8_t> uni_scratch;
     DevBuf<uint8_t> h2d_text;
     DevBuf<uint64_t> h2d_off, h2d_label_off;
@@ -492,16 +492,17 @@ struct sdl_batcher {
             // overflow is flagged in d_tokenize_errors); their ids go to the pool
             // long items: one wave each; 256 CUs x 9 resident (k_unigram_long<20>: 17 KB of LDS, 154 VGPRs)
             const int lane_blocks = (int)env_int("SDL_UNI_LONG_BLOCKS", 2304), huge_blocks = 8;
-            uni_counters.ensure(4);
+            uni_counters.ensure(8);
             uni_err.ensure(1);
             uni_items.ensure((size_t)(N / 8 + n_chunks + 64));
+            uni_items2.ensure((size_t)(N / 64 + 64));
             uni_huge.ensure((size_t)(N / 256 + 64));
             uni_pool.ensure((size_t)N + 1024 * 1024);
             uni_scratch.ensure(unigram_scratch_bytes(lane_blocks, huge_blocks));
             chunk_ent.ensure((size_t)n_chunks + 1);
             UniWork W{uni_counters.p, uni_items.p, (uint32_t)std::min<size_t>(uni_items.cap, 0xFFFFFFFFu), uni_pool.p,
                       (uint32_t)std::min<size_t>(uni_pool.cap, 0x3FFFFFFF), uni_huge.p, (uint32_t)uni_huge.cap,
-                      uni_scratch.p, lane_blocks, huge_blocks, uni_err.p};
+                      uni_items2.p, (uint32_t)uni_items2.cap, uni_scratch.p, lane_blocks, huge_blocks, uni_err.p};
             HIP_TRY(launch_unigram_chunks(dt, d_text, N, d_off, R, ranges.p, tokc.p, chunk_cnt.p, chunk_ent.p,
                                           rec_local.p, W, st));
             downstream(0, st);

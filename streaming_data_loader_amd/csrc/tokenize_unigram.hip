@@ -1213,25 +1213,27 @@ __device__ Scratch make_scratch(uint8_t *mine, int cap) {
 // starts from LDS, then backtracks.  Items past LONG_NORM normalized bytes go
 // to the huge list.  KMAX bounds a row's candidate ends (max(Mm + 1, Mf));
 // the LDS footprint (~20 KB at KMAX 32) sets how many items a CU keeps in flight.
-constexpr int LONG_NORM = 512;
+constexpr int LONG_NORM = 512;  // stage 2; stage 1 takes items of <= LONG_NORM1 normalized bytes
+constexpr int LONG_NORM1 = 128;
 #ifndef SDL_LONG_UNROLL
 #define SDL_LONG_UNROLL 2
 #endif
 constexpr int LONG_UNROLL = SDL_LONG_UNROLL;  // candidate probes in flight per lane (k_unigram_long)
 constexpr int LONG_RAW = 1024;
 
-template <int KMAX>
+template <int KMAX, int NORM>
 __global__ __launch_bounds__(64) void k_unigram_long(DevTok T, const uint8_t *__restrict__ text, int64_t N,
                                                      const uint64_t *__restrict__ off, int64_t R,
                                                      const uint32_t *__restrict__ ranges,
                                                      const uint4 *__restrict__ items, uint32_t item_cap,
-                                                     uint32_t *counters, uint32_t *tokc, uint32_t *chunk_cnt,
-                                                     uint32_t *rec_local, uint32_t *pool, uint32_t pool_cap,
-                                                     uint4 *huge, uint32_t huge_cap, uint32_t *err) {
-    __shared__ __attribute__((aligned(16))) uint8_t s_nb[LONG_NORM + 32];
-    __shared__ double s_sc[LONG_NORM + 8];
-    __shared__ uint32_t s_st[LONG_NORM + 8];  // node start | id << 16 (0xFFFF: unset)
-    __shared__ uint16_t s_ids[2 * LONG_NORM + 16];
+                                                     const uint32_t *n_in, uint32_t *counters, uint32_t *tokc,
+                                                     uint32_t *chunk_cnt, uint32_t *rec_local, uint32_t *pool,
+                                                     uint32_t pool_cap, uint4 *over, uint32_t over_cap,
+                                                     uint32_t *n_over, uint32_t *err) {
+    __shared__ __attribute__((aligned(16))) uint8_t s_nb[NORM + 32];
+    __shared__ double s_sc[NORM + 8];
+    __shared__ uint32_t s_st[NORM + 8];  // node start | id << 16 (0xFFFF: unset)
+    __shared__ uint16_t s_ids[2 * NORM + 16];
     __shared__ uint16_t s_cid[KMAX * 64];     // [k][lane]: id of row lane's k-th end
     __shared__ __attribute__((aligned(16))) float s_csc[KMAX * 64];
     // the item's raw bytes are staged where the candidate scores go later (the
@@ -1244,7 +1246,7 @@ __global__ __launch_bounds__(64) void k_unigram_long(DevTok T, const uint8_t *__
     lds_u8 *nb = (lds_u8 *)s_nb;
     const lds_u32 *w32 = (const lds_u32 *)s_nb;
     const int Mm = T.maxlen_meta, Mf = T.maxlen_first;
-    uint32_t n_items = counters[0];
+    uint32_t n_items = *n_in;
     if (n_items > item_cap) n_items = item_cap;
 #ifdef SDL_STAMPS
     unsigned long long lstamp_ = __builtin_amdgcn_s_memtime();
@@ -1282,7 +1284,7 @@ __global__ __launch_bounds__(64) void k_unigram_long(DevTok T, const uint8_t *__
         // a word of printable ASCII is its own normalization (host-checked
         // charsmap facts, as the chunk kernel's simple words): copied by the wave
         const int wl = (int)(end - p);
-        bool ascii = wl <= LONG_NORM && p - pa + wl <= LONG_RAW;
+        bool ascii = wl <= NORM && p - pa + wl <= LONG_RAW;
         if (ascii) {
             bool mine = true;
             for (int j = lane; j < wl; j += 64) mine = mine && (uint32_t)s_raw[p - pa + j] - 0x21u < 0x5Eu;
@@ -1301,7 +1303,7 @@ __global__ __launch_bounds__(64) void k_unigram_long(DevTok T, const uint8_t *__
             int nl = 0;
             const bool ok = normalize_span(T, byte, p, end, p > rs && byte(p - 1) == (uint32_t)' ',
                                            [&](uint32_t x) -> bool {
-                                               if (nl >= LONG_NORM) return false;
+                                               if (nl >= NORM) return false;
                                                nb[nl++] = (uint8_t)x;
                                                return true;
                                            });
@@ -1319,8 +1321,8 @@ __global__ __launch_bounds__(64) void k_unigram_long(DevTok T, const uint8_t *__
         LONG_STAMP(1);
         if (nl < 0) {
             if (lane == 0) {
-                const uint32_t h = atomicAdd(&counters[3], 1u);
-                if (h < huge_cap) huge[h] = it;
+                const uint32_t h = atomicAdd(n_over, 1u);  // normalized past NORM: the next stage
+                if (h < over_cap) over[h] = it;
                 else atomicOr(err, 8u);
             }
             __syncthreads();
@@ -1498,7 +1500,7 @@ __global__ __launch_bounds__(64) void k_unigram_long(DevTok T, const uint8_t *__
                 } nodes{s_st};
                 const int k0 = s_misc[5];
                 const int k = unigram_backtrack(n, cand, nodes, T.unk_id, [&](int x, int id) {
-                    if (k0 + x < 2 * LONG_NORM + 16) s_ids[k0 + x] = (uint16_t)id;
+                    if (k0 + x < 2 * NORM + 16) s_ids[k0 + x] = (uint16_t)id;
                 });
                 s_misc[5] = k0 + k;
             }
@@ -1507,7 +1509,7 @@ __global__ __launch_bounds__(64) void k_unigram_long(DevTok T, const uint8_t *__
         }
         if (lane == 0) {
             int k = s_misc[5];
-            if (k > 2 * LONG_NORM + 16) {
+            if (k > 2 * NORM + 16) {
                 atomicOr(err, 2u);
                 k = 0;
             }
@@ -1547,7 +1549,7 @@ hipError_t launch_unigram_chunks(const DevTok &T, const uint8_t *text, int64_t N
                                  uint32_t *rec_local, const UniWork &W, hipStream_t st) {
     const int64_t n_chunks = (N + CHUNK - 1) / CHUNK;
     if (n_chunks == 0) return hipSuccess;
-    hipError_t e = hipMemsetAsync(W.counters, 0, 4 * sizeof(uint32_t), st);  // items, -, pool, huge
+    hipError_t e = hipMemsetAsync(W.counters, 0, 8 * sizeof(uint32_t), st);  // items, -, pool, huge, items2
     if (e != hipSuccess) return e;
     e = hipMemsetAsync(W.err, 0, sizeof(uint32_t), st);
     if (e != hipSuccess) return e;
@@ -1555,19 +1557,25 @@ hipError_t launch_unigram_chunks(const DevTok &T, const uint8_t *text, int64_t N
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_unigram_chunks, dim3((unsigned)n_chunks), dim3(TOK_THREADS), 0, st, T, text, N, off, R, ranges,
                        tokc, chunk_cnt, chunk_ent, rec_local, W.counters, W.items, W.item_cap, W.err);
-    // a row's candidate ends: <= Mm + 1 ("▁" row) or <= Mf
-    if (T.maxlen_meta + 1 <= 20 && T.maxlen_first <= 20)  // smaller LDS: more items in flight
-        hipLaunchKernelGGL(k_unigram_long<20>, dim3((unsigned)W.lane_blocks), dim3(64), 0, st, T, text, N, off, R,
-                           ranges, W.items, W.item_cap, W.counters, tokc, chunk_cnt, rec_local, W.pool, W.pool_cap, W.huge,
-                           W.huge_cap, W.err);
-    else if (T.maxlen_meta + 1 <= 32 && T.maxlen_first <= 32)
-        hipLaunchKernelGGL(k_unigram_long<32>, dim3((unsigned)W.lane_blocks), dim3(64), 0, st, T, text, N, off, R,
-                           ranges, W.items, W.item_cap, W.counters, tokc, chunk_cnt, rec_local, W.pool, W.pool_cap, W.huge,
-                           W.huge_cap, W.err);
-    else
-        hipLaunchKernelGGL(k_unigram_long<64>, dim3((unsigned)W.lane_blocks), dim3(64), 0, st, T, text, N, off, R,
-                           ranges, W.items, W.item_cap, W.counters, tokc, chunk_cnt, rec_local, W.pool, W.pool_cap, W.huge,
-                           W.huge_cap, W.err);
+    // a row's candidate ends: <= Mm + 1 ("▁" row) or <= Mf.  Two stages: items of <= 128
+    // normalized bytes (nearly all) with a small LDS footprint and more of them in
+    // flight, then the rest (<= 512) from the first stage's overflow list.
+    const int g1 = W.lane_blocks * 4 / 3;
+#define SDL_UNI_LONG_STAGES(KM)                                                                                     \
+    hipLaunchKernelGGL((k_unigram_long<KM, LONG_NORM1>), dim3((unsigned)g1), dim3(64), 0, st, T, text, N, off, R,    \
+                       ranges, W.items, W.item_cap, W.counters, W.counters, tokc, chunk_cnt, rec_local, W.pool,      \
+                       W.pool_cap, W.items2, W.items2_cap, W.counters + 4, W.err);                                    \
+    hipLaunchKernelGGL((k_unigram_long<KM, LONG_NORM>), dim3((unsigned)W.lane_blocks), dim3(64), 0, st, T, text, N,  \
+                       off, R, ranges, W.items2, W.items2_cap, W.counters + 4, W.counters, tokc, chunk_cnt,           \
+                       rec_local, W.pool, W.pool_cap, W.huge, W.huge_cap, W.counters + 3, W.err);
+    if (T.maxlen_meta + 1 <= 20 && T.maxlen_first <= 20) {  // smaller LDS: more items in flight
+        SDL_UNI_LONG_STAGES(20)
+    } else if (T.maxlen_meta + 1 <= 32 && T.maxlen_first <= 32) {
+        SDL_UNI_LONG_STAGES(32)
+    } else {
+        SDL_UNI_LONG_STAGES(64)
+    }
+#undef SDL_UNI_LONG_STAGES
     hipLaunchKernelGGL(k_unigram_huge, dim3((unsigned)W.huge_blocks), dim3(64), 0, st, T, text, N, off, R, W.counters,
                        tokc, chunk_cnt, rec_local, W.scratch, W.pool, W.pool_cap, W.huge, W.huge_cap, W.err);
     return hipGetLastError();
