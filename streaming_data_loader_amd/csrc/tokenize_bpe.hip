@@ -320,6 +320,32 @@ __device__ int bpe_wave_seg(const DevTok &T, uint32_t &sym, int n, uint64_t &hea
 
 }  // namespace
 
+// Diagnostic build (-DSDL_STAMPS): lane 0 of every block adds the s_memtime
+// cycles between phase boundaries into sdl_bpe_cycles[]; never in the product.
+#ifdef SDL_STAMPS
+__device__ unsigned long long sdl_bpe_cycles[8];
+#define BPE_STAMP(k)                                                                  \
+    do {                                                                              \
+        if (threadIdx.x == 0) {                                                       \
+            const unsigned long long t_ = __builtin_amdgcn_s_memtime();              \
+            atomicAdd(&sdl_bpe_cycles[k], t_ - stamp_prev_);                          \
+            stamp_prev_ = t_;                                                         \
+        }                                                                             \
+    } while (0)
+void print_bpe_cycles() {
+    unsigned long long h[8];
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(sdl_bpe_cycles), sizeof(h)) != hipSuccess) return;
+    static const char *names[] = {"", "load+classify", "pre-token starts", "word-table probes", "wave BPE",
+                                  "compact", "-", "-"};
+    unsigned long long tot = 0;
+    for (int i = 1; i < 6; ++i) tot += h[i];
+    for (int i = 1; i < 6; ++i)
+        fprintf(stderr, "[bpe stamps] %-18s %6.2f%%\n", names[i], tot ? 100.0 * (double)h[i] / (double)tot : 0.0);
+}
+#else
+#define BPE_STAMP(k) do {} while (0)
+#endif
+
 // ---------------------------------------------------------------------------
 // Register budget for 5 waves/SIMD (the 7.9 KB of LDS per one-wave block admits 5).
 #ifndef SDL_BPE_WAVES
@@ -341,6 +367,9 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
     __shared__ uint32_t s_scratch[8];
 
     const int tid = threadIdx.x;
+#ifdef SDL_STAMPS
+    unsigned long long stamp_prev_ = __builtin_amdgcn_s_memtime();
+#endif
     const int lane = tid;
     const int64_t c0 = (int64_t)blockIdx.x * CHUNK;
     const int64_t c1 = c0 + CHUNK < N ? c0 + CHUNK : N;
@@ -386,32 +415,57 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
     __syncthreads();
 
     const Ctx C{&T, win, rbits, w0, text, N, off, R};
-    // rare bytes, block-parallel: lead bytes (decode: class, and the
-    // continuation bytes they cover), then added tokens (override)
-    for (int wi = tid; wi < WIN; wi += TOK_THREADS) {
-        const uint32_t b = win[wi];
-        const int64_t p = w0 + wi;
-        if (b < 0xC0u || p < 0 || p >= N) continue;
-        int len;
-        const uint32_t cp = decode(C, p, b, &len);
-        if (len == 1) continue;  // malformed: a one-byte O char
-        cls[wi] = (uint8_t)k_of_gc(gclass(T, cp));
-        for (int k = 1; k < len && wi + k < WIN; ++k) cls[wi + k] = K_CONT;
-    }
+    // rare bytes: each lane finds its own 16 bytes' (and halo bytes') lead bytes
+    // and added-token openers in registers and handles only those -- lead bytes
+    // (decode: class, and the continuation bytes they cover), then added tokens
+    // (override)
+    auto rare_masks = [&](const uint4 &x, uint32_t &leads, uint32_t &opens) {
+        const uint32_t wv[4] = {x.x, x.y, x.z, x.w};
+        leads = opens = 0u;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const uint32_t b = (wv[i >> 2] >> (8 * (i & 3))) & 0xFFu;
+            leads |= (b >= 0xC0u ? 1u : 0u) << i;
+            opens |= (b == T.opener ? 1u : 0u) << i;
+        }
+    };
+    uint32_t lead_m, open_m, hlead_m = 0, hopen_m = 0;
+    rare_masks(v, lead_m, open_m);
+    if (tid < (WIN - CHUNK) / 16) rare_masks(hv, hlead_m, hopen_m);
+    auto do_leads = [&](uint32_t m, int wi0) {
+        for (; m; m &= m - 1) {
+            const int wi = wi0 + __builtin_ctz(m);
+            const int64_t p = w0 + wi;
+            if (p < 0 || p >= N) continue;
+            int len;
+            const uint32_t cp = decode(C, p, win[wi], &len);
+            if (len == 1) continue;  // malformed: a one-byte O char
+            cls[wi] = (uint8_t)k_of_gc(gclass(T, cp));
+            for (int k = 1; k < len && wi + k < WIN; ++k) cls[wi + k] = K_CONT;
+        }
+    };
+    do_leads(lead_m, HALO_L + 16 * tid);
+    if (hlead_m) do_leads(hlead_m, (int)(hp - w0));
     __syncthreads();
     if (T.n_special) {
-        for (int wi = tid; wi < WIN; wi += TOK_THREADS) {
-            const int64_t p = w0 + wi;
-            if (win[wi] != T.opener || p < 0 || p >= N) continue;
-            const int m = special_match(C, p);
-            if (m < 0) continue;
-            const int l = T.special_len[m];
-            cls[wi] = K_SPEC;
-            for (int j = 1; j < l && wi + j < WIN; ++j) cls[wi + j] = K_SPX;
-        }
+        auto do_opens = [&](uint32_t m, int wi0) {
+            for (; m; m &= m - 1) {
+                const int wi = wi0 + __builtin_ctz(m);
+                const int64_t p = w0 + wi;
+                if (p < 0 || p >= N) continue;
+                const int mt = special_match(C, p);
+                if (mt < 0) continue;
+                const int l = T.special_len[mt];
+                cls[wi] = K_SPEC;
+                for (int j = 1; j < l && wi + j < WIN; ++j) cls[wi + j] = K_SPX;
+            }
+        };
+        do_opens(open_m, HALO_L + 16 * tid);
+        if (hopen_m) do_opens(hopen_m, (int)(hp - w0));
         __syncthreads();
     }
 
+    BPE_STAMP(1);
     // ---- 2. pre-token starts -------------------------------------------------
     const LdsAcc A{win, cls, rbits, w0, N};
     const int64_t s0 = c0 + 16 * tid;
@@ -445,6 +499,7 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
     const int e_last = (int)s_scratch[0];
     s_pieces[np] = (uint16_t)(e_last < 0 ? 0xFFFFu : (uint32_t)e_last);
 
+    BPE_STAMP(2);
     // ---- 3. word-table probe per piece ----------------------------------------
     lds_u16 *stage = (lds_u16 *)s_stage;
     lds_u8 *cnt = (lds_u8 *)s_cnt;
@@ -532,6 +587,7 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
     }
     __syncthreads();
 
+    BPE_STAMP(3);
     // ---- 4. wave BPE of the misses, packed: consecutive misses share the lanes --
     const int npend = (int)s_scratch[1];
     for (int q = 0; q < npend;) {
@@ -568,6 +624,7 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
         __syncthreads();
     }
 
+    BPE_STAMP(4);
     // ---- 5. compact ids into this chunk's tokc slice ------------------------------
     const int per = (np + TOK_THREADS - 1) / TOK_THREADS;
     const int a0 = tid * per < np ? tid * per : np;
@@ -619,6 +676,7 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
         base += s_cnt[i] == CNT_LONG ? 1u : s_cnt[i];
     }
     __syncthreads();
+    BPE_STAMP(5);
     if (tid == 0) chunk_cnt[blockIdx.x] = chunk_ent[blockIdx.x] = total;
     // record boundaries owned by this chunk: local entry offset of the first
     // piece at or after the boundary (k_bpe_long adds long pieces' extra ids)
