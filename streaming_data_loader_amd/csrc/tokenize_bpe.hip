@@ -470,9 +470,46 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
     const LdsAcc A{win, cls, rbits, w0, N};
     const int64_t s0 = c0 + 16 * tid;
     const int nown = s0 >= c1 ? 0 : (int)(c1 - s0 < 16 ? c1 - s0 : 16);
-    uint32_t pmask = 0;
-    for (int i = 0; i < nown; ++i)
-        if (is_start(A, HALO_L + 16 * tid + i)) pmask |= 1u << i;
+    // the rules over the lane's class bytes in registers; bytes whose rule looks
+    // further (apostrophes, a multi-byte previous char, whitespace before a
+    // continuation byte) take is_start
+    const int wi0 = HALO_L + 16 * tid;
+    const uint4 kc = *reinterpret_cast<const uint4 *>(s_cls + wi0);
+    const uint32_t kw[6] = {*reinterpret_cast<const uint32_t *>(s_cls + wi0 - 4), kc.x, kc.y, kc.z, kc.w,
+                            *reinterpret_cast<const uint32_t *>(s_cls + wi0 + 16)};
+    const uint64_t rb = ((uint64_t)s_rbits[(wi0 >> 5) + 1] << 32 | s_rbits[wi0 >> 5]) >> (wi0 & 31);
+    auto K = [&](int j) -> uint32_t { return (kw[(j + 4) >> 2] >> (8 * ((j + 4) & 3))) & 0xFFu; };
+    uint32_t fmask = 0, cmask = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const uint32_t c = K(i), p = K(i - 1), n = K(i + 1);
+        const bool rsq = (rb >> i) & 1u, rsn = (rb >> (i + 1)) & 1u;
+        const bool pastn = s0 + i + 1 >= N;
+        bool st = false, cx = false;
+        if (c == K_CONT || c == K_SPX) st = false;
+        else if (c == K_SPEC) st = true;
+        else if (rsq || p == K_SPEC || p == K_SPX) st = true;
+        else if (p == K_CONT || p == K_AP || c == K_AP) cx = true;
+        else if (is_w((int)c)) {
+            if (!is_w((int)p)) st = true;
+            else if (pastn || rsn || n == K_SPEC) st = false;
+            else if (n == K_CONT) cx = true;
+            else st = !is_w((int)n);
+        } else if (p == K_SP) st = false;
+        else if (p == K_W) st = true;
+        else if (c == K_O) st = p != K_O;
+        else if (c == K_N) st = p != K_N;
+        else if (p != K_L) st = true;  // K_L
+        else cx = K(i - 2) == K_AP || K(i - 3) == K_AP;
+        fmask |= (st ? 1u : 0u) << i;
+        cmask |= (cx ? 1u : 0u) << i;
+    }
+    const uint32_t own = nown >= 16 ? 0xFFFFu : (1u << nown) - 1u;
+    uint32_t pmask = fmask & own;
+    for (uint32_t m = cmask & own; m; m &= m - 1) {
+        const int i = __builtin_ctz(m);
+        if (is_start(A, wi0 + i)) pmask |= 1u << i;
+    }
     uint32_t np_total;
     uint32_t pbase = block_excl_sum<TOK_THREADS>((uint32_t)__builtin_popcount(pmask), &np_total, s_scratch + 2);
     for (uint32_t m = pmask; m;) {
