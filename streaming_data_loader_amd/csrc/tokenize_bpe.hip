@@ -39,7 +39,8 @@ namespace sdl {
 namespace {
 
 // per-byte class in LDS
-enum : uint8_t { K_CONT = 0, K_L = 1, K_N = 2, K_W = 3, K_O = 4, K_SP = 5, K_AP = 6, K_SPEC = 7, K_SPX = 8 };
+// (one bit per class, continuation bytes 0: the start rules run byte-parallel)
+enum : uint8_t { K_CONT = 0, K_L = 1, K_N = 2, K_W = 4, K_SP = 8, K_AP = 0x10, K_O = 0x20, K_SPEC = 0x40, K_SPX = 0x80 };
 constexpr int K_BND = 15;  // "no char" (record start / added-token edge / text end)
 constexpr int BPE_MAX_WAVE = 64;  // pieces up to this many bytes are merged in the chunk kernel
 constexpr uint8_t CNT_LONG = 0xFF;  // s_cnt of a long piece (k_bpe_long)
@@ -478,31 +479,42 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
     const uint32_t kw[6] = {*reinterpret_cast<const uint32_t *>(s_cls + wi0 - 4), kc.x, kc.y, kc.z, kc.w,
                             *reinterpret_cast<const uint32_t *>(s_cls + wi0 + 16)};
     const uint64_t rb = ((uint64_t)s_rbits[(wi0 >> 5) + 1] << 32 | s_rbits[wi0 >> 5]) >> (wi0 & 31);
-    auto K = [&](int j) -> uint32_t { return (kw[(j + 4) >> 2] >> (8 * ((j + 4) & 3))) & 0xFFu; };
+    // byte-parallel over 4 bytes per dword, each predicate in bit 7 of its byte
+    constexpr uint32_t H = 0x80808080u;
+    auto nzb = [](uint32_t x) { return (((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u; };
+    auto bit7 = [](uint32_t x, int k) { return (x << (7 - k)) & 0x80808080u; };
+    auto fullb = [](uint32_t m) { return (m >> 7) * 0xFFu; };
+    auto expand4 = [](uint32_t b4) { return ((b4 * 0x00204081u) & 0x01010101u) << 7; };
+    auto gather4 = [](uint32_t m) { return (((m >> 7) * 0x00204081u) >> 21) & 0xFu; };
+    const int64_t lim64 = N - s0 - 1;  // bytes i >= lim: the next byte is past the text
+    const int lim = lim64 < 0 ? 0 : lim64 > 16 ? 16 : (int)lim64;
+    const uint32_t rsq_bits = (uint32_t)rb & 0xFFFFu;
+    const uint32_t bndn_bits = ((uint32_t)(rb >> 1) | (0xFFFFu << lim)) & 0xFFFFu;
     uint32_t fmask = 0, cmask = 0;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        const uint32_t c = K(i), p = K(i - 1), n = K(i + 1);
-        const bool rsq = (rb >> i) & 1u, rsn = (rb >> (i + 1)) & 1u;
-        const bool pastn = s0 + i + 1 >= N;
-        bool st = false, cx = false;
-        if (c == K_CONT || c == K_SPX) st = false;
-        else if (c == K_SPEC) st = true;
-        else if (rsq || p == K_SPEC || p == K_SPX) st = true;
-        else if (p == K_CONT || p == K_AP || c == K_AP) cx = true;
-        else if (is_w((int)c)) {
-            if (!is_w((int)p)) st = true;
-            else if (pastn || rsn || n == K_SPEC) st = false;
-            else if (n == K_CONT) cx = true;
-            else st = !is_w((int)n);
-        } else if (p == K_SP) st = false;
-        else if (p == K_W) st = true;
-        else if (c == K_O) st = p != K_O;
-        else if (c == K_N) st = p != K_N;
-        else if (p != K_L) st = true;  // K_L
-        else cx = K(i - 2) == K_AP || K(i - 3) == K_AP;
-        fmask |= (st ? 1u : 0u) << i;
-        cmask |= (cx ? 1u : 0u) << i;
+    for (int j = 1; j <= 4; ++j) {
+        const uint32_t c = kw[j], lo = kw[j - 1];
+        const uint32_t p = __builtin_amdgcn_alignbyte(c, lo, 3), p2 = __builtin_amdgcn_alignbyte(c, lo, 2),
+                       p3 = __builtin_amdgcn_alignbyte(c, lo, 1);
+        const uint32_t n = __builtin_amdgcn_alignbyte(kw[j + 1], c, 1);
+        // class of the previous char (a continuation byte's lead is <= 3 bytes back)
+        const uint32_t pe = p | (~fullb(nzb(p)) & (p2 | (~fullb(nzb(p2)) & (p3 | (~fullb(nzb(p3)) & lo)))));
+        const uint32_t rsq = expand4((rsq_bits >> (4 * (j - 1))) & 0xFu);
+        const uint32_t bndn = expand4((bndn_bits >> (4 * (j - 1))) & 0xFu) | bit7(n, 6);
+        const uint32_t dead = (~nzb(c) & H) | bit7(c, 7);  // CONT, SPX: never a start
+        const uint32_t spec = bit7(c, 6);
+        const uint32_t bnd = rsq | nzb(pe & 0xC0C0C0C0u);  // pc is BND
+        const uint32_t wc = nzb(c & 0x0C0C0C0Cu), wp = nzb(pe & 0x0C0C0C0Cu), wn = nzb(n & 0x0C0C0C0Cu);
+        const uint32_t contn = ~nzb(n) & H;
+        const uint32_t lc = bit7(c, 0), app = bit7(pe, 4);
+        // left to is_start: L after an apostrophe or after L after one, whitespace
+        // run before a multi-byte char
+        const uint32_t cx = (lc & app) | (lc & bit7(pe, 0) & bit7(p2 | p3, 4)) | (wc & wp & contn);
+        const uint32_t st = (wc & (~wp | (~bndn & ~wn & ~contn))) | (bit7(c, 4) & nzb(pe & 0x07070707u)) |
+                            (nzb(c & ~pe & 0x23232323u) & ~bit7(pe, 3) & ~(app & bit7(c, 5)));
+        const uint32_t live = ~dead & ~spec & ~bnd & H;
+        fmask |= gather4(spec | (~dead & bnd & H) | (st & live & ~cx)) << (4 * (j - 1));
+        cmask |= gather4(cx & live) << (4 * (j - 1));
     }
     const uint32_t own = nown >= 16 ? 0xFFFFu : (1u << nown) - 1u;
     uint32_t pmask = fmask & own;
