@@ -55,6 +55,28 @@ __device__ __forceinline__ uint32_t ascii_k(uint32_t b) {
     return K_O;
 }
 
+// ---- byte-parallel helpers: 4 bytes per dword, predicates in bit 7 of each byte
+constexpr uint32_t B7 = 0x80808080u;
+__device__ __forceinline__ uint32_t nzb(uint32_t x) { return (((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & B7; }
+__device__ __forceinline__ uint32_t bit7(uint32_t x, int k) { return (x << (7 - k)) & B7; }
+__device__ __forceinline__ uint32_t fullb(uint32_t m) { return (m >> 7) * 0xFFu; }
+__device__ __forceinline__ uint32_t expand4(uint32_t b4) { return ((b4 * 0x00204081u) & 0x01010101u) << 7; }
+__device__ __forceinline__ uint32_t gather4(uint32_t m) { return ((((m >> 7) & 0x01010101u) * 0x00204081u) >> 21) & 0xFu; }
+__device__ __forceinline__ uint32_t gather16(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+    return gather4(a) | gather4(b) << 4 | gather4(c) << 8 | gather4(d) << 12;
+}
+// bytes y < 0x80: y >= lo, lo <= y <= hi
+__device__ __forceinline__ uint32_t ge7(uint32_t y, uint32_t lo) { return (y + (0x80u - lo) * 0x01010101u) & B7; }
+__device__ __forceinline__ uint32_t in7(uint32_t y, uint32_t lo, uint32_t hi) { return ge7(y, lo) & ~ge7(y, hi + 1); }
+// ascii_k of 4 bytes (bytes >= 0x80: K_O)
+__device__ __forceinline__ uint32_t ascii_k4(uint32_t x) {
+    const uint32_t lo7 = ~(x & B7), a = x & 0x7F7F7F7Fu;
+    const uint32_t l = in7(a | 0x20202020u, 'a', 'z') & lo7, n = in7(a, '0', '9') & lo7, w = in7(a, 9, 13) & lo7,
+                   sp = in7(a, ' ', ' ') & lo7, ap = in7(a, '\'', '\'') & lo7;
+    const uint32_t o = B7 & ~(l | n | w | sp | ap);
+    return (l >> 7) | (n >> 6) | (w >> 5) | (sp >> 4) | (ap >> 3) | (o >> 2);
+}
+
 __device__ __forceinline__ uint32_t gclass(const DevTok &T, uint32_t cp) {
     if (cp >= 0x110000u) return GC_O;
     return (T.gblock[(uint32_t)T.gpage[cp >> 8] * 64u + ((cp & 255u) >> 2)] >> (2 * (cp & 3u))) & 3u;
@@ -400,16 +422,8 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
     }
     // ASCII classes (bytes >= 0x80 provisionally O; text past N is O too)
     auto classify16 = [&](const uint4 &x, int wi0, int64_t p0) {
-        const uint32_t wv[4] = {x.x, x.y, x.z, x.w};
-        uint32_t o[4] = {0, 0, 0, 0};
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const uint32_t b = (wv[i >> 2] >> (8 * (i & 3))) & 0xFFu;
-            const uint32_t k = b < 0x80u ? ascii_k(b) : (uint32_t)K_O;
-            o[i >> 2] |= k << (8 * (i & 3));
-        }
         (void)p0;
-        *reinterpret_cast<uint4 *>(s_cls + wi0) = make_uint4(o[0], o[1], o[2], o[3]);
+        *reinterpret_cast<uint4 *>(s_cls + wi0) = make_uint4(ascii_k4(x.x), ascii_k4(x.y), ascii_k4(x.z), ascii_k4(x.w));
     };
     classify16(v, HALO_L + 16 * tid, c0 + 16 * tid);
     if (tid < (WIN - CHUNK) / 16) classify16(hv, (int)(hp - w0), hp);
@@ -421,14 +435,9 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
     // (decode: class, and the continuation bytes they cover), then added tokens
     // (override)
     auto rare_masks = [&](const uint4 &x, uint32_t &leads, uint32_t &opens) {
-        const uint32_t wv[4] = {x.x, x.y, x.z, x.w};
-        leads = opens = 0u;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const uint32_t b = (wv[i >> 2] >> (8 * (i & 3))) & 0xFFu;
-            leads |= (b >= 0xC0u ? 1u : 0u) << i;
-            opens |= (b == T.opener ? 1u : 0u) << i;
-        }
+        leads = gather16(x.x & (x.x << 1), x.y & (x.y << 1), x.z & (x.z << 1), x.w & (x.w << 1));  // >= 0xC0
+        const uint32_t o4 = T.opener * 0x01010101u;
+        opens = gather16(~nzb(x.x ^ o4), ~nzb(x.y ^ o4), ~nzb(x.z ^ o4), ~nzb(x.w ^ o4));
     };
     uint32_t lead_m, open_m, hlead_m = 0, hopen_m = 0;
     rare_masks(v, lead_m, open_m);
@@ -480,12 +489,7 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
                             *reinterpret_cast<const uint32_t *>(s_cls + wi0 + 16)};
     const uint64_t rb = ((uint64_t)s_rbits[(wi0 >> 5) + 1] << 32 | s_rbits[wi0 >> 5]) >> (wi0 & 31);
     // byte-parallel over 4 bytes per dword, each predicate in bit 7 of its byte
-    constexpr uint32_t H = 0x80808080u;
-    auto nzb = [](uint32_t x) { return (((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u; };
-    auto bit7 = [](uint32_t x, int k) { return (x << (7 - k)) & 0x80808080u; };
-    auto fullb = [](uint32_t m) { return (m >> 7) * 0xFFu; };
-    auto expand4 = [](uint32_t b4) { return ((b4 * 0x00204081u) & 0x01010101u) << 7; };
-    auto gather4 = [](uint32_t m) { return (((m >> 7) * 0x00204081u) >> 21) & 0xFu; };
+    constexpr uint32_t H = B7;
     const int64_t lim64 = N - s0 - 1;  // bytes i >= lim: the next byte is past the text
     const int lim = lim64 < 0 ? 0 : lim64 > 16 ? 16 : (int)lim64;
     const uint32_t rsq_bits = (uint32_t)rb & 0xFFFFu;
