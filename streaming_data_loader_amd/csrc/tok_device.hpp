@@ -100,6 +100,33 @@ __device__ __forceinline__ uint32_t msb4(uint32_t m) {
     return ((m >> 7) & 1u) | ((m >> 14) & 2u) | ((m >> 21) & 4u) | ((m >> 28) & 8u);
 }
 
+// ---- byte-parallel helpers: 4 bytes per dword, predicates in bit 7 of each byte
+constexpr uint32_t B7 = 0x80808080u;
+__device__ __forceinline__ uint32_t nzb(uint32_t x) { return (((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & B7; }
+__device__ __forceinline__ uint32_t bit7(uint32_t x, int k) { return (x << (7 - k)) & B7; }
+__device__ __forceinline__ uint32_t fullb(uint32_t m) { return (m >> 7) * 0xFFu; }
+__device__ __forceinline__ uint32_t expand4(uint32_t b4) { return ((b4 * 0x00204081u) & 0x01010101u) << 7; }
+__device__ __forceinline__ uint32_t gather4(uint32_t m) { return ((((m >> 7) & 0x01010101u) * 0x00204081u) >> 21) & 0xFu; }
+__device__ __forceinline__ uint32_t gather16(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+    return gather4(a) | gather4(b) << 4 | gather4(c) << 8 | gather4(d) << 12;
+}
+// bytes y < 0x80: y >= lo, lo <= y <= hi
+__device__ __forceinline__ uint32_t ge7(uint32_t y, uint32_t lo) { return (y + (0x80u - lo) * 0x01010101u) & B7; }
+__device__ __forceinline__ uint32_t in7(uint32_t y, uint32_t lo, uint32_t hi) { return ge7(y, lo) & ~ge7(y, hi + 1); }
+// 4 bytes of values < 16 -> 4 nibbles (byte k -> bits 4k..4k+3)
+__device__ __forceinline__ uint32_t nibpack4(uint32_t x) {
+    const uint32_t z = x | (x >> 4);
+    return (z & 0xFFu) | ((z >> 8) & 0xFF00u);
+}
+// 16-bit mask -> bit 4i per bit i
+__device__ __forceinline__ uint64_t nib_spread(uint32_t m16) {
+    uint64_t x = m16;
+    x = (x | (x << 24)) & 0x000000FF000000FFull;
+    x = (x | (x << 12)) & 0x000F000F000F000Full;
+    x = (x | (x << 6)) & 0x0303030303030303ull;
+    return (x | (x << 3)) & 0x1111111111111111ull;
+}
+
 // Strict UTF-8 decode of the char at lead byte b = byte(p); must not cross a
 // record start.  Invalid -> U+FFFD (class DEL), 1 byte.
 __device__ __forceinline__ uint32_t decode(const Ctx &C, int64_t p, uint32_t b, int *len) {

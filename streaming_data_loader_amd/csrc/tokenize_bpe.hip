@@ -55,19 +55,6 @@ __device__ __forceinline__ uint32_t ascii_k(uint32_t b) {
     return K_O;
 }
 
-// ---- byte-parallel helpers: 4 bytes per dword, predicates in bit 7 of each byte
-constexpr uint32_t B7 = 0x80808080u;
-__device__ __forceinline__ uint32_t nzb(uint32_t x) { return (((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & B7; }
-__device__ __forceinline__ uint32_t bit7(uint32_t x, int k) { return (x << (7 - k)) & B7; }
-__device__ __forceinline__ uint32_t fullb(uint32_t m) { return (m >> 7) * 0xFFu; }
-__device__ __forceinline__ uint32_t expand4(uint32_t b4) { return ((b4 * 0x00204081u) & 0x01010101u) << 7; }
-__device__ __forceinline__ uint32_t gather4(uint32_t m) { return ((((m >> 7) & 0x01010101u) * 0x00204081u) >> 21) & 0xFu; }
-__device__ __forceinline__ uint32_t gather16(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
-    return gather4(a) | gather4(b) << 4 | gather4(c) << 8 | gather4(d) << 12;
-}
-// bytes y < 0x80: y >= lo, lo <= y <= hi
-__device__ __forceinline__ uint32_t ge7(uint32_t y, uint32_t lo) { return (y + (0x80u - lo) * 0x01010101u) & B7; }
-__device__ __forceinline__ uint32_t in7(uint32_t y, uint32_t lo, uint32_t hi) { return ge7(y, lo) & ~ge7(y, hi + 1); }
 // ascii_k of 4 bytes (bytes >= 0x80: K_O)
 __device__ __forceinline__ uint32_t ascii_k4(uint32_t x) {
     const uint32_t lo7 = ~(x & B7), a = x & 0x7F7F7F7Fu;

@@ -48,6 +48,16 @@ __device__ __forceinline__ uint32_t ascii_vclass(uint32_t b) {
     return V_ISO;
 }
 
+// ascii_vclass of 4 bytes as 4 nibbles (bytes >= 0x80: V_NONE)
+__device__ __forceinline__ uint32_t vclass4(uint32_t x) {
+    const uint32_t lo7 = ~x & B7, a = x & 0x7F7F7F7Fu;
+    const uint32_t an = swar_alnum(x);
+    const uint32_t ws = (in7(a, 9, 10) | in7(a, 13, 13) | in7(a, ' ', ' ')) & lo7;
+    const uint32_t ctl = ~ge7(a, 32) | ge7(a, 127);  // includes \t \n \r (ws wins)
+    const uint32_t iso = lo7 & ~an & ~ws & ~ctl;
+    return nibpack4(((an | ws) >> 7) | ((an | iso) >> 6));  // OTHER 3, WS 1, ISO 2, NONE 0
+}
+
 // Device Unicode entry (assets.cpp: device_entry): bits 0-1 class, bit 2
 // identity, bit 3 inline (bits 4-5 nbytes-1, 6-7 nchars-1, 8-31 the bytes),
 // else bits 8-31 = pool offset.  One load for the BMP, two beyond it.
@@ -472,17 +482,20 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
     const uint32_t rmask = (rbits[rel0 >> 5] >> (rel0 & 31)) & 0xFFFFu;
     const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
     uint64_t cls = 0;
-    uint32_t leads = 0;
+    uint32_t leads = 0, opens = 0;
+    const uint32_t o4 = T.opener * 0x01010101u;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        const uint32_t b = (wv[i >> 2] >> (8 * (i & 3))) & 0xFFu;
-        const uint32_t c = b < 0x80u ? ascii_vclass(b) : V_NONE;
-        cls |= (uint64_t)c << (4 * i);
-        leads |= (b >= 0xC0u ? 1u : 0u) << i;
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t x = wv[j];
+        cls |= (uint64_t)vclass4(x) << (16 * j);
+        leads |= gather4(x & (x << 1)) << (4 * j);  // >= 0xC0
+        opens |= gather4(~nzb(x ^ o4)) << (4 * j);
     }
+    if (!T.n_special) opens = 0;
     if (nown < 16) {
         cls &= nown ? ((1ull << (4 * nown)) - 1ull) : 0ull;
         leads &= (1u << nown) - 1u;
+        opens &= (1u << nown) - 1u;
     }
     uint8_t *s_ovr = s_cnt;
     *reinterpret_cast<uint4 *>(s_ovr + 16 * tid) = make_uint4(~0u, ~0u, ~0u, ~0u);
@@ -492,15 +505,6 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
     //   (a) non-ASCII lead bytes: decode + two-level Unicode table;
     //   (b) added tokens: every opener byte that starts a match marks its bytes
     //       (SPEC at the start, invisible after); applied after (a).
-    uint32_t opens = 0;
-    if (T.n_special) {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const uint32_t b = (wv[i >> 2] >> (8 * (i & 3))) & 0xFFu;
-            opens |= (b == T.opener ? 1u : 0u) << i;
-        }
-        opens &= nown == 16 ? 0xFFFFu : ((1u << nown) - 1u);
-    }
     // tid 0 also owns openers in [c0 - max_special_len + 1, c0): a token starting
     // there may cover this chunk's first bytes
     uint32_t opens_left = 0;
@@ -579,32 +583,31 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
     {
         const uint4 o = *reinterpret_cast<const uint4 *>(s_ovr + 16 * tid);
         const uint32_t ov[4] = {o.x, o.y, o.z, o.w};
+        uint64_t onib = 0, keep = 0;  // override classes, nibbles without one (0xFF)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const uint32_t c = (ov[i >> 2] >> (8 * (i & 3))) & 0xFFu;
-            if (c != 0xFFu) cls = (cls & ~(0xFull << (4 * i))) | ((uint64_t)c << (4 * i));
+        for (int j = 0; j < 4; ++j) {
+            onib |= (uint64_t)nibpack4(ov[j] & 0x0F0F0F0Fu) << (16 * j);
+            keep |= (uint64_t)nibpack4(fullb(ov[j] & B7) & 0x0F0F0F0Fu) << (16 * j);
         }
+        cls = (cls & keep) | (onib & ~keep);
     }
-    // Fast case (nearly every lane): 16 owned bytes, all visible, no record start.
-    // Then the carry summary is the last char's class and the piece starts are
-    // nibble-parallel: start_i = SPEC/ISO, or OTHER after a non-OTHER char.
+    // Each byte's previous visible class, byte-parallel: a record start at byte
+    // i + 1 puts a stopper (8) at byte i, then the visible classes and stoppers
+    // fill forward over the invisible bytes in four doubling steps.
     constexpr uint64_t NIB1 = 0x1111111111111111ull;
     auto nib_zero = [](uint64_t x) -> uint64_t {  // 1 at the base bit of every zero nibble
         return ~(x | (x >> 1) | (x >> 2) | (x >> 3)) & NIB1;
     };
-    const bool fast_lane = rmask == 0u && nown == 16 && nib_zero(cls) == 0ull;
-    // lane summary for the carry scan: 0 = pass-through, 0x100 | v = state after
-    uint32_t summ = 0;
-    if (fast_lane) {
-        summ = 0x100u | (uint32_t)(cls >> 60);
-    } else {
+    const uint64_t stop = nib_spread(rmask >> 1);
+    uint64_t fill = (cls & ~((stop << 4) - stop)) | (stop << 3);
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            if ((rmask >> i) & 1u) summ = 0x100u | V_NONE;
-            const uint32_t c = (uint32_t)(cls >> (4 * i)) & 0xFu;
-            if (c != V_NONE) summ = 0x100u | c;
-        }
+    for (int sh = 4; sh < 64; sh <<= 1) {
+        const uint64_t z = nib_zero(fill);
+        fill |= (fill << sh) & ((z << 4) - z);
     }
+    // lane summary for the carry scan: 0 = pass-through, 0x100 | v = state after
+    const uint32_t last = (uint32_t)(fill >> 60);
+    const uint32_t summ = (last != 0u || (rmask & 1u)) ? 0x100u | (last & 7u) : 0u;
     // state before the chunk: last visible char of the same record before c0
     if (tid == 0) {
         uint32_t st = V_NONE;
@@ -626,29 +629,19 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
     const uint32_t st_in = block_excl_last_scan<TOK_THREADS>(summ, s_scratch);
 
     // ---- 3. piece starts -------------------------------------------------------
-    uint32_t pmask = 0;
+    uint32_t pmask;
     {
-        uint32_t st = (st_in & 0x100u) ? (st_in & 0xFFu) : chunk_state;
-        if (fast_lane) {
-            const uint64_t is_o = nib_zero(cls ^ (NIB1 * V_OTHER));
-            const uint64_t is_si = nib_zero(cls ^ (NIB1 * V_ISO)) | nib_zero(cls ^ (NIB1 * V_SPEC));
-            const uint64_t prev_o = (is_o << 4) | (st == V_OTHER ? 1ull : 0ull);
-            uint64_t m = (is_si | (is_o & ~prev_o)) & NIB1;  // bit 4i: a piece starts at byte i
-            m = (m | (m >> 3)) & 0x0303030303030303ull;
-            m = (m | (m >> 6)) & 0x000F000F000F000Full;
-            m = (m | (m >> 12)) & 0x000000FF000000FFull;
-            pmask = (uint32_t)((m | (m >> 24)) & 0xFFFFull);
-        } else {
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                if ((rmask >> i) & 1u) st = V_NONE;
-                const uint32_t c = (uint32_t)(cls >> (4 * i)) & 0xFu;
-                if (c != V_NONE) {
-                    if (c == V_SPEC || c == V_ISO || (c == V_OTHER && st != V_OTHER)) pmask |= 1u << i;
-                    st = c;
-                }
-            }
-        }
+        const uint32_t st = (rmask & 1u) ? (uint32_t)V_NONE : (st_in & 0x100u) ? (st_in & 0xFFu) : chunk_state;
+        uint64_t pv = fill << 4;  // previous visible class (stopper 8: none)
+        const uint64_t z = nib_zero(pv);  // nothing visible before in the lane: the incoming state
+        pv = (pv | (((z << 4) - z) & (NIB1 * st))) & 0x7777777777777777ull;
+        const uint64_t is_o = nib_zero(cls ^ (NIB1 * V_OTHER));
+        const uint64_t is_si = nib_zero(cls ^ (NIB1 * V_ISO)) | nib_zero(cls ^ (NIB1 * V_SPEC));
+        uint64_t m = (is_si | (is_o & ~nib_zero(pv ^ (NIB1 * V_OTHER)))) & NIB1;  // bit 4i: a piece starts at byte i
+        m = (m | (m >> 3)) & 0x0303030303030303ull;
+        m = (m | (m >> 6)) & 0x000F000F000F000Full;
+        m = (m | (m >> 12)) & 0x000000FF000000FFull;
+        pmask = (uint32_t)((m | (m >> 24)) & 0xFFFFull);
     }
     uint32_t np_total;
     uint32_t pbase = block_excl_sum<TOK_THREADS>((uint32_t)__builtin_popcount(pmask), &np_total, s_scratch);
