@@ -171,14 +171,18 @@ __device__ __forceinline__ Probe probe_load(const DevTok &T, uint32_t h) {
     const uint4 *e2 = reinterpret_cast<const uint4 *>(T.slots + cuckoo_slot2(h, T.slot_mask));
     return Probe{e1[0], e1[1], e2[0], e2[1]};
 }
+// (one OR of differences and one compare: a chain of && costs a scalar mask op per term)
+__device__ __forceinline__ uint32_t slot_diff(const uint4 &a, const uint4 &b, uint32_t key, const W16 &c) {
+    return (a.x ^ key) | (b.x ^ c.x) | (b.y ^ c.y) | (b.z ^ c.z) | (b.w ^ c.w) | (a.y >> 31);
+}
 __device__ __forceinline__ bool slot_match(const uint4 &a, const uint4 &b, uint32_t key, const W16 &c) {
-    return (int32_t)a.y >= 0 && a.x == key && b.x == c.x && b.y == c.y && b.z == c.z && b.w == c.w;
+    return slot_diff(a, b, key, c) == 0u;
 }
 // id of the piece (payload <= 16 bytes in c, zero padded) or -1: exact
 __device__ __forceinline__ int probe_result(const Probe &P, uint32_t key, const W16 &c) {
-    if (slot_match(P.a1, P.b1, key, c)) return (int32_t)P.a1.y;
-    if (slot_match(P.a2, P.b2, key, c)) return (int32_t)P.a2.y;
-    return -1;
+    const uint32_t d1 = slot_diff(P.a1, P.b1, key, c), d2 = slot_diff(P.a2, P.b2, key, c);
+    const int r2 = d2 == 0u ? (int32_t)P.a2.y : -1;
+    return d1 == 0u ? (int32_t)P.a1.y : r2;
 }
 __device__ __forceinline__ uint32_t hash16(const W16 &c, uint32_t n, uint32_t cont) {
     uint32_t h = hinit(n, cont);

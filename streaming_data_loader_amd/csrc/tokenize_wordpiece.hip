@@ -707,10 +707,10 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
         } else {
             const uint32_t t =
                 Lw < 16 ? (((Lw < 4 ? raw.x : Lw < 8 ? raw.y : Lw < 12 ? raw.z : raw.w) >> (8 * (Lw & 3))) & 0xFFu) : b16;
-            const uint32_t tc = t < 0x80u ? ascii_vclass(t) : V_NONE;
+            const uint32_t tc = vclass4(t) & 0xFu;  // t >= 0x80: V_NONE
             const int te = prel + Lw;  // a non-ASCII WS/ISO char there ends the word too
-            fast = tc == V_WS || tc == V_ISO || c0 + prel + Lw >= N ||
-                   (t >= 0xC0u && te < CHUNK && ((s_nabits[te >> 5] >> (te & 31)) & 1u));
+            const uint32_t na = t >= 0xC0u && te < CHUNK ? (s_nabits[te >> 5] >> (te & 31)) & 1u : 0u;
+            fast = (((0x6u >> tc) & 1u) | na) != 0u || c0 + prel + Lw >= N;  // WS, ISO
         }
         lw = keep_bytes(W16{swar_lower(raw.x), swar_lower(raw.y), swar_lower(raw.z), swar_lower(raw.w)}, Lw);
         Lout = Lw;
