@@ -40,7 +40,8 @@ namespace sdl {
 
 namespace {
 
-enum : uint8_t { U_WS = 0, U_P = 1, U_X = 2, U_SPEC = 3, U_SPX = 4 };
+// (one bit per class: the starts and word ends are found byte-parallel)
+enum : uint8_t { U_WS = 1, U_P = 2, U_X = 4, U_SPEC = 8, U_SPX = 16 };
 constexpr uint32_t LMARK = 0x80000000u;
 // byte x (< 3) of "▁" (U+2581) -- arithmetic, not a global table: a load here
 // would make the DP wait for every probe in flight (vmcnt counts in order)
@@ -77,6 +78,13 @@ __device__ __forceinline__ uint32_t uni_ascii(uint32_t b) {
     if (b == 32u || b == 9u || b == 10u || b == 12u || b == 13u) return U_WS;
     if (b - 0x21u < 0x5Eu) return U_P;
     return U_X;
+}
+// uni_ascii of 4 bytes
+__device__ __forceinline__ uint32_t uni_ascii4(uint32_t x) {
+    const uint32_t lo7 = ~x & B7, a = x & 0x7F7F7F7Fu;
+    const uint32_t ws = (in7(a, 9, 10) | in7(a, 12, 13) | in7(a, 32, 32)) & lo7;
+    const uint32_t p = in7(a, 0x21, 0x7E) & lo7;
+    return (ws >> 7) | (p >> 6) | ((B7 & ~ws & ~p) >> 5);
 }
 __device__ __forceinline__ bool ascii_ws(uint32_t b) { return b == 32u || b == 9u || b == 10u || b == 12u || b == 13u; }
 
@@ -610,11 +618,7 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
         atomicOr(&s_rbits[rel >> 5], 1u << (rel & 31));
     }
     auto classify16 = [&](const uint4 &x, int wi0) {
-        const uint32_t wv[4] = {x.x, x.y, x.z, x.w};
-        uint32_t o[4] = {0, 0, 0, 0};
-#pragma unroll
-        for (int i = 0; i < 16; ++i) o[i >> 2] |= uni_ascii((wv[i >> 2] >> (8 * (i & 3))) & 0xFFu) << (8 * (i & 3));
-        *reinterpret_cast<uint4 *>(s_cls + wi0) = make_uint4(o[0], o[1], o[2], o[3]);
+        *reinterpret_cast<uint4 *>(s_cls + wi0) = make_uint4(uni_ascii4(x.x), uni_ascii4(x.y), uni_ascii4(x.z), uni_ascii4(x.w));
     };
     classify16(v, HALO_L + 16 * tid);
     if (tid < (WIN - CHUNK) / 16) classify16(hv, (int)(hp - w0));
@@ -625,15 +629,24 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
     auto cbnd = [&](int64_t q) -> bool { return C.rstart(q); };
     auto is_rs = [&](int wi) -> bool { return (rbits[wi >> 5] >> (wi & 31)) & 1u; };
     // added tokens (override the classes of their bytes)
-    if (T.n_special) {
-        for (int wi = tid; wi < WIN; wi += TOK_THREADS) {
-            const int64_t p = w0 + wi;
-            if (win[wi] != (uint8_t)'<' || p < 0 || p >= N) continue;
-            int l = 0;
-            if (uni_special(T, p, N, cbyte, cbnd, &l) < 0) continue;
-            cls[wi] = U_SPEC;
-            for (int j = 1; j < l && wi + j < WIN; ++j) cls[wi + j] = U_SPX;
-        }
+    if (T.n_special) {  // openers found in the lane's registers
+        auto opens16 = [](const uint4 &x) {
+            constexpr uint32_t o4 = (uint32_t)'<' * 0x01010101u;
+            return gather16(~nzb(x.x ^ o4), ~nzb(x.y ^ o4), ~nzb(x.z ^ o4), ~nzb(x.w ^ o4));
+        };
+        auto do_opens = [&](uint32_t m, int wi0) {
+            for (; m; m &= m - 1) {
+                const int wi = wi0 + __builtin_ctz(m);
+                const int64_t p = w0 + wi;
+                if (p < 0 || p >= N) continue;
+                int l = 0;
+                if (uni_special(T, p, N, cbyte, cbnd, &l) < 0) continue;
+                cls[wi] = U_SPEC;
+                for (int j = 1; j < l && wi + j < WIN; ++j) cls[wi + j] = U_SPX;
+            }
+        };
+        do_opens(opens16(v), HALO_L + 16 * tid);
+        if (tid < (WIN - CHUNK) / 16) do_opens(opens16(hv), (int)(hp - w0));
         __syncthreads();
     }
 
@@ -641,22 +654,32 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
     // ---- 2. piece starts: added tokens, and the first byte of every word ------
     const int64_t s0 = c0 + 16 * tid;
     const int nown = s0 >= c1 ? 0 : (int)(c1 - s0 < 16 ? c1 - s0 : 16);
-    uint32_t pmask = 0;
-    for (int i = 0; i < nown; ++i) {
-        const int wi = HALO_L + 16 * tid + i;
-        const uint32_t k = cls[wi];
-        if (k == U_SPEC) { pmask |= 1u << i; continue; }
-        if (k != U_P && k != U_X) continue;
-        const uint32_t pk = cls[wi - 1];
-        if (pk == U_WS || pk == U_SPX || pk == U_SPEC || is_rs(wi)) pmask |= 1u << i;
+    // a word starts at P/X after WS, an added token or a record start;
+    // byte-parallel over the lane's class bytes
+    uint32_t pmask, smask;
+    {
+        const int wi0 = HALO_L + 16 * tid;
+        const uint4 kc = *reinterpret_cast<const uint4 *>(s_cls + wi0);
+        const uint32_t kw[5] = {*reinterpret_cast<const uint32_t *>(s_cls + wi0 - 4), kc.x, kc.y, kc.z, kc.w};
+        const uint32_t rs16 = (uint32_t)((((uint64_t)s_rbits[(wi0 >> 5) + 1] << 32) | s_rbits[wi0 >> 5]) >> (wi0 & 31));
+        uint32_t st[4], sp[4];
+#pragma unroll
+        for (int j = 1; j <= 4; ++j) {
+            const uint32_t c = kw[j], pc = __builtin_amdgcn_alignbyte(kw[j], kw[j - 1], 3);
+            const uint32_t rsq = expand4((rs16 >> (4 * (j - 1))) & 0xFu);
+            sp[j - 1] = bit7(c, 3);  // U_SPEC
+            st[j - 1] = sp[j - 1] | (nzb(c & 0x06060606u) & (nzb(pc & 0x19191919u) | rsq));
+        }
+        const uint32_t own = nown >= 16 ? 0xFFFFu : (1u << nown) - 1u;
+        pmask = gather16(st[0], st[1], st[2], st[3]) & own;
+        smask = gather16(sp[0], sp[1], sp[2], sp[3]);
     }
     uint32_t np_total;
     uint32_t pbase = block_excl_sum<TOK_THREADS>((uint32_t)__builtin_popcount(pmask), &np_total, s_scratch + 8);
     for (uint32_t m = pmask; m;) {
         const int i = __builtin_ctz(m);
         m &= m - 1;
-        const int wi = HALO_L + 16 * tid + i;
-        s_pieces[pbase++] = (uint16_t)((16 * tid + i) | (cls[wi] == U_SPEC ? 1u << 12 : 0u));
+        s_pieces[pbase++] = (uint16_t)((16 * tid + i) | (((smask >> i) & 1u) << 12));
     }
     __syncthreads();
     const int np = (int)np_total;
@@ -685,12 +708,8 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
 #pragma unroll
         for (int k = 0; k < 5; ++k) {
             const uint32_t c = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
-#pragma unroll
-            for (int b = 0; b < 4; ++b) {
-                const uint32_t v = (c >> (8 * b)) & 0xFFu;
-                bnd |= (v == U_WS || v == U_SPEC ? 1u : 0u) << (4 * k + b);
-                nonp |= (v != U_P ? 1u : 0u) << (4 * k + b);
-            }
+            bnd |= gather4(nzb(c & 0x09090909u)) << (4 * k);  // U_WS, U_SPEC
+            nonp |= gather4(~bit7(c, 1)) << (4 * k);          // not U_P
         }
         const uint64_t rw = ((uint64_t)rbits[(wi0 >> 5) + 1] << 32) | rbits[wi0 >> 5];
         bnd |= (uint32_t)(rw >> (wi0 & 31));            // record starts
@@ -880,7 +899,18 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
     __syncthreads();
     UNI_STAMP(3);
     // ---- 4./5. batched Viterbi of the pending words, in rounds ------------------
-    const int nj = (int)(s_scratch[0] < (uint32_t)JOB_CAP ? s_scratch[0] : (uint32_t)JOB_CAP);
+    int nj = (int)(s_scratch[0] < (uint32_t)JOB_CAP ? s_scratch[0] : (uint32_t)JOB_CAP);
+#if defined(SDL_ABLATE_UNI)
+    // diagnostic: every Viterbi job yields one [UNK] (2: no candidate probes either)
+    for (int jb = lane; jb < nj; jb += 64) {
+        const int pi = s_job_pi[jb];
+        stage[s_pieces[pi] & 0xFFFu] = (uint16_t)T.unk_id;
+        cnt[pi] = 1;
+    }
+#if SDL_ABLATE_UNI == 2
+    nj = 0;
+#endif
+#endif
     uint32_t carry = 0, rcarry = 0;  // task and row bases per job (job order)
     for (int j0 = 0; j0 < nj; j0 += 64) {
         const int j = j0 + lane;
@@ -1046,7 +1076,11 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
             };
+#if defined(SDL_ABLATE_UNI)
+            for (int jb = j1; jb < j1; jb += 64 / DPG) {
+#else
             for (int jb = j0 + grp; jb < j1; jb += 64 / DPG) {
+#endif
                 const int pi = s_job_pi[jb];
                 const int prel = (int)(s_pieces[pi] & 0xFFFu);
                 int toff = (int)(s_job_tb[jb] - T0);

@@ -5,7 +5,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-O=gpurun_out/insts; mkdir -p $O
+O=gpurun_out/insts; rm -rf $O; mkdir -p $O
 i=0
 for lib in "$@"; do
   i=$((i+1))
