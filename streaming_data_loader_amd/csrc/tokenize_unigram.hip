@@ -1092,8 +1092,11 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
                     const int n = L + 3;  // "▁" + payload
                     auto acc = [&](int x) -> uint32_t { return x < 3 ? meta_byte(x) : (uint32_t)bytes[src + x - 3]; };
                     auto rowmask = [&](int st) -> uint32_t { return s_rowmask[roff + (st == 0 ? 0 : st - 2)]; };
+                    // (unreached nodes at -inf: every candidate beats them; a start
+                    // is always reached -- by its char's [UNK] at least -- before it
+                    // is visited)
                     for (int x = gl; x <= n; x += DPG) {
-                        gsc[x] = 0.0;
+                        gsc[x] = x == 0 ? 0.0 : -__builtin_inf();
                         gbp[x] = 0xFFFFFFFFu;
                     }
                     wave_sync();
@@ -1104,20 +1107,23 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
                         const int fe = st == 0 ? 3 : st + 1;
                         const uint32_t m = rowmask(st);
                         const bool single = (m >> (st + mb - fe)) & 1u;
-                        for (int k = gl; k < 32 && (m >> k); k += DPG) {
-                            if (!((m >> k) & 1u)) continue;
+                        // the start's candidates are consecutive tasks: candidate k
+                        // (ending at fe + k) is task rb + k
+                        const int rb = toff + (st == 0 ? 0 : vp_c0(L, Mm) + vp_rowoff(st - 3, L, Mf));
+                        int k = gl;
+                        for (uint32_t mm = m >> gl; mm; mm >>= DPG, k += DPG) {
+                            if (!(mm & 1u)) continue;
                             const int e = fe + k;
-                            const int loc = toff + vp_local(st == 0 ? -1 : st - 3, e - 3, L, Mm, Mf);
-                            const double c = (double)s_tsc[loc] + base;
-                            if (gbp[e] == 0xFFFFFFFFu || c > gsc[e]) {
+                            const double c = (double)s_tsc[rb + k] + base;
+                            if (c > gsc[e]) {
                                 gsc[e] = c;
-                                gbp[e] = (uint32_t)st | ((uint32_t)s_tid[loc] << 16);
+                                gbp[e] = (uint32_t)st | ((uint32_t)s_tid[rb + k] << 16);
                             }
                         }
                         if (!single && gl == DPG - 1) {  // unk: ends where no piece candidate does
                             const double c = T.unk_score + base;
                             const int e = st + mb;
-                            if (gbp[e] == 0xFFFFFFFFu || c > gsc[e]) {
+                            if (c > gsc[e]) {
                                 gsc[e] = c;
                                 gbp[e] = (uint32_t)st | ((uint32_t)T.unk_id << 16);
                             }
