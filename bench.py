@@ -211,6 +211,7 @@ def reference_engine_rate(task, records, order, seconds=6.0):
 
 PMC_DIR = os.path.join(REPO, "profiles", "pmc")
 VALU_ISSUE_PEAK = 256 * 4 * 2.4e9 / 2  # wave64 VALU instr/s: 256 CUs x 4 SIMD32, 2 cycles each, 2.4 GHz
+SALU_ISSUE_PEAK = 256 * 2.4e9  # scalar instr/s: one scalar unit per CU issuing one per cycle
 
 
 def pmc_path(task, arena_mib):
@@ -239,8 +240,10 @@ def load_pmc(task, arena_mib, kernel):
 
 def pmc_roofline(pmc, launch_ms, alg_bytes):
     """traffic = HBM bytes per launch (2 x FETCH_SIZE gfx950 correction +
-    WRITE_SIZE, MI355X_MICROARCH.md §HBM); issue = VALU wave-instructions per
-    launch over this run's HIP-event launch time against the issue peak.
+    WRITE_SIZE, MI355X_MICROARCH.md §HBM); issue = VALU and SALU wave-
+    instructions per launch over this run's HIP-event launch time against
+    their issue peaks (the byte-walking kernels are bound by the scalar unit:
+    one per CU, shared by its four SIMDs); `bound` names the busier one.
     A figure that cannot describe the timed launch (issue above its peak) is
     dropped with the reason."""
     traffic = pmc.get("hbm_bytes_per_launch")
@@ -248,15 +251,16 @@ def pmc_roofline(pmc, launch_ms, alg_bytes):
     valu, salu = c.get("SQ_INSTS_VALU"), c.get("SQ_INSTS_SALU")
     issue, note = None, None
     if valu:
-        rate = valu / (launch_ms * 1e-3)
-        frac = rate / VALU_ISSUE_PEAK
-        if frac > 1.0:
-            note = f"PMC VALU count over this launch time gives issue frac {frac:.3f} > 1: not this launch"
+        secs = launch_ms * 1e-3
+        vf, sf = valu / secs / VALU_ISSUE_PEAK, (salu or 0) / secs / SALU_ISSUE_PEAK
+        if max(vf, sf) > 1.0:
+            note = f"PMC instruction counts over this launch time give issue frac {max(vf, sf):.3f} > 1: not this launch"
         else:
-            issue = {"bound": "valu_issue", "valu_wave_instr_per_launch": int(valu),
-                     "salu_wave_instr_per_launch": int(salu or 0),
-                     "achieved_T_per_s": round(rate / 1e12, 4), "peak_T_per_s": round(VALU_ISSUE_PEAK / 1e12, 4),
-                     "frac": round(frac, 4),
+            issue = {"bound": "salu_issue" if sf > vf else "valu_issue", "frac": round(max(vf, sf), 4),
+                     "valu_wave_instr_per_launch": int(valu), "salu_wave_instr_per_launch": int(salu or 0),
+                     "valu_frac": round(vf, 4), "salu_frac": round(sf, 4),
+                     "peak_valu_T_per_s": round(VALU_ISSUE_PEAK / 1e12, 4),
+                     "peak_salu_T_per_s": round(SALU_ISSUE_PEAK / 1e12, 4),
                      "wait_frac": round(c["SQ_WAIT_ANY"] / c["SQ_WAVE_CYCLES"], 4) if c.get("SQ_WAVE_CYCLES") else None,
                      "source": pmc["_file"]}
     if traffic is not None and traffic < 0.9 * alg_bytes:
