@@ -27,6 +27,7 @@ communication.
 """
 import argparse
 import json
+import struct
 import os
 import sys
 import time
@@ -284,6 +285,8 @@ def parse_args(argv=None):
     ap.add_argument("--e2e", action="store_true", help="also time the host record path (H2D + kernels + D2H)")
     ap.add_argument("--json", action="store_true",
                     help="also time the provider's JsonText filter on the device (JSON lines -> text arena)")
+    ap.add_argument("--gz", action="store_true",
+                    help="also time the provider's gzip inflate on the device (BGZF members of the JSON lines)")
     ap.add_argument("--e2e-frames", action="store_true",
                     help="end to end from host JSON lines to host pickle frames: H2D, JsonText filter, "
                          "tokenize+mask, transport frames, D2H (the provider -> batcher -> transport path)")
@@ -539,6 +542,8 @@ def main(argv=None):
         line["end_to_end"] = end_to_end(args.task, records, order)
     if args.json and rank == 0:
         line["provider_json"] = provider_json(db, records, order, dev, args.steps, args.warmup, step_ms)
+    if args.gz and rank == 0:
+        line["provider_gzip"] = provider_gzip(db, records, order, dev, args.steps, args.warmup, step_ms)
     if args.frames and rank == 0:
         line["transport_frames"] = transport_frames(db, res, args.task, stream, dev, args.steps, args.warmup,
                                                     not args.no_cpu_baseline)
@@ -712,6 +717,91 @@ def provider_json(db, records, order, dev, steps, warmup, step_ms):
             "invalid_lines": int(out.n_invalid),
             "json_to_batches_MBps": round(len(buf) / (ms + step_ms) / 1e3, 2),
             "note": "host-timed (the call synchronises twice to size its outputs); JSON bytes / time"}
+
+
+def provider_gzip(db, records, order, dev, steps, warmup, step_ms, json_mib=64, block=65280):
+    """The provider's gzip inflate on the device (sdl_gzip_inflate_device): this
+    rank's record stream as JSON lines (as provider_json), gzip-compressed as
+    BGZF members of `block` input bytes (zlib level 6), already in HBM -> the
+    inflated JSON lines (CRC-32 and ISIZE checked) -> JsonText -> text arena.
+    CPU beside it: zlib inflate of the same lines as ONE gzip member on one
+    thread (what the reference's GzipDecoder does), and the BGZF members on 16
+    threads."""
+    import zlib
+    import torch
+    from concurrent.futures import ThreadPoolExecutor
+    from streaming_data_loader_amd import native
+    lines, size = [], 0
+    for i, k in enumerate(order):
+        ln = json.dumps({"id": i, "title": f"t{i}", "text": records[k]}).encode("utf-8") + b"\n"
+        lines.append(ln)
+        size += len(ln)
+        if size >= json_mib << 20:
+            break
+    buf = b"".join(lines)
+    t0 = time.perf_counter()
+    parts = [buf[i:i + block] for i in range(0, len(buf), block)]
+    with ThreadPoolExecutor(16) as ex:
+        def raw(p):
+            co = zlib.compressobj(6, zlib.DEFLATED, -15)
+            return co.compress(p) + co.flush()
+        comp = list(ex.map(raw, parts))
+    members = []
+    for p, c in zip(parts, comp):
+        hdr = b"\x1f\x8b\x08\x04\x00\x00\x00\x00\x00\xff\x06\x00BC\x02\x00"
+        m = hdr + b"\x00\x00" + c + struct.pack("<II", zlib.crc32(p), len(p))
+        members.append(m[:16] + struct.pack("<H", len(m) - 1) + m[18:])
+    gz = b"".join(members)
+    log(f"gzip: {len(buf) / 1e6:.1f} MB JSON -> {len(gz) / 1e6:.1f} MB in {len(members)} BGZF members "
+        f"({time.perf_counter() - t0:.1f} s to compress)")
+    off = native.gzip_split_members(gz)
+    assert len(off) == len(members) + 1
+    a = np.zeros(len(gz) + 32, np.uint8)
+    a[:len(gz)] = np.frombuffer(gz, np.uint8)
+    d_gz = torch.from_numpy(a).to(dev)
+    d_off = torch.from_numpy(off.view(np.int64)).to(dev)
+    n = len(members)
+
+    def inflate():
+        return db.gzip_inflate(d_gz.data_ptr(), len(gz), d_off.data_ptr(), n)
+    for _ in range(warmup):
+        out = inflate()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        out = inflate()
+    torch.cuda.synchronize(dev)
+    ms = (time.perf_counter() - t0) / steps * 1e3
+    assert int(out.out_bytes) == len(buf) and int(out.n_bad) == 0
+    chk = np.zeros(min(len(buf), 1 << 20), np.uint8)
+    native.d2h(db._h, chk, out.d_out, chk.nbytes)
+    assert chk.tobytes() == buf[:chk.size], "device inflate differs from the JSON lines"
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        out = inflate()
+        jt = db.json_text(out.d_out, int(out.out_bytes))
+    torch.cuda.synchronize(dev)
+    ms_text = (time.perf_counter() - t0) / steps * 1e3
+    # CPU: one member on one thread (the reference), BGZF members on 16 threads
+    co = zlib.compressobj(6, zlib.DEFLATED, 31)
+    single = co.compress(buf) + co.flush()
+    t0 = time.perf_counter()
+    assert len(zlib.decompress(single, 31)) == len(buf)
+    cpu1 = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(16) as ex:
+        got = sum(ex.map(lambda m: len(zlib.decompress(m, 31)), members))
+    cpu16 = time.perf_counter() - t0
+    assert got == len(buf)
+    return {"inflated_MBps": round(len(buf) / ms / 1e3, 2), "compressed_MBps": round(len(gz) / ms / 1e3, 2),
+            "ms": round(ms, 4), "json_bytes": len(buf), "gz_bytes": len(gz), "members": n,
+            "gz_to_text_ms": round(ms_text, 4), "gz_to_text_MBps": round(len(buf) / ms_text / 1e3, 2),
+            "records": int(jt.n_records),
+            "gz_to_batches_MBps": round(len(buf) / (ms_text + step_ms * len(buf) / (256 << 20)) / 1e3, 2),
+            "cpu_zlib_1thread_one_member_MBps": round(len(buf) / cpu1 / 1e6, 2),
+            "cpu_zlib_16threads_bgzf_MBps": round(len(buf) / cpu16 / 1e6, 2),
+            "note": "host-timed, includes the call's two synchronisations (trailer sizes, status); "
+                    "MB/s of inflated JSON unless named; gz_to_batches scales the 256 MiB step time to this text"}
 
 
 def end_to_end(task, records, order, nbytes=64 << 20, reps=2):

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define SDL_ABI_VERSION 6
+#define SDL_ABI_VERSION 7
 
 enum {
     SDL_OK = 0,
@@ -42,7 +42,8 @@ enum {
     SDL_ERR_UNSUPPORTED = -4, /* task / tokenizer feature not implemented */
     SDL_ERR_NODEV = -5,       /* no HIP device: the product never falls back to the CPU */
     SDL_ERR_STATE = -6,       /* call out of order */
-    SDL_ERR_CAPACITY = -7     /* input larger than one call supports (>= 4 GiB of text) */
+    SDL_ERR_CAPACITY = -7,    /* input larger than one call supports (>= 4 GiB of text) */
+    SDL_ERR_DATA = -8         /* corrupt input the reference's unwrap() panics on (gzip) */
 };
 
 /* TaskType -> DataSet selection (rust/src/config.rs:20-62). */
@@ -193,6 +194,40 @@ typedef struct sdl_json_text {
     uint64_t n_invalid;    /* lines the reference would panic on (skipped) */
 } sdl_json_text;
 int sdl_json_text_device(sdl_batcher *h, const uint8_t *d_jsonl, uint64_t len, void *stream, sdl_json_text *out);
+
+/* ---- Provider step: gzip inflate on the device -----------------------------
+ * Replaces the GzipDecoder under the provider's lines (gzip_file_provider.rs:
+ * 13-28, async-compression 0.3.14 / flate2 1.0.24 / miniz_oxide 0.5.4): every
+ * gzip member (RFC 1952; DEFLATE, RFC 1951) in `d_gz` is inflated by one wave,
+ * members in parallel, and its CRC-32 and ISIZE are checked.  Member m is bytes
+ * [d_member_offsets[m], d_member_offsets[m+1]) of d_gz (device, u64[n + 1]):
+ * one file each (the reference decodes a file's first member), or the BGZF
+ * blocks sdl_gzip_split_members finds in one file.  The outputs are written
+ * back to back -- the JSON lines sdl_json_text_device takes as is.  d_gz is
+ * device memory, 16-byte aligned, gz_len < 4 GiB, total output < 4 GiB.  A
+ * corrupt member (where the reference's `next_line().await.unwrap()` panics)
+ * makes the call return SDL_ERR_DATA with its index and reason; per-member
+ * status codes stay readable in d_status.  The buffers are owned by the handle
+ * until the next call; the call synchronises `stream` (the output size comes
+ * from the members' trailers before anything is decoded). */
+typedef struct sdl_inflated {
+    uint8_t *d_out;             /* device, 16-byte aligned, 32 zero bytes after out_bytes */
+    uint32_t *d_member_out;     /* device [n_members + 1]: member m's output is [d_member_out[m], [m+1]) */
+    int32_t *d_status;          /* device [n_members]: 0 ok, else a GZ_* reason code */
+    uint64_t out_bytes;
+    uint64_t n_members;
+    uint64_t n_bad;             /* members that failed */
+} sdl_inflated;
+int sdl_gzip_inflate_device(sdl_batcher *h, const uint8_t *d_gz, uint64_t gz_len, const uint64_t *d_member_offsets,
+                            uint64_t n_members, void *stream, sdl_inflated *out);
+
+/* Host only (no GPU): member byte ranges of one gzip file for
+ * sdl_gzip_inflate_device.  BGZF files (every member carries the 'BC' extra
+ * subfield with its size, as bgzip writes them) split into their members; any
+ * other file is one member (async-compression's GzipDecoder reads the first
+ * member of a file).  offsets gets *n_members + 1 entries (capacity `cap`
+ * entries; SDL_ERR_CAPACITY with *n_members set when too small). */
+int sdl_gzip_split_members(const uint8_t *gz, uint64_t len, uint64_t *offsets, uint64_t cap, uint64_t *n_members);
 
 /* ---- Transport step: batches as serde_pickle frames on the device ----------
  * Replaces serde_pickle::to_vec(&dataset, Default::default()) of each finished

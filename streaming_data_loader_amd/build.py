@@ -20,7 +20,7 @@ BUILD = os.path.join(REPO, "build", "sdl")
 LIB = os.path.join(PKG, "libsdl_batcher.so")
 ARCH = os.environ.get("SDL_OFFLOAD_ARCH", "gfx950")
 
-SOURCES = ["tokenize_wordpiece.hip", "tokenize_bpe.hip", "tokenize_unigram.hip", "pipeline.hip", "json_text.hip", "transport_frame.hip",
+SOURCES = ["tokenize_wordpiece.hip", "tokenize_bpe.hip", "tokenize_unigram.hip", "pipeline.hip", "json_text.hip", "transport_frame.hip", "inflate.hip",
            "assets.cpp", "sdl_batcher.cpp"]
 HEADERS = ["common.hpp", "device_util.hpp", "kernels.hpp", "tok_device.hpp", "assets.hpp", "json.hpp", "unigram.hpp"]
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",

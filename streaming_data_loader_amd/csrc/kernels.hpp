@@ -76,6 +76,34 @@ hipError_t launch_json_write(const uint8_t *buf, int64_t len, const uint32_t *nl
                              const uint32_t *is_rec, const uint2 *span, const uint32_t *toff, const uint32_t *ridx,
                              uint8_t *text, uint64_t *offsets, hipStream_t st);
 
+// inflate.hip: gzip members -> their bytes back to back (the provider's GzipDecoder).
+// Per-member status (GZ_*); the output of member m is [ooff[m], ooff[m+1]).
+enum : int32_t {
+    GZ_OK = 0,
+    GZ_E_RANGE = 1,   // member range outside the buffer
+    GZ_E_TRUNC = 2,   // input ends inside the member
+    GZ_E_HEADER = 3,  // not a gzip/deflate header, or reserved flags
+    GZ_E_HCRC = 4,    // header CRC16 mismatch
+    GZ_E_BTYPE = 5,   // block type 3
+    GZ_E_STORED = 6,  // stored block LEN != ~NLEN
+    GZ_E_CODES = 7,   // bad dynamic code lengths (sets, repeats, symbol counts, no end-of-block)
+    GZ_E_CODE = 8,    // invalid literal/length or distance code
+    GZ_E_FAR = 9,     // distance too far back
+    GZ_E_OVER = 10,   // more output than the trailer's ISIZE
+    GZ_E_SIZE = 11,   // output length != ISIZE
+    GZ_E_TRAIL = 12,  // bytes after the member's trailer
+    GZ_E_CRC = 13     // CRC-32 mismatch
+};
+struct X2N {
+    uint32_t t[32];  // x^(2^k) mod P (zlib's x2n_table)
+};
+hipError_t launch_gz_size(const uint8_t *in, uint64_t in_len, const uint64_t *moff, uint64_t n, uint32_t *size,
+                          int32_t *status, unsigned long long *total, hipStream_t st);
+hipError_t launch_inflate(const uint8_t *in, const uint64_t *moff, uint64_t n, const uint32_t *ooff, uint8_t *out,
+                          int32_t *status, uint32_t *tcrc, hipStream_t st);
+hipError_t launch_gz_crc(const uint32_t *ooff, const uint8_t *out, uint64_t n, const uint32_t *tcrc, const X2N &x2n,
+                         int32_t *status, uint32_t *bad, hipStream_t st);
+
 // pipeline.hip
 // out[0..n) = exclusive prefix sum of in[0..n) (+ *carry_in when given),
 // out[n] = total.  tmp needs scan_tmp_words(n) words.  carry_in may alias out[0].

@@ -282,6 +282,11 @@ struct sdl_batcher {
     DevBuf<uint2> j_span;
     DevBuf<uint8_t> j_text;
     DevBuf<uint64_t> j_off;
+    // gzip inflate provider step (sdl_gzip_inflate_device)
+    DevBuf<uint32_t> z_size, z_off, z_tcrc, z_bad;
+    DevBuf<int32_t> z_status;
+    DevBuf<unsigned long long> z_total;
+    DevBuf<uint8_t> z_out;
     // Transport frames (sdl_pickle_frames_device)
     DevBuf<uint8_t> f_out, f_out2;
     DevBuf<uint8_t> *f_target = &f_out;  // where the next frames go
@@ -1127,6 +1132,139 @@ int sdl_json_text_device(sdl_batcher *h, const uint8_t *d_jsonl, uint64_t len, v
     } catch (std::exception &e) {
         return fail(SDL_ERR_ARG, e.what());
     }
+}
+
+namespace {
+
+const char *gz_reason(int32_t s) {
+    static const char *names[] = {"ok",
+                                  "member range outside the buffer",
+                                  "truncated",
+                                  "not a gzip header (magic, method or reserved flags)",
+                                  "header crc mismatch",
+                                  "invalid block type",
+                                  "invalid stored block lengths",
+                                  "invalid code lengths set",
+                                  "invalid literal/length or distance code",
+                                  "invalid distance too far back",
+                                  "more output than the trailer's size",
+                                  "incorrect length check",
+                                  "bytes after the member's trailer",
+                                  "incorrect data check"};
+    return s >= 0 && s < (int32_t)(sizeof(names) / sizeof(names[0])) ? names[s] : "unknown";
+}
+
+X2N make_x2n() {  // zlib's x2n_table: x^(2^k) mod P(x), reflected
+    auto mult = [](uint32_t a, uint32_t b) {
+        uint32_t m = 1u << 31, p = 0;
+        for (;;) {
+            if (a & m) {
+                p ^= b;
+                if ((a & (m - 1)) == 0) break;
+            }
+            m >>= 1;
+            b = b & 1u ? (b >> 1) ^ 0xEDB88320u : b >> 1;
+        }
+        return p;
+    };
+    X2N x{};
+    uint32_t p = 1u << 30;  // x^1
+    x.t[0] = p;
+    for (int k = 1; k < 32; ++k) x.t[k] = p = mult(p, p);
+    return x;
+}
+
+}  // namespace
+
+int sdl_gzip_inflate_device(sdl_batcher *h, const uint8_t *d_gz, uint64_t gz_len, const uint64_t *d_member_offsets,
+                            uint64_t n_members, void *stream, sdl_inflated *out) {
+    if (!h || !out || (n_members && (!d_gz || !d_member_offsets))) return fail(SDL_ERR_ARG, "null argument");
+    if (gz_len >= (1ull << 32)) return fail(SDL_ERR_CAPACITY, "gzip buffer must be < 4 GiB per call");
+    if (n_members >= (1ull << 31)) return fail(SDL_ERR_CAPACITY, "too many gzip members in one call");
+    if (((uintptr_t)d_gz & 15u) != 0) return fail(SDL_ERR_ARG, "d_gz must be 16-byte aligned");
+    try {
+        hipStream_t st = stream ? (hipStream_t)stream : h->stream;
+        const size_t n = (size_t)n_members;
+        h->z_size.ensure(n + 1);
+        h->z_off.ensure(n + 1);
+        h->z_tcrc.ensure(n + 1);
+        h->z_status.ensure(n + 1);
+        h->z_total.ensure(1);
+        h->z_bad.ensure(2);
+        h->scan_tmp.ensure((size_t)scan_tmp_words(std::max<int64_t>((int64_t)n, 1)) + 1);
+        HIP_TRY(hipMemsetAsync(h->z_total.p, 0, sizeof(unsigned long long), st));
+        unsigned long long total = 0;
+        if (n) {
+            HIP_TRY(launch_gz_size(d_gz, gz_len, d_member_offsets, n_members, h->z_size.p, h->z_status.p, h->z_total.p, st));
+            HIP_TRY(launch_exclusive_scan(h->z_size.p, h->z_off.p, (int64_t)n, h->scan_tmp.p, st));
+            HIP_TRY(hipMemcpyAsync(&total, h->z_total.p, sizeof(total), hipMemcpyDeviceToHost, st));
+            HIP_TRY(hipStreamSynchronize(st));
+        }
+        // the trailers' sizes are untrusted until decoded: bound the arena, never the kernel's writes
+        if (total >= (1ull << 32) - 64) return fail(SDL_ERR_CAPACITY, "gzip members inflate to >= 4 GiB in one call");
+        h->z_out.ensure((size_t)total + 48);
+        HIP_TRY(hipMemsetAsync(h->z_out.p + total, 0, 32, st));
+        uint32_t bad[2] = {0, 0xFFFFFFFFu};
+        if (n) {
+            HIP_TRY(hipMemcpyAsync(h->z_bad.p, bad, sizeof(bad), hipMemcpyHostToDevice, st));
+            HIP_TRY(launch_inflate(d_gz, d_member_offsets, n_members, h->z_off.p, h->z_out.p, h->z_status.p, h->z_tcrc.p, st));
+            static const X2N x2n = make_x2n();
+            HIP_TRY(launch_gz_crc(h->z_off.p, h->z_out.p, n_members, h->z_tcrc.p, x2n, h->z_status.p, h->z_bad.p, st));
+            HIP_TRY(hipMemcpyAsync(bad, h->z_bad.p, sizeof(bad), hipMemcpyDeviceToHost, st));
+            HIP_TRY(hipStreamSynchronize(st));
+        }
+        std::memset(out, 0, sizeof(*out));
+        out->d_out = h->z_out.p;
+        out->d_member_out = h->z_off.p;
+        out->d_status = h->z_status.p;
+        out->out_bytes = total;
+        out->n_members = n_members;
+        out->n_bad = bad[0];
+        if (bad[0]) {
+            int32_t s = 0;
+            HIP_TRY(hipMemcpy(&s, h->z_status.p + bad[1], sizeof(s), hipMemcpyDeviceToHost));
+            return fail(SDL_ERR_DATA, "gzip member " + std::to_string(bad[1]) + ": " + gz_reason(s) + " (" +
+                                          std::to_string(bad[0]) + " of " + std::to_string(n_members) +
+                                          " members failed)");
+        }
+        return SDL_OK;
+    } catch (HipError &e) {
+        return fail(SDL_ERR_HIP, e.what());
+    } catch (std::exception &e) {
+        return fail(SDL_ERR_ARG, e.what());
+    }
+}
+
+int sdl_gzip_split_members(const uint8_t *gz, uint64_t len, uint64_t *offsets, uint64_t cap, uint64_t *n_members) {
+    if ((!gz && len) || !n_members) return fail(SDL_ERR_ARG, "null argument");
+    // BGZF: FEXTRA with subfield SI1 'B' SI2 'C' SLEN 2 holding the member size - 1
+    auto bsize = [&](uint64_t a) -> uint64_t {
+        if (a + 18 > len || gz[a] != 0x1f || gz[a + 1] != 0x8b || gz[a + 2] != 8 || !(gz[a + 3] & 4)) return 0;
+        const uint64_t xlen = (uint64_t)gz[a + 10] | (uint64_t)gz[a + 11] << 8;
+        for (uint64_t q = a + 12; q + 4 <= a + 12 + xlen && q + 4 <= len;) {
+            const uint64_t sl = (uint64_t)gz[q + 2] | (uint64_t)gz[q + 3] << 8;
+            if (gz[q] == 'B' && gz[q + 1] == 'C' && sl == 2 && q + 6 <= len)
+                return ((uint64_t)gz[q + 4] | (uint64_t)gz[q + 5] << 8) + 1;
+            q += 4 + sl;
+        }
+        return 0;
+    };
+    std::vector<uint64_t> off{0};
+    if (len) {
+        uint64_t a = 0, b;
+        while (a < len && (b = bsize(a)) != 0 && a + b <= len) {
+            a += b;
+            off.push_back(a);
+        }
+        if (a < len) {
+            if (off.size() > 1) return fail(SDL_ERR_DATA, "BGZF member at byte " + std::to_string(a) + " has no block size");
+            off.push_back(len);  // not BGZF: the file is one member
+        }
+    }
+    *n_members = off.size() - 1;
+    if (!offsets || cap < off.size()) return fail(SDL_ERR_CAPACITY, "offsets needs n_members + 1 entries");
+    std::memcpy(offsets, off.data(), off.size() * sizeof(uint64_t));
+    return SDL_OK;
 }
 
 namespace {

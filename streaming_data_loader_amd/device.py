@@ -155,6 +155,20 @@ class DeviceBatcher:
                                                         ctypes.c_void_p(stream or None), ctypes.byref(out)))
         return out
 
+    def gzip_inflate(self, gz_ptr, gz_len, member_offsets_ptr, n_members, stream=0, check=True):
+        """The provider's gzip inflate on the device (sdl_gzip_inflate_device):
+        gzip members in a 16-B aligned device buffer -> their bytes back to back
+        in a device arena owned by this handle (native.Inflated).  check=False
+        returns (rc, Inflated) instead of raising on corrupt members."""
+        out = native.Inflated()
+        rc = native.load().sdl_gzip_inflate_device(self._h, ctypes.c_void_p(gz_ptr), gz_len,
+                                                   ctypes.c_void_p(member_offsets_ptr), n_members,
+                                                   ctypes.c_void_p(stream or None), ctypes.byref(out))
+        if check:
+            native.check(rc)
+            return out
+        return rc, out
+
     def pickle_frames(self, result, n_rows=None, flush_partial=True, stream=0):
         """Transport step on the device: the batches of `result` (the last
         process*() call) as serde_pickle frames (DeviceFrames)."""

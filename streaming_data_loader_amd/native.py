@@ -22,6 +22,7 @@ EXPORTS = [
     "sdl_batcher_push_many", "sdl_batcher_next", "sdl_batcher_flush", "sdl_batch_release",
     "sdl_process_device", "sdl_process_device_labels", "sdl_json_text_device", "sdl_pickle_frames_device", "sdl_device_to_host", "sdl_set_profiling", "sdl_stage_times",
     "sdl_tokenizer_info_get", "sdl_last_error", "sdl_abi_version", "sdl_json_to_frames",
+    "sdl_gzip_inflate_device", "sdl_gzip_split_members",
 ]
 
 
@@ -85,6 +86,19 @@ class JsonFramesStats(ctypes.Structure):
     ]
 
 
+class Inflated(ctypes.Structure):
+    _fields_ = [
+        ("d_out", ctypes.c_void_p), ("d_member_out", ctypes.c_void_p), ("d_status", ctypes.c_void_p),
+        ("out_bytes", ctypes.c_uint64), ("n_members", ctypes.c_uint64), ("n_bad", ctypes.c_uint64),
+    ]
+
+
+# per-member status codes of sdl_gzip_inflate_device (csrc/kernels.hpp GZ_*)
+GZ_OK, GZ_E_RANGE, GZ_E_TRUNC, GZ_E_HEADER, GZ_E_HCRC, GZ_E_BTYPE, GZ_E_STORED, GZ_E_CODES, GZ_E_CODE, \
+    GZ_E_FAR, GZ_E_OVER, GZ_E_SIZE, GZ_E_TRAIL, GZ_E_CRC = range(14)
+SDL_ERR_DATA = -8
+
+
 FRAME_SINK = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint8), ctypes.c_uint64)
 
 
@@ -133,6 +147,10 @@ def load(path=LIB_PATH):
     L.sdl_pickle_frames_device.argtypes = [vp, ctypes.POINTER(DeviceRows), u64, i64, vp, ctypes.POINTER(Frames)]
     L.sdl_json_to_frames.argtypes = [vp, vp, u64, u64, i64, FRAME_SINK, vp, ctypes.POINTER(JsonFramesStats)]
     L.sdl_json_to_frames.restype = i64
+    L.sdl_gzip_inflate_device.argtypes = [vp, vp, u64, vp, u64, vp, ctypes.POINTER(Inflated)]
+    L.sdl_gzip_inflate_device.restype = i64
+    L.sdl_gzip_split_members.argtypes = [vp, u64, vp, u64, ctypes.POINTER(u64)]
+    L.sdl_gzip_split_members.restype = i64
     L.sdl_set_profiling.argtypes = [vp, i64]
     L.sdl_stage_times.argtypes = [vp, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_float), i64]
     L.sdl_last_error.restype = ctypes.c_char_p
@@ -166,6 +184,20 @@ def default_config(task):
     c = Config()
     load().sdl_config_default(ctypes.byref(c), task)
     return c
+
+
+def gzip_split_members(buf):
+    """sdl_gzip_split_members (host only): member offsets (numpy u64 [n + 1]) of one gzip file."""
+    import numpy as np
+    L = load()
+    b = bytes(buf)
+    n = ctypes.c_uint64(0)
+    rc = L.sdl_gzip_split_members(b, len(b), None, 0, ctypes.byref(n))
+    if rc < 0 and rc != -7:
+        check(rc)
+    off = np.zeros(n.value + 1, dtype=np.uint64)
+    check(L.sdl_gzip_split_members(b, len(b), off.ctypes.data, off.size, ctypes.byref(n)))
+    return off
 
 
 def d2h(handle, dst_numpy, src_ptr, nbytes, stream=None):

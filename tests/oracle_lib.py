@@ -335,3 +335,23 @@ def pickle_dataset(task, B, S, LW, rows, input_ids, attention_mask, token_type_i
     out = np.zeros(n, np.uint8)
     assert L.orc_pickle_dataset(*args, out.ctypes.data, n) == n
     return out.tobytes()
+
+
+def gz_inflate(member):
+    """oracle/orc_inflate.c: one gzip member -> (status, inflated bytes); status
+    codes are the device's GZ_* codes (0 ok)."""
+    L = lib()
+    if not hasattr(L, "_gz_ready"):
+        L.orc_gz_isize.restype = ctypes.c_uint32
+        L.orc_gz_isize.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
+        L.orc_gz_inflate.restype = ctypes.c_int
+        L.orc_gz_inflate.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t,
+                                     ctypes.POINTER(ctypes.c_size_t)]
+        L._gz_ready = True
+    m = bytes(member)
+    cap = L.orc_gz_isize(m, len(m)) if len(m) >= 18 else 0
+    cap = min(cap, 1032 * len(m) + 64)  # DEFLATE expands at most ~1032:1 (the device's sizing bound)
+    buf = ctypes.create_string_buffer(max(cap, 1))
+    got = ctypes.c_size_t(0)
+    st = L.orc_gz_inflate(m, len(m), buf, cap, ctypes.byref(got))
+    return st, buf.raw[:got.value]

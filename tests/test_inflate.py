@@ -1,0 +1,277 @@
+"""The provider's gzip inflate: sdl_gzip_inflate_device
+(inflate.hip, one wave per member) against the CPU oracle (oracle/orc_inflate.c,
+an RFC 1951/1952 restatement with zlib's error rules), which is pinned here
+against CPython's zlib on streams of every block type, every gzip header field,
+and the reference's own data/test.json.gz (tests/golden/test.json.gz).  Member
+outputs must be bit-exact; corrupt members must fail (the reference's
+`next_line().await.unwrap()` panics) with the oracle's reason where the reason
+is well defined."""
+import gzip
+import json
+import os
+import random
+import struct
+import zlib
+
+import numpy as np
+import pytest
+
+import oracle_lib
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+REF_GZ = os.path.join(GOLDEN, "test.json.gz")
+
+STRATEGIES = [zlib.Z_DEFAULT_STRATEGY, zlib.Z_FILTERED, zlib.Z_HUFFMAN_ONLY, zlib.Z_RLE, zlib.Z_FIXED]
+
+
+def gz_member(data, level=6, strategy=zlib.Z_DEFAULT_STRATEGY, flags=0, extra=b"", name=b"", comment=b"",
+              mem_level=8, flush_every=0):
+    """One gzip member with the given header fields around zlib's raw DEFLATE."""
+    co = zlib.compressobj(level, zlib.DEFLATED, -15, mem_level, strategy)
+    if flush_every:
+        body = b"".join(co.compress(data[i:i + flush_every]) + co.flush(zlib.Z_FULL_FLUSH)
+                        for i in range(0, len(data), flush_every)) + co.flush()
+    else:
+        body = co.compress(data) + co.flush()
+    flg = flags
+    hdr = bytearray(b"\x1f\x8b\x08\x00" + struct.pack("<I", 0) + b"\x00\xff")
+    if extra:
+        flg |= 4
+        hdr += struct.pack("<H", len(extra)) + extra
+    if name:
+        flg |= 8
+        hdr += name + b"\x00"
+    if comment:
+        flg |= 16
+        hdr += comment + b"\x00"
+    hdr[3] = flg
+    if flg & 2:
+        hdr += struct.pack("<H", zlib.crc32(bytes(hdr)) & 0xFFFF)
+    return bytes(hdr) + body + struct.pack("<II", zlib.crc32(data), len(data) & 0xFFFFFFFF)
+
+
+def bgzf(data, block=65280, level=6):
+    """BGZF (bgzip's layout): members of <= `block` input bytes, each with the
+    'BC' extra subfield holding its size - 1, then the empty EOF member."""
+    out = []
+    for i in range(0, len(data), block):
+        m = gz_member(data[i:i + block], level, extra=b"BC\x02\x00\x00\x00")
+        m = bytearray(m)
+        m[16:18] = struct.pack("<H", len(m) - 1)
+        out.append(bytes(m))
+    eof = bytearray(gz_member(b"", 6, extra=b"BC\x02\x00\x00\x00"))
+    eof[16:18] = struct.pack("<H", len(eof) - 1)
+    return b"".join(out) + bytes(eof)
+
+
+def payloads(records):
+    rng = random.Random(7)
+    lines = "".join(json.dumps({"id": i, "text": t}) + "\n" for i, t in enumerate(records)).encode()
+    return {
+        "empty": b"",
+        "one": b"x",
+        "jsonl": lines,
+        "jsonl_x3": lines * 3,
+        "random": bytes(rng.randrange(256) for _ in range(70000)),  # stored blocks
+        "run": b"a" * 100000,                                          # distance-1 copies
+        "period": (b"abcdefghij" * 9000)[:90000],
+        "mixed": lines[:20000] + bytes(rng.randrange(256) for _ in range(3000)) + b"z" * 5000 + lines[20000:60000],
+    }
+
+
+def corpus(records):
+    """(name, member bytes, expected inflated bytes)"""
+    out = []
+    for pname, data in payloads(records).items():
+        for level in (0, 1, 6, 9):
+            for st in STRATEGIES:
+                if level == 0 and st != zlib.Z_DEFAULT_STRATEGY:
+                    continue
+                out.append((f"{pname}/l{level}/s{st}", gz_member(data, level, st), data))
+    data = payloads(records)["jsonl"]
+    out.append(("header fields", gz_member(data, extra=b"ab\x03\x00xyz", name=b"file.json", comment=b"c",
+                                           flags=2), data))
+    out.append(("full flushes", gz_member(data, flush_every=4096), data))
+    out.append(("memlevel 1", gz_member(data, 9, mem_level=1), data))
+    out.append(("gzip module", gzip.compress(data, 9), data))
+    return out
+
+
+def corrupt_cases(records):
+    """(name, member bytes, expected status) -- reasons that do not depend on
+    where a decoder notices the damage"""
+    data = payloads(records)["jsonl"][:30000]
+    good = gz_member(data)
+    bad_crc = bytearray(good)
+    bad_crc[-8] ^= 1
+    bad_size = bytearray(good)
+    bad_size[-4] ^= 1
+    bad_magic = bytearray(good)
+    bad_magic[1] = 0x8c
+    reserved = bytearray(good)
+    reserved[3] |= 0x20
+    hcrc = bytearray(gz_member(data, flags=2))
+    hcrc[10] ^= 1
+    btype3 = bytearray(gz_member(b"hello"))
+    btype3[10] = 0x07  # BFINAL 1, BTYPE 3
+    stored = bytearray(gz_member(b"hello world", level=0))
+    stored[13] ^= 0xFF  # NLEN
+    far = gz_member(b"")[:10] + bytes([0x03, 0x02]) + gz_member(b"")[12:]  # fixed block: match before any output
+    return [
+        ("crc", bytes(bad_crc), 13),
+        ("isize", bytes(bad_size), 11),
+        ("magic", bytes(bad_magic), 3),
+        ("reserved flag", bytes(reserved), 3),
+        ("header crc", bytes(hcrc), 4),
+        ("btype 3", bytes(btype3), 5),
+        ("stored nlen", bytes(stored), 6),
+        # zlib (and, with multiple_members off, the reference's GzipDecoder) stops at the first
+        # trailer and ignores what follows; a member range here must end at its trailer, so the
+        # size is read from the wrong place and the member fails (documented gap)
+        ("trailing bytes", good + b"\x00\x01", None),
+        ("truncated", good[:len(good) // 2], None),
+        ("short", good[:12], 2),
+        ("far", far, 9),
+    ]
+
+
+# ---- CPU: the oracle pinned against zlib ----------------------------------------
+
+def test_oracle_matches_zlib(records):
+    for name, member, want in corpus(records):
+        assert zlib.decompress(member, 31) == want, name
+        st, got = oracle_lib.gz_inflate(member)
+        assert st == 0 and got == want, name
+
+
+def test_oracle_reference_fixture(records):
+    gz = open(REF_GZ, "rb").read()
+    st, got = oracle_lib.gz_inflate(gz)
+    assert st == 0 and got == gzip.decompress(gz)
+    # cirrussearch layout: an {"index": ...} line before each document; JsonText keeps the 50 texts
+    texts = [json.loads(l)["text"] for l in got.decode().splitlines() if "text" in json.loads(l)]
+    assert texts == records
+
+
+def test_oracle_rejects_corrupt_members(records):
+    for name, member, want in corrupt_cases(records):
+        st, _ = oracle_lib.gz_inflate(member)
+        assert st != 0, name
+        if want is not None:
+            assert st == want, (name, st)
+        if name != "trailing bytes":
+            with pytest.raises(zlib.error):
+                zlib.decompress(member, 31)
+
+
+def test_split_members_host_only(native_lib, records):
+    from streaming_data_loader_amd import native
+    data = payloads(records)["jsonl_x3"]
+    b = bgzf(data, block=20000)
+    off = native.gzip_split_members(b)
+    assert off[0] == 0 and off[-1] == len(b) and len(off) == (len(data) + 19999) // 20000 + 2
+    assert b"".join(zlib.decompress(b[int(off[i]):int(off[i + 1])], 31) for i in range(len(off) - 1)) == data
+    plain = gz_member(data)
+    assert list(native.gzip_split_members(plain)) == [0, len(plain)]
+    assert list(native.gzip_split_members(b"")) == [0]
+
+
+# ---- GPU: the device inflate against the oracle ------------------------------------
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch as t
+    assert t.cuda.is_available(), "GPU tests need a HIP device"
+    return t
+
+
+def device_inflate(torch, db, members, check=True):
+    from streaming_data_loader_amd import native
+    buf = b"".join(members)
+    off = np.zeros(len(members) + 1, np.uint64)
+    np.cumsum([len(m) for m in members], out=off[1:])
+    a = np.zeros(len(buf) + 32, np.uint8)
+    a[:len(buf)] = np.frombuffer(buf, np.uint8)
+    d_gz = torch.from_numpy(a).cuda()
+    d_off = torch.from_numpy(off.view(np.int64)).cuda()
+    rc, out = db.gzip_inflate(d_gz.data_ptr(), len(buf), d_off.data_ptr(), len(members), check=False)
+    if check:
+        native.check(rc)
+    n = len(members)
+    status = np.zeros(n, np.int32)
+    mo = np.zeros(n + 1, np.uint32)
+    arena = np.zeros(int(out.out_bytes) + 32, np.uint8)
+    if n:
+        native.d2h(db._h, status, out.d_status, status.nbytes)
+        native.d2h(db._h, mo, out.d_member_out, mo.nbytes)
+    native.d2h(db._h, arena, out.d_out, arena.nbytes)
+    assert (arena[int(out.out_bytes):] == 0).all()
+    return rc, out, status, [arena[int(mo[i]):int(mo[i + 1])].tobytes() for i in range(n)], arena
+
+
+@pytest.mark.gpu
+def test_device_inflate_matches_oracle(torch, native_lib, records):
+    from streaming_data_loader_amd.device import DeviceBatcher
+    db = DeviceBatcher(batch_size=8, sequence_length=128)
+    cases = corpus(records)
+    rc, out, status, got, arena = device_inflate(torch, db, [m for _, m, _ in cases])
+    assert rc == 0 and out.n_bad == 0
+    for (name, member, want), st, g in zip(cases, status, got):
+        ost, ogot = oracle_lib.gz_inflate(member)
+        assert ost == 0 and st == 0, name
+        assert g == ogot == want, name
+    assert arena[:int(out.out_bytes)].tobytes() == b"".join(w for _, _, w in cases)
+
+
+@pytest.mark.gpu
+def test_device_reference_fixture_to_records(torch, native_lib, records):
+    """data/test.json.gz -> device inflate -> device JsonText: the records the
+    reference's provider sends (gzip_file_provider.rs:30-50)."""
+    from streaming_data_loader_amd.device import DeviceBatcher
+    from streaming_data_loader_amd import native
+    db = DeviceBatcher(batch_size=8, sequence_length=128)
+    gz = open(REF_GZ, "rb").read()
+    rc, out, status, got, _ = device_inflate(torch, db, [gz])
+    assert got[0] == gzip.decompress(gz)
+    jt = db.json_text(out.d_out, int(out.out_bytes))
+    offs = np.zeros(jt.n_records + 1, np.uint64)
+    native.d2h(db._h, offs, jt.d_offsets, offs.nbytes)
+    text = np.zeros(int(jt.text_bytes), np.uint8)
+    native.d2h(db._h, text, jt.d_text, text.nbytes)
+    recs = [text[int(offs[i]):int(offs[i + 1])].tobytes().decode() for i in range(jt.n_records)]
+    assert recs == records
+
+
+@pytest.mark.gpu
+def test_device_bgzf_and_many_members(torch, native_lib, records):
+    from streaming_data_loader_amd.device import DeviceBatcher
+    from streaming_data_loader_amd import native
+    db = DeviceBatcher(batch_size=8, sequence_length=128)
+    data = payloads(records)["jsonl"] * 40  # ~21 MB
+    b = bgzf(data)
+    off = native.gzip_split_members(b)
+    members = [b[int(off[i]):int(off[i + 1])] for i in range(len(off) - 1)]
+    rc, out, status, got, arena = device_inflate(torch, db, members)
+    assert rc == 0 and (status == 0).all()
+    assert arena[:int(out.out_bytes)].tobytes() == data
+
+
+@pytest.mark.gpu
+def test_device_rejects_corrupt_members(torch, native_lib, records):
+    from streaming_data_loader_amd.device import DeviceBatcher
+    from streaming_data_loader_amd import native
+    db = DeviceBatcher(batch_size=8, sequence_length=128)
+    good = gz_member(payloads(records)["jsonl"][:5000])
+    cases = corrupt_cases(records)
+    members = [good] + [m for _, m, _ in cases] + [good]
+    rc, out, status, got, _ = device_inflate(torch, db, members, check=False)
+    assert rc == native.SDL_ERR_DATA and out.n_bad == len(cases)
+    assert status[0] == 0 and status[-1] == 0 and got[0] == got[-1] == zlib.decompress(good, 31)
+    for (name, member, want), st in zip(cases, status[1:-1]):
+        ost, _ = oracle_lib.gz_inflate(member)
+        assert st != 0, name
+        if want is not None:
+            assert st == want == ost, (name, st, ost)
+    # the handle stays usable after a failed call
+    rc, out, status, got, _ = device_inflate(torch, db, [good])
+    assert rc == 0 and got[0] == zlib.decompress(good, 31)
