@@ -10,7 +10,7 @@
 //               output before anything is decoded)
 //   k_inflate   one wave per member.  DEFLATE (RFC 1951) is a serial bit stream:
 //               lane 0 decodes Huffman tokens through 10-bit (lit/len) and
-//               8-bit (dist) LDS tables built by the whole wave per block, and
+//               10-bit (dist) LDS tables built by the whole wave per block, and
 //               emits literals and (length, distance) records into an LDS batch;
 //               the wave then expands the matches and resolves them by pointer
 //               jumping (a byte copied from an earlier byte of the same batch
@@ -31,13 +31,15 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdio>
 
+#include "device_util.hpp"
 #include "kernels.hpp"
 
 namespace sdl {
 namespace {
 
-constexpr int LB = 10, DB = 8;     // primary table bits: lit/len, dist
+constexpr int LB = 10, DB = 10;    // primary table bits: lit/len, dist
 constexpr int IN_STAGE = 2048;     // staged compressed bytes per wave
 constexpr int OBUF = 2048;         // output batch bytes
 constexpr int MLCAP = 256;         // matches per batch
@@ -68,19 +70,19 @@ __device__ __forceinline__ uint32_t sym_entry(int t, int s, int n) {
     return 0;  // 30, 31: invalid distance code
 }
 
-// canonical decode of a code longer than the primary table (puff's decode()):
-// needs >= 15 bits in bb
-__device__ uint32_t slow_decode(uint64_t bb, const uint16_t *cnt, const uint16_t *syms, int t) {
-    int code = 0, first = 0, index = 0;
-    for (int len = 1; len <= 15; ++len) {
-        code |= (int)((bb >> (len - 1)) & 1u);
-        const int count = cnt[len];
-        if (code - first < count) return sym_entry(t, syms[index + code - first], len);
-        index += count;
-        first = (first + count) << 1;
-        code <<= 1;
-    }
-    return 0;
+// A code longer than the primary table (11..15 bits): canonical decode by
+// limits.  c = the next 15 stream bits, first bit most significant; the code
+// has length L for the smallest L with c < lim[L - 11] (lim = one past the
+// last code of length L, left-aligned to 15 bits); its symbol is sorted entry
+// base[L - 11] + (c >> (15 - L)).  All lanes can do this (one LDS load).
+__device__ __forceinline__ uint32_t long_decode(uint64_t bits, const uint32_t *lim, const uint32_t *base,
+                                                const uint32_t *sent) {
+    const uint32_t c = __builtin_bitreverse32((uint32_t)bits) >> 17;
+    uint32_t idx = ~0u;
+#pragma unroll
+    for (int i = 4; i >= 0; --i)
+        if (c < lim[i]) idx = base[i] + (c >> (4 - i));
+    return idx == ~0u ? 0u : sent[idx];
 }
 
 __device__ __forceinline__ uint32_t bfl(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
@@ -111,6 +113,35 @@ __device__ uint32_t x2nmodp(uint64_t n, int k, const X2N &x2n) {
 
 }  // namespace
 
+// Diagnostic build (-DSDL_STAMPS): lane 0 of every wave adds the s_memtime
+// cycles of each phase and event counts; never in the product.
+#ifdef SDL_STAMPS
+__device__ unsigned long long sdl_gz_cycles[8], sdl_gz_counts[8];
+#define GZ_STAMP(k)                                                       \
+    do {                                                                  \
+        if (threadIdx.x == 0) {                                           \
+            const unsigned long long t_ = __builtin_amdgcn_s_memtime();  \
+            atomicAdd(&sdl_gz_cycles[k], t_ - gz_prev_);                  \
+            gz_prev_ = t_;                                                \
+        }                                                                 \
+    } while (0)
+#define GZ_COUNT(k) do { if (threadIdx.x == 0) atomicAdd(&sdl_gz_counts[k], 1ull); } while (0)
+void print_gz_cycles() {
+    unsigned long long h[8], c[8];
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(sdl_gz_cycles), sizeof(h)) != hipSuccess) return;
+    if (hipMemcpyFromSymbol(c, HIP_SYMBOL(sdl_gz_counts), sizeof(c)) != hipSuccess) return;
+    static const char *names[] = {"header+stage", "block hdr+emit", "tables", "token decode", "expand", "resolve", "store", "walk"};
+    unsigned long long tot = 0;
+    for (int i = 0; i < 8; ++i) tot += h[i];
+    for (int i = 0; i < 8; ++i)
+        fprintf(stderr, "[gz stamps] %-14s %6.2f%%  count %llu  cycles/count %.0f\n", names[i],
+                tot ? 100.0 * (double)h[i] / (double)tot : 0.0, c[i], c[i] ? (double)h[i] / (double)c[i] : 0.0);
+}
+#else
+#define GZ_STAMP(k) do {} while (0)
+#define GZ_COUNT(k) do {} while (0)
+#endif
+
 // ---- lane per member: header magic + ISIZE ------------------------------------
 __global__ void k_gz_size(const uint8_t *__restrict__ in, uint64_t in_len, const uint64_t *__restrict__ moff, uint64_t n,
                           uint32_t *__restrict__ size, int32_t *__restrict__ status, unsigned long long *__restrict__ total) {
@@ -137,19 +168,24 @@ __global__ void k_gz_size(const uint8_t *__restrict__ in, uint64_t in_len, const
 }
 
 // ---- one wave per member --------------------------------------------------------
+// Tokens are decoded speculatively by all lanes: lane i decodes the token that
+// would start at bit bp + i (lit/len code, length extra bits, distance code and
+// extra bits: <= 48 bits from a 64-bit window of the staged input), and the
+// scalar unit walks the real chain from bit bp through the lanes' token lengths
+// (v_readlane), so one pass settles every token starting in the next 64 bits.
+// Literals and match records then go to the LDS batch in parallel (positions
+// by a wave prefix sum of the tokens' output lengths).
 __global__ __launch_bounds__(64) void k_inflate(const uint8_t *__restrict__ in, const uint64_t *__restrict__ moff,
                                                uint64_t n, const uint32_t *__restrict__ ooff, uint8_t *__restrict__ out,
                                                int32_t *__restrict__ status, uint32_t *__restrict__ tcrc) {
     __shared__ uint32_t s_lit[1 << LB], s_dst[1 << DB];
-    __shared__ uint16_t s_cnt[2][16];
-    __shared__ uint16_t s_sym[NSYM];     // symbols sorted by code: lit/len [0, 288), dist [288, 320)
-    __shared__ uint16_t s_rc[NSYM];      // bit-reversed canonical code per symbol
+    __shared__ uint32_t s_sent[NSYM];     // table entries of the symbols sorted by code: lit/len [0, 288), dist [288, 320)
     __shared__ uint8_t s_len[NSYM + 32];  // code lengths (lit/len, then dist); code-length code at NSYM..
-    __shared__ __attribute__((aligned(16))) uint8_t s_in[IN_STAGE + 16];
+    __shared__ __attribute__((aligned(16))) uint32_t s_in32[IN_STAGE / 4 + 4];
     __shared__ uint8_t s_ob[OBUF];
-    __shared__ uint16_t s_ref[OBUF];     // 0: byte known; d: byte equals the one d back
-    __shared__ uint32_t s_mpl[MLCAP];    // match: batch offset | length << 16
-    __shared__ uint16_t s_md[MLCAP];     // match distance
+    __shared__ uint16_t s_ref[OBUF];      // 0: byte known; d: byte equals the one d back
+    __shared__ uint32_t s_mpl[MLCAP];     // match: batch offset | length << 16
+    __shared__ uint16_t s_md[MLCAP];      // match distance
 
     const uint64_t m = blockIdx.x;
     const int lane = (int)threadIdx.x;
@@ -158,27 +194,13 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t *__restrict__ in, 
     uint8_t *const dst = out + ooff[m];
     const uint32_t cap = ooff[m + 1] - ooff[m];
     const uint32_t mlen = (uint32_t)(mz - ma);
-    typedef __attribute__((address_space(3))) uint32_t lds_w;
-    const lds_w *in32 = (const lds_w *)s_in;
+    uint8_t *const s_in = reinterpret_cast<uint8_t *>(s_in32);
+#ifdef SDL_STAMPS
+    unsigned long long gz_prev_ = __builtin_amdgcn_s_memtime();
+#endif
 
-    // lane 0's decoder state (other lanes' copies unused)
-    uint64_t bb = 0;
-    int bc = 0, ip = 0;
+    // ---- member header (lane 0, straight from global memory) ----
     int32_t err = GZ_OK;
-    bool in_block = false, final_seen = false;
-    uint32_t nb = 0, nm = 0;
-    auto need = [&](int k) {  // byte refill to >= k bits (k <= 57)
-        while (bc < k) {
-            bb |= (uint64_t)s_in[ip++] << bc;
-            bc += 8;
-        }
-    };
-    auto drop = [&](int k) {
-        bb >>= k;
-        bc -= k;
-    };
-
-    // ---- header (lane 0, straight from global memory) ----
     uint32_t p = 10;  // member-relative
     if (lane == 0) {
         const uint32_t flg = in[ma + 3];
@@ -211,9 +233,10 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t *__restrict__ in, 
         return;
     }
 
-    // ---- staging of compressed bytes: s_in[0] is member byte sbase (16-B aligned in `in`) ----
-    uint64_t sbase = 0;  // absolute
-    auto restage = [&](uint64_t abs) {
+    // ---- staged input: s_in[0] is byte sbase (16-B aligned in `in`); bp = bit position in s_in ----
+    uint64_t sbase = 0;  // wave-uniform
+    uint32_t bp = 0;     // wave-uniform
+    auto restage = [&](uint64_t abs, uint32_t bit) {
         sbase = abs & ~(uint64_t)15;
 #pragma unroll
         for (int k = 0; k < IN_STAGE / 16 / 64; ++k) {
@@ -231,321 +254,427 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t *__restrict__ in, 
         }
         if (lane == 0) *reinterpret_cast<uint4 *>(s_in + IN_STAGE) = make_uint4(0, 0, 0, 0);
         __syncthreads();
-        if (lane == 0) ip = (int)(abs - sbase);
+        bp = (uint32_t)(abs - sbase) * 8u + bit;
     };
-    restage(ma + bfl(p));
+    auto peek = [&](uint32_t pos) -> uint32_t {  // 32 bits from bit `pos` of the stage
+        const uint32_t a = pos >> 5;
+        return __builtin_amdgcn_alignbit(s_in32[a + 1], s_in32[a], pos & 31u);
+    };
+    restage(ma + bfl(p), 0);
+    GZ_STAMP(0);
+    GZ_COUNT(0);
 
-    enum : uint32_t { A_DONE, A_ERR, A_RESTAGE, A_BUILD, A_FLUSH, A_STORED };
-    uint32_t produced = 0;  // wave-uniform
+    enum : uint32_t { A_ERR, A_BUILD, A_STORED };
+    uint32_t produced = 0, nb = 0, nm = 0;  // wave-uniform
+    bool in_block = false, final_seen = false;
+    uint32_t limL[5], baseL[5], limD[5], baseD[5];  // long codes (11..15 bits) of the block, long_decode
     for (;;) {
-        uint32_t act = A_DONE, x0 = 0, x1 = 0;
-        if (lane == 0) {
-            if (!in_block) {
-                if (final_seen) act = A_DONE;
-                else if (ip > IN_STAGE - HDR_ROOM) act = A_RESTAGE;
-                else {
-                    need(3);
-                    final_seen = bb & 1u;
-                    const uint32_t type = (uint32_t)(bb >> 1) & 3u;
-                    drop(3);
-                    if (type == 0) {  // stored
-                        drop(bc & 7);
-                        need(32);
-                        const uint32_t len = (uint32_t)bb & 0xFFFFu, nlen = (uint32_t)(bb >> 16) & 0xFFFFu;
-                        drop(32);
-                        if (len != (~nlen & 0xFFFFu)) {
-                            err = GZ_E_STORED;
-                            act = A_ERR;
-                        } else {
-                            act = A_STORED;
-                            x0 = (uint32_t)(sbase + (uint64_t)ip - (uint64_t)(bc >> 3) - ma);  // data start
-                            x1 = len;
-                            bb = 0;
-                            bc = 0;
-                        }
-                    } else if (type == 1) {  // fixed codes
-                        for (int s = 0; s < 288; ++s) s_len[s] = s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : 8;
-                        for (int s = 0; s < 32; ++s) s_len[288 + s] = 5;
-                        act = A_BUILD;
-                        x0 = 288;
-                        x1 = 32 | 1u << 16;
-                    } else if (type == 2) {  // dynamic codes
-                        need(14);
-                        const int hlit = (int)(bb & 31u) + 257, hdist = (int)((bb >> 5) & 31u) + 1,
-                                  hclen = (int)((bb >> 10) & 15u) + 4;
-                        drop(14);
-                        if (hlit > 286 || hdist > 30) err = GZ_E_CODES;
-                        uint8_t *cl = s_len + NSYM;
-                        for (int i = 0; i < 19; ++i) cl[i] = 0;
-                        for (int i = 0; i < hclen && !err; ++i) {
-                            need(3);
-                            cl[c_cl_order[i]] = (uint8_t)(bb & 7u);
-                            drop(3);
-                        }
-                        // code-length code: complete, <= 7 bits; its 128-entry table in s_dst
-                        uint16_t cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0}, next[8];
-                        for (int i = 0; i < 19; ++i) ++cnt[cl[i]];
-                        int left = 1;
-                        for (int l = 1; l < 8; ++l) left = (left << 1) - cnt[l];
-                        if (!err && left != 0) err = GZ_E_CODES;  // over-subscribed or incomplete (or empty)
-                        if (!err) {
-                            uint32_t code = 0;
-                            cnt[0] = 0;
-                            for (int l = 1; l < 8; ++l) {
-                                code = (code + cnt[l - 1]) << 1;
-                                next[l] = (uint16_t)code;
-                            }
-                            for (int s = 0; s < 19; ++s)
-                                if (cl[s]) {
-                                    const int l = cl[s];
-                                    const uint32_t r = __builtin_bitreverse32((uint32_t)next[l]++) >> (32 - l);
-                                    for (uint32_t i = r; i < 128; i += 1u << l) s_dst[i] = (uint32_t)l | (uint32_t)s << 16;
-                                }
-                            const int total = hlit + hdist;
-                            int i = 0;
-                            while (i < total && !err) {
-                                need(14);
-                                const uint32_t e = s_dst[bb & 127u];
-                                const int sym = (int)(e >> 16);
-                                drop((int)(e & 15u));
-                                if (sym < 16) {
-                                    s_len[i++] = (uint8_t)sym;
-                                    continue;
-                                }
-                                int rep;
-                                uint8_t v = 0;
-                                if (sym == 16) {
-                                    if (i == 0) { err = GZ_E_CODES; break; }
-                                    v = s_len[i - 1];
-                                    rep = 3 + (int)(bb & 3u);
-                                    drop(2);
-                                } else if (sym == 17) {
-                                    rep = 3 + (int)(bb & 7u);
-                                    drop(3);
-                                } else {
-                                    rep = 11 + (int)(bb & 127u);
-                                    drop(7);
-                                }
-                                if (i + rep > total) { err = GZ_E_CODES; break; }
-                                while (rep--) s_len[i++] = v;
-                            }
-                            if (!err && s_len[256] == 0) err = GZ_E_CODES;  // missing end-of-block code
-                        }
-                        if (err) act = A_ERR;
-                        else {
-                            act = A_BUILD;
-                            x0 = (uint32_t)hlit;
-                            x1 = (uint32_t)hdist;
-                        }
-                    } else {
-                        err = GZ_E_BTYPE;
-                        act = A_ERR;
-                    }
-                }
-            } else {
-                // ---- Huffman tokens into the batch ----
-                bool eob = false, rs = false;
-                for (;;) {
-                    if (nb > (uint32_t)(OBUF - 259) || nm >= (uint32_t)MLCAP) break;
-                    if (ip > IN_STAGE - 16) { rs = true; break; }
-                    if (bc <= 32) {
-                        const int a = ip >> 2;
-                        const uint32_t w = __builtin_amdgcn_alignbyte(in32[a + 1], in32[a], (uint32_t)(ip & 3));
-                        bb |= (uint64_t)w << bc;
-                        ip += 4;
-                        bc += 32;
-                    }
-                    uint32_t e = s_lit[bb & ((1u << LB) - 1u)];
-                    if (((e >> 4) & 3u) == K_SLOW) e = slow_decode(bb, s_cnt[0], s_sym, 0);
-                    const int nbits = (int)(e & 15u);
-                    if (nbits == 0) { err = GZ_E_CODE; break; }
-                    drop(nbits);
-                    const uint32_t kind = (e >> 4) & 3u;
-                    if (kind == K_LIT) {
-                        if (produced + nb >= cap) { err = GZ_E_OVER; break; }
-                        s_ob[nb] = (uint8_t)(e >> 16);
-                        s_ref[nb] = 0;
-                        ++nb;
-                        continue;
-                    }
-                    if (kind == K_EOB) { eob = true; break; }
-                    const int eb = (int)((e >> 8) & 15u);
-                    const uint32_t len = (e >> 16) + ((uint32_t)bb & ((1u << eb) - 1u));
-                    drop(eb);
-                    if (bc <= 32) {
-                        const int a = ip >> 2;
-                        const uint32_t w = __builtin_amdgcn_alignbyte(in32[a + 1], in32[a], (uint32_t)(ip & 3));
-                        bb |= (uint64_t)w << bc;
-                        ip += 4;
-                        bc += 32;
-                    }
-                    uint32_t d = s_dst[bb & ((1u << DB) - 1u)];
-                    if (((d >> 4) & 3u) == K_SLOW) d = slow_decode(bb, s_cnt[1], s_sym + 288, 1);
-                    const int dbits = (int)(d & 15u);
-                    if (dbits == 0) { err = GZ_E_CODE; break; }
-                    drop(dbits);
-                    const int db = (int)((d >> 8) & 15u);
-                    const uint32_t dist = (d >> 16) + ((uint32_t)bb & ((1u << db) - 1u));
-                    drop(db);
-                    if (dist > produced + nb) { err = GZ_E_FAR; break; }
-                    if (produced + nb + len > cap) { err = GZ_E_OVER; break; }
-                    s_mpl[nm] = nb | len << 16;
-                    s_md[nm] = (uint16_t)dist;
-                    ++nm;
-                    nb += len;
-                }
-                if (err) act = A_ERR;
-                else {
-                    act = A_FLUSH;
-                    x0 = nb;
-                    x1 = nm | (eob ? 1u << 16 : 0u) | (rs ? 1u << 17 : 0u);
-                    if (eob) in_block = false;
-                    // input consumed past the member: truncated
-                    if (sbase + (uint64_t)ip - (uint64_t)(bc >> 3) > mz) {
-                        err = GZ_E_TRUNC;
-                        act = A_ERR;
-                    }
-                }
+        if (!in_block) {
+            if (final_seen) break;
+            if (bp > 8u * (IN_STAGE - HDR_ROOM)) {
+                restage(sbase + (bp >> 3), bp & 7u);
+                continue;
             }
-        }
-        act = bfl(act);
-        x0 = bfl(x0);
-        x1 = bfl(x1);
-        if (act == A_DONE || act == A_ERR) break;
-        if (act == A_RESTAGE) {
-            const uint64_t abs = (uint64_t)bfl((uint32_t)(sbase + (uint64_t)ip - ma)) + ma;
-            restage(abs);
-            continue;
-        }
-        if (act == A_BUILD) {
-            // canonical codes (lane 0), then the primary tables (all lanes)
+            // ---- block header (lane 0): a 64-bit reader refilled 32 bits at a time ----
+            uint32_t act = A_ERR, x0 = 0, x1 = 0, nbp = 0, fin = 0;
+            if (lane == 0) {
+                uint64_t bb = 0;
+                int bc = 0;
+                uint32_t fill = bp;
+                auto need = [&](int k) {  // k <= 32
+                    if (bc < k) {
+                        bb |= (uint64_t)peek(fill) << bc;
+                        fill += 32;
+                        bc += 32;
+                    }
+                };
+                auto drop = [&](int k) {
+                    bb >>= k;
+                    bc -= k;
+                };
+                need(3);
+                fin = (uint32_t)bb & 1u;
+                const uint32_t type = (uint32_t)(bb >> 1) & 3u;
+                drop(3);
+                if (type == 0) {  // stored: LEN, NLEN at the next byte boundary
+                    const uint32_t at = (fill - (uint32_t)bc + 7u) & ~7u;
+                    const uint32_t w = peek(at);
+                    if ((w & 0xFFFFu) != (~(w >> 16) & 0xFFFFu)) err = GZ_E_STORED;
+                    else {
+                        act = A_STORED;
+                        x0 = (uint32_t)(sbase + (at >> 3) + 4 - ma);  // data start, member-relative
+                        x1 = w & 0xFFFFu;
+                    }
+                } else if (type == 1) {  // fixed codes
+                    for (int s = 0; s < 288; ++s) s_len[s] = s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : 8;
+                    for (int s = 0; s < 32; ++s) s_len[288 + s] = 5;
+                    act = A_BUILD;
+                    x0 = 288;
+                    x1 = 32 | 1u << 16;
+                } else if (type == 2) {  // dynamic codes
+                    need(14);
+                    const int hlit = (int)(bb & 31u) + 257, hdist = (int)((bb >> 5) & 31u) + 1,
+                              hclen = (int)((bb >> 10) & 15u) + 4;
+                    drop(14);
+                    if (hlit > 286 || hdist > 30) err = GZ_E_CODES;
+                    uint8_t *cl = s_len + NSYM;
+                    for (int i = 0; i < 19; ++i) cl[i] = 0;
+                    for (int i = 0; i < hclen && !err; ++i) {
+                        need(3);
+                        cl[c_cl_order[i]] = (uint8_t)(bb & 7u);
+                        drop(3);
+                    }
+                    // code-length code: complete, <= 7 bits; its 128-entry table in s_dst
+                    uint16_t cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0}, next[8];
+                    for (int i = 0; i < 19; ++i) ++cnt[cl[i]];
+                    int left = 1;
+                    for (int l = 1; l < 8; ++l) left = (left << 1) - cnt[l];
+                    if (!err && left != 0) err = GZ_E_CODES;  // over-subscribed or incomplete (or empty)
+                    if (!err) {
+                        uint32_t code = 0;
+                        cnt[0] = 0;
+                        for (int l = 1; l < 8; ++l) {
+                            code = (code + cnt[l - 1]) << 1;
+                            next[l] = (uint16_t)code;
+                        }
+                        for (int s = 0; s < 19; ++s)
+                            if (cl[s]) {
+                                const int l = cl[s];
+                                const uint32_t r = __builtin_bitreverse32((uint32_t)next[l]++) >> (32 - l);
+                                for (uint32_t i = r; i < 128; i += 1u << l) s_dst[i] = (uint32_t)l | (uint32_t)s << 16;
+                            }
+                        const int total = hlit + hdist;
+                        int i = 0;
+                        while (i < total && !err) {
+                            need(14);
+                            const uint32_t e = s_dst[bb & 127u];
+                            const int sym = (int)(e >> 16);
+                            drop((int)(e & 15u));
+                            if (sym < 16) {
+                                s_len[i++] = (uint8_t)sym;
+                                continue;
+                            }
+                            int rep;
+                            uint8_t v = 0;
+                            if (sym == 16) {
+                                if (i == 0) { err = GZ_E_CODES; break; }
+                                v = s_len[i - 1];
+                                rep = 3 + (int)(bb & 3u);
+                                drop(2);
+                            } else if (sym == 17) {
+                                rep = 3 + (int)(bb & 7u);
+                                drop(3);
+                            } else {
+                                rep = 11 + (int)(bb & 127u);
+                                drop(7);
+                            }
+                            if (i + rep > total) { err = GZ_E_CODES; break; }
+                            while (rep--) s_len[i++] = v;
+                        }
+                        if (!err && s_len[256] == 0) err = GZ_E_CODES;  // missing end-of-block code
+                    }
+                    if (!err) {
+                        act = A_BUILD;
+                        x0 = (uint32_t)hlit;
+                        x1 = (uint32_t)hdist;
+                    }
+                } else {
+                    err = GZ_E_BTYPE;
+                }
+                nbp = fill - (uint32_t)bc;
+            }
+            act = bfl(act);
+            x0 = bfl(x0);
+            x1 = bfl(x1);
+            final_seen = bfl(fin) != 0;
+            GZ_STAMP(1);
+            GZ_COUNT(1);
+            if (act == A_ERR) break;
+            if (act == A_STORED) {
+                const uint32_t start = x0, len = x1;
+                int32_t e2 = GZ_OK;
+                if ((uint64_t)start + len + 8 > mlen) e2 = GZ_E_TRUNC;
+                else if (produced + len > cap) e2 = GZ_E_OVER;
+                if (e2 != GZ_OK) {
+                    if (lane == 0) err = e2;
+                    break;
+                }
+                for (uint32_t i = (uint32_t)lane; i < len; i += 64) dst[produced + i] = in[ma + start + i];
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                produced += len;
+                restage(ma + start + len, 0);
+                continue;
+            }
+            // ---- A_BUILD: canonical codes by ballots, primary tables filled from registers ----
+            bp = bfl(nbp);
             const int nl = (int)x0, nd = (int)(x1 & 0xFFFFu);
             const bool fixed = (x1 >> 16) & 1u;
-            if (lane == 0) {
-                for (int t = 0; t < 2 && !err; ++t) {
-                    const int base = t ? nl : 0, cntn = t ? nd : nl;
-                    uint16_t cnt[16], next[16];
-                    for (int l = 0; l < 16; ++l) cnt[l] = 0;
-                    for (int s = 0; s < cntn; ++s) ++cnt[s_len[base + s]];
-                    cnt[0] = 0;
-                    int left = 1, mx = 0;
-                    for (int l = 1; l < 16; ++l) {
-                        left = (left << 1) - cnt[l];
-                        if (left < 0) break;
-                        if (cnt[l]) mx = l;
-                    }
-                    // over-subscribed; incomplete unless a single 1-bit code (zlib's inflate_table)
-                    if (!fixed && (left < 0 || (mx > 0 && left > 0 && mx != 1))) err = GZ_E_CODES;
-                    uint32_t code = 0, off = 0;
-                    uint16_t offs[16];
-                    for (int l = 1; l < 16; ++l) {
-                        code = (code + cnt[l - 1]) << 1;
-                        next[l] = (uint16_t)code;
-                        offs[l] = (uint16_t)off;
-                        off += cnt[l];
-                    }
-                    uint16_t *syms = s_sym + (t ? 288 : 0);
-                    for (int s = 0; s < cntn; ++s) {
-                        const int l = s_len[base + s];
-                        if (!l) continue;
-                        s_rc[base + s] = (uint16_t)(__builtin_bitreverse32((uint32_t)next[l]++) >> (32 - l));
-                        syms[offs[l]++] = (uint16_t)s;
-                    }
-                    for (int l = 0; l < 16; ++l) s_cnt[t][l] = cnt[l];
-                }
-                if (!err) in_block = true;
-            }
-            if (bfl((uint32_t)err) != GZ_OK) break;
             for (int i = lane; i < (1 << LB); i += 64) s_lit[i] = 0;
             for (int i = lane; i < (1 << DB); i += 64) s_dst[i] = 0;
             __syncthreads();
-            for (int s = lane; s < nl + nd; s += 64) {
-                const int t = s < nl ? 0 : 1, sym = t ? s - nl : s, l = s_len[s];
-                if (!l) continue;
-                const int bits = t ? DB : LB;
+            const uint64_t below = (1ull << lane) - 1ull;
+            bool bad_codes = false;  // wave-uniform (from ballots): loop exits must not depend on lane state
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                const int base = t ? nl : 0, cntn = t ? nd : nl, bits = t ? DB : LB;
                 uint32_t *tab = t ? s_dst : s_lit;
-                const uint32_t r = s_rc[s];
-                if (l <= bits) {
-                    const uint32_t e = sym_entry(t, sym, l);
-                    if (e)
-                        for (uint32_t i = r; i < (1u << bits); i += 1u << l) tab[i] = e;
-                } else {
-                    tab[r & ((1u << bits) - 1u)] = K_SLOW << 4;
+                uint32_t *sent = s_sent + (t ? 288 : 0);
+                uint32_t *lim = t ? limD : limL, *lbase = t ? baseD : baseL;
+                uint32_t lj[5];
+#pragma unroll
+                for (int j = 0; j < 5; ++j) lj[j] = 64 * j + lane < cntn ? s_len[base + 64 * j + lane] : 0u;
+                uint32_t count[16];
+                count[0] = 0;
+                int left = 1, mx = 0;
+                for (int l = 1; l < 16; ++l) {
+                    uint32_t c = 0;
+#pragma unroll
+                    for (int j = 0; j < 5; ++j) c += (uint32_t)__popcll(__ballot(lj[j] == (uint32_t)l));
+                    count[l] = c;
+                    left = (left << 1) - (int)c;
+                    if (left < 0) break;
+                    if (c) mx = l;
+                }
+                // over-subscribed; incomplete unless a single 1-bit code (zlib's inflate_table)
+                if (!fixed && (left < 0 || (mx > 0 && left > 0 && mx != 1))) {
+                    bad_codes = true;
+                    break;
+                }
+                uint32_t code = 0, off = 0;
+                for (int l = 1; l < 16; ++l) {
+                    code = (code + count[l - 1]) << 1;  // first code of length l
+                    if (l > 10) {
+                        lim[l - 11] = (code + count[l]) << (15 - l);
+                        lbase[l - 11] = off - code;
+                    }
+                    uint32_t run = 0;
+#pragma unroll
+                    for (int j = 0; j < 5; ++j) {
+                        const uint64_t b = __ballot(lj[j] == (uint32_t)l);
+                        if (lj[j] == (uint32_t)l) {
+                            const uint32_t rank = run + (uint32_t)__popcll(b & below);
+                            const int s = 64 * j + lane;
+                            const uint32_t e = sym_entry(t, s, l);
+                            sent[off + rank] = e;
+                            const uint32_t r = __builtin_bitreverse32(code + rank) >> (32 - l);
+                            if (l <= bits) {
+                                if (e)
+                                    for (uint32_t i = r; i < (1u << bits); i += 1u << l) tab[i] = e;
+                            } else {
+                                tab[r & ((1u << bits) - 1u)] = K_SLOW << 4;
+                            }
+                        }
+                        run += (uint32_t)__popcll(b);
+                    }
+                    off += count[l];
                 }
             }
-            __syncthreads();
-            continue;
-        }
-        if (act == A_STORED) {
-            const uint32_t start = x0, len = x1;
-            int32_t e2 = GZ_OK;
-            if ((uint64_t)start + len + 8 > mlen) e2 = GZ_E_TRUNC;
-            else if (produced + len > cap) e2 = GZ_E_OVER;
-            if (e2 != GZ_OK) {
-                if (lane == 0) err = e2;
+            if (bad_codes) {
+                if (lane == 0) err = GZ_E_CODES;
                 break;
             }
-            for (uint32_t i = (uint32_t)lane; i < len; i += 64) dst[produced + i] = in[ma + start + i];
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-            produced += len;
-            restage(ma + start + len);
+            __syncthreads();
+            in_block = true;
+            GZ_STAMP(2);
+            GZ_COUNT(2);
             continue;
         }
-        // ---- A_FLUSH: expand the matches, resolve them, store the batch ----
-        const uint32_t fnb = x0, fnm = x1 & 0xFFFFu;
-        __syncthreads();  // lane 0's batch and match list
-        for (uint32_t k = (uint32_t)lane; k < fnm; k += 64) {
-            const uint32_t pl = s_mpl[k], pos = pl & 0xFFFFu, len = pl >> 16;
+        // ---- Huffman tokens: two 64-bit windows of starts per pass ----
+        if (bp > 8u * IN_STAGE - 320u) restage(sbase + (bp >> 3), bp & 7u);
+        // The token that would start at bit `pos`: packed length | kind << 6 | output bytes << 8.
+        auto token = [&](uint32_t pos, uint32_t &dist, uint32_t &val) -> uint32_t {
+            const uint32_t a = pos >> 5, sh = pos & 31u;
+            const uint32_t w0 = s_in32[a], w1 = s_in32[a + 1], w2 = s_in32[a + 2];
+            const uint64_t x = (uint64_t)__builtin_amdgcn_alignbit(w1, w0, sh) |
+                               (uint64_t)__builtin_amdgcn_alignbit(w2, w1, sh) << 32;
+            uint32_t e = s_lit[x & ((1u << LB) - 1u)];
+            if (((e >> 4) & 3u) == K_SLOW) e = long_decode(x, limL, baseL, s_sent);
+            const uint32_t n1 = e & 15u, kind = (e >> 4) & 3u;
+            uint32_t tl = n1, ol = kind == K_EOB ? 0u : 1u;
+            dist = 0;
+            val = e >> 16;
+            if (n1 && kind == K_LEN) {
+                const uint32_t eb = (e >> 8) & 15u;
+                val += (uint32_t)(x >> n1) & ((1u << eb) - 1u);
+                const uint64_t y = x >> (n1 + eb);
+                uint32_t d = s_dst[y & ((1u << DB) - 1u)];
+                if (((d >> 4) & 3u) == K_SLOW) d = long_decode(y, limD, baseD, s_sent + 288);
+                const uint32_t n2 = d & 15u, db = (d >> 8) & 15u;
+                dist = (d >> 16) + ((uint32_t)(y >> n2) & ((1u << db) - 1u));
+                tl = n2 ? n1 + eb + n2 + db : 0u;
+                ol = val;
+            }
+            if (!tl) ol = 0;
+            const uint32_t stopbit = (tl == 0 || kind == K_EOB) ? 64u : 0u;  // the chain ends here
+            return tl | stopbit | kind << 7 | ol << 9;
+        };
+        uint32_t dist0, val0, dist1, val1;
+        const uint32_t pk0 = token(bp + (uint32_t)lane, dist0, val0);
+        const uint32_t pk1 = token(bp + 64u + (uint32_t)lane, dist1, val1);
+        GZ_STAMP(3);
+        // The real chain from bit bp: the scalar unit only follows the token
+        // lengths (v_readlane, add, bit set); the batch offsets, match slots and
+        // capacity cut are then found lane-parallel.
+        uint32_t q = 0;
+        uint64_t M0 = 0, M1 = 0;
+        bool stopped = false;
+        while (q < 64) {
+            const uint32_t info = (uint32_t)__builtin_amdgcn_readlane((int)pk0, (int)q);
+            M0 |= 1ull << q;
+            q += info & 63u;
+            if (info & 64u) { stopped = true; break; }
+        }
+        if (!stopped)
+            while (q < 128) {
+                const uint32_t info = (uint32_t)__builtin_amdgcn_readlane((int)pk1, (int)(q - 64));
+                M1 |= 1ull << (q - 64);
+                q += info & 63u;
+                if (info & 64u) { stopped = true; break; }
+            }
+        GZ_STAMP(7);
+        uint32_t stop = 0;  // 0 window done, 1 end of block, 2 batch full, 3 invalid code
+        if (stopped) {
+            const uint32_t last = M1 ? 127u - (uint32_t)__builtin_clzll(M1) : 63u - (uint32_t)__builtin_clzll(M0);
+            const uint32_t info = last < 64 ? (uint32_t)__builtin_amdgcn_readlane((int)pk0, (int)last)
+                                            : (uint32_t)__builtin_amdgcn_readlane((int)pk1, (int)(last - 64));
+            stop = (info & 63u) ? 1u : 3u;
+        }
+        const uint64_t below = (1ull << lane) - 1ull;
+        const uint32_t kind0 = (pk0 >> 7) & 3u, kind1 = (pk1 >> 7) & 3u;
+        uint32_t olen0 = ((M0 >> lane) & 1u) ? pk0 >> 9 : 0u, olen1 = ((M1 >> lane) & 1u) ? pk1 >> 9 : 0u;
+        const uint32_t inc0 = wave_incl_sum(olen0);
+        const uint32_t tot0 = (uint32_t)__builtin_amdgcn_readlane((int)inc0, 63);
+        const uint32_t inc1 = wave_incl_sum(olen1) + tot0;
+        const uint64_t mb0 = __ballot(((M0 >> lane) & 1u) && kind0 == K_LEN && olen0);
+        const uint64_t mb1 = __ballot(((M1 >> lane) & 1u) && kind1 == K_LEN && olen1);
+        const uint32_t mr0 = (uint32_t)__popcll(mb0 & below), mr1 = (uint32_t)__popcll(mb0) + (uint32_t)__popcll(mb1 & below);
+        const int opos0 = (int)(nb + inc0 - olen0), opos1 = (int)(nb + inc1 - olen1);
+        const int midx0 = (int)(nm + mr0), midx1 = (int)(nm + mr1);
+        // batch capacity: the first chain token that does not fit ends this pass before it
+        const uint64_t fb0 = __ballot(olen0 && (nb + inc0 > (uint32_t)OBUF || (kind0 == K_LEN && nm + mr0 >= (uint32_t)MLCAP)));
+        const uint64_t fb1 = __ballot(olen1 && (nb + inc1 > (uint32_t)OBUF || (kind1 == K_LEN && nm + mr1 >= (uint32_t)MLCAP)));
+        uint32_t acc = (uint32_t)__builtin_amdgcn_readlane((int)inc1, 63);
+        if (fb0 | fb1) {
+            const uint32_t first = fb0 ? (uint32_t)__builtin_ctzll(fb0) : 64u + (uint32_t)__builtin_ctzll(fb1);
+            if (first < 64) {
+                M0 &= (1ull << first) - 1ull;
+                M1 = 0;
+                acc = (uint32_t)__builtin_amdgcn_readlane(opos0, (int)first) - nb;
+            } else {
+                M1 &= (1ull << (first - 64)) - 1ull;
+                acc = (uint32_t)__builtin_amdgcn_readlane(opos1, (int)(first - 64)) - nb;
+            }
+            q = first;
+            stop = 2;
+            olen0 = ((M0 >> lane) & 1u) ? olen0 : 0u;
+            olen1 = ((M1 >> lane) & 1u) ? olen1 : 0u;
+        }
+        if (stop == 3) {  // an invalid code on the chain
+            if (lane == 0) err = GZ_E_CODE;
+            break;
+        }
+        const uint32_t nmat = (uint32_t)__popcll(mb0 & M0) + (uint32_t)__popcll(mb1 & M1);
+        const bool on0 = olen0 != 0, on1 = olen1 != 0;  // chain tokens with output (not end of block)
+        int32_t bad = GZ_OK;
+        if (on0 && kind0 == K_LEN && dist0 > produced + (uint32_t)opos0) bad = GZ_E_FAR;
+        else if (on0 && produced + (uint32_t)opos0 + olen0 > cap) bad = GZ_E_OVER;
+        else if (on1 && kind1 == K_LEN && dist1 > produced + (uint32_t)opos1) bad = GZ_E_FAR;
+        else if (on1 && produced + (uint32_t)opos1 + olen1 > cap) bad = GZ_E_OVER;
+        const uint64_t badm = __ballot(bad != GZ_OK);
+        if (badm) {
+            const int32_t b0 = __builtin_amdgcn_readlane(bad, (int)__builtin_ctzll(badm));
+            if (lane == 0) err = b0;
+            break;
+        }
+        if (on0 && kind0 == K_LIT) {
+            s_ob[opos0] = (uint8_t)val0;
+            s_ref[opos0] = 0;
+        } else if (on0 && kind0 == K_LEN) {
+            s_mpl[midx0] = (uint32_t)opos0 | val0 << 16;
+            s_md[midx0] = (uint16_t)dist0;
+        }
+        if (on1 && kind1 == K_LIT) {
+            s_ob[opos1] = (uint8_t)val1;
+            s_ref[opos1] = 0;
+        } else if (on1 && kind1 == K_LEN) {
+            s_mpl[midx1] = (uint32_t)opos1 | val1 << 16;
+            s_md[midx1] = (uint16_t)dist1;
+        }
+        nb = bfl(nb + acc);  // (readfirstlane: the batch state stays in SGPRs)
+        nm = bfl(nm + nmat);
+        bp = bfl(bp + q);
+        if (sbase + (bp >> 3) > mz) {  // consumed past the member: truncated
+            if (lane == 0) err = GZ_E_TRUNC;
+            break;
+        }
+        if (stop == 1) in_block = false;
+        GZ_STAMP(1);
+        GZ_COUNT(3);
+        if (stop == 0 || nb == 0) continue;
+        // ---- flush: expand the matches, resolve them, store the batch ----
+        __syncthreads();
+        for (uint32_t k = (uint32_t)lane; k < nm; k += 64) {
+            const uint32_t pl = s_mpl[k], mp = pl & 0xFFFFu, len = pl >> 16;
             const uint16_t d = s_md[k];
-            for (uint32_t i = 0; i < len; ++i) s_ref[pos + i] = d;
+            for (uint32_t i = 0; i < len; ++i) s_ref[mp + i] = d;
         }
         __syncthreads();
-        if (fnm) {
+        GZ_STAMP(4);
+        GZ_COUNT(4);
+        if (nm) {
             for (;;) {
                 bool more = false;
-                for (uint32_t q = (uint32_t)lane; q < fnb; q += 64) {
-                    const uint32_t d = s_ref[q];
-                    if (!d) continue;
-                    const int src = (int)q - (int)d;
-                    uint32_t v;
-                    if (src < 0) {
-                        v = dst[(int64_t)produced + src];  // history: an earlier batch (distance checked)
-                    } else {
-                        const uint32_t d2 = s_ref[src];
-                        if (d2) {  // the source is itself a copy: follow it
-                            s_ref[q] = (uint16_t)(d + d2);
-                            more = true;
-                            continue;
-                        }
-                        v = s_ob[src];
+                for (uint32_t b0 = 0; b0 < nb; b0 += 64 * 8) {
+                    uint32_t d[8], v[8];
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        const uint32_t qq = b0 + (uint32_t)lane + 64u * j;
+                        d[j] = qq < nb ? (uint32_t)s_ref[qq] : 0u;
                     }
-                    s_ob[q] = (uint8_t)v;
-                    s_ref[q] = 0;
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {  // history sources: all loads in flight
+                        const int src = (int)(b0 + (uint32_t)lane + 64u * j) - (int)d[j];
+                        v[j] = d[j] && src < 0 ? (uint32_t)dst[(int64_t)produced + src] : 0u;
+                    }
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        if (!d[j]) continue;
+                        const uint32_t qq = b0 + (uint32_t)lane + 64u * j;
+                        const int src = (int)qq - (int)d[j];
+                        if (src >= 0) {
+                            const uint32_t d2 = s_ref[src];
+                            if (d2) {  // the source is itself a copy: follow it
+                                s_ref[qq] = (uint16_t)(d[j] + d2);
+                                more = true;
+                                continue;
+                            }
+                            v[j] = s_ob[src];
+                        }
+                        s_ob[qq] = (uint8_t)v[j];
+                        s_ref[qq] = 0;
+                    }
                 }
                 __syncthreads();
+                GZ_COUNT(5);
                 if (!__any(more)) break;
             }
         }
-        for (uint32_t q = (uint32_t)lane; q < fnb; q += 64) dst[produced + q] = s_ob[q];
+        GZ_STAMP(5);
+        for (uint32_t qq = (uint32_t)lane; qq < nb; qq += 64) dst[produced + qq] = s_ob[qq];
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         __syncthreads();
-        produced += fnb;
-        if (lane == 0) {
-            nb = 0;
-            nm = 0;
-        }
-        if ((x1 >> 17) & 1u) {
-            const uint64_t abs = (uint64_t)bfl((uint32_t)(sbase + (uint64_t)ip - ma)) + ma;
-            restage(abs);
-        }
+        produced += nb;
+        nb = 0;
+        nm = 0;
+        GZ_STAMP(6);
+        GZ_COUNT(6);
     }
     // ---- trailer ----
     if (lane == 0) {
         if (!err) {
-            drop(bc & 7);
-            const uint64_t t = sbase + (uint64_t)ip - (uint64_t)(bc >> 3);  // absolute
+            const uint64_t t = sbase + ((bp + 7u) >> 3);  // absolute
             if (t + 8 > mz) err = GZ_E_TRUNC;
             else if (t + 8 != mz) err = GZ_E_TRAIL;  // bytes after the member's trailer
             else {

@@ -1212,6 +1212,9 @@ int sdl_gzip_inflate_device(sdl_batcher *h, const uint8_t *d_gz, uint64_t gz_len
             HIP_TRY(launch_gz_crc(h->z_off.p, h->z_out.p, n_members, h->z_tcrc.p, x2n, h->z_status.p, h->z_bad.p, st));
             HIP_TRY(hipMemcpyAsync(bad, h->z_bad.p, sizeof(bad), hipMemcpyDeviceToHost, st));
             HIP_TRY(hipStreamSynchronize(st));
+#ifdef SDL_STAMPS
+            print_gz_cycles();
+#endif
         }
         std::memset(out, 0, sizeof(*out));
         out->d_out = h->z_out.p;
