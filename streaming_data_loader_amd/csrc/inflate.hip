@@ -16,7 +16,7 @@
 //               jumping (a byte copied from an earlier byte of the same batch
 //               follows that byte's own source, so overlapping copies resolve in
 //               log(depth) rounds) and stores the batch.  Compressed bytes are
-//               staged in LDS 2 KiB at a time by 16-B loads of all lanes.
+//               staged in LDS 1 KiB at a time by 16-B loads of all lanes.
 //   k_gz_crc    one wave per member: CRC-32 of 64 lane segments (LDS table),
 //               folded with crc32_combine's x^(8n) mod P shift, against the
 //               trailer's CRC.
@@ -39,10 +39,17 @@
 namespace sdl {
 namespace {
 
-constexpr int LB = 10, DB = 10;    // primary table bits: lit/len, dist
-constexpr int IN_STAGE = 2048;     // staged compressed bytes per wave
-constexpr int OBUF = 2048;         // output batch bytes
-constexpr int MLCAP = 256;         // matches per batch
+constexpr int LB = 10, DB = 10;    // primary table bits: lit/len, dist (long_decode covers 11..15)
+#ifndef SDL_GZ_STAGE
+#define SDL_GZ_STAGE 1024
+#endif
+#ifndef SDL_GZ_OBUF
+#define SDL_GZ_OBUF 512
+#endif
+constexpr int IN_STAGE = SDL_GZ_STAGE;  // staged compressed bytes per wave
+constexpr int OBUF = SDL_GZ_OBUF;       // output batch bytes
+constexpr int MLCAP = OBUF / 8;         // matches per batch
+static_assert(OBUF >= 512, "a batch must take any 258-byte match (else an empty batch never fills: no progress)");
 constexpr int HDR_ROOM = 640;      // a block header (<= ~600 B) fits in this many staged bytes
 constexpr int NSYM = 320;          // lit/len (<= 288) + dist (<= 32) code lengths
 constexpr uint32_t POLY = 0xEDB88320u;
