@@ -9,7 +9,23 @@ namespace sdl {
 
 __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
 
-// Inclusive wave64 prefix sum (6 shuffle steps).
+// Inclusive wave64 prefix sum in six DPP steps (the GFX9 wave scan): row_shr
+// 1, 2, 4, 8 within each 16-lane row (lanes without a source add 0), then
+// row_bcast:15 adds row 0's total to row 1 and row 2's to row 3, and
+// row_bcast:31 adds lane 31's running total to rows 2 and 3.  DPP moves data
+// inside the VALU -- no ds_bpermute round trip through the LDS crossbar per step.
+#ifndef SDL_SCAN_SHFL
+__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t x) {
+    int v = (int)x;
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, false);  // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, false);  // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, false);  // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, false);  // row_shr:8
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
+    return (uint32_t)v;
+}
+#else  // (diagnostic A/B) six ds_bpermute shuffle steps
 __device__ __forceinline__ uint32_t wave_incl_sum(uint32_t x) {
     const int lane = lane_id();
 #pragma unroll
@@ -19,6 +35,7 @@ __device__ __forceinline__ uint32_t wave_incl_sum(uint32_t x) {
     }
     return x;
 }
+#endif
 
 // Exclusive prefix sum over a workgroup of NT threads; *total = sum of all.
 // `scratch` needs NT/64 words.  Contains two barriers.
