@@ -9,6 +9,30 @@ namespace sdl {
 
 __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
 
+// Value of lane l (l wave-uniform) in every lane: v_readlane into a scalar
+// register, no ds_bpermute round trip.
+template <class T>
+__device__ __forceinline__ T lane_bcast(T x, int l) {
+    return (T)__builtin_amdgcn_readlane((int)x, l);
+}
+
+// DPP data movement for the wave scans below: lanes without a source (or rows
+// outside row_mask) read 0, the identity of every scan here.
+#define SDL_DPP(v, ctrl, rows) ((uint32_t)__builtin_amdgcn_update_dpp(0, (int)(v), (ctrl), (rows), 0xF, false))
+// Inclusive wave64 scan of an associative op with identity 0 in six DPP steps.
+#define SDL_DPP_SCAN(v, COMBINE)                          \
+    do {                                                  \
+        uint32_t y_;                                      \
+        y_ = SDL_DPP(v, 0x111, 0xF); v = COMBINE(y_, v);  \
+        y_ = SDL_DPP(v, 0x112, 0xF); v = COMBINE(y_, v);  \
+        y_ = SDL_DPP(v, 0x114, 0xF); v = COMBINE(y_, v);  \
+        y_ = SDL_DPP(v, 0x118, 0xF); v = COMBINE(y_, v);  \
+        y_ = SDL_DPP(v, 0x142, 0xA); v = COMBINE(y_, v);  \
+        y_ = SDL_DPP(v, 0x143, 0xC); v = COMBINE(y_, v);  \
+    } while (0)
+// previous lane's value (lane 0: 0): DPP wave_shr:1
+__device__ __forceinline__ uint32_t wave_prev(uint32_t v) { return SDL_DPP(v, 0x138, 0xF); }
+
 // Inclusive wave64 prefix sum in six DPP steps (the GFX9 wave scan): row_shr
 // 1, 2, 4, 8 within each 16-lane row (lanes without a source add 0), then
 // row_bcast:15 adds row 0's total to row 1 and row 2's to row 3, and
@@ -64,14 +88,9 @@ __device__ __forceinline__ uint32_t last_set(uint32_t a, uint32_t b) { return (b
 template <int NT>
 __device__ __forceinline__ uint32_t block_excl_last_scan(uint32_t v, uint32_t *scratch) {
     const int lane = lane_id(), wid = (int)(threadIdx.x >> 6);
-    uint32_t x = v;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        uint32_t y = __shfl_up(x, d, 64);
-        if (lane >= d) x = last_set(y, x);
-    }
-    uint32_t ex = __shfl_up(x, 1, 64);
-    if (lane == 0) ex = 0;
+    uint32_t x = v;  // (0 = pass-through: the DPP scan's identity)
+    SDL_DPP_SCAN(x, last_set);
+    const uint32_t ex = wave_prev(x);
     if (lane == 63) scratch[wid] = x;
     __syncthreads();
     uint32_t carry = 0;

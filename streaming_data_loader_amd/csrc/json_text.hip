@@ -428,23 +428,13 @@ __device__ __forceinline__ JMask jmask(const uint4 &x, int64_t p0, int64_t s, in
 // Exclusive "last set wins" scan over the wave: x = 0x100 | bit sets the carry,
 // 0 passes through; returns the carry before this lane (0 if none).
 __device__ __forceinline__ uint32_t wave_excl_last(uint32_t x) {
-    const int lane = lane_id();
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_up(x, d, 64);
-        if (lane >= d) x = (x & 0x100u) ? x : y;
-    }
-    uint32_t ex = __shfl_up(x, 1, 64);
-    return lane == 0 ? 0u : ex;
+    SDL_DPP_SCAN(x, last_set);  // (DPP steps, device_util.hpp)
+    return wave_prev(x);
 }
+__device__ __forceinline__ uint32_t xor_op(uint32_t a, uint32_t b) { return a ^ b; }
 __device__ __forceinline__ uint32_t wave_excl_xor(uint32_t x) {
-    const int lane = lane_id();
     uint32_t v = x;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_up(v, d, 64);
-        if (lane >= d) v ^= y;
-    }
+    SDL_DPP_SCAN(v, xor_op);
     return v ^ x;
 }
 
@@ -591,8 +581,8 @@ __global__ __launch_bounds__(64) void k_json_parse_long(const uint8_t *__restric
             const int64_t pn = b0 + CHUNK;
             uint4 nxt = make_uint4(0, 0, 0, 0);
             if (lane == 0 && pn < e) nxt = *reinterpret_cast<const uint4 *>(buf + pn);
-            const uint4 pv = make_uint4(__shfl(prev.x, 63, 64), __shfl(prev.y, 63, 64), __shfl(prev.z, 63, 64),
-                                        __shfl(prev.w, 63, 64));
+            const uint4 pv = make_uint4(lane_bcast(prev.x, 63), lane_bcast(prev.y, 63), lane_bcast(prev.z, 63),
+                                        lane_bcast(prev.w, 63));
             __syncthreads();  // the previous step's readers are done with the window and lists
             *reinterpret_cast<uint4 *>(s_win + JW_PRE + 16 * lane) = x;
             if (lane == 0) {
@@ -606,7 +596,7 @@ __global__ __launch_bounds__(64) void k_json_parse_long(const uint8_t *__restric
             uint32_t E;
             const uint32_t par_in = esc_carry_in(m.b, m.v, esc_par);
             const uint32_t par_out = esc_mask(m.b, m.v, par_in, &E);
-            esc_par = __shfl(par_out, 63, 64);
+            esc_par = lane_bcast(par_out, 63);
             const uint32_t uq = m.q & ~E;
             // in-string mask: bit k = inside a string just before byte k
             const uint32_t sp = wave_excl_xor((uint32_t)__builtin_popcount(uq) & 1u) ^ str_par;
@@ -616,7 +606,7 @@ __global__ __launch_bounds__(64) void k_json_parse_long(const uint8_t *__restric
                 ins |= par << k;
                 par ^= (uq >> k) & 1u;
             }
-            str_par = __shfl(par, 63, 64);
+            str_par = lane_bcast(par, 63);
             const uint32_t ct = ins & ~uq & m.v;  // string content bytes
             const int lim = (int)((e - b0) < (int64_t)(CHUNK + 16) ? (e - b0) : (int64_t)(CHUNK + 16)) + JW_PRE;
             const uint8_t *w = s_win;
@@ -672,15 +662,15 @@ __global__ __launch_bounds__(64) void k_json_parse_long(const uint8_t *__restric
                 dl_pre[k] = dsum;
                 dsum += dl;
             }
-            spill = __shfl((uint32_t)skip, 63, 64);  // into the next step's lane 0
+            spill = lane_bcast((uint32_t)skip, 63);  // into the next step's lane 0
             // decoded-length prefix at every byte
             const uint32_t dex = wave_incl_sum(dsum) - dsum + D;
-            D = __shfl(dex + dsum, 63, 64);
+            D = lane_bcast(dex + dsum, 63);
             // tokens: quotes and non-ws bytes outside strings
             const uint32_t tk = m.v & (uq | (~ins & ~m.w));
             const uint32_t nt_l = (uint32_t)__builtin_popcount(tk);
             const uint32_t tb = wave_incl_sum(nt_l) - nt_l;
-            const uint32_t ntok = __shfl(tb + nt_l, 63, 64);
+            const uint32_t ntok = lane_bcast(tb + nt_l, 63);
             {
                 uint32_t at = tb;
 #pragma unroll
@@ -864,7 +854,7 @@ __global__ __launch_bounds__(64) void k_json_write_long(const uint8_t *__restric
             uint32_t E;
             const uint32_t par_in = esc_carry_in(m.b, m.v, esc_par);
             const uint32_t par_out = esc_mask(m.b, m.v, par_in, &E);
-            esc_par = __shfl(par_out, 63, 64);
+            esc_par = lane_bcast(par_out, 63);
             const int lim = (int)((e - b0) < (int64_t)(CHUNK + 16) ? (e - b0) : (int64_t)(CHUNK + 16)) + JW_PRE;
             const uint8_t *w = s_win;
             const int wi0 = JW_PRE + 16 * lane;
@@ -893,8 +883,8 @@ __global__ __launch_bounds__(64) void k_json_write_long(const uint8_t *__restric
                 sk_end = sk;
             }
             const uint32_t at = wave_incl_sum(cnt) - cnt + O;
-            O = __shfl(at + cnt, 63, 64);
-            const uint32_t sp_last = __shfl((uint32_t)sk_end, 63, 64);
+            O = lane_bcast(at + cnt, 63);
+            const uint32_t sp_last = lane_bcast((uint32_t)sk_end, 63);
             // pass 2: write
             {
                 uint32_t q = at;

@@ -250,7 +250,7 @@ __global__ __launch_bounds__(256) void k_compact_tokens(const uint32_t *__restri
                 for (uint32_t j = 0; j < L.k; ++j) dst[at + j] = long_scratch[L.pos + j];
             }
         }
-        written += (uint32_t)__shfl((int)incl, 63, 64);
+        written += (uint32_t)lane_bcast((int)incl, 63);
     }
 }
 
@@ -845,8 +845,8 @@ __global__ __launch_bounds__(256) void k_rows_span(RowParams P, const uint32_t *
                 ap_end = __shfl(ap_end, Pl, 64);
                 break;
             }
-            I0 += (int)__shfl((int)incl, 63, 64);
-            A0 += (int)__shfl((int)incl_s, 63, 64);
+            I0 += (int)lane_bcast((int)incl, 63);
+            A0 += (int)lane_bcast((int)incl_s, 63);
         }
         for (int j = lp_end + lane; j < S; j += 64) ids_o[j] = 0;
         for (int j = ap_end + 1 + lane; j < LW; j += 64) lb_o[j] = -100;

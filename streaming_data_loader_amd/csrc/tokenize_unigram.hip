@@ -926,8 +926,8 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
             s_job_tb[j] = (uint16_t)(carry + incl - t);
             s_job_rb[j] = (uint16_t)(rcarry + rincl - rw);
         }
-        carry += (uint32_t)__shfl((int)incl, 63, 64);
-        rcarry += (uint32_t)__shfl((int)rincl, 63, 64);
+        carry += (uint32_t)lane_bcast((int)incl, 63);
+        rcarry += (uint32_t)lane_bcast((int)rincl, 63);
     }
     if (lane == 0) {
         s_job_tb[nj] = (uint16_t)carry;

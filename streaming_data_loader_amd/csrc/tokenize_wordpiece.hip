@@ -785,7 +785,7 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
                 const int leader = __builtin_ctzll(pm);
                 uint32_t base = 0;
                 if (lane == leader) base = atomicAdd(&s_scratch[TOK_THREADS / 64 + 1], (uint32_t)__popcll(pm));
-                base = __shfl(base, leader, 64);
+                base = lane_bcast(base, leader);
                 if (pend[u]) s_pend[base + __popcll(pm & ((1ull << lane) - 1ull))] = (uint16_t)pi;
             }
         }
@@ -816,7 +816,7 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
                 const int leader = __builtin_ctzll(nm);
                 uint32_t base = 0;
                 if (lane == leader) base = atomicAdd(&s_scratch[TOK_THREADS / 64 + 1], (uint32_t)__popcll(nm));
-                base = __shfl(base, leader, 64);
+                base = lane_bcast(base, leader);
                 if (need) {
                     const int q = (int)base + __popcll(nm & ((1ull << lane) - 1ull));
                     if (q >= npend) {
