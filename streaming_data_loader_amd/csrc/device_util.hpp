@@ -30,6 +30,21 @@ __device__ __forceinline__ T lane_bcast(T x, int l) {
         y_ = SDL_DPP(v, 0x142, 0xA); v = COMBINE(y_, v);  \
         y_ = SDL_DPP(v, 0x143, 0xC); v = COMBINE(y_, v);  \
     } while (0)
+// The same with identity `id` (DPP lanes without a source read `id`).
+#define SDL_DPP_ID(v, ctrl, rows, id) \
+    ((uint32_t)__builtin_amdgcn_update_dpp((int)(id), (int)(v), (ctrl), (rows), 0xF, false))
+#define SDL_DPP_SCAN_ID(v, COMBINE, id)                              \
+    do {                                                             \
+        uint32_t y_;                                                 \
+        y_ = SDL_DPP_ID(v, 0x111, 0xF, id); v = COMBINE(y_, v);      \
+        y_ = SDL_DPP_ID(v, 0x112, 0xF, id); v = COMBINE(y_, v);      \
+        y_ = SDL_DPP_ID(v, 0x114, 0xF, id); v = COMBINE(y_, v);      \
+        y_ = SDL_DPP_ID(v, 0x118, 0xF, id); v = COMBINE(y_, v);      \
+        y_ = SDL_DPP_ID(v, 0x142, 0xA, id); v = COMBINE(y_, v);      \
+        y_ = SDL_DPP_ID(v, 0x143, 0xC, id); v = COMBINE(y_, v);      \
+    } while (0)
+// next lane's value (lane 63: 0): DPP wave_shl:1
+__device__ __forceinline__ uint32_t wave_next(uint32_t v) { return SDL_DPP(v, 0x130, 0xF); }
 // previous lane's value (lane 0: 0): DPP wave_shr:1
 __device__ __forceinline__ uint32_t wave_prev(uint32_t v) { return SDL_DPP(v, 0x138, 0xF); }
 

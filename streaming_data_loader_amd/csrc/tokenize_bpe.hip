@@ -85,13 +85,17 @@ __device__ __forceinline__ uint32_t merge_val(const DevTok &T, uint32_t a, uint3
     return 0xFFFFFFFFu;
 }
 
+__device__ __forceinline__ uint32_t min_u32(uint32_t a, uint32_t b) { return a < b ? a : b; }
+// wave minimum: a DPP min-scan, lane 63's total read back (no ds_bpermute steps)
 __device__ __forceinline__ uint32_t wave_min_u32(uint32_t x) {
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) {
-        const uint32_t y = (uint32_t)__shfl_xor((int)x, d, 64);
-        x = y < x ? y : x;
-    }
-    return x;
+    SDL_DPP_SCAN_ID(x, min_u32, 0xFFFFFFFFu);
+    return lane_bcast(x, 63);
+}
+// segmented min-scan operator on (head flag << 16 | rank <= 0xFFFF): a head
+// starts a new segment (its own value stands), else the running min carries
+// and so does "a head was seen"
+__device__ __forceinline__ uint32_t seg_min(uint32_t a, uint32_t b) {
+    return (b & 0x10000u) ? b : ((a & 0x10000u) | min_u32(a & 0xFFFFu, b & 0xFFFFu));
 }
 
 // Of the candidate pairs in m (bit j = pair (j, j+1)), those merged left to
@@ -262,7 +266,7 @@ __device__ int bpe_wave(const DevTok &T, uint32_t &sym, int n, lds_u16 *tmp) {
     const int lane = lane_id();
     const uint64_t lt = (1ull << lane) - 1ull;
     while (n > 1) {
-        const uint32_t nxt = (uint32_t)__shfl_down((int)sym, 1, 64);
+        const uint32_t nxt = wave_next(sym);
         const uint32_t v = lane < n - 1 ? merge_val(T, sym, nxt) : 0xFFFFFFFFu;
         const uint32_t rank = v >> 16;
         const uint32_t rmin = wave_min_u32(rank);
@@ -292,22 +296,14 @@ __device__ int bpe_wave_seg(const DevTok &T, uint32_t &sym, int n, uint64_t &hea
     const int lane = lane_id();
     const uint64_t lt = (1ull << lane) - 1ull;
     for (;;) {
-        const uint32_t nxt = (uint32_t)__shfl_down((int)sym, 1, 64);
+        const uint32_t nxt = wave_next(sym);
         const bool pair = lane < n - 1 && !((heads >> (lane + 1)) & 1ull);
         const uint32_t v = pair ? merge_val(T, sym, nxt) : 0xFFFFFFFFu;
         const uint32_t rank = v >> 16;
-        // segmented inclusive min scan, then each lane takes its word's last value
-        uint32_t x = rank;
-        bool f = (heads >> lane) & 1ull;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t y = (uint32_t)__shfl_up((int)x, d, 64);
-            const bool fy = __shfl_up(f ? 1 : 0, d, 64) != 0;
-            if (lane >= d) {
-                if (!f) x = y < x ? y : x;
-                f = f || fy;
-            }
-        }
+        // segmented inclusive min scan (DPP), then each lane takes its word's last value
+        uint32_t x = rank | ((uint32_t)((heads >> lane) & 1ull) << 16);
+        SDL_DPP_SCAN_ID(x, seg_min, 0xFFFFu);
+        x &= 0xFFFFu;
         const uint64_t after = lane == 63 ? 0ull : heads & ~((2ull << lane) - 1ull);
         const int last = after ? __builtin_ctzll(after) - 1 : n - 1;
         const uint32_t rmin = (uint32_t)__shfl((int)x, last < 0 ? 0 : last, 64);
