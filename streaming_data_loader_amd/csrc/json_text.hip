@@ -541,7 +541,7 @@ __device__ __forceinline__ int lane_skip_in(const uint8_t *w, int wi0, uint32_t 
     uint32_t in = lane == 0 ? carry : 0u;
     for (;;) {
         const uint32_t so = lane_spill(w, wi0, ct, b, lim, (int)in);
-        uint32_t ni = __shfl_up(so, 1, 64);
+        uint32_t ni = wave_prev(so);
         if (lane == 0) ni = carry;
         if (!__any(ni != in)) break;
         in = ni;

@@ -921,7 +921,7 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
 #pragma unroll
                 for (int j = 1; j < PEND_CAP / 64; ++j)
                     if ((d >> 6) == j) mine = dl[j];
-                const int dpi = __shfl((int)mine, d & 63, 64);
+                const int dpi = lane_bcast((int)mine, d & 63);
                 const int dprel = (int)(s_pieces[dpi] & 0xFFFu);
                 const int64_t dp = c0 + dprel;
                 lds_u16 *dout = stage + dprel;
@@ -940,7 +940,7 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
                         for (int k = dL; k < dL + 20; ++k) wb[k] = 0;
                     }
                 }
-                dL = __shfl(dL, 0, 64);
+                dL = lane_bcast(dL, 0);
                 if (dL == 0) continue;  // wave-uniform
                 for (int k = lane; k < dL; k += 64) best[k] = 0u;
                 __syncthreads();
