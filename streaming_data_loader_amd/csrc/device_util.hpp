@@ -82,6 +82,14 @@ template <int NT>
 __device__ __forceinline__ uint32_t block_excl_sum(uint32_t v, uint32_t *total, uint32_t *scratch) {
     const int lane = lane_id(), wid = (int)(threadIdx.x >> 6);
     uint32_t x = wave_incl_sum(v);
+    if constexpr (NT == 64) {  // one-wave blocks: the total is lane 63's (no LDS round trip);
+        (void)lane;              // one barrier is kept -- callers rely on it to order their
+        (void)wid;               // LDS writes before other lanes' reads
+        (void)scratch;
+        *total = lane_bcast(x, 63);
+        __syncthreads();
+        return x - v;
+    }
     if (lane == 63) scratch[wid] = x;
     __syncthreads();
     uint32_t wbase = 0, tot = 0;
@@ -106,6 +114,13 @@ __device__ __forceinline__ uint32_t block_excl_last_scan(uint32_t v, uint32_t *s
     uint32_t x = v;  // (0 = pass-through: the DPP scan's identity)
     SDL_DPP_SCAN(x, last_set);
     const uint32_t ex = wave_prev(x);
+    if constexpr (NT == 64) {  // one wave: nothing carries in (one barrier kept, as above)
+        (void)lane;
+        (void)wid;
+        (void)scratch;
+        __syncthreads();
+        return ex;
+    }
     if (lane == 63) scratch[wid] = x;
     __syncthreads();
     uint32_t carry = 0;
