@@ -292,7 +292,7 @@ __device__ int bpe_wave(const DevTok &T, uint32_t &sym, int n, lds_u16 *tmp) {
 // right.  Pairs never straddle a word, so the runs of candidate bits do not
 // either and one leftmost_alternating serves every word.  Returns the final
 // symbol count; `heads` then marks where each word's ids start.
-__device__ int bpe_wave_seg(const DevTok &T, uint32_t &sym, int n, uint64_t &heads, lds_u16 *tmp) {
+__device__ int bpe_wave_seg(const DevTok &T, uint32_t &sym, int n, uint64_t &heads, lds_u32 *tmp) {
     const int lane = lane_id();
     const uint64_t lt = (1ull << lane) - 1ull;
     for (;;) {
@@ -312,13 +312,14 @@ __device__ int bpe_wave_seg(const DevTok &T, uint32_t &sym, int n, uint64_t &hea
         const uint64_t sel = leftmost_alternating(cand, false);
         if ((sel >> lane) & 1ull) sym = v & 0xFFFFu;
         const uint64_t live = (n == 64 ? ~0ull : ((1ull << n) - 1ull)) & ~(sel << 1);
-        if ((live >> lane) & 1ull) tmp[__popcll(live & lt)] = (uint16_t)sym;
-        uint64_t nh = 0;  // heads survive every step: their new positions
-        for (uint64_t m = heads; m; m &= m - 1) nh |= 1ull << __popcll(live & ((1ull << __builtin_ctzll(m)) - 1ull));
-        heads = nh;
+        // heads are never merged away (no pair straddles one): each travels with
+        // its symbol through the compaction and is re-balloted at its new lane
+        if ((live >> lane) & 1ull) tmp[__popcll(live & lt)] = (sym & 0xFFFFu) | (uint32_t)((heads >> lane) & 1ull) << 16;
         __builtin_amdgcn_wave_barrier();
         n = __popcll(live);
-        sym = lane < n ? tmp[lane] : 0u;
+        const uint32_t w = lane < n ? tmp[lane] : 0u;
+        sym = w & 0xFFFFu;
+        heads = __ballot(w >> 16);
         __builtin_amdgcn_wave_barrier();
     }
     return n;
@@ -369,7 +370,7 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
     __shared__ uint16_t s_pieces[CHUNK + 1];  // prel | SPEC << 12 | LONG << 13
     __shared__ uint16_t s_stage[STAGE];       // ids staged at their piece's byte position
     __shared__ uint8_t s_cnt[CHUNK];          // ids per piece (<= BPE_MAX_WAVE), CNT_LONG = long piece
-    __shared__ uint16_t s_tmp[64];
+    __shared__ uint32_t s_tmp[64];
     __shared__ uint32_t s_scratch[8];
 
     const int tid = threadIdx.x;
@@ -646,7 +647,7 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
             ++nw;
             ++q;
         }
-        const int k = bpe_wave_seg(T, sym, total, heads, (lds_u16 *)s_tmp);
+        const int k = bpe_wave_seg(T, sym, total, heads, (lds_u32 *)s_tmp);
         const uint64_t upto = lane == 63 ? heads : heads & ((2ull << lane) - 1ull);
         const int seg = __popcll(upto) - 1;
         const int start = upto ? 63 - __builtin_clzll(upto) : 0;
