@@ -407,6 +407,52 @@ __device__ __forceinline__ void select_k_smallest(const uint32_t (&key)[MR][4], 
     }
 }
 
+// The same selection, usually in far fewer steps: the Philox keys are uniform,
+// so an interpolation search over the key range (the next threshold guessed
+// from the counts at the bracket's ends) lands on a threshold with exactly k
+// keys below it in ~3-4 counts instead of the radix descent's ~log2(S) + 2.
+// Any threshold with exactly k keys below it marks the same k-smallest set; a
+// tie at the k-th key (no such threshold) or a slow bracket falls back to the
+// radix select.  (SDL_ROWS_INTERP_STEPS=0: the radix select alone.)
+#ifndef SDL_ROWS_INTERP_STEPS
+#define SDL_ROWS_INTERP_STEPS 8
+#endif
+template <int MR>
+__device__ __forceinline__ void select_k_smallest_interp(const uint32_t (&key)[MR][4], int k, int nvalid,
+                                                         bool (&sel)[MR][4]) {
+    if (k > 0 && k < nvalid) {
+        uint32_t lo = 0, hi = 0xFFFFFFFFu;  // count(key < lo) = c_lo < k < c_hi ~ count(key < hi)
+        int c_lo = 0, c_hi = nvalid;
+#pragma unroll 1
+        for (int it = 0; it < SDL_ROWS_INTERP_STEPS && hi - lo > 1u; ++it) {
+            const float f = ((float)(k - c_lo) + 0.5f) / (float)(c_hi - c_lo);
+            uint32_t cand = lo + (uint32_t)((float)(hi - lo) * f);
+            cand = cand <= lo ? lo + 1u : cand >= hi ? hi - 1u : cand;
+            cand = __builtin_amdgcn_readfirstlane(cand);
+            int c = 0;
+#pragma unroll
+            for (int m = 0; m < MR; ++m)
+#pragma unroll
+                for (int w = 0; w < 4; ++w) c += __popcll(__ballot(key[m][w] < cand));
+            if (c == k) {
+#pragma unroll
+                for (int m = 0; m < MR; ++m)
+#pragma unroll
+                    for (int w = 0; w < 4; ++w) sel[m][w] = key[m][w] < cand;
+                return;
+            }
+            if (c < k) {
+                lo = cand;
+                c_lo = c;
+            } else {
+                hi = cand;
+                c_hi = c;
+            }
+        }
+    }
+    select_k_smallest<MR>(key, k, sel);
+}
+
 __device__ __forceinline__ void store4(int32_t *p, int j0, int S, bool vec, int32_t a, int32_t b, int32_t c,
                                        int32_t d) {
     if (vec) {  // the planes stream out: non-temporal, they are not re-read by this pass
@@ -505,7 +551,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SDL_ROWS_WA
                     key[m][2] = j0 + 2 < S ? c.z : 0xFFFFFFFFu;
                     key[m][3] = j0 + 3 < S ? c.w : 0xFFFFFFFFu;
                 }
+#if SDL_ROWS_INTERP_STEPS > 0
+                select_k_smallest_interp<MR>(key, P.mask_length, S < 256 * MR ? S : 256 * MR, sel);
+#else
                 select_k_smallest<MR>(key, P.mask_length, sel);
+#endif
             }
 #pragma unroll
             for (int m = 0; m < MR; ++m) {

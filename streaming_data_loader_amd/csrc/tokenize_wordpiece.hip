@@ -409,6 +409,15 @@ __device__ unsigned long long sdl_phase_cycles[16];
 #ifndef SDL_WP_WAVES
 #define SDL_WP_WAVES 5
 #endif
+#ifndef SDL_WP_NPROBE
+#define SDL_WP_NPROBE 2
+#endif
+// candidate lengths the pending-word state machine probes per step (longest
+// first).  3 and 4 were measured: parity-green and no faster (4: 96 VGPRs,
+// fixture 1.14 -> 1.19 ms, held-out 2.32 -> 2.40; 3: within noise) -- the
+// machine is bound by its lanes' probe latency, not by its step count.
+constexpr int WP_NPROBE = SDL_WP_NPROBE;
+static_assert(WP_NPROBE >= 1, "at least one candidate per step");
 __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL_WP_WAVES, 8))) void k_wordpiece_chunks(
     DevTok T, const uint8_t *__restrict__ text, int64_t N, const uint64_t *__restrict__ off, int64_t R,
     const uint32_t *__restrict__ ranges, uint32_t *__restrict__ tokc, uint32_t *__restrict__ chunk_cnt,
@@ -859,20 +868,31 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
                 }
             }
             if (!__any(active || !exhausted)) break;
-            if (active) {  // probe the candidates ending at `end` and one char earlier together
+            if (active) {  // probe the candidates ending at `end` and WP_NPROBE - 1 chars earlier together
                 const W16 sh = start ? shift_right_bytes(w, start) : w;
                 const uint32_t cont = start > 0 ? 1u : 0u;
-                const int e1 = w16_prev_char(w, end, start);
-                const int n0 = end - start, n1 = e1 - start;
-                const W16 c0w = keep_bytes(sh, n0), c1w = keep_bytes(sh, n1);
-                const Probe P0 = probe_load(T, hash16(c0w, (uint32_t)n0, cont));
-                const Probe P1 = probe_load(T, hash16(c1w, (uint32_t)n1, cont));
-                int id = probe_result(P0, (uint32_t)n0 | (cont << 8), c0w);
-                int got = n0;
-                if (id < 0 && n1 > 0) {
-                    id = probe_result(P1, (uint32_t)n1 | (cont << 8), c1w);
-                    got = n1;
+                int ek[WP_NPROBE];
+                ek[0] = end;
+#pragma unroll
+                for (int k = 1; k < WP_NPROBE; ++k) ek[k] = ek[k - 1] > start ? w16_prev_char(w, ek[k - 1], start) : start;
+                W16 cw[WP_NPROBE];
+                Probe Pk[WP_NPROBE];
+#pragma unroll
+                for (int k = 0; k < WP_NPROBE; ++k) {
+                    const int nk = ek[k] - start;
+                    cw[k] = keep_bytes(sh, nk);
+                    Pk[k] = probe_load(T, hash16(cw[k], (uint32_t)nk, cont));
                 }
+                int id = -1, got = 0;
+#pragma unroll
+                for (int k = 0; k < WP_NPROBE; ++k) {
+                    const int nk = ek[k] - start;
+                    if (id < 0 && (k == 0 || nk > 0)) {
+                        id = probe_result(Pk[k], (uint32_t)nk | (cont << 8), cw[k]);
+                        got = nk;
+                    }
+                }
+                const int e1 = ek[WP_NPROBE - 1], n1 = e1 - start;
                 lds_u16 *out = stage + prel;
                 if (id >= 0) {
                     out[nout++] = (uint16_t)id;
