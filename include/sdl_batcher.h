@@ -303,6 +303,9 @@ int sdl_tokenizer_info_get(const char *tokenizer_path, const char *data_dir, sdl
 /* Last error message of the calling thread. */
 const char *sdl_last_error(void);
 int sdl_abi_version(void);
+/* sha256 (hex) of the sources, headers and flags this library was built from
+ * (streaming_data_loader_amd/build.py source_hash): proves which build ran. */
+const char *sdl_build_id(void);
 
 #ifdef __cplusplus
 }

@@ -1,7 +1,9 @@
 /* orc_json.c -- minimal JSON parser for the CPU oracle (TEST INFRASTRUCTURE ONLY). */
 #include "orc_json.h"
 
+#include <math.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -13,6 +15,111 @@ typedef struct {
 
 static void ws(ps *p) {
     while (p->i < p->n && (p->s[p->i] == ' ' || p->s[p->i] == '\n' || p->s[p->i] == '\r' || p->s[p->i] == '\t')) p->i++;
+}
+
+/* A JSON number as serde_json 1.0.87 reads it into an f64 with its default
+ * features (rust/Cargo.lock:2037-2040; `float_roundtrip` off), which is how
+ * tokenizers' Unigram gets its piece scores (Vec<(String, f64)>):
+ * de.rs parse_integer / parse_long_integer / parse_decimal /
+ * parse_decimal_overflow / parse_exponent / f64_from_parts.  Digits
+ * accumulate in a u64 significand; a digit that would overflow it ends the
+ * accumulation (later integer digits only raise the exponent, later fraction
+ * digits are dropped); then (double)significand is multiplied or divided by
+ * the correctly rounded 10^|e| (e beyond 308 divides by 1e308 first).  Two
+ * roundings, so a 17-digit score can land one ulp from strtod's value --
+ * which decides Viterbi ties (tests/test_serde_numbers.py pins this against
+ * tokenizers itself). */
+static double pow10_tab(int k) {
+    static double t[309];
+    static int init;
+    if (!init) {
+        char b[16];
+        for (int i = 0; i < 309; ++i) {
+            snprintf(b, sizeof b, "1e%d", i);
+            t[i] = strtod(b, NULL); /* correctly rounded, like Rust's POW10 literals */
+        }
+        init = 1;
+    }
+    return t[k];
+}
+
+static int isdig(const ps *p) { return p->i < p->n && p->s[p->i] >= '0' && p->s[p->i] <= '9'; }
+
+static int serde_number(ps *p, double *out) {
+    const uint64_t M10 = UINT64_MAX / 10, R10 = UINT64_MAX % 10;
+    int pos = 1;
+    if (p->i < p->n && p->s[p->i] == '-') { pos = 0; p->i++; }
+    if (!isdig(p)) return -1;
+    uint64_t sig = 0;
+    long exp = 0;
+    if (p->s[p->i] == '0') {
+        p->i++;
+        if (isdig(p)) return -1; /* one leading zero only */
+    } else {
+        while (isdig(p)) {
+            const uint64_t d = (uint64_t)(p->s[p->i] - '0');
+            if (sig >= M10 && (sig > M10 || d > R10)) { /* parse_long_integer */
+                while (isdig(p)) { p->i++; exp++; }
+                break;
+            }
+            sig = sig * 10 + d;
+            p->i++;
+        }
+    }
+    if (p->i < p->n && p->s[p->i] == '.') {
+        p->i++;
+        if (!isdig(p)) return -1;
+        while (isdig(p)) {
+            const uint64_t d = (uint64_t)(p->s[p->i] - '0');
+            if (sig >= M10 && (sig > M10 || d > R10)) { /* parse_decimal_overflow */
+                while (isdig(p)) p->i++;
+                break;
+            }
+            sig = sig * 10 + d;
+            exp--;
+            p->i++;
+        }
+    }
+    if (p->i < p->n && (p->s[p->i] == 'e' || p->s[p->i] == 'E')) {
+        p->i++;
+        int pe = 1;
+        if (p->i < p->n && (p->s[p->i] == '+' || p->s[p->i] == '-')) pe = p->s[p->i++] == '+';
+        if (!isdig(p)) return -1;
+        long e = 0;
+        int ovf = 0;
+        while (isdig(p)) {
+            const long d = p->s[p->i++] - '0';
+            if (e >= INT32_MAX / 10 && (e > INT32_MAX / 10 || d > INT32_MAX % 10)) ovf = 1;
+            if (!ovf) e = e * 10 + d;
+        }
+        if (ovf) { /* parse_exponent_overflow: 0 for a zero significand or a negative exponent */
+            if (sig != 0 && pe) return -1;
+            *out = pos ? 0.0 : -0.0;
+            return 0;
+        }
+        exp = pe ? exp + e : exp - e;
+        if (exp > INT32_MAX) exp = INT32_MAX; /* i32 saturating add/sub */
+        if (exp < INT32_MIN) exp = INT32_MIN;
+    }
+    double f = (double)sig;
+    for (;;) {
+        const long k = exp < 0 ? -exp : exp;
+        if (k <= 308) {
+            if (exp >= 0) {
+                f *= pow10_tab((int)k);
+                if (isinf(f)) return -1; /* NumberOutOfRange */
+            } else {
+                f /= pow10_tab((int)k);
+            }
+            break;
+        }
+        if (f == 0.0) break;
+        if (exp >= 0) return -1;
+        f /= 1e308;
+        exp += 308;
+    }
+    *out = pos ? f : -f;
+    return 0;
 }
 
 static void put_utf8(char *o, size_t *k, uint32_t cp) {
@@ -134,11 +241,14 @@ static void value(ps *p, oj *v) {
     if (!strncmp(p->s + p->i, "true", 4)) { v->kind = OJ_BOOL; v->b = 1; p->i += 4; return; }
     if (!strncmp(p->s + p->i, "false", 5)) { v->kind = OJ_BOOL; p->i += 5; return; }
     if (!strncmp(p->s + p->i, "null", 4)) { v->kind = OJ_NULL; p->i += 4; return; }
-    char *end;
     v->kind = OJ_NUM;
-    v->num = strtod(p->s + p->i, &end);
-    if (end == p->s + p->i) { p->err = 1; return; }
-    p->i = (size_t)(end - p->s);
+    if (serde_number(p, &v->num)) p->err = 1;
+}
+
+int orc_json_number(const char *text, size_t n, double *out) {
+    ps p = {text, n, 0, 0};
+    if (serde_number(&p, out) || p.i != n) return -1;
+    return 0;
 }
 
 oj *oj_parse(const char *text, size_t n) {

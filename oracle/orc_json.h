@@ -21,5 +21,8 @@ typedef struct oj {
 /* Parses text[0..n); NULL on error. */
 oj *oj_parse(const char *text, size_t n);
 void oj_free(oj *v);
+/* One JSON number as serde_json 1.0.87 parses it into an f64 (default
+ * features); 0 ok, -1 not a number / out of range. */
+int orc_json_number(const char *text, size_t n, double *out);
 const oj *oj_get(const oj *obj, const char *key);
 #endif

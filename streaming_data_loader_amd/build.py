@@ -8,6 +8,7 @@ git-ignored but travels to the GPU box with the repo snapshot.  hipcc
 cross-compiles without a GPU.
 """
 import concurrent.futures as cf
+import hashlib
 import os
 import shutil
 import subprocess
@@ -41,17 +42,46 @@ def _newer(dst, srcs):
     return all(os.path.getmtime(s) <= t for s in srcs)
 
 
+BUILD_ID_MARK = b"sdl-build-id:"
+
+
+def source_hash(defines=()):
+    """sha256 over the contents of every source, header and flag the library is
+    built from -- what sdl_build_id() of an up-to-date library returns."""
+    h = hashlib.sha256()
+    for path in [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [os.path.join(REPO, "include", "sdl_batcher.h")]:
+        h.update(os.path.basename(path).encode() + b"\0")
+        with open(path, "rb") as f:
+            h.update(f.read())
+    h.update(" ".join(FLAGS[:-4] + [f"-D{d}" for d in defines]).encode())
+    return h.hexdigest()
+
+
+def embedded_id(lib):
+    """The build id compiled into a library file (read from its bytes, no dlopen), or None."""
+    try:
+        with open(lib, "rb") as f:
+            data = f.read()
+    except OSError:
+        return None
+    i = data.find(BUILD_ID_MARK)
+    return data[i + len(BUILD_ID_MARK):i + len(BUILD_ID_MARK) + 64].decode("ascii", "replace") if i >= 0 else None
+
+
 def build(verbose=False, force=False, jobs=4, defines=(), lib=None, build_dir=None):
-    """defines: extra -D macros (diagnostic builds go to their own lib/build_dir)."""
+    """defines: extra -D macros (diagnostic builds go to their own lib/build_dir).
+
+    A library whose embedded build id equals source_hash() is used as is (the
+    GPU box gets the library but not the objects: nothing is recompiled
+    there); otherwise the changed objects are rebuilt and the id relinked."""
     lib = lib or LIB
     bdir = build_dir or BUILD
     os.makedirs(bdir, exist_ok=True)
+    want = source_hash(defines)
+    if not force and embedded_id(lib) == want:
+        return lib
     hipcc = _hipcc()
     hdrs = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(REPO, "include", "sdl_batcher.h")]
-    # a prebuilt library newer than every source is used as is (the GPU box
-    # gets the library but not the objects: nothing is recompiled there)
-    if not force and _newer(lib, [os.path.join(CSRC, s) for s in SOURCES] + hdrs):
-        return lib
     objs, todo = [], []
     for s in SOURCES:
         src = os.path.join(CSRC, s)
@@ -60,6 +90,14 @@ def build(verbose=False, force=False, jobs=4, defines=(), lib=None, build_dir=No
         if force or not _newer(obj, [src] + hdrs):
             lang = ["-x", "hip"] if s.endswith(".hip") else []
             todo.append([hipcc] + FLAGS + [f"-D{d}" for d in defines] + lang + ["-c", src, "-o", obj])
+    # the build id: a one-line translation unit regenerated per link
+    idsrc = os.path.join(bdir, "build_id.cpp")
+    with open(idsrc, "w") as f:
+        f.write('extern "C" const char *sdl_build_id(void) {\n'
+                f'    static const char id[] = "{BUILD_ID_MARK.decode()}{want}";\n'
+                f'    return id + {len(BUILD_ID_MARK)};\n}}\n')
+    idobj = idsrc + ".o"
+    todo.append([hipcc, "-O2", "-fPIC", "-c", idsrc, "-o", idobj])
 
     def run(cmd):
         if verbose:
@@ -73,8 +111,9 @@ def build(verbose=False, force=False, jobs=4, defines=(), lib=None, build_dir=No
         for err in ex.map(run, todo):
             if verbose and err:
                 print(err, file=sys.stderr)
-    if force or todo or not _newer(lib, objs):
-        run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib] + objs + ["-ldl"])
+    run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib] + objs + [idobj, "-ldl"])
+    if embedded_id(lib) != want:
+        raise RuntimeError(f"{lib}: build id not embedded")
     return lib
 
 

@@ -47,7 +47,8 @@ struct HostTokenizer {
 
     // ---- Unigram (t5) ------------------------------------------------------
     std::vector<double> uscore;            // id -> score
-    std::vector<float> uscore32;           // ... as f32 (exact, checked)
+    std::vector<float> uscore32;           // ... nearest f32
+    std::vector<int8_t> uscore_adj;        // ... f64 ulps from it (-1, 0, 1)
     std::vector<uint16_t> wres;            // word-table results of > 1 id
     std::vector<VSlot> wslots;             // word table (UC_WORD), apart from the pieces in `slots`
     uint32_t wslot_mask = 0;

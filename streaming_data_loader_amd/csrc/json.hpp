@@ -151,14 +151,94 @@ class JParser {
         } else if (s_.compare(i_, 4, "null") == 0) {
             i_ += 4;
         } else {
-            const char *b = s_.c_str() + i_;
-            char *e = nullptr;
             v.kind = JValue::NUM;
-            v.num = std::strtod(b, &e);
-            if (e == b) fail("bad value");
-            i_ += (size_t)(e - b);
+            v.num = number();
         }
         return v;
+    }
+
+    // A number read the way serde_json (1.0.87 in the reference's Cargo.lock,
+    // default features, no `float_roundtrip`) reads it into the f64 that
+    // tokenizers' Unigram keeps as a piece score: the digits go into a u64
+    // mantissa until one more would overflow it (then integer digits only
+    // scale, fraction digits are ignored), and the result is
+    // (double)mantissa * or / the correctly rounded power of ten -- not the
+    // correctly rounded value strtod gives.  The difference (an ulp for ~1/4
+    // of 17-digit scores) decides Viterbi ties between equal-sum paths.
+    double number() {
+        static const std::vector<double> p10 = [] {
+            std::vector<double> t(309);
+            for (int k = 0; k < 309; ++k) t[(size_t)k] = std::strtod(("1e" + std::to_string(k)).c_str(), nullptr);
+            return t;
+        }();
+        auto digit = [&]() -> int {
+            return i_ < s_.size() && s_[i_] >= '0' && s_[i_] <= '9' ? s_[i_] - '0' : -1;
+        };
+        const bool neg = i_ < s_.size() && s_[i_] == '-';
+        if (neg) ++i_;
+        if (digit() < 0) fail("bad value");
+        uint64_t m = 0;
+        int64_t e10 = 0;
+        bool full = false;  // the mantissa took its last digit
+        auto take = [&](int d, bool fraction) {
+            if (!full && (m > UINT64_MAX / 10 || (m == UINT64_MAX / 10 && (uint64_t)d > UINT64_MAX % 10))) full = true;
+            if (full) {
+                if (!fraction) ++e10;
+                return;
+            }
+            m = m * 10 + (uint64_t)d;
+            if (fraction) --e10;
+        };
+        if (digit() == 0) {
+            ++i_;
+            if (digit() >= 0) fail("leading zero");
+        } else {
+            for (int d; (d = digit()) >= 0; ++i_) take(d, false);
+        }
+        if (i_ < s_.size() && s_[i_] == '.') {
+            ++i_;
+            if (digit() < 0) fail("bad fraction");
+            // (after an integer-part overflow serde_json retries each fraction
+            // digit against the same u64 bound, as `take` does)
+            full = false;
+            for (int d; (d = digit()) >= 0; ++i_) take(d, true);
+        }
+        if (i_ < s_.size() && (s_[i_] == 'e' || s_[i_] == 'E')) {
+            ++i_;
+            bool eneg = false;
+            if (i_ < s_.size() && (s_[i_] == '+' || s_[i_] == '-')) eneg = s_[i_++] == '-';
+            if (digit() < 0) fail("bad exponent");
+            int64_t x = 0;
+            bool big = false;
+            for (int d; (d = digit()) >= 0; ++i_) {
+                if (x > INT32_MAX / 10 || (x == INT32_MAX / 10 && d > INT32_MAX % 10)) big = true;
+                if (!big) x = x * 10 + d;
+            }
+            if (big) {
+                if (m != 0 && !eneg) fail("number out of range");
+                return neg ? -0.0 : 0.0;
+            }
+            e10 = eneg ? e10 - x : e10 + x;
+            e10 = e10 > INT32_MAX ? INT32_MAX : e10 < INT32_MIN ? INT32_MIN : e10;
+        }
+        double f = (double)m;
+        while (true) {
+            const int64_t a = e10 < 0 ? -e10 : e10;
+            if (a <= 308) {
+                if (e10 >= 0) {
+                    f *= p10[(size_t)a];
+                    if (f > 1.7976931348623157e308) fail("number out of range");
+                } else {
+                    f /= p10[(size_t)a];
+                }
+                break;
+            }
+            if (f == 0.0) break;
+            if (e10 >= 0) fail("number out of range");
+            f /= 1e308;
+            e10 += 308;
+        }
+        return neg ? -f : f;
     }
 };
 

@@ -103,7 +103,8 @@ __device__ __forceinline__ Probe probe_load_words(const DevTok &T, uint32_t h) {
 
 // id of the slot (payload bytes acc(start .. start+n), cont) or -1: exact
 template <class Acc>
-__device__ int probe_acc(const DevTok &T, const Acc &acc, int start, int n, uint32_t cont, uint32_t *w3 = nullptr) {
+__device__ int probe_acc(const DevTok &T, const Acc &acc, int start, int n, uint32_t cont, uint32_t *w3 = nullptr,
+                          uint32_t *zw = nullptr) {
     uint32_t h = hinit((uint32_t)n, cont);
     W16 first{0, 0, 0, 0};
     int b0 = 0;
@@ -121,20 +122,33 @@ __device__ int probe_acc(const DevTok &T, const Acc &acc, int start, int n, uint
         const uint4 a = which ? P.a2 : P.a1, b = which ? P.b2 : P.b1;
         if (!slot_match(a, b, key, first)) continue;
         bool ok = true;
-        for (int k = 16; k < n && ok; ++k) ok = T.vpool[a.z + k] == acc(start + k);
+        for (int k = 16; k < n && ok; ++k) ok = T.vpool[(a.z & SLOT_POOL_MASK) + k] == acc(start + k);
         if (ok) {
             if (w3) *w3 = a.w;
+            if (zw) *zw = a.z;
             return (int32_t)a.y;
         }
     }
     return -1;
 }
 
-// probe_result that also returns the slot's word 3 (a Unigram piece's f32 score)
-__device__ __forceinline__ int probe_result_w3(const Probe &P, uint32_t key, const W16 &c, uint32_t *w3) {
-    if (slot_match(P.a1, P.b1, key, c)) { *w3 = P.a1.w; return (int32_t)P.a1.y; }
-    if (slot_match(P.a2, P.b2, key, c)) { *w3 = P.a2.w; return (int32_t)P.a2.y; }
+// probe_result that also returns the slot's words 3 and 2 (a Unigram piece's
+// f32 score and, in word 2's top bits, its f64 ulp correction: uni_score64)
+__device__ __forceinline__ int probe_result_w3(const Probe &P, uint32_t key, const W16 &c, uint32_t *w3, uint32_t *zw) {
+    if (slot_match(P.a1, P.b1, key, c)) { *w3 = P.a1.w; *zw = P.a1.z; return (int32_t)P.a1.y; }
+    if (slot_match(P.a2, P.b2, key, c)) { *w3 = P.a2.w; *zw = P.a2.z; return (int32_t)P.a2.y; }
     return -1;
+}
+
+// A candidate's LDS record: id | the slot's 2-bit ulp correction << 16
+__device__ __forceinline__ uint32_t uni_cand(int id, uint32_t zw) { return (uint32_t)id | (zw >> 30) << 16; }
+__device__ __forceinline__ int uni_cand_id(uint32_t v) { return (int)(v & 0xFFFFu); }
+// The piece's score as tokenizers holds it: serde_json's f64 parse of the
+// tokenizer.json number (json.hpp), which is the f32 score or one ulp off it
+// (the host checks); the correction is sign-extended from bits 16-17.
+__device__ __forceinline__ double uni_score64(float f32, uint32_t cand) {
+    const int adj = (int32_t)(cand << 14) >> 30;
+    return __longlong_as_double(__double_as_longlong((double)f32) + adj);
 }
 
 // Added token "<...>" starting at p: the bytes up to the first '>' (within
@@ -579,7 +593,7 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
     __shared__ uint32_t s_rowmask[TASK_CAP];    // per row: which candidate ends exist (<= UNI_WMAX + 1)
     __shared__ uint16_t s_vp_src[VP_CAP];
     __shared__ uint8_t s_vp_len[VP_CAP];
-    __shared__ uint16_t s_tid[TASK_CAP];
+    __shared__ uint32_t s_tid[TASK_CAP];  // uni_cand: id | score correction
     __shared__ float s_tsc[TASK_CAP];
 
     const int tid = threadIdx.x;
@@ -951,7 +965,7 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
     W16 W[TASK_UNROLL];
     uint32_t meta[TASK_UNROLL];  // row | k << 16 | n << 22 | cont << 29; ~0u: no probe
     int gen[TASK_UNROLL];        // generic probe result (payload > 16 bytes); -2: use P
-    uint32_t gw3[TASK_UNROLL];
+    uint32_t gw3[TASK_UNROLL], gzw[TASK_UNROLL];
     // A lane takes TASK_UNROLL consecutive tasks (4 lane + u): one job/vp search
     // and one candidate decode per lane, then (i, j) steps along the rows, and
     // the 16 payload bytes of a row are read from LDS once for its candidates.
@@ -989,6 +1003,7 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
             meta[u] = ~0u;
             gen[u] = -2;
             gw3[u] = 0;
+            gzw[u] = 0;
             W[u] = W16{0, 0, 0, 0};
             if (t0 + u >= nt) continue;
             if (u > 0) {  // the next candidate: (i, j + 1), else the next row / vp / job
@@ -1030,7 +1045,7 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
                 W[u] = keep_bytes(rowb, n);
                 P[u] = probe_load(T, hash16(W[u], (uint32_t)n, cont));
             } else {
-                gen[u] = probe_acc(T, [&](int x) -> uint32_t { return bytes[src + x]; }, ps, n, cont, &gw3[u]);
+                gen[u] = probe_acc(T, [&](int x) -> uint32_t { return bytes[src + x]; }, ps, n, cont, &gw3[u], &gzw[u]);
             }
         }
     };
@@ -1044,13 +1059,13 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
 #pragma unroll
         for (int u = 0; u < TASK_UNROLL; ++u) {
             if (meta[u] == ~0u) continue;
-            uint32_t w3 = gw3[u];
+            uint32_t w3 = gw3[u], zw = gzw[u];
             const uint32_t key = ((meta[u] >> 22) & 0x7Fu) | ((meta[u] >> 29) << 8);
-            const int id = gen[u] != -2 ? gen[u] : probe_result_w3(P[u], key, W[u], &w3);
+            const int id = gen[u] != -2 ? gen[u] : probe_result_w3(P[u], key, W[u], &w3, &zw);
             if (id < 0) continue;
             const int t = TASK_UNROLL * lane + u;
-            s_tid[t] = (uint16_t)id;
-            s_tsc[t] = __uint_as_float(w3);  // the slot's score (f32, exact)
+            s_tid[t] = uni_cand(id, zw);
+            s_tsc[t] = __uint_as_float(w3);  // the slot's f32 score (+ s_tid's correction: uni_score64)
             atomicOr(&s_rowmask[meta[u] & 0xFFFFu], 1u << ((meta[u] >> 16) & 0x3Fu));
         }
         __syncthreads();
@@ -1114,10 +1129,11 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
                         for (uint32_t mm = m >> gl; mm; mm >>= DPG, k += DPG) {
                             if (!(mm & 1u)) continue;
                             const int e = fe + k;
-                            const double c = (double)s_tsc[rb + k] + base;
+                            const uint32_t cv = s_tid[rb + k];
+                            const double c = uni_score64(s_tsc[rb + k], cv) + base;
                             if (c > gsc[e]) {
                                 gsc[e] = c;
-                                gbp[e] = (uint32_t)st | ((uint32_t)s_tid[rb + k] << 16);
+                                gbp[e] = (uint32_t)st | ((uint32_t)uni_cand_id(cv) << 16);
                             }
                         }
                         if (!single && gl == DPG - 1) {  // unk: ends where no piece candidate does
@@ -1140,8 +1156,8 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
                         auto cand = [&](int st, int e, double *sc) -> int {  // the fused-unk lookup
                             const int loc = vp_local(st == 0 ? -1 : st - 3, e - 3, L, Mm, Mf);
                             if (loc < 0 || !((rowmask(st) >> (e - (st == 0 ? 3 : st + 1))) & 1u)) return -1;
-                            *sc = (double)s_tsc[toff + loc];
-                            return (int)s_tid[toff + loc];
+                            *sc = uni_score64(s_tsc[toff + loc], s_tid[toff + loc]);
+                            return uni_cand_id(s_tid[toff + loc]);
                         };
                         const int base = ktot;
                         ktot += unigram_backtrack(n, cand, gnodes, T.unk_id,
@@ -1274,7 +1290,7 @@ __global__ __launch_bounds__(64) void k_unigram_long(DevTok T, const uint8_t *__
     __shared__ double s_sc[NORM + 8];
     __shared__ uint32_t s_st[NORM + 8];  // node start | id << 16 (0xFFFF: unset)
     __shared__ uint16_t s_ids[2 * NORM + 16];
-    __shared__ uint16_t s_cid[KMAX * 64];     // [k][lane]: id of row lane's k-th end
+    __shared__ uint32_t s_cid[KMAX * 64];     // [k][lane]: uni_cand of row lane's k-th end
     __shared__ __attribute__((aligned(16))) float s_csc[KMAX * 64];
     // the item's raw bytes are staged where the candidate scores go later (the
     // normalization is done before the first probe): 1 KB less LDS per item
@@ -1434,13 +1450,14 @@ __global__ __launch_bounds__(64) void k_unigram_long(DevTok T, const uint8_t *__
                     Probe P[LONG_UNROLL];
                     W16 Wd[LONG_UNROLL];
                     int gen[LONG_UNROLL];
-                    uint32_t gw3[LONG_UNROLL], meta[LONG_UNROLL];  // row | k << 8 | len << 16 | cont << 24; ~0u: none
+                    uint32_t gw3[LONG_UNROLL], gzw[LONG_UNROLL], meta[LONG_UNROLL];  // row | k << 8 | len << 16 | cont << 24; ~0u: none
 #pragma unroll
                     for (int u = 0; u < LONG_UNROLL; ++u) {
                         const int t = tq + 64 * u + lane;
                         meta[u] = ~0u;
                         gen[u] = -2;
                         gw3[u] = 0;
+                        gzw[u] = 0;
                         Wd[u] = W16{0, 0, 0, 0};
                         if (t >= tz) continue;
                         int i, j;
@@ -1463,13 +1480,13 @@ __global__ __launch_bounds__(64) void k_unigram_long(DevTok T, const uint8_t *__
                             P[u] = probe_load(T, hfinal(h));
                             gen[u] = -3;
                         } else {
-                            gen[u] = probe_acc(T, nbr, src + ps, len, cont, &gw3[u]);
+                            gen[u] = probe_acc(T, nbr, src + ps, len, cont, &gw3[u], &gzw[u]);
                         }
                     }
 #pragma unroll
                     for (int u = 0; u < LONG_UNROLL; ++u) {
                         if (meta[u] == ~0u) continue;
-                        uint32_t w3 = gw3[u];
+                        uint32_t w3 = gw3[u], zw = gzw[u];
                         const uint32_t key = ((meta[u] >> 16) & 0xFFu) | ((meta[u] >> 24) << 8);
                         int id;
                         if (gen[u] == -3) {  // 17..32 bytes: header + first 16 bytes, then the pool
@@ -1480,19 +1497,21 @@ __global__ __launch_bounds__(64) void k_unigram_long(DevTok T, const uint8_t *__
                                 const uint4 sa = which ? P[u].a2 : P[u].a1, sb = which ? P[u].b2 : P[u].b1;
                                 if (!slot_match(sa, sb, key, Wd[u])) continue;
                                 bool ok = true;
-                                for (int x = 16; x < len && ok; ++x) ok = T.vpool[sa.z + x] == nb[src + (ps < 0 ? 0 : ps) + x];
+                                for (int x = 16; x < len && ok; ++x)
+                                    ok = T.vpool[(sa.z & SLOT_POOL_MASK) + x] == nb[src + (ps < 0 ? 0 : ps) + x];
                                 if (ok) {
                                     id = (int32_t)sa.y;
                                     w3 = sa.w;
+                                    zw = sa.z;
                                 }
                             }
                         } else {
-                            id = gen[u] != -2 ? gen[u] : probe_result_w3(P[u], key, Wd[u], &w3);
+                            id = gen[u] != -2 ? gen[u] : probe_result_w3(P[u], key, Wd[u], &w3, &zw);
                         }
                         if (id < 0) continue;
                         const int q = (int)(meta[u] & 0xFFu), k = (int)((meta[u] >> 8) & 0xFFu);
-                        s_cid[k * 64 + q] = (uint16_t)id;
-                        s_csc[k * 64 + q] = __uint_as_float(w3);  // the slot's score (f32, exact; k < KMAX host-checked)
+                        s_cid[k * 64 + q] = uni_cand(id, zw);
+                        s_csc[k * 64 + q] = __uint_as_float(w3);  // the slot's f32 score (k < KMAX host-checked)
                         atomicOr(&s_mask[q], 1ull << k);
                     }
                 }
@@ -1513,10 +1532,11 @@ __global__ __launch_bounds__(64) void k_unigram_long(DevTok T, const uint8_t *__
                     const bool single = (m >> (st + mb - fe)) & 1ull;
                     if (lane < KMAX && ((m >> lane) & 1ull)) {
                         const int e = fe + lane;
-                        const double c = (double)s_csc[lane * 64 + q] + base;
+                        const uint32_t cv = s_cid[lane * 64 + q];
+                        const double c = uni_score64(s_csc[lane * 64 + q], cv) + base;
                         if (s_st[e] == 0xFFFFFFFFu || c > s_sc[e]) {
                             s_sc[e] = c;
-                            s_st[e] = (uint32_t)st | ((uint32_t)s_cid[lane * 64 + q] << 16);
+                            s_st[e] = (uint32_t)st | ((uint32_t)uni_cand_id(cv) << 16);
                         }
                     }
                     if (!single && lane == 63) {  // the unk candidate ends where no piece candidate does

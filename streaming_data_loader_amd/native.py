@@ -22,7 +22,7 @@ EXPORTS = [
     "sdl_batcher_push_many", "sdl_batcher_next", "sdl_batcher_flush", "sdl_batch_release",
     "sdl_process_device", "sdl_process_device_labels", "sdl_json_text_device", "sdl_pickle_frames_device", "sdl_device_to_host", "sdl_set_profiling", "sdl_stage_times",
     "sdl_tokenizer_info_get", "sdl_last_error", "sdl_abi_version", "sdl_json_to_frames",
-    "sdl_gzip_inflate_device", "sdl_gzip_split_members",
+    "sdl_gzip_inflate_device", "sdl_gzip_split_members", "sdl_build_id",
 ]
 
 
@@ -128,6 +128,16 @@ def load(path=LIB_PATH):
     except Exception:
         pass
     L = ctypes.CDLL(path)
+    L.sdl_build_id.restype = ctypes.c_char_p
+    L.sdl_build_id.argtypes = []
+    if os.path.abspath(path) == os.path.join(PKG, "libsdl_batcher.so"):
+        # the product library must be built from the sources beside it
+        # (build.py embeds their content hash): a stale prebuilt library fails here
+        from . import build as _build
+        got, want = L.sdl_build_id().decode(), _build.source_hash()
+        if got != want:
+            raise SDLError(-4, f"{path} was built from other sources (build id {got[:12]}, sources {want[:12]}): "
+                               "rebuild with `python -m streaming_data_loader_amd.build`")
     vp, sz, u64, i32, i64 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_int32, ctypes.c_int
     L.sdl_config_default.argtypes = [ctypes.POINTER(Config), i32]
     L.sdl_config_default.restype = None
@@ -165,6 +175,11 @@ def load(path=LIB_PATH):
         getattr(L, name).restype = i64
     _lib = L
     return L
+
+
+def build_id():
+    """Content hash of the sources the loaded library was built from (build.source_hash)."""
+    return load().sdl_build_id().decode()
 
 
 def check(rc):

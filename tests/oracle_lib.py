@@ -88,6 +88,8 @@ def lib():
         L.orc_pickle_dataset.restype = ctypes.c_size_t
         L.orc_pickle_dataset.argtypes = [ctypes.c_int] * 5 + [vp] * 5 + [vp, ctypes.c_size_t]
         L.orc_batcher_span_errors.restype = ctypes.c_uint64
+        L.orc_json_number.restype = ctypes.c_int
+        L.orc_json_number.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_double)]
         _lib = L
     return _lib
 
@@ -355,3 +357,12 @@ def gz_inflate(member):
     got = ctypes.c_size_t(0)
     st = L.orc_gz_inflate(m, len(m), buf, cap, ctypes.byref(got))
     return st, buf.raw[:got.value]
+
+
+def json_number(text):
+    """A JSON number as serde_json 1.0.87 parses it into an f64 (oracle/orc_json.c)."""
+    b = text.encode() if isinstance(text, str) else bytes(text)
+    out = ctypes.c_double()
+    if lib().orc_json_number(b, len(b), ctypes.byref(out)):
+        raise ValueError(f"not a JSON number: {b!r}")
+    return out.value

@@ -1,13 +1,15 @@
 """Full bench-size (256 MiB arena) checks for span (t5 Unigram) and clm (gpt2
 byte-BPE), like test_gpu_parity.test_full_size_properties does for mlm, plus
-the held-out corpus through all three tokenizers.
+the held-out corpus and 3000 generated strings through all three tokenizers
+against `tokenizers`' own ids (tests/golden/heldout_ids.npz).
 
 At 256 MiB the oracle cannot recompute everything, so the checks are
 size-independent properties: every record's row count and the total id count
 equal what the oracle gives for its text, no capacity flag is raised, and 24
 seeded records' rows (global record index kept) are recomputed by the oracle
 bit-exactly.  The held-out corpus (tests/golden/heldout_records.jsonl: text on
-the image never used to build or tune a table) is compared id for id."""
+the image the proxy vocabularies were not trained on) is compared with the
+goldens record for record."""
 import json
 import os
 
@@ -118,19 +120,43 @@ def device_ids(torch, blobs, task, tok_path, S=2048):
     return out
 
 
+KINDS = {"bert": native.BERT_PROXY_TOKENIZER, "gpt2": native.GPT2_PROXY_TOKENIZER, "t5": native.T5_PROXY_TOKENIZER}
+
+
+def framed(kind, ids):
+    """encode_mask framing around tokenizer ids (the template's [CLS]/[SEP] and </s> are in `ids`)."""
+    if kind == "bert":
+        return [101] + list(ids) + [102, 102]
+    eos = 50256 if kind == "gpt2" else 1
+    return [eos] + list(ids) + [eos]
+
+
 @pytest.mark.parametrize("kind", ["bert", "gpt2", "t5"])
-def test_heldout_corpus_ids_match_oracle(torch, native_lib, kind):
+def test_heldout_corpus_ids_match_tokenizers_goldens(torch, native_lib, kind):
+    """The HIP path on the 3 MB held-out corpus against `tokenizers` itself
+    (tests/golden/make_heldout_goldens.py: per-record id count + blake2b-64
+    digest of Tokenizer.encode(text, True).ids)."""
+    from test_heldout_goldens import digest_ids
+    g = np.load(os.path.join(GOLDEN, "heldout_ids.npz"))
     recs = heldout_records()
     blobs = [r.encode("utf-8") for r in recs]
-    tok_path = {"bert": native.BERT_PROXY_TOKENIZER, "gpt2": native.GPT2_PROXY_TOKENIZER,
-                "t5": native.T5_PROXY_TOKENIZER}[kind]
-    got = device_ids(torch, blobs, kind, tok_path)
-    if kind == "bert":
-        tok = oracle_lib.Tok()
-        want = [[101] + tok.encode(b) + [102, 102] for b in blobs]  # encode() has the template's [CLS]/[SEP]
-    else:
-        tok = oracle_tok(kind)
-        eos = tok.eos
-        want = [[eos] + tok.encode(b) + [eos] for b in blobs]  # t5 encode() ends with the template's </s>
-    bad = [i for i, (g, w) in enumerate(zip(got, want)) if g != w]
+    got = device_ids(torch, blobs, kind, KINDS[kind])
+    bad = []
+    for i, seq in enumerate(got):
+        ids = seq[1:-2] if kind == "bert" else seq[1:-1]  # strip the encode_mask framing
+        if framed(kind, ids) != seq or len(ids) != int(g[f"{kind}_n"][i]) or digest_ids(ids) != int(g[f"{kind}_digest"][i]):
+            bad.append(i)
     assert not bad, f"{len(bad)} of {len(blobs)} records differ, first {bad[:5]}: {recs[bad[0]][:80]!r}"
+
+
+@pytest.mark.parametrize("kind", ["bert", "gpt2", "t5"])
+def test_generated_strings_match_tokenizers_goldens(torch, native_lib, kind):
+    """3000 seeded random-Unicode and long-identifier strings, id for id
+    against `tokenizers` (tests/golden/heldout_ids.npz)."""
+    g = np.load(os.path.join(GOLDEN, "heldout_ids.npz"))
+    t, o = g["gen_text"], g["gen_off"]
+    blobs = [t[o[i]:o[i + 1]].tobytes() for i in range(len(o) - 1)]
+    got = device_ids(torch, blobs, kind, KINDS[kind])
+    ids, off = g[f"{kind}_ids"], g[f"{kind}_off"]
+    bad = [i for i in range(len(blobs)) if got[i] != framed(kind, ids[off[i]:off[i + 1]].tolist())]
+    assert not bad, f"{len(bad)} of {len(blobs)} strings differ, e.g. {[blobs[i][:40] for i in bad[:3]]}"
