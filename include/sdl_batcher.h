@@ -73,10 +73,12 @@ typedef struct sdl_config {
     uint64_t seed;           /* RNG contract seed */
     uint64_t first_record;   /* global index of this handle's first record (sharding) */
     int32_t device;          /* HIP device ordinal */
-    int32_t rng_mode;        /* MLM masks: 0 = the Philox contract (default);
-                                1 = rand 0.8.5: position_base.shuffle(&mut StdRng::from_seed(
-                                seed | record | chunk, little-endian, zero padded)) per row
-                                (bert_data.rs:40-43 with a seeded StdRng; S <= 2048) */
+    int32_t rng_mode;        /* 0 = the Philox contract (default);
+                                1 = the reference's own draws on a per-row StdRng::from_seed(
+                                seed | record | chunk, little-endian, zero padded):
+                                MLM masks = rand 0.8.5 position_base.shuffle (bert_data.rs:40-43;
+                                S <= 2048); span gap / size = rand_distr 0.4.3 StandardNormal,
+                                gap then size per pass (t5_data.rs:165-176) */
     int32_t reserved[6];
 } sdl_config;
 

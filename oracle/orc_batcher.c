@@ -11,7 +11,9 @@
  *   encode_mask framing    rust/src/tokenizer/tokenizer_wrapper.rs:107-134
  *   RNG contract           DESIGN.md §3 (replaces the unseedable thread_rng)
  */
+#include <float.h>
 #include <math.h>
+#include <stdint.h>
 #include <stdio.h>
 #include <string.h>
 
@@ -132,6 +134,117 @@ void orc_rand_positions(uint64_t seed, uint64_t record, uint32_t chunk, int S, u
         pos[i] = pos[j];
         pos[j] = t;
     }
+}
+
+/* ------------------------------------------------------------------------- */
+/* Optional rand-compatible span mode (cfg.rng_mode = 1): T5Data::put_data's   */
+/* random_data_gap / random_data_size (t5_data.rs:165-176) draw               */
+/* `thread_rng().sample(StandardNormal)` as f64; with thread_rng replaced by   */
+/* the row's StdRng (same row_seed as the MLM mode) they are, in order, gap    */
+/* then size of pass 0, gap then size of pass 1, ...  Restated from the        */
+/* published sources (not vendored, not buildable here):                        */
+/*   rand_distr 0.4.3 StandardNormal for f64 = utils::ziggurat(rng, symmetric,  */
+/*     ZIG_NORM_X, ZIG_NORM_F, pdf = exp(-x*x/2), zero_case): bits = next_u64; */
+/*     i = bits & 0xff; u = f64 from bits>>12 with exponent 1, minus 3 ([-1,1));*/
+/*     x = u * X[i]; |x| < X[i+1] -> x; i == 0 -> tail: x = ln(Open01)/R,       */
+/*     y = ln(Open01) until -2y >= x*x, +-(R - x); else the wedge test          */
+/*     F[i+1] + (F[i] - F[i+1]) * gen::<f64>() < pdf(x) -> x, else retry;      */
+/*   the tables come from rand's ziggurat_tables.py (R = 3.6541528853610088,    */
+/*     V = 0.00492867323399, 256 layers) printed with %.18f;                  */
+/*   rand 0.8.5 Open01 (52-bit fraction in [1,2) minus 1 - EPSILON/2),          */
+/*     Standard f64 ((next_u64 >> 11) * 2^-53).                               */
+/* `distance as usize` saturates: NaN and negatives give 0.                    */
+/* Pinned (tests/test_rand_mode.py) by rand_distr's value-stability vector for  */
+/* StandardNormal (seed 213 of its Pcg32 test rng): -0.11844188827977231,      */
+/* 0.7813779637772346, 0.06563993969580051, -1.1932899004186373.             */
+/* ------------------------------------------------------------------------- */
+#define ZIG_R 3.6541528853610088
+static double ZX[257], ZF[257];
+static void zig_tables(void) {
+    static int init;
+    if (init) return;
+    const double V = 0.00492867323399;
+    double x[257];
+    x[0] = V / exp(-ZIG_R * ZIG_R / 2.0);
+    x[1] = ZIG_R;
+    for (int i = 2; i < 256; ++i) x[i] = sqrt(-2.0 * log(V / x[i - 1] + exp(-x[i - 1] * x[i - 1] / 2.0)));
+    x[256] = 0.0;
+    char buf[64];
+    for (int i = 0; i < 257; ++i) { /* the Rust source holds the %.18f texts */
+        snprintf(buf, sizeof buf, "%.18f", x[i]);
+        ZX[i] = strtod(buf, NULL);
+        snprintf(buf, sizeof buf, "%.18f", exp(-x[i] * x[i] / 2.0));
+        ZF[i] = strtod(buf, NULL);
+    }
+    init = 1;
+}
+typedef uint64_t (*u64_source)(void *);
+static double f64_bits(uint64_t b) { double d; memcpy(&d, &b, 8); return d; }
+static double std_normal(u64_source next, void *st) {
+    zig_tables();
+    for (;;) {
+        const uint64_t bits = next(st);
+        const int i = (int)(bits & 0xff);
+        const double u = f64_bits((bits >> 12) | (uint64_t)1024 << 52) - 3.0;
+        const double x = u * ZX[i];
+        if (fabs(x) < ZX[i + 1]) return x;
+        if (i == 0) { /* zero_case: the tail beyond R */
+            double xt = 1.0, yt = 0.0;
+            while (-2.0 * yt < xt * xt) {
+                const double a = f64_bits((next(st) >> 12) | (uint64_t)1023 << 52) - (1.0 - DBL_EPSILON / 2.0);
+                const double c = f64_bits((next(st) >> 12) | (uint64_t)1023 << 52) - (1.0 - DBL_EPSILON / 2.0);
+                xt = log(a) / ZIG_R;
+                yt = log(c);
+            }
+            return u < 0.0 ? xt - ZIG_R : ZIG_R - xt;
+        }
+        const double g = (double)(next(st) >> 11) * (1.0 / 9007199254740992.0);
+        if (ZF[i + 1] + (ZF[i] - ZF[i + 1]) * g < exp(-x * x / 2.0)) return x;
+    }
+}
+static uint64_t stdrng_u64(void *r) { /* BlockRng::next_u64 at an even index: low word first */
+    const uint64_t lo = stdrng_u32((orc_stdrng *)r);
+    return lo | (uint64_t)stdrng_u32((orc_stdrng *)r) << 32;
+}
+/* rand_pcg 0.3 Pcg32::new(state, stream) (Lcg64Xsh32), next_u64 = two next_u32, low first */
+typedef struct { uint64_t state, inc; } orc_pcg32;
+static uint32_t pcg32_u32(orc_pcg32 *p) {
+    const uint64_t s = p->state;
+    p->state = s * 6364136223846793005ull + p->inc;
+    const uint32_t rot = (uint32_t)(s >> 59), xsh = (uint32_t)(((s >> 18) ^ s) >> 27);
+    return (xsh >> rot) | (xsh << ((32 - rot) & 31));
+}
+static uint64_t pcg32_u64(void *p) {
+    const uint64_t lo = pcg32_u32((orc_pcg32 *)p);
+    return lo | (uint64_t)pcg32_u32((orc_pcg32 *)p) << 32;
+}
+/* n StandardNormal f64 samples from Pcg32::new(state, stream) -- for the KAT */
+void orc_normal_pcg32(uint64_t state, uint64_t stream, int n, double *out) {
+    orc_pcg32 p = {0, (stream << 1) | 1u};
+    p.state = state + p.inc;
+    p.state = p.state * 6364136223846793005ull + p.inc;
+    for (int k = 0; k < n; ++k) out[k] = std_normal(pcg32_u64, &p);
+}
+/* n StandardNormal f64 samples from the row's StdRng (the span mode's stream) */
+static void row_stdrng(orc_stdrng *r, uint64_t seed, uint64_t record, uint32_t chunk) {
+    uint8_t sd[32] = {0};
+    for (int b = 0; b < 8; ++b) {
+        sd[b] = (uint8_t)(seed >> (8 * b));
+        sd[8 + b] = (uint8_t)(record >> (8 * b));
+    }
+    for (int b = 0; b < 4; ++b) sd[16 + b] = (uint8_t)(chunk >> (8 * b));
+    stdrng_from_seed(r, sd);
+}
+void orc_normal_row(uint64_t seed, uint64_t record, uint32_t chunk, int n, double *out) {
+    orc_stdrng r;
+    row_stdrng(&r, seed, record, chunk);
+    for (int k = 0; k < n; ++k) out[k] = std_normal(stdrng_u64, &r);
+}
+/* `f as usize` (Rust saturating float -> int cast) */
+static size_t sat_usize(double d) {
+    if (!(d > 0.0)) return 0; /* NaN, negatives, -0.0 */
+    if (d >= 18446744073709551616.0) return SIZE_MAX;
+    return (size_t)d;
 }
 
 /* Span draws: the reference's trunc(avg - z) with z ~ StandardNormal
@@ -335,18 +448,28 @@ static int put_data(orc_batcher *b, obatch *x, const uint32_t *ids, size_t n, ui
         for (size_t j = 0; j < l; ++j) in[j] = 0; /* rewritten below */
         size_t ip = 0, lp = 0, ap = 0;
         uint32_t pass = 0;
+        const int rnd = b->c.rng_mode == 1;
+        orc_stdrng rr;
+        if (rnd) row_stdrng(&rr, b->c.seed, rec, chunk);
 #define EXTRA(k) ((k) < 100 ? (int32_t)b->enc.extra[k] : (b->span_errors++, (int32_t)b->enc.extra[99]))
 #define LAB(i, v) do { if ((i) < LW) lb[i] = (v); else b->span_errors++; } while (0)
         while (lp < S) {
-            uint32_t xg, xs;
-            span_draws(b->c.seed, rec, chunk, pass, &xg, &xs);
-            size_t g = span_pick(b->gap_kmin, b->gap_n, b->gap_thr, xg);
+            uint32_t xg = 0, xs = 0;
+            if (!rnd) span_draws(b->c.seed, rec, chunk, pass, &xg, &xs);
+            size_t g = rnd ? sat_usize(b->c.avg_span_gap - std_normal(stdrng_u64, &rr))
+                           : span_pick(b->gap_kmin, b->gap_n, b->gap_thr, xg);
             if (g > S - lp) g = S - lp;
             if (g > n - ip) g = n - ip;
             for (size_t j = 0; j < g; ++j) in[lp + j] = (int32_t)ids[ip + j];
             lp += g;
             ip += g;
-            size_t sz = span_pick(b->size_kmin, b->size_n, b->size_thr, xs);
+            size_t sz;
+            if (rnd) {
+                sz = sat_usize(b->c.avg_span_size - std_normal(stdrng_u64, &rr));
+                if (sz < 1) sz = 1; /* std::cmp::max(distance as usize, 1) */
+            } else {
+                sz = span_pick(b->size_kmin, b->size_n, b->size_thr, xs);
+            }
             if (sz > S - lp) sz = S - lp;
             if (sz > n - ip) sz = n - ip;
             if (sz > 0) {

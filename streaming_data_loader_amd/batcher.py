@@ -90,6 +90,11 @@ class TrainingConfig:
     dataset_config: DataSetConfig
     seed: int = 0
     device: int = 0
+    # 0: the Philox contract; 1: the reference's own draws on a
+    # per-row StdRng::from_seed(seed | record | chunk) -- rand 0.8.5 shuffle
+    # for MLM masks, rand_distr 0.4.3 StandardNormal for span gaps / sizes
+    # (INTEGRATION.md "Provable parity")
+    rng_mode: int = 0
 
 
 def get_mask_length(sequence_length: int) -> int:
@@ -98,19 +103,22 @@ def get_mask_length(sequence_length: int) -> int:
 
 
 def get_case(task: TaskType, test: bool, sequence_length: int = 128, batch_size: Optional[int] = None,
-             seed: int = 0) -> TrainingConfig:
+             seed: int = 0, rng_mode: int = 0) -> TrainingConfig:
     """masking_cases::get_case: B=4096 (test: 1), S=128 unless overridden."""
     b = batch_size if batch_size is not None else (1 if test else 4096)
     batch = BatchConfig(b, sequence_length)
     if task == TaskType.Mlm:
         return TrainingConfig(ModelType.Bert, TokenizerConfig(), batch, Mask(get_mask_length(sequence_length), 103),
-                              seed)
+                              seed, rng_mode=rng_mode)
     if task == TaskType.Clm:  # masking_cases.rs:66: gpt2
-        return TrainingConfig(ModelType.Gpt2, TokenizerConfig(native.GPT2_PROXY_TOKENIZER), batch, Gpt(), seed)
+        return TrainingConfig(ModelType.Gpt2, TokenizerConfig(native.GPT2_PROXY_TOKENIZER), batch, Gpt(), seed,
+                              rng_mode=rng_mode)
     if task == TaskType.Span:  # masking_cases.rs:78-90: t5-small, Span{16.0, 2.0}
-        return TrainingConfig(ModelType.T5, TokenizerConfig(native.T5_PROXY_TOKENIZER), batch, Span(16.0, 2.0), seed)
+        return TrainingConfig(ModelType.T5, TokenizerConfig(native.T5_PROXY_TOKENIZER), batch, Span(16.0, 2.0), seed,
+                              rng_mode=rng_mode)
     return TrainingConfig(ModelType.Bert, TokenizerConfig(), BatchConfig(2048 if batch_size is None else b,
-                                                                        sequence_length), MultiLabel(9), seed)
+                                                                        sequence_length), MultiLabel(9), seed,
+                          rng_mode=rng_mode)
 
 
 # ---- channel messages --------------------------------------------------------
@@ -233,7 +241,7 @@ class _NativeBatcher(Batcher):
 
     def __init__(self, model_type: ModelType, batch_config: BatchConfig, dataset_config: DataSetConfig,
                  tokenizer: TokenizerConfig, chunk: bool = True, seed: int = 0, device: int = 0,
-                 first_record: int = 0):
+                 first_record: int = 0, rng_mode: int = 0):
         L = native.load()
         if isinstance(dataset_config, Mask):
             task, self.kind = native.SDL_TASK_MLM, "bert"
@@ -254,7 +262,7 @@ class _NativeBatcher(Batcher):
             c.avg_span_gap, c.avg_span_size = dataset_config.avg_span_gap, dataset_config.avg_span_size
         if isinstance(dataset_config, MultiLabel):
             c.number_labels = dataset_config.number_labels
-        c.seed, c.device, c.first_record = seed, device, first_record
+        c.seed, c.device, c.first_record, c.rng_mode = seed, device, first_record, rng_mode
         h = ctypes.c_void_p()
         native.check(L.sdl_batcher_create(ctypes.byref(c), tokenizer.path.encode(), native.DATA_DIR.encode(),
                                           ctypes.byref(h)))
@@ -265,7 +273,8 @@ class _NativeBatcher(Batcher):
     @classmethod
     def from_config(cls, cfg: TrainingConfig, chunk: bool = True):
         """masking_runner::create_generator (masking_runner.rs:55-62)."""
-        return cls(cfg.model_config, cfg.batch, cfg.dataset_config, cfg.tokenizer, chunk, cfg.seed, cfg.device)
+        return cls(cfg.model_config, cfg.batch, cfg.dataset_config, cfg.tokenizer, chunk, cfg.seed, cfg.device,
+                   rng_mode=cfg.rng_mode)
 
     def close(self):
         if getattr(self, "_h", None):
@@ -333,15 +342,17 @@ class SimpleBatcher(_NativeBatcher):
     current (possibly empty) batch and starts a new one."""
 
     def __init__(self, model_type: ModelType, dataset_config: DataSetConfig, batch_config: BatchConfig,
-                 tokenizer: TokenizerConfig, seed: int = 0, device: int = 0):
+                 tokenizer: TokenizerConfig, seed: int = 0, device: int = 0, rng_mode: int = 0):
         if not isinstance(dataset_config, (MultiLabel, SingleClass)):
             raise ValueError("SimpleBatcher on the GPU path supports DataSetConfig::MultiLabel / SingleClass")
-        super().__init__(model_type, batch_config, dataset_config, tokenizer, False, seed, device)
+        # (these tasks draw nothing at random; rng_mode is accepted and checked like everywhere)
+        super().__init__(model_type, batch_config, dataset_config, tokenizer, False, seed, device, rng_mode=rng_mode)
 
     @classmethod
     def from_config(cls, cfg: TrainingConfig):
         """single_class::runner::create_generator (single_class/runner.rs:40-49)."""
-        return cls(cfg.model_config, cfg.dataset_config, cfg.batch, cfg.tokenizer, cfg.seed, cfg.device)
+        return cls(cfg.model_config, cfg.dataset_config, cfg.batch, cfg.tokenizer, cfg.seed, cfg.device,
+                   rng_mode=cfg.rng_mode)
 
     def create_sync_batch(self, data: SimpleTransport) -> Optional[DataSet]:
         text = data.data.text

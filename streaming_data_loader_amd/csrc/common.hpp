@@ -194,6 +194,9 @@ struct RowParams {
     int32_t gap_kmin, gap_n, size_kmin, size_n;
     uint32_t gap_thr[32], size_thr[32];
     const int32_t *extra_ids;
+    // span rng_mode 1: the reference's own draws (rand_distr StandardNormal)
+    double avg_span_gap, avg_span_size;
+    const double *zig_x, *zig_f;   // ZIG_NORM_X / ZIG_NORM_F (257 each, device)
 };
 
 __host__ __device__ inline uint32_t ceil_div_u32(uint32_t a, uint32_t b) { return (a + b - 1) / b; }

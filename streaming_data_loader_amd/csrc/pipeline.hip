@@ -792,13 +792,20 @@ hipError_t launch_rows(const RowParams &P, const uint32_t *tok, const uint32_t *
 // ---------------------------------------------------------------------------
 // T5Data::put_data (models/t5_data.rs:162-226) for every row, task=span.
 // A row is one chunk of n <= S framed ids.  Pass p draws gap g_p and span size
-// s_p (RNG contract: Philox(p, chunk | 1 << 30, record; seed) words 0/1 through
-// the CDF tables).  Because the input cursor never passes the id cursor
-// (lp <= ip <= n <= S), the only clamp that binds is n - ip, and only in the
-// last pass P (the first whose g + s reaches n).  So lanes take passes: a wave
-// prefix sum gives every pass's id cursor I_p, input cursor lp_p = I_p - A_p + p
-// (A_p = ids spanned before p) and label cursor ap_p = A_p + p, and each lane
-// writes its pass's gap ids, sentinel and label run; rounds of 64 passes carry.
+// s_p; because the input cursor never passes the id cursor (lp <= ip <= n <= S),
+// the only clamp that binds is n - ip, and only in the last pass (the first
+// whose g + s reaches n).  One wave per row, in rounds of up to 64 passes:
+//   A. lanes take passes: each lane's draws, then wave prefix sums give every
+//      pass's id cursor I_p, input cursor lp_p = I_p - A_p + p (A_p = ids
+//      spanned before p) and label cursor ap_p = A_p + p; the ballot finds
+//      the last pass; the round's pass records go to LDS;
+//   B. the planes are written position-parallel (lane = position, coalesced
+//      stores): a position's pass is the last one starting at or before it
+//      (a scalar walk over the few pass starts inside each 64-position group),
+//      and its value is a gap id, the sentinel, or a spanned id.
+// Draws: rng_mode 0 = the RNG contract (Philox(p, chunk | 1 << 30, record;
+// seed) words 0/1 through the CDF tables); rng_mode 1 = the reference's
+// random_data_gap / random_data_size on the row's StdRng (span_draws_rand).
 // Labels past the S/4 label width (the reference panics) are skipped and
 // counted in *err; so is a sentinel index >= 100 (extra[99] is written).
 // ---------------------------------------------------------------------------
@@ -809,25 +816,213 @@ __device__ __forceinline__ uint32_t span_pick(int32_t kmin, int32_t n, const uin
     return (uint32_t)v;
 }
 
+// ---- rng_mode 1: rand_distr 0.4.3 StandardNormal (f64) on the row's StdRng ----
+// (oracle/orc_batcher.c std_normal).  utils::ziggurat: bits = next_u64,
+// i = bits & 0xff, u = [2,4) float of bits >> 12 minus 3, x = u * X[i];
+// |x| < X[i+1] returns x (~99 % of draws, one u64); i == 0 takes the tail
+// (pairs of Open01 until -2 ln c >= (ln a / R)^2); else the wedge test with
+// one more u64.  The row's stream: u64 k = ChaCha12 words 2k (low), 2k+1.
+constexpr int SPAN_WBLK = 17;             // ChaCha12 blocks per window (lanes 0..16)
+constexpr int SPAN_WU64 = 8 * SPAN_WBLK;  // 136 u64 draws-worth of stream per window
+constexpr double ZIG_R = 3.6541528853610088;
+
+struct SpanStream {
+    uint32_t key[8];
+    const uint32_t *win;  // LDS: blocks [wblk, wblk + SPAN_WBLK)
+    uint64_t wblk;
+    uint32_t cblk[16];    // one block computed beyond the window (rare)
+    int64_t chave;
+    __device__ uint64_t at(uint64_t k) {
+        const uint64_t b = k >> 3;
+        uint32_t lo, hi;
+        if (b - wblk < (uint64_t)SPAN_WBLK) {
+            const uint32_t w = (uint32_t)(2 * (k - 8 * wblk));
+            lo = win[w];
+            hi = win[w + 1];
+        } else {
+            if ((int64_t)b != chave) {
+                chacha12_block(key, (uint32_t)b, cblk);
+                chave = (int64_t)b;
+            }
+            lo = cblk[2 * (k & 7)];
+            hi = cblk[2 * (k & 7) + 1];
+        }
+        return (uint64_t)hi << 32 | lo;
+    }
+};
+
+__device__ __forceinline__ double bits_f64(uint64_t b) { return __longlong_as_double((long long)b); }
+
+// the ziggurat's fast exit for the draw starting with `bits` (x in *x)
+__device__ __forceinline__ bool zig_fast(uint64_t bits, const double *__restrict__ ZX, double *x) {
+#pragma clang fp contract(off)
+    const int i = (int)(bits & 0xffu);
+    const double u = bits_f64((bits >> 12) | (1024ull << 52)) - 3.0;
+    *x = u * ZX[i];
+    return fabs(*x) < ZX[i + 1];
+}
+
+// The whole draw starting at stream word k: value and u64 words consumed.
+__device__ double zig_normal(SpanStream &s, uint64_t k, const double *__restrict__ ZX,
+                             const double *__restrict__ ZF, uint32_t *len) {
+#pragma clang fp contract(off)
+    const uint64_t k0 = k;
+    for (;;) {
+        const uint64_t bits = s.at(k++);
+        const int i = (int)(bits & 0xffu);
+        const double u = bits_f64((bits >> 12) | (1024ull << 52)) - 3.0;
+        const double x = u * ZX[i];
+        if (fabs(x) < ZX[i + 1]) {
+            *len = (uint32_t)(k - k0);
+            return x;
+        }
+        if (i == 0) {  // zero_case
+            double xt = 1.0, yt = 0.0;
+            while (-2.0 * yt < xt * xt) {
+                const double a = bits_f64((s.at(k++) >> 12) | (1023ull << 52)) - (1.0 - 0x1p-53);
+                const double c = bits_f64((s.at(k++) >> 12) | (1023ull << 52)) - (1.0 - 0x1p-53);
+                xt = log(a) / ZIG_R;
+                yt = log(c);
+            }
+            *len = (uint32_t)(k - k0);
+            return u < 0.0 ? xt - ZIG_R : ZIG_R - xt;
+        }
+        const double g = (double)(s.at(k++) >> 11) * 0x1p-53;
+        if (ZF[i + 1] + (ZF[i] - ZF[i + 1]) * g < exp(-x * x / 2.0)) {
+            *len = (uint32_t)(k - k0);
+            return x;
+        }
+    }
+}
+
+// `f as usize` (saturating; NaN and negatives 0), then min with n
+__device__ __forceinline__ uint32_t sat_draw(double d, int n) {
+    if (!(d > 0.0)) return 0u;
+    return d >= (double)n ? (uint32_t)n : (uint32_t)d;
+}
+
+// The round's draws (up to 128 = 64 passes) from stream word *spos on:
+// lanes compute the window's blocks and test every draw start for the fast
+// exit; a wave-uniform walk over the rare slow starts (each one's length from
+// the lane that owns it) finds which words start draws; draw d lands in
+// s_draw[d].  Returns the draws this round can use (even, >= 2) and advances
+// *spos past them.
+__device__ int span_draws_rand(SpanStream &s, uint64_t *spos, const double *__restrict__ ZX,
+                               const double *__restrict__ ZF, uint32_t *s_win, double *s_draw, uint16_t *s_dend) {
+    const int lane = lane_id();
+    const uint64_t p0 = *spos;
+    s.wblk = p0 >> 3;
+    s.chave = -1;
+    s.win = s_win;
+    if (lane < SPAN_WBLK) {
+        uint32_t o[16];
+        chacha12_block(s.key, (uint32_t)(s.wblk + (uint64_t)lane), o);
+#pragma unroll
+        for (int q = 0; q < 16; ++q) s_win[16 * lane + q] = o[q];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    // offsets o = lane, lane + 64 from p0: fast exit or the full draw
+    double v[2];
+    uint32_t L[2];
+    bool slow[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        slow[h] = !zig_fast(s.at(p0 + (uint64_t)(lane + 64 * h)), ZX, &v[h]);
+        L[h] = 1u;
+    }
+    const uint64_t m0 = __ballot(slow[0]), m1 = __ballot(slow[1]);
+    if (m0 | m1) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+            if (slow[h]) v[h] = zig_normal(s, p0 + (uint64_t)(lane + 64 * h), ZX, ZF, &L[h]);
+    }
+    // which offsets start draws: fast runs between slow starts; a slow start
+    // at o covers o .. o + L(o) - 1
+    uint64_t mem0 = ~0ull, mem1 = ~0ull;
+    uint32_t cur = 0;
+    uint64_t q0 = m0, q1 = m1;
+    while (q0 | q1) {
+        const uint32_t sl = q0 ? (uint32_t)__builtin_ctzll(q0) : 64u + (uint32_t)__builtin_ctzll(q1);
+        const uint32_t Ls = sl < 64 ? (uint32_t)__builtin_amdgcn_readlane((int)L[0], (int)sl)
+                                    : (uint32_t)__builtin_amdgcn_readlane((int)L[1], (int)(sl - 64));
+        const uint32_t nxt = sl + Ls;  // offsets sl + 1 .. nxt - 1 are consumed by this draw
+        for (uint32_t o = sl + 1; o < nxt && o < 128u; ++o) {  // (few words: a wedge test adds one)
+            if (o < 64) mem0 &= ~(1ull << o); else mem1 &= ~(1ull << (o - 64));
+        }
+        cur = nxt;
+        if (cur >= 128u) break;
+        // the next slow start at or after cur
+        q0 = cur < 64 ? m0 & (~0ull << cur) : 0ull;
+        q1 = cur < 64 ? m1 : (cur < 128 ? m1 & (~0ull << (cur - 64)) : 0ull);
+    }
+    (void)cur;
+    // draw numbers: members below each offset; draw d ends (relative) at o + L
+    const int n0 = __builtin_popcountll(mem0);
+    const int D = n0 + __builtin_popcountll(mem1);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const uint64_t mm = h ? mem1 : mem0;
+        if ((mm >> lane) & 1ull) {
+            const int d = (h ? n0 : 0) + __builtin_popcountll(mm & ((1ull << lane) - 1ull));
+            s_draw[d] = v[h];
+            s_dend[d] = (uint16_t)(lane + 64 * h + (int)L[h]);
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    int nd = D & ~1;
+    if (nd == 0) {  // (a slow draw at offset 0 ran past offset 128) one pass, drawn in order
+        if (lane == 0) {
+            uint32_t l1, l2;
+            s_draw[0] = zig_normal(s, p0, ZX, ZF, &l1);
+            s_draw[1] = zig_normal(s, p0 + l1, ZX, ZF, &l2);
+            s_dend[1] = (uint16_t)(l1 + l2);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        nd = 2;
+    }
+    return nd;
+}
+
+struct SpanPass {  // one pass of a round (LDS): cursors and lengths
+    uint32_t lp_gg;   // input cursor | gap ids written << 16
+    uint32_t ip_sz;   // id cursor | spanned ids written << 16
+    uint32_t ap;      // label cursor
+    uint32_t pass;    // pass index in the row
+};
+
+__device__ __forceinline__ void st_nt(int32_t *p, int32_t v) { __builtin_nontemporal_store(v, p); }
+
+template <int RAND>  // draws: 0 the Philox contract, 1 the row's StdRng (rng_mode 1)
 __global__ __launch_bounds__(256) void k_rows_span(RowParams P, const uint32_t *__restrict__ tok,
                                                    const uint32_t *__restrict__ rec_tok,
                                                    const uint32_t *__restrict__ rec_cnt,
                                                    const uint32_t *__restrict__ row_off,
                                                    const uint32_t *__restrict__ row_rec, SegSel sel,
                                                    int64_t rows_cap, RowOut out, uint32_t *__restrict__ err) {
+    __shared__ SpanPass s_pass[4][64];
+    __shared__ uint32_t s_win[4][SPAN_WBLK * 16];
+    __shared__ double s_draw[4][128];
+    __shared__ uint16_t s_dend[4][128];
     const int lane = lane_id();
     const int wid = (int)(threadIdx.x >> 6);
     const int S = P.S, LW = P.label_width;
     const RowSpan rs = row_span(sel, row_off, P.B, rows_cap);
     const int64_t G = rs.g_real;
+    SpanPass *sp = s_pass[wid];
     for (int64_t g = rs.g_lo + (int64_t)blockIdx.x * 4 + wid; g < rs.g_end; g += (int64_t)gridDim.x * 4) {
         int32_t *ids_o = out.input_ids + g * S;
         int32_t *am_o = out.attention_mask + g * S;
         int32_t *lb_o = out.labels + g * (int64_t)LW;
-        for (int j = lane; j < S; j += 64) am_o[j] = 1;  // attention stays 1 (the zeroing loop is empty)
+        for (int j = lane; j < S; j += 64) st_nt(am_o + j, 1);  // attention stays 1 (the zeroing loop is empty)
         if (g >= (int64_t)G) {
-            for (int j = lane; j < S; j += 64) ids_o[j] = 0;
-            for (int j = lane; j < LW; j += 64) lb_o[j] = -100;
+            for (int j = lane; j < S; j += 64) st_nt(ids_o + j, 0);
+            for (int j = lane; j < LW; j += 64) st_nt(lb_o + j, -100);
             continue;
         }
         const int64_t r = row_rec[g];
@@ -844,63 +1039,128 @@ __global__ __launch_bounds__(256) void k_rows_span(RowParams P, const uint32_t *
             if (f < P.n_pre + (int64_t)cnt) return (int32_t)tok[t0 + (f - P.n_pre)];
             return frame_id(P.post, (int)(f - P.n_pre - cnt));
         };
+        auto extra = [&](uint32_t q) -> int32_t { return P.extra_ids[q < 100u ? q : 99u]; };
         const uint64_t rec = P.first_record + (uint64_t)r;
+        SpanStream ss;
+        uint64_t spos = 0;
+        if (RAND) {
+            const uint32_t kk[8] = {(uint32_t)P.seed, (uint32_t)(P.seed >> 32), (uint32_t)rec, (uint32_t)(rec >> 32),
+                                    k, 0u, 0u, 0u};
+#pragma unroll
+            for (int q = 0; q < 8; ++q) ss.key[q] = kk[q];
+        }
         uint32_t bad = 0;
-        auto extra = [&](uint32_t q) -> int32_t {
-            if (q >= 100u) { ++bad; q = 99u; }
-            return P.extra_ids[q];
-        };
-        auto setlab = [&](int64_t i, int32_t v) {
-            if (i < LW) lb_o[i] = v;
-            else ++bad;
-        };
         int I0 = 0, A0 = 0;  // ids consumed / ids spanned before this round
         int lp_end = 0, ap_end = 0;
-        for (uint32_t p0 = 0;; p0 += 64) {
+        for (uint32_t p0 = 0;;) {
+            // ---- A. this round's passes ----
+            int np = 64;
+            uint32_t gr, sr;
+            if (RAND) {
+                np = span_draws_rand(ss, &spos, P.zig_x, P.zig_f, s_win[wid], s_draw[wid], s_dend[wid]) >> 1;
+                np = np < 64 ? np : 64;
+                gr = sat_draw(P.avg_span_gap - s_draw[wid][2 * (lane < np ? lane : 0)], n);
+                const uint32_t sz = sat_draw(P.avg_span_size - s_draw[wid][2 * (lane < np ? lane : 0) + 1], n);
+                sr = sz > 1u ? sz : 1u;  // std::cmp::max(distance as usize, 1)
+                spos += s_dend[wid][2 * np - 1];
+            } else {
+                const uint32_t p = p0 + (uint32_t)lane;
+                const uint4 c = philox4x32_10(make_uint4(p, k | 0x40000000u, (uint32_t)rec, (uint32_t)(rec >> 32)),
+                                              (uint32_t)P.seed, (uint32_t)(P.seed >> 32));
+                gr = span_pick(P.gap_kmin, P.gap_n, P.gap_thr, c.x);
+                sr = span_pick(P.size_kmin, P.size_n, P.size_thr, c.y);
+            }
+            const bool act = lane < np;
             const uint32_t p = p0 + (uint32_t)lane;
-            const uint4 c = philox4x32_10(make_uint4(p, k | 0x40000000u, (uint32_t)rec, (uint32_t)(rec >> 32)),
-                                          (uint32_t)P.seed, (uint32_t)(P.seed >> 32));
-            const uint32_t gr = span_pick(P.gap_kmin, P.gap_n, P.gap_thr, c.x);
-            const uint32_t sr = span_pick(P.size_kmin, P.size_n, P.size_thr, c.y);
             // saturate so the prefix sums cannot wrap (any value >= n ends the row)
-            const uint32_t gs = gr > (uint32_t)n ? (uint32_t)n : gr, ss = sr > (uint32_t)n ? (uint32_t)n : sr;
-            const uint32_t step = gs + ss;
-            const uint32_t incl = wave_incl_sum(step), incl_s = wave_incl_sum(ss);
+            const uint32_t gs = !act ? 0u : gr > (uint32_t)n ? (uint32_t)n : gr;
+            const uint32_t ss_ = !act ? 0u : sr > (uint32_t)n ? (uint32_t)n : sr;
+            const uint32_t step = gs + ss_;
+            const uint32_t incl = wave_incl_sum(step), incl_s = wave_incl_sum(ss_);
             const int Ip = I0 + (int)(incl - step);            // id cursor at the start of pass p
-            const int Ap = A0 + (int)(incl_s - ss);            // ids spanned before p
-            const bool last = Ip + (int)step >= n && Ip < n;   // the pass where ip reaches n
+            const int Ap = A0 + (int)(incl_s - ss_);           // ids spanned before p
+            const bool last = act && Ip + (int)step >= n && Ip < n;  // the pass where ip reaches n
             const uint64_t lm = __ballot(last);
-            const int Pl = lm ? __builtin_ctzll(lm) : 64;      // lane of the last pass (64: none this round)
-            if (lane <= Pl) {  // passes up to and including the last one write
-                const int lp = Ip - Ap + (int)p;  // input cursor
-                const int ap = Ap + (int)p;       // label cursor
-                const int gg = lane == Pl ? ((int)gs < n - Ip ? (int)gs : n - Ip) : (int)gs;
-                for (int j = 0; j < gg; ++j) ids_o[lp + j] = fid(Ip + j);
-                const int ip1 = Ip + gg;
-                const int sz = lane == Pl ? ((int)ss < n - ip1 ? (int)ss : n - ip1) : (int)ss;
+            const int Pl = lm ? __builtin_ctzll(lm) : 64;     // lane of the last pass (64: none this round)
+            const int nr = Pl < 64 ? Pl + 1 : np;             // passes written this round
+            const int lp = Ip - Ap + (int)p;                   // input cursor
+            const int ap = Ap + (int)p;                        // label cursor
+            const int gg = lane == Pl ? ((int)gs < n - Ip ? (int)gs : n - Ip) : (int)gs;
+            const int ip1 = Ip + gg;
+            const int sz = lane == Pl ? ((int)ss_ < n - ip1 ? (int)ss_ : n - ip1) : (int)ss_;
+            if (lane < nr) {
+                sp[lane] = SpanPass{(uint32_t)lp | (uint32_t)gg << 16, (uint32_t)Ip | (uint32_t)sz << 16, (uint32_t)ap, p};
+                // the reference's panics, counted: a sentinel index >= 100, label writes past S/4
                 if (sz > 0) {
-                    const int32_t e = extra(p);
-                    ids_o[lp + gg] = e;
-                    setlab(ap, e);
-                    for (int j = 0; j < sz; ++j) setlab(ap + 1 + j, fid(ip1 + j));
+                    bad += p >= 100u ? 1u : 0u;
+                    const int lo = ap > LW ? ap : LW, hi = ap + sz + 1;
+                    bad += hi > lo ? (uint32_t)(hi - lo) : 0u;
                 }
                 if (lane == Pl) {
-                    lp_end = lp + gg + (sz > 0 ? 1 : 0);
-                    ap_end = ap + (sz > 0 ? sz + 1 : 0);
-                    setlab(ap_end, extra(p + 1));
+                    bad += p + 1u >= 100u ? 1u : 0u;
+                    bad += ap + (sz > 0 ? sz + 1 : 0) >= LW ? 1u : 0u;
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            // ---- B. this round's positions ----
+            const int lpA = lane_bcast(lp, 0);
+            const int lpB = lane_bcast(lp + gg + (sz > 0 ? 1 : 0), nr - 1);
+            const int apA = lane_bcast(ap, 0);
+            const int apB = lane_bcast(ap + (sz > 0 ? sz + 1 : 0), nr - 1);
+            int own = 0;  // pass of the group's first position (wave-uniform)
+            for (int b = lpA; b < lpB; b += 64) {
+                const int q = b + lane;
+                int o = own;
+                for (int t = own + 1; t < nr; ++t) {
+                    const int st = lane_bcast(lp, t);
+                    if (st >= b + 64) break;
+                    o = q >= st ? t : o;
+                }
+                own = lane_bcast(o, 63);
+                if (q < lpB) {
+                    const SpanPass e = sp[o];
+                    const int off = q - (int)(e.lp_gg & 0xFFFFu);
+                    const int ge = (int)(e.lp_gg >> 16);
+                    st_nt(ids_o + q, off < ge ? fid((int)(e.ip_sz & 0xFFFFu) + off) : extra(e.pass));
+                }
+            }
+            own = 0;
+            const int apLim = apB < LW ? apB : LW;
+            for (int b = apA; b < apLim; b += 64) {
+                const int q = b + lane;
+                int o = own;
+                for (int t = own + 1; t < nr; ++t) {
+                    const int st = lane_bcast(ap, t);
+                    if (st >= b + 64) break;
+                    o = q >= st ? t : o;
+                }
+                own = lane_bcast(o, 63);
+                if (q < apLim) {
+                    const SpanPass e = sp[o];
+                    const int off = q - (int)e.ap;
+                    st_nt(lb_o + q, off == 0 ? extra(e.pass)
+                                            : fid((int)(e.ip_sz & 0xFFFFu) + (int)(e.lp_gg >> 16) + off - 1));
                 }
             }
             if (Pl < 64) {
-                lp_end = __shfl(lp_end, Pl, 64);
-                ap_end = __shfl(ap_end, Pl, 64);
+                lp_end = lpB;
+                ap_end = apB;
+                if (lane == 0 && ap_end < LW) st_nt(lb_o + ap_end, extra((uint32_t)lane_bcast((int)p, Pl) + 1u));
                 break;
             }
             I0 += (int)lane_bcast((int)incl, 63);
             A0 += (int)lane_bcast((int)incl_s, 63);
+            p0 += (uint32_t)np;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         }
-        for (int j = lp_end + lane; j < S; j += 64) ids_o[j] = 0;
-        for (int j = ap_end + 1 + lane; j < LW; j += 64) lb_o[j] = -100;
-        if (bad) atomicAdd(err, bad);
+        for (int j = lp_end + lane; j < S; j += 64) st_nt(ids_o + j, 0);
+        for (int j = ap_end + 1 + lane; j < LW; j += 64) st_nt(lb_o + j, -100);
+        for (int d = 32; d >= 1; d >>= 1) bad += __shfl_xor(bad, d, 64);
+        if (lane == 0 && bad) atomicAdd(err, bad);
     }
 }
 
@@ -908,14 +1168,19 @@ hipError_t launch_rows_span(const RowParams &P, const uint32_t *tok, const uint3
                             const uint32_t *row_off, const uint32_t *row_rec, SegSel sel, int64_t rows_cap,
                             RowOut out, uint32_t *err, hipStream_t st) {
     if (rows_cap == 0) return hipSuccess;
+    if (P.S > 65535 || (P.rng_mode == 1 && (!P.zig_x || !P.zig_f))) return hipErrorInvalidValue;
     const int64_t want = (rows_cap + 3) / 4;
     const unsigned grid = (unsigned)(want < 4096 ? want : 4096);
     if (sel.k == 0) {  // the error count covers the whole call
         hipError_t e = hipMemsetAsync(err, 0, sizeof(uint32_t), st);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(k_rows_span, dim3(grid), dim3(256), 0, st, P, tok, rec_tok, rec_cnt, row_off, row_rec, sel,
-                       rows_cap, out, err);
+    if (P.rng_mode == 1)
+        hipLaunchKernelGGL(k_rows_span<1>, dim3(grid), dim3(256), 0, st, P, tok, rec_tok, rec_cnt, row_off, row_rec,
+                           sel, rows_cap, out, err);
+    else
+        hipLaunchKernelGGL(k_rows_span<0>, dim3(grid), dim3(256), 0, st, P, tok, rec_tok, rec_cnt, row_off, row_rec,
+                           sel, rows_cap, out, err);
     return hipGetLastError();
 }
 

@@ -263,6 +263,7 @@ struct sdl_batcher {
     DevBuf<uint8_t> d_tnorm;
     DevBuf<uint32_t> d_trie;
     DevBuf<int32_t> d_extra;
+    DevBuf<double> d_zig;  // span rng_mode 1: ZIG_NORM_X then ZIG_NORM_F (257 each)
 
     // per-call workspace
     DevBuf<uint32_t> ranges, tokc, chunk_cnt, chunk_off, rec_local, tok_ids, rec_tok, rec_cnt, rec_rows, row_off,
@@ -690,6 +691,29 @@ void span_table(double avg, int lo, int32_t *kmin, int32_t *n, uint32_t *thr) {
     for (int j = m; j < 32; ++j) thr[j] = 0xFFFFFFFFu;
 }
 
+// rand_distr 0.4.3's ziggurat tables for StandardNormal (ZIG_NORM_X /
+// ZIG_NORM_F) as its ziggurat_tables.py writes them: 256 layers with
+// R = 3.6541528853610088, V = 0.00492867323399, x[i] = f^-1(V / x[i-1] +
+// f(x[i-1])), f(x) = exp(-x^2 / 2), each value printed with %.18f and read
+// back as the Rust literal.  (oracle/orc_batcher.c zig_tables is the checker's
+// restatement; tests/test_rand_mode.py pins the printed head of both.)
+void zig_norm_tables(double *X, double *F) {
+    const double R = 3.6541528853610088, V = 0.00492867323399;
+    auto f = [](double x) { return std::exp(-x * x / 2.0); };
+    double x[257];
+    x[0] = V / f(R);
+    x[1] = R;
+    for (int i = 2; i < 256; ++i) x[i] = std::sqrt(-2.0 * std::log(V / x[i - 1] + f(x[i - 1])));
+    x[256] = 0.0;
+    char buf[64];
+    for (int i = 0; i < 257; ++i) {
+        std::snprintf(buf, sizeof buf, "%.18f", x[i]);
+        X[i] = std::strtod(buf, nullptr);
+        std::snprintf(buf, sizeof buf, "%.18f", f(x[i]));
+        F[i] = std::strtod(buf, nullptr);
+    }
+}
+
 std::string default_data_dir() {
     Dl_info info;
     if (dladdr((void *)&default_data_dir, &info) && info.dli_fname) {
@@ -885,6 +909,16 @@ int sdl_batcher_create(const sdl_config *cfg, const char *tokenizer_path, const 
             span_table(cfg->avg_span_gap, 0, &P.gap_kmin, &P.gap_n, P.gap_thr);
             span_table(cfg->avg_span_size, 1, &P.size_kmin, &P.size_n, P.size_thr);
             P.extra_ids = h->d_extra.p;
+            P.avg_span_gap = cfg->avg_span_gap;
+            P.avg_span_size = cfg->avg_span_size;
+            if (cfg->rng_mode == 1) {  // random_data_gap / random_data_size on the row's StdRng
+                std::vector<double> zt(2 * 257);
+                zig_norm_tables(zt.data(), zt.data() + 257);
+                h->d_zig.ensure(zt.size());
+                HIP_TRY(hipMemcpy(h->d_zig.p, zt.data(), zt.size() * 8, hipMemcpyHostToDevice));
+                P.zig_x = h->d_zig.p;
+                P.zig_f = h->d_zig.p + 257;
+            }
         }
         if (cfg->task == SDL_TASK_MULTI_LABEL || cfg->task == SDL_TASK_SINGLE_CLASS) {  // SimpleBatcher: one row per record, no filter
             P.chunk = 0;

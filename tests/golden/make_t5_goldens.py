@@ -13,7 +13,11 @@
                     the fixture stream at seq_len=128, batch=8, then the
                     end-of-stream flush (gen_batcher.rs:69-98,
                     t5_data.rs:162-226), under the RNG contract,
-                    from the pure-Python restatement below.
+                    from the pure-Python restatement below;
+  span_rand_s128_b8.npz  the same in rng_mode 1: each row's gap / size draws are
+                    rand_distr StandardNormal samples of StdRng::from_seed(seed |
+                    record | chunk) (randref.py, pinned by rand_distr's
+                    value-stability vector).
 
 Run in the build container:  python tests/golden/make_t5_goldens.py
 """
@@ -32,6 +36,7 @@ REPO = os.path.dirname(os.path.dirname(HERE))
 ASSET = os.path.join(REPO, "streaming_data_loader_amd", "assets", "t5_proxy", "tokenizer.json")
 sys.path.insert(0, HERE)
 from make_goldens import philox4x32_10, records  # noqa: E402
+from randref import StdRng, row_seed, sat_usize, std_normal  # noqa: E402
 
 M32 = 0xFFFFFFFF
 
@@ -84,8 +89,9 @@ def span_pick(tab, x):
 class PySpan:
     """GenTokenizer(chunk=true) + T5Data (Span) restated in Python."""
 
-    def __init__(self, tok, B, S, seed, gap=16.0, size=2.0):
+    def __init__(self, tok, B, S, seed, gap=16.0, size=2.0, rng_mode=0):
         self.tok, self.B, self.S, self.seed = tok, B, S, seed
+        self.rng_mode, self.avg_gap, self.avg_size = rng_mode, gap, size
         self.eos = tok.token_to_id("</s>")
         self.extra = [tok.token_to_id(f"<extra_id_{k}>") for k in range(100)]
         self.gap, self.size = span_table(gap, 0), span_table(size, 1)
@@ -110,13 +116,19 @@ class PySpan:
 
         ip = lp = ap = 0
         p = 0
+        rng = StdRng(row_seed(self.seed, rec, chunk)) if self.rng_mode == 1 else None
         while lp < S:
-            xg, xs = philox4x32_10([p, chunk | 0x40000000, rec & M32, rec >> 32], self.seed & M32, self.seed >> 32)[:2]
-            g = min(span_pick(self.gap, xg), S - lp, n - ip)
+            if rng is None:
+                xg, xs = philox4x32_10([p, chunk | 0x40000000, rec & M32, rec >> 32], self.seed & M32, self.seed >> 32)[:2]
+                g = span_pick(self.gap, xg)
+            else:  # rng_mode 1: random_data_gap / random_data_size on the row's StdRng (t5_data.rs:165-176)
+                g = sat_usize(self.avg_gap - std_normal(rng))
+            g = min(g, S - lp, n - ip)
             inp[lp:lp + g] = ids[ip:ip + g]
             lp += g
             ip += g
-            s = min(span_pick(self.size, xs), S - lp, n - ip)
+            s = span_pick(self.size, xs) if rng is None else max(sat_usize(self.avg_size - std_normal(rng)), 1)
+            s = min(s, S - lp, n - ip)
             if s > 0:
                 inp[lp] = self.extra[p]
                 setlab(ap, self.extra[p])
@@ -161,7 +173,12 @@ def main():
         json.dump({"generator": "tokenizers " + __import__("tokenizers").__version__ + ", regex " + regex.__version__,
                    "asset": "streaming_data_loader_amd/assets/t5_proxy/tokenizer.json",
                    "n_fixture_records": len(recs), "cases": cases}, f, ensure_ascii=False)
-    ps = PySpan(tok, 8, 128, seed=1234)
+    for mode, name in ((0, "span_s128_b8.npz"), (1, "span_rand_s128_b8.npz")):
+        write_span_batches(tok, recs, mode, name)
+
+
+def write_span_batches(tok, recs, rng_mode, name):
+    ps = PySpan(tok, 8, 128, seed=1234, rng_mode=rng_mode)
     out = [b for b in (ps.create_sync_batch(t) for t in recs) if b is not None]
     out.append(ps.get_working_batch())
     arrs = {}
@@ -173,8 +190,8 @@ def main():
     arrs["span_errors"] = np.int64(ps.errors)
     arrs["gap_table"] = np.array([ps.gap[0]] + ps.gap[1], np.int64)
     arrs["size_table"] = np.array([ps.size[0]] + ps.size[1], np.int64)
-    np.savez_compressed(os.path.join(HERE, "span_s128_b8.npz"), **arrs)
-    print(f"{len(cases)} id cases, {len(out)} span batches (last has {out[-1]['index']} rows), "
+    np.savez_compressed(os.path.join(HERE, name), **arrs)
+    print(f"{name}: {len(out)} span batches (last has {out[-1]['index']} rows), "
           f"{ps.errors} label overflows", file=sys.stderr)
 
 

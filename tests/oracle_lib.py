@@ -88,6 +88,10 @@ def lib():
         L.orc_pickle_dataset.restype = ctypes.c_size_t
         L.orc_pickle_dataset.argtypes = [ctypes.c_int] * 5 + [vp] * 5 + [vp, ctypes.c_size_t]
         L.orc_batcher_span_errors.restype = ctypes.c_uint64
+        L.orc_normal_pcg32.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int, vp]
+        L.orc_normal_pcg32.restype = None
+        L.orc_normal_row.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int, vp]
+        L.orc_normal_row.restype = None
         L.orc_json_number.restype = ctypes.c_int
         L.orc_json_number.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_double)]
         _lib = L

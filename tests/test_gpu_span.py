@@ -118,10 +118,13 @@ def test_chunk_boundaries(torch, native_lib, t5tok, shift):
         assert g == t5tok.encode(b)
 
 
-def test_span_stream_matches_golden(native_lib, records):
-    """GenTokenizer + T5Data at seq_len 128, batch 8 over the fixture stream."""
-    g = np.load(os.path.join(GOLDEN, "span_s128_b8.npz"))
-    cfg = B.get_case(B.TaskType.Span, test=False, sequence_length=128, batch_size=8, seed=1234)
+@pytest.mark.parametrize("rng_mode,golden", [(0, "span_s128_b8.npz"), (1, "span_rand_s128_b8.npz")])
+def test_span_stream_matches_golden(native_lib, records, rng_mode, golden):
+    """GenTokenizer + T5Data at seq_len 128, batch 8 over the fixture stream
+    (rng_mode 1: the golden's draws are rand_distr StandardNormal samples of
+    each row's StdRng, tests/golden/randref.py)."""
+    g = np.load(os.path.join(GOLDEN, golden))
+    cfg = B.get_case(B.TaskType.Span, test=False, sequence_length=128, batch_size=8, seed=1234, rng_mode=rng_mode)
     gt = B.GenTokenizer.from_config(cfg)
     got = [b for b in (gt.create_sync_batch(t) for t in records) if b is not None]
     got.append(gt.get_working_batch())
@@ -135,9 +138,9 @@ def test_span_stream_matches_golden(native_lib, records):
     assert set(got[0].to_dict()) == {"input_ids", "attention_mask", "labels"}
 
 
-def oracle_span_rows(t5tok, blobs, B_, S, seed, gap=16.0, size=2.0, first_record=0):
+def oracle_span_rows(t5tok, blobs, B_, S, seed, gap=16.0, size=2.0, first_record=0, rng_mode=0):
     ob = oracle_lib.OracleBatcherEx(oracle_lib.Encoder("t5", t5tok), oracle_lib.SPAN, B_, S, seed=seed,
-                                    avg_span_gap=gap, avg_span_size=size)
+                                    avg_span_gap=gap, avg_span_size=size, rng_mode=rng_mode)
     ob.set_next_record(first_record)
     want = [r for r in (ob.push(b) for b in blobs) if r is not None]
     while True:
@@ -149,23 +152,26 @@ def oracle_span_rows(t5tok, blobs, B_, S, seed, gap=16.0, size=2.0, first_record
     return cat, ob.span_errors()
 
 
+@pytest.mark.parametrize("rng_mode", [0, 1])
 @pytest.mark.parametrize("S,B_,gap,size", [(512, 256, 16.0, 2.0), (128, 8, 16.0, 2.0), (512, 64, 3.0, 3.0),
-                                           (64, 16, 1.0, 1.0)])
-def test_span_rows_match_oracle(torch, native_lib, t5tok, records, S, B_, gap, size):
+                                           (64, 16, 1.0, 1.0), (1024, 32, 0.5, 0.2), (256, 16, 200.0, 9.0)])
+def test_span_rows_match_oracle(torch, native_lib, t5tok, records, S, B_, gap, size, rng_mode):
     """BASELINE configs[2] (span, S=512, B=256) and other span configs -- some
-    overflowing the S/4 label width -- on a seeded permutation of the fixture
-    plus hard records, every row vs the oracle Batcher, pad rows included."""
+    overflowing the S/4 label width or the 100 sentinels, some with gaps of
+    several 64-position groups -- on a seeded permutation of the fixture plus
+    hard records, every row vs the oracle Batcher, pad rows included; in both
+    RNG modes (1: rand_distr StandardNormal draws on the row's StdRng)."""
     rng = random.Random(S + B_)
     blobs = [r.encode() for r in records] * 4 + hard_blobs(11, 150)
     rng.shuffle(blobs)
     db = DeviceBatcher(task=native.SDL_TASK_SPAN, batch_size=B_, sequence_length=S, seed=77,
-                       tokenizer=native.T5_PROXY_TOKENIZER, avg_span_gap=gap, avg_span_size=size)
+                       tokenizer=native.T5_PROXY_TOKENIZER, avg_span_gap=gap, avg_span_size=size, rng_mode=rng_mode)
     res = run(torch, db, blobs, first_record=5)
     G = res.rows()
     n_pad = (-G) % B_
     ids, am, tt, lab = res.planes(G + n_pad)
     assert tt is None and lab.shape[1] == S // 4
-    want, errs = oracle_span_rows(t5tok, blobs, B_, S, 77, gap, size, first_record=5)
+    want, errs = oracle_span_rows(t5tok, blobs, B_, S, 77, gap, size, first_record=5, rng_mode=rng_mode)
     assert G == want["input_ids"].shape[0]
     np.testing.assert_array_equal(ids[:G], want["input_ids"])
     np.testing.assert_array_equal(am[:G], want["attention_mask"])

@@ -12,6 +12,14 @@ pieces it is built from:
   - gen_index / gen_range(0..n) / shuffle: rand's value_stability_slice
     (Pcg32 test rng seeded 414, 13 elements), through the pure-Python
     restatement below, which then checks the C oracle's positions.
+The span mode (rng_mode = 1 with task span): T5Data::put_data's
+random_data_gap / random_data_size (rust/src/models/t5_data.rs:165-176) draw
+rand_distr 0.4.3 StandardNormal f64 samples from the same per-row StdRng, gap
+then size per pass.  The ziggurat restatement (oracle/orc_batcher.c
+std_normal, tests/golden/randref.py) is pinned by rand_distr's value-stability
+vector (tests/value_stability.rs normal_distributions_stability, seed 213 of
+its Pcg32 test rng); the tail and wedge exits are exercised beyond it by the
+two restatements agreeing on long streams.
 The device path is checked against the oracle in test_gpu_rand_mode.py.
 """
 import ctypes
@@ -185,3 +193,61 @@ def test_oracle_rand_rows_exact(oracle_tok, records):
         np.testing.assert_array_equal(labs, want_lab)
         checked += 1
     assert checked >= 20
+
+
+# ---- span: rand_distr StandardNormal over the row's StdRng ------------------------
+import randref  # noqa: E402  (tests/golden on sys.path via conftest)
+
+RAND_DISTR_NORMAL_213 = [-0.11844188827977231, 0.7813779637772346, 0.06563993969580051, -1.1932899004186373]
+
+
+def test_standard_normal_value_stability():
+    """rand_distr 0.4.3 tests/value_stability.rs: StandardNormal f64 from
+    Pcg32::new(213, 11634580027462260723) -- bit for bit, both restatements."""
+    r = randref.Pcg32(213, 11634580027462260723)
+    assert [randref.std_normal(r) for _ in range(4)] == RAND_DISTR_NORMAL_213
+    out = np.zeros(4)
+    oracle_lib.lib().orc_normal_pcg32(213, 11634580027462260723, 4, out.ctypes.data)
+    assert out.tolist() == RAND_DISTR_NORMAL_213
+    # Normal::new(2.0, 0.5) of the same draws (mean + std * z), as the vector file lists
+    assert [2.0 + 0.5 * z for z in RAND_DISTR_NORMAL_213][0] == 1.940779055860114
+
+
+def test_ziggurat_tables_published_head():
+    """The first entries of rand_distr's ziggurat_tables.rs as printed there (%.18f)."""
+    assert randref.ZX[:4] == [3.910757959537090045, 3.654152885361008796, 3.449278298560964462, 3.320244733839166074]
+    assert randref.ZF[:3] == [0.000477467764586655, 0.001260285930498598, 0.002609072746106363]
+    assert randref.ZX[256] == 0.0 and randref.ZF[256] == 1.0
+
+
+def test_oracle_row_normals_match_restatement():
+    """Long per-row streams (every exit of the ziggurat taken) agree bit for bit."""
+    stats = {}
+    for seed, rec, chunk in ((1234, 0, 0), (1234, 17, 3), (2 ** 63 + 5, 10 ** 7 + 11, 1)):
+        n = 30000
+        r = randref.StdRng(randref.row_seed(seed, rec, chunk))
+        want = [randref.std_normal(r, stats) for _ in range(n)]
+        got = np.zeros(n)
+        oracle_lib.lib().orc_normal_row(seed, rec, chunk, n, got.ctypes.data)
+        assert got.tolist() == want, (seed, rec, chunk)
+    assert stats["tail"] > 0 and stats["wedge"] > 50 and stats["retry"] > 50, stats
+    z = np.array(want)
+    assert abs(z.mean()) < 0.03 and abs(z.std() - 1.0) < 0.03
+
+
+def test_oracle_span_rand_batches_match_golden(records):
+    """GenTokenizer + T5Data in rng_mode 1 at S=128 B=8 over the fixture stream
+    vs tests/golden/span_rand_s128_b8.npz (ids from tokenizers, draws from randref)."""
+    g = np.load(os.path.join(GOLDEN, "span_rand_s128_b8.npz"))
+    tok = oracle_lib.T5Tok()
+    ob = oracle_lib.OracleBatcherEx(oracle_lib.Encoder("t5", tok), oracle_lib.SPAN, 8, 128, seed=1234, rng_mode=1)
+    got = [r for r in (ob.push(t) for t in records) if r is not None]
+    got.append(ob.flush())
+    assert len(got) == int(g["n_batches"])
+    for i, r in enumerate(got):
+        assert r["rows"] == int(g[f"b{i}_rows"])
+        for k in ("input_ids", "attention_mask", "labels"):
+            np.testing.assert_array_equal(r[k], g[f"b{i}_{k}"], err_msg=f"batch {i} {k}")
+    assert ob.span_errors() == int(g["span_errors"])
+    philox = np.load(os.path.join(GOLDEN, "span_s128_b8.npz"))
+    assert not np.array_equal(philox["b0_labels"], g["b0_labels"])
