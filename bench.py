@@ -215,23 +215,24 @@ VALU_ISSUE_PEAK = 256 * 4 * 2.4e9 / 2  # wave64 VALU instr/s: 256 CUs x 4 SIMD32
 SALU_ISSUE_PEAK = 256 * 2.4e9  # scalar instr/s: one scalar unit per CU issuing one per cycle
 
 
-def pmc_path(task, arena_mib):
-    return os.path.join(PMC_DIR, f"{task}_{arena_mib}mib.json")
+def pmc_path(task, arena_mib, corpus="fixture"):
+    return os.path.join(PMC_DIR, f"{task}_{arena_mib}mib" + ("" if corpus == "fixture" else f"_{corpus}") + ".json")
 
 
-def load_pmc(task, arena_mib, kernel):
+def load_pmc(task, arena_mib, kernel, corpus="fixture"):
     """The committed rocprofv3 --pmc summary of `kernel` (tools/pmc.sh +
-    tools/pmc_summary.py) for THIS task and arena size, or (None, reason).
-    Counters of another task or arena never describe the timed launch, so they
-    are not used."""
-    p = pmc_path(task, arena_mib)
+    tools/pmc_summary.py) for THIS task, arena size and corpus, or (None,
+    reason).  Counters of another task, arena or corpus never describe the
+    timed launch, so they are not used."""
+    p = pmc_path(task, arena_mib, corpus)
     if not os.path.exists(p):
-        return None, f"no PMC summary for task={task} arena={arena_mib} MiB ({os.path.relpath(p, REPO)})"
+        return None, f"no PMC summary for task={task} arena={arena_mib} MiB corpus={corpus} ({os.path.relpath(p, REPO)})"
     try:
         with open(p) as f:
             d = json.load(f)
-        if d.get("task") != task or int(d.get("arena_mib", -1)) != arena_mib:
-            return None, f"{os.path.relpath(p, REPO)} was collected for task={d.get('task')} arena={d.get('arena_mib')}"
+        if d.get("task") != task or int(d.get("arena_mib", -1)) != arena_mib or d.get("corpus", "fixture") != corpus:
+            return None, (f"{os.path.relpath(p, REPO)} was collected for task={d.get('task')} "
+                          f"arena={d.get('arena_mib')} corpus={d.get('corpus', 'fixture')}")
         k = d["kernels"]["sdl::" + kernel]
         k["_file"] = os.path.relpath(p, REPO)
         return k, None
@@ -278,10 +279,12 @@ def parse_args(argv=None):
     ap.add_argument("--arena-mib", type=int, default=256)
     ap.add_argument("--corpus", default="fixture", choices=["fixture", "heldout"],
                     help="fixture: data/test.json.gz records tiled (default); heldout: English text on the image "
-                         "never used to build or tune the tables (tests/golden/heldout_records.jsonl)")
+                         "the proxy vocabularies were not trained on (tests/golden/heldout_records.jsonl; "
+                         "a second kernel-tuning corpus, not an untouched one)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--rng-mode", type=int, default=0, choices=[0, 1],
-                    help="MLM masks: 0 the Philox contract (default), 1 rand 0.8.5 StdRng per row")
+                    help="0 the Philox contract (default); 1 the reference's own draws on a per-row StdRng: "
+                         "rand 0.8.5 shuffle (mlm masks), rand_distr StandardNormal (span gaps / sizes)")
     ap.add_argument("--e2e", action="store_true", help="also time the host record path (H2D + kernels + D2H)")
     ap.add_argument("--json", action="store_true",
                     help="also time the provider's JsonText filter on the device (JSON lines -> text arena)")
@@ -321,14 +324,19 @@ def launch_ranks(n, argv):
                    MASTER_ADDR=os.environ.get("MASTER_ADDR", "127.0.0.1"), MASTER_PORT=port)
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
     rc = 0
-    for p in procs:
-        c = p.wait()
-        if c != 0 and rc == 0:
-            rc = c
-    if rc:  # a rank failed: do not leave its peers waiting in a barrier
-        for p in procs:
-            if p.poll() is None:
-                p.kill()
+    live = list(procs)
+    while live:  # poll every rank: one that fails must not leave its peers waiting in a barrier
+        for p in list(live):
+            c = p.poll()
+            if c is None:
+                continue
+            live.remove(p)
+            if c != 0 and rc == 0:
+                rc = c
+                for q in live:
+                    q.kill()
+        if live:
+            time.sleep(0.05)
     return rc
 
 
@@ -364,7 +372,8 @@ def base_line(args, world, step_ms, value, task, N, R, rows, toks):
         "warmup": args.warmup, "ms_per_step": round(step_ms, 4), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "u8->int32",
         "data": ("synthetic: data/test.json.gz records tiled (seeded)" if args.corpus == "fixture" else
-                 "synthetic: held-out English text on the image (never used for tuning) tiled (seeded)"),
+                 "synthetic: held-out English text on the image (not in the proxy vocabularies' training text; "
+                 "also used to tune kernels) tiled (seeded)"),
         "config": {"workload": f"{task['workload']}, one step = one rank's {args.arena_mib} MiB text arena -> "
                                "all packed batches",
                    "task": args.task, "seq_len": S, "batch": B, "corpus": args.corpus,
@@ -374,8 +383,9 @@ def base_line(args, world, step_ms, value, task, N, R, rows, toks):
                                  "t5": "t5-small layout (Precompiled nmt_nfkc + Unigram), offline proxy vocab (32,100)"}
                                 .get(task["tok"], "bert-base-uncased layout, offline proxy vocab (30,522)"),
                    "parallelism": f"record shards x{world}, no collective",
-                   "mlm_masks": "rand 0.8.5 StdRng per row (rng_mode 1)" if getattr(args, "rng_mode", 0) == 1
-                                else "Philox contract (rng_mode 0)"},
+                   "rng": ("rng_mode 1: the reference's draws on a per-row StdRng (rand 0.8.5 shuffle for mlm "
+                           "masks, rand_distr 0.4.3 StandardNormal for span gaps / sizes)"
+                           if getattr(args, "rng_mode", 0) == 1 else "rng_mode 0: the Philox contract (DESIGN.md §3)")},
     }
 
 
@@ -523,15 +533,22 @@ def main(argv=None):
     # whole path, per step: text + offsets + the int32 [rows, S] planes
     path_bytes = N + 8 * (R + 1) + int(4 * task["planes"] * rows * S)
     line = base_line(args, world, step_ms, value, task, N, R, rows, toks)
-    pmc, pmc_note = load_pmc(args.task, args.arena_mib, task["kernel"]) if args.corpus == "fixture" else \
-        (None, "PMC summaries are collected on the fixture corpus")
+    pmc, pmc_note = load_pmc(args.task, args.arena_mib, task["kernel"], args.corpus)
     traffic, issue = None, None
     if pmc is not None:
         traffic, issue, pmc_note = pmc_roofline(pmc, tok_ms, tok_bytes)
-    line["roofline"] = {"bound": "hbm", "kernel": task["kernel"], "achieved": round(achieved, 2),
-                        "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 5),
+    # achieved / peak / frac are against HBM (the metric's roofline); `bound`
+    # names the roofline that binds the kernel: the busier issue unit when the
+    # PMC summary shows it closer to its peak than HBM traffic is to its own
+    hbm_frac = achieved / HBM_PEAK_GBPS
+    bound = issue["bound"] if issue is not None and issue["frac"] > hbm_frac else "hbm"
+    line["roofline"] = {"bound": bound, "kernel": task["kernel"], "achieved": round(achieved, 2),
+                        "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(hbm_frac, 5),
                         "traffic": traffic, "issue": issue,
                         "algorithmic_bytes_per_launch": tok_bytes, "avg_launch_ms": round(tok_ms, 4)}
+    if bound != "hbm":
+        line["roofline"]["bound_note"] = (f"{bound} at {issue['frac']:.2f} of its issue peak binds this kernel; "
+                                          "achieved/peak/frac are its algorithmic HBM bytes against 8 TB/s")
     if pmc_note:
         line["roofline"]["pmc_note"] = pmc_note
     line["stage_ms"] = {k: round(v, 4) for k, v in stage_ms.items()}

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define SDL_ABI_VERSION 7
+#define SDL_ABI_VERSION 8
 
 enum {
     SDL_OK = 0,

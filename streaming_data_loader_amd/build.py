@@ -77,6 +77,7 @@ def build(verbose=False, force=False, jobs=4, defines=(), lib=None, build_dir=No
     lib = lib or LIB
     bdir = build_dir or BUILD
     os.makedirs(bdir, exist_ok=True)
+    os.makedirs(os.path.dirname(lib), exist_ok=True)
     want = source_hash(defines)
     if not force and embedded_id(lib) == want:
         return lib

@@ -49,7 +49,9 @@ constexpr int LB = 10, DB = 10;    // primary table bits: lit/len, dist (long_de
 constexpr int IN_STAGE = SDL_GZ_STAGE;  // staged compressed bytes per wave
 constexpr int OBUF = SDL_GZ_OBUF;       // output batch bytes
 constexpr int MLCAP = OBUF / 8;         // matches per batch
+#ifndef SDL_GZ_ALLOW_SMALL_OBUF  // (diagnostic builds only: exercises the no-progress exit below)
 static_assert(OBUF >= 512, "a batch must take any 258-byte match (else an empty batch never fills: no progress)");
+#endif
 constexpr int HDR_ROOM = 640;      // a block header (<= ~600 B) fits in this many staged bytes
 constexpr int NSYM = 320;          // lit/len (<= 288) + dist (<= 32) code lengths
 constexpr uint32_t POLY = 0xEDB88320u;
@@ -275,7 +277,17 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t *__restrict__ in, 
     uint32_t produced = 0, nb = 0, nm = 0;  // wave-uniform
     bool in_block = false, final_seen = false;
     uint32_t limL[5], baseL[5], limD[5], baseD[5];  // long codes (11..15 bits) of the block, long_decode
+    // Every pass consumes bits, flushes a non-empty batch or restages, so a
+    // member takes fewer than 4 (8 mlen + cap) + 64 passes; the cap and the
+    // explicit no-progress test below turn a decoder bug or an unforeseen
+    // input into GZ_E_STALL instead of a wave that never finishes.
+    const uint64_t pass_cap = 4ull * (8ull * (uint64_t)mlen + (uint64_t)cap) + 64ull;
+    uint64_t passes = 0;  // wave-uniform
     for (;;) {
+        if (++passes > pass_cap) {
+            if (lane == 0) err = GZ_E_STALL;
+            break;
+        }
         if (!in_block) {
             if (final_seen) break;
             if (bp > 8u * (IN_STAGE - HDR_ROOM)) {
@@ -579,6 +591,10 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t *__restrict__ in, 
         }
         if (stop == 3) {  // an invalid code on the chain
             if (lane == 0) err = GZ_E_CODE;
+            break;
+        }
+        if (stop == 2 && q == 0 && nb == 0) {  // the first token does not fit an empty batch: no progress
+            if (lane == 0) err = GZ_E_STALL;
             break;
         }
         const uint32_t nmat = (uint32_t)__popcll(mb0 & M0) + (uint32_t)__popcll(mb1 & M1);

@@ -93,7 +93,8 @@ enum : int32_t {
     GZ_E_OVER = 10,   // more output than the trailer's ISIZE
     GZ_E_SIZE = 11,   // output length != ISIZE
     GZ_E_TRAIL = 12,  // bytes after the member's trailer
-    GZ_E_CRC = 13     // CRC-32 mismatch
+    GZ_E_CRC = 13,    // CRC-32 mismatch
+    GZ_E_STALL = 14   // the decoder made no progress (a guard: unreachable with the shipped batch size)
 };
 struct X2N {
     uint32_t t[32];  // x^(2^k) mod P (zlib's x2n_table)

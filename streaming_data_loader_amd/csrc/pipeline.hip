@@ -616,9 +616,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SDL_ROWS_WA
 // One wave per row: lanes compute the ChaCha12 blocks of the S-1 draws the
 // shuffle takes when nothing is rejected and every swap's index j_i at once;
 // a rejection anywhere in the row (probability ~S^2 / 2^32) sends lane 0 through
-// the draws in order.  The first mask_length shuffled positions follow each
-// x < mask_length back through the swaps (last applied first): a lane per x,
-// the S-1 swap indices read from LDS.  Output: the row's mask bits.
+// the draws in order.  mask_batch only uses the SET of the first k shuffled
+// positions, and Fisher-Yates from the end never moves a value out of
+// [0, k) once steps i < k begin (j_i <= i), so the set is what [0, k) holds
+// after steps S-1 .. k.  The value at position p just before step p came from
+// the latest earlier swap into p -- step next(p) = min{i > p : j_i = p,
+// j_i != i} -- so it is val(next(p)), or p if there was none; and [0, k)
+// receives val(min{i >= k : j_i = x}) at each x.  next() is one LDS atomicMin
+// per step; each x then follows a chain of ~2 hops (S=512, k=76) instead of
+// tracing through all S-1 swaps.  Output: the row's mask bits.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
 #define CC_QR(a, b, c, d)                                                         \
@@ -646,10 +652,12 @@ __global__ __launch_bounds__(64) void k_mask_rand(RowParams P, const uint32_t *_
     __shared__ uint32_t s_draw[RAND_MAX_S + 16];
     __shared__ uint16_t s_j[RAND_MAX_S];
     __shared__ uint32_t s_bits[RAND_MAX_S / 32];
+    uint32_t *const s_next = s_draw;  // next(p), once the draws are spent
     const int lane = lane_id();
     const int S = P.S, W = (S + 31) >> 5, kmask = P.mask_length < S ? P.mask_length : S;
     const int nblk = (S - 1 + 15) >> 4;
     const RowSpan rs = row_span(sel, row_off, P.B, rows_cap);
+    constexpr uint32_t NONE = 0xFFFFFFFFu;
     for (int64_t g = rs.g_lo + blockIdx.x; g < (int64_t)rs.g_real; g += gridDim.x) {
         const int64_t r = row_rec[g];
         const uint32_t chunk = (uint32_t)(g - row_off[r]);
@@ -702,16 +710,20 @@ __global__ __launch_bounds__(64) void k_mask_rand(RowParams P, const uint32_t *_
             }
         }
         __syncthreads();
-        // the first kmask shuffled positions: x traced back through swaps 1 .. S-1
-        for (int x0 = 0; x0 < kmask; x0 += 128) {
-            int p0 = x0 + lane, p1 = x0 + 64 + lane;
-            for (int i = 1; i < S; ++i) {
-                const int ji = s_j[i];
-                p0 = p0 == i ? ji : p0 == ji ? i : p0;
-                p1 = p1 == i ? ji : p1 == ji ? i : p1;
-            }
-            if (x0 + lane < kmask) atomicOr(&s_bits[p0 >> 5], 1u << (p0 & 31));
-            if (x0 + 64 + lane < kmask) atomicOr(&s_bits[p1 >> 5], 1u << (p1 & 31));
+        for (int p = lane; p < S; p += 64) s_next[p] = NONE;
+        __syncthreads();
+        // next(p): the latest swap into p among steps i >= k (a self swap moves nothing)
+        const int i0 = kmask > 1 ? kmask : 1;
+        for (int i = i0 + lane; i < S; i += 64) {
+            const int j = s_j[i];
+            if (j != i) atomicMin(&s_next[j], (uint32_t)i);
+        }
+        __syncthreads();
+        // [0, k) holds val(next(x)) (or x): follow each chain to its end
+        for (int x = lane; x < kmask; x += 64) {
+            uint32_t p = (uint32_t)x;
+            for (uint32_t q = s_next[p]; q != NONE; q = s_next[p]) p = q;
+            atomicOr(&s_bits[p >> 5], 1u << (p & 31));
         }
         __syncthreads();
         uint32_t *dst = bits + g * (int64_t)W;

@@ -1184,7 +1184,8 @@ const char *gz_reason(int32_t s) {
                                   "more output than the trailer's size",
                                   "incorrect length check",
                                   "bytes after the member's trailer",
-                                  "incorrect data check"};
+                                  "incorrect data check",
+                                  "decoder made no progress"};
     return s >= 0 && s < (int32_t)(sizeof(names) / sizeof(names[0])) ? names[s] : "unknown";
 }
 

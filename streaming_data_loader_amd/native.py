@@ -95,7 +95,7 @@ class Inflated(ctypes.Structure):
 
 # per-member status codes of sdl_gzip_inflate_device (csrc/kernels.hpp GZ_*)
 GZ_OK, GZ_E_RANGE, GZ_E_TRUNC, GZ_E_HEADER, GZ_E_HCRC, GZ_E_BTYPE, GZ_E_STORED, GZ_E_CODES, GZ_E_CODE, \
-    GZ_E_FAR, GZ_E_OVER, GZ_E_SIZE, GZ_E_TRAIL, GZ_E_CRC = range(14)
+    GZ_E_FAR, GZ_E_OVER, GZ_E_SIZE, GZ_E_TRAIL, GZ_E_CRC, GZ_E_STALL = range(15)
 SDL_ERR_DATA = -8
 
 
@@ -128,9 +128,11 @@ def load(path=LIB_PATH):
     except Exception:
         pass
     L = ctypes.CDLL(path)
-    L.sdl_build_id.restype = ctypes.c_char_p
-    L.sdl_build_id.argtypes = []
-    if os.path.abspath(path) == os.path.join(PKG, "libsdl_batcher.so"):
+    product = os.path.abspath(path) == os.path.join(PKG, "libsdl_batcher.so")
+    if product or hasattr(L, "sdl_build_id"):  # (SDL_LIB diagnostic builds of older sources may lack it)
+        L.sdl_build_id.restype = ctypes.c_char_p
+        L.sdl_build_id.argtypes = []
+    if product:
         # the product library must be built from the sources beside it
         # (build.py embeds their content hash): a stale prebuilt library fails here
         from . import build as _build

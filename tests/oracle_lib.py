@@ -11,7 +11,7 @@ import numpy as np
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ORACLE_DIR = os.path.join(REPO, "oracle")
-ORACLE_SO = os.path.join(ORACLE_DIR, "build", "liboracle.so")
+ORACLE_SO = os.environ.get("ORACLE_SO") or os.path.join(ORACLE_DIR, "build", "liboracle.so")
 VOCAB_TXT = os.path.join(REPO, "streaming_data_loader_amd", "assets", "bert_proxy", "vocab.txt")
 UNICODE_BIN = os.path.join(REPO, "streaming_data_loader_amd", "data", "bert_uncased_unicode.bin")
 GPT2_JSON = os.path.join(REPO, "streaming_data_loader_amd", "assets", "gpt2_proxy", "tokenizer.json")
@@ -23,6 +23,8 @@ _lib = None
 
 
 def build():
+    if os.environ.get("ORACLE_SO"):  # a prebuilt variant (the sanitizer build of test_inflate_fuzz.py)
+        return ORACLE_SO
     srcs = [os.path.join(ORACLE_DIR, f) for f in os.listdir(ORACLE_DIR) if f.endswith((".c", ".h"))]
     if not os.path.exists(ORACLE_SO) or os.path.getmtime(ORACLE_SO) < max(os.path.getmtime(f) for f in srcs):
         subprocess.run(["make", "-s", "-C", ORACLE_DIR], check=True)

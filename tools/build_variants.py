@@ -1,6 +1,8 @@
 #!/usr/bin/env python3
 """Diagnostic builds of libsdl_batcher.so with extra -D macros, for A/B timing
-on the GPU (tools/variants.sh): python tools/build_variants.py NAME=MACRO[,MACRO] ..."""
+on the GPU (tools/gpu_ab.sh): python tools/build_variants.py NAME=MACRO[,MACRO] ...
+Libraries go to var/NAME/ (git-ignored, but they travel to the GPU box; the
+objects stay in build/, which does not)."""
 import os
 import sys
 
@@ -10,7 +12,7 @@ from streaming_data_loader_amd import build  # noqa: E402
 
 for spec in sys.argv[1:]:
     name, _, macros = spec.partition("=")
-    d = os.path.join(REPO, "build", "var", name)
-    lib = build.build(defines=tuple(m for m in macros.split(",") if m), lib=os.path.join(d, "libsdl_batcher.so"),
-                      build_dir=os.path.join(d, "obj"))
+    lib = build.build(defines=tuple(m for m in macros.split(",") if m),
+                      lib=os.path.join(REPO, "var", name, "libsdl_batcher.so"),
+                      build_dir=os.path.join(REPO, "build", "var", name, "obj"))
     print(lib)

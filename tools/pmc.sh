@@ -5,10 +5,11 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 TASK="${1:-mlm}"
 ARENA="${2:-256}"
-D=gpurun_out/pmc_${TASK}_${ARENA}
+CORPUS="${3:-fixture}"
+D=gpurun_out/pmc_${TASK}_${ARENA}_${CORPUS}
 mkdir -p $D
 export TMPDIR=/tmp
-ARGS="--task $TASK --steps 2 --warmup 1 --arena-mib $ARENA --no-cpu-baseline"
+ARGS="--task $TASK --steps 2 --warmup 1 --arena-mib $ARENA --corpus $CORPUS --no-cpu-baseline"
 i=0
 while IFS= read -r group; do
   [[ -z "$group" ]] && continue

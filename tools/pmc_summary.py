@@ -6,7 +6,7 @@ HBM bytes per launch = 2 x FETCH_SIZE + WRITE_SIZE (KiB units), the gfx950
 FETCH_SIZE correction of MI355X_MICROARCH.md §HBM (FETCH_SIZE reports half the
 bytes of a 16 B/lane streaming read).  Averaged over every launch of a kernel.
 
-    python tools/pmc_summary.py gpurun_out/pmc TASK ARENA_MIB
+    python tools/pmc_summary.py gpurun_out/pmc TASK ARENA_MIB [CORPUS]
 """
 import csv
 import glob
@@ -24,8 +24,9 @@ def main():
     src = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
     task = sys.argv[2] if len(sys.argv) > 2 else "mlm"
     arena = int(sys.argv[3]) if len(sys.argv) > 3 else 256
+    corpus = sys.argv[4] if len(sys.argv) > 4 else "fixture"
     os.makedirs("profiles/pmc", exist_ok=True)
-    dst = f"profiles/pmc/{task}_{arena}mib.json"
+    dst = f"profiles/pmc/{task}_{arena}mib" + ("" if corpus == "fixture" else f"_{corpus}") + ".json"
     vals = defaultdict(lambda: defaultdict(list))  # kernel -> counter -> per-dispatch values
     for f in sorted(glob.glob(os.path.join(src, "**", "*counter_collection.csv"), recursive=True)):
         per = defaultdict(float)
@@ -37,8 +38,9 @@ def main():
                 names[row["Dispatch_Id"]] = short(row["Kernel_Name"])
         for (d, c), v in per.items():
             vals[names[d]][c].append(v)
-    out = {"source": f"rocprofv3 --pmc passes of bench.py --task {task} --arena-mib {arena} (tools/pmc.sh)",
-           "task": task, "arena_mib": arena, "kernels": {}}
+    out = {"source": f"rocprofv3 --pmc passes of bench.py --task {task} --arena-mib {arena} --corpus {corpus} "
+                     "(tools/pmc.sh)",
+           "task": task, "arena_mib": arena, "corpus": corpus, "kernels": {}}
     for k, cs in vals.items():
         avg = {c: sum(v) / len(v) for c, v in cs.items()}
         ent = {"launches": max(len(v) for v in cs.values()), "counters": avg}
