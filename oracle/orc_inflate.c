@@ -204,6 +204,12 @@ int orc_gz_inflate(const uint8_t *m, size_t n, uint8_t *out, size_t cap, size_t 
     *produced = 0;
     if (n < 18) return E_TRUNC;
     if (m[0] != 0x1f || m[1] != 0x8b || m[2] != 8) return E_HEADER;
+    /* The product sizes each member's output from its trailer before decoding
+     * (sdl_gzip_inflate_device), so an ISIZE that DEFLATE cannot reach (more
+     * than 1032:1, + 64) fails the member here, ahead of any decode error zlib
+     * would report first; which reason a corrupt member gets is the device
+     * contract's (GZ_*), the fact that it fails is zlib's. */
+    if ((uint64_t)orc_gz_isize(m, n) > 1032ull * n + 64) return E_SIZE;
     const uint8_t flg = m[3];
     if (flg & 0xE0) return E_HEADER;
     size_t p = 10;

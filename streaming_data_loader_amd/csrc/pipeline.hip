@@ -610,21 +610,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SDL_ROWS_WA
 // ---------------------------------------------------------------------------
 // rand-compatible MLM masks (rng_mode 1, oracle/orc_batcher.c orc_rand_positions):
 // BertData::mask_batch's position_base.shuffle (bert_data.rs:40-43; rand 0.8.5
-// SliceRandom::shuffle -> gen_index -> UniformInt<u32> widening-multiply
-// rejection) driven by StdRng::from_seed(seed | record | chunk) (rand_chacha
-// 0.3.1 ChaCha12: 64-bit block counter, stream 0, words in block order).
-// One wave per row: lanes compute the ChaCha12 blocks of the S-1 draws the
-// shuffle takes when nothing is rejected and every swap's index j_i at once;
-// a rejection anywhere in the row (probability ~S^2 / 2^32) sends lane 0 through
-// the draws in order.  mask_batch only uses the SET of the first k shuffled
-// positions, and Fisher-Yates from the end never moves a value out of
-// [0, k) once steps i < k begin (j_i <= i), so the set is what [0, k) holds
-// after steps S-1 .. k.  The value at position p just before step p came from
-// the latest earlier swap into p -- step next(p) = min{i > p : j_i = p,
-// j_i != i} -- so it is val(next(p)), or p if there was none; and [0, k)
-// receives val(min{i >= k : j_i = x}) at each x.  next() is one LDS atomicMin
-// per step; each x then follows a chain of ~2 hops (S=512, k=76) instead of
-// tracing through all S-1 swaps.  Output: the row's mask bits.
+// SliceRandom::shuffle -> gen_index -> UniformInt<u32>::sample_single_inclusive)
+// driven by StdRng::from_seed(seed | record | chunk) (rand_chacha 0.3.1 ChaCha12:
+// 64-bit block counter, stream 0, words in block order).
+// The draws are sequential: swap i = S-1 .. 1 takes words until one is
+// accepted, lo32(v * n) <= zone(n) = (n << lz(n)) - 1 with n = i + 1 -- rand's
+// "conservative" zone rejects up to half the words for n just above a power of
+// two, so about 30 % of a row's ~730 words are rejected and every row has
+// rejections.  Phase A runs each row's walk in one lane (64 rows per wave):
+// the lane computes its ChaCha12 blocks in registers, 16 words per block in an
+// unrolled loop, and writes each swap index j_i to the row's slice of `jbuf`.
+// Phase B, a wave per row: mask_batch only uses the SET of the first k shuffled
+// positions, and Fisher-Yates from the end never moves a value out of [0, k)
+// once steps i < k begin (j_i <= i), so the set is what [0, k) holds after steps
+// S-1 .. k.  The value at position p just before step p came from the latest
+// earlier swap into p -- step next(p) = min{i > p : j_i = p, j_i != i} -- so it
+// is val(next(p)), or p; [0, k) receives val(min{i >= k : j_i = x}) at each x.
+// next() is one LDS atomicMin per step; each x follows a chain of ~2 hops
+// (S=512, k=76).  Output: the row's mask bits.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
 #define CC_QR(a, b, c, d)                                                         \
@@ -648,95 +651,85 @@ __device__ __forceinline__ void chacha12_block(const uint32_t (&k)[8], uint32_t 
 
 __global__ __launch_bounds__(64) void k_mask_rand(RowParams P, const uint32_t *__restrict__ row_off,
                                                   const uint32_t *__restrict__ row_rec, SegSel sel, int64_t rows_cap,
-                                                  uint32_t *__restrict__ bits) {
-    __shared__ uint32_t s_draw[RAND_MAX_S + 16];
+                                                  uint16_t *__restrict__ jbuf, uint32_t *__restrict__ bits) {
     __shared__ uint16_t s_j[RAND_MAX_S];
+    __shared__ uint32_t s_next[RAND_MAX_S];
     __shared__ uint32_t s_bits[RAND_MAX_S / 32];
-    uint32_t *const s_next = s_draw;  // next(p), once the draws are spent
     const int lane = lane_id();
     const int S = P.S, W = (S + 31) >> 5, kmask = P.mask_length < S ? P.mask_length : S;
-    const int nblk = (S - 1 + 15) >> 4;
     const RowSpan rs = row_span(sel, row_off, P.B, rows_cap);
     constexpr uint32_t NONE = 0xFFFFFFFFu;
-    for (int64_t g = rs.g_lo + blockIdx.x; g < (int64_t)rs.g_real; g += gridDim.x) {
-        const int64_t r = row_rec[g];
-        const uint32_t chunk = (uint32_t)(g - row_off[r]);
-        const uint64_t rec = P.first_record + (uint64_t)r;
-        const uint32_t key[8] = {(uint32_t)P.seed, (uint32_t)(P.seed >> 32), (uint32_t)rec, (uint32_t)(rec >> 32),
-                                 chunk, 0u, 0u, 0u};
-        for (int b = lane; b < nblk; b += 64) {
+    for (int64_t g0 = rs.g_lo + (int64_t)blockIdx.x * 64; g0 < (int64_t)rs.g_real; g0 += (int64_t)gridDim.x * 64) {
+        // ---- A. lane per row: the shuffle's swap indices -------------------------
+        const int64_t g = g0 + lane;
+        int i = 0;
+        uint32_t key[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+        uint16_t *jrow = jbuf + (g < (int64_t)rs.g_real ? g : 0) * (int64_t)S;
+        if (g < (int64_t)rs.g_real) {
+            const int64_t r = row_rec[g];
+            const uint32_t chunk = (uint32_t)(g - row_off[r]);
+            const uint64_t rec = P.first_record + (uint64_t)r;
+            key[0] = (uint32_t)P.seed;
+            key[1] = (uint32_t)(P.seed >> 32);
+            key[2] = (uint32_t)rec;
+            key[3] = (uint32_t)(rec >> 32);
+            key[4] = chunk;
+            i = S - 1;
+        }
+        uint32_t n = (uint32_t)i + 1u, zone = (n << __builtin_clz(n)) - 1u;
+        for (uint32_t blk = 0; __any(i >= 1); ++blk) {
             uint32_t o[16];
-            chacha12_block(key, (uint32_t)b, o);
+            chacha12_block(key, blk, o);
 #pragma unroll
-            for (int q = 0; q < 16; ++q) s_draw[16 * b + q] = o[q];
-        }
-        for (int w = lane; w < W; w += 64) s_bits[w] = 0u;
-        __syncthreads();
-        // draw t feeds swap i = S-1-t when nothing before it was rejected
-        bool rej = false;
-        for (int t = lane; t < S - 1; t += 64) {
-            const uint32_t n = (uint32_t)(S - t), zone = (n << __builtin_clz(n)) - 1u;
-            const uint64_t m = (uint64_t)s_draw[t] * n;
-            rej = rej || (uint32_t)m > zone;
-            s_j[S - 1 - t] = (uint16_t)(m >> 32);
-        }
-        if (__any(rej)) {  // (rare) the draws in order, blocks past the buffer computed on demand
-            __syncthreads();
-            if (lane == 0) {
-                uint32_t blk[16];
-                int have = -1;
-                int t = 0;
-                for (int i = S - 1; i >= 1; --i) {
-                    const uint32_t n = (uint32_t)i + 1u, zone = (n << __builtin_clz(n)) - 1u;
-                    for (;;) {
-                        uint32_t v;
-                        if (t < 16 * nblk) {
-                            v = s_draw[t];
-                        } else {
-                            if ((t >> 4) != have) {
-                                have = t >> 4;
-                                chacha12_block(key, (uint32_t)have, blk);
-                            }
-                            v = blk[t & 15];
-                        }
-                        ++t;
-                        const uint64_t m = (uint64_t)v * n;
-                        if ((uint32_t)m <= zone) {
-                            s_j[i] = (uint16_t)(m >> 32);
-                            break;
-                        }
-                    }
+            for (int q = 0; q < 16; ++q) {
+                const uint64_t m = (uint64_t)o[q] * n;
+                if (i >= 1 && (uint32_t)m <= zone) {
+                    jrow[i] = (uint16_t)(m >> 32);
+                    --i;
+                    n = (uint32_t)i + 1u;
+                    zone = (n << __builtin_clz(n)) - 1u;
                 }
             }
         }
-        __syncthreads();
-        for (int p = lane; p < S; p += 64) s_next[p] = NONE;
-        __syncthreads();
-        // next(p): the latest swap into p among steps i >= k (a self swap moves nothing)
-        const int i0 = kmask > 1 ? kmask : 1;
-        for (int i = i0 + lane; i < S; i += 64) {
-            const int j = s_j[i];
-            if (j != i) atomicMin(&s_next[j], (uint32_t)i);
+        __syncthreads();  // (workgroup scope: the rows' indices are visible to the whole wave)
+        // ---- B. wave per row: the first k positions' set -------------------------
+        const int64_t gz = g0 + 64 < (int64_t)rs.g_real ? g0 + 64 : (int64_t)rs.g_real;
+        for (int64_t h = g0; h < gz; ++h) {
+            const uint16_t *jr = jbuf + h * (int64_t)S;
+            for (int t = lane; t < S; t += 64) {
+                s_j[t] = t >= 1 ? jr[t] : (uint16_t)0;
+                s_next[t] = NONE;
+            }
+            for (int w = lane; w < W; w += 64) s_bits[w] = 0u;
+            __syncthreads();
+            // next(p): the latest swap into p among steps i >= k (a self swap moves nothing)
+            const int i0 = kmask > 1 ? kmask : 1;
+            for (int t = i0 + lane; t < S; t += 64) {
+                const int j = s_j[t];
+                if (j != t) atomicMin(&s_next[j], (uint32_t)t);
+            }
+            __syncthreads();
+            // [0, k) holds val(next(x)) (or x): follow each chain to its end
+            for (int x = lane; x < kmask; x += 64) {
+                uint32_t p = (uint32_t)x;
+                for (uint32_t q = s_next[p]; q != NONE; q = s_next[p]) p = q;
+                atomicOr(&s_bits[p >> 5], 1u << (p & 31));
+            }
+            __syncthreads();
+            uint32_t *dst = bits + h * (int64_t)W;
+            for (int w = lane; w < W; w += 64) dst[w] = s_bits[w];
+            __syncthreads();
         }
-        __syncthreads();
-        // [0, k) holds val(next(x)) (or x): follow each chain to its end
-        for (int x = lane; x < kmask; x += 64) {
-            uint32_t p = (uint32_t)x;
-            for (uint32_t q = s_next[p]; q != NONE; q = s_next[p]) p = q;
-            atomicOr(&s_bits[p >> 5], 1u << (p & 31));
-        }
-        __syncthreads();
-        uint32_t *dst = bits + g * (int64_t)W;
-        for (int w = lane; w < W; w += 64) dst[w] = s_bits[w];
-        __syncthreads();
     }
 }
 
 hipError_t launch_mask_rand(const RowParams &P, const uint32_t *row_off, const uint32_t *row_rec, SegSel sel,
-                            int64_t rows_cap, uint32_t *bits, hipStream_t st) {
+                            int64_t rows_cap, uint16_t *jbuf, uint32_t *bits, hipStream_t st) {
     if (rows_cap <= 0) return hipSuccess;
-    const int64_t grid = rows_cap < 16384 ? rows_cap : 16384;
-    hipLaunchKernelGGL(k_mask_rand, dim3((unsigned)grid), dim3(64), 0, st, P, row_off, row_rec, sel, rows_cap, bits);
+    const int64_t want = (rows_cap + 63) / 64;
+    const int64_t grid = want < 4096 ? want : 4096;
+    hipLaunchKernelGGL(k_mask_rand, dim3((unsigned)grid), dim3(64), 0, st, P, row_off, row_rec, sel, rows_cap, jbuf,
+                       bits);
     return hipGetLastError();
 }
 
@@ -1021,6 +1014,7 @@ __global__ __launch_bounds__(256) void k_rows_span(RowParams P, const uint32_t *
     __shared__ uint32_t s_win[4][SPAN_WBLK * 16];
     __shared__ double s_draw[4][128];
     __shared__ uint16_t s_dend[4][128];
+    extern __shared__ int32_t s_rid[];  // [4][S]: each wave's row of framed ids (dynamic)
     const int lane = lane_id();
     const int wid = (int)(threadIdx.x >> 6);
     const int S = P.S, LW = P.label_width;
@@ -1052,6 +1046,22 @@ __global__ __launch_bounds__(256) void k_rows_span(RowParams P, const uint32_t *
             return frame_id(P.post, (int)(f - P.n_pre - cnt));
         };
         auto extra = [&](uint32_t q) -> int32_t { return P.extra_ids[q < 100u ? q : 99u]; };
+        // the row's framed ids into LDS first: one coalesced burst with every
+        // load in flight, so the position-parallel writes below read LDS only
+        int32_t *rid = s_rid + (size_t)wid * S;
+        for (int j0 = 0; j0 < n; j0 += 64 * 8) {
+            int32_t v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int j = j0 + 64 * u + lane;
+                v[u] = j < n ? fid(j) : 0;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int j = j0 + 64 * u + lane;
+                if (j < n) rid[j] = v[u];
+            }
+        }
         const uint64_t rec = P.first_record + (uint64_t)r;
         SpanStream ss;
         uint64_t spos = 0;
@@ -1135,7 +1145,7 @@ __global__ __launch_bounds__(256) void k_rows_span(RowParams P, const uint32_t *
                     const SpanPass e = sp[o];
                     const int off = q - (int)(e.lp_gg & 0xFFFFu);
                     const int ge = (int)(e.lp_gg >> 16);
-                    st_nt(ids_o + q, off < ge ? fid((int)(e.ip_sz & 0xFFFFu) + off) : extra(e.pass));
+                    st_nt(ids_o + q, off < ge ? rid[(int)(e.ip_sz & 0xFFFFu) + off] : extra(e.pass));
                 }
             }
             own = 0;
@@ -1153,7 +1163,7 @@ __global__ __launch_bounds__(256) void k_rows_span(RowParams P, const uint32_t *
                     const SpanPass e = sp[o];
                     const int off = q - (int)e.ap;
                     st_nt(lb_o + q, off == 0 ? extra(e.pass)
-                                            : fid((int)(e.ip_sz & 0xFFFFu) + (int)(e.lp_gg >> 16) + off - 1));
+                                            : rid[(int)(e.ip_sz & 0xFFFFu) + (int)(e.lp_gg >> 16) + off - 1]);
                 }
             }
             if (Pl < 64) {
@@ -1187,11 +1197,12 @@ hipError_t launch_rows_span(const RowParams &P, const uint32_t *tok, const uint3
         hipError_t e = hipMemsetAsync(err, 0, sizeof(uint32_t), st);
         if (e != hipSuccess) return e;
     }
+    const size_t dyn = (size_t)4 * P.S * sizeof(int32_t);  // s_rid
     if (P.rng_mode == 1)
-        hipLaunchKernelGGL(k_rows_span<1>, dim3(grid), dim3(256), 0, st, P, tok, rec_tok, rec_cnt, row_off, row_rec,
+        hipLaunchKernelGGL(k_rows_span<1>, dim3(grid), dim3(256), dyn, st, P, tok, rec_tok, rec_cnt, row_off, row_rec,
                            sel, rows_cap, out, err);
     else
-        hipLaunchKernelGGL(k_rows_span<0>, dim3(grid), dim3(256), 0, st, P, tok, rec_tok, rec_cnt, row_off, row_rec,
+        hipLaunchKernelGGL(k_rows_span<0>, dim3(grid), dim3(256), dyn, st, P, tok, rec_tok, rec_cnt, row_off, row_rec,
                            sel, rows_cap, out, err);
     return hipGetLastError();
 }

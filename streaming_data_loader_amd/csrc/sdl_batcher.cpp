@@ -270,6 +270,7 @@ struct sdl_batcher {
         row_rec, scan_tmp;
     DevBuf<int32_t> o_ids, o_am, o_tt, o_lab;
     DevBuf<uint32_t> mask_bits;  // rng_mode 1: per-row mask bits (k_mask_rand)
+    DevBuf<uint16_t> mask_j;     // rng_mode 1: per-row shuffle swap indices (k_mask_rand phase A)
     DevBuf<float> o_f32;
     DevBuf<uint32_t> lab_err;
     // byte-level BPE long pieces
@@ -417,7 +418,10 @@ struct sdl_batcher {
         }
         row_rec.ensure((size_t)std::max<int64_t>(rows_cap, 1));
         if (P.task == SDL_TASK_MLM && P.rng_mode == 1)
+        {
             mask_bits.ensure((size_t)std::max<int64_t>(rows_cap, 1) * (size_t)((P.S + 31) / 32));
+            mask_j.ensure((size_t)std::max<int64_t>(rows_cap, 1) * (size_t)P.S);
+        }
 
         RowParams p = P;
         p.first_record = first_record;
@@ -482,7 +486,7 @@ struct sdl_batcher {
                                          span_err.p, s));
             } else {
                 if (p.task == SDL_TASK_MLM && p.rng_mode == 1)
-                    HIP_TRY(launch_mask_rand(p, row_off.p, row_rec.p, sel, rows_cap, mask_bits.p, s));
+                    HIP_TRY(launch_mask_rand(p, row_off.p, row_rec.p, sel, rows_cap, mask_j.p, mask_bits.p, s));
                 HIP_TRY(launch_rows(p, tok_ids.p, rec_tok.p, rec_cnt.p, row_off.p, row_rec.p, sel, rows_cap, out, s));
             }
             if (multi())

@@ -593,7 +593,21 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
     __shared__ uint32_t s_rowmask[TASK_CAP];    // per row: which candidate ends exist (<= UNI_WMAX + 1)
     __shared__ uint16_t s_vp_src[VP_CAP];
     __shared__ uint8_t s_vp_len[VP_CAP];
+#ifdef SDL_UNI_ADJ_U8  // (diagnostic: 2-byte ids + a byte of correction instead of 4-byte records)
+    __shared__ uint16_t s_tid16[TASK_CAP];
+    __shared__ uint8_t s_tadj[TASK_CAP];
+    struct TidRef {
+        uint16_t *a; uint8_t *b; int i;
+        __device__ operator uint32_t() const { return (uint32_t)a[i] | (uint32_t)b[i] << 16; }
+        __device__ void operator=(uint32_t v) { a[i] = (uint16_t)v; b[i] = (uint8_t)(v >> 16); }
+    };
+    struct TidArr {
+        uint16_t *a; uint8_t *b;
+        __device__ TidRef operator[](int i) const { return TidRef{a, b, i}; }
+    } s_tid{s_tid16, s_tadj};
+#else
     __shared__ uint32_t s_tid[TASK_CAP];  // uni_cand: id | score correction
+#endif
     __shared__ float s_tsc[TASK_CAP];
 
     const int tid = threadIdx.x;

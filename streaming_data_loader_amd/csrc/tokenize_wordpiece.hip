@@ -775,13 +775,21 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
             }
         }
         Probe pr[TOK_UNROLL];
+#ifndef SDL_ABLATE_FIRST_PROBE
 #pragma unroll
         for (int u = 0; u < TOK_UNROLL; ++u) pr[u] = probe_load(T, hsh[u]);
+#endif
 #pragma unroll
         for (int u = 0; u < TOK_UNROLL; ++u) {
             const int pi = r0 + u * TOK_THREADS + tid;
             if (probe[u]) {
+#ifdef SDL_ABLATE_FIRST_PROBE
+                // diagnostic upper bound for an on-chip vocabulary: every first probe
+                // "hits" without a memory access (ids are wrong; timing only)
+                const int id = (int)(hsh[u] & 0x3FFFu) | (int)(cand[u].x & 1u);
+#else
                 const int id = probe_result(pr[u], key[u], cand[u]);
+#endif
                 if (id >= 0) {
                     stage[prel_u[u]] = (uint16_t)id;
                     s_cnt[pi] = 1;
