@@ -119,20 +119,16 @@ def build(verbose=False, force=False, jobs=4, defines=(), lib=None, build_dir=No
 
 
 def build_stamps():
-    """Diagnostic build with per-phase s_memtime stamps -> build/stamps/libsdl_batcher.so."""
-    d = os.path.join(REPO, "build", "stamps")
-    return build(defines=("SDL_STAMPS=1",), lib=os.path.join(d, "libsdl_batcher.so"), build_dir=os.path.join(d, "obj"))
+    """Diagnostic build with per-phase s_memtime stamps -> var/stamps/libsdl_batcher.so (travels to the GPU box)."""
+    return build(defines=("SDL_STAMPS=1",), lib=os.path.join(REPO, "var", "stamps", "libsdl_batcher.so"),
+                 build_dir=os.path.join(REPO, "build", "stamps"))
 
 
 def build_ablations(levels=(1, 2, 3)):
     """Diagnostic builds with phases of the tokenize kernel compiled out
-    (SDL_ABLATE=1: first probes only; 2: no WordPiece; 3: load only) -> build/abl<N>/libsdl_batcher.so."""
-    out = []
-    for n in levels:
-        d = os.path.join(REPO, "build", f"abl{n}")
-        out.append(build(defines=(f"SDL_ABLATE={n}",), lib=os.path.join(d, "libsdl_batcher.so"),
-                         build_dir=os.path.join(d, "obj")))
-    return out
+    (SDL_ABLATE=1: first probes only; 2: no WordPiece; 3: load only) -> var/abl<N>/libsdl_batcher.so."""
+    return [build(defines=(f"SDL_ABLATE={n}",), lib=os.path.join(REPO, "var", f"abl{n}", "libsdl_batcher.so"),
+                  build_dir=os.path.join(REPO, "build", f"abl{n}")) for n in levels]
 
 
 if __name__ == "__main__":

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Diagnostic: phase cycle split of k_unigram_chunks and the long-item counters
-(run with SDL_LIB=build/stamps/libsdl_batcher.so)."""
+(run with SDL_LIB=var/stamps/libsdl_batcher.so)."""
 import os
 import sys
 import time

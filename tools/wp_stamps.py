@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Diagnostic: phase cycle split of the WordPiece/BPE chunk kernels (run with
-SDL_LIB=build/stamps/libsdl_batcher.so): one process_device over the bench arena."""
+SDL_LIB=var/stamps/libsdl_batcher.so): one process_device over the bench arena."""
 import os
 import sys
 
