@@ -542,7 +542,7 @@ static int host_probe(const HostTokenizer &t, const uint8_t *pay, size_t n, uint
     const uint32_t key = (uint32_t)n | (cont << 8);
     for (uint32_t s : {cuckoo_slot1(h, t.slot_mask), cuckoo_slot2(h, t.slot_mask)}) {
         const VSlot &v = t.slots[s];
-        if (v.id >= 0 && v.key == key && std::memcmp(&t.vpool[v.pool_off & SLOT_POOL_MASK], pay, n) == 0) return v.id;
+        if (v.id >= 0 && v.key == key && std::memcmp(&t.vpool[v.pool_off], pay, n) == 0) return v.id;
     }
     return -1;
 }
@@ -635,7 +635,8 @@ static void load_unigram(const JValue &root, const std::string &data_dir, HostTo
     t.unk_id = (int)unk->num;
     if (t.unk_id < 0 || (size_t)t.unk_id >= nv) throw std::runtime_error("Unigram: unk_id out of range");
     // The kernels keep a candidate's score as the nearest f32 plus a 2-bit
-    // ulp correction (VSlot.pool_off's top bits) that restores the exact f64.
+    // ulp correction (bits 28-29 of the device slot's id, sdl_batcher.cpp)
+    // that restores the exact f64.
     // Scores written from sentencepiece's f32 (hub tokenizer.json: 17-digit
     // decimals) come back from serde_json's two-rounding parse (json.hpp) as
     // that f32 or one f64 ulp away from it; anything further is refused.
@@ -896,15 +897,12 @@ static void load_unigram(const JValue &root, const std::string &data_dir, HostTo
     t.vpool.resize(t.vpool.size() + 64, 0);
     build_cuckoo(t.wslots, t.wslot_mask, wentries);
     t.max_word = maxw;
-    // device slots: word 3 (the host's cuckoo hash) carries a piece's f32
-    // score, pool_off's top bits its f64 correction (SLOT_POOL_MASK)
-    if (t.vpool.size() > SLOT_POOL_MASK) throw std::runtime_error("vocab pool too large");
+    // device slots: word 3 (the host's cuckoo hash) carries a piece's f32 score
     for (VSlot &v : t.slots) {
         const uint32_t cont = v.key >> 8;
         if (v.id >= 0 && (cont == UC_PIECE || cont == UC_META)) {
             float f = t.uscore32[(size_t)v.id];
             std::memcpy(&v.hash, &f, 4);
-            v.pool_off |= ((uint32_t)t.uscore_adj[(size_t)v.id] & 3u) << 30;
         }
     }
     // the kernels emit printable ASCII without a table load: it must be GCB Other

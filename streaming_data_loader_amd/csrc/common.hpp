@@ -82,10 +82,6 @@ __host__ __device__ inline uint32_t cuckoo_slot2(uint32_t h, uint32_t mask) {
     return g & mask;
 }
 static_assert(sizeof(VSlot) == 32, "VSlot must be 32 bytes");
-// pool_off's top two bits: a Unigram piece's f64 score correction (ulps added
-// to the f32 score in `hash`, two's complement; assets.cpp), so pool offsets
-// stay below 2^30
-constexpr uint32_t SLOT_POOL_MASK = 0x3FFFFFFFu;
 static_assert(PEND_CAP % 64 == 0 && 2 * PEND_CAP >= LW_BUF + 4 * LW_MAX, "the WordPiece lattice buffer reuses the pending list");
 
 // Byte-level BPE merge table (cuckoo, 2 slots of 8 B): key = left id << 16 |

@@ -311,6 +311,16 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t *__restrict__ in, 
                     bb >>= k;
                     bc -= k;
                 };
+                // the first error and the bits consumed when it was found: a reader
+                // that ran past the deflate data (the trailer's 8 bytes are not
+                // input) fails with GZ_E_TRUNC first, as zlib's does
+                uint32_t err_bits = 0;
+                auto seterr = [&](int32_t code, uint32_t at_bits) {
+                    if (!err) {
+                        err = code;
+                        err_bits = at_bits;
+                    }
+                };
                 need(3);
                 fin = (uint32_t)bb & 1u;
                 const uint32_t type = (uint32_t)(bb >> 1) & 3u;
@@ -318,7 +328,8 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t *__restrict__ in, 
                 if (type == 0) {  // stored: LEN, NLEN at the next byte boundary
                     const uint32_t at = (fill - (uint32_t)bc + 7u) & ~7u;
                     const uint32_t w = peek(at);
-                    if ((w & 0xFFFFu) != (~(w >> 16) & 0xFFFFu)) err = GZ_E_STORED;
+                    if ((w & 0xFFFFu) != (~(w >> 16) & 0xFFFFu)) seterr(GZ_E_STORED, at + 32u);
+                    else if ((int64_t)at + 32 > 8 * ((int64_t)mz - 8 - (int64_t)sbase)) seterr(GZ_E_TRUNC, at + 32u);
                     else {
                         act = A_STORED;
                         x0 = (uint32_t)(sbase + (at >> 3) + 4 - ma);  // data start, member-relative
@@ -335,7 +346,7 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t *__restrict__ in, 
                     const int hlit = (int)(bb & 31u) + 257, hdist = (int)((bb >> 5) & 31u) + 1,
                               hclen = (int)((bb >> 10) & 15u) + 4;
                     drop(14);
-                    if (hlit > 286 || hdist > 30) err = GZ_E_CODES;
+                    if (hlit > 286 || hdist > 30) seterr(GZ_E_CODES, fill - (uint32_t)bc);
                     uint8_t *cl = s_len + NSYM;
                     for (int i = 0; i < 19; ++i) cl[i] = 0;
                     for (int i = 0; i < hclen && !err; ++i) {
@@ -348,7 +359,7 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t *__restrict__ in, 
                     for (int i = 0; i < 19; ++i) ++cnt[cl[i]];
                     int left = 1;
                     for (int l = 1; l < 8; ++l) left = (left << 1) - cnt[l];
-                    if (!err && left != 0) err = GZ_E_CODES;  // over-subscribed or incomplete (or empty)
+                    if (!err && left != 0) seterr(GZ_E_CODES, fill - (uint32_t)bc);  // over-subscribed or incomplete (or empty)
                     if (!err) {
                         uint32_t code = 0;
                         cnt[0] = 0;
@@ -376,7 +387,7 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t *__restrict__ in, 
                             int rep;
                             uint8_t v = 0;
                             if (sym == 16) {
-                                if (i == 0) { err = GZ_E_CODES; break; }
+                                if (i == 0) { seterr(GZ_E_CODES, fill - (uint32_t)bc); break; }
                                 v = s_len[i - 1];
                                 rep = 3 + (int)(bb & 3u);
                                 drop(2);
@@ -387,10 +398,10 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t *__restrict__ in, 
                                 rep = 11 + (int)(bb & 127u);
                                 drop(7);
                             }
-                            if (i + rep > total) { err = GZ_E_CODES; break; }
+                            if (i + rep > total) { seterr(GZ_E_CODES, fill - (uint32_t)bc); break; }
                             while (rep--) s_len[i++] = v;
                         }
-                        if (!err && s_len[256] == 0) err = GZ_E_CODES;  // missing end-of-block code
+                        if (!err && s_len[256] == 0) seterr(GZ_E_CODES, fill - (uint32_t)bc);  // missing end-of-block code
                     }
                     if (!err) {
                         act = A_BUILD;
@@ -398,9 +409,14 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t *__restrict__ in, 
                         x1 = (uint32_t)hdist;
                     }
                 } else {
-                    err = GZ_E_BTYPE;
+                    seterr(GZ_E_BTYPE, fill - (uint32_t)bc);
                 }
                 nbp = fill - (uint32_t)bc;
+                const int64_t lim = 8 * ((int64_t)mz - 8 - (int64_t)sbase);
+                if ((int64_t)(err ? err_bits : nbp) > lim) {  // the header ran out of input first
+                    err = GZ_E_TRUNC;
+                    act = A_ERR;
+                }
             }
             act = bfl(act);
             x0 = bfl(x0);
@@ -589,25 +605,38 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t *__restrict__ in, 
             olen0 = ((M0 >> lane) & 1u) ? olen0 : 0u;
             olen1 = ((M1 >> lane) & 1u) ? olen1 : 0u;
         }
+        const uint32_t nmat = (uint32_t)__popcll(mb0 & M0) + (uint32_t)__popcll(mb1 & M1);
+        const bool on0 = olen0 != 0, on1 = olen1 != 0;  // chain tokens with output (not end of block)
+        // The first error in stream order, as zlib meets it: per chain token,
+        // its bits running past the deflate data (the trailer's 8 bytes are not
+        // input), then a distance too far back, then output past ISIZE; the
+        // window-0 tokens precede the window-1 ones; an invalid code ends the
+        // chain, so every token before it comes first.
+        const int64_t lim = 8 * ((int64_t)mz - 8 - (int64_t)sbase);
+        auto tok_bad = [&](uint64_t M, uint32_t pk, uint32_t start, bool on, uint32_t kind, uint32_t dist, int opos,
+                           uint32_t olen) -> int32_t {
+            const uint32_t tl = pk & 63u;
+            if (!((M >> lane) & 1ull) || tl == 0) return GZ_OK;
+            if ((int64_t)start + tl > lim) return GZ_E_TRUNC;
+            if (on && kind == K_LEN && dist > produced + (uint32_t)opos) return GZ_E_FAR;
+            if (on && produced + (uint32_t)opos + olen > cap) return GZ_E_OVER;
+            return GZ_OK;
+        };
+        const int32_t bad0 = tok_bad(M0, pk0, bp + (uint32_t)lane, on0, kind0, dist0, opos0, olen0);
+        const int32_t bad1 = tok_bad(M1, pk1, bp + 64u + (uint32_t)lane, on1, kind1, dist1, opos1, olen1);
+        const uint64_t bm0 = __ballot(bad0 != GZ_OK), bm1 = __ballot(bad1 != GZ_OK);
+        if (bm0 | bm1) {
+            const int32_t b0 = bm0 ? __builtin_amdgcn_readlane(bad0, (int)__builtin_ctzll(bm0))
+                                   : __builtin_amdgcn_readlane(bad1, (int)__builtin_ctzll(bm1));
+            if (lane == 0) err = b0;
+            break;
+        }
         if (stop == 3) {  // an invalid code on the chain
             if (lane == 0) err = GZ_E_CODE;
             break;
         }
         if (stop == 2 && q == 0 && nb == 0) {  // the first token does not fit an empty batch: no progress
             if (lane == 0) err = GZ_E_STALL;
-            break;
-        }
-        const uint32_t nmat = (uint32_t)__popcll(mb0 & M0) + (uint32_t)__popcll(mb1 & M1);
-        const bool on0 = olen0 != 0, on1 = olen1 != 0;  // chain tokens with output (not end of block)
-        int32_t bad = GZ_OK;
-        if (on0 && kind0 == K_LEN && dist0 > produced + (uint32_t)opos0) bad = GZ_E_FAR;
-        else if (on0 && produced + (uint32_t)opos0 + olen0 > cap) bad = GZ_E_OVER;
-        else if (on1 && kind1 == K_LEN && dist1 > produced + (uint32_t)opos1) bad = GZ_E_FAR;
-        else if (on1 && produced + (uint32_t)opos1 + olen1 > cap) bad = GZ_E_OVER;
-        const uint64_t badm = __ballot(bad != GZ_OK);
-        if (badm) {
-            const int32_t b0 = __builtin_amdgcn_readlane(bad, (int)__builtin_ctzll(badm));
-            if (lane == 0) err = b0;
             break;
         }
         if (on0 && kind0 == K_LIT) {

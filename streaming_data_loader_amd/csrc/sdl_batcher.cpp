@@ -798,7 +798,19 @@ int sdl_batcher_create(const sdl_config *cfg, const char *tokenizer_path, const 
         HIP_TRY(hipMemcpy(h->d_upage.p, t.upage.data(), t.upage.size() * 2, hipMemcpyHostToDevice));
         HIP_TRY(hipMemcpy(h->d_uentry.p, t.uentry.data(), t.uentry.size() * 4, hipMemcpyHostToDevice));
         HIP_TRY(hipMemcpy(h->d_upool.p, t.upool.data(), t.upool.size(), hipMemcpyHostToDevice));
-        HIP_TRY(hipMemcpy(h->d_slots.p, t.slots.data(), t.slots.size() * sizeof(VSlot), hipMemcpyHostToDevice));
+        if (t.kind == TOK_UNIGRAM) {
+            // the device copy of the pieces table: bits 28-29 of a piece's id carry
+            // the f64 correction of its f32 score (tokenize_unigram.hip uni_cand)
+            std::vector<VSlot> ds(t.slots);
+            for (VSlot &v : ds) {
+                const uint32_t cont = v.key >> 8;
+                if (v.id >= 0 && (cont == UC_PIECE || cont == UC_META))
+                    v.id |= (int32_t)(((uint32_t)t.uscore_adj[(size_t)v.id] & 3u) << 28);
+            }
+            HIP_TRY(hipMemcpy(h->d_slots.p, ds.data(), ds.size() * sizeof(VSlot), hipMemcpyHostToDevice));
+        } else {
+            HIP_TRY(hipMemcpy(h->d_slots.p, t.slots.data(), t.slots.size() * sizeof(VSlot), hipMemcpyHostToDevice));
+        }
         HIP_TRY(hipMemcpy(h->d_vpool.p, t.vpool.data(), t.vpool.size(), hipMemcpyHostToDevice));
         DevTok &d = h->dt;
         d.kind = t.kind;

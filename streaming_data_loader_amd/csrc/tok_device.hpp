@@ -219,7 +219,7 @@ __device__ __forceinline__ int probe_general(const DevTok &T, const uint8_t *w, 
         const uint4 a = which ? P.a2 : P.a1, b = which ? P.b2 : P.b1;
         if (!slot_match(a, b, key, first)) continue;
         bool ok = true;
-        for (uint32_t k = 16; k < n && ok; ++k) ok = T.vpool[(a.z & SLOT_POOL_MASK) + k] == w[start + k];
+        for (uint32_t k = 16; k < n && ok; ++k) ok = T.vpool[a.z + k] == w[start + k];
         if (ok) return (int32_t)a.y;
     }
     return -1;

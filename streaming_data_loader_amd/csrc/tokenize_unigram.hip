@@ -103,8 +103,7 @@ __device__ __forceinline__ Probe probe_load_words(const DevTok &T, uint32_t h) {
 
 // id of the slot (payload bytes acc(start .. start+n), cont) or -1: exact
 template <class Acc>
-__device__ int probe_acc(const DevTok &T, const Acc &acc, int start, int n, uint32_t cont, uint32_t *w3 = nullptr,
-                          uint32_t *zw = nullptr) {
+__device__ int probe_acc(const DevTok &T, const Acc &acc, int start, int n, uint32_t cont, uint32_t *w3 = nullptr) {
     uint32_t h = hinit((uint32_t)n, cont);
     W16 first{0, 0, 0, 0};
     int b0 = 0;
@@ -122,32 +121,32 @@ __device__ int probe_acc(const DevTok &T, const Acc &acc, int start, int n, uint
         const uint4 a = which ? P.a2 : P.a1, b = which ? P.b2 : P.b1;
         if (!slot_match(a, b, key, first)) continue;
         bool ok = true;
-        for (int k = 16; k < n && ok; ++k) ok = T.vpool[(a.z & SLOT_POOL_MASK) + k] == acc(start + k);
+        for (int k = 16; k < n && ok; ++k) ok = T.vpool[a.z + k] == acc(start + k);
         if (ok) {
             if (w3) *w3 = a.w;
-            if (zw) *zw = a.z;
             return (int32_t)a.y;
         }
     }
     return -1;
 }
 
-// probe_result that also returns the slot's words 3 and 2 (a Unigram piece's
-// f32 score and, in word 2's top bits, its f64 ulp correction: uni_score64)
-__device__ __forceinline__ int probe_result_w3(const Probe &P, uint32_t key, const W16 &c, uint32_t *w3, uint32_t *zw) {
-    if (slot_match(P.a1, P.b1, key, c)) { *w3 = P.a1.w; *zw = P.a1.z; return (int32_t)P.a1.y; }
-    if (slot_match(P.a2, P.b2, key, c)) { *w3 = P.a2.w; *zw = P.a2.z; return (int32_t)P.a2.y; }
+// probe_result that also returns the slot's word 3 (a Unigram piece's f32 score)
+__device__ __forceinline__ int probe_result_w3(const Probe &P, uint32_t key, const W16 &c, uint32_t *w3) {
+    if (slot_match(P.a1, P.b1, key, c)) { *w3 = P.a1.w; return (int32_t)P.a1.y; }
+    if (slot_match(P.a2, P.b2, key, c)) { *w3 = P.a2.w; return (int32_t)P.a2.y; }
     return -1;
 }
 
-// A candidate's LDS record: id | the slot's 2-bit ulp correction << 16
-__device__ __forceinline__ uint32_t uni_cand(int id, uint32_t zw) { return (uint32_t)id | (zw >> 30) << 16; }
+// A Unigram piece slot's id word carries, in bits 28-29, the ulp correction
+// that restores the piece's f64 score from the f32 in word 3 (the device copy
+// of the table only; sdl_batcher.cpp).  The score tokenizers holds is serde_
+// json's f64 parse of the tokenizer.json number (json.hpp), the f32 score or
+// one ulp off it.  Candidates keep id | correction << 16 in LDS.
+__device__ __forceinline__ uint32_t uni_cand(int y) { return ((uint32_t)y & 0xFFFFu) | (((uint32_t)y >> 28) & 3u) << 16; }
 __device__ __forceinline__ int uni_cand_id(uint32_t v) { return (int)(v & 0xFFFFu); }
-// The piece's score as tokenizers holds it: serde_json's f64 parse of the
-// tokenizer.json number (json.hpp), which is the f32 score or one ulp off it
-// (the host checks); the correction is sign-extended from bits 16-17.
+__device__ __forceinline__ int uni_piece_id(int y) { return y < 0 ? y : (int)((uint32_t)y & 0xFFFFu); }
 __device__ __forceinline__ double uni_score64(float f32, uint32_t cand) {
-    const int adj = (int32_t)(cand << 14) >> 30;
+    const int adj = (int32_t)(cand << 14) >> 30;  // bits 16-17, sign-extended
     return __longlong_as_double(__double_as_longlong((double)f32) + adj);
 }
 
@@ -362,6 +361,7 @@ __device__ int tokenize_normalized(const DevTok &T, const Scratch &S, int nl) {
                 int id;
                 if (s == 0) id = (e - 3 <= T.maxlen_meta) ? probe_acc(T, acc, 3, e - 3, UC_META) : -1;
                 else id = (e - s <= T.maxlen_first) ? probe_acc(T, acc, s, e - s, UC_PIECE) : -1;
+                id = uni_piece_id(id);
                 if (id >= 0) *sc = T.uscore[id];
                 return id;
             };
@@ -593,21 +593,7 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
     __shared__ uint32_t s_rowmask[TASK_CAP];    // per row: which candidate ends exist (<= UNI_WMAX + 1)
     __shared__ uint16_t s_vp_src[VP_CAP];
     __shared__ uint8_t s_vp_len[VP_CAP];
-#ifdef SDL_UNI_ADJ_U8  // (diagnostic: 2-byte ids + a byte of correction instead of 4-byte records)
-    __shared__ uint16_t s_tid16[TASK_CAP];
-    __shared__ uint8_t s_tadj[TASK_CAP];
-    struct TidRef {
-        uint16_t *a; uint8_t *b; int i;
-        __device__ operator uint32_t() const { return (uint32_t)a[i] | (uint32_t)b[i] << 16; }
-        __device__ void operator=(uint32_t v) { a[i] = (uint16_t)v; b[i] = (uint8_t)(v >> 16); }
-    };
-    struct TidArr {
-        uint16_t *a; uint8_t *b;
-        __device__ TidRef operator[](int i) const { return TidRef{a, b, i}; }
-    } s_tid{s_tid16, s_tadj};
-#else
-    __shared__ uint32_t s_tid[TASK_CAP];  // uni_cand: id | score correction
-#endif
+    __shared__ uint32_t s_tid[TASK_CAP];  // uni_cand: id | score correction << 16
     __shared__ float s_tsc[TASK_CAP];
 
     const int tid = threadIdx.x;
@@ -979,7 +965,7 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
     W16 W[TASK_UNROLL];
     uint32_t meta[TASK_UNROLL];  // row | k << 16 | n << 22 | cont << 29; ~0u: no probe
     int gen[TASK_UNROLL];        // generic probe result (payload > 16 bytes); -2: use P
-    uint32_t gw3[TASK_UNROLL], gzw[TASK_UNROLL];
+    uint32_t gw3[TASK_UNROLL];
     // A lane takes TASK_UNROLL consecutive tasks (4 lane + u): one job/vp search
     // and one candidate decode per lane, then (i, j) steps along the rows, and
     // the 16 payload bytes of a row are read from LDS once for its candidates.
@@ -1017,7 +1003,6 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
             meta[u] = ~0u;
             gen[u] = -2;
             gw3[u] = 0;
-            gzw[u] = 0;
             W[u] = W16{0, 0, 0, 0};
             if (t0 + u >= nt) continue;
             if (u > 0) {  // the next candidate: (i, j + 1), else the next row / vp / job
@@ -1059,7 +1044,7 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
                 W[u] = keep_bytes(rowb, n);
                 P[u] = probe_load(T, hash16(W[u], (uint32_t)n, cont));
             } else {
-                gen[u] = probe_acc(T, [&](int x) -> uint32_t { return bytes[src + x]; }, ps, n, cont, &gw3[u], &gzw[u]);
+                gen[u] = probe_acc(T, [&](int x) -> uint32_t { return bytes[src + x]; }, ps, n, cont, &gw3[u]);
             }
         }
     };
@@ -1073,13 +1058,13 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
 #pragma unroll
         for (int u = 0; u < TASK_UNROLL; ++u) {
             if (meta[u] == ~0u) continue;
-            uint32_t w3 = gw3[u], zw = gzw[u];
+            uint32_t w3 = gw3[u];
             const uint32_t key = ((meta[u] >> 22) & 0x7Fu) | ((meta[u] >> 29) << 8);
-            const int id = gen[u] != -2 ? gen[u] : probe_result_w3(P[u], key, W[u], &w3, &zw);
+            const int id = gen[u] != -2 ? gen[u] : probe_result_w3(P[u], key, W[u], &w3);
             if (id < 0) continue;
             const int t = TASK_UNROLL * lane + u;
-            s_tid[t] = uni_cand(id, zw);
-            s_tsc[t] = __uint_as_float(w3);  // the slot's f32 score (+ s_tid's correction: uni_score64)
+            s_tid[t] = uni_cand(id);
+            s_tsc[t] = __uint_as_float(w3);  // the slot's f32 score (+ its correction: uni_score64)
             atomicOr(&s_rowmask[meta[u] & 0xFFFFu], 1u << ((meta[u] >> 16) & 0x3Fu));
         }
         __syncthreads();
@@ -1448,6 +1433,7 @@ __global__ __launch_bounds__(64) void k_unigram_long(DevTok T, const uint8_t *__
                 int id;
                 if (st2 == 0) id = (e2 - 3 <= Mm) ? probe_acc(T, nbr, src, e2 - 3, UC_META) : -1;
                 else id = (e2 - st2 <= Mf) ? probe_acc(T, nbr, src + st2 - 3, e2 - st2, UC_PIECE) : -1;
+                id = uni_piece_id(id);
                 if (id >= 0) *sc = T.uscore[id];
                 return id;
             };
@@ -1464,14 +1450,13 @@ __global__ __launch_bounds__(64) void k_unigram_long(DevTok T, const uint8_t *__
                     Probe P[LONG_UNROLL];
                     W16 Wd[LONG_UNROLL];
                     int gen[LONG_UNROLL];
-                    uint32_t gw3[LONG_UNROLL], gzw[LONG_UNROLL], meta[LONG_UNROLL];  // row | k << 8 | len << 16 | cont << 24; ~0u: none
+                    uint32_t gw3[LONG_UNROLL], meta[LONG_UNROLL];  // row | k << 8 | len << 16 | cont << 24; ~0u: none
 #pragma unroll
                     for (int u = 0; u < LONG_UNROLL; ++u) {
                         const int t = tq + 64 * u + lane;
                         meta[u] = ~0u;
                         gen[u] = -2;
                         gw3[u] = 0;
-                        gzw[u] = 0;
                         Wd[u] = W16{0, 0, 0, 0};
                         if (t >= tz) continue;
                         int i, j;
@@ -1494,13 +1479,13 @@ __global__ __launch_bounds__(64) void k_unigram_long(DevTok T, const uint8_t *__
                             P[u] = probe_load(T, hfinal(h));
                             gen[u] = -3;
                         } else {
-                            gen[u] = probe_acc(T, nbr, src + ps, len, cont, &gw3[u], &gzw[u]);
+                            gen[u] = probe_acc(T, nbr, src + ps, len, cont, &gw3[u]);
                         }
                     }
 #pragma unroll
                     for (int u = 0; u < LONG_UNROLL; ++u) {
                         if (meta[u] == ~0u) continue;
-                        uint32_t w3 = gw3[u], zw = gzw[u];
+                        uint32_t w3 = gw3[u];
                         const uint32_t key = ((meta[u] >> 16) & 0xFFu) | ((meta[u] >> 24) << 8);
                         int id;
                         if (gen[u] == -3) {  // 17..32 bytes: header + first 16 bytes, then the pool
@@ -1511,20 +1496,18 @@ __global__ __launch_bounds__(64) void k_unigram_long(DevTok T, const uint8_t *__
                                 const uint4 sa = which ? P[u].a2 : P[u].a1, sb = which ? P[u].b2 : P[u].b1;
                                 if (!slot_match(sa, sb, key, Wd[u])) continue;
                                 bool ok = true;
-                                for (int x = 16; x < len && ok; ++x)
-                                    ok = T.vpool[(sa.z & SLOT_POOL_MASK) + x] == nb[src + (ps < 0 ? 0 : ps) + x];
+                                for (int x = 16; x < len && ok; ++x) ok = T.vpool[sa.z + x] == nb[src + (ps < 0 ? 0 : ps) + x];
                                 if (ok) {
                                     id = (int32_t)sa.y;
                                     w3 = sa.w;
-                                    zw = sa.z;
                                 }
                             }
                         } else {
-                            id = gen[u] != -2 ? gen[u] : probe_result_w3(P[u], key, Wd[u], &w3, &zw);
+                            id = gen[u] != -2 ? gen[u] : probe_result_w3(P[u], key, Wd[u], &w3);
                         }
                         if (id < 0) continue;
                         const int q = (int)(meta[u] & 0xFFu), k = (int)((meta[u] >> 8) & 0xFFu);
-                        s_cid[k * 64 + q] = uni_cand(id, zw);
+                        s_cid[k * 64 + q] = uni_cand(id);
                         s_csc[k * 64 + q] = __uint_as_float(w3);  // the slot's f32 score (k < KMAX host-checked)
                         atomicOr(&s_mask[q], 1ull << k);
                     }

@@ -1000,7 +1000,7 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
                         const uint4 a = which ? P.a2 : P.a1, b = which ? P.b2 : P.b1;
                         if (!slot_match(a, b, key, first)) continue;
                         bool ok = true;
-                        for (int x = 16; x < n && ok; ++x) ok = T.vpool[(a.z & SLOT_POOL_MASK) + x] == wb[st + x];
+                        for (int x = 16; x < n && ok; ++x) ok = T.vpool[a.z + x] == wb[st + x];
                         if (ok) id = (int32_t)a.y;
                     }
                     if (id >= 0)
