@@ -57,6 +57,7 @@ constexpr int NSYM = 320;          // lit/len (<= 288) + dist (<= 32) code lengt
 constexpr uint32_t POLY = 0xEDB88320u;
 
 enum : uint32_t { K_LIT = 0, K_LEN = 1, K_EOB = 2, K_SLOW = 3 };
+constexpr uint32_t K_BAD = 3;  // (token kinds: K_SLOW never names a decoded token)
 
 __constant__ uint16_t c_len_base[29] = {3,  4,  5,  6,  7,  8,  9,  10, 11,  13,  15,  17,  19,  23, 27,
                                         31, 35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
@@ -66,17 +67,21 @@ __constant__ uint16_t c_dist_base[30] = {1,   2,   3,   4,   5,   7,    9,    13
 __constant__ uint8_t c_dist_extra[30] = {0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6, 6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13};
 __constant__ uint8_t c_cl_order[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
 
-// table entry: bits 0-3 code length (0: invalid code), 4-5 kind, 8-11 extra
-// bits, 16-31 value (literal byte / length base / distance base)
+// table entry: bits 0-3 code length (0: no such code), 4-5 kind, 8-11 extra
+// bits, 16-31 value (literal byte / length base / distance base).  The symbols
+// a code may name but DEFLATE does not define (lit/len 286, 287; distance 30,
+// 31) keep their code length with extra = 15 (no real symbol has that many),
+// so a decoder knows how many bits zlib reads before it rejects them.
+constexpr uint32_t X_BADSYM = 15u;
 __device__ __forceinline__ uint32_t sym_entry(int t, int s, int n) {
     if (t == 0) {
         if (s < 256) return (uint32_t)n | K_LIT << 4 | (uint32_t)s << 16;
         if (s == 256) return (uint32_t)n | K_EOB << 4;
         if (s < 286) return (uint32_t)n | K_LEN << 4 | (uint32_t)c_len_extra[s - 257] << 8 | (uint32_t)c_len_base[s - 257] << 16;
-        return 0;  // 286, 287: invalid literal/length code
+        return (uint32_t)n | K_LEN << 4 | X_BADSYM << 8;  // 286, 287: invalid literal/length symbol
     }
     if (s < 30) return (uint32_t)n | K_LEN << 4 | (uint32_t)c_dist_extra[s] << 8 | (uint32_t)c_dist_base[s] << 16;
-    return 0;  // 30, 31: invalid distance code
+    return (uint32_t)n | K_LEN << 4 | X_BADSYM << 8;  // 30, 31: invalid distance symbol
 }
 
 // A code longer than the primary table (11..15 bits): canonical decode by
@@ -517,7 +522,10 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t *__restrict__ in, 
         }
         // ---- Huffman tokens: two 64-bit windows of starts per pass ----
         if (bp > 8u * IN_STAGE - 320u) restage(sbase + (bp >> 3), bp & 7u);
-        // The token that would start at bit `pos`: packed length | kind << 6 | output bytes << 8.
+        // The token that would start at bit `pos`: packed length | stop << 6 | kind << 7 |
+        // output bytes << 9.  An invalid code is kind K_BAD with, as its length, the bits
+        // zlib reads before rejecting it (all 15 of a missing code, the code's own for an
+        // undefined symbol), so running out of input first is reported first, as zlib does.
         auto token = [&](uint32_t pos, uint32_t &dist, uint32_t &val) -> uint32_t {
             const uint32_t a = pos >> 5, sh = pos & 31u;
             const uint32_t w0 = s_in32[a], w1 = s_in32[a + 1], w2 = s_in32[a + 2];
@@ -525,23 +533,31 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t *__restrict__ in, 
                                (uint64_t)__builtin_amdgcn_alignbit(w2, w1, sh) << 32;
             uint32_t e = s_lit[x & ((1u << LB) - 1u)];
             if (((e >> 4) & 3u) == K_SLOW) e = long_decode(x, limL, baseL, s_sent);
-            const uint32_t n1 = e & 15u, kind = (e >> 4) & 3u;
+            const uint32_t n1 = e & 15u, eb = (e >> 8) & 15u;
+            uint32_t kind = (e >> 4) & 3u;
             uint32_t tl = n1, ol = kind == K_EOB ? 0u : 1u;
             dist = 0;
             val = e >> 16;
-            if (n1 && kind == K_LEN) {
-                const uint32_t eb = (e >> 8) & 15u;
+            if (!n1 || (kind == K_LEN && eb == X_BADSYM)) {
+                tl = n1 ? n1 : 15u;
+                kind = K_BAD;
+            } else if (kind == K_LEN) {
                 val += (uint32_t)(x >> n1) & ((1u << eb) - 1u);
                 const uint64_t y = x >> (n1 + eb);
                 uint32_t d = s_dst[y & ((1u << DB) - 1u)];
                 if (((d >> 4) & 3u) == K_SLOW) d = long_decode(y, limD, baseD, s_sent + 288);
                 const uint32_t n2 = d & 15u, db = (d >> 8) & 15u;
-                dist = (d >> 16) + ((uint32_t)(y >> n2) & ((1u << db) - 1u));
-                tl = n2 ? n1 + eb + n2 + db : 0u;
-                ol = val;
+                if (!n2 || db == X_BADSYM) {
+                    tl = n1 + eb + (n2 ? n2 : 15u);
+                    kind = K_BAD;
+                } else {
+                    dist = (d >> 16) + ((uint32_t)(y >> n2) & ((1u << db) - 1u));
+                    tl = n1 + eb + n2 + db;
+                    ol = val;
+                }
             }
-            if (!tl) ol = 0;
-            const uint32_t stopbit = (tl == 0 || kind == K_EOB) ? 64u : 0u;  // the chain ends here
+            if (kind == K_BAD) ol = 0;
+            const uint32_t stopbit = (kind == K_BAD || kind == K_EOB) ? 64u : 0u;  // the chain ends here
             return tl | stopbit | kind << 7 | ol << 9;
         };
         uint32_t dist0, val0, dist1, val1;
@@ -573,7 +589,7 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t *__restrict__ in, 
             const uint32_t last = M1 ? 127u - (uint32_t)__builtin_clzll(M1) : 63u - (uint32_t)__builtin_clzll(M0);
             const uint32_t info = last < 64 ? (uint32_t)__builtin_amdgcn_readlane((int)pk0, (int)last)
                                             : (uint32_t)__builtin_amdgcn_readlane((int)pk1, (int)(last - 64));
-            stop = (info & 63u) ? 1u : 3u;
+            stop = ((info >> 7) & 3u) == K_BAD ? 3u : 1u;
         }
         const uint64_t below = (1ull << lane) - 1ull;
         const uint32_t kind0 = (pk0 >> 7) & 3u, kind1 = (pk1 >> 7) & 3u;
@@ -616,7 +632,7 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t *__restrict__ in, 
         auto tok_bad = [&](uint64_t M, uint32_t pk, uint32_t start, bool on, uint32_t kind, uint32_t dist, int opos,
                            uint32_t olen) -> int32_t {
             const uint32_t tl = pk & 63u;
-            if (!((M >> lane) & 1ull) || tl == 0) return GZ_OK;
+            if (!((M >> lane) & 1ull)) return GZ_OK;
             if ((int64_t)start + tl > lim) return GZ_E_TRUNC;
             if (on && kind == K_LEN && dist > produced + (uint32_t)opos) return GZ_E_FAR;
             if (on && produced + (uint32_t)opos + olen > cap) return GZ_E_OVER;

@@ -799,13 +799,23 @@ int sdl_batcher_create(const sdl_config *cfg, const char *tokenizer_path, const 
         HIP_TRY(hipMemcpy(h->d_uentry.p, t.uentry.data(), t.uentry.size() * 4, hipMemcpyHostToDevice));
         HIP_TRY(hipMemcpy(h->d_upool.p, t.upool.data(), t.upool.size(), hipMemcpyHostToDevice));
         if (t.kind == TOK_UNIGRAM) {
-            // the device copy of the pieces table: bits 28-29 of a piece's id carry
-            // the f64 correction of its f32 score (tokenize_unigram.hip uni_cand)
+            // the device copy of the pieces table: a piece whose f64 score is one ulp
+            // off its f32 has bit 15 of its id set, and the f32 in word 3 negated when
+            // the ulp is towards zero (tokenize_unigram.hip uni_score64)
             std::vector<VSlot> ds(t.slots);
             for (VSlot &v : ds) {
                 const uint32_t cont = v.key >> 8;
-                if (v.id >= 0 && (cont == UC_PIECE || cont == UC_META))
-                    v.id |= (int32_t)(((uint32_t)t.uscore_adj[(size_t)v.id] & 3u) << 28);
+                if (v.id < 0 || (cont != UC_PIECE && cont != UC_META)) continue;
+                const int adj = t.uscore_adj[(size_t)v.id];
+                if (adj == 0) continue;
+                const float f = t.uscore32[(size_t)v.id];
+                if (v.id > 0x7FFF || !(f < 0.0f))
+                    throw std::runtime_error("Unigram: a score off its f32 needs id < 32768 and a negative score");
+                v.id |= 0x8000;
+                if (adj < 0) {
+                    const float g = -f;
+                    std::memcpy(&v.hash, &g, 4);
+                }
             }
             HIP_TRY(hipMemcpy(h->d_slots.p, ds.data(), ds.size() * sizeof(VSlot), hipMemcpyHostToDevice));
         } else {

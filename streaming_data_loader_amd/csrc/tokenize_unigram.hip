@@ -137,18 +137,22 @@ __device__ __forceinline__ int probe_result_w3(const Probe &P, uint32_t key, con
     return -1;
 }
 
-// A Unigram piece slot's id word carries, in bits 28-29, the ulp correction
-// that restores the piece's f64 score from the f32 in word 3 (the device copy
-// of the table only; sdl_batcher.cpp).  The score tokenizers holds is serde_
-// json's f64 parse of the tokenizer.json number (json.hpp), the f32 score or
-// one ulp off it.  Candidates keep id | correction << 16 in LDS.
-__device__ __forceinline__ uint32_t uni_cand(int y) { return ((uint32_t)y & 0xFFFFu) | (((uint32_t)y >> 28) & 3u) << 16; }
-__device__ __forceinline__ int uni_cand_id(uint32_t v) { return (int)(v & 0xFFFFu); }
-__device__ __forceinline__ int uni_piece_id(int y) { return y < 0 ? y : (int)((uint32_t)y & 0xFFFFu); }
-__device__ __forceinline__ double uni_score64(float f32, uint32_t cand) {
-    const int adj = (int32_t)(cand << 14) >> 30;  // bits 16-17, sign-extended
-    return __longlong_as_double(__double_as_longlong((double)f32) + adj);
+// The score tokenizers holds for a piece is serde_json's f64 parse of the
+// tokenizer.json number (json.hpp): the f32 score or one f64 ulp off it.  The
+// device pieces table (sdl_batcher.cpp) marks a piece one ulp off with bit 15
+// of its id and gives the direction by the sign of the f32 in word 3 (scores
+// are negative log-probabilities: stored as is, one ulp further from zero;
+// negated, one ulp nearer); LDS keeps the 16-bit id and the f32 as before.
+constexpr uint32_t UNI_ID_MASK = 0x7FFFu;
+__device__ __forceinline__ double uni_score64(float f, uint32_t id16) {
+    double d = (double)f;
+    if (id16 & 0x8000u) {
+        const long long b = __double_as_longlong(f < 0.0f ? d : -d);
+        d = __longlong_as_double(f < 0.0f ? b + 1 : b - 1);
+    }
+    return d;
 }
+__device__ __forceinline__ int uni_piece_id(int y) { return y < 0 ? y : (int)((uint32_t)y & UNI_ID_MASK); }
 
 // Added token "<...>" starting at p: the bytes up to the first '>' (within
 // max_special_len, not crossing a boundary) probed as UC_ADDED.  Returns the id
@@ -593,7 +597,7 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
     __shared__ uint32_t s_rowmask[TASK_CAP];    // per row: which candidate ends exist (<= UNI_WMAX + 1)
     __shared__ uint16_t s_vp_src[VP_CAP];
     __shared__ uint8_t s_vp_len[VP_CAP];
-    __shared__ uint32_t s_tid[TASK_CAP];  // uni_cand: id | score correction << 16
+    __shared__ uint16_t s_tid[TASK_CAP];
     __shared__ float s_tsc[TASK_CAP];
 
     const int tid = threadIdx.x;
@@ -1063,8 +1067,8 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
             const int id = gen[u] != -2 ? gen[u] : probe_result_w3(P[u], key, W[u], &w3);
             if (id < 0) continue;
             const int t = TASK_UNROLL * lane + u;
-            s_tid[t] = uni_cand(id);
-            s_tsc[t] = __uint_as_float(w3);  // the slot's f32 score (+ its correction: uni_score64)
+            s_tid[t] = (uint16_t)id;
+            s_tsc[t] = __uint_as_float(w3);  // the slot's f32 score, decoded with s_tid by uni_score64
             atomicOr(&s_rowmask[meta[u] & 0xFFFFu], 1u << ((meta[u] >> 16) & 0x3Fu));
         }
         __syncthreads();
@@ -1128,11 +1132,11 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
                         for (uint32_t mm = m >> gl; mm; mm >>= DPG, k += DPG) {
                             if (!(mm & 1u)) continue;
                             const int e = fe + k;
-                            const uint32_t cv = s_tid[rb + k];
-                            const double c = uni_score64(s_tsc[rb + k], cv) + base;
+                            const uint32_t id16 = s_tid[rb + k];
+                            const double c = uni_score64(s_tsc[rb + k], id16) + base;
                             if (c > gsc[e]) {
                                 gsc[e] = c;
-                                gbp[e] = (uint32_t)st | ((uint32_t)uni_cand_id(cv) << 16);
+                                gbp[e] = (uint32_t)st | ((id16 & UNI_ID_MASK) << 16);
                             }
                         }
                         if (!single && gl == DPG - 1) {  // unk: ends where no piece candidate does
@@ -1156,7 +1160,7 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
                             const int loc = vp_local(st == 0 ? -1 : st - 3, e - 3, L, Mm, Mf);
                             if (loc < 0 || !((rowmask(st) >> (e - (st == 0 ? 3 : st + 1))) & 1u)) return -1;
                             *sc = uni_score64(s_tsc[toff + loc], s_tid[toff + loc]);
-                            return uni_cand_id(s_tid[toff + loc]);
+                            return (int)(s_tid[toff + loc] & UNI_ID_MASK);
                         };
                         const int base = ktot;
                         ktot += unigram_backtrack(n, cand, gnodes, T.unk_id,
@@ -1289,7 +1293,7 @@ __global__ __launch_bounds__(64) void k_unigram_long(DevTok T, const uint8_t *__
     __shared__ double s_sc[NORM + 8];
     __shared__ uint32_t s_st[NORM + 8];  // node start | id << 16 (0xFFFF: unset)
     __shared__ uint16_t s_ids[2 * NORM + 16];
-    __shared__ uint32_t s_cid[KMAX * 64];     // [k][lane]: uni_cand of row lane's k-th end
+    __shared__ uint16_t s_cid[KMAX * 64];     // [k][lane]: id of row lane's k-th end
     __shared__ __attribute__((aligned(16))) float s_csc[KMAX * 64];
     // the item's raw bytes are staged where the candidate scores go later (the
     // normalization is done before the first probe): 1 KB less LDS per item
@@ -1507,8 +1511,8 @@ __global__ __launch_bounds__(64) void k_unigram_long(DevTok T, const uint8_t *__
                         }
                         if (id < 0) continue;
                         const int q = (int)(meta[u] & 0xFFu), k = (int)((meta[u] >> 8) & 0xFFu);
-                        s_cid[k * 64 + q] = uni_cand(id);
-                        s_csc[k * 64 + q] = __uint_as_float(w3);  // the slot's f32 score (k < KMAX host-checked)
+                        s_cid[k * 64 + q] = (uint16_t)id;
+                        s_csc[k * 64 + q] = __uint_as_float(w3);  // the slot's f32 score (uni_score64; k < KMAX host-checked)
                         atomicOr(&s_mask[q], 1ull << k);
                     }
                 }
@@ -1529,11 +1533,11 @@ __global__ __launch_bounds__(64) void k_unigram_long(DevTok T, const uint8_t *__
                     const bool single = (m >> (st + mb - fe)) & 1ull;
                     if (lane < KMAX && ((m >> lane) & 1ull)) {
                         const int e = fe + lane;
-                        const uint32_t cv = s_cid[lane * 64 + q];
-                        const double c = uni_score64(s_csc[lane * 64 + q], cv) + base;
+                        const uint32_t id16 = s_cid[lane * 64 + q];
+                        const double c = uni_score64(s_csc[lane * 64 + q], id16) + base;
                         if (s_st[e] == 0xFFFFFFFFu || c > s_sc[e]) {
                             s_sc[e] = c;
-                            s_st[e] = (uint32_t)st | ((uint32_t)uni_cand_id(cv) << 16);
+                            s_st[e] = (uint32_t)st | ((id16 & UNI_ID_MASK) << 16);
                         }
                     }
                     if (!single && lane == 63) {  // the unk candidate ends where no piece candidate does
