@@ -619,7 +619,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SDL_ROWS_WA
 // two, so about 30 % of a row's ~730 words are rejected and every row has
 // rejections.  Phase A runs each row's walk in one lane (64 rows per wave):
 // the lane computes its ChaCha12 blocks in registers, 16 words per block in an
-// unrolled loop, and writes each swap index j_i to the row's slice of `jbuf`.
+// unrolled loop, and writes each swap index j_i to the row's slice of `jbuf`;
+// the walk stops after step k (steps k-1 .. 1 only permute [0, k) among itself).
 // Phase B, a wave per row: mask_batch only uses the SET of the first k shuffled
 // positions, and Fisher-Yates from the end never moves a value out of [0, k)
 // once steps i < k begin (j_i <= i), so the set is what [0, k) holds after steps
@@ -649,18 +650,20 @@ __device__ __forceinline__ void chacha12_block(const uint32_t (&k)[8], uint32_t 
     o[12] = x12 + ctr; o[13] = x13; o[14] = x14; o[15] = x15;
 }
 
+template <int MR>
 __global__ __launch_bounds__(64) void k_mask_rand(RowParams P, const uint32_t *__restrict__ row_off,
                                                   const uint32_t *__restrict__ row_rec, SegSel sel, int64_t rows_cap,
                                                   uint16_t *__restrict__ jbuf, uint32_t *__restrict__ bits) {
-    __shared__ uint16_t s_j[RAND_MAX_S];
-    __shared__ uint32_t s_next[RAND_MAX_S];
-    __shared__ uint32_t s_bits[RAND_MAX_S / 32];
+    __shared__ uint32_t s_next[64 * MR];
+    __shared__ uint32_t s_bits[2 * MR];
     const int lane = lane_id();
     const int S = P.S, W = (S + 31) >> 5, kmask = P.mask_length < S ? P.mask_length : S;
+    // only steps i >= k move values into or out of [0, k): the walk stops there
+    const int i0 = kmask > 1 ? kmask : 1;
     const RowSpan rs = row_span(sel, row_off, P.B, rows_cap);
     constexpr uint32_t NONE = 0xFFFFFFFFu;
     for (int64_t g0 = rs.g_lo + (int64_t)blockIdx.x * 64; g0 < (int64_t)rs.g_real; g0 += (int64_t)gridDim.x * 64) {
-        // ---- A. lane per row: the shuffle's swap indices -------------------------
+        // ---- A. lane per row: the shuffle's swap indices j_i, i = S-1 .. k --------
         const int64_t g = g0 + lane;
         int i = 0;
         uint32_t key[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
@@ -677,13 +680,13 @@ __global__ __launch_bounds__(64) void k_mask_rand(RowParams P, const uint32_t *_
             i = S - 1;
         }
         uint32_t n = (uint32_t)i + 1u, zone = (n << __builtin_clz(n)) - 1u;
-        for (uint32_t blk = 0; __any(i >= 1); ++blk) {
+        for (uint32_t blk = 0; __any(i >= i0); ++blk) {
             uint32_t o[16];
             chacha12_block(key, blk, o);
 #pragma unroll
             for (int q = 0; q < 16; ++q) {
                 const uint64_t m = (uint64_t)o[q] * n;
-                if (i >= 1 && (uint32_t)m <= zone) {
+                if (i >= i0 && (uint32_t)m <= zone) {
                     jrow[i] = (uint16_t)(m >> 32);
                     --i;
                     n = (uint32_t)i + 1u;
@@ -693,21 +696,31 @@ __global__ __launch_bounds__(64) void k_mask_rand(RowParams P, const uint32_t *_
         }
         __syncthreads();  // (workgroup scope: the rows' indices are visible to the whole wave)
         // ---- B. wave per row: the first k positions' set -------------------------
+        // Row h+1's indices are loaded into registers while row h is resolved in LDS.
         const int64_t gz = g0 + 64 < (int64_t)rs.g_real ? g0 + 64 : (int64_t)rs.g_real;
-        for (int64_t h = g0; h < gz; ++h) {
+        uint32_t jn[MR];
+        auto load_row = [&](int64_t h) {
             const uint16_t *jr = jbuf + h * (int64_t)S;
-            for (int t = lane; t < S; t += 64) {
-                s_j[t] = t >= 1 ? jr[t] : (uint16_t)0;
-                s_next[t] = NONE;
+#pragma unroll
+            for (int m = 0; m < MR; ++m) {
+                const int t = lane + 64 * m;
+                jn[m] = t >= i0 && t < S ? (uint32_t)jr[t] : (uint32_t)t;  // (t, t): no move
             }
-            for (int w = lane; w < W; w += 64) s_bits[w] = 0u;
+        };
+        load_row(g0);
+        for (int64_t h = g0; h < gz; ++h) {
+            uint32_t jc[MR];
+#pragma unroll
+            for (int m = 0; m < MR; ++m) jc[m] = jn[m];
+            if (h + 1 < gz) load_row(h + 1);
+#pragma unroll
+            for (int m = 0; m < MR; ++m) s_next[lane + 64 * m] = NONE;
+            if (lane < 2 * MR) s_bits[lane] = 0u;
             __syncthreads();
             // next(p): the latest swap into p among steps i >= k (a self swap moves nothing)
-            const int i0 = kmask > 1 ? kmask : 1;
-            for (int t = i0 + lane; t < S; t += 64) {
-                const int j = s_j[t];
-                if (j != t) atomicMin(&s_next[j], (uint32_t)t);
-            }
+#pragma unroll
+            for (int m = 0; m < MR; ++m)
+                if (jc[m] != (uint32_t)(lane + 64 * m)) atomicMin(&s_next[jc[m]], (uint32_t)(lane + 64 * m));
             __syncthreads();
             // [0, k) holds val(next(x)) (or x): follow each chain to its end
             for (int x = lane; x < kmask; x += 64) {
@@ -716,8 +729,7 @@ __global__ __launch_bounds__(64) void k_mask_rand(RowParams P, const uint32_t *_
                 atomicOr(&s_bits[p >> 5], 1u << (p & 31));
             }
             __syncthreads();
-            uint32_t *dst = bits + h * (int64_t)W;
-            for (int w = lane; w < W; w += 64) dst[w] = s_bits[w];
+            if (lane < W) bits[h * (int64_t)W + lane] = s_bits[lane];
             __syncthreads();
         }
     }
@@ -726,10 +738,18 @@ __global__ __launch_bounds__(64) void k_mask_rand(RowParams P, const uint32_t *_
 hipError_t launch_mask_rand(const RowParams &P, const uint32_t *row_off, const uint32_t *row_rec, SegSel sel,
                             int64_t rows_cap, uint16_t *jbuf, uint32_t *bits, hipStream_t st) {
     if (rows_cap <= 0) return hipSuccess;
+    if (P.S > RAND_MAX_S) return hipErrorInvalidValue;
     const int64_t want = (rows_cap + 63) / 64;
     const int64_t grid = want < 4096 ? want : 4096;
-    hipLaunchKernelGGL(k_mask_rand, dim3((unsigned)grid), dim3(64), 0, st, P, row_off, row_rec, sel, rows_cap, jbuf,
-                       bits);
+    if (P.S <= 512)
+        hipLaunchKernelGGL(k_mask_rand<8>, dim3((unsigned)grid), dim3(64), 0, st, P, row_off, row_rec, sel, rows_cap,
+                           jbuf, bits);
+    else if (P.S <= 1024)
+        hipLaunchKernelGGL(k_mask_rand<16>, dim3((unsigned)grid), dim3(64), 0, st, P, row_off, row_rec, sel, rows_cap,
+                           jbuf, bits);
+    else
+        hipLaunchKernelGGL(k_mask_rand<RAND_MAX_S / 64>, dim3((unsigned)grid), dim3(64), 0, st, P, row_off, row_rec,
+                           sel, rows_cap, jbuf, bits);
     return hipGetLastError();
 }
 
@@ -1014,9 +1034,12 @@ __global__ __launch_bounds__(256) void k_rows_span(RowParams P, const uint32_t *
     __shared__ uint32_t s_win[4][SPAN_WBLK * 16];
     __shared__ double s_draw[4][128];
     __shared__ uint16_t s_dend[4][128];
+    __shared__ int32_t s_extra[100];    // <extra_id_0..99>: a sentinel store reads LDS, not global memory
     extern __shared__ int32_t s_rid[];  // [4][S]: each wave's row of framed ids (dynamic)
     const int lane = lane_id();
     const int wid = (int)(threadIdx.x >> 6);
+    if (threadIdx.x < 100) s_extra[threadIdx.x] = P.extra_ids[threadIdx.x];
+    __syncthreads();
     const int S = P.S, LW = P.label_width;
     const RowSpan rs = row_span(sel, row_off, P.B, rows_cap);
     const int64_t G = rs.g_real;
@@ -1045,7 +1068,7 @@ __global__ __launch_bounds__(256) void k_rows_span(RowParams P, const uint32_t *
             if (f < P.n_pre + (int64_t)cnt) return (int32_t)tok[t0 + (f - P.n_pre)];
             return frame_id(P.post, (int)(f - P.n_pre - cnt));
         };
-        auto extra = [&](uint32_t q) -> int32_t { return P.extra_ids[q < 100u ? q : 99u]; };
+        auto extra = [&](uint32_t q) -> int32_t { return s_extra[q < 100u ? q : 99u]; };
         // the row's framed ids into LDS first: one coalesced burst with every
         // load in flight, so the position-parallel writes below read LDS only
         int32_t *rid = s_rid + (size_t)wid * S;
