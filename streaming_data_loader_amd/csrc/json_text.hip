@@ -192,7 +192,8 @@ __global__ __launch_bounds__(64) void k_json_nl_count(const uint8_t *__restrict_
 }
 
 __global__ __launch_bounds__(64) void k_json_nl_write(const uint8_t *__restrict__ buf, int64_t len,
-                                                      const uint32_t *__restrict__ base, uint32_t *__restrict__ nl) {
+                                                      const uint32_t *__restrict__ base, uint32_t *__restrict__ nl,
+                                                      uint32_t cap) {
     const int64_t p0 = (int64_t)blockIdx.x * CHUNK + 16 * threadIdx.x;
     uint32_t m = 0;
     if (p0 < len) {
@@ -202,7 +203,8 @@ __global__ __launch_bounds__(64) void k_json_nl_write(const uint8_t *__restrict_
     }
     const uint32_t c = (uint32_t)__builtin_popcount(m);
     uint32_t at = base[blockIdx.x] + wave_incl_sum(c) - c;
-    for (; m; m &= m - 1) nl[at++] = (uint32_t)(p0 + __builtin_ctz(m));
+    for (; m; m &= m - 1, ++at)  // past `cap` the host grows the list and writes it again
+        if (at < cap) nl[at] = (uint32_t)(p0 + __builtin_ctz(m));
 }
 
 // line i = [start, end): after newline i - 1 up to newline i (or the end)
@@ -935,24 +937,26 @@ hipError_t launch_json_nl_count(const uint8_t *buf, int64_t len, uint32_t *cnt, 
     return launch_exclusive_scan(cnt, base, nb, scan_tmp, st);
 }
 
-hipError_t launch_json_nl_write(const uint8_t *buf, int64_t len, const uint32_t *base, uint32_t *nl, hipStream_t st) {
+hipError_t launch_json_nl_write(const uint8_t *buf, int64_t len, const uint32_t *base, uint32_t *nl, uint32_t cap,
+                                hipStream_t st) {
     const int64_t nb = (len + CHUNK - 1) / CHUNK;
     if (nb == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_json_nl_write, dim3((unsigned)nb), dim3(64), 0, st, buf, len, base, nl);
+    hipLaunchKernelGGL(k_json_nl_write, dim3((unsigned)nb), dim3(64), 0, st, buf, len, base, nl, cap);
     return hipGetLastError();
 }
 
 // {newline count, position of the last newline} in one word pair, so the host
 // reads both with one copy and one synchronisation
-__global__ void k_json_nl_tail(const uint32_t *__restrict__ total, const uint32_t *__restrict__ nl,
+// (the position is only valid when the list held every newline, n <= cap)
+__global__ void k_json_nl_tail(const uint32_t *__restrict__ total, const uint32_t *__restrict__ nl, uint32_t cap,
                                uint32_t *__restrict__ out) {
     const uint32_t n = *total;
     out[0] = n;
-    out[1] = n ? nl[n - 1] : 0u;
+    out[1] = n && n <= cap ? nl[n - 1] : 0u;
 }
 
-hipError_t launch_json_nl_tail(const uint32_t *total, const uint32_t *nl, uint32_t *out, hipStream_t st) {
-    hipLaunchKernelGGL(k_json_nl_tail, dim3(1), dim3(1), 0, st, total, nl, out);
+hipError_t launch_json_nl_tail(const uint32_t *total, const uint32_t *nl, uint32_t cap, uint32_t *out, hipStream_t st) {
+    hipLaunchKernelGGL(k_json_nl_tail, dim3(1), dim3(1), 0, st, total, nl, cap, out);
     return hipGetLastError();
 }
 

@@ -69,8 +69,11 @@ void print_bpe_cycles();
 // positions, parse and decode: lane per line below JL_MIN bytes, wave per line above)
 hipError_t launch_json_nl_count(const uint8_t *buf, int64_t len, uint32_t *cnt, uint32_t *base, uint32_t *scan_tmp,
                                 hipStream_t st);
-hipError_t launch_json_nl_write(const uint8_t *buf, int64_t len, const uint32_t *base, uint32_t *nl, hipStream_t st);
-hipError_t launch_json_nl_tail(const uint32_t *total, const uint32_t *nl, uint32_t *out, hipStream_t st);
+// the newline list holds `cap` positions; the count comes back in full, so a
+// caller whose list was too small grows it and writes it again
+hipError_t launch_json_nl_write(const uint8_t *buf, int64_t len, const uint32_t *base, uint32_t *nl, uint32_t cap,
+                                hipStream_t st);
+hipError_t launch_json_nl_tail(const uint32_t *total, const uint32_t *nl, uint32_t cap, uint32_t *out, hipStream_t st);
 hipError_t launch_json_parse(const uint8_t *buf, int64_t len, const uint32_t *nl, uint32_t n_nl, int64_t n_lines,
                              uint32_t *out_len, uint32_t *is_rec, uint2 *span, uint32_t *n_invalid, hipStream_t st);
 hipError_t launch_json_write(const uint8_t *buf, int64_t len, const uint32_t *nl, uint32_t n_nl, int64_t n_lines,

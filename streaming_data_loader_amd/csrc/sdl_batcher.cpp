@@ -1136,19 +1136,31 @@ int sdl_json_text_device(sdl_batcher *h, const uint8_t *d_jsonl, uint64_t len, v
         h->j_cnt.ensure((size_t)nb + 1);
         h->j_base.ensure((size_t)nb + 1);
         h->scan_tmp.ensure((size_t)scan_tmp_words(std::max<int64_t>(nb, 1)) + 1);
-        // the newline list is sized for the worst case (every byte), so the count and the last
-        // position come back together: one synchronisation instead of two
+        // the newline list is sized for JSON lines of >= 64 B on average (a record line is
+        // {"text": ...} plus the dump's fields), so the count and the last position come back
+        // together in one synchronisation; denser input grows the list and writes it again
         uint32_t n_nl = 0, last_nl = 0;
-        h->j_nl.ensure((size_t)N + 2);
+        const size_t nl_want = std::min<size_t>((size_t)N / 64 + 4096, (size_t)N + 2);
+        h->j_nl.ensure(nl_want);
         h->j_tail.ensure(2);
         if (nb) {
+            const uint32_t cap = (uint32_t)std::min<size_t>(h->j_nl.cap, 0xFFFFFFFFu);
             HIP_TRY(launch_json_nl_count(d_jsonl, N, h->j_cnt.p, h->j_base.p, h->scan_tmp.p, st));
-            HIP_TRY(launch_json_nl_write(d_jsonl, N, h->j_base.p, h->j_nl.p, st));
-            HIP_TRY(launch_json_nl_tail(h->j_base.p + nb, h->j_nl.p, h->j_tail.p, st));
+            HIP_TRY(launch_json_nl_write(d_jsonl, N, h->j_base.p, h->j_nl.p, cap, st));
+            HIP_TRY(launch_json_nl_tail(h->j_base.p + nb, h->j_nl.p, cap, h->j_tail.p, st));
             HIP_TRY(hipMemcpyAsync(h->pin_u32_2, h->j_tail.p, 8, hipMemcpyDeviceToHost, st));
             HIP_TRY(hipStreamSynchronize(st));
             n_nl = h->pin_u32_2[0];
             last_nl = h->pin_u32_2[1];
+            if (n_nl > cap) {  // more lines than the list held: grow it to the count, write again
+                h->j_nl.ensure((size_t)n_nl + 2);
+                const uint32_t cap2 = (uint32_t)std::min<size_t>(h->j_nl.cap, 0xFFFFFFFFu);
+                HIP_TRY(launch_json_nl_write(d_jsonl, N, h->j_base.p, h->j_nl.p, cap2, st));
+                HIP_TRY(launch_json_nl_tail(h->j_base.p + nb, h->j_nl.p, cap2, h->j_tail.p, st));
+                HIP_TRY(hipMemcpyAsync(h->pin_u32_2, h->j_tail.p, 8, hipMemcpyDeviceToHost, st));
+                HIP_TRY(hipStreamSynchronize(st));
+                last_nl = h->pin_u32_2[1];
+            }
         }
         // tokio lines(): a last line without '\n' counts, an empty tail does not
         const int64_t tail0 = n_nl ? (int64_t)last_nl + 1 : 0;

@@ -164,6 +164,41 @@ def test_oracle_rejects_corrupt_members(records):
                 zlib.decompress(member, 31)
 
 
+def first_member(data):
+    """What the reference's GzipDecoder (async-compression 0.3.14, `multiple_members`
+    off; gzip_file_provider.rs:18) yields for a file: the first member's bytes, the
+    rest of the file ignored.  zlib's decompressobj(31) stops the same way."""
+    d = zlib.decompressobj(31)
+    out = d.decompress(data) + d.flush()
+    assert d.eof
+    return out, d.unused_data
+
+
+def test_member_semantics_vs_reference(native_lib, records):
+    """The two deliberate divergences INTEGRATION.md ("Provider: gzip inflate")
+    states, pinned against the reference's single-member semantics."""
+    from streaming_data_loader_amd import native
+    data = payloads(records)["jsonl_x3"]
+    # BGZF: the reference stops after the first block; this path inflates every block.
+    b = bgzf(data, block=20000)
+    ref, rest = first_member(b)
+    assert ref == data[:20000] and len(rest) > 0
+    off = native.gzip_split_members(b)
+    ours = b"".join(oracle_lib.gz_inflate(b[int(off[i]):int(off[i + 1])])[1] for i in range(len(off) - 1))
+    assert ours == data == gzip.decompress(b)
+    # ...and the reference's output is exactly the first range's
+    assert oracle_lib.gz_inflate(b[int(off[0]):int(off[1])]) == (0, ref)
+    # `cat a.gz b.gz` as one range: the reference returns a; here the range fails loudly
+    a, c = gz_member(data[:7000]), gz_member(data[7000:9000])
+    ref, rest = first_member(a + c)
+    assert ref == data[:7000] and rest == c
+    assert list(native.gzip_split_members(a + c)) == [0, len(a + c)]  # not BGZF: one range
+    st, _ = oracle_lib.gz_inflate(a + c)
+    assert st != 0
+    # one range per file: every file's first (only) member, as the reference reads each file
+    assert [oracle_lib.gz_inflate(m)[1] for m in (a, c)] == [first_member(a)[0], first_member(c)[0]]
+
+
 def test_split_members_host_only(native_lib, records):
     from streaming_data_loader_amd import native
     data = payloads(records)["jsonl_x3"]
@@ -254,6 +289,28 @@ def test_device_bgzf_and_many_members(torch, native_lib, records):
     rc, out, status, got, arena = device_inflate(torch, db, members)
     assert rc == 0 and (status == 0).all()
     assert arena[:int(out.out_bytes)].tobytes() == data
+
+
+@pytest.mark.gpu
+def test_device_unaligned_files_as_integration_describes(torch, native_lib, records):
+    """INTEGRATION.md's recipe: .json.gz files concatenated with no padding,
+    offsets[k] = start of file k, only the base of d_gz aligned.  Every file
+    length here is odd, so no member after the first starts 16-B aligned."""
+    from streaming_data_loader_amd.device import DeviceBatcher
+    db = DeviceBatcher(batch_size=8, sequence_length=128)
+    lines = payloads(records)["jsonl"]
+    files, want = [], []
+    for k in range(7):
+        d = lines[k * 1111:(k + 1) * 1111 + 37 * k] + b"\n"
+        m = gz_member(d, level=(1, 6, 9)[k % 3], name=b"f%d.json" % k if k % 2 else b"")
+        if len(m) % 2 == 0:
+            m = gz_member(d, level=(1, 6, 9)[k % 3], name=b"f%d.jsonx" % k)
+        assert len(m) % 2 == 1
+        files.append(m)
+        want.append(d)
+    rc, out, status, got, arena = device_inflate(torch, db, files)
+    assert rc == 0 and (status == 0).all()
+    assert got == want and [first_member(f)[0] for f in files] == want
 
 
 @pytest.mark.gpu

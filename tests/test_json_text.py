@@ -137,6 +137,31 @@ def test_fixture_lines_and_noise(torch, native_lib, records, seed):
 
 
 @pytest.mark.gpu
+def test_dense_newlines_grow_the_line_list(torch, native_lib, records):
+    """The newline list is sized for ~64-B lines; blank and tiny lines past that
+    make the call grow it and write it again (one extra synchronisation).  Then
+    a normal buffer on the same handle: the grown list is reused."""
+    from streaming_data_loader_amd.device import DeviceBatcher
+    db = DeviceBatcher(batch_size=8, sequence_length=128)
+    rng = random.Random(11)
+    lines = fixture_jsonl(records, 4)
+    for i in range(30000):
+        lines.append(rng.choice([b"", b"{}", b'{"text":""}', b'{"text":"a"}', b" ", b"1"]))
+    rng.shuffle(lines)
+    buf = b"\n".join(lines) + b"\n\n"
+    assert buf.count(b"\n") > len(buf) // 64 + 4096
+    recs, out, _ = device_records(torch, db, buf)
+    want, n_lines, n_bad = J.json_text(buf)
+    assert (out.n_lines, out.n_invalid, out.n_records) == (n_lines, n_bad, len(want))
+    assert recs == want
+    buf2 = b"\n".join(fixture_jsonl(records, 5))  # no trailing newline
+    recs, out, _ = device_records(torch, db, buf2)
+    want, n_lines, n_bad = J.json_text(buf2)
+    assert (out.n_lines, out.n_records) == (n_lines, len(want)) and recs == want
+    db.close()
+
+
+@pytest.mark.gpu
 def test_json_lines_to_batches_on_device(torch, native_lib, records, oracle_tok):
     """JSON lines in HBM -> JsonText -> Batcher (mlm S=128 B=8) without leaving
     the device: the same rows as the oracle Batcher over the extracted texts."""
