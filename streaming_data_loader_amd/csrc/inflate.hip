@@ -32,6 +32,7 @@
 
 #include <cstdint>
 #include <cstdio>
+#include <type_traits>
 
 #include "device_util.hpp"
 #include "kernels.hpp"
@@ -189,24 +190,50 @@ __global__ void k_gz_size(const uint8_t *__restrict__ in, uint64_t in_len, const
 // (v_readlane), so one pass settles every token starting in the next 64 bits.
 // Literals and match records then go to the LDS batch in parallel (positions
 // by a wave prefix sum of the tokens' output lengths).
-__global__ __launch_bounds__(64) void k_inflate(const uint8_t *__restrict__ in, const uint64_t *__restrict__ moff,
-                                               uint64_t n, const uint32_t *__restrict__ ooff, uint8_t *__restrict__ out,
-                                               int32_t *__restrict__ status, uint32_t *__restrict__ tcrc) {
+//
+// CH (chunked members, see kernels.hpp): a wave decodes one chunk of a large
+// member -- from its start bit (or the member header) to the first block
+// boundary at or past its stop bit -- into a 16-bit slot: a byte, or 256 + w for
+// a copy from byte w of the 32 KiB window before the chunk (resolved later, in
+// stream order).  A block that would overflow the slot ends the chunk at that
+// block's start (GZC_SOFT) unless it is the chunk's first.
+template <bool CH>
+__global__ __launch_bounds__(64) void k_inflate_t(const uint8_t *__restrict__ in, const uint64_t *__restrict__ moff,
+                                                 uint64_t n, const uint32_t *__restrict__ ooff, uint8_t *__restrict__ out,
+                                                 int32_t *__restrict__ status, uint32_t *__restrict__ tcrc,
+                                                 GzChunkArgs ca) {
+    typedef typename std::conditional<CH, uint16_t, uint8_t>::type OT;  // batch / output values
     __shared__ uint32_t s_lit[1 << LB], s_dst[1 << DB];
     __shared__ uint32_t s_sent[NSYM];     // table entries of the symbols sorted by code: lit/len [0, 288), dist [288, 320)
     __shared__ uint8_t s_len[NSYM + 32];  // code lengths (lit/len, then dist); code-length code at NSYM..
     __shared__ __attribute__((aligned(16))) uint32_t s_in32[IN_STAGE / 4 + 4];
-    __shared__ uint8_t s_ob[OBUF];
+    __shared__ OT s_ob[OBUF];
     __shared__ uint16_t s_ref[OBUF];      // 0: byte known; d: byte equals the one d back
     __shared__ uint32_t s_mpl[MLCAP];     // match: batch offset | length << 16
     __shared__ uint16_t s_md[MLCAP];      // match distance
 
     const uint64_t m = blockIdx.x;
     const int lane = (int)threadIdx.x;
-    if (status[m] != GZ_OK) return;  // sizing found the member unusable
-    const uint64_t ma = moff[m], mz = moff[m + 1];
-    uint8_t *const dst = out + ooff[m];
-    const uint32_t cap = ooff[m + 1] - ooff[m];
+    uint64_t ma, mz, start_bit = GZ_START_HEADER, stop_bit = GZ_NO_BIT, hdr_bit = GZ_START_HEADER;
+    uint32_t cap, c = 0;
+    OT *dst;
+    if constexpr (CH) {
+        c = ca.list[m];
+        ma = ca.ma;
+        mz = ca.mz;
+        cap = ca.cap;
+        dst = ca.slots + (uint64_t)c * ca.cap;
+        start_bit = ca.start_bit[c];
+        stop_bit = ca.stop_bit[c];
+        hdr_bit = ca.hdr_bit[c];
+    } else {
+        if (status[m] != GZ_OK) return;  // sizing found the member unusable
+        ma = moff[m];
+        mz = moff[m + 1];
+        dst = out + ooff[m];
+        cap = ooff[m + 1] - ooff[m];
+    }
+    const bool from_header = start_bit == GZ_START_HEADER;
     const uint32_t mlen = (uint32_t)(mz - ma);
     uint8_t *const s_in = reinterpret_cast<uint8_t *>(s_in32);
 #ifdef SDL_STAMPS
@@ -216,7 +243,7 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t *__restrict__ in, 
     // ---- member header (lane 0, straight from global memory) ----
     int32_t err = GZ_OK;
     uint32_t p = 10;  // member-relative
-    if (lane == 0) {
+    if (lane == 0 && from_header) {
         const uint32_t flg = in[ma + 3];
         if (flg & 0xE0u) err = GZ_E_HEADER;  // reserved flag bits (zlib: "unknown header flags set")
         if (!err && (flg & 4u)) {  // FEXTRA
@@ -243,7 +270,10 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t *__restrict__ in, 
         if (!err && (uint64_t)p + 8 > mlen) err = GZ_E_TRUNC;
     }
     if (bfl((uint32_t)err) != GZ_OK) {
-        if (lane == 0) status[m] = err;
+        if (lane == 0) {
+            if constexpr (CH) ca.status[c] = err;
+            else status[m] = err;
+        }
         return;
     }
 
@@ -274,13 +304,22 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t *__restrict__ in, 
         const uint32_t a = pos >> 5;
         return __builtin_amdgcn_alignbit(s_in32[a + 1], s_in32[a], pos & 31u);
     };
-    restage(ma + bfl(p), 0);
+    // (CH) a chunk that resumes inside a block parses that block's header first
+    bool resume = !from_header && hdr_bit != start_bit;  // wave-uniform
+    if (from_header) restage(ma + bfl(p), 0);
+    else restage(hdr_bit >> 3, (uint32_t)(hdr_bit & 7u));
     GZ_STAMP(0);
     GZ_COUNT(0);
 
     enum : uint32_t { A_ERR, A_BUILD, A_STORED };
     uint32_t produced = 0, nb = 0, nm = 0;  // wave-uniform
     bool in_block = false, final_seen = false;
+    uint64_t blk_bit = 0;    // (CH) the current block's header bit
+    // (CH) the last point the output was flushed at -- a block boundary or a batch inside a
+    // block (with that block's header bit): where a chunk stops when its slot is full
+    uint64_t cut_bit = start_bit, cut_hdr = hdr_bit;
+    uint32_t cut_prod = 0;
+    bool soft = false;       // (CH) stopped at the cut: the slot is full
     uint32_t limL[5], baseL[5], limD[5], baseD[5];  // long codes (11..15 bits) of the block, long_decode
     // Every pass consumes bits, flushes a non-empty batch or restages, so a
     // member takes fewer than 4 (8 mlen + cap) + 64 passes; the cap and the
@@ -295,6 +334,14 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t *__restrict__ in, 
         }
         if (!in_block) {
             if (final_seen) break;
+            if constexpr (CH) {
+                blk_bit = 8 * sbase + bp;
+                if (!resume) {
+                    cut_bit = cut_hdr = blk_bit;
+                    cut_prod = produced;
+                    if (blk_bit >= stop_bit) break;  // the next chunk's block
+                }
+            }
             if (bp > 8u * (IN_STAGE - HDR_ROOM)) {
                 restage(sbase + (bp >> 3), bp & 7u);
                 continue;
@@ -435,6 +482,10 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t *__restrict__ in, 
                 int32_t e2 = GZ_OK;
                 if ((uint64_t)start + len + 8 > mlen) e2 = GZ_E_TRUNC;
                 else if (produced + len > cap) e2 = GZ_E_OVER;
+                if (CH && e2 == GZ_E_OVER && cut_prod > 0) {
+                    soft = true;
+                    break;
+                }
                 if (e2 != GZ_OK) {
                     if (lane == 0) err = e2;
                     break;
@@ -516,6 +567,10 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t *__restrict__ in, 
             }
             __syncthreads();
             in_block = true;
+            if (CH && resume) {  // the tables are built: continue at the chunk's start inside the block
+                restage(start_bit >> 3, (uint32_t)(start_bit & 7u));
+                resume = false;
+            }
             GZ_STAMP(2);
             GZ_COUNT(2);
             continue;
@@ -634,7 +689,7 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t *__restrict__ in, 
             const uint32_t tl = pk & 63u;
             if (!((M >> lane) & 1ull)) return GZ_OK;
             if ((int64_t)start + tl > lim) return GZ_E_TRUNC;
-            if (on && kind == K_LEN && dist > produced + (uint32_t)opos) return GZ_E_FAR;
+            if (on && kind == K_LEN && dist > produced + (uint32_t)opos && from_header) return GZ_E_FAR;
             if (on && produced + (uint32_t)opos + olen > cap) return GZ_E_OVER;
             return GZ_OK;
         };
@@ -644,6 +699,10 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t *__restrict__ in, 
         if (bm0 | bm1) {
             const int32_t b0 = bm0 ? __builtin_amdgcn_readlane(bad0, (int)__builtin_ctzll(bm0))
                                    : __builtin_amdgcn_readlane(bad1, (int)__builtin_ctzll(bm1));
+            if (CH && b0 == GZ_E_OVER && cut_prod > 0) {  // the slot is full: the chunk ends at the last cut
+                soft = true;
+                break;
+            }
             if (lane == 0) err = b0;
             break;
         }
@@ -656,14 +715,14 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t *__restrict__ in, 
             break;
         }
         if (on0 && kind0 == K_LIT) {
-            s_ob[opos0] = (uint8_t)val0;
+            s_ob[opos0] = (OT)val0;
             s_ref[opos0] = 0;
         } else if (on0 && kind0 == K_LEN) {
             s_mpl[midx0] = (uint32_t)opos0 | val0 << 16;
             s_md[midx0] = (uint16_t)dist0;
         }
         if (on1 && kind1 == K_LIT) {
-            s_ob[opos1] = (uint8_t)val1;
+            s_ob[opos1] = (OT)val1;
             s_ref[opos1] = 0;
         } else if (on1 && kind1 == K_LEN) {
             s_mpl[midx1] = (uint32_t)opos1 | val1 << 16;
@@ -703,7 +762,11 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t *__restrict__ in, 
 #pragma unroll
                     for (int j = 0; j < 8; ++j) {  // history sources: all loads in flight
                         const int src = (int)(b0 + (uint32_t)lane + 64u * j) - (int)d[j];
-                        v[j] = d[j] && src < 0 ? (uint32_t)dst[(int64_t)produced + src] : 0u;
+                        const int64_t hp = (int64_t)produced + src;
+                        if (CH && hp < 0)  // before the chunk: a window marker (distances are <= 32 KiB)
+                            v[j] = d[j] && src < 0 ? 256u + (uint32_t)(32768 + hp) : 0u;
+                        else
+                            v[j] = d[j] && src < 0 ? (uint32_t)dst[hp] : 0u;
                     }
 #pragma unroll
                     for (int j = 0; j < 8; ++j) {
@@ -719,7 +782,7 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t *__restrict__ in, 
                             }
                             v[j] = s_ob[src];
                         }
-                        s_ob[qq] = (uint8_t)v[j];
+                        s_ob[qq] = (OT)v[j];
                         s_ref[qq] = 0;
                     }
                 }
@@ -736,8 +799,31 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t *__restrict__ in, 
         produced += nb;
         nb = 0;
         nm = 0;
+        if constexpr (CH) {
+            cut_bit = 8 * sbase + bp;
+            cut_hdr = in_block ? blk_bit : cut_bit;
+            cut_prod = produced;
+        }
         GZ_STAMP(6);
         GZ_COUNT(6);
+    }
+    if constexpr (CH) {
+        if (lane == 0) {
+            const uint64_t at = 8 * sbase + bp;
+            if (!err && final_seen && !soft) {  // the final block ended here: the trailer's CRC
+                const uint64_t t = (at + 7) >> 3;
+                if (t + 8 > mz) err = GZ_E_TRUNC;
+                else
+                    ca.tcrc[0] = (uint32_t)in[t] | (uint32_t)in[t + 1] << 8 | (uint32_t)in[t + 2] << 16 |
+                                 (uint32_t)in[t + 3] << 24;
+            }
+            ca.status[c] = err;
+            ca.len[c] = soft ? cut_prod : produced;
+            ca.end_bit[c] = soft ? cut_bit : at;
+            ca.end_hdr[c] = soft ? cut_hdr : at;
+            ca.flags[c] = (final_seen && !soft ? (uint32_t)GZC_FINAL : 0u) | (soft ? (uint32_t)GZC_SOFT : 0u);
+        }
+        return;
     }
     // ---- trailer ----
     if (lane == 0) {
@@ -772,7 +858,10 @@ __global__ __launch_bounds__(64) void k_gz_crc(const uint32_t *__restrict__ ooff
         T[i] = c;
     }
     __syncthreads();
-    if (status[m] == GZ_OK) {
+    int32_t s0 = status[m];
+    const bool pre = (s0 & GZ_VERIFIED) != 0;  // a chunked member: decoded and CRC-checked already
+    s0 &= ~GZ_VERIFIED;
+    if (s0 == GZ_OK && !pre) {
         const uint32_t a = ooff[m], len = ooff[m + 1] - a;
         const uint32_t seg = ((len + 63u) / 64u + 15u) & ~15u;
         const uint32_t la = (uint32_t)lane * seg < len ? (uint32_t)lane * seg : len;
@@ -805,10 +894,326 @@ __global__ __launch_bounds__(64) void k_gz_crc(const uint32_t *__restrict__ ooff
         }
     }
     __syncthreads();
-    if (lane == 0 && status[m] != GZ_OK) {
+    if (lane == 0 && pre) status[m] = s0;
+    if (lane == 0 && (pre ? s0 : status[m]) != GZ_OK) {
         atomicAdd(&bad[0], 1u);
         atomicMin(&bad[1], (uint32_t)m);
     }
+}
+
+// ---- chunked members: block-header search ----------------------------------------
+// One wave per chunk scans bit offsets from the chunk's nominal start: every lane
+// tests one offset for a dynamic-block header whose fixed fields are legal and
+// whose code-length code is complete (Kraft sum exactly 1, as zlib requires);
+// the survivors, in offset order, get the full check by lane 0 -- the code
+// lengths decoded with their repeat rules, an end-of-block code, literal/length
+// and distance codes neither over-subscribed nor incomplete (zlib's
+// inflate_table rules).  A wrong pick only costs time: the host accepts a chunk
+// only when it starts exactly where its predecessor stopped.
+constexpr int FIND_STAGE = 4096;  // staged bytes per step
+__global__ __launch_bounds__(64) void k_gz_find(const uint8_t *__restrict__ in, uint64_t ma, uint64_t mz,
+                                               const uint64_t *__restrict__ nominal, uint64_t span,
+                                               uint64_t *__restrict__ found) {
+    __shared__ __attribute__((aligned(16))) uint32_t s_in32[FIND_STAGE / 4 + 4];
+    __shared__ uint8_t s_len[NSYM];
+    __shared__ uint16_t s_cl[128];
+    const int lane = (int)threadIdx.x;
+    const uint64_t c = blockIdx.x;
+    const uint64_t q0 = nominal[c];
+    const uint64_t lim = 8 * (mz - 8);  // the deflate data ends before the trailer
+    uint64_t res = GZ_NO_BIT;
+    const uint64_t qz = q0 + span < lim ? q0 + span : lim;
+    for (uint64_t base = q0; base < qz && res == GZ_NO_BIT;) {
+        const uint64_t sb = (base >> 3) & ~(uint64_t)15;  // staged from this byte
+        for (int k = lane; k < FIND_STAGE / 16; k += 64) {
+            const uint64_t q = sb + 16 * (uint64_t)k;
+            uint4 v = make_uint4(0, 0, 0, 0);
+            if (q + 16 <= mz) v = *reinterpret_cast<const uint4 *>(in + q);
+            else if (q < mz) {
+                uint32_t w[4] = {0, 0, 0, 0};
+                for (int b = 0; b < 16 && q + b < mz; ++b) w[b >> 2] |= (uint32_t)in[q + b] << (8 * (b & 3));
+                v = make_uint4(w[0], w[1], w[2], w[3]);
+            }
+            reinterpret_cast<uint4 *>(s_in32)[k] = v;
+        }
+        if (lane == 0) reinterpret_cast<uint4 *>(s_in32)[FIND_STAGE / 16] = make_uint4(0, 0, 0, 0);
+        __syncthreads();
+        auto peek = [&](uint32_t pos) -> uint32_t {  // 32 stage bits from bit pos
+            const uint32_t a = pos >> 5;
+            return __builtin_amdgcn_alignbit(s_in32[a + 1], s_in32[a], pos & 31u);
+        };
+        // offsets tested from this stage: a full header (<= ~600 B) must fit behind them
+        const uint32_t p0 = (uint32_t)(base - 8 * sb);
+        const uint32_t pz = 8u * (FIND_STAGE - HDR_ROOM);
+        for (uint32_t pb = p0; pb < pz && res == GZ_NO_BIT; pb += 64) {
+            const uint32_t pos = pb + (uint32_t)lane;
+            const uint64_t abs = 8 * sb + pos;
+            const uint32_t lo = peek(pos), mid = peek(pos + 32), hi = peek(pos + 64);
+            bool ok = abs < qz && ((lo >> 1) & 3u) == 2u && ((lo >> 3) & 31u) <= 29u && ((lo >> 8) & 31u) <= 29u;
+            if (ok) {
+                const int hclen = (int)((lo >> 13) & 15u) + 4;
+                const uint64_t y = (((uint64_t)mid << 32 | lo) >> 17) | ((uint64_t)hi << 47);
+                uint32_t kraft = 0;
+                for (int i = 0; i < hclen; ++i) {
+                    const uint32_t l = (uint32_t)(y >> (3 * i)) & 7u;
+                    kraft += l ? 1u << (7 - l) : 0u;
+                }
+                ok = kraft == 128u;
+            }
+            for (uint64_t cand = __ballot(ok); cand && res == GZ_NO_BIT; cand &= cand - 1) {
+                const uint32_t at = pb + (uint32_t)__builtin_ctzll(cand);
+                uint32_t good = 0;
+                if (lane == 0) {  // the full check (k_inflate's header parse, no tables kept)
+                    uint64_t bb = 0;
+                    int bc = 0;
+                    uint32_t fill = at;
+                    auto need = [&](int k) {
+                        if (bc < k) {
+                            bb |= (uint64_t)peek(fill) << bc;
+                            fill += 32;
+                            bc += 32;
+                        }
+                    };
+                    auto drop = [&](int k) {
+                        bb >>= k;
+                        bc -= k;
+                    };
+                    need(17);
+                    const int hlit = (int)((bb >> 3) & 31u) + 257, hdist = (int)((bb >> 8) & 31u) + 1,
+                              hclen = (int)((bb >> 13) & 15u) + 4;
+                    drop(17);
+                    uint8_t cl[19];
+                    for (int i = 0; i < 19; ++i) cl[i] = 0;
+                    for (int i = 0; i < hclen; ++i) {
+                        need(3);
+                        cl[c_cl_order[i]] = (uint8_t)(bb & 7u);
+                        drop(3);
+                    }
+                    uint16_t cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0}, next[8];
+                    for (int i = 0; i < 19; ++i) ++cnt[cl[i]];
+                    uint32_t code = 0;
+                    cnt[0] = 0;
+                    for (int l = 1; l < 8; ++l) {
+                        code = (code + cnt[l - 1]) << 1;
+                        next[l] = (uint16_t)code;
+                    }
+                    for (int i = 0; i < 128; ++i) s_cl[i] = 0;
+                    for (int sy = 0; sy < 19; ++sy)
+                        if (cl[sy]) {
+                            const int l = cl[sy];
+                            const uint32_t r = __builtin_bitreverse32((uint32_t)next[l]++) >> (32 - l);
+                            for (uint32_t i = r; i < 128; i += 1u << l) s_cl[i] = (uint16_t)(l | sy << 8);
+                        }
+                    const int total = hlit + hdist;
+                    int i = 0;
+                    bool bad = false;
+                    while (i < total && !bad) {
+                        need(14);
+                        const uint32_t e = s_cl[bb & 127u];
+                        const int sy = (int)(e >> 8);
+                        drop((int)(e & 15u));
+                        if (sy < 16) {
+                            s_len[i++] = (uint8_t)sy;
+                            continue;
+                        }
+                        int rep;
+                        uint8_t v = 0;
+                        if (sy == 16) {
+                            if (i == 0) { bad = true; break; }
+                            v = s_len[i - 1];
+                            rep = 3 + (int)(bb & 3u);
+                            drop(2);
+                        } else if (sy == 17) {
+                            rep = 3 + (int)(bb & 7u);
+                            drop(3);
+                        } else {
+                            rep = 11 + (int)(bb & 127u);
+                            drop(7);
+                        }
+                        if (i + rep > total) { bad = true; break; }
+                        while (rep--) s_len[i++] = v;
+                    }
+                    if (!bad && s_len[256] == 0) bad = true;
+                    for (int t = 0; t < 2 && !bad; ++t) {  // inflate_table: LENS, then DISTS
+                        const int b0 = t ? hlit : 0, nn = t ? hdist : hlit;
+                        uint16_t count[16];
+                        for (int l = 0; l < 16; ++l) count[l] = 0;
+                        for (int k = 0; k < nn; ++k) ++count[s_len[b0 + k]];
+                        int left = 1, mx = 0;
+                        for (int l = 1; l < 16; ++l) {
+                            left = (left << 1) - count[l];
+                            if (left < 0) bad = true;
+                            if (count[l]) mx = l;
+                        }
+                        if (mx > 0 && left > 0 && mx != 1) bad = true;
+                    }
+                    // the header must end inside the data
+                    good = !bad && 8 * sb + (uint64_t)(fill - (uint32_t)bc) <= lim;
+                }
+                if (bfl(good)) res = 8 * sb + at;
+            }
+        }
+        base = 8 * sb + pz;  // the next stage starts where this one's offsets stopped
+        __syncthreads();
+    }
+    if (lane == 0) found[c] = res;
+}
+
+// ---- chunked members: the window chain, in stream order ---------------------------
+// window[j] = the last 32 KiB of the output through ordered chunk j: its own
+// values, or (a chunk shorter than the window) the tail of window[j - 1]; a
+// marker 256 + w is byte w of window[j - 1].  One block walks the chain; the next
+// chunk's slot values are loaded while the current one resolves.
+constexpr int WIN32K = 32768;
+constexpr int GZW_THREADS = 1024;
+constexpr int GZW_PER = WIN32K / GZW_THREADS;
+__global__ __launch_bounds__(GZW_THREADS) void k_gz_windows(const uint16_t *__restrict__ slots, uint32_t cap,
+                                                           const uint32_t *__restrict__ order,
+                                                           const uint32_t *__restrict__ len, uint64_t n_order,
+                                                           uint8_t *__restrict__ windows) {
+    __shared__ uint8_t w[2][WIN32K];
+    const int t = (int)threadIdx.x;
+    for (int i = t; i < WIN32K; i += GZW_THREADS) w[0][i] = 0;
+    uint32_t nv[GZW_PER];
+    auto fetch = [&](uint64_t j) {  // chunk j's last 32 KiB (slot values; below 0: the previous window)
+        const uint32_t c = order[j], L = len[c];
+        const uint16_t *sl = slots + (uint64_t)c * cap;
+#pragma unroll
+        for (int k = 0; k < GZW_PER; ++k) {
+            const int i = t + GZW_THREADS * k;
+            const int64_t q = (int64_t)L - WIN32K + i;  // position in the chunk
+            nv[k] = q >= 0 ? (uint32_t)sl[q] : 0x10000u | (uint32_t)(i + (int)L);  // 0x10000: window byte
+        }
+    };
+    if (n_order) fetch(0);
+    __syncthreads();
+    for (uint64_t j = 0; j < n_order; ++j) {
+        uint32_t cv[GZW_PER];
+#pragma unroll
+        for (int k = 0; k < GZW_PER; ++k) cv[k] = nv[k];
+        if (j + 1 < n_order) fetch(j + 1);
+        const uint8_t *cur = w[j & 1];
+        uint8_t *nxt = w[(j + 1) & 1];
+        uint8_t *gw = windows + j * (uint64_t)WIN32K;
+#pragma unroll
+        for (int k = 0; k < GZW_PER; ++k) {
+            const int i = t + GZW_THREADS * k;
+            const uint32_t v = cv[k];
+            const uint32_t b = v >= 0x10000u ? cur[v & 0xFFFFu] : v >= 256u ? cur[v - 256u] : v;
+            nxt[i] = (uint8_t)b;
+            gw[i] = (uint8_t)b;
+        }
+        __syncthreads();
+    }
+}
+
+// ---- chunked members: bytes, CRC-32 per chunk ----------------------------------------
+constexpr int GZR_THREADS = 256;
+__global__ __launch_bounds__(GZR_THREADS) void k_gz_resolve(const uint16_t *__restrict__ slots, uint32_t cap,
+                                                           const uint32_t *__restrict__ order,
+                                                           const uint32_t *__restrict__ len,
+                                                           const uint64_t *__restrict__ pos,
+                                                           const uint8_t *__restrict__ windows, uint8_t *__restrict__ out,
+                                                           uint32_t *__restrict__ crc, uint32_t *__restrict__ shift,
+                                                           X2N x2n, int32_t *__restrict__ status) {
+    __shared__ uint32_t T[256];
+    __shared__ uint32_t s_p[GZR_THREADS];
+    const uint64_t j = blockIdx.x;
+    const int t = (int)threadIdx.x;
+    for (int i = t; i < 256; i += GZR_THREADS) {
+        uint32_t c = (uint32_t)i;
+        for (int k = 0; k < 8; ++k) c = c & 1u ? (c >> 1) ^ POLY : c >> 1;
+        T[i] = c;
+    }
+    const uint32_t c = order[j], L = len[c];
+    const uint64_t P = pos[j];
+    const uint16_t *sl = slots + (uint64_t)c * cap;
+    const uint8_t *win = j ? windows + (j - 1) * (uint64_t)WIN32K : windows;
+    // a marker w is the byte P - 32768 + w of the stream: before the stream is too far back
+    const uint32_t wmin = P >= (uint64_t)WIN32K ? 0u : (uint32_t)(WIN32K - P);
+    uint8_t *dst = out + P;
+    bool far = false;
+    for (uint32_t i = (uint32_t)t; i < L; i += GZR_THREADS) {
+        uint32_t v = sl[i];
+        if (v >= 256u) {
+            far |= v - 256u < wmin || j == 0;
+            v = win[v - 256u];
+        }
+        dst[i] = (uint8_t)v;
+    }
+    if (__syncthreads_or(far) && t == 0) status[0] = GZ_E_FAR;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    // CRC-32 of GZR_THREADS segments, folded with crc32_combine's shift
+    const uint32_t seg = ((L + GZR_THREADS - 1u) / GZR_THREADS + 15u) & ~15u;
+    const uint32_t la = (uint32_t)t * seg < L ? (uint32_t)t * seg : L;
+    const uint32_t lz = la + seg < L ? la + seg : L;
+    uint32_t cc = ~0u;
+    for (uint32_t i = la; i < lz; ++i) cc = T[(cc ^ dst[i]) & 255u] ^ (cc >> 8);
+    s_p[t] = ~cc;
+    __syncthreads();
+    if (t == 0) {
+        const uint32_t xs = x2nmodp(seg, 3, x2n);
+        uint32_t tot = L ? s_p[0] : 0u;
+        for (int l = 1; l < GZR_THREADS; ++l) {
+            const uint32_t sa = (uint32_t)l * seg;
+            if (sa >= L) break;
+            const uint32_t sln = sa + seg <= L ? seg : L - sa;
+            tot = multmodp(sln == seg ? xs : x2nmodp(sln, 3, x2n), tot) ^ s_p[l];
+        }
+        crc[j] = tot;
+        shift[j] = x2nmodp(L, 3, x2n);
+    }
+}
+
+// the member's CRC-32: crc(A B) = crc(A) x^(8|B|) mod P ^ crc(B), in stream order
+// (the member's status gets GZ_VERIFIED: k_inflate skips it, k_gz_crc only counts it)
+__global__ void k_gz_crc_fold(const uint32_t *__restrict__ crc, const uint32_t *__restrict__ shift, uint64_t n,
+                              const uint32_t *__restrict__ tcrc, const int32_t *__restrict__ status,
+                              int32_t *__restrict__ mstatus) {
+    if (threadIdx.x != 0) return;
+    uint32_t tot = 0;
+    for (uint64_t j = 0; j < n; ++j) tot = multmodp(shift[j], tot) ^ crc[j];
+    int32_t st = status[0];
+    if (st == GZ_OK && tot != tcrc[0]) st = GZ_E_CRC;
+    mstatus[0] = st | GZ_VERIFIED;
+}
+
+hipError_t launch_gz_find(const uint8_t *in, uint64_t ma, uint64_t mz, const uint64_t *nominal, uint64_t n_chunks,
+                          uint64_t span, uint64_t *found, hipStream_t st) {
+    if (!n_chunks) return hipSuccess;
+    hipLaunchKernelGGL(k_gz_find, dim3((unsigned)n_chunks), dim3(64), 0, st, in, ma, mz, nominal, span, found);
+    return hipGetLastError();
+}
+
+hipError_t launch_inflate_chunks(const uint8_t *in, const GzChunkArgs &a, uint64_t n_list, hipStream_t st) {
+    if (!n_list) return hipSuccess;
+    hipLaunchKernelGGL(k_inflate_t<true>, dim3((unsigned)n_list), dim3(64), 0, st, in, (const uint64_t *)nullptr,
+                       (uint64_t)0, (const uint32_t *)nullptr, (uint8_t *)nullptr, (int32_t *)nullptr,
+                       (uint32_t *)nullptr, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_gz_windows(const uint16_t *slots, uint32_t cap, const uint32_t *order, const uint32_t *len,
+                             uint64_t n_order, uint8_t *windows, hipStream_t st) {
+    if (!n_order) return hipSuccess;
+    hipLaunchKernelGGL(k_gz_windows, dim3(1), dim3(GZW_THREADS), 0, st, slots, cap, order, len, n_order, windows);
+    return hipGetLastError();
+}
+
+hipError_t launch_gz_resolve(const uint16_t *slots, uint32_t cap, const uint32_t *order, const uint32_t *len,
+                             const uint64_t *pos, uint64_t n_order, const uint8_t *windows, uint8_t *out,
+                             uint32_t *crc, uint32_t *shift, const X2N &x2n, int32_t *status, hipStream_t st) {
+    if (!n_order) return hipSuccess;
+    hipLaunchKernelGGL(k_gz_resolve, dim3((unsigned)n_order), dim3(GZR_THREADS), 0, st, slots, cap, order, len, pos,
+                       windows, out, crc, shift, x2n, status);
+    return hipGetLastError();
+}
+
+hipError_t launch_gz_crc_fold(const uint32_t *crc, const uint32_t *shift, uint64_t n_order, const uint32_t *tcrc,
+                              const int32_t *status, int32_t *mstatus, hipStream_t st) {
+    hipLaunchKernelGGL(k_gz_crc_fold, dim3(1), dim3(64), 0, st, crc, shift, n_order, tcrc, status, mstatus);
+    return hipGetLastError();
 }
 
 hipError_t launch_gz_size(const uint8_t *in, uint64_t in_len, const uint64_t *moff, uint64_t n, uint32_t *size,
@@ -822,7 +1227,8 @@ hipError_t launch_gz_size(const uint8_t *in, uint64_t in_len, const uint64_t *mo
 hipError_t launch_inflate(const uint8_t *in, const uint64_t *moff, uint64_t n, const uint32_t *ooff, uint8_t *out,
                           int32_t *status, uint32_t *tcrc, hipStream_t st) {
     if (!n) return hipSuccess;
-    hipLaunchKernelGGL(k_inflate, dim3((unsigned)n), dim3(64), 0, st, in, moff, n, ooff, out, status, tcrc);
+    hipLaunchKernelGGL(k_inflate_t<false>, dim3((unsigned)n), dim3(64), 0, st, in, moff, n, ooff, out, status, tcrc,
+                       GzChunkArgs{});
     return hipGetLastError();
 }
 

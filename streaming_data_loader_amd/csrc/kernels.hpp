@@ -97,7 +97,8 @@ enum : int32_t {
     GZ_E_SIZE = 11,   // output length != ISIZE
     GZ_E_TRAIL = 12,  // bytes after the member's trailer
     GZ_E_CRC = 13,    // CRC-32 mismatch
-    GZ_E_STALL = 14   // the decoder made no progress (a guard: unreachable with the shipped batch size)
+    GZ_E_STALL = 14,  // the decoder made no progress (a guard: unreachable with the shipped batch size)
+    GZ_VERIFIED = 0x100  // (internal) a member finished by the chunked path: k_inflate skips it, k_gz_crc counts it
 };
 struct X2N {
     uint32_t t[32];  // x^(2^k) mod P (zlib's x2n_table)
@@ -108,6 +109,51 @@ hipError_t launch_inflate(const uint8_t *in, const uint64_t *moff, uint64_t n, c
                           int32_t *status, uint32_t *tcrc, hipStream_t st);
 hipError_t launch_gz_crc(const uint32_t *ooff, const uint8_t *out, uint64_t n, const uint32_t *tcrc, const X2N &x2n,
                          int32_t *status, uint32_t *bad, hipStream_t st);
+
+// One large gzip member inflated in parallel (inflate.hip, "chunked members"):
+// the deflate stream is cut into chunks of the compressed bytes; each chunk
+// after the first starts at a dynamic-block header found by search, decodes into
+// a 16-bit slot (bytes < 256, 256 + w = byte w of the 32 KiB window before the
+// chunk), and stops at the first block boundary at or past the next chunk's
+// nominal start; the host checks that every chunk starts where its predecessor
+// stopped (and redecodes the ones that do not), the window chain is resolved in
+// stream order, then every chunk's bytes are written and CRC'd in parallel.
+constexpr uint64_t GZ_NO_BIT = ~0ull;          // chunk: no start found / never stop
+constexpr uint64_t GZ_START_HEADER = ~0ull - 1;  // chunk: start at the member's gzip header
+enum : uint32_t { GZC_FINAL = 1, GZC_SOFT = 2 };  // chunk flags: final block reached; stopped: slot full
+struct GzChunkArgs {
+    uint64_t ma, mz;            // the member's byte range in `in`
+    const uint32_t *list;       // blockIdx.x -> chunk index
+    const uint64_t *start_bit;  // per chunk: absolute bit in `in`, or GZ_START_HEADER
+    const uint64_t *hdr_bit;    // per chunk: the header of the block it starts in (== start_bit at a boundary)
+    const uint64_t *stop_bit;   // per chunk: stop at the first block boundary at or past it
+    uint16_t *slots;            // per chunk: `cap` values
+    uint32_t cap;
+    uint64_t *end_bit;          // out: where the chunk stopped: a block boundary, or (GZC_SOFT, slot
+                                //      full) a flush point inside a block ...
+    uint64_t *end_hdr;          // out: ... with that block's header bit (else == end_bit)
+    uint32_t *len;              // out: values produced
+    uint32_t *flags;            // out: GZC_*
+    int32_t *status;            // out: GZ_*
+    uint32_t *tcrc;             // out: the trailer's CRC-32 (a chunk that reaches the final block)
+};
+// first dynamic-block header at or past nominal[c] (bits), searching `span` bits;
+// found[c] = its bit or GZ_NO_BIT
+hipError_t launch_gz_find(const uint8_t *in, uint64_t ma, uint64_t mz, const uint64_t *nominal, uint64_t n_chunks,
+                          uint64_t span, uint64_t *found, hipStream_t st);
+hipError_t launch_inflate_chunks(const uint8_t *in, const GzChunkArgs &a, uint64_t n_list, hipStream_t st);
+// windows[j] = the 32 KiB before chunk order[j + 1], for the chunks in stream order
+hipError_t launch_gz_windows(const uint16_t *slots, uint32_t cap, const uint32_t *order, const uint32_t *len,
+                             uint64_t n_order, uint8_t *windows, hipStream_t st);
+// every ordered chunk's bytes to out + pos[j] (markers through windows[j - 1]), its CRC-32
+// and x^(8 len) mod P; status[0] = GZ_E_FAR when a marker reaches before the stream
+hipError_t launch_gz_resolve(const uint16_t *slots, uint32_t cap, const uint32_t *order, const uint32_t *len,
+                             const uint64_t *pos, uint64_t n_order, const uint8_t *windows, uint8_t *out,
+                             uint32_t *crc, uint32_t *shift, const X2N &x2n, int32_t *status, hipStream_t st);
+// the member's CRC-32 from the chunks' (crc, shift), checked against tcrc; writes
+// mstatus[0] = (status[0], or GZ_E_CRC) | GZ_VERIFIED
+hipError_t launch_gz_crc_fold(const uint32_t *crc, const uint32_t *shift, uint64_t n_order, const uint32_t *tcrc,
+                              const int32_t *status, int32_t *mstatus, hipStream_t st);
 
 // pipeline.hip
 // out[0..n) = exclusive prefix sum of in[0..n) (+ *carry_in when given),

@@ -289,6 +289,12 @@ struct sdl_batcher {
     DevBuf<int32_t> z_status;
     DevBuf<unsigned long long> z_total;
     DevBuf<uint8_t> z_out;
+    // ... large members in chunks (inflate_chunked)
+    DevBuf<uint64_t> zc_nominal, zc_start, zc_hdr, zc_stop, zc_end, zc_endhdr, zc_pos;
+    DevBuf<uint32_t> zc_list, zc_len, zc_flags, zc_order, zc_crc, zc_shift, zc_tcrc;
+    DevBuf<int32_t> zc_status, zc_rstatus;
+    DevBuf<uint16_t> zc_slots;
+    DevBuf<uint8_t> zc_windows;
     // Transport frames (sdl_pickle_frames_device)
     DevBuf<uint8_t> f_out, f_out2;
     DevBuf<uint8_t> *f_target = &f_out;  // where the next frames go
@@ -1249,6 +1255,168 @@ X2N make_x2n() {  // zlib's x2n_table: x^(2^k) mod P(x), reflected
 
 }  // namespace
 
+// A gzip member of >= GZ_SPLIT_MIN compressed bytes -- a single-member .json.gz,
+// the reference's own input -- is inflated in chunks (kernels.hpp, "chunked
+// members"): header search per chunk, all chunks decoded at once into 16-bit
+// slots, then the host walks them in stream order and accepts a chunk only where
+// it starts exactly at its predecessor's stop (any other is decoded again from
+// there: a wrong header pick, a boundary the search skips -- stored or fixed
+// blocks --, or one behind a chunk whose slot filled up: that chunk stopped at its
+// last flush point, inside a block, and the next resumes there after parsing the
+// block's header again), and the window
+// chain, bytes, CRC-32 and ISIZE follow on the device.  The member's status gets
+// GZ_VERIFIED so the one-wave path skips it.
+constexpr uint64_t GZ_SPLIT_MIN = 1u << 20;  // smaller members: one wave each
+constexpr uint64_t GZ_CHUNK = 64u << 10;     // compressed bytes per chunk (at least)
+constexpr uint64_t GZ_MAX_CHUNKS = 4096;     // (larger members: larger chunks)
+constexpr uint32_t GZ_SLOT_RATIO = 16;       // slot values per compressed byte of a chunk
+constexpr uint64_t GZ_FIND_SPAN = 2;         // header search: this many chunk lengths of bits
+constexpr uint64_t GZ_EXTRA_CHUNKS = 256;    // chunks appended behind one that stopped for capacity
+
+void inflate_chunked(sdl_batcher *h, const uint8_t *d_gz, uint64_t m, uint64_t ma, uint64_t mz, uint32_t isize,
+                     uint32_t ooff_m, hipStream_t st) {
+    const uint64_t len = mz - ma;
+    uint64_t ch = GZ_CHUNK;
+    while ((len + ch - 1) / ch > GZ_MAX_CHUNKS) ch *= 2;
+    const uint64_t C0 = (len - 8 + ch - 1) / ch;  // nominal starts ma + c ch < mz - 8
+    const uint64_t CT = C0 + GZ_EXTRA_CHUNKS;
+    const uint32_t cap = (uint32_t)(ch * GZ_SLOT_RATIO);
+    h->zc_nominal.ensure(CT);
+    h->zc_start.ensure(CT);
+    h->zc_hdr.ensure(CT);
+    h->zc_stop.ensure(CT);
+    h->zc_end.ensure(CT);
+    h->zc_endhdr.ensure(CT);
+    h->zc_pos.ensure(CT);
+    h->zc_list.ensure(CT);
+    h->zc_len.ensure(CT);
+    h->zc_flags.ensure(CT);
+    h->zc_order.ensure(CT);
+    h->zc_crc.ensure(CT);
+    h->zc_shift.ensure(CT);
+    h->zc_tcrc.ensure(1);
+    h->zc_status.ensure(CT);
+    h->zc_rstatus.ensure(1);
+    h->zc_slots.ensure((size_t)CT * cap);
+    std::vector<uint64_t> nominal(CT, GZ_NO_BIT), start(CT, GZ_NO_BIT), hdr(CT, GZ_NO_BIT), stop(CT, GZ_NO_BIT),
+        end(CT, 0), endhdr(CT, 0);
+    std::vector<uint32_t> clen(CT, 0), flags(CT, 0);
+    std::vector<int32_t> status(CT, GZ_OK);
+    for (uint64_t c = 1; c < C0; ++c) nominal[c] = 8 * (ma + c * ch);
+    for (uint64_t c = 0; c + 1 < C0; ++c) stop[c] = nominal[c + 1];
+    HIP_TRY(hipMemcpyAsync(h->zc_nominal.p, nominal.data(), C0 * 8, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(h->zc_stop.p, stop.data(), C0 * 8, hipMemcpyHostToDevice, st));
+    if (C0 > 1)
+        HIP_TRY(launch_gz_find(d_gz, ma, mz, h->zc_nominal.p + 1, C0 - 1, 8 * GZ_FIND_SPAN * ch, h->zc_start.p + 1, st));
+    HIP_TRY(hipMemcpyAsync(start.data() + 1, h->zc_start.p + 1, (C0 - 1) * 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    start[0] = GZ_START_HEADER;
+    for (uint64_t c = 0; c < C0; ++c) hdr[c] = start[c];  // found starts are block boundaries
+    HIP_TRY(hipMemcpyAsync(h->zc_start.p, start.data(), 8, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(h->zc_hdr.p, hdr.data(), C0 * 8, hipMemcpyHostToDevice, st));
+    GzChunkArgs a{};
+    a.ma = ma;
+    a.mz = mz;
+    a.list = h->zc_list.p;
+    a.start_bit = h->zc_start.p;
+    a.hdr_bit = h->zc_hdr.p;
+    a.stop_bit = h->zc_stop.p;
+    a.slots = h->zc_slots.p;
+    a.cap = cap;
+    a.end_bit = h->zc_end.p;
+    a.end_hdr = h->zc_endhdr.p;
+    a.len = h->zc_len.p;
+    a.flags = h->zc_flags.p;
+    a.status = h->zc_status.p;
+    a.tcrc = h->zc_tcrc.p;
+    // (i) every chunk with a start, at once
+    std::vector<uint32_t> list;
+    for (uint64_t c = 0; c < C0; ++c)
+        if (start[c] != GZ_NO_BIT) list.push_back((uint32_t)c);
+    HIP_TRY(hipMemcpyAsync(h->zc_list.p, list.data(), list.size() * 4, hipMemcpyHostToDevice, st));
+    HIP_TRY(launch_inflate_chunks(d_gz, a, list.size(), st));
+    HIP_TRY(hipMemcpyAsync(end.data(), h->zc_end.p, C0 * 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(endhdr.data(), h->zc_endhdr.p, C0 * 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(clen.data(), h->zc_len.p, C0 * 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(flags.data(), h->zc_flags.p, C0 * 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(status.data(), h->zc_status.p, C0 * 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    // (ii) the chain in stream order; a chunk that does not start where its
+    // predecessor stopped is decoded again from there
+    auto redo = [&](uint64_t d, uint64_t from, uint64_t from_hdr) {
+        start[d] = from;
+        hdr[d] = from_hdr;
+        const uint32_t one = (uint32_t)d;
+        HIP_TRY(hipMemcpyAsync(h->zc_start.p + d, &start[d], 8, hipMemcpyHostToDevice, st));
+        HIP_TRY(hipMemcpyAsync(h->zc_hdr.p + d, &hdr[d], 8, hipMemcpyHostToDevice, st));
+        HIP_TRY(hipMemcpyAsync(h->zc_stop.p + d, &stop[d], 8, hipMemcpyHostToDevice, st));
+        HIP_TRY(hipMemcpyAsync(h->zc_list.p, &one, 4, hipMemcpyHostToDevice, st));
+        HIP_TRY(launch_inflate_chunks(d_gz, a, 1, st));
+        HIP_TRY(hipMemcpyAsync(&end[d], h->zc_end.p + d, 8, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(&endhdr[d], h->zc_endhdr.p + d, 8, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(&clen[d], h->zc_len.p + d, 4, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(&flags[d], h->zc_flags.p + d, 4, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(&status[d], h->zc_status.p + d, 4, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+    };
+    std::vector<uint32_t> order;
+    std::vector<uint64_t> pos;
+    uint64_t C = C0, total = 0;
+    int32_t err = GZ_OK;
+    bool done = false;
+    for (uint64_t c = 0;;) {
+        if (status[c] != GZ_OK) {
+            err = status[c];
+            break;
+        }
+        order.push_back((uint32_t)c);
+        pos.push_back(total);
+        total += clen[c];
+        if (flags[c] & GZC_FINAL) {
+            done = true;
+            break;
+        }
+        uint64_t d = c + 1;
+        if (d >= C) {  // the last chunk stopped for capacity: one more behind it
+            if (C >= CT) {
+                err = GZ_E_OVER;
+                break;
+            }
+            d = C++;
+            stop[d] = GZ_NO_BIT;
+            start[d] = GZ_NO_BIT;
+        }
+        if (start[d] != end[c] || hdr[d] != endhdr[c]) redo(d, end[c], endhdr[c]);
+        c = d;
+    }
+    if (err == GZ_OK && !done) err = GZ_E_TRUNC;
+    if (err == GZ_OK) {  // the trailer right behind the final block, and ISIZE
+        const uint64_t t = (end[order.back()] + 7) >> 3;
+        if (t + 8 > mz) err = GZ_E_TRUNC;
+        else if (t + 8 != mz) err = GZ_E_TRAIL;
+        else if (total != isize) err = GZ_E_SIZE;
+    }
+    if (err == GZ_E_OVER || err == GZ_E_STALL) return;  // (chunk slots exhausted: the one-wave path decodes it)
+    if (err != GZ_OK) {
+        const int32_t v = err | GZ_VERIFIED;
+        HIP_TRY(hipMemcpyAsync(h->z_status.p + m, &v, 4, hipMemcpyHostToDevice, st));
+        HIP_TRY(hipStreamSynchronize(st));  // (v is on this stack)
+        return;
+    }
+    // (iii) window chain, bytes + CRC per chunk, the member's CRC
+    const uint64_t no = order.size();
+    h->zc_windows.ensure((size_t)no * 32768);
+    HIP_TRY(hipMemcpyAsync(h->zc_order.p, order.data(), no * 4, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(h->zc_pos.p, pos.data(), no * 8, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemsetAsync(h->zc_rstatus.p, 0, 4, st));
+    static const X2N x2n = make_x2n();
+    HIP_TRY(launch_gz_windows(h->zc_slots.p, cap, h->zc_order.p, h->zc_len.p, no, h->zc_windows.p, st));
+    HIP_TRY(launch_gz_resolve(h->zc_slots.p, cap, h->zc_order.p, h->zc_len.p, h->zc_pos.p, no, h->zc_windows.p,
+                              h->z_out.p + ooff_m, h->zc_crc.p, h->zc_shift.p, x2n, h->zc_rstatus.p, st));
+    HIP_TRY(launch_gz_crc_fold(h->zc_crc.p, h->zc_shift.p, no, h->zc_tcrc.p, h->zc_rstatus.p, h->z_status.p + m, st));
+    HIP_TRY(hipStreamSynchronize(st));  // (order / pos are host vectors)
+}
+
 int sdl_gzip_inflate_device(sdl_batcher *h, const uint8_t *d_gz, uint64_t gz_len, const uint64_t *d_member_offsets,
                             uint64_t n_members, void *stream, sdl_inflated *out) {
     if (!h || !out || (n_members && (!d_gz || !d_member_offsets))) return fail(SDL_ERR_ARG, "null argument");
@@ -1278,6 +1446,24 @@ int sdl_gzip_inflate_device(sdl_batcher *h, const uint8_t *d_gz, uint64_t gz_len
         h->z_out.ensure((size_t)total + 48);
         HIP_TRY(hipMemsetAsync(h->z_out.p + total, 0, 32, st));
         uint32_t bad[2] = {0, 0xFFFFFFFFu};
+        if (n) {  // large members first, in chunks (they leave GZ_VERIFIED statuses)
+            std::vector<uint64_t> mo(n + 1);
+            HIP_TRY(hipMemcpyAsync(mo.data(), d_member_offsets, (n + 1) * 8, hipMemcpyDeviceToHost, st));
+            HIP_TRY(hipStreamSynchronize(st));
+            std::vector<uint64_t> big;
+            for (size_t m = 0; m < n; ++m)
+                if (mo[m + 1] > mo[m] && mo[m + 1] - mo[m] >= GZ_SPLIT_MIN && mo[m + 1] <= gz_len) big.push_back(m);
+            if (!big.empty()) {
+                std::vector<uint32_t> sz(n), oo(n);
+                std::vector<int32_t> zs(n);
+                HIP_TRY(hipMemcpyAsync(sz.data(), h->z_size.p, n * 4, hipMemcpyDeviceToHost, st));
+                HIP_TRY(hipMemcpyAsync(oo.data(), h->z_off.p, n * 4, hipMemcpyDeviceToHost, st));
+                HIP_TRY(hipMemcpyAsync(zs.data(), h->z_status.p, n * 4, hipMemcpyDeviceToHost, st));
+                HIP_TRY(hipStreamSynchronize(st));
+                for (uint64_t m : big)
+                    if (zs[m] == GZ_OK) inflate_chunked(h, d_gz, m, mo[m], mo[m + 1], sz[m], oo[m], st);
+            }
+        }
         if (n) {
             HIP_TRY(hipMemcpyAsync(h->z_bad.p, bad, sizeof(bad), hipMemcpyHostToDevice, st));
             HIP_TRY(launch_inflate(d_gz, d_member_offsets, n_members, h->z_off.p, h->z_out.p, h->z_status.p, h->z_tcrc.p, st));

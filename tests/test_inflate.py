@@ -332,3 +332,99 @@ def test_device_rejects_corrupt_members(torch, native_lib, records):
     # the handle stays usable after a failed call
     rc, out, status, got, _ = device_inflate(torch, db, [good])
     assert rc == 0 and got[0] == zlib.decompress(good, 31)
+
+
+# ---- GPU: large single members, inflated in chunks (the reference's input shape) ----
+
+def big_lines(records, mib, seed=0):
+    rng = random.Random(seed)
+    out, size = [], 0
+    while size < mib << 20:
+        t = records[rng.randrange(len(records))]
+        ln = json.dumps({"id": len(out), "text": t}).encode() + b"\n"
+        out.append(ln)
+        size += len(ln)
+    return b"".join(out)
+
+
+def chunked_cases(records):
+    """(name, member, expected bytes): members of >= 1 MiB compressed take the
+    chunked path (GZ_SPLIT_MIN in sdl_batcher.cpp)."""
+    rng = random.Random(3)
+    lines = big_lines(records, 8)
+    noise = bytes(rng.randrange(256) for _ in range(1_200_000))
+    cases = [
+        ("jsonl l6", gz_member(lines, 6), lines),
+        ("jsonl l1", gz_member(lines, 1), lines),
+        ("jsonl l9 filtered", gz_member(lines, 9, zlib.Z_FILTERED), lines),
+        ("jsonl huffman-only", gz_member(lines[:3_000_000], 6, zlib.Z_HUFFMAN_ONLY), lines[:3_000_000]),
+        ("jsonl rle", gz_member(lines[:4_000_000], 6, zlib.Z_RLE), lines[:4_000_000]),
+        ("jsonl header fields + full flushes", gz_member(lines, 6, name=b"dump.json", comment=b"x", flags=2,
+                                                         flush_every=1 << 20), lines),
+        # no dynamic blocks to find: every chunk is decoded again from its predecessor's end
+        ("fixed codes", gz_member(lines[:3_000_000], 6, zlib.Z_FIXED), lines[:3_000_000]),
+        ("stored + text", gz_member(noise + lines[:2_000_000], 6), noise + lines[:2_000_000]),
+        # a block that outgrows a chunk's slot (long runs): the one-wave path takes the member
+        ("runs", gz_member(noise + b"a" * 5_000_000 + lines[:500_000], 9), noise + b"a" * 5_000_000 + lines[:500_000]),
+    ]
+    for name, m, _ in cases:
+        assert len(m) >= 1 << 20, (name, len(m))
+    return cases
+
+
+@pytest.mark.gpu
+def test_device_chunked_members_match_zlib(torch, native_lib, records):
+    from streaming_data_loader_amd.device import DeviceBatcher
+    db = DeviceBatcher(batch_size=8, sequence_length=128)
+    for name, member, want in chunked_cases(records):
+        rc, out, status, got, _ = device_inflate(torch, db, [member])
+        assert rc == 0 and status[0] == 0, (name, rc, status[0])
+        assert got[0] == want == zlib.decompress(member, 31), name
+
+
+@pytest.mark.gpu
+def test_device_chunked_member_among_small_ones(torch, native_lib, records):
+    """One call: small members (one wave each) around a large one (chunked),
+    the reference fixture among them."""
+    from streaming_data_loader_amd.device import DeviceBatcher
+    db = DeviceBatcher(batch_size=8, sequence_length=128)
+    lines = big_lines(records, 6, seed=1)
+    ref = open(REF_GZ, "rb").read()
+    small = [gz_member(lines[:5000]), ref, gz_member(b"")]
+    members = [small[0], gz_member(lines), small[1], gz_member(lines[::-1]), small[2]]
+    want = [zlib.decompress(m, 31) for m in members]
+    rc, out, status, got, arena = device_inflate(torch, db, members)
+    assert rc == 0 and (status == 0).all()
+    assert got == want
+
+
+@pytest.mark.gpu
+def test_device_chunked_member_errors(torch, native_lib, records):
+    """Damage in a large member fails it (not its neighbours) with the oracle's
+    status where the reason does not depend on where a decoder notices it."""
+    from streaming_data_loader_amd.device import DeviceBatcher
+    from streaming_data_loader_amd import native
+    db = DeviceBatcher(batch_size=8, sequence_length=128)
+    lines = big_lines(records, 6, seed=2)
+    good = gz_member(lines)
+    bad_crc = bytearray(good)
+    bad_crc[-8] ^= 1
+    bad_size = bytearray(good)
+    bad_size[-2] ^= 1                      # ISIZE still within DEFLATE's bound
+    trunc = good[:len(good) * 2 // 3]
+    trailing = good + b"\x00\x01"
+    mid = bytearray(good)
+    mid[len(good) // 2] ^= 0xFF            # damage deep inside: some GZ_E_* (where it is noticed varies)
+    cases = [("crc", bytes(bad_crc), 13), ("isize", bytes(bad_size), None), ("truncated", trunc, None),
+             ("trailing", trailing, None), ("middle", bytes(mid), None)]
+    small = gz_member(lines[:3000])
+    for name, m, want in cases:
+        rc, out, status, got, _ = device_inflate(torch, db, [small, m, small], check=False)
+        ost, _ = oracle_lib.gz_inflate(m)
+        assert rc == native.SDL_ERR_DATA and out.n_bad == 1, name
+        assert status[0] == 0 and status[2] == 0 and got[0] == got[2] == lines[:3000], name
+        assert status[1] != 0 and ost != 0, name
+        if want is not None:
+            assert status[1] == want == ost, (name, status[1], ost)
+    rc, out, status, got, _ = device_inflate(torch, db, [good])  # the handle stays usable
+    assert rc == 0 and got[0] == lines
