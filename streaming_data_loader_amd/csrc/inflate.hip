@@ -214,7 +214,8 @@ __global__ __launch_bounds__(64) void k_inflate_t(const uint8_t *__restrict__ in
 
     const uint64_t m = blockIdx.x;
     const int lane = (int)threadIdx.x;
-    uint64_t ma, mz, start_bit = GZ_START_HEADER, stop_bit = GZ_NO_BIT, hdr_bit = GZ_START_HEADER;
+    uint64_t ma, mz, start_bit = GZ_START_HEADER, hdr_bit = GZ_START_HEADER;
+    uint32_t tgt = 0;  // (CH) the next chunk this one may hand over to
     uint32_t cap, c = 0;
     OT *dst;
     if constexpr (CH) {
@@ -224,7 +225,6 @@ __global__ __launch_bounds__(64) void k_inflate_t(const uint8_t *__restrict__ in
         cap = ca.cap;
         dst = ca.slots + (uint64_t)c * ca.cap;
         start_bit = ca.start_bit[c];
-        stop_bit = ca.stop_bit[c];
         hdr_bit = ca.hdr_bit[c];
     } else {
         if (status[m] != GZ_OK) return;  // sizing found the member unusable
@@ -320,6 +320,8 @@ __global__ __launch_bounds__(64) void k_inflate_t(const uint8_t *__restrict__ in
     uint64_t cut_bit = start_bit, cut_hdr = hdr_bit;
     uint32_t cut_prod = 0;
     bool soft = false;       // (CH) stopped at the cut: the slot is full
+    if constexpr (CH) tgt = ca.tgt0[c];
+    bool handed = false;     // (CH) stopped at chunk tgt's start
     uint32_t limL[5], baseL[5], limD[5], baseD[5];  // long codes (11..15 bits) of the block, long_decode
     // Every pass consumes bits, flushes a non-empty batch or restages, so a
     // member takes fewer than 4 (8 mlen + cap) + 64 passes; the cap and the
@@ -339,7 +341,19 @@ __global__ __launch_bounds__(64) void k_inflate_t(const uint8_t *__restrict__ in
                 if (!resume) {
                     cut_bit = cut_hdr = blk_bit;
                     cut_prod = produced;
-                    if (blk_bit >= stop_bit) break;  // the next chunk's block
+                    // hand over to the first later chunk whose searched start is this block: a
+                    // candidate behind us was no block start; a block start the search did not
+                    // pick (stored, fixed, past its span) is decoded through
+                    while (tgt < ca.n_chunks && blk_bit >= ca.nominal[tgt]) {
+                        const uint64_t f = ca.found[tgt];
+                        if (blk_bit == f) {
+                            handed = true;
+                            break;
+                        }
+                        if (blk_bit < f) break;
+                        ++tgt;
+                    }
+                    if (handed) break;
                 }
             }
             if (bp > 8u * (IN_STAGE - HDR_ROOM)) {
@@ -822,6 +836,7 @@ __global__ __launch_bounds__(64) void k_inflate_t(const uint8_t *__restrict__ in
             ca.end_bit[c] = soft ? cut_bit : at;
             ca.end_hdr[c] = soft ? cut_hdr : at;
             ca.flags[c] = (final_seen && !soft ? (uint32_t)GZC_FINAL : 0u) | (soft ? (uint32_t)GZC_SOFT : 0u);
+            ca.next[c] = handed ? tgt : ~0u;
         }
         return;
     }
@@ -902,30 +917,140 @@ __global__ __launch_bounds__(64) void k_gz_crc(const uint32_t *__restrict__ ooff
 }
 
 // ---- chunked members: block-header search ----------------------------------------
-// One wave per chunk scans bit offsets from the chunk's nominal start: every lane
-// tests one offset for a dynamic-block header whose fixed fields are legal and
-// whose code-length code is complete (Kraft sum exactly 1, as zlib requires);
-// the survivors, in offset order, get the full check by lane 0 -- the code
-// lengths decoded with their repeat rules, an end-of-block code, literal/length
-// and distance codes neither over-subscribed nor incomplete (zlib's
-// inflate_table rules).  A wrong pick only costs time: the host accepts a chunk
-// only when it starts exactly where its predecessor stopped.
+// A block of 4 waves per chunk scans bit offsets from the chunk's nominal start, a
+// staged 4 KiB of input at a time.  Every offset of the stage is tested first for
+// a dynamic-block header whose fixed fields are legal and whose code-length code is
+// complete (Kraft sum exactly 1, as zlib requires) -- about 0.09 % of offsets in
+// real DEFLATE data survive -- and the survivors are then checked in full, one per
+// thread, all at once (dyn_header_ok); the lowest passing offset is the chunk's
+// start.  A wrong pick only costs time: a chunk is used only where its
+// predecessor's decode hands over to it.
 constexpr int FIND_STAGE = 4096;  // staged bytes per step
-__global__ __launch_bounds__(64) void k_gz_find(const uint8_t *__restrict__ in, uint64_t ma, uint64_t mz,
-                                               const uint64_t *__restrict__ nominal, uint64_t span,
-                                               uint64_t *__restrict__ found) {
+constexpr int FIND_THREADS = 256;
+constexpr int FIND_CAP = 2048;    // survivors checked per stage (more: the rest are passed over)
+
+// The full check of a dynamic-block header at stage bit `at`, in registers: the
+// code-length code decoded canonically (puff's decode), the HLIT + HDIST lengths
+// with their repeat rules and running Kraft sums (an over-subscribed code fails as
+// soon as it is), an end-of-block code, and zlib's inflate_table rules (no
+// incomplete lit/len or distance code except a single one-bit code).  `lim`: the
+// header must end at or before this stage bit.
+template <class Peek>
+__device__ bool dyn_header_ok(const Peek &peek, uint32_t at, int64_t lim) {
+    uint64_t bb = 0;
+    int bc = 0;
+    uint32_t fill = at;
+    auto need = [&](int k) {
+        if (bc < k) {
+            bb |= (uint64_t)peek(fill) << bc;
+            fill += 32;
+            bc += 32;
+        }
+    };
+    auto drop = [&](int k) {
+        bb >>= k;
+        bc -= k;
+    };
+    need(17);
+    const int hlit = (int)((bb >> 3) & 31u) + 257, hdist = (int)((bb >> 8) & 31u) + 1,
+              hclen = (int)((bb >> 13) & 15u) + 4;
+    drop(17);
+    if (hlit > 286 || hdist > 30) return false;
+    uint64_t cls = 0;  // 3-bit code-length-code length per symbol 0..18
+    for (int i = 0; i < hclen; ++i) {
+        need(3);
+        cls |= (bb & 7u) << (3 * c_cl_order[i]);
+        drop(3);
+    }
+    uint64_t cnt = 0;  // 5-bit count per length 0..7
+    for (int sy = 0; sy < 19; ++sy) cnt += 1ull << (5 * ((cls >> (3 * sy)) & 7u));
+    const int total = hlit + hdist;
+    int i = 0, prev = 0;
+    uint32_t kr = 0, nz = 0, mx = 0;  // Kraft sum, nonzero lengths, longest length of the current code
+    bool eob = false;
+    auto put = [&](int l) -> bool {  // length of symbol i
+        if (i == hlit) {             // the lit/len code is complete (or one 1-bit code)
+            if (kr != 32768u && !(nz == 1 && mx == 1)) return false;
+            kr = nz = mx = 0;
+        }
+        if (i == 256) eob = l != 0;
+        if (l) {
+            kr += 1u << (15 - l);
+            ++nz;
+            mx = (uint32_t)l > mx ? (uint32_t)l : mx;
+            if (kr > 32768u) return false;
+        }
+        ++i;
+        return true;
+    };
+    while (i < total) {
+        need(14);
+        // canonical decode of one code-length symbol (codes are stored bit-reversed)
+        int code = 0, first = 0, index = 0, sy = -1;
+        for (int len = 1; len <= 7; ++len) {
+            code |= (int)(bb & 1u);
+            drop(1);
+            const int count = (int)((cnt >> (5 * len)) & 31u);
+            if (code - count < first) {
+                int k = index + (code - first), s = 0;  // the k-th symbol in (length, symbol) order
+                for (int l2 = 1; l2 < len; ++l2) k -= (int)((cnt >> (5 * l2)) & 31u);
+                for (; s < 19; ++s)
+                    if ((int)((cls >> (3 * s)) & 7u) == len && k-- == 0) break;
+                sy = s;
+                break;
+            }
+            index += count;
+            first = (first + count) << 1;
+            code <<= 1;
+        }
+        if (sy < 0) return false;
+        if (sy < 16) {
+            if (!put(sy)) return false;
+            prev = sy;
+            continue;
+        }
+        int rep, v = 0;
+        need(7);
+        if (sy == 16) {
+            if (i == 0) return false;
+            v = prev;
+            rep = 3 + (int)(bb & 3u);
+            drop(2);
+        } else if (sy == 17) {
+            rep = 3 + (int)(bb & 7u);
+            drop(3);
+        } else {
+            rep = 11 + (int)(bb & 127u);
+            drop(7);
+        }
+        if (i + rep > total) return false;
+        while (rep--)
+            if (!put(v)) return false;
+        prev = v;
+    }
+    if (!eob) return false;
+    if (kr != 32768u && !(nz <= 1 && mx <= 1)) return false;  // distances: complete, one 1-bit code, or none
+    return (int64_t)(fill - (uint32_t)bc) <= lim;
+}
+
+__global__ __launch_bounds__(FIND_THREADS) void k_gz_find(const uint8_t *__restrict__ in, uint64_t ma, uint64_t mz,
+                                                         const uint64_t *__restrict__ nominal, uint64_t span,
+                                                         uint64_t *__restrict__ found, uint32_t *__restrict__ stats) {
     __shared__ __attribute__((aligned(16))) uint32_t s_in32[FIND_STAGE / 4 + 4];
-    __shared__ uint8_t s_len[NSYM];
-    __shared__ uint16_t s_cl[128];
-    const int lane = (int)threadIdx.x;
+    __shared__ uint32_t s_surv[FIND_CAP];
+    __shared__ uint32_t s_n;
+    __shared__ unsigned long long s_best;
+    const int tid = (int)threadIdx.x, lane = tid & 63;
     const uint64_t c = blockIdx.x;
     const uint64_t q0 = nominal[c];
     const uint64_t lim = 8 * (mz - 8);  // the deflate data ends before the trailer
     uint64_t res = GZ_NO_BIT;
     const uint64_t qz = q0 + span < lim ? q0 + span : lim;
+    uint32_t n_stages = 0, n_checks = 0;  // (stats: diagnostic)
+    unsigned long long cyc_scan = 0, cyc_check = 0;
     for (uint64_t base = q0; base < qz && res == GZ_NO_BIT;) {
         const uint64_t sb = (base >> 3) & ~(uint64_t)15;  // staged from this byte
-        for (int k = lane; k < FIND_STAGE / 16; k += 64) {
+        for (int k = tid; k < FIND_STAGE / 16; k += FIND_THREADS) {
             const uint64_t q = sb + 16 * (uint64_t)k;
             uint4 v = make_uint4(0, 0, 0, 0);
             if (q + 16 <= mz) v = *reinterpret_cast<const uint4 *>(in + q);
@@ -936,8 +1061,13 @@ __global__ __launch_bounds__(64) void k_gz_find(const uint8_t *__restrict__ in, 
             }
             reinterpret_cast<uint4 *>(s_in32)[k] = v;
         }
-        if (lane == 0) reinterpret_cast<uint4 *>(s_in32)[FIND_STAGE / 16] = make_uint4(0, 0, 0, 0);
+        if (tid == 0) {
+            reinterpret_cast<uint4 *>(s_in32)[FIND_STAGE / 16] = make_uint4(0, 0, 0, 0);
+            s_best = GZ_NO_BIT;
+            s_n = 0;
+        }
         __syncthreads();
+        const unsigned long long t0 = stats ? __builtin_amdgcn_s_memtime() : 0ull;
         auto peek = [&](uint32_t pos) -> uint32_t {  // 32 stage bits from bit pos
             const uint32_t a = pos >> 5;
             return __builtin_amdgcn_alignbit(s_in32[a + 1], s_in32[a], pos & 31u);
@@ -945,11 +1075,11 @@ __global__ __launch_bounds__(64) void k_gz_find(const uint8_t *__restrict__ in, 
         // offsets tested from this stage: a full header (<= ~600 B) must fit behind them
         const uint32_t p0 = (uint32_t)(base - 8 * sb);
         const uint32_t pz = 8u * (FIND_STAGE - HDR_ROOM);
-        for (uint32_t pb = p0; pb < pz && res == GZ_NO_BIT; pb += 64) {
-            const uint32_t pos = pb + (uint32_t)lane;
-            const uint64_t abs = 8 * sb + pos;
+        for (uint32_t pb = p0; pb < pz; pb += FIND_THREADS) {
+            const uint32_t pos = pb + (uint32_t)tid;
             const uint32_t lo = peek(pos), mid = peek(pos + 32), hi = peek(pos + 64);
-            bool ok = abs < qz && ((lo >> 1) & 3u) == 2u && ((lo >> 3) & 31u) <= 29u && ((lo >> 8) & 31u) <= 29u;
+            bool ok = 8 * sb + pos < qz && ((lo >> 1) & 3u) == 2u && ((lo >> 3) & 31u) <= 29u &&
+                      ((lo >> 8) & 31u) <= 29u;
             if (ok) {
                 const int hclen = (int)((lo >> 13) & 15u) + 4;
                 const uint64_t y = (((uint64_t)mid << 32 | lo) >> 17) | ((uint64_t)hi << 47);
@@ -960,148 +1090,149 @@ __global__ __launch_bounds__(64) void k_gz_find(const uint8_t *__restrict__ in, 
                 }
                 ok = kraft == 128u;
             }
-            for (uint64_t cand = __ballot(ok); cand && res == GZ_NO_BIT; cand &= cand - 1) {
-                const uint32_t at = pb + (uint32_t)__builtin_ctzll(cand);
-                uint32_t good = 0;
-                if (lane == 0) {  // the full check (k_inflate's header parse, no tables kept)
-                    uint64_t bb = 0;
-                    int bc = 0;
-                    uint32_t fill = at;
-                    auto need = [&](int k) {
-                        if (bc < k) {
-                            bb |= (uint64_t)peek(fill) << bc;
-                            fill += 32;
-                            bc += 32;
-                        }
-                    };
-                    auto drop = [&](int k) {
-                        bb >>= k;
-                        bc -= k;
-                    };
-                    need(17);
-                    const int hlit = (int)((bb >> 3) & 31u) + 257, hdist = (int)((bb >> 8) & 31u) + 1,
-                              hclen = (int)((bb >> 13) & 15u) + 4;
-                    drop(17);
-                    uint8_t cl[19];
-                    for (int i = 0; i < 19; ++i) cl[i] = 0;
-                    for (int i = 0; i < hclen; ++i) {
-                        need(3);
-                        cl[c_cl_order[i]] = (uint8_t)(bb & 7u);
-                        drop(3);
-                    }
-                    uint16_t cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0}, next[8];
-                    for (int i = 0; i < 19; ++i) ++cnt[cl[i]];
-                    uint32_t code = 0;
-                    cnt[0] = 0;
-                    for (int l = 1; l < 8; ++l) {
-                        code = (code + cnt[l - 1]) << 1;
-                        next[l] = (uint16_t)code;
-                    }
-                    for (int i = 0; i < 128; ++i) s_cl[i] = 0;
-                    for (int sy = 0; sy < 19; ++sy)
-                        if (cl[sy]) {
-                            const int l = cl[sy];
-                            const uint32_t r = __builtin_bitreverse32((uint32_t)next[l]++) >> (32 - l);
-                            for (uint32_t i = r; i < 128; i += 1u << l) s_cl[i] = (uint16_t)(l | sy << 8);
-                        }
-                    const int total = hlit + hdist;
-                    int i = 0;
-                    bool bad = false;
-                    while (i < total && !bad) {
-                        need(14);
-                        const uint32_t e = s_cl[bb & 127u];
-                        const int sy = (int)(e >> 8);
-                        drop((int)(e & 15u));
-                        if (sy < 16) {
-                            s_len[i++] = (uint8_t)sy;
-                            continue;
-                        }
-                        int rep;
-                        uint8_t v = 0;
-                        if (sy == 16) {
-                            if (i == 0) { bad = true; break; }
-                            v = s_len[i - 1];
-                            rep = 3 + (int)(bb & 3u);
-                            drop(2);
-                        } else if (sy == 17) {
-                            rep = 3 + (int)(bb & 7u);
-                            drop(3);
-                        } else {
-                            rep = 11 + (int)(bb & 127u);
-                            drop(7);
-                        }
-                        if (i + rep > total) { bad = true; break; }
-                        while (rep--) s_len[i++] = v;
-                    }
-                    if (!bad && s_len[256] == 0) bad = true;
-                    for (int t = 0; t < 2 && !bad; ++t) {  // inflate_table: LENS, then DISTS
-                        const int b0 = t ? hlit : 0, nn = t ? hdist : hlit;
-                        uint16_t count[16];
-                        for (int l = 0; l < 16; ++l) count[l] = 0;
-                        for (int k = 0; k < nn; ++k) ++count[s_len[b0 + k]];
-                        int left = 1, mx = 0;
-                        for (int l = 1; l < 16; ++l) {
-                            left = (left << 1) - count[l];
-                            if (left < 0) bad = true;
-                            if (count[l]) mx = l;
-                        }
-                        if (mx > 0 && left > 0 && mx != 1) bad = true;
-                    }
-                    // the header must end inside the data
-                    good = !bad && 8 * sb + (uint64_t)(fill - (uint32_t)bc) <= lim;
-                }
-                if (bfl(good)) res = 8 * sb + at;
+            const uint64_t m = __ballot(ok);
+            if (m) {
+                uint32_t at = 0;
+                if (lane == 0) at = atomicAdd(&s_n, (uint32_t)__popcll(m));
+                at = (uint32_t)__shfl(at, 0, 64) + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+                if (ok && at < (uint32_t)FIND_CAP) s_surv[at] = pos;
             }
         }
+        __syncthreads();
+        const unsigned long long t1 = stats ? __builtin_amdgcn_s_memtime() : 0ull;
+        const uint32_t n = s_n < (uint32_t)FIND_CAP ? s_n : (uint32_t)FIND_CAP;
+        for (uint32_t j = (uint32_t)tid; j < n; j += FIND_THREADS) {  // the survivors, all at once
+            const uint32_t pos = s_surv[j];
+            if (dyn_header_ok(peek, pos, (int64_t)(lim - 8 * sb))) atomicMin(&s_best, (unsigned long long)(8 * sb + pos));
+        }
+        n_checks += n;
+        ++n_stages;
+        __syncthreads();
+        if (stats) {
+            const unsigned long long t2 = __builtin_amdgcn_s_memtime();
+            cyc_scan += t1 - t0;
+            cyc_check += t2 - t1;
+        }
+        res = s_best;
         base = 8 * sb + pz;  // the next stage starts where this one's offsets stopped
         __syncthreads();
     }
-    if (lane == 0) found[c] = res;
+    if (tid == 0) {
+        found[c] = res;
+        if (stats) {
+            stats[3 * c] = n_stages;
+            stats[3 * c + 1] = n_checks;
+            stats[3 * c + 2] = (uint32_t)(cyc_check >> 10);  // (kilo-ticks; the scan's in the high half below)
+            stats[3 * c + 1] = n_checks | (uint32_t)((cyc_scan >> 10) << 12);
+        }
+    }
 }
 
 // ---- chunked members: the window chain, in stream order ---------------------------
-// window[j] = the last 32 KiB of the output through ordered chunk j: its own
-// values, or (a chunk shorter than the window) the tail of window[j - 1]; a
-// marker 256 + w is byte w of window[j - 1].  One block walks the chain; the next
-// chunk's slot values are loaded while the current one resolves.
+// window[j] = the last 32 KiB of the output through ordered chunk j.  As a map over
+// window[j - 1], position i of it is a byte (< 256) or 256 + w (byte w of window
+// [j - 1]): the chunk's own slot values, or -- a chunk shorter than the window --
+// the tail of window[j - 1].  Maps compose (M_b after M_a: M_b's markers look up
+// M_a), so the chain runs in two levels instead of one step per chunk: groups of
+// G chunks compose their maps in parallel (A), one block walks the group maps
+// (B), and every group applies its chunks' maps from its start window (C).
 constexpr int WIN32K = 32768;
 constexpr int GZW_THREADS = 1024;
 constexpr int GZW_PER = WIN32K / GZW_THREADS;
-__global__ __launch_bounds__(GZW_THREADS) void k_gz_windows(const uint16_t *__restrict__ slots, uint32_t cap,
-                                                           const uint32_t *__restrict__ order,
-                                                           const uint32_t *__restrict__ len, uint64_t n_order,
-                                                           uint8_t *__restrict__ windows) {
-    __shared__ uint8_t w[2][WIN32K];
-    const int t = (int)threadIdx.x;
-    for (int i = t; i < WIN32K; i += GZW_THREADS) w[0][i] = 0;
-    uint32_t nv[GZW_PER];
-    auto fetch = [&](uint64_t j) {  // chunk j's last 32 KiB (slot values; below 0: the previous window)
+struct WinMaps {  // ordered chunk j's map, loaded GZW_PER values per thread
+    const uint16_t *slots;
+    uint32_t cap;
+    const uint32_t *order, *len;
+    __device__ void load(uint64_t j, int t, uint32_t (&v)[GZW_PER]) const {
         const uint32_t c = order[j], L = len[c];
         const uint16_t *sl = slots + (uint64_t)c * cap;
 #pragma unroll
         for (int k = 0; k < GZW_PER; ++k) {
             const int i = t + GZW_THREADS * k;
-            const int64_t q = (int64_t)L - WIN32K + i;  // position in the chunk
-            nv[k] = q >= 0 ? (uint32_t)sl[q] : 0x10000u | (uint32_t)(i + (int)L);  // 0x10000: window byte
+            const int64_t q = (int64_t)L - WIN32K + i;  // position in the chunk; below 0: window[j - 1]
+            v[k] = q >= 0 ? (uint32_t)sl[q] : 256u + (uint32_t)(i + (int)L);
         }
-    };
-    if (n_order) fetch(0);
-    __syncthreads();
-    for (uint64_t j = 0; j < n_order; ++j) {
-        uint32_t cv[GZW_PER];
+    }
+};
+
+// (A) group g's composed map: M_{last} after ... after M_{first}
+__global__ __launch_bounds__(GZW_THREADS) void k_gz_wcompose(WinMaps M, uint64_t n, uint64_t G,
+                                                            uint16_t *__restrict__ Q) {
+    __shared__ uint16_t q[WIN32K];
+    const int t = (int)threadIdx.x;
+    const uint64_t j0 = (uint64_t)blockIdx.x * G, j1 = j0 + G < n ? j0 + G : n;
+    uint32_t nv[GZW_PER];
+    M.load(j0, t, nv);
 #pragma unroll
-        for (int k = 0; k < GZW_PER; ++k) cv[k] = nv[k];
-        if (j + 1 < n_order) fetch(j + 1);
-        const uint8_t *cur = w[j & 1];
-        uint8_t *nxt = w[(j + 1) & 1];
-        uint8_t *gw = windows + j * (uint64_t)WIN32K;
+    for (int k = 0; k < GZW_PER; ++k) q[t + GZW_THREADS * k] = (uint16_t)nv[k];
+    if (j0 + 1 < j1) M.load(j0 + 1, t, nv);
+    __syncthreads();
+    for (uint64_t j = j0 + 1; j < j1; ++j) {
+        uint32_t r[GZW_PER];
+#pragma unroll
+        for (int k = 0; k < GZW_PER; ++k) r[k] = nv[k] < 256u ? nv[k] : (uint32_t)q[nv[k] - 256u];
+        if (j + 1 < j1) M.load(j + 1, t, nv);
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < GZW_PER; ++k) q[t + GZW_THREADS * k] = (uint16_t)r[k];
+        __syncthreads();
+    }
+    uint16_t *dst = Q + (uint64_t)blockIdx.x * WIN32K;
+#pragma unroll
+    for (int k = 0; k < GZW_PER; ++k) dst[t + GZW_THREADS * k] = q[t + GZW_THREADS * k];
+}
+
+// (B) the window after every group, in order
+__global__ __launch_bounds__(GZW_THREADS) void k_gz_wchain(const uint16_t *__restrict__ Q, uint64_t ng,
+                                                          uint8_t *__restrict__ wend) {
+    __shared__ uint8_t w[WIN32K];
+    const int t = (int)threadIdx.x;
+    for (int i = t; i < WIN32K; i += GZW_THREADS) w[i] = 0;
+    uint32_t nv[GZW_PER];
+    auto load = [&](uint64_t g) {
+#pragma unroll
+        for (int k = 0; k < GZW_PER; ++k) nv[k] = Q[g * WIN32K + t + GZW_THREADS * k];
+    };
+    load(0);
+    __syncthreads();
+    for (uint64_t g = 0; g < ng; ++g) {
+        uint32_t r[GZW_PER];
+#pragma unroll
+        for (int k = 0; k < GZW_PER; ++k) r[k] = nv[k] < 256u ? nv[k] : (uint32_t)w[nv[k] - 256u];
+        if (g + 1 < ng) load(g + 1);
+        __syncthreads();
+        uint8_t *dst = wend + g * WIN32K;
 #pragma unroll
         for (int k = 0; k < GZW_PER; ++k) {
-            const int i = t + GZW_THREADS * k;
-            const uint32_t v = cv[k];
-            const uint32_t b = v >= 0x10000u ? cur[v & 0xFFFFu] : v >= 256u ? cur[v - 256u] : v;
-            nxt[i] = (uint8_t)b;
-            gw[i] = (uint8_t)b;
+            w[t + GZW_THREADS * k] = (uint8_t)r[k];
+            dst[t + GZW_THREADS * k] = (uint8_t)r[k];
+        }
+        __syncthreads();
+    }
+}
+
+// (C) every chunk's window, groups in parallel from their start windows
+__global__ __launch_bounds__(GZW_THREADS) void k_gz_wapply(WinMaps M, uint64_t n, uint64_t G,
+                                                          const uint8_t *__restrict__ wend,
+                                                          uint8_t *__restrict__ windows) {
+    __shared__ uint8_t w[WIN32K];
+    const int t = (int)threadIdx.x;
+    const uint64_t g = blockIdx.x, j0 = g * G, j1 = j0 + G < n ? j0 + G : n;
+    for (int i = t; i < WIN32K; i += GZW_THREADS) w[i] = g ? wend[(g - 1) * WIN32K + i] : (uint8_t)0;
+    uint32_t nv[GZW_PER];
+    M.load(j0, t, nv);
+    __syncthreads();
+    for (uint64_t j = j0; j < j1; ++j) {
+        uint32_t r[GZW_PER];
+#pragma unroll
+        for (int k = 0; k < GZW_PER; ++k) r[k] = nv[k] < 256u ? nv[k] : (uint32_t)w[nv[k] - 256u];
+        if (j + 1 < j1) M.load(j + 1, t, nv);
+        __syncthreads();
+        uint8_t *dst = windows + j * WIN32K;
+#pragma unroll
+        for (int k = 0; k < GZW_PER; ++k) {
+            w[t + GZW_THREADS * k] = (uint8_t)r[k];
+            dst[t + GZW_THREADS * k] = (uint8_t)r[k];
         }
         __syncthreads();
     }
@@ -1133,13 +1264,24 @@ __global__ __launch_bounds__(GZR_THREADS) void k_gz_resolve(const uint16_t *__re
     const uint32_t wmin = P >= (uint64_t)WIN32K ? 0u : (uint32_t)(WIN32K - P);
     uint8_t *dst = out + P;
     bool far = false;
-    for (uint32_t i = (uint32_t)t; i < L; i += GZR_THREADS) {
-        uint32_t v = sl[i];
-        if (v >= 256u) {
-            far |= v - 256u < wmin || j == 0;
-            v = win[v - 256u];
+    for (uint32_t i0 = 0; i0 < L; i0 += 8 * GZR_THREADS) {  // eight values in flight per thread
+        uint32_t v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const uint32_t i = i0 + (uint32_t)t + GZR_THREADS * k;
+            v[k] = i < L ? (uint32_t)sl[i] : 0u;
         }
-        dst[i] = (uint8_t)v;
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            if (v[k] >= 256u) {
+                far |= v[k] - 256u < wmin || j == 0;
+                v[k] = win[v[k] - 256u];
+            }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const uint32_t i = i0 + (uint32_t)t + GZR_THREADS * k;
+            if (i < L) dst[i] = (uint8_t)v[k];
+        }
     }
     if (__syncthreads_or(far) && t == 0) status[0] = GZ_E_FAR;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -1149,7 +1291,15 @@ __global__ __launch_bounds__(GZR_THREADS) void k_gz_resolve(const uint16_t *__re
     const uint32_t la = (uint32_t)t * seg < L ? (uint32_t)t * seg : L;
     const uint32_t lz = la + seg < L ? la + seg : L;
     uint32_t cc = ~0u;
-    for (uint32_t i = la; i < lz; ++i) cc = T[(cc ^ dst[i]) & 255u] ^ (cc >> 8);
+    uint32_t i = la;
+    for (; i + 16 <= lz; i += 16) {  // sixteen loads in flight, then the table steps
+        uint32_t b[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) b[k] = dst[i + k];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) cc = T[(cc ^ b[k]) & 255u] ^ (cc >> 8);
+    }
+    for (; i < lz; ++i) cc = T[(cc ^ dst[i]) & 255u] ^ (cc >> 8);
     s_p[t] = ~cc;
     __syncthreads();
     if (t == 0) {
@@ -1166,23 +1316,46 @@ __global__ __launch_bounds__(GZR_THREADS) void k_gz_resolve(const uint16_t *__re
     }
 }
 
-// the member's CRC-32: crc(A B) = crc(A) x^(8|B|) mod P ^ crc(B), in stream order
+// the member's CRC-32: crc(A B) = crc(A) x^(8|B|) mod P ^ crc(B).  Pairs (crc,
+// x^(8 len)) combine associatively -- (A then B) = (crc_A x_B ^ crc_B, x_A x_B) --
+// so the chunks fold as a block reduction in stream order.
 // (the member's status gets GZ_VERIFIED: k_inflate skips it, k_gz_crc only counts it)
-__global__ void k_gz_crc_fold(const uint32_t *__restrict__ crc, const uint32_t *__restrict__ shift, uint64_t n,
-                              const uint32_t *__restrict__ tcrc, const int32_t *__restrict__ status,
-                              int32_t *__restrict__ mstatus) {
-    if (threadIdx.x != 0) return;
-    uint32_t tot = 0;
-    for (uint64_t j = 0; j < n; ++j) tot = multmodp(shift[j], tot) ^ crc[j];
-    int32_t st = status[0];
-    if (st == GZ_OK && tot != tcrc[0]) st = GZ_E_CRC;
-    mstatus[0] = st | GZ_VERIFIED;
+constexpr int GZF_THREADS = 256;
+__global__ __launch_bounds__(GZF_THREADS) void k_gz_crc_fold(const uint32_t *__restrict__ crc,
+                                                            const uint32_t *__restrict__ shift, uint64_t n,
+                                                            const uint32_t *__restrict__ tcrc,
+                                                            const int32_t *__restrict__ status,
+                                                            int32_t *__restrict__ mstatus) {
+    __shared__ uint32_t s_c[GZF_THREADS], s_x[GZF_THREADS];
+    const int t = (int)threadIdx.x;
+    const uint64_t per = (n + GZF_THREADS - 1) / GZF_THREADS;
+    uint32_t c = 0, x = 1u << 31;  // the empty string: crc 0, x^0
+    for (uint64_t j = (uint64_t)t * per; j < n && j < (uint64_t)(t + 1) * per; ++j) {
+        c = multmodp(shift[j], c) ^ crc[j];
+        x = multmodp(x, shift[j]);
+    }
+    s_c[t] = c;
+    s_x[t] = x;
+    __syncthreads();
+    for (int d = 1; d < GZF_THREADS; d <<= 1) {  // pairs (t, t + d) with t a multiple of 2d
+        if ((t & (2 * d - 1)) == 0 && t + d < GZF_THREADS) {
+            s_c[t] = multmodp(s_x[t + d], s_c[t]) ^ s_c[t + d];
+            s_x[t] = multmodp(s_x[t], s_x[t + d]);
+        }
+        __syncthreads();
+    }
+    if (t == 0) {
+        int32_t st = status[0];
+        if (st == GZ_OK && s_c[0] != tcrc[0]) st = GZ_E_CRC;
+        mstatus[0] = st | GZ_VERIFIED;
+    }
 }
 
 hipError_t launch_gz_find(const uint8_t *in, uint64_t ma, uint64_t mz, const uint64_t *nominal, uint64_t n_chunks,
-                          uint64_t span, uint64_t *found, hipStream_t st) {
+                          uint64_t span, uint64_t *found, uint32_t *stats, hipStream_t st) {
     if (!n_chunks) return hipSuccess;
-    hipLaunchKernelGGL(k_gz_find, dim3((unsigned)n_chunks), dim3(64), 0, st, in, ma, mz, nominal, span, found);
+    hipLaunchKernelGGL(k_gz_find, dim3((unsigned)n_chunks), dim3(FIND_THREADS), 0, st, in, ma, mz, nominal, span,
+                       found, stats);
     return hipGetLastError();
 }
 
@@ -1195,9 +1368,13 @@ hipError_t launch_inflate_chunks(const uint8_t *in, const GzChunkArgs &a, uint64
 }
 
 hipError_t launch_gz_windows(const uint16_t *slots, uint32_t cap, const uint32_t *order, const uint32_t *len,
-                             uint64_t n_order, uint8_t *windows, hipStream_t st) {
+                             uint64_t n_order, uint8_t *windows, uint16_t *gmaps, uint8_t *gwin, hipStream_t st) {
     if (!n_order) return hipSuccess;
-    hipLaunchKernelGGL(k_gz_windows, dim3(1), dim3(GZW_THREADS), 0, st, slots, cap, order, len, n_order, windows);
+    const uint64_t G = gz_window_group(n_order), ng = (n_order + G - 1) / G;
+    const WinMaps M{slots, cap, order, len};
+    hipLaunchKernelGGL(k_gz_wcompose, dim3((unsigned)ng), dim3(GZW_THREADS), 0, st, M, n_order, G, gmaps);
+    hipLaunchKernelGGL(k_gz_wchain, dim3(1), dim3(GZW_THREADS), 0, st, gmaps, ng, gwin);
+    hipLaunchKernelGGL(k_gz_wapply, dim3((unsigned)ng), dim3(GZW_THREADS), 0, st, M, n_order, G, gwin, windows);
     return hipGetLastError();
 }
 
@@ -1212,7 +1389,7 @@ hipError_t launch_gz_resolve(const uint16_t *slots, uint32_t cap, const uint32_t
 
 hipError_t launch_gz_crc_fold(const uint32_t *crc, const uint32_t *shift, uint64_t n_order, const uint32_t *tcrc,
                               const int32_t *status, int32_t *mstatus, hipStream_t st) {
-    hipLaunchKernelGGL(k_gz_crc_fold, dim3(1), dim3(64), 0, st, crc, shift, n_order, tcrc, status, mstatus);
+    hipLaunchKernelGGL(k_gz_crc_fold, dim3(1), dim3(GZF_THREADS), 0, st, crc, shift, n_order, tcrc, status, mstatus);
     return hipGetLastError();
 }
 

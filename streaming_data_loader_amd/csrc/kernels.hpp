@@ -111,14 +111,16 @@ hipError_t launch_gz_crc(const uint32_t *ooff, const uint8_t *out, uint64_t n, c
                          int32_t *status, uint32_t *bad, hipStream_t st);
 
 // One large gzip member inflated in parallel (inflate.hip, "chunked members"):
-// the deflate stream is cut into chunks of the compressed bytes; each chunk
-// after the first starts at a dynamic-block header found by search, decodes into
-// a 16-bit slot (bytes < 256, 256 + w = byte w of the 32 KiB window before the
-// chunk), and stops at the first block boundary at or past the next chunk's
-// nominal start; the host checks that every chunk starts where its predecessor
-// stopped (and redecodes the ones that do not), the window chain is resolved in
-// stream order, then every chunk's bytes are written and CRC'd in parallel.
-constexpr uint64_t GZ_NO_BIT = ~0ull;          // chunk: no start found / never stop
+// the deflate stream is cut into chunks of the compressed bytes; each chunk after
+// the first starts at the first dynamic-block header a search finds at or past
+// its nominal start, decodes into a 16-bit slot (bytes < 256, 256 + w = byte w
+// of the 32 KiB window before the chunk), and hands over at the first block start
+// that equals a later chunk's searched start (decoding through wrong or missing
+// picks); the host follows the hand-overs in stream order (a chunk whose slot
+// fills stops at its last flush point, inside a block, and a new chunk resumes
+// there), the window chain is resolved, then every chunk's bytes are written and
+// CRC'd in parallel.
+constexpr uint64_t GZ_NO_BIT = ~0ull;            // chunk: no start found
 constexpr uint64_t GZ_START_HEADER = ~0ull - 1;  // chunk: start at the member's gzip header
 enum : uint32_t { GZC_FINAL = 1, GZC_SOFT = 2 };  // chunk flags: final block reached; stopped: slot full
 struct GzChunkArgs {
@@ -126,12 +128,16 @@ struct GzChunkArgs {
     const uint32_t *list;       // blockIdx.x -> chunk index
     const uint64_t *start_bit;  // per chunk: absolute bit in `in`, or GZ_START_HEADER
     const uint64_t *hdr_bit;    // per chunk: the header of the block it starts in (== start_bit at a boundary)
-    const uint64_t *stop_bit;   // per chunk: stop at the first block boundary at or past it
+    const uint64_t *nominal;    // per searched chunk: where its search began (bits)
+    const uint64_t *found;      // per searched chunk: its start (GZ_NO_BIT: none)
+    uint32_t n_chunks;          // searched chunks
+    const uint32_t *tgt0;       // per chunk: the first chunk it may hand over to
     uint16_t *slots;            // per chunk: `cap` values
     uint32_t cap;
     uint64_t *end_bit;          // out: where the chunk stopped: a block boundary, or (GZC_SOFT, slot
                                 //      full) a flush point inside a block ...
     uint64_t *end_hdr;          // out: ... with that block's header bit (else == end_bit)
+    uint32_t *next;             // out: the chunk it handed over to (~0u: none)
     uint32_t *len;              // out: values produced
     uint32_t *flags;            // out: GZC_*
     int32_t *status;            // out: GZ_*
@@ -139,12 +145,19 @@ struct GzChunkArgs {
 };
 // first dynamic-block header at or past nominal[c] (bits), searching `span` bits;
 // found[c] = its bit or GZ_NO_BIT
+// (stats: null, or per chunk {search steps, full checks, code-length symbols decoded}, zeroed; diagnostic)
 hipError_t launch_gz_find(const uint8_t *in, uint64_t ma, uint64_t mz, const uint64_t *nominal, uint64_t n_chunks,
-                          uint64_t span, uint64_t *found, hipStream_t st);
+                          uint64_t span, uint64_t *found, uint32_t *stats, hipStream_t st);
 hipError_t launch_inflate_chunks(const uint8_t *in, const GzChunkArgs &a, uint64_t n_list, hipStream_t st);
-// windows[j] = the 32 KiB before chunk order[j + 1], for the chunks in stream order
+// windows[j] = the 32 KiB before chunk order[j + 1], for the chunks in stream order;
+// gmaps (u16) / gwin (u8) hold 32 KiB per group of gz_window_group(n_order) chunks
+inline uint64_t gz_window_group(uint64_t n) {
+    uint64_t g = 1;
+    while (g * g < n) ++g;
+    return g;
+}
 hipError_t launch_gz_windows(const uint16_t *slots, uint32_t cap, const uint32_t *order, const uint32_t *len,
-                             uint64_t n_order, uint8_t *windows, hipStream_t st);
+                             uint64_t n_order, uint8_t *windows, uint16_t *gmaps, uint8_t *gwin, hipStream_t st);
 // every ordered chunk's bytes to out + pos[j] (markers through windows[j - 1]), its CRC-32
 // and x^(8 len) mod P; status[0] = GZ_E_FAR when a marker reaches before the stream
 hipError_t launch_gz_resolve(const uint16_t *slots, uint32_t cap, const uint32_t *order, const uint32_t *len,

@@ -290,11 +290,12 @@ struct sdl_batcher {
     DevBuf<unsigned long long> z_total;
     DevBuf<uint8_t> z_out;
     // ... large members in chunks (inflate_chunked)
-    DevBuf<uint64_t> zc_nominal, zc_start, zc_hdr, zc_stop, zc_end, zc_endhdr, zc_pos;
-    DevBuf<uint32_t> zc_list, zc_len, zc_flags, zc_order, zc_crc, zc_shift, zc_tcrc;
+    DevBuf<uint64_t> zc_nominal, zc_found, zc_start, zc_hdr, zc_end, zc_endhdr, zc_pos;
+    DevBuf<uint32_t> zc_list, zc_tgt, zc_next, zc_len, zc_flags, zc_order, zc_crc, zc_shift, zc_tcrc, zc_stats;
     DevBuf<int32_t> zc_status, zc_rstatus;
     DevBuf<uint16_t> zc_slots;
-    DevBuf<uint8_t> zc_windows;
+    DevBuf<uint8_t> zc_windows, zc_gwin;
+    DevBuf<uint16_t> zc_gmaps;
     // Transport frames (sdl_pickle_frames_device)
     DevBuf<uint8_t> f_out, f_out2;
     DevBuf<uint8_t> *f_target = &f_out;  // where the next frames go
@@ -1257,14 +1258,13 @@ X2N make_x2n() {  // zlib's x2n_table: x^(2^k) mod P(x), reflected
 
 // A gzip member of >= GZ_SPLIT_MIN compressed bytes -- a single-member .json.gz,
 // the reference's own input -- is inflated in chunks (kernels.hpp, "chunked
-// members"): header search per chunk, all chunks decoded at once into 16-bit
-// slots, then the host walks them in stream order and accepts a chunk only where
-// it starts exactly at its predecessor's stop (any other is decoded again from
-// there: a wrong header pick, a boundary the search skips -- stored or fixed
-// blocks --, or one behind a chunk whose slot filled up: that chunk stopped at its
-// last flush point, inside a block, and the next resumes there after parsing the
-// block's header again), and the window
-// chain, bytes, CRC-32 and ISIZE follow on the device.  The member's status gets
+// members"): a header search per chunk, every chunk decoded at once into 16-bit
+// slots, each handing over where a later chunk's searched start is a real block
+// start (so wrong picks and block starts the search skips -- stored or fixed
+// blocks -- are decoded through in the same launch); the host follows the
+// hand-overs in stream order and continues a chunk whose slot filled up with a
+// new one resuming inside the block (its header parsed again); the window chain,
+// bytes, CRC-32 and ISIZE follow on the device.  The member's status gets
 // GZ_VERIFIED so the one-wave path skips it.
 constexpr uint64_t GZ_SPLIT_MIN = 1u << 20;  // smaller members: one wave each
 constexpr uint64_t GZ_CHUNK = 64u << 10;     // compressed bytes per chunk (at least)
@@ -1276,19 +1276,33 @@ constexpr uint64_t GZ_EXTRA_CHUNKS = 256;    // chunks appended behind one that 
 void inflate_chunked(sdl_batcher *h, const uint8_t *d_gz, uint64_t m, uint64_t ma, uint64_t mz, uint32_t isize,
                      uint32_t ooff_m, hipStream_t st) {
     const uint64_t len = mz - ma;
-    uint64_t ch = GZ_CHUNK;
+    static const uint64_t chunk0 = [] {  // (SDL_GZ_CHUNK: diagnostic override of the chunk size)
+        const char *e = std::getenv("SDL_GZ_CHUNK");
+        const uint64_t v = e ? std::strtoull(e, nullptr, 10) : 0;
+        return v >= 4096 ? v : GZ_CHUNK;
+    }();
+    uint64_t ch = chunk0;
     while ((len + ch - 1) / ch > GZ_MAX_CHUNKS) ch *= 2;
     const uint64_t C0 = (len - 8 + ch - 1) / ch;  // nominal starts ma + c ch < mz - 8
     const uint64_t CT = C0 + GZ_EXTRA_CHUNKS;
     const uint32_t cap = (uint32_t)(ch * GZ_SLOT_RATIO);
+    static const bool dbg = std::getenv("SDL_GZ_DEBUG") != nullptr;  // diagnostic: phase times to stderr
+    auto now = [] { return std::chrono::steady_clock::now(); };
+    auto ms_since = [&](std::chrono::steady_clock::time_point t) {
+        return std::chrono::duration<double, std::milli>(now() - t).count();
+    };
+    const auto t_begin = now();
+    int redos = 0;
     h->zc_nominal.ensure(CT);
+    h->zc_found.ensure(CT);
     h->zc_start.ensure(CT);
     h->zc_hdr.ensure(CT);
-    h->zc_stop.ensure(CT);
     h->zc_end.ensure(CT);
     h->zc_endhdr.ensure(CT);
     h->zc_pos.ensure(CT);
     h->zc_list.ensure(CT);
+    h->zc_tgt.ensure(CT);
+    h->zc_next.ensure(CT);
     h->zc_len.ensure(CT);
     h->zc_flags.ensure(CT);
     h->zc_order.ensure(CT);
@@ -1298,21 +1312,48 @@ void inflate_chunked(sdl_batcher *h, const uint8_t *d_gz, uint64_t m, uint64_t m
     h->zc_status.ensure(CT);
     h->zc_rstatus.ensure(1);
     h->zc_slots.ensure((size_t)CT * cap);
-    std::vector<uint64_t> nominal(CT, GZ_NO_BIT), start(CT, GZ_NO_BIT), hdr(CT, GZ_NO_BIT), stop(CT, GZ_NO_BIT),
-        end(CT, 0), endhdr(CT, 0);
-    std::vector<uint32_t> clen(CT, 0), flags(CT, 0);
+    std::vector<uint64_t> nominal(CT, GZ_NO_BIT), start(CT, GZ_NO_BIT), hdr(CT, GZ_NO_BIT), end(CT, 0),
+        endhdr(CT, 0);
+    std::vector<uint32_t> clen(CT, 0), flags(CT, 0), tgt(CT, 0), next(CT, ~0u);
     std::vector<int32_t> status(CT, GZ_OK);
+    nominal[0] = 0;
     for (uint64_t c = 1; c < C0; ++c) nominal[c] = 8 * (ma + c * ch);
-    for (uint64_t c = 0; c + 1 < C0; ++c) stop[c] = nominal[c + 1];
+    for (uint64_t c = 0; c < C0; ++c) tgt[c] = (uint32_t)(c + 1);
     HIP_TRY(hipMemcpyAsync(h->zc_nominal.p, nominal.data(), C0 * 8, hipMemcpyHostToDevice, st));
-    HIP_TRY(hipMemcpyAsync(h->zc_stop.p, stop.data(), C0 * 8, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(h->zc_tgt.p, tgt.data(), C0 * 4, hipMemcpyHostToDevice, st));
+    if (dbg) {
+        h->zc_stats.ensure(3 * C0);
+        HIP_TRY(hipMemsetAsync(h->zc_stats.p, 0, 3 * C0 * 4, st));
+    }
     if (C0 > 1)
-        HIP_TRY(launch_gz_find(d_gz, ma, mz, h->zc_nominal.p + 1, C0 - 1, 8 * GZ_FIND_SPAN * ch, h->zc_start.p + 1, st));
-    HIP_TRY(hipMemcpyAsync(start.data() + 1, h->zc_start.p + 1, (C0 - 1) * 8, hipMemcpyDeviceToHost, st));
+        HIP_TRY(launch_gz_find(d_gz, ma, mz, h->zc_nominal.p + 1, C0 - 1, 8 * GZ_FIND_SPAN * ch, h->zc_found.p + 1,
+                               dbg ? h->zc_stats.p : nullptr, st));
+    HIP_TRY(hipMemcpyAsync(start.data() + 1, h->zc_found.p + 1, (C0 - 1) * 8, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
+    const double t_find = ms_since(t_begin);
+    if (dbg && C0 > 1) {
+        std::vector<uint32_t> sv(3 * (C0 - 1));
+        HIP_TRY(hipMemcpy(sv.data(), h->zc_stats.p, sv.size() * 4, hipMemcpyDeviceToHost));
+        double m[4] = {0, 0, 0, 0};
+        uint32_t mx[4] = {0, 0, 0, 0};
+        uint64_t nf = 0;
+        for (uint64_t c = 0; c + 1 < C0; ++c) {
+            nf += start[c + 1] == GZ_NO_BIT;
+            const uint32_t v[4] = {sv[3 * c], sv[3 * c + 1] & 4095u, sv[3 * c + 1] >> 12, sv[3 * c + 2]};
+            for (int k = 0; k < 4; ++k) {
+                m[k] += v[k];
+                mx[k] = std::max(mx[k], v[k]);
+            }
+        }
+        fprintf(stderr, "[gz find] per chunk: stages mean %.1f max %u, full checks mean %.1f max %u, "
+                "scan kticks mean %.0f max %u, check kticks mean %.0f max %u; %llu without a start\n",
+                m[0] / (C0 - 1), mx[0], m[1] / (C0 - 1), mx[1], m[2] / (C0 - 1), mx[2], m[3] / (C0 - 1), mx[3],
+                (unsigned long long)nf);
+    }
     start[0] = GZ_START_HEADER;
-    for (uint64_t c = 0; c < C0; ++c) hdr[c] = start[c];  // found starts are block boundaries
-    HIP_TRY(hipMemcpyAsync(h->zc_start.p, start.data(), 8, hipMemcpyHostToDevice, st));
+    for (uint64_t c = 0; c < C0; ++c) hdr[c] = start[c];  // searched starts are block boundaries
+    HIP_TRY(hipMemcpyAsync(h->zc_found.p, start.data(), 8, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(h->zc_start.p, start.data(), C0 * 8, hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemcpyAsync(h->zc_hdr.p, hdr.data(), C0 * 8, hipMemcpyHostToDevice, st));
     GzChunkArgs a{};
     a.ma = ma;
@@ -1320,11 +1361,15 @@ void inflate_chunked(sdl_batcher *h, const uint8_t *d_gz, uint64_t m, uint64_t m
     a.list = h->zc_list.p;
     a.start_bit = h->zc_start.p;
     a.hdr_bit = h->zc_hdr.p;
-    a.stop_bit = h->zc_stop.p;
+    a.nominal = h->zc_nominal.p;
+    a.found = h->zc_found.p;
+    a.n_chunks = (uint32_t)C0;
+    a.tgt0 = h->zc_tgt.p;
     a.slots = h->zc_slots.p;
     a.cap = cap;
     a.end_bit = h->zc_end.p;
     a.end_hdr = h->zc_endhdr.p;
+    a.next = h->zc_next.p;
     a.len = h->zc_len.p;
     a.flags = h->zc_flags.p;
     a.status = h->zc_status.p;
@@ -1337,26 +1382,33 @@ void inflate_chunked(sdl_batcher *h, const uint8_t *d_gz, uint64_t m, uint64_t m
     HIP_TRY(launch_inflate_chunks(d_gz, a, list.size(), st));
     HIP_TRY(hipMemcpyAsync(end.data(), h->zc_end.p, C0 * 8, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipMemcpyAsync(endhdr.data(), h->zc_endhdr.p, C0 * 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(next.data(), h->zc_next.p, C0 * 4, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipMemcpyAsync(clen.data(), h->zc_len.p, C0 * 4, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipMemcpyAsync(flags.data(), h->zc_flags.p, C0 * 4, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipMemcpyAsync(status.data(), h->zc_status.p, C0 * 4, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
-    // (ii) the chain in stream order; a chunk that does not start where its
-    // predecessor stopped is decoded again from there
-    auto redo = [&](uint64_t d, uint64_t from, uint64_t from_hdr) {
-        start[d] = from;
-        hdr[d] = from_hdr;
-        const uint32_t one = (uint32_t)d;
-        HIP_TRY(hipMemcpyAsync(h->zc_start.p + d, &start[d], 8, hipMemcpyHostToDevice, st));
-        HIP_TRY(hipMemcpyAsync(h->zc_hdr.p + d, &hdr[d], 8, hipMemcpyHostToDevice, st));
-        HIP_TRY(hipMemcpyAsync(h->zc_stop.p + d, &stop[d], 8, hipMemcpyHostToDevice, st));
+    const double t_decode = ms_since(t_begin);
+    // (ii) the hand-overs in stream order; a chunk whose slot filled up is continued
+    // by a new chunk from its last flush point
+    auto resume_from = [&](uint64_t r, uint64_t from, uint64_t from_hdr) {
+        start[r] = from;
+        hdr[r] = from_hdr;
+        uint32_t d = 1;  // the first searched chunk whose search began past `from`
+        while (d < C0 && nominal[d] <= from) ++d;
+        tgt[r] = d;
+        const uint32_t one = (uint32_t)r;
+        HIP_TRY(hipMemcpyAsync(h->zc_start.p + r, &start[r], 8, hipMemcpyHostToDevice, st));
+        HIP_TRY(hipMemcpyAsync(h->zc_hdr.p + r, &hdr[r], 8, hipMemcpyHostToDevice, st));
+        HIP_TRY(hipMemcpyAsync(h->zc_tgt.p + r, &tgt[r], 4, hipMemcpyHostToDevice, st));
         HIP_TRY(hipMemcpyAsync(h->zc_list.p, &one, 4, hipMemcpyHostToDevice, st));
         HIP_TRY(launch_inflate_chunks(d_gz, a, 1, st));
-        HIP_TRY(hipMemcpyAsync(&end[d], h->zc_end.p + d, 8, hipMemcpyDeviceToHost, st));
-        HIP_TRY(hipMemcpyAsync(&endhdr[d], h->zc_endhdr.p + d, 8, hipMemcpyDeviceToHost, st));
-        HIP_TRY(hipMemcpyAsync(&clen[d], h->zc_len.p + d, 4, hipMemcpyDeviceToHost, st));
-        HIP_TRY(hipMemcpyAsync(&flags[d], h->zc_flags.p + d, 4, hipMemcpyDeviceToHost, st));
-        HIP_TRY(hipMemcpyAsync(&status[d], h->zc_status.p + d, 4, hipMemcpyDeviceToHost, st));
+        ++redos;
+        HIP_TRY(hipMemcpyAsync(&end[r], h->zc_end.p + r, 8, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(&endhdr[r], h->zc_endhdr.p + r, 8, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(&next[r], h->zc_next.p + r, 4, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(&clen[r], h->zc_len.p + r, 4, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(&flags[r], h->zc_flags.p + r, 4, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(&status[r], h->zc_status.p + r, 4, hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
     };
     std::vector<uint32_t> order;
@@ -1376,18 +1428,21 @@ void inflate_chunked(sdl_batcher *h, const uint8_t *d_gz, uint64_t m, uint64_t m
             done = true;
             break;
         }
-        uint64_t d = c + 1;
-        if (d >= C) {  // the last chunk stopped for capacity: one more behind it
+        if (flags[c] & GZC_SOFT) {
             if (C >= CT) {
                 err = GZ_E_OVER;
                 break;
             }
-            d = C++;
-            stop[d] = GZ_NO_BIT;
-            start[d] = GZ_NO_BIT;
+            const uint64_t r = C++;
+            resume_from(r, end[c], endhdr[c]);
+            c = r;
+            continue;
         }
-        if (start[d] != end[c] || hdr[d] != endhdr[c]) redo(d, end[c], endhdr[c]);
-        c = d;
+        if (next[c] >= C0) {  // (a chunk stops only at a hand-over, the final block or a full slot)
+            err = GZ_E_STALL;
+            break;
+        }
+        c = next[c];
     }
     if (err == GZ_OK && !done) err = GZ_E_TRUNC;
     if (err == GZ_OK) {  // the trailer right behind the final block, and ISIZE
@@ -1406,15 +1461,33 @@ void inflate_chunked(sdl_batcher *h, const uint8_t *d_gz, uint64_t m, uint64_t m
     // (iii) window chain, bytes + CRC per chunk, the member's CRC
     const uint64_t no = order.size();
     h->zc_windows.ensure((size_t)no * 32768);
+    const uint64_t ngroups = (no + gz_window_group(no) - 1) / gz_window_group(no);
+    h->zc_gmaps.ensure((size_t)ngroups * 32768);
+    h->zc_gwin.ensure((size_t)ngroups * 32768);
     HIP_TRY(hipMemcpyAsync(h->zc_order.p, order.data(), no * 4, hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemcpyAsync(h->zc_pos.p, pos.data(), no * 8, hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemsetAsync(h->zc_rstatus.p, 0, 4, st));
     static const X2N x2n = make_x2n();
-    HIP_TRY(launch_gz_windows(h->zc_slots.p, cap, h->zc_order.p, h->zc_len.p, no, h->zc_windows.p, st));
+    const double t_walk = ms_since(t_begin);
+    HIP_TRY(launch_gz_windows(h->zc_slots.p, cap, h->zc_order.p, h->zc_len.p, no, h->zc_windows.p, h->zc_gmaps.p,
+                              h->zc_gwin.p, st));
+    if (dbg) HIP_TRY(hipStreamSynchronize(st));
+    const double t_win = ms_since(t_begin);
     HIP_TRY(launch_gz_resolve(h->zc_slots.p, cap, h->zc_order.p, h->zc_len.p, h->zc_pos.p, no, h->zc_windows.p,
                               h->z_out.p + ooff_m, h->zc_crc.p, h->zc_shift.p, x2n, h->zc_rstatus.p, st));
+    if (dbg) HIP_TRY(hipStreamSynchronize(st));
+    const double t_res = ms_since(t_begin);
     HIP_TRY(launch_gz_crc_fold(h->zc_crc.p, h->zc_shift.p, no, h->zc_tcrc.p, h->zc_rstatus.p, h->z_status.p + m, st));
     HIP_TRY(hipStreamSynchronize(st));  // (order / pos are host vectors)
+    if (dbg) {
+        int soft = 0;
+        for (uint32_t c : order) soft += (flags[c] & GZC_SOFT) != 0;
+        fprintf(stderr, "[gz chunked] %llu B member: %llu chunks of %llu B, %zu decoded at once, %d resumed, %llu in "
+                "order (%d stopped full); ms: find %.2f decode %.2f walk %.2f windows %.2f resolve %.2f fold %.2f\n",
+                (unsigned long long)len, (unsigned long long)C0, (unsigned long long)ch, list.size(), redos,
+                (unsigned long long)no, soft, t_find, t_decode - t_find, t_walk - t_decode, t_win - t_walk,
+                t_res - t_win, ms_since(t_begin) - t_res);
+    }
 }
 
 int sdl_gzip_inflate_device(sdl_batcher *h, const uint8_t *d_gz, uint64_t gz_len, const uint64_t *d_member_offsets,
