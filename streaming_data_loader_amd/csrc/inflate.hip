@@ -921,116 +921,117 @@ __global__ __launch_bounds__(64) void k_gz_crc(const uint32_t *__restrict__ ooff
 // staged 4 KiB of input at a time.  Every offset of the stage is tested first for
 // a dynamic-block header whose fixed fields are legal and whose code-length code is
 // complete (Kraft sum exactly 1, as zlib requires) -- about 0.09 % of offsets in
-// real DEFLATE data survive -- and the survivors are then checked in full, one per
-// thread, all at once (dyn_header_ok); the lowest passing offset is the chunk's
-// start.  A wrong pick only costs time: a chunk is used only where its
+// real DEFLATE data survive -- and the survivors are then checked in full, a wave
+// per survivor (wave_header_ok); the lowest passing offset is the chunk's start.  A wrong pick only costs time: a chunk is used only where its
 // predecessor's decode hands over to it.
 constexpr int FIND_STAGE = 4096;  // staged bytes per step
 constexpr int FIND_THREADS = 256;
 constexpr int FIND_CAP = 2048;    // survivors checked per stage (more: the rest are passed over)
 
-// The full check of a dynamic-block header at stage bit `at`, in registers: the
-// code-length code decoded canonically (puff's decode), the HLIT + HDIST lengths
-// with their repeat rules and running Kraft sums (an over-subscribed code fails as
-// soon as it is), an end-of-block code, and zlib's inflate_table rules (no
-// incomplete lit/len or distance code except a single one-bit code).  `lim`: the
-// header must end at or before this stage bit.
+// The full check of a dynamic-block header at stage bit `at`, by a whole wave
+// (at: wave-uniform) -- the code lengths with their repeat rules, an
+// end-of-block code, and zlib's inflate_table rules (no over-subscribed code; no
+// incomplete lit/len or distance code except a single one-bit code; no distance
+// code at all is allowed).  The code-length code's
+// canonical table is built by the lanes holding its 19 lengths (ballot counts,
+// rank in symbol order) into `tab` (128 entries); then the code-length symbols
+// are decoded speculatively -- lane i decodes the symbol that would start at bit
+// bp + i, the scalar unit follows the chain from bp -- and each pass takes the
+// chain's lengths at once: positions by a prefix sum of the symbols' counts, a
+// '16' repeating the last length before it by a last-set scan, Kraft sums and
+// nonzero / one-bit counts per code by wave sums, the end-of-block length where
+// position 256 falls.  An over-subscribed code fails at the end of its pass.
 template <class Peek>
-__device__ bool dyn_header_ok(const Peek &peek, uint32_t at, int64_t lim) {
-    uint64_t bb = 0;
-    int bc = 0;
-    uint32_t fill = at;
-    auto need = [&](int k) {
-        if (bc < k) {
-            bb |= (uint64_t)peek(fill) << bc;
-            fill += 32;
-            bc += 32;
-        }
-    };
-    auto drop = [&](int k) {
-        bb >>= k;
-        bc -= k;
-    };
-    need(17);
-    const int hlit = (int)((bb >> 3) & 31u) + 257, hdist = (int)((bb >> 8) & 31u) + 1,
-              hclen = (int)((bb >> 13) & 15u) + 4;
-    drop(17);
+__device__ bool wave_header_ok(const Peek &peek, uint32_t at, int64_t lim, uint16_t *tab) {
+    const int lane = lane_id();
+    const uint32_t x = peek(at);
+    const int hlit = (int)((x >> 3) & 31u) + 257, hdist = (int)((x >> 8) & 31u) + 1,
+              hclen = (int)((x >> 13) & 15u) + 4;
     if (hlit > 286 || hdist > 30) return false;
-    uint64_t cls = 0;  // 3-bit code-length-code length per symbol 0..18
-    for (int i = 0; i < hclen; ++i) {
-        need(3);
-        cls |= (bb & 7u) << (3 * c_cl_order[i]);
-        drop(3);
+    uint32_t sym = 31, len = 0;
+    if (lane < 19) {
+        sym = c_cl_order[lane];
+        if (lane < hclen) len = peek(at + 17 + 3 * (uint32_t)lane) & 7u;
     }
-    uint64_t cnt = 0;  // 5-bit count per length 0..7
-    for (int sy = 0; sy < 19; ++sy) cnt += 1ull << (5 * ((cls >> (3 * sy)) & 7u));
-    const int total = hlit + hdist;
-    int i = 0, prev = 0;
-    uint32_t kr = 0, nz = 0, mx = 0;  // Kraft sum, nonzero lengths, longest length of the current code
+    uint32_t first = 0, cnt_prev = 0, my_first = 0;
+    for (int l = 1; l <= 7; ++l) {
+        first = (first + cnt_prev) << 1;  // the first code of length l
+        if (len == (uint32_t)l) my_first = first;
+        cnt_prev = (uint32_t)__popcll(__ballot(len == (uint32_t)l));
+    }
+    uint32_t rank = 0;  // among the codes of the same length, in symbol order
+    for (int j = 0; j < 19; ++j) {
+        const uint32_t lj = (uint32_t)__builtin_amdgcn_readlane((int)len, j);
+        const uint32_t sj = (uint32_t)__builtin_amdgcn_readlane((int)sym, j);
+        rank += lj == len && sj < sym ? 1u : 0u;
+    }
+    for (int i = lane; i < 128; i += 64) tab[i] = 0;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    if (len) {
+        const uint32_t r = __builtin_bitreverse32(my_first + rank) >> (32 - len);
+        for (uint32_t i = r; i < 128; i += 1u << len) tab[i] = (uint16_t)(len | sym << 4);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    const uint32_t total = (uint32_t)(hlit + hdist);
+    uint32_t bp = at + 17 + 3 * (uint32_t)hclen;  // wave-uniform from here on
+    uint32_t got = 0, prev = 0;                   // lengths so far; the last one (bit 8: there is one)
+    uint32_t krl = 0, krd = 0, nzl = 0, nzd = 0, n1l = 0, n1d = 0;
     bool eob = false;
-    auto put = [&](int l) -> bool {  // length of symbol i
-        if (i == hlit) {             // the lit/len code is complete (or one 1-bit code)
-            if (kr != 32768u && !(nz == 1 && mx == 1)) return false;
-            kr = nz = mx = 0;
+    auto wsum = [](uint32_t v) { return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_sum(v), 63); };
+    while (got < total) {
+        const uint32_t w = peek(bp + (uint32_t)lane);
+        const uint32_t e = tab[w & 127u];
+        const uint32_t l = e & 15u, s = e >> 4;
+        const uint32_t xb = s == 16 ? 2u : s == 17 ? 3u : s == 18 ? 7u : 0u;
+        const uint32_t tl = l ? l + xb : 0u;
+        const uint32_t xv = (w >> l) & ((1u << xb) - 1u);
+        const uint32_t n = s < 16 ? 1u : s == 18 ? 11u + xv : 3u + xv;
+        uint64_t M = 0;  // the real chain from bp
+        bool broken = false;
+        for (uint32_t q = 0; q < 64;) {
+            M |= 1ull << q;
+            const uint32_t t = (uint32_t)__builtin_amdgcn_readlane((int)tl, (int)q);
+            if (t == 0) { broken = true; break; }  // (no code: impossible for a complete code)
+            q += t;
         }
-        if (i == 256) eob = l != 0;
-        if (l) {
-            kr += 1u << (15 - l);
-            ++nz;
-            mx = (uint32_t)l > mx ? (uint32_t)l : mx;
-            if (kr > 32768u) return false;
-        }
-        ++i;
-        return true;
-    };
-    while (i < total) {
-        need(14);
-        // canonical decode of one code-length symbol (codes are stored bit-reversed)
-        int code = 0, first = 0, index = 0, sy = -1;
-        for (int len = 1; len <= 7; ++len) {
-            code |= (int)(bb & 1u);
-            drop(1);
-            const int count = (int)((cnt >> (5 * len)) & 31u);
-            if (code - count < first) {
-                int k = index + (code - first), s = 0;  // the k-th symbol in (length, symbol) order
-                for (int l2 = 1; l2 < len; ++l2) k -= (int)((cnt >> (5 * l2)) & 31u);
-                for (; s < 19; ++s)
-                    if ((int)((cls >> (3 * s)) & 7u) == len && k-- == 0) break;
-                sy = s;
-                break;
-            }
-            index += count;
-            first = (first + count) << 1;
-            code <<= 1;
-        }
-        if (sy < 0) return false;
-        if (sy < 16) {
-            if (!put(sy)) return false;
-            prev = sy;
-            continue;
-        }
-        int rep, v = 0;
-        need(7);
-        if (sy == 16) {
-            if (i == 0) return false;
-            v = prev;
-            rep = 3 + (int)(bb & 3u);
-            drop(2);
-        } else if (sy == 17) {
-            rep = 3 + (int)(bb & 7u);
-            drop(3);
-        } else {
-            rep = 11 + (int)(bb & 127u);
-            drop(7);
-        }
-        if (i + rep > total) return false;
-        while (rep--)
-            if (!put(v)) return false;
-        prev = v;
+        if (broken) return false;
+        const bool real = (M >> lane) & 1ull;
+        const uint32_t nn = real ? n : 0u;
+        const uint32_t P = got + wave_incl_sum(nn) - nn;  // this symbol's first length position
+        const bool valid = real && P < total;
+        const uint64_t V = __ballot(valid);
+        const int lv = 63 - __builtin_clzll(V);           // the pass ends with this symbol
+        const uint32_t endP = (uint32_t)__builtin_amdgcn_readlane((int)(P + nn), lv);
+        if (endP > total) return false;                   // a repeat past the last length
+        uint32_t sc = valid && s != 16 ? 0x100u | (s < 16 ? s : 0u) : 0u;
+        SDL_DPP_SCAN(sc, last_set);
+        const uint32_t ex = wave_prev(sc);
+        const uint32_t before = (ex & 0x100u) ? ex : prev;
+        if (__ballot(valid && s == 16 && !(before & 0x100u))) return false;  // '16' with no length before it
+        const uint32_t v = s < 16 ? s : s == 16 ? (before & 0xFFu) : 0u;
+        const uint32_t nl = !valid ? 0u : P >= (uint32_t)hlit ? 0u : ((uint32_t)hlit - P < nn ? (uint32_t)hlit - P : nn);
+        const uint32_t nd = valid ? nn - nl : 0u;
+        const uint32_t wg = v ? 1u << (15 - v) : 0u;
+        krl += wsum(nl * wg);
+        krd += wsum(nd * wg);
+        nzl += wsum(v ? nl : 0u);
+        nzd += wsum(v ? nd : 0u);
+        n1l += wsum(v == 1 ? nl : 0u);
+        n1d += wsum(v == 1 ? nd : 0u);
+        eob = eob || __ballot(valid && P <= 256u && 256u < P + nn && v != 0) != 0;
+        if (krl > 32768u || krd > 32768u) return false;
+        got = endP;
+        prev = 0x100u | (uint32_t)__builtin_amdgcn_readlane((int)v, lv);
+        bp += (uint32_t)lv + (uint32_t)__builtin_amdgcn_readlane((int)tl, lv);
     }
     if (!eob) return false;
-    if (kr != 32768u && !(nz <= 1 && mx <= 1)) return false;  // distances: complete, one 1-bit code, or none
-    return (int64_t)(fill - (uint32_t)bc) <= lim;
+    if (krl != 32768u && !(nzl == 1 && n1l == 1)) return false;
+    if (krd != 32768u && !(nzd == 0 || (nzd == 1 && n1d == 1))) return false;
+    return (int64_t)bp <= lim;
 }
 
 __global__ __launch_bounds__(FIND_THREADS) void k_gz_find(const uint8_t *__restrict__ in, uint64_t ma, uint64_t mz,
@@ -1038,6 +1039,7 @@ __global__ __launch_bounds__(FIND_THREADS) void k_gz_find(const uint8_t *__restr
                                                          uint64_t *__restrict__ found, uint32_t *__restrict__ stats) {
     __shared__ __attribute__((aligned(16))) uint32_t s_in32[FIND_STAGE / 4 + 4];
     __shared__ uint32_t s_surv[FIND_CAP];
+    __shared__ uint16_t s_tab[FIND_THREADS / 64][128];
     __shared__ uint32_t s_n;
     __shared__ unsigned long long s_best;
     const int tid = (int)threadIdx.x, lane = tid & 63;
@@ -1101,9 +1103,12 @@ __global__ __launch_bounds__(FIND_THREADS) void k_gz_find(const uint8_t *__restr
         __syncthreads();
         const unsigned long long t1 = stats ? __builtin_amdgcn_s_memtime() : 0ull;
         const uint32_t n = s_n < (uint32_t)FIND_CAP ? s_n : (uint32_t)FIND_CAP;
-        for (uint32_t j = (uint32_t)tid; j < n; j += FIND_THREADS) {  // the survivors, all at once
+        const int wv = tid >> 6;
+        for (uint32_t j = (uint32_t)wv; j < n; j += FIND_THREADS / 64) {  // a wave per survivor
             const uint32_t pos = s_surv[j];
-            if (dyn_header_ok(peek, pos, (int64_t)(lim - 8 * sb))) atomicMin(&s_best, (unsigned long long)(8 * sb + pos));
+            if ((unsigned long long)(8 * sb + pos) >= *(volatile unsigned long long *)&s_best) continue;
+            if (wave_header_ok(peek, pos, (int64_t)(lim - 8 * sb), s_tab[wv]) && lane == 0)
+                atomicMin(&s_best, (unsigned long long)(8 * sb + pos));
         }
         n_checks += n;
         ++n_stages;
