@@ -168,3 +168,46 @@ def test_device_no_progress_exit(records):
     assert p.returncode == 0, p.stderr[-2000:]
     rc, rest = p.stdout.split(None, 1)
     assert int(rc) == -8 and rest.strip() == f"[{GZ_E_STALL}, 0]", p.stdout
+
+
+def chunked_fuzz_cases(records, n=24, seed=0x7C3D):
+    """Mutations of large members (>= 1 MiB compressed: the chunked path, whose
+    header search and hand-overs read untrusted bits everywhere in the member)."""
+    from test_inflate import big_lines
+    rng = random.Random(seed)
+    lines = big_lines(records, 6, seed=9)
+    bases = [gz_member(lines, 6), gz_member(lines, 1), gz_member(lines[:4_500_000], 6, zlib.Z_FIXED)]
+    out = []
+    for k in range(n):
+        m = bytearray(bases[k % len(bases)])
+        kind = k % 4
+        if kind == 0:  # bit flips deep inside
+            for _ in range(rng.randrange(1, 4)):
+                q = rng.randrange(12, len(m) - 8)
+                m[q] ^= 1 << rng.randrange(8)
+        elif kind == 1:  # a spliced-in random run
+            q = rng.randrange(12, len(m) - 8)
+            m[q:q + 64] = bytes(rng.randrange(256) for _ in range(64))
+        elif kind == 2:  # truncated, trailer re-attached (sizes stay plausible)
+            q = rng.randrange(max(len(m) // 2, 1_100_000), len(m) - 16)
+            m = m[:q] + m[-8:]
+        else:  # a duplicated range
+            q = rng.randrange(12, len(m) // 2)
+            m = m[:q] + m[q:q + 4096] + m[q:]
+        out.append(bytes(m))
+    return out
+
+
+@pytest.mark.gpu
+def test_device_chunked_fuzz_matches_oracle(torch, native_lib, records):
+    """Corrupt large members through the chunked path: the device accepts exactly
+    the members the oracle accepts (bit-exact), rejects the others, and returns."""
+    from streaming_data_loader_amd.device import DeviceBatcher
+    db = DeviceBatcher(batch_size=8, sequence_length=128)
+    for m in chunked_fuzz_cases(records):
+        assert len(m) >= 1 << 20
+        rc, out, status, got, _ = device_inflate(torch, db, [m], check=False)
+        ost, obytes = oracle_lib.gz_inflate(m)
+        assert (status[0] == GZ_OK) == (ost == GZ_OK), (status[0], ost)
+        if ost == GZ_OK:
+            assert got[0] == obytes
