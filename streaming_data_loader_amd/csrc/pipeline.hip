@@ -508,6 +508,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SDL_ROWS_WA
         const int64_t n = (int64_t)cnt + P.n_pre + P.n_post;
         const int64_t base = P.chunk ? (int64_t)k * S : 0;
         const int l = (int)((n - base) < S ? (n - base) : S);
+        // (rng_mode 1) the row's mask words, loaded with the ids below: one memory round trip
+        uint32_t mwd[MR];
+        if (P.task == 0 && P.rng_mode == 1) {
+            const uint32_t *mb = P.mask_bits + g * (int64_t)((S + 31) >> 5);
+#pragma unroll
+            for (int m = 0; m < MR; ++m) {
+                const int j0 = 256 * m + 4 * lane;
+                mwd[m] = j0 < S ? mb[j0 >> 5] : 0u;
+            }
+        }
 
         int32_t id[MR][4];
 #pragma unroll
@@ -530,13 +540,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SDL_ROWS_WA
         if (P.task == 0) {  // MLM: BertData::mask_batch
             bool sel[MR][4];
             if (P.rng_mode == 1) {  // rand-compatible mode: the row's bits from k_mask_rand
-                const uint32_t *mb = P.mask_bits + g * (int64_t)((S + 31) >> 5);
 #pragma unroll
                 for (int m = 0; m < MR; ++m) {
                     const int j0 = 256 * m + 4 * lane;
-                    const uint32_t wd = j0 < S ? mb[j0 >> 5] : 0u;
 #pragma unroll
-                    for (int w = 0; w < 4; ++w) sel[m][w] = (wd >> ((j0 + w) & 31)) & 1u;
+                    for (int w = 0; w < 4; ++w) sel[m][w] = (mwd[m] >> ((j0 + w) & 31)) & 1u;
                 }
             } else {
                 uint32_t key[MR][4];
@@ -617,11 +625,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SDL_ROWS_WA
 // accepted, lo32(v * n) <= zone(n) = (n << lz(n)) - 1 with n = i + 1 -- rand's
 // "conservative" zone rejects up to half the words for n just above a power of
 // two, so about 30 % of a row's ~730 words are rejected and every row has
-// rejections.  Phase A runs each row's walk in one lane (64 rows per wave):
-// the lane computes its ChaCha12 blocks in registers, 16 words per block in an
-// unrolled loop, and writes each swap index j_i to the row's slice of `jbuf`;
-// the walk stops after step k (steps k-1 .. 1 only permute [0, k) among itself).
-// Phase B, a wave per row: mask_batch only uses the SET of the first k shuffled
+// rejections.  Phase A (k_mask_rand_walk) runs each row's walk in one lane (64
+// rows per wave): the lane computes its ChaCha12 blocks in registers, 16 words
+// per block in an unrolled loop, and writes each swap index j_i to the row's
+// slice of `jbuf`; the walk stops after step k (steps k-1 .. 1 only permute
+// [0, k) among itself).  Phase B (k_mask_rand_set, its own launch so that every
+// row is a wave and the waves hide each other's LDS latency), a wave per row: mask_batch only uses the SET of the first k shuffled
 // positions, and Fisher-Yates from the end never moves a value out of [0, k)
 // once steps i < k begin (j_i <= i), so the set is what [0, k) holds after steps
 // S-1 .. k.  The value at position p just before step p came from the latest
@@ -650,20 +659,17 @@ __device__ __forceinline__ void chacha12_block(const uint32_t (&k)[8], uint32_t 
     o[12] = x12 + ctr; o[13] = x13; o[14] = x14; o[15] = x15;
 }
 
+// Phase A: one lane per row, 64 rows per wave
 template <int MR>
-__global__ __launch_bounds__(64) void k_mask_rand(RowParams P, const uint32_t *__restrict__ row_off,
-                                                  const uint32_t *__restrict__ row_rec, SegSel sel, int64_t rows_cap,
-                                                  uint16_t *__restrict__ jbuf, uint32_t *__restrict__ bits) {
-    __shared__ uint32_t s_next[64 * MR];
-    __shared__ uint32_t s_bits[2 * MR];
+__global__ __launch_bounds__(64) void k_mask_rand_walk(RowParams P, const uint32_t *__restrict__ row_off,
+                                                       const uint32_t *__restrict__ row_rec, SegSel sel,
+                                                       int64_t rows_cap, uint16_t *__restrict__ jbuf) {
     const int lane = lane_id();
-    const int S = P.S, W = (S + 31) >> 5, kmask = P.mask_length < S ? P.mask_length : S;
+    const int S = P.S, kmask = P.mask_length < S ? P.mask_length : S;
     // only steps i >= k move values into or out of [0, k): the walk stops there
     const int i0 = kmask > 1 ? kmask : 1;
     const RowSpan rs = row_span(sel, row_off, P.B, rows_cap);
-    constexpr uint32_t NONE = 0xFFFFFFFFu;
     for (int64_t g0 = rs.g_lo + (int64_t)blockIdx.x * 64; g0 < (int64_t)rs.g_real; g0 += (int64_t)gridDim.x * 64) {
-        // ---- A. lane per row: the shuffle's swap indices j_i, i = S-1 .. k --------
         const int64_t g = g0 + lane;
         int i = 0;
         uint32_t key[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
@@ -680,58 +686,102 @@ __global__ __launch_bounds__(64) void k_mask_rand(RowParams P, const uint32_t *_
             i = S - 1;
         }
         uint32_t n = (uint32_t)i + 1u, zone = (n << __builtin_clz(n)) - 1u;
+        // (S % 8 == 0) indices are collected eight at a time -- positions 8b .. 8b + 7, the
+        // walk runs downwards -- in a 128-bit shift register and stored as one 16-B store:
+        // a lane's own row, so each per-index 2-B store would touch its own line
+        const bool vec = (S & 7) == 0;
+        uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
         for (uint32_t blk = 0; __any(i >= i0); ++blk) {
             uint32_t o[16];
             chacha12_block(key, blk, o);
+            if (vec) {
+                // branch-free per word (selects, no exec-mask work on the one scalar unit per
+                // CU); only the store of a completed group of eight is predicated
 #pragma unroll
-            for (int q = 0; q < 16; ++q) {
-                const uint64_t m = (uint64_t)o[q] * n;
-                if (i >= i0 && (uint32_t)m <= zone) {
-                    jrow[i] = (uint16_t)(m >> 32);
-                    --i;
+                for (int q = 0; q < 16; ++q) {
+                    const uint64_t m = (uint64_t)o[q] * n;
+                    const bool acc = i >= i0 && (uint32_t)m <= zone;
+                    const uint32_t v = (uint32_t)(m >> 32);
+                    a3 = acc ? (a3 << 16) | (a2 >> 16) : a3;
+                    a2 = acc ? (a2 << 16) | (a1 >> 16) : a2;
+                    a1 = acc ? (a1 << 16) | (a0 >> 16) : a1;
+                    a0 = acc ? (a0 << 16) | v : a0;
+                    if (acc && (i & 7) == 0)  // positions i .. i + 7 are complete
+                        *reinterpret_cast<uint4 *>(jrow + i) = make_uint4(a0, a1, a2, a3);
+                    i -= acc ? 1 : 0;
                     n = (uint32_t)i + 1u;
                     zone = (n << __builtin_clz(n)) - 1u;
                 }
+            } else {
+#pragma unroll
+                for (int q = 0; q < 16; ++q) {
+                    const uint64_t m = (uint64_t)o[q] * n;
+                    if (i >= i0 && (uint32_t)m <= zone) {
+                        jrow[i] = (uint16_t)(m >> 32);
+                        --i;
+                        n = (uint32_t)i + 1u;
+                        zone = (n << __builtin_clz(n)) - 1u;
+                    }
+                }
             }
         }
-        __syncthreads();  // (workgroup scope: the rows' indices are visible to the whole wave)
-        // ---- B. wave per row: the first k positions' set -------------------------
-        // Row h+1's indices are loaded into registers while row h is resolved in LDS.
-        const int64_t gz = g0 + 64 < (int64_t)rs.g_real ? g0 + 64 : (int64_t)rs.g_real;
-        uint32_t jn[MR];
-        auto load_row = [&](int64_t h) {
-            const uint16_t *jr = jbuf + h * (int64_t)S;
-#pragma unroll
-            for (int m = 0; m < MR; ++m) {
-                const int t = lane + 64 * m;
-                jn[m] = t >= i0 && t < S ? (uint32_t)jr[t] : (uint32_t)t;  // (t, t): no move
+        if (vec && g < (int64_t)rs.g_real && (i0 & 7) != 0) {  // the partial block [i0, (i0 | 7)]
+            const uint32_t w[4] = {a0, a1, a2, a3};
+            for (int p = i0; p <= (i0 | 7); ++p) {  // position p is the (p - i0)-th newest value
+                const int d = p - i0;
+                jrow[p] = (uint16_t)(w[d >> 1] >> (16 * (d & 1)));
             }
-        };
-        load_row(g0);
-        for (int64_t h = g0; h < gz; ++h) {
-            uint32_t jc[MR];
-#pragma unroll
-            for (int m = 0; m < MR; ++m) jc[m] = jn[m];
-            if (h + 1 < gz) load_row(h + 1);
-#pragma unroll
-            for (int m = 0; m < MR; ++m) s_next[lane + 64 * m] = NONE;
-            if (lane < 2 * MR) s_bits[lane] = 0u;
-            __syncthreads();
-            // next(p): the latest swap into p among steps i >= k (a self swap moves nothing)
-#pragma unroll
-            for (int m = 0; m < MR; ++m)
-                if (jc[m] != (uint32_t)(lane + 64 * m)) atomicMin(&s_next[jc[m]], (uint32_t)(lane + 64 * m));
-            __syncthreads();
-            // [0, k) holds val(next(x)) (or x): follow each chain to its end
-            for (int x = lane; x < kmask; x += 64) {
-                uint32_t p = (uint32_t)x;
-                for (uint32_t q = s_next[p]; q != NONE; q = s_next[p]) p = q;
-                atomicOr(&s_bits[p >> 5], 1u << (p & 31));
-            }
-            __syncthreads();
-            if (lane < W) bits[h * (int64_t)W + lane] = s_bits[lane];
-            __syncthreads();
         }
+    }
+}
+
+// Phase B: one wave per row (four rows per block, each wave on its own LDS); the
+// waves of a block run different row counts, so they meet only through wave
+// barriers
+template <int MR>
+__global__ __launch_bounds__(256) void k_mask_rand_set(RowParams P, const uint32_t *__restrict__ row_off,
+                                                      SegSel sel, int64_t rows_cap,
+                                                      const uint16_t *__restrict__ jbuf, uint32_t *__restrict__ bits) {
+    __shared__ uint32_t s_next[4][64 * MR];
+    __shared__ uint32_t s_bits[4][2 * MR];
+    const int lane = lane_id(), wv = (int)(threadIdx.x >> 6);
+    const int S = P.S, W = (S + 31) >> 5, kmask = P.mask_length < S ? P.mask_length : S;
+    const int i0 = kmask > 1 ? kmask : 1;
+    const RowSpan rs = row_span(sel, row_off, P.B, rows_cap);
+    constexpr uint32_t NONE = 0xFFFFFFFFu;
+    uint32_t *nx = s_next[wv];
+    uint32_t *bt = s_bits[wv];
+    auto wave_sync = [] {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    };
+    for (int64_t h = rs.g_lo + (int64_t)blockIdx.x * 4 + wv; h < (int64_t)rs.g_real; h += (int64_t)gridDim.x * 4) {
+        const uint16_t *jr = jbuf + h * (int64_t)S;
+        uint32_t jc[MR];
+#pragma unroll
+        for (int m = 0; m < MR; ++m) {
+            const int t = lane + 64 * m;
+            jc[m] = t >= i0 && t < S ? (uint32_t)jr[t] : (uint32_t)t;  // (t, t): no move
+        }
+#pragma unroll
+        for (int m = 0; m < MR; ++m) nx[lane + 64 * m] = NONE;
+        if (lane < 2 * MR) bt[lane] = 0u;
+        wave_sync();
+        // next(p): the latest swap into p among steps i >= k (a self swap moves nothing)
+#pragma unroll
+        for (int m = 0; m < MR; ++m)
+            if (jc[m] != (uint32_t)(lane + 64 * m)) atomicMin(&nx[jc[m]], (uint32_t)(lane + 64 * m));
+        wave_sync();
+        // [0, k) holds val(next(x)) (or x): follow each chain to its end
+        for (int x = lane; x < kmask; x += 64) {
+            uint32_t p = (uint32_t)x;
+            for (uint32_t q = nx[p]; q != NONE; q = nx[p]) p = q;
+            atomicOr(&bt[p >> 5], 1u << (p & 31));
+        }
+        wave_sync();
+        if (lane < W) bits[h * (int64_t)W + lane] = bt[lane];
+        wave_sync();
     }
 }
 
@@ -741,15 +791,19 @@ hipError_t launch_mask_rand(const RowParams &P, const uint32_t *row_off, const u
     if (P.S > RAND_MAX_S) return hipErrorInvalidValue;
     const int64_t want = (rows_cap + 63) / 64;
     const int64_t grid = want < 4096 ? want : 4096;
-    if (P.S <= 512)
-        hipLaunchKernelGGL(k_mask_rand<8>, dim3((unsigned)grid), dim3(64), 0, st, P, row_off, row_rec, sel, rows_cap,
-                           jbuf, bits);
-    else if (P.S <= 1024)
-        hipLaunchKernelGGL(k_mask_rand<16>, dim3((unsigned)grid), dim3(64), 0, st, P, row_off, row_rec, sel, rows_cap,
-                           jbuf, bits);
-    else
-        hipLaunchKernelGGL(k_mask_rand<RAND_MAX_S / 64>, dim3((unsigned)grid), dim3(64), 0, st, P, row_off, row_rec,
-                           sel, rows_cap, jbuf, bits);
+    const int64_t want_b = (rows_cap + 3) / 4;
+    const int64_t grid_b = want_b < 32768 ? want_b : 32768;
+#define SDL_MASK_RAND(MR)                                                                                            \
+    do {                                                                                                             \
+        hipLaunchKernelGGL(k_mask_rand_walk<MR>, dim3((unsigned)grid), dim3(64), 0, st, P, row_off, row_rec, sel,   \
+                           rows_cap, jbuf);                                                                          \
+        hipLaunchKernelGGL(k_mask_rand_set<MR>, dim3((unsigned)grid_b), dim3(256), 0, st, P, row_off, sel, rows_cap, \
+                           (const uint16_t *)jbuf, bits);                                                            \
+    } while (0)
+    if (P.S <= 512) SDL_MASK_RAND(8);
+    else if (P.S <= 1024) SDL_MASK_RAND(16);
+    else SDL_MASK_RAND(RAND_MAX_S / 64);
+#undef SDL_MASK_RAND
     return hipGetLastError();
 }
 
