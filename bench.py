@@ -275,6 +275,9 @@ def parse_args(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--soak-s", type=float, default=4.0,
+                    help="after the timed region (never part of it): re-run the step for this long and check "
+                         "that every run writes the same planes as the timed one (device checksums); 0: off")
     ap.add_argument("--task", default="mlm", choices=sorted(TASKS))
     ap.add_argument("--arena-mib", type=int, default=256)
     ap.add_argument("--corpus", default="fixture", choices=["fixture", "heldout"],
@@ -363,6 +366,49 @@ def max_over_ranks(dt, world, device=None):
     t = torch.tensor([dt], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+class _DevView:
+    """__cuda_array_interface__ of a device buffer the library owns (int32)"""
+    def __init__(self, ptr, n):
+        self.__cuda_array_interface__ = {"shape": (n,), "typestr": "<i4", "data": (ptr, False), "version": 3}
+
+
+def plane_checksums(res, rows, task, dev):
+    """Device-side sums of the int32 planes of a result (all elements, and the
+    odd ones): a cheap fingerprint of what a step wrote."""
+    import torch
+    out = []
+    for ptr, w in ((res.r.input_ids, task["S"]), (res.r.attention_mask, task["S"]),
+                   (res.r.token_type_ids, task["S"]), (res.r.labels, res.r.label_width)):
+        if not ptr or rows == 0:
+            out.append((0, 0))
+            continue
+        t = torch.as_tensor(_DevView(ptr, rows * w), device=dev)
+        out.append((int(t.sum(dtype=torch.int64)), int(t[1::2].sum(dtype=torch.int64))))
+    return out
+
+
+def determinism_soak(step, res, rows, task, dev, seconds):
+    """Re-run the step (outside the timed region) for `seconds` and compare each
+    run's rows, tokens and plane checksums with the timed run's: the kernels must
+    be deterministic (every mask and span draw is keyed by record, not by
+    scheduling).  Keeps the device busy long enough for an external sampler to
+    see it; exits 4 on any difference."""
+    import torch
+    want = (rows, res.tokens(), plane_checksums(res, rows, task, dev))
+    t0 = time.perf_counter()
+    n = 0
+    while time.perf_counter() - t0 < seconds:
+        r2 = step()
+        torch.cuda.synchronize(dev)
+        n += 1
+        got = (r2.rows(), r2.tokens(), plane_checksums(r2, r2.rows(), task, dev))
+        if got != want:
+            print(f"bench.py: run {n} after the timed region differs from it: {got} vs {want}", file=sys.stderr)
+            sys.exit(4)
+    log(f"determinism soak: {n} more runs in {time.perf_counter() - t0:.1f} s, identical planes")
+    return {"runs": n, "seconds": round(time.perf_counter() - t0, 2), "identical": True}
 
 
 def base_line(args, world, step_ms, value, task, N, R, rows, toks):
@@ -522,6 +568,7 @@ def main(argv=None):
         sys.exit(3)
 
     rows, toks = res.rows(), res.tokens()
+    soak = determinism_soak(step, res, rows, task, dev, args.soak_s) if args.soak_s > 0 else None
     stage_ms = {k: v / args.steps for k, v in stage_sum.items()}
     tok_ms = stage_ms["tokenize"]
     step_ms = dt / args.steps * 1e3
@@ -542,6 +589,8 @@ def main(argv=None):
     # PMC summary shows it closer to its peak than HBM traffic is to its own
     hbm_frac = achieved / HBM_PEAK_GBPS
     bound = issue["bound"] if issue is not None and issue["frac"] > hbm_frac else "hbm"
+    if soak is not None:
+        line["determinism"] = soak
     line["roofline"] = {"bound": bound, "kernel": task["kernel"], "achieved": round(achieved, 2),
                         "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(hbm_frac, 5),
                         "traffic": traffic, "issue": issue,
