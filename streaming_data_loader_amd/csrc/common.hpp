@@ -113,6 +113,18 @@ constexpr int UNI_HUGE_NORM = 1 << 18;  // ... per wave of the huge-item kernel
 enum : uint32_t { GB_OTHER = 0, GB_CR, GB_LF, GB_CONTROL, GB_EXTEND, GB_ZWJ, GB_RI, GB_PREPEND, GB_SPACING,
                   GB_L, GB_V, GB_T, GB_LV, GB_LVT };
 constexpr uint32_t GP_EXTPICT = 0x10u, GP_WS = 0x80u;
+// White_Space (char::is_whitespace; tools/make_t5_tables.py WHITE_SPACE) and the
+// property byte of an ASCII char, as arithmetic: the host checks the loaded
+// tables agree (sdl_batcher.cpp), so the kernels test them without a load
+__host__ __device__ inline bool uni_white_space(uint32_t cp) {
+    if (cp < 0x80u) return (cp >= 9u && cp <= 13u) || cp == 32u;
+    return cp == 0x85u || cp == 0xA0u || cp == 0x1680u || cp - 0x2000u <= 0xAu || cp == 0x2028u || cp == 0x2029u ||
+           cp == 0x202Fu || cp == 0x205Fu || cp == 0x3000u;
+}
+__host__ __device__ inline uint32_t uni_ascii_props(uint32_t c) {
+    const uint32_t gcb = c == 13u ? GB_CR : c == 10u ? GB_LF : (c < 32u || c == 127u) ? GB_CONTROL : GB_OTHER;
+    return gcb | (uni_white_space(c) ? GP_WS : 0u);
+}
 // per-code-point entry of the t5 normalizer (x, y):
 //   x bits 0-7 grapheme/whitespace properties, bit 8 the char is a charsmap
 //   key, bit 9 it is a proper prefix of a longer key, bit 10 its normalization

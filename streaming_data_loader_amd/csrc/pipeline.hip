@@ -473,7 +473,10 @@ __device__ __forceinline__ void store4(int32_t *p, int j0, int S, bool vec, int3
 #ifndef SDL_ROWS_WAVES
 #define SDL_ROWS_WAVES 1
 #endif
-template <int MR>
+// RM1: MLM under rng_mode 1 (mask bits from k_mask_rand).  A template flag, not
+// a runtime branch: the mask-word registers would cost the Philox path a wave
+// per SIMD (k_rows<2>: 80 -> 82 VGPRs, 6 -> 5 waves, 0.267 -> 0.295 ms).
+template <int MR, bool RM1>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SDL_ROWS_WAVES, 8))) void k_rows(RowParams P, const uint32_t *__restrict__ tok,
                                               const uint32_t *__restrict__ rec_tok, const uint32_t *__restrict__ rec_cnt,
                                               const uint32_t *__restrict__ row_off, const uint32_t *__restrict__ row_rec,
@@ -510,7 +513,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SDL_ROWS_WA
         const int l = (int)((n - base) < S ? (n - base) : S);
         // (rng_mode 1) the row's mask words, loaded with the ids below: one memory round trip
         uint32_t mwd[MR];
-        if (P.task == 0 && P.rng_mode == 1) {
+        if (RM1) {
             const uint32_t *mb = P.mask_bits + g * (int64_t)((S + 31) >> 5);
 #pragma unroll
             for (int m = 0; m < MR; ++m) {
@@ -539,7 +542,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SDL_ROWS_WA
         const uint64_t rec = P.first_record + (uint64_t)r;
         if (P.task == 0) {  // MLM: BertData::mask_batch
             bool sel[MR][4];
-            if (P.rng_mode == 1) {  // rand-compatible mode: the row's bits from k_mask_rand
+            if (RM1) {  // rand-compatible mode: the row's bits from k_mask_rand
 #pragma unroll
                 for (int m = 0; m < MR; ++m) {
                     const int j0 = 256 * m + 4 * lane;
@@ -856,9 +859,15 @@ hipError_t launch_rows(const RowParams &P, const uint32_t *tok, const uint32_t *
     const unsigned grid = (unsigned)(want < SDL_ROWS_GRID_CAP ? want : SDL_ROWS_GRID_CAP);
     const int MR = (P.S + 255) / 256;
     if (P.label_width > 256 * MR) return hipErrorInvalidValue;
+    const bool rm1 = P.task == 0 && P.rng_mode == 1;
+    if (rm1 && !P.mask_bits) return hipErrorInvalidValue;
 #define SDL_ROWS(MM)                                                                                                 \
-    hipLaunchKernelGGL(k_rows<MM>, dim3(grid), dim3(256), 0, st, P, tok, rec_tok, rec_cnt, row_off, row_rec, sel, \
-                       rows_cap, out)
+    if (rm1)                                                                                                          \
+        hipLaunchKernelGGL((k_rows<MM, true>), dim3(grid), dim3(256), 0, st, P, tok, rec_tok, rec_cnt, row_off,      \
+                           row_rec, sel, rows_cap, out);                                                              \
+    else                                                                                                              \
+        hipLaunchKernelGGL((k_rows<MM, false>), dim3(grid), dim3(256), 0, st, P, tok, rec_tok, rec_cnt, row_off,     \
+                           row_rec, sel, rows_cap, out)
     if (MR <= 1) SDL_ROWS(1);
     else if (MR <= 2) SDL_ROWS(2);
     else if (MR <= 4) SDL_ROWS(4);

@@ -878,6 +878,14 @@ int sdl_batcher_create(const sdl_config *cfg, const char *tokenizer_path, const 
                     flat[2 * cp] = t.cent[at];
                     flat[2 * cp + 1] = t.cent[at + 1];
                 }
+                // the kernels compute White_Space and the ASCII property bytes
+                // (uni_white_space / uni_ascii_props): the tables must agree
+                for (uint32_t cp = 0; cp < 0x110000; ++cp) {
+                    const uint32_t x = t.cent[2 * ((size_t)t.cpage[cp >> 8] * 256 + (cp & 255))] & 0xFFu;
+                    if (((x & GP_WS) != 0) != uni_white_space(cp) || (cp < 0x80 && x != uni_ascii_props(cp)))
+                        throw std::runtime_error("t5 grapheme table: White_Space / ASCII properties differ from "
+                                                 "the kernels' built-in ones at U+" + std::to_string(cp));
+                }
                 h->d_cbmp.ensure(0x10000);
                 HIP_TRY(hipMemcpy(h->d_cbmp.p, flat.data(), flat.size() * 4, hipMemcpyHostToDevice));
                 d.cbmp = h->d_cbmp.p;

@@ -221,7 +221,7 @@ template <class RB, class Put>
 __device__ bool normalize_span(const DevTok &T, const RB &rb, int64_t a, int64_t b, bool ctx_space, const Put &put) {
     GState g;
     gstate_reset(g);
-    if (ctx_space) gcb_break(g, cp_ent(T, 0x20u).x & 0xFFu);
+    if (ctx_space) gcb_break(g, uni_ascii_props(0x20u));
     auto put_entry = [&](uint2 e, uint32_t bytes, int bl) -> bool {
         if (!(e.x & CP_KEY)) {
             for (int k = 0; k < bl; ++k)
@@ -240,6 +240,11 @@ __device__ bool normalize_span(const DevTok &T, const RB &rb, int64_t a, int64_t
     };
     bool first = true;
     int64_t q = a;
+    // the entry of the char that ended the last cluster (its load is reused as
+    // the next cluster's first: the chain of dependent loads is one per non-ASCII
+    // char, and ASCII chars only need their property byte -- uni_ascii_props)
+    uint32_t c_cp = 0xFFFFFFFFu;
+    uint2 c_e = make_uint2(0u, 0u);
     while (q < b) {
         const int64_t cs = q;
         {  // printable ASCII followed by ASCII (or the end): a one-char cluster of
@@ -256,7 +261,7 @@ __device__ bool normalize_span(const DevTok &T, const RB &rb, int64_t a, int64_t
         uint32_t cp0, by0;
         int bl0;
         q += dec_char(rb, q, b, &cp0, &by0, &bl0);
-        const uint2 e0 = cp_ent(T, cp0);
+        const uint2 e0 = cp0 == c_cp ? c_e : cp_ent(T, cp0);
         const bool brk = gcb_break(g, e0.x & 0xFFu);
         const bool forced = first && ctx_space && !brk;
         first = false;
@@ -266,8 +271,16 @@ __device__ bool normalize_span(const DevTok &T, const RB &rb, int64_t a, int64_t
             uint32_t cp2, by2;
             int bl2;
             const int rl = dec_char(rb, q, b, &cp2, &by2, &bl2);
+            uint32_t pr2;
+            if (cp2 < 0x80u) {
+                pr2 = uni_ascii_props(cp2);
+            } else {
+                c_e = cp_ent(T, cp2);
+                c_cp = cp2;
+                pr2 = c_e.x & 0xFFu;
+            }
             GState g2 = g;
-            if (gcb_break(g2, cp_ent(T, cp2).x & 0xFFu)) break;
+            if (gcb_break(g2, pr2)) break;
             g = g2;
             for (int k = 0; k < bl2; ++k, ++L) {
                 const uint32_t v = (by2 >> (8 * k)) & 0xFFu;
@@ -320,7 +333,7 @@ __device__ __forceinline__ bool norm_ws(const DevTok &T, const NB &nb, int i, in
     uint32_t cp = b & (l == 2 ? 0x1Fu : l == 3 ? 0x0Fu : 0x07u);
     for (int j = 1; j < l; ++j) cp = cp << 6 | (nb(i + j) & 0x3Fu);
     *len = l;
-    return (cp_ent(T, cp).x & GP_WS) != 0u;
+    return uni_white_space(cp);  // (host-checked against the table's GP_WS bits)
 }
 
 // ---- long items: global scratch, one lane, sequential -------------------------
