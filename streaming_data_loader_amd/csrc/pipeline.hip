@@ -201,6 +201,10 @@ hipError_t launch_chunk_ranges(const uint64_t *off, int64_t R, int64_t N, uint32
 // ---------------------------------------------------------------------------
 // Per-chunk token lists -> one dense token array in arena order.
 // ---------------------------------------------------------------------------
+#ifndef SDL_COMPACT_CPW
+#define SDL_COMPACT_CPW 4
+#endif
+constexpr int COMPACT_CPW = SDL_COMPACT_CPW;  // chunks per wave: their loads are in flight together
 __global__ __launch_bounds__(256) void k_compact_tokens(const uint32_t *__restrict__ tokc,
                                                         const uint32_t *__restrict__ chunk_cnt,
                                                         const uint32_t *__restrict__ chunk_off, int64_t n_chunks,
@@ -209,48 +213,83 @@ __global__ __launch_bounds__(256) void k_compact_tokens(const uint32_t *__restri
                                                         const BpeLong *__restrict__ long_list,
                                                         const uint16_t *__restrict__ long_scratch,
                                                         const uint32_t *__restrict__ long_pool, int64_t stride) {
-    const int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);  // one wave per chunk
-    if (c >= n_chunks) return;
-    const uint32_t n = chunk_cnt[c];
-    const uint32_t *src = tokc + c * stride;
-    uint32_t *dst = tok + chunk_off[c];
+    const int64_t cb = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * COMPACT_CPW;  // the wave's first chunk
+    if (cb >= n_chunks) return;
     const int lane = threadIdx.x & 63;
+    uint32_t n[COMPACT_CPW], o[COMPACT_CPW];
+#pragma unroll
+    for (int j = 0; j < COMPACT_CPW; ++j) {
+        const bool in = cb + j < n_chunks;
+        n[j] = in ? chunk_cnt[cb + j] : 0u;
+        o[j] = in ? chunk_off[cb + j] : 0u;
+    }
     if (!long_count || *long_count == 0) {
-        // 16-B loads of the (16-B aligned) chunk list, 4 dword stores per lane
-        for (uint32_t i = 4 * lane; i < n; i += 256) {
-            typedef uint32_t u4v __attribute__((ext_vector_type(4)));
-            const u4v vv = __builtin_nontemporal_load(reinterpret_cast<const u4v *>(src + i));
-            const uint4 v = make_uint4(vv.x, vv.y, vv.z, vv.w);
-            dst[i] = v.x;
-            if (i + 1 < n) dst[i + 1] = v.y;
-            if (i + 2 < n) dst[i + 2] = v.z;
-            if (i + 3 < n) dst[i + 3] = v.w;
+        // lane-contiguous dwords: every store instruction writes 256 B of the
+        // dense array back to back (at any alignment); the first 256 ids of all
+        // the wave's chunks are loaded before any is stored
+        uint32_t v[COMPACT_CPW][4];
+#pragma unroll
+        for (int j = 0; j < COMPACT_CPW; ++j)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t i = 64 * k + lane;
+                v[j][k] = i < n[j] ? __builtin_nontemporal_load(tokc + (cb + j) * stride + i) : 0u;
+            }
+#pragma unroll
+        for (int j = 0; j < COMPACT_CPW; ++j)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t i = 64 * k + lane;
+                if (i < n[j]) tok[(uint64_t)o[j] + i] = v[j][k];
+            }
+        for (int j = 0; j < COMPACT_CPW; ++j) {  // chunks with more than 256 ids
+            const uint32_t *src = tokc + (cb + j) * stride;
+            for (uint32_t i0 = 256; i0 < n[j]; i0 += 256) {
+                uint32_t w[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const uint32_t i = i0 + 64 * k + lane;
+                    w[k] = i < n[j] ? __builtin_nontemporal_load(src + i) : 0u;
+                }
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const uint32_t i = i0 + 64 * k + lane;
+                    if (i < n[j]) tok[(uint64_t)o[j] + i] = w[k];
+                }
+            }
         }
         return;
     }
-    // byte-level BPE with long pieces: an entry LONG_MARK | i stands for the
-    // k ids of long piece i (in long_scratch at its byte position)
-    const uint32_t ne = chunk_ent[c];  // entries written by the chunk kernel
-    uint32_t written = 0;
-    for (uint32_t e0 = 0; e0 < ne; e0 += 64) {
-        const uint32_t e = e0 + lane;
-        const uint32_t x = e < ne ? __builtin_nontemporal_load(src + e) : 0u;
-        const bool mark = (x & 0x80000000u) != 0u;
-        const uint32_t w = e >= ne ? 0u : !mark ? 1u : long_pool ? long_pool[x & 0x7FFFFFFFu] : long_list[x & 0x7FFFFFFFu].k;
-        const uint32_t incl = wave_incl_sum(w);
-        const uint32_t at = written + incl - w;
-        if (e < ne && at < n) {
-            if (!mark) {
-                dst[at] = x;
-            } else if (long_pool) {  // unigram long item: [k, ids...] in the pool
-                const uint32_t o = x & 0x7FFFFFFFu;
-                for (uint32_t j = 0; j < w; ++j) dst[at + j] = long_pool[o + 1 + j];
-            } else {
-                const BpeLong L = long_list[x & 0x7FFFFFFFu];
-                for (uint32_t j = 0; j < L.k; ++j) dst[at + j] = long_scratch[L.pos + j];
+    // byte-level BPE / unigram with long items: an entry LONG_MARK | i stands
+    // for the k ids of long piece i (in long_scratch at its byte position) or
+    // of pool item i
+    for (int j = 0; j < COMPACT_CPW; ++j) {
+        const int64_t c = cb + j;
+        if (c >= n_chunks) break;
+        const uint32_t *src = tokc + c * stride;
+        uint32_t *dst = tok + o[j];
+        const uint32_t ne = chunk_ent[c];  // entries written by the chunk kernel
+        uint32_t written = 0;
+        for (uint32_t e0 = 0; e0 < ne; e0 += 64) {
+            const uint32_t e = e0 + lane;
+            const uint32_t x = e < ne ? __builtin_nontemporal_load(src + e) : 0u;
+            const bool mark = (x & 0x80000000u) != 0u;
+            const uint32_t w = e >= ne ? 0u : !mark ? 1u : long_pool ? long_pool[x & 0x7FFFFFFFu] : long_list[x & 0x7FFFFFFFu].k;
+            const uint32_t incl = wave_incl_sum(w);
+            const uint32_t at = written + incl - w;
+            if (e < ne && at < n[j]) {
+                if (!mark) {
+                    dst[at] = x;
+                } else if (long_pool) {  // unigram long item: [k, ids...] in the pool
+                    const uint32_t po = x & 0x7FFFFFFFu;
+                    for (uint32_t q = 0; q < w; ++q) dst[at + q] = long_pool[po + 1 + q];
+                } else {
+                    const BpeLong L = long_list[x & 0x7FFFFFFFu];
+                    for (uint32_t q = 0; q < L.k; ++q) dst[at + q] = long_scratch[L.pos + q];
+                }
             }
+            written += (uint32_t)lane_bcast((int)incl, 63);
         }
-        written += (uint32_t)lane_bcast((int)incl, 63);
     }
 }
 
@@ -259,7 +298,8 @@ hipError_t launch_compact_tokens(const uint32_t *tokc, const uint32_t *chunk_cnt
                                  const uint32_t *chunk_ent, const BpeLong *long_list, const uint16_t *long_scratch,
                                  hipStream_t st, const uint32_t *long_pool, int64_t stride) {
     if (n_chunks == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_compact_tokens, dim3((unsigned)((n_chunks + 3) / 4)), dim3(256), 0, st, tokc, chunk_cnt,
+    const int64_t waves = (n_chunks + COMPACT_CPW - 1) / COMPACT_CPW;
+    hipLaunchKernelGGL(k_compact_tokens, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, tokc, chunk_cnt,
                        chunk_off, n_chunks, tok, long_count, chunk_ent, long_list, long_scratch, long_pool, stride);
     return hipGetLastError();
 }
