@@ -915,6 +915,13 @@ def provider_gzip(db, records, order, dev, steps, warmup, step_ms, json_mib=64, 
     native.d2h(db._h, full, out1.d_out, full.nbytes)
     assert full.tobytes() == buf, "device inflate of the single member differs from the JSON lines"
     del full
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        out1 = inflate_one()
+        jt1 = db.json_text(out1.d_out, int(out1.out_bytes))
+    torch.cuda.synchronize(dev)
+    ms1_text = (time.perf_counter() - t0) / steps * 1e3
+    assert int(jt1.n_records) == int(jt.n_records)
     # CPU: one member on one thread (the reference), BGZF members on 16 threads
     t0 = time.perf_counter()
     assert len(zlib.decompress(single, 31)) == len(buf)
@@ -931,6 +938,10 @@ def provider_gzip(db, records, order, dev, steps, warmup, step_ms, json_mib=64, 
             "gz_to_batches_MBps": round(len(buf) / (ms_text + step_ms * len(buf) / N_text) / 1e3, 2),
             "single_member": {"inflated_MBps": round(len(buf) / ms1 / 1e3, 2), "ms": round(ms1, 4),
                               "gz_bytes": len(single),
+                              "gz_to_text_ms": round(ms1_text, 4),
+                              "gz_to_text_MBps": round(len(buf) / ms1_text / 1e3, 2),
+                              "gz_to_batches_MBps": round(len(buf) / (ms1_text + step_ms * len(buf) / N_text) / 1e3,
+                                                          2),
                               "path": "one gzip member (zlib level 6) in HBM -> sdl_gzip_inflate_device (chunked: "
                                       "header search, chunks in parallel, window chain, CRC-32 + ISIZE), host-timed"},
             "cpu_zlib_1thread_one_member_MBps": round(len(buf) / cpu1 / 1e6, 2),

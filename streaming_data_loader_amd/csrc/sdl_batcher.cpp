@@ -1275,7 +1275,7 @@ X2N make_x2n() {  // zlib's x2n_table: x^(2^k) mod P(x), reflected
 // bytes, CRC-32 and ISIZE follow on the device.  The member's status gets
 // GZ_VERIFIED so the one-wave path skips it.
 constexpr uint64_t GZ_SPLIT_MIN = 1u << 20;  // smaller members: one wave each
-constexpr uint64_t GZ_CHUNK = 32u << 10;     // compressed bytes per chunk (at least; 64 KiB measured slower held-out)
+constexpr uint64_t GZ_CHUNK = 24u << 10;     // compressed bytes per chunk (at least; 16/20/28/32/64 KiB measured slower)
 constexpr uint64_t GZ_MAX_CHUNKS = 8192;     // (larger members: larger chunks)
 constexpr uint32_t GZ_SLOT_RATIO = 16;       // slot values per compressed byte of a chunk
 constexpr uint64_t GZ_FIND_SPAN = 2;         // header search: this many chunk lengths of bits
