@@ -139,3 +139,27 @@ def test_span_row_invariants(t5tok, records):
             rows += 1
     assert rows > 20
     assert ob.span_errors() == 0
+
+
+def test_grapheme_table_whitespace_and_ascii_match_kernel_arithmetic():
+    """tokenize_unigram.hip tests White_Space and an ASCII char's property byte
+    arithmetically (common.hpp uni_white_space / uni_ascii_props) instead of
+    loading them; the handle checks the loaded table agrees at creation.  The
+    same check here on the committed table, without a GPU."""
+    import struct
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "streaming_data_loader_amd",
+                        "data", "t5_graphemes.bin")
+    raw = open(path, "rb").read()
+    assert raw[:4] == b"SDLU"
+    _, n_pages, n_blocks = struct.unpack_from("<III", raw, 4)
+    pages = np.frombuffer(raw, np.uint16, n_pages, 16)
+    blocks = np.frombuffer(raw, np.uint8, n_blocks * 256, 16 + 2 * n_pages).reshape(n_blocks, 256)
+    props = blocks[pages].reshape(-1)
+    assert props.size == 0x110000
+    ws = {0x85, 0xA0, 0x1680, 0x2028, 0x2029, 0x202F, 0x205F, 0x3000} | set(range(0x2000, 0x200B)) | \
+        set(range(9, 14)) | {32}
+    got = set(np.nonzero(props & 0x80)[0].tolist())
+    assert got == ws
+    for c in range(128):
+        gcb = 1 if c == 13 else 2 if c == 10 else 3 if (c < 32 or c == 127) else 0
+        assert int(props[c]) == gcb | (0x80 if c in ws else 0), hex(c)
