@@ -10,12 +10,22 @@ import numpy as np
 from . import native
 
 
+class _CudaView:
+    """__cuda_array_interface__ (v3) of device memory the library owns: what
+    torch.as_tensor / cupy / numba take without a copy."""
+
+    def __init__(self, ptr, shape, typestr):
+        self.__cuda_array_interface__ = {"shape": tuple(shape), "typestr": typestr, "data": (int(ptr), False),
+                                         "version": 3}
+
+
 class DeviceResult:
-    def __init__(self, handle, rows_struct, n_records, S):
+    def __init__(self, handle, rows_struct, n_records, S, B=None):
         self.h = handle
         self.r = rows_struct
         self.n_records = n_records
         self.S = S
+        self.B = B
 
     def rows(self):
         v = np.zeros(1, np.uint32)
@@ -64,6 +74,37 @@ class DeviceResult:
 
         lab = get(self.r.labels_f32, LW, np.float32) if self.r.labels_f32 else get(self.r.labels, LW)
         return (get(self.r.input_ids, S), get(self.r.attention_mask, S), get(self.r.token_type_ids, S), lab)
+
+    def tensors(self, n_rows=None, device=None):
+        """The planes as zero-copy torch tensors on the device, keyed as the
+        reference's DataSet (input_ids, attention_mask, token_type_ids when the
+        task has them, labels: int32 [n, S], float32 [n, number_labels] for
+        multi-label).  Views of the handle's buffers: valid until its next call."""
+        import torch
+        n = self.rows() if n_rows is None else n_rows
+        S, LW = self.S, self.r.label_width
+        dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+        out = {}
+        for key, ptr, w, ts in (("input_ids", self.r.input_ids, S, "<i4"),
+                                ("attention_mask", self.r.attention_mask, S, "<i4"),
+                                ("token_type_ids", self.r.token_type_ids, S, "<i4"),
+                                ("labels", self.r.labels_f32 or self.r.labels, LW, "<f4" if self.r.labels_f32 else "<i4")):
+            if ptr and n > 0:
+                out[key] = torch.as_tensor(_CudaView(ptr, (n, w), ts), device=dev)
+        return out
+
+    def batches(self, n_rows=None, device=None):
+        """Consumer side without the pickle (a zero-copy tensor
+        frame instead of serde_pickle -> pickle.loads, external_dataset.py:52):
+        every batch as a dict of [B, ...] device tensor views plus its "rows"
+        (the last batch holds the rest; its pad rows keep the initial values)."""
+        if not self.B:
+            raise ValueError("batches() needs the batch size (DeviceBatcher results carry it)")
+        n = self.rows() if n_rows is None else n_rows
+        nb = -(-n // self.B)
+        full = self.tensors(nb * self.B, device)
+        return [dict({k: v[b * self.B:(b + 1) * self.B] for k, v in full.items()}, rows=min(self.B, n - b * self.B))
+                for b in range(nb)]
 
 
 class DeviceFrames:
@@ -134,7 +175,7 @@ class DeviceBatcher:
         native.check(native.load().sdl_process_device(self._h, ctypes.c_void_p(text_ptr), text_len,
                                                       ctypes.c_void_p(offsets_ptr), n_records, first_record,
                                                       ctypes.c_void_p(stream or None), ctypes.byref(out)))
-        return DeviceResult(self._h, out, n_records, self.cfg.sequence_length)
+        return DeviceResult(self._h, out, n_records, self.cfg.sequence_length, self.cfg.batch_size)
 
     def process_labels(self, text_ptr, text_len, offsets_ptr, n_records, labels_ptr, label_offsets_ptr,
                        first_record=0, stream=0):
@@ -144,7 +185,7 @@ class DeviceBatcher:
             self._h, ctypes.c_void_p(text_ptr), text_len, ctypes.c_void_p(offsets_ptr), n_records,
             ctypes.c_void_p(labels_ptr or None), ctypes.c_void_p(label_offsets_ptr or None), first_record,
             ctypes.c_void_p(stream or None), ctypes.byref(out)))
-        return DeviceResult(self._h, out, n_records, self.cfg.sequence_length)
+        return DeviceResult(self._h, out, n_records, self.cfg.sequence_length, self.cfg.batch_size)
 
     def json_text(self, jsonl_ptr, jsonl_len, stream=0):
         """The provider's JsonText filter on the device (sdl_json_text_device):

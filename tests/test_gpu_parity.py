@@ -319,3 +319,43 @@ def test_pipelined_segments_match_oracle(torch, native_lib, oracle_tok, records,
     res2 = run_device(torch, db, texts, first_record=17)
     assert res2.rows() == G
     np.testing.assert_array_equal(res2.planes(G)[0], want[0])
+
+
+def test_zero_copy_tensors_and_batches(torch, native_lib, oracle_tok, records):
+    """DeviceResult.tensors() / batches(): zero-copy device views of the planes
+    (the consumer without serde_pickle) equal the copied planes and the oracle's
+    batches, the last one padded with initial values; multi-label's float32 labels."""
+    texts = records[:300]
+    db = DeviceBatcher(batch_size=32, sequence_length=128, seed=11)
+    res = run_device(torch, db, texts, first_record=5)
+    G = res.rows()
+    want = oracle_lib.oracle_rows(oracle_tok, texts, 128, 19, 103, seed=11, B=32, first_record=5)
+    t = res.tensors()
+    assert set(t) == {"input_ids", "attention_mask", "token_type_ids", "labels"}
+    for j, k in enumerate(("input_ids", "attention_mask", "token_type_ids", "labels")):
+        assert t[k].is_cuda and t[k].dtype == torch.int32 and tuple(t[k].shape) == (G, 128)
+        np.testing.assert_array_equal(t[k].cpu().numpy(), want[j])
+    bs = res.batches()
+    assert len(bs) == -(-G // 32) and sum(b["rows"] for b in bs) == G
+    for b_i, b in enumerate(bs):
+        assert tuple(b["input_ids"].shape) == (32, 128)
+        r = b["rows"]
+        np.testing.assert_array_equal(b["input_ids"][:r].cpu().numpy(), want[0][b_i * 32:b_i * 32 + r])
+    last = bs[-1]
+    if last["rows"] < 32:
+        assert (last["input_ids"][last["rows"]:] == 0).all() and (last["labels"][last["rows"]:] == -100).all()
+    db.close()
+    ml = DeviceBatcher(task=native.SDL_TASK_MULTI_LABEL, batch_size=16, sequence_length=128, number_labels=9)
+    arena, offs = arena_from_texts(texts[:40])
+    labels = np.array([i % 9 for i in range(40)], np.uint32)
+    loff = np.arange(41, dtype=np.uint64)
+    ta = torch.from_numpy(np.concatenate([arena, np.zeros(16, np.uint8)])).cuda()
+    to = torch.from_numpy(offs.astype(np.int64)).cuda()
+    tl = torch.from_numpy(labels.astype(np.int32)).cuda()
+    tlo = torch.from_numpy(loff.astype(np.int64)).cuda()
+    r2 = ml.process_labels(ta.data_ptr(), len(arena), to.data_ptr(), 40, tl.data_ptr(), tlo.data_ptr())
+    torch.cuda.synchronize()
+    t2 = r2.tensors()
+    assert t2["labels"].dtype == torch.float32 and tuple(t2["labels"].shape) == (r2.rows(), 9)
+    np.testing.assert_array_equal(t2["labels"].cpu().numpy(), r2.planes()[3])
+    ml.close()
