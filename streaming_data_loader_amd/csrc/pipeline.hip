@@ -1126,8 +1126,14 @@ struct SpanPass {  // one pass of a round (LDS): cursors and lengths
 
 __device__ __forceinline__ void st_nt(int32_t *p, int32_t v) { __builtin_nontemporal_store(v, p); }
 
+#ifndef SDL_SPAN_WAVES
+#define SDL_SPAN_WAVES 6  // (RAND 0) 75 VGPRs, no spills: 0.507 -> 0.428 ms; 7 and 8 spill
+#endif
+#ifndef SDL_SPAN_GRID_CAP
+#define SDL_SPAN_GRID_CAP 16384  // with 6 waves per SIMD: 0.428 -> 0.414 ms
+#endif
 template <int RAND>  // draws: 0 the Philox contract, 1 the row's StdRng (rng_mode 1)
-__global__ __launch_bounds__(256) void k_rows_span(RowParams P, const uint32_t *__restrict__ tok,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RAND ? 1 : SDL_SPAN_WAVES, 8))) void k_rows_span(RowParams P, const uint32_t *__restrict__ tok,
                                                    const uint32_t *__restrict__ rec_tok,
                                                    const uint32_t *__restrict__ rec_cnt,
                                                    const uint32_t *__restrict__ row_off,
@@ -1318,7 +1324,7 @@ hipError_t launch_rows_span(const RowParams &P, const uint32_t *tok, const uint3
     if (rows_cap == 0) return hipSuccess;
     if (P.S > 65535 || (P.rng_mode == 1 && (!P.zig_x || !P.zig_f))) return hipErrorInvalidValue;
     const int64_t want = (rows_cap + 3) / 4;
-    const unsigned grid = (unsigned)(want < 4096 ? want : 4096);
+    const unsigned grid = (unsigned)(want < SDL_SPAN_GRID_CAP ? want : SDL_SPAN_GRID_CAP);
     if (sel.k == 0) {  // the error count covers the whole call
         hipError_t e = hipMemsetAsync(err, 0, sizeof(uint32_t), st);
         if (e != hipSuccess) return e;
