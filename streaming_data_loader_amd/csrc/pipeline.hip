@@ -510,14 +510,21 @@ __device__ __forceinline__ void store4(int32_t *p, int j0, int S, bool vec, int3
     }
 }
 
+// occupancy asked of the compiler (r03i): MR <= 2 Philox rows at 7 waves per SIMD
+// (k_rows<2>: 74 -> 71 VGPRs, no spills; mlm rows 0.270 -> 0.262 ms, multi-label
+// 0.080 -> 0.074; 8 spills and is slower); MR >= 4 and rng_mode 1 as they come
+// (asking 5-6 of them spills)
 #ifndef SDL_ROWS_WAVES
-#define SDL_ROWS_WAVES 1
+#define SDL_ROWS_WAVES 7
+#endif
+#ifndef SDL_ROWS_WAVES4
+#define SDL_ROWS_WAVES4 1
 #endif
 // RM1: MLM under rng_mode 1 (mask bits from k_mask_rand).  A template flag, not
 // a runtime branch: the mask-word registers would cost the Philox path a wave
 // per SIMD (k_rows<2>: 80 -> 82 VGPRs, 6 -> 5 waves, 0.267 -> 0.295 ms).
 template <int MR, bool RM1>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SDL_ROWS_WAVES, 8))) void k_rows(RowParams P, const uint32_t *__restrict__ tok,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MR >= 4 ? SDL_ROWS_WAVES4 : RM1 ? 1 : SDL_ROWS_WAVES, 8))) void k_rows(RowParams P, const uint32_t *__restrict__ tok,
                                               const uint32_t *__restrict__ rec_tok, const uint32_t *__restrict__ rec_cnt,
                                               const uint32_t *__restrict__ row_off, const uint32_t *__restrict__ row_rec,
                                               SegSel sel, int64_t rows_cap, RowOut out) {
