@@ -166,14 +166,16 @@ class _BatchOwner:
     """Keeps a finished sdl_batch alive while numpy views of its planes exist;
     the batch's pinned block returns to the handle's pool when the last view
     goes (sdl_batch_release)."""
-    __slots__ = ("b",)
+    __slots__ = ("b", "_release", "_byref")
 
     def __init__(self, b):
         self.b = b
+        self._release = native.load().sdl_batch_release  # bound now (teardown-safe)
+        self._byref = ctypes.byref
 
     def __del__(self):
         try:
-            native.load().sdl_batch_release(ctypes.byref(self.b))
+            self._release(self._byref(self.b))
         except Exception:  # interpreter shutdown
             pass
 
@@ -267,6 +269,8 @@ class _NativeBatcher(Batcher):
         native.check(L.sdl_batcher_create(ctypes.byref(c), tokenizer.path.encode(), native.DATA_DIR.encode(),
                                           ctypes.byref(h)))
         self._h = h
+        self._destroy = L.sdl_batcher_destroy  # bound now: close() may run at interpreter teardown
+        native.track(self)
         self.batch_config = batch_config
         self.dataset_config = dataset_config
 
@@ -278,7 +282,7 @@ class _NativeBatcher(Batcher):
 
     def close(self):
         if getattr(self, "_h", None):
-            native.load().sdl_batcher_destroy(self._h)
+            self._destroy(self._h)
             self._h = None
 
     __del__ = close

@@ -124,6 +124,17 @@ def build_stamps():
                  build_dir=os.path.join(REPO, "build", "stamps"))
 
 
+GZ256_LIB = os.path.join(REPO, "var", "gz256", "libsdl_batcher.so")
+
+
+def build_gz256():
+    """Diagnostic build whose inflate output batch (256 B) cannot hold a 258-byte match, the
+    r02 hang: the decoder must leave through its no-progress exit (GZ_E_STALL) instead ->
+    var/gz256/libsdl_batcher.so (tests/test_inflate_fuzz.py::test_device_no_progress_exit)."""
+    return build(defines=("SDL_GZ_OBUF=256", "SDL_GZ_ALLOW_SMALL_OBUF"), lib=GZ256_LIB,
+                 build_dir=os.path.join(REPO, "build", "var", "gz256", "obj"))
+
+
 def build_ablations(levels=(1, 2, 3)):
     """Diagnostic builds with phases of the tokenize kernel compiled out
     (SDL_ABLATE=1: first probes only; 2: no WordPiece; 3: load only) -> var/abl<N>/libsdl_batcher.so."""

@@ -152,10 +152,12 @@ class DeviceBatcher:
         native.check(L.sdl_batcher_create(ctypes.byref(c), tokenizer.encode(), native.DATA_DIR.encode(),
                                           ctypes.byref(h)))
         self._h = h
+        self._destroy = L.sdl_batcher_destroy  # bound now: close() may run at interpreter teardown
+        native.track(self)
 
     def close(self):
         if getattr(self, "_h", None):
-            native.load().sdl_batcher_destroy(self._h)
+            self._destroy(self._h)
             self._h = None
 
     __del__ = close

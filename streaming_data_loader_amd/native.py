@@ -3,8 +3,10 @@
 The product path is the HIP library only: if it is missing, or no GPU is
 visible, these calls raise -- there is no CPU fallback.
 """
+import atexit
 import ctypes
 import os
+import weakref
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SDL_LIB") or os.path.join(PKG, "libsdl_batcher.so")
@@ -111,6 +113,22 @@ class TokenizerInfo(ctypes.Structure):
 
 
 _lib = None
+_live_handles = weakref.WeakSet()
+
+
+def track(owner):
+    """Objects holding an sdl_batcher handle: closed by atexit while the HIP runtime and this
+    module are still alive (a __del__ at interpreter teardown would find both gone)."""
+    _live_handles.add(owner)
+
+
+@atexit.register
+def _close_live_handles():
+    for owner in list(_live_handles):
+        try:
+            owner.close()
+        except Exception:
+            pass
 
 
 def load(path=LIB_PATH):

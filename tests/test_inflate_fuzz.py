@@ -154,10 +154,11 @@ def test_device_fuzz_matches_oracle(torch, native_lib, records):
 def test_device_no_progress_exit(records):
     """SDL_GZ_OBUF=256 (var/gz256): an empty batch cannot take a 258-byte
     match, which hung the decoder before the no-progress exit existed."""
-    lib = os.path.join(REPO, "var", "gz256", "libsdl_batcher.so")
-    if not os.path.exists(lib):
-        pytest.skip("diagnostic build missing: python tools/build_variants.py "
-                    "gz256=SDL_GZ_OBUF=256,SDL_GZ_ALLOW_SMALL_OBUF")
+    from streaming_data_loader_amd import build
+    lib = build.GZ256_LIB
+    # __graft_entry__.build() makes it (build.build_gz256); it travels with the tree
+    assert build.embedded_id(lib) == build.source_hash(("SDL_GZ_OBUF=256", "SDL_GZ_ALLOW_SMALL_OBUF")), \
+        "var/gz256 diagnostic library missing or stale: run __graft_entry__.build()"
     code = ("import sys; sys.path[:0] = [%r, %r]; import torch, test_inflate as t;"
             "from streaming_data_loader_amd.device import DeviceBatcher;"
             "db = DeviceBatcher(batch_size=8, sequence_length=128);"
