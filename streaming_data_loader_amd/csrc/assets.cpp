@@ -635,9 +635,11 @@ static void load_unigram(const JValue &root, const std::string &data_dir, HostTo
     }
     t.unk_id = (int)unk->num;
     if (t.unk_id < 0 || (size_t)t.unk_id >= nv) throw std::runtime_error("Unigram: unk_id out of range");
-    // The kernels keep a candidate's score as the nearest f32 plus a 2-bit
-    // ulp correction (bits 28-29 of the device slot's id, sdl_batcher.cpp)
-    // that restores the exact f64.
+    // The kernels keep a candidate's score as the nearest f32; a piece whose f64 is one ulp
+    // off it is marked by bit 15 of its id in the device slot, the direction by the sign of
+    // the stored f32 (sdl_batcher.cpp, tokenize_unigram.hip uni_score64), which restores the
+    // exact f64. So such a piece needs an id < 32768 (t5-small: 32,100 pieces); a vocabulary
+    // with a marked piece above that is refused at create (INTEGRATION.md "Limits").
     // Scores written from sentencepiece's f32 (hub tokenizer.json: 17-digit
     // decimals) come back from serde_json's two-rounding parse (json.hpp) as
     // that f32 or one f64 ulp away from it; anything further is refused.

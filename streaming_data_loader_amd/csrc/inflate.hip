@@ -824,13 +824,10 @@ __global__ __launch_bounds__(64) void k_inflate_t(const uint8_t *__restrict__ in
     if constexpr (CH) {
         if (lane == 0) {
             const uint64_t at = 8 * sbase + bp;
-            if (!err && final_seen && !soft) {  // the final block ended here: the trailer's CRC
-                const uint64_t t = (at + 7) >> 3;
-                if (t + 8 > mz) err = GZ_E_TRUNC;
-                else
-                    ca.tcrc[0] = (uint32_t)in[t] | (uint32_t)in[t + 1] << 8 | (uint32_t)in[t + 2] << 16 |
-                                 (uint32_t)in[t + 3] << 24;
-            }
+            // the final block ended here; the host checks that the trailer follows it and the
+            // fold reads its CRC from the member's last 8 bytes (no word shared between chunks:
+            // a chunk decoding from a wrong header pick may also "see" a final block)
+            if (!err && final_seen && !soft && ((at + 7) >> 3) + 8 > mz) err = GZ_E_TRUNC;
             ca.status[c] = err;
             ca.len[c] = soft ? cut_prod : produced;
             ca.end_bit[c] = soft ? cut_bit : at;
@@ -1328,7 +1325,7 @@ __global__ __launch_bounds__(GZR_THREADS) void k_gz_resolve(const uint16_t *__re
 constexpr int GZF_THREADS = 256;
 __global__ __launch_bounds__(GZF_THREADS) void k_gz_crc_fold(const uint32_t *__restrict__ crc,
                                                             const uint32_t *__restrict__ shift, uint64_t n,
-                                                            const uint32_t *__restrict__ tcrc,
+                                                            const uint8_t *__restrict__ trailer,
                                                             const int32_t *__restrict__ status,
                                                             int32_t *__restrict__ mstatus) {
     __shared__ uint32_t s_c[GZF_THREADS], s_x[GZF_THREADS];
@@ -1351,7 +1348,9 @@ __global__ __launch_bounds__(GZF_THREADS) void k_gz_crc_fold(const uint32_t *__r
     }
     if (t == 0) {
         int32_t st = status[0];
-        if (st == GZ_OK && s_c[0] != tcrc[0]) st = GZ_E_CRC;
+        const uint32_t want = (uint32_t)trailer[0] | (uint32_t)trailer[1] << 8 | (uint32_t)trailer[2] << 16 |
+                              (uint32_t)trailer[3] << 24;
+        if (st == GZ_OK && s_c[0] != want) st = GZ_E_CRC;
         mstatus[0] = st | GZ_VERIFIED;
     }
 }
@@ -1392,9 +1391,9 @@ hipError_t launch_gz_resolve(const uint16_t *slots, uint32_t cap, const uint32_t
     return hipGetLastError();
 }
 
-hipError_t launch_gz_crc_fold(const uint32_t *crc, const uint32_t *shift, uint64_t n_order, const uint32_t *tcrc,
+hipError_t launch_gz_crc_fold(const uint32_t *crc, const uint32_t *shift, uint64_t n_order, const uint8_t *trailer,
                               const int32_t *status, int32_t *mstatus, hipStream_t st) {
-    hipLaunchKernelGGL(k_gz_crc_fold, dim3(1), dim3(GZF_THREADS), 0, st, crc, shift, n_order, tcrc, status, mstatus);
+    hipLaunchKernelGGL(k_gz_crc_fold, dim3(1), dim3(GZF_THREADS), 0, st, crc, shift, n_order, trailer, status, mstatus);
     return hipGetLastError();
 }
 

@@ -141,7 +141,6 @@ struct GzChunkArgs {
     uint32_t *len;              // out: values produced
     uint32_t *flags;            // out: GZC_*
     int32_t *status;            // out: GZ_*
-    uint32_t *tcrc;             // out: the trailer's CRC-32 (a chunk that reaches the final block)
 };
 // first dynamic-block header at or past nominal[c] (bits), searching `span` bits;
 // found[c] = its bit or GZ_NO_BIT
@@ -163,9 +162,9 @@ hipError_t launch_gz_windows(const uint16_t *slots, uint32_t cap, const uint32_t
 hipError_t launch_gz_resolve(const uint16_t *slots, uint32_t cap, const uint32_t *order, const uint32_t *len,
                              const uint64_t *pos, uint64_t n_order, const uint8_t *windows, uint8_t *out,
                              uint32_t *crc, uint32_t *shift, const X2N &x2n, int32_t *status, hipStream_t st);
-// the member's CRC-32 from the chunks' (crc, shift), checked against tcrc; writes
-// mstatus[0] = (status[0], or GZ_E_CRC) | GZ_VERIFIED
-hipError_t launch_gz_crc_fold(const uint32_t *crc, const uint32_t *shift, uint64_t n_order, const uint32_t *tcrc,
+// the member's CRC-32 from the chunks' (crc, shift), checked against the trailer's CRC-32 (the
+// 4 bytes at `trailer`, the member's end - 8); writes mstatus[0] = (status[0], or GZ_E_CRC) | GZ_VERIFIED
+hipError_t launch_gz_crc_fold(const uint32_t *crc, const uint32_t *shift, uint64_t n_order, const uint8_t *trailer,
                               const int32_t *status, int32_t *mstatus, hipStream_t st);
 
 // pipeline.hip

@@ -291,7 +291,7 @@ struct sdl_batcher {
     DevBuf<uint8_t> z_out;
     // ... large members in chunks (inflate_chunked)
     DevBuf<uint64_t> zc_nominal, zc_found, zc_start, zc_hdr, zc_end, zc_endhdr, zc_pos;
-    DevBuf<uint32_t> zc_list, zc_tgt, zc_next, zc_len, zc_flags, zc_order, zc_crc, zc_shift, zc_tcrc, zc_stats;
+    DevBuf<uint32_t> zc_list, zc_tgt, zc_next, zc_len, zc_flags, zc_order, zc_crc, zc_shift, zc_stats;
     DevBuf<int32_t> zc_status, zc_rstatus;
     DevBuf<uint16_t> zc_slots;
     DevBuf<uint8_t> zc_windows, zc_gwin;
@@ -1293,7 +1293,13 @@ void inflate_chunked(sdl_batcher *h, const uint8_t *d_gz, uint64_t m, uint64_t m
     while ((len + ch - 1) / ch > GZ_MAX_CHUNKS) ch *= 2;
     const uint64_t C0 = (len - 8 + ch - 1) / ch;  // nominal starts ma + c ch < mz - 8
     const uint64_t CT = C0 + GZ_EXTRA_CHUNKS;
-    const uint32_t cap = (uint32_t)(ch * GZ_SLOT_RATIO);
+    // 16-bit slot values per chunk: GZ_SLOT_RATIO x its compressed bytes, unless the member's
+    // slots together would exceed 8x its ISIZE in bytes (~4x the output per chunk on average);
+    // a chunk whose slot fills stops at a flush point and is resumed (GZC_SOFT)
+    uint64_t cap64 = ch * GZ_SLOT_RATIO;
+    const uint64_t slot_budget = std::max<uint64_t>(8ull * isize, 256ull << 20);
+    if (CT * cap64 * 2 > slot_budget) cap64 = std::max<uint64_t>(2 * ch, slot_budget / (2 * CT));
+    const uint32_t cap = (uint32_t)cap64;
     static const bool dbg = std::getenv("SDL_GZ_DEBUG") != nullptr;  // diagnostic: phase times to stderr
     auto now = [] { return std::chrono::steady_clock::now(); };
     auto ms_since = [&](std::chrono::steady_clock::time_point t) {
@@ -1301,6 +1307,7 @@ void inflate_chunked(sdl_batcher *h, const uint8_t *d_gz, uint64_t m, uint64_t m
     };
     const auto t_begin = now();
     int redos = 0;
+    try {  // device memory for the chunked path; without it the one-wave path decodes the member
     h->zc_nominal.ensure(CT);
     h->zc_found.ensure(CT);
     h->zc_start.ensure(CT);
@@ -1316,10 +1323,13 @@ void inflate_chunked(sdl_batcher *h, const uint8_t *d_gz, uint64_t m, uint64_t m
     h->zc_order.ensure(CT);
     h->zc_crc.ensure(CT);
     h->zc_shift.ensure(CT);
-    h->zc_tcrc.ensure(1);
     h->zc_status.ensure(CT);
     h->zc_rstatus.ensure(1);
     h->zc_slots.ensure((size_t)CT * cap);
+    } catch (const HipError &) {
+        (void)hipGetLastError();  // (clear the allocation failure so later launches do not report it)
+        return;
+    }
     std::vector<uint64_t> nominal(CT, GZ_NO_BIT), start(CT, GZ_NO_BIT), hdr(CT, GZ_NO_BIT), end(CT, 0),
         endhdr(CT, 0);
     std::vector<uint32_t> clen(CT, 0), flags(CT, 0), tgt(CT, 0), next(CT, ~0u);
@@ -1381,7 +1391,6 @@ void inflate_chunked(sdl_batcher *h, const uint8_t *d_gz, uint64_t m, uint64_t m
     a.len = h->zc_len.p;
     a.flags = h->zc_flags.p;
     a.status = h->zc_status.p;
-    a.tcrc = h->zc_tcrc.p;
     // (i) every chunk with a start, at once
     std::vector<uint32_t> list;
     for (uint64_t c = 0; c < C0; ++c)
@@ -1485,7 +1494,7 @@ void inflate_chunked(sdl_batcher *h, const uint8_t *d_gz, uint64_t m, uint64_t m
                               h->z_out.p + ooff_m, h->zc_crc.p, h->zc_shift.p, x2n, h->zc_rstatus.p, st));
     if (dbg) HIP_TRY(hipStreamSynchronize(st));
     const double t_res = ms_since(t_begin);
-    HIP_TRY(launch_gz_crc_fold(h->zc_crc.p, h->zc_shift.p, no, h->zc_tcrc.p, h->zc_rstatus.p, h->z_status.p + m, st));
+    HIP_TRY(launch_gz_crc_fold(h->zc_crc.p, h->zc_shift.p, no, d_gz + mz - 8, h->zc_rstatus.p, h->z_status.p + m, st));
     HIP_TRY(hipStreamSynchronize(st));  // (order / pos are host vectors)
     if (dbg) {
         int soft = 0;

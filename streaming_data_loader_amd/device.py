@@ -14,18 +14,22 @@ class _CudaView:
     """__cuda_array_interface__ (v3) of device memory the library owns: what
     torch.as_tensor / cupy / numba take without a copy."""
 
-    def __init__(self, ptr, shape, typestr):
+    def __init__(self, ptr, shape, typestr, stream=None):
         self.__cuda_array_interface__ = {"shape": tuple(shape), "typestr": typestr, "data": (int(ptr), False),
                                          "version": 3}
+        if stream:  # the producer's stream: the consumer orders its reads after it
+            self.__cuda_array_interface__["stream"] = int(stream)
 
 
 class DeviceResult:
-    def __init__(self, handle, rows_struct, n_records, S, B=None):
+    def __init__(self, handle, rows_struct, n_records, S, B=None, device=0, stream=0):
         self.h = handle
         self.r = rows_struct
         self.n_records = n_records
         self.S = S
         self.B = B
+        self.device = device
+        self.stream = stream  # the caller's stream the work was queued on (0: the handle's own)
 
     def rows(self):
         v = np.zeros(1, np.uint32)
@@ -81,16 +85,19 @@ class DeviceResult:
         task has them, labels: int32 [n, S], float32 [n, number_labels] for
         multi-label).  Views of the handle's buffers: valid until its next call."""
         import torch
-        n = self.rows() if n_rows is None else n_rows
+        # rows() synchronizes the handle's stream (work queued without a caller stream); work
+        # on a caller's stream is ordered through the interface's "stream" key instead
+        rows = self.rows()
+        n = rows if n_rows is None else n_rows
         S, LW = self.S, self.r.label_width
-        dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+        dev = device if device is not None else torch.device("cuda", self.device)
         out = {}
         for key, ptr, w, ts in (("input_ids", self.r.input_ids, S, "<i4"),
                                 ("attention_mask", self.r.attention_mask, S, "<i4"),
                                 ("token_type_ids", self.r.token_type_ids, S, "<i4"),
                                 ("labels", self.r.labels_f32 or self.r.labels, LW, "<f4" if self.r.labels_f32 else "<i4")):
             if ptr and n > 0:
-                out[key] = torch.as_tensor(_CudaView(ptr, (n, w), ts), device=dev)
+                out[key] = torch.as_tensor(_CudaView(ptr, (n, w), ts, self.stream), device=dev)
         return out
 
     def batches(self, n_rows=None, device=None):
@@ -177,7 +184,8 @@ class DeviceBatcher:
         native.check(native.load().sdl_process_device(self._h, ctypes.c_void_p(text_ptr), text_len,
                                                       ctypes.c_void_p(offsets_ptr), n_records, first_record,
                                                       ctypes.c_void_p(stream or None), ctypes.byref(out)))
-        return DeviceResult(self._h, out, n_records, self.cfg.sequence_length, self.cfg.batch_size)
+        return DeviceResult(self._h, out, n_records, self.cfg.sequence_length, self.cfg.batch_size, self.cfg.device,
+                            stream)
 
     def process_labels(self, text_ptr, text_len, offsets_ptr, n_records, labels_ptr, label_offsets_ptr,
                        first_record=0, stream=0):
@@ -187,7 +195,8 @@ class DeviceBatcher:
             self._h, ctypes.c_void_p(text_ptr), text_len, ctypes.c_void_p(offsets_ptr), n_records,
             ctypes.c_void_p(labels_ptr or None), ctypes.c_void_p(label_offsets_ptr or None), first_record,
             ctypes.c_void_p(stream or None), ctypes.byref(out)))
-        return DeviceResult(self._h, out, n_records, self.cfg.sequence_length, self.cfg.batch_size)
+        return DeviceResult(self._h, out, n_records, self.cfg.sequence_length, self.cfg.batch_size, self.cfg.device,
+                            stream)
 
     def json_text(self, jsonl_ptr, jsonl_len, stream=0):
         """The provider's JsonText filter on the device (sdl_json_text_device):

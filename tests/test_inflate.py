@@ -428,3 +428,50 @@ def test_device_chunked_member_errors(torch, native_lib, records):
             assert status[1] == want == ost, (name, status[1], ost)
     rc, out, status, got, _ = device_inflate(torch, db, [good])  # the handle stays usable
     assert rc == 0 and got[0] == lines
+
+
+def decoy_member(records):
+    """A >= 1 MiB member whose middle is a stored block full of complete final dynamic-Huffman
+    DEFLATE streams (the 'decoys'): a chunk whose header search lands in the stored bytes picks
+    a decoy and decodes a final block that is not the member's.  Raw DEFLATE is assembled by
+    hand: text (full flush, byte-aligned) + stored block of decoys + text (final)."""
+    lines = big_lines(records, 4, seed=5)
+    head, tail = lines[:3_000_000], lines[3_000_000:]
+    rng = random.Random(11)
+    decoys = []
+    while sum(map(len, decoys)) < 60_000:
+        text = bytes(rng.choice(b"abcdefghij klmnop,.\n") for _ in range(rng.randrange(600, 1400)))
+        d = zlib.compressobj(9, zlib.DEFLATED, -15)
+        raw = d.compress(text) + d.flush()
+        assert raw[0] & 7 == 0b101  # BFINAL 1, BTYPE 10 (dynamic)
+        decoys.append(raw)
+    payload = b"".join(decoys)[:65535]
+    a = zlib.compressobj(6, zlib.DEFLATED, -15)
+    deflate = a.compress(head) + a.flush(zlib.Z_FULL_FLUSH)  # ends byte-aligned, not final
+    n = len(payload)
+    deflate += bytes([0]) + n.to_bytes(2, "little") + (n ^ 0xFFFF).to_bytes(2, "little") + payload
+    c = zlib.compressobj(6, zlib.DEFLATED, -15)
+    deflate += c.compress(tail) + c.flush()
+    data = head + payload + tail
+    member = (b"\x1f\x8b\x08\x00\x00\x00\x00\x00\x00\x03" + deflate
+              + (zlib.crc32(data) & 0xFFFFFFFF).to_bytes(4, "little") + (len(data) & 0xFFFFFFFF).to_bytes(4, "little"))
+    assert len(member) >= 1 << 20 and zlib.decompress(member, 31) == data
+    return member, data
+
+
+def test_decoy_member_is_valid_gzip(records):
+    member, data = decoy_member(records)
+    assert oracle_lib.gz_inflate(member) == (0, data)
+
+
+@pytest.mark.gpu
+def test_device_chunked_member_with_decoy_final_blocks(torch, native_lib, records):
+    """chunks that start from a wrong header pick may decode a final block; the
+    trailer CRC must not come from whichever chunk wrote last.  Repeated to catch a race."""
+    from streaming_data_loader_amd.device import DeviceBatcher
+    db = DeviceBatcher(batch_size=8, sequence_length=128)
+    member, data = decoy_member(records)
+    for _ in range(6):
+        rc, out, status, got, _ = device_inflate(torch, db, [member])
+        assert rc == 0 and status[0] == 0, (rc, status[0])
+        assert got[0] == data
