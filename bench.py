@@ -76,20 +76,33 @@ def corpus_records(corpus="fixture"):
         return [json.loads(l)["text"] for l in f]
 
 
-def build_arena(records, nbytes, seed):
-    """Fixture records (data/test.json.gz) tiled in seeded permutations."""
-    blobs = [r.encode("utf-8") for r in records]
+def build_order(records, nbytes, seed):
+    """The record stream: fixture records (data/test.json.gz) tiled in seeded permutations
+    until nbytes of text (record indices into `records`)."""
+    lens = [len(r.encode("utf-8")) for r in records]
     rng = np.random.default_rng(seed)
     order, total = [], 0
     while total < nbytes:
-        for i in rng.permutation(len(blobs)):
+        for i in rng.permutation(len(records)):
             order.append(int(i))
-            total += len(blobs[i])
+            total += lens[i]
             if total >= nbytes:
                 break
+    return order
+
+
+def arena_of(records, order):
+    blobs = [r.encode("utf-8") for r in records]
     offs = np.zeros(len(order) + 1, np.uint64)
     np.cumsum(np.array([len(blobs[i]) for i in order], np.uint64), out=offs[1:])
     arena = np.concatenate([np.frombuffer(blobs[i], np.uint8) for i in order] + [np.zeros(16, np.uint8)])
+    return arena, offs
+
+
+def build_arena(records, nbytes, seed):
+    """Fixture records (data/test.json.gz) tiled in seeded permutations."""
+    order = build_order(records, nbytes, seed)
+    arena, offs = arena_of(records, order)
     return arena, offs, order
 
 
@@ -348,13 +361,22 @@ def rank_env():
             int(os.environ.get("LOCAL_RANK", "0")))
 
 
-def shard(rank, nbytes, corpus="fixture"):
-    """This rank's disjoint shard of the global record stream: its own seeded
-    arena of the corpus records and its global record indices (first_record),
-    so mask keys never collide across ranks."""
+def shard(rank, nbytes, corpus="fixture", world=1):
+    """This rank's shard of ONE global record stream (world x nbytes of the corpus records
+    tiled in seeded permutations): the product's byte-balanced contiguous split
+    (sdl_shard_records, host only), its records materialised, first_record = the global
+    index of its first record, so mask keys are those of the whole stream."""
+    from streaming_data_loader_amd import native
     records = corpus_records(corpus)
-    arena, offs, order = build_arena(records, nbytes, seed=0x5D1B + rank)
-    return records, arena, offs, order, rank * 10_000_000
+    order = build_order(records, world * nbytes, seed=0x5D1B)
+    lens = np.array([len(records[i].encode("utf-8")) for i in order], np.uint64)
+    goffs = np.zeros(len(order) + 1, np.uint64)
+    np.cumsum(lens, out=goffs[1:])
+    bounds = native.shard_records(goffs, world)
+    r0, r1 = int(bounds[rank]), int(bounds[rank + 1])
+    mine = order[r0:r1]
+    arena, offs = arena_of(records, mine)
+    return records, arena, offs, mine, r0
 
 
 def max_over_ranks(dt, world, device=None):
@@ -442,7 +464,7 @@ def dry_run(args, world, rank):
     import torch.distributed as dist
     if world > 1:
         dist.init_process_group("gloo", rank=rank, world_size=world)
-    records, arena, offs, order, first = shard(rank, args.arena_mib << 20, args.corpus)
+    records, arena, offs, order, first = shard(rank, args.arena_mib << 20, args.corpus, world)
     N, R = len(arena) - 16, len(order)
     sums = []
     if world > 1:
@@ -498,7 +520,7 @@ def main(argv=None):
 
     if not os.path.exists(build.LIB):
         build.build()
-    records, arena, offs, order, first_record = shard(rank, args.arena_mib << 20, args.corpus)
+    records, arena, offs, order, first_record = shard(rank, args.arena_mib << 20, args.corpus, world)
     N, R = len(arena) - 16, len(order)
     log(f"rank {rank}/{world}: task {args.task}, corpus {args.corpus}, arena {N} bytes, {R} records, "
         f"first record {first_record}")

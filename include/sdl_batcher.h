@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define SDL_ABI_VERSION 8
+#define SDL_ABI_VERSION 9
 
 enum {
     SDL_OK = 0,
@@ -276,6 +276,39 @@ typedef struct sdl_json_frames_stats {
 } sdl_json_frames_stats;
 int sdl_json_to_frames(sdl_batcher *h, const uint8_t *jsonl, uint64_t len, uint64_t chunk_bytes, int flush_partial,
                        sdl_frame_sink sink, void *user, sdl_json_frames_stats *stats);
+
+/* ---- Several GPUs, one record stream ---------------------------------------
+ * Records are independent (gen_batcher.rs:69-94 touches only the record's ids and
+ * the row cursor), so N Batchers on N contiguous record ranges emit what N
+ * reference Batchers (runner_simple.rs:68-112 runs one) would on those shards;
+ * masks are keyed by the global record index, so every row equals the row one
+ * handle would give over the whole stream.  No collective is involved.
+ *
+ * Host only: cut records [0, n_records) into n_shards contiguous ranges of about
+ * equal bytes -- bounds[k] = the first record starting at or past
+ * offsets[0] + k * (offsets[n_records] - offsets[0]) / n_shards, bounds[0] = 0,
+ * bounds[n_shards] = n_records (n_shards + 1 entries; a range may be empty). */
+int sdl_shard_records(const uint64_t *offsets, uint64_t n_records, uint32_t n_shards, uint64_t *bounds);
+
+typedef struct sdl_multi sdl_multi;
+/* One handle (own HIP stream) per entry of devices[0 .. n_devices), cfg->device
+ * ignored; a device may repeat.  cfg->first_record is the global index of the
+ * first record of the first push. */
+int sdl_multi_create(const sdl_config *cfg, const char *tokenizer_path, const char *data_dir,
+                     const int32_t *devices, uint32_t n_devices, sdl_multi **out);
+void sdl_multi_destroy(sdl_multi *m);
+/* sdl_batcher_push_many over one record stream: cut by sdl_shard_records into
+ * one shard per handle, every shard pushed into its handle on its own host thread
+ * (after hipSetDevice of its device; the calling thread runs shard 0 and is left on
+ * devices[0]), shard k's records keyed from the global index of its first record.
+ * n_emitted[k] (n_devices entries, may be NULL) = batches shard k queued; pop them
+ * with sdl_batcher_next / sdl_batcher_flush on sdl_multi_handle(m, k).  The global
+ * record index continues across calls. */
+int sdl_multi_push_many(sdl_multi *m, const uint8_t *arena, const uint64_t *offsets, size_t n_records,
+                        const uint32_t *labels, const uint64_t *label_offsets, size_t *n_emitted);
+/* Shard k's handle (also for sdl_process_device on a device-resident shard with
+ * first_record = its bound); NULL when k >= n_devices. */
+sdl_batcher *sdl_multi_handle(sdl_multi *m, uint32_t k);
 
 /* Copies `bytes` from device memory (e.g. sdl_device_rows planes) to host
  * memory with the handle's HIP runtime, ordered after the handle's work on

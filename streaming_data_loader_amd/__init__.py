@@ -6,7 +6,7 @@ kernels behind the C ABI in include/sdl_batcher.h (libsdl_batcher.so).  This
 package is the Python host mirror of the reference's Batcher interface.
 """
 from .batcher import (Batcher, BatchConfig, DataSet, GenTokenizer, Gpt, Label, Mask, ModelType,  # noqa: F401
-                      MultiLabel, ProviderChannel, SimpleBatcher, SimpleData, SimpleTransport, SingleClass, Span,
+                      MultiLabel, ProviderChannel, ShardedGenTokenizer, SimpleBatcher, SimpleData, SimpleTransport, SingleClass, Span,
                       TaskType,
                       TokenizerConfig, TrainingConfig, create_batch, create_batch_drained, get_case,
                       get_mask_length)

@@ -162,6 +162,31 @@ class DataSet:
         return {"input_ids": self.input_ids, "attention_mask": self.attention_mask, "labels": self.labels}
 
 
+def _native_config(batch_config, dataset_config, chunk, seed, device, first_record, rng_mode):
+    """sdl_config for a ModelType/DataSetConfig pair (config.rs:43-62) -> (config, batch kind)."""
+    if isinstance(dataset_config, Mask):
+        task, kind = native.SDL_TASK_MLM, "bert"
+    elif isinstance(dataset_config, Gpt):
+        task, kind = native.SDL_TASK_CLM, "gpt2"
+    elif isinstance(dataset_config, Span):
+        task, kind = native.SDL_TASK_SPAN, "t5"
+    elif isinstance(dataset_config, SingleClass):
+        task, kind = native.SDL_TASK_SINGLE_CLASS, "bert-single"
+    else:
+        task, kind = native.SDL_TASK_MULTI_LABEL, "bert"
+    c = native.default_config(task)
+    c.batch_size, c.sequence_length = batch_config.batch_size, batch_config.sequence_length
+    c.chunk = 1 if chunk else 0
+    if isinstance(dataset_config, Mask):
+        c.mask_length, c.mask_id = dataset_config.mask_length, dataset_config.mask
+    if isinstance(dataset_config, Span):
+        c.avg_span_gap, c.avg_span_size = dataset_config.avg_span_gap, dataset_config.avg_span_size
+    if isinstance(dataset_config, MultiLabel):
+        c.number_labels = dataset_config.number_labels
+    c.seed, c.device, c.first_record, c.rng_mode = seed, device, first_record, rng_mode
+    return c, kind
+
+
 class _BatchOwner:
     """Keeps a finished sdl_batch alive while numpy views of its planes exist;
     the batch's pinned block returns to the handle's pool when the last view
@@ -245,26 +270,7 @@ class _NativeBatcher(Batcher):
                  tokenizer: TokenizerConfig, chunk: bool = True, seed: int = 0, device: int = 0,
                  first_record: int = 0, rng_mode: int = 0):
         L = native.load()
-        if isinstance(dataset_config, Mask):
-            task, self.kind = native.SDL_TASK_MLM, "bert"
-        elif isinstance(dataset_config, Gpt):
-            task, self.kind = native.SDL_TASK_CLM, "gpt2"
-        elif isinstance(dataset_config, Span):
-            task, self.kind = native.SDL_TASK_SPAN, "t5"
-        elif isinstance(dataset_config, SingleClass):
-            task, self.kind = native.SDL_TASK_SINGLE_CLASS, "bert-single"
-        else:
-            task, self.kind = native.SDL_TASK_MULTI_LABEL, "bert"
-        c = native.default_config(task)
-        c.batch_size, c.sequence_length = batch_config.batch_size, batch_config.sequence_length
-        c.chunk = 1 if chunk else 0
-        if isinstance(dataset_config, Mask):
-            c.mask_length, c.mask_id = dataset_config.mask_length, dataset_config.mask
-        if isinstance(dataset_config, Span):
-            c.avg_span_gap, c.avg_span_size = dataset_config.avg_span_gap, dataset_config.avg_span_size
-        if isinstance(dataset_config, MultiLabel):
-            c.number_labels = dataset_config.number_labels
-        c.seed, c.device, c.first_record, c.rng_mode = seed, device, first_record, rng_mode
+        c, self.kind = _native_config(batch_config, dataset_config, chunk, seed, device, first_record, rng_mode)
         h = ctypes.c_void_p()
         native.check(L.sdl_batcher_create(ctypes.byref(c), tokenizer.path.encode(), native.DATA_DIR.encode(),
                                           ctypes.byref(h)))
@@ -473,3 +479,67 @@ def create_batch_drained(rx, tx, batcher: _NativeBatcher, max_bytes: int = 64 <<
                 tx.put(ProviderChannel.Data(cur))
             tx.put(ProviderChannel.Complete())
             break
+
+
+class ShardedGenTokenizer:
+    """One record stream over several GPUs (sdl_multi_*): every push is cut
+    into byte-balanced contiguous record ranges (sdl_shard_records), one per device; each
+    shard runs on its own handle, HIP stream and host thread, concurrently.  Shard k's
+    batches are those a GenTokenizer (gen_batcher.rs:65-98) over its record range emits, and
+    masks are keyed by the global record index, so every row equals the row one handle would
+    give over the whole stream -- N reference Batchers on disjoint shards, no collective.
+    `devices` may repeat a device (tests drive several shards on one GPU)."""
+
+    def __init__(self, model_type: ModelType, batch_config: BatchConfig, dataset_config: DataSetConfig,
+                 tokenizer: TokenizerConfig, devices, chunk: bool = True, seed: int = 0, first_record: int = 0,
+                 rng_mode: int = 0):
+        L = native.load()
+        c, self.kind = _native_config(batch_config, dataset_config, chunk, seed, 0, first_record, rng_mode)
+        devs = (ctypes.c_int32 * len(devices))(*devices)
+        m = ctypes.c_void_p()
+        native.check(L.sdl_multi_create(ctypes.byref(c), tokenizer.path.encode(), native.DATA_DIR.encode(), devs,
+                                        len(devices), ctypes.byref(m)))
+        self._m = m
+        self._destroy = L.sdl_multi_destroy
+        self.n = len(devices)
+        self.batch_config = batch_config
+        native.track(self)
+
+    def close(self):
+        if getattr(self, "_m", None):
+            self._destroy(self._m)
+            self._m = None
+
+    __del__ = close
+
+    def handle(self, k):
+        """Shard k's sdl_batcher handle (owned by this object)."""
+        return native.load().sdl_multi_handle(self._m, k)
+
+    def push_arena(self, arena, offsets):
+        """sdl_multi_push_many: returns, per shard, the batches it emitted (in order)."""
+        arena = np.ascontiguousarray(arena, np.uint8)
+        offsets = np.ascontiguousarray(offsets, np.uint64)
+        n = (ctypes.c_size_t * self.n)()
+        L = native.load()
+        native.check(L.sdl_multi_push_many(self._m, arena.ctypes.data, offsets.ctypes.data, offsets.size - 1,
+                                           None, None, n))
+        out = []
+        for k in range(self.n):
+            got, b, h = [], native.Batch(), self.handle(k)
+            while native.check(L.sdl_batcher_next(h, ctypes.byref(b))):
+                got.append(_dataset_from(b, self.kind))
+            out.append(got)
+        return out
+
+    def create_sync_batches(self, texts):
+        blobs = [t.encode("utf-8") if isinstance(t, str) else t for t in texts]
+        offs = np.zeros(len(blobs) + 1, np.uint64)
+        np.cumsum(np.fromiter(map(len, blobs), np.uint64, len(blobs)), out=offs[1:])
+        return self.push_arena(np.frombuffer(b"".join(blobs), np.uint8), offs)
+
+    def get_working_batch(self, k) -> Optional[DataSet]:
+        """Shard k's Batcher::get_working_batch (its flushed partial batch)."""
+        b = native.Batch()
+        got = native.check(native.load().sdl_batcher_flush(self.handle(k), ctypes.byref(b)))
+        return _dataset_from(b, self.kind) if got else None

@@ -520,11 +520,14 @@ __device__ __forceinline__ void store4(int32_t *p, int j0, int S, bool vec, int3
 #ifndef SDL_ROWS_WAVES4
 #define SDL_ROWS_WAVES4 1
 #endif
+#ifndef SDL_ROWS_WAVES_RM1
+#define SDL_ROWS_WAVES_RM1 7  // (r04: left to the compiler it took 103 VGPRs, 4 waves: rows 0.347 -> 0.274 ms)
+#endif
 // RM1: MLM under rng_mode 1 (mask bits from k_mask_rand).  A template flag, not
 // a runtime branch: the mask-word registers would cost the Philox path a wave
 // per SIMD (k_rows<2>: 80 -> 82 VGPRs, 6 -> 5 waves, 0.267 -> 0.295 ms).
 template <int MR, bool RM1>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MR >= 4 ? SDL_ROWS_WAVES4 : RM1 ? 1 : SDL_ROWS_WAVES, 8))) void k_rows(RowParams P, const uint32_t *__restrict__ tok,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MR >= 4 ? SDL_ROWS_WAVES4 : RM1 ? SDL_ROWS_WAVES_RM1 : SDL_ROWS_WAVES, 8))) void k_rows(RowParams P, const uint32_t *__restrict__ tok,
                                               const uint32_t *__restrict__ rec_tok, const uint32_t *__restrict__ rec_cnt,
                                               const uint32_t *__restrict__ row_off, const uint32_t *__restrict__ row_rec,
                                               SegSel sel, int64_t rows_cap, RowOut out) {
@@ -553,6 +556,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MR >= 4 ? S
         }
         const int64_t r = row_rec[g];
         const uint32_t k = (uint32_t)(g - row_off[r]);
+        const uint32_t *mb = RM1 ? P.mask_bits + g * (int64_t)((S + 31) >> 5) : nullptr;
         const uint32_t cnt = rec_cnt[r];
         const uint32_t t0 = rec_tok[r];
         const int64_t n = (int64_t)cnt + P.n_pre + P.n_post;
@@ -561,7 +565,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MR >= 4 ? S
         // (rng_mode 1) the row's mask words, loaded with the ids below: one memory round trip
         uint32_t mwd[MR];
         if (RM1) {
-            const uint32_t *mb = P.mask_bits + g * (int64_t)((S + 31) >> 5);
 #pragma unroll
             for (int m = 0; m < MR; ++m) {
                 const int j0 = 256 * m + 4 * lane;
@@ -709,80 +712,131 @@ __device__ __forceinline__ void chacha12_block(const uint32_t (&k)[8], uint32_t 
     o[12] = x12 + ctr; o[13] = x13; o[14] = x14; o[15] = x15;
 }
 
+// Phase A for one row per lane: the lane's row is (rec, chunk) when `active`; writes the swap
+// indices j_i, i = S-1 .. k, to jrow.  Every lane of the wave calls it (the block loop is
+// wave-uniform).
+__device__ __forceinline__ void rand_walk_lane(const RowParams &P, bool active, uint64_t rec, uint32_t chunk,
+                                               uint16_t *__restrict__ jrow) {
+    const int S = P.S, kmask = P.mask_length < S ? P.mask_length : S;
+    // only steps i >= k move values into or out of [0, k): the walk stops there
+    const int i0 = kmask > 1 ? kmask : 1;
+    int i = 0;
+    uint32_t key[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+    if (active) {
+        key[0] = (uint32_t)P.seed;
+        key[1] = (uint32_t)(P.seed >> 32);
+        key[2] = (uint32_t)rec;
+        key[3] = (uint32_t)(rec >> 32);
+        key[4] = chunk;
+        i = S - 1;
+    }
+    uint32_t n = (uint32_t)i + 1u, zone = (n << __builtin_clz(n)) - 1u;
+    // (S % 8 == 0) indices are collected eight at a time -- positions 8b .. 8b + 7, the
+    // walk runs downwards -- in a 128-bit shift register and stored as one 16-B store:
+    // a lane's own row, so each per-index 2-B store would touch its own line
+    const bool vec = (S & 7) == 0;
+    uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+    for (uint32_t blk = 0; __any(i >= i0); ++blk) {
+        uint32_t o[16];
+        chacha12_block(key, blk, o);
+        if (vec) {
+            // branch-free per word (selects, no exec-mask work on the one scalar unit per
+            // CU); only the store of a completed group of eight is predicated
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const uint64_t m = (uint64_t)o[q] * n;
+                const bool acc = i >= i0 && (uint32_t)m <= zone;
+                const uint32_t v = (uint32_t)(m >> 32);
+                a3 = acc ? (a3 << 16) | (a2 >> 16) : a3;
+                a2 = acc ? (a2 << 16) | (a1 >> 16) : a2;
+                a1 = acc ? (a1 << 16) | (a0 >> 16) : a1;
+                a0 = acc ? (a0 << 16) | v : a0;
+                if (acc && (i & 7) == 0)  // positions i .. i + 7 are complete
+                    *reinterpret_cast<uint4 *>(jrow + i) = make_uint4(a0, a1, a2, a3);
+                i -= acc ? 1 : 0;
+                n = (uint32_t)i + 1u;
+                zone = (n << __builtin_clz(n)) - 1u;
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const uint64_t m = (uint64_t)o[q] * n;
+                if (i >= i0 && (uint32_t)m <= zone) {
+                    jrow[i] = (uint16_t)(m >> 32);
+                    --i;
+                    n = (uint32_t)i + 1u;
+                    zone = (n << __builtin_clz(n)) - 1u;
+                }
+            }
+        }
+    }
+    if (vec && active && (i0 & 7) != 0) {  // the partial block [i0, (i0 | 7)]
+        const uint32_t w[4] = {a0, a1, a2, a3};
+        for (int p = i0; p <= (i0 | 7); ++p) {  // position p is the (p - i0)-th newest value
+            const int d = p - i0;
+            jrow[p] = (uint16_t)(w[d >> 1] >> (16 * (d & 1)));
+        }
+    }
+}
+
 // Phase A: one lane per row, 64 rows per wave
 template <int MR>
 __global__ __launch_bounds__(64) void k_mask_rand_walk(RowParams P, const uint32_t *__restrict__ row_off,
                                                        const uint32_t *__restrict__ row_rec, SegSel sel,
                                                        int64_t rows_cap, uint16_t *__restrict__ jbuf) {
     const int lane = lane_id();
-    const int S = P.S, kmask = P.mask_length < S ? P.mask_length : S;
-    // only steps i >= k move values into or out of [0, k): the walk stops there
-    const int i0 = kmask > 1 ? kmask : 1;
+    const int S = P.S;
     const RowSpan rs = row_span(sel, row_off, P.B, rows_cap);
     for (int64_t g0 = rs.g_lo + (int64_t)blockIdx.x * 64; g0 < (int64_t)rs.g_real; g0 += (int64_t)gridDim.x * 64) {
         const int64_t g = g0 + lane;
-        int i = 0;
-        uint32_t key[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
-        uint16_t *jrow = jbuf + (g < (int64_t)rs.g_real ? g : 0) * (int64_t)S;
-        if (g < (int64_t)rs.g_real) {
+        const bool active = g < (int64_t)rs.g_real;
+        uint64_t rec = 0;
+        uint32_t chunk = 0;
+        if (active) {
             const int64_t r = row_rec[g];
-            const uint32_t chunk = (uint32_t)(g - row_off[r]);
-            const uint64_t rec = P.first_record + (uint64_t)r;
-            key[0] = (uint32_t)P.seed;
-            key[1] = (uint32_t)(P.seed >> 32);
-            key[2] = (uint32_t)rec;
-            key[3] = (uint32_t)(rec >> 32);
-            key[4] = chunk;
-            i = S - 1;
+            chunk = (uint32_t)(g - row_off[r]);
+            rec = P.first_record + (uint64_t)r;
         }
-        uint32_t n = (uint32_t)i + 1u, zone = (n << __builtin_clz(n)) - 1u;
-        // (S % 8 == 0) indices are collected eight at a time -- positions 8b .. 8b + 7, the
-        // walk runs downwards -- in a 128-bit shift register and stored as one 16-B store:
-        // a lane's own row, so each per-index 2-B store would touch its own line
-        const bool vec = (S & 7) == 0;
-        uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
-        for (uint32_t blk = 0; __any(i >= i0); ++blk) {
-            uint32_t o[16];
-            chacha12_block(key, blk, o);
-            if (vec) {
-                // branch-free per word (selects, no exec-mask work on the one scalar unit per
-                // CU); only the store of a completed group of eight is predicated
-#pragma unroll
-                for (int q = 0; q < 16; ++q) {
-                    const uint64_t m = (uint64_t)o[q] * n;
-                    const bool acc = i >= i0 && (uint32_t)m <= zone;
-                    const uint32_t v = (uint32_t)(m >> 32);
-                    a3 = acc ? (a3 << 16) | (a2 >> 16) : a3;
-                    a2 = acc ? (a2 << 16) | (a1 >> 16) : a2;
-                    a1 = acc ? (a1 << 16) | (a0 >> 16) : a1;
-                    a0 = acc ? (a0 << 16) | v : a0;
-                    if (acc && (i & 7) == 0)  // positions i .. i + 7 are complete
-                        *reinterpret_cast<uint4 *>(jrow + i) = make_uint4(a0, a1, a2, a3);
-                    i -= acc ? 1 : 0;
-                    n = (uint32_t)i + 1u;
-                    zone = (n << __builtin_clz(n)) - 1u;
-                }
-            } else {
-#pragma unroll
-                for (int q = 0; q < 16; ++q) {
-                    const uint64_t m = (uint64_t)o[q] * n;
-                    if (i >= i0 && (uint32_t)m <= zone) {
-                        jrow[i] = (uint16_t)(m >> 32);
-                        --i;
-                        n = (uint32_t)i + 1u;
-                        zone = (n << __builtin_clz(n)) - 1u;
-                    }
-                }
-            }
-        }
-        if (vec && g < (int64_t)rs.g_real && (i0 & 7) != 0) {  // the partial block [i0, (i0 | 7)]
-            const uint32_t w[4] = {a0, a1, a2, a3};
-            for (int p = i0; p <= (i0 | 7); ++p) {  // position p is the (p - i0)-th newest value
-                const int d = p - i0;
-                jrow[p] = (uint16_t)(w[d >> 1] >> (16 * (d & 1)));
-            }
-        }
+        rand_walk_lane(P, active, rec, chunk, jbuf + (active ? g : 0) * (int64_t)S);
     }
+}
+
+// Phase B for one row, one wave: jr = the row's swap indices -> its mask bits
+template <int MR>
+__device__ __forceinline__ void rand_set_row(const RowParams &P, const uint16_t *__restrict__ jr,
+                                             uint32_t *__restrict__ bits_out, uint32_t *nx, uint32_t *bt, int lane) {
+    const int S = P.S, W = (S + 31) >> 5, kmask = P.mask_length < S ? P.mask_length : S;
+    const int i0 = kmask > 1 ? kmask : 1;
+    constexpr uint32_t NONE = 0xFFFFFFFFu;
+    auto wave_sync = [] {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    };
+    uint32_t jc[MR];
+#pragma unroll
+    for (int m = 0; m < MR; ++m) {
+        const int t = lane + 64 * m;
+        jc[m] = t >= i0 && t < S ? (uint32_t)jr[t] : (uint32_t)t;  // (t, t): no move
+    }
+#pragma unroll
+    for (int m = 0; m < MR; ++m) nx[lane + 64 * m] = NONE;
+    if (lane < 2 * MR) bt[lane] = 0u;
+    wave_sync();
+    // next(p): the latest swap into p among steps i >= k (a self swap moves nothing)
+#pragma unroll
+    for (int m = 0; m < MR; ++m)
+        if (jc[m] != (uint32_t)(lane + 64 * m)) atomicMin(&nx[jc[m]], (uint32_t)(lane + 64 * m));
+    wave_sync();
+    // [0, k) holds val(next(x)) (or x): follow each chain to its end
+    for (int x = lane; x < kmask; x += 64) {
+        uint32_t p = (uint32_t)x;
+        for (uint32_t q = nx[p]; q != NONE; q = nx[p]) p = q;
+        atomicOr(&bt[p >> 5], 1u << (p & 31));
+    }
+    wave_sync();
+    if (lane < W) bits_out[lane] = bt[lane];
+    wave_sync();
 }
 
 // Phase B: one wave per row (four rows per block, each wave on its own LDS); the
@@ -795,44 +849,10 @@ __global__ __launch_bounds__(256) void k_mask_rand_set(RowParams P, const uint32
     __shared__ uint32_t s_next[4][64 * MR];
     __shared__ uint32_t s_bits[4][2 * MR];
     const int lane = lane_id(), wv = (int)(threadIdx.x >> 6);
-    const int S = P.S, W = (S + 31) >> 5, kmask = P.mask_length < S ? P.mask_length : S;
-    const int i0 = kmask > 1 ? kmask : 1;
+    const int S = P.S, W = (S + 31) >> 5;
     const RowSpan rs = row_span(sel, row_off, P.B, rows_cap);
-    constexpr uint32_t NONE = 0xFFFFFFFFu;
-    uint32_t *nx = s_next[wv];
-    uint32_t *bt = s_bits[wv];
-    auto wave_sync = [] {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    };
-    for (int64_t h = rs.g_lo + (int64_t)blockIdx.x * 4 + wv; h < (int64_t)rs.g_real; h += (int64_t)gridDim.x * 4) {
-        const uint16_t *jr = jbuf + h * (int64_t)S;
-        uint32_t jc[MR];
-#pragma unroll
-        for (int m = 0; m < MR; ++m) {
-            const int t = lane + 64 * m;
-            jc[m] = t >= i0 && t < S ? (uint32_t)jr[t] : (uint32_t)t;  // (t, t): no move
-        }
-#pragma unroll
-        for (int m = 0; m < MR; ++m) nx[lane + 64 * m] = NONE;
-        if (lane < 2 * MR) bt[lane] = 0u;
-        wave_sync();
-        // next(p): the latest swap into p among steps i >= k (a self swap moves nothing)
-#pragma unroll
-        for (int m = 0; m < MR; ++m)
-            if (jc[m] != (uint32_t)(lane + 64 * m)) atomicMin(&nx[jc[m]], (uint32_t)(lane + 64 * m));
-        wave_sync();
-        // [0, k) holds val(next(x)) (or x): follow each chain to its end
-        for (int x = lane; x < kmask; x += 64) {
-            uint32_t p = (uint32_t)x;
-            for (uint32_t q = nx[p]; q != NONE; q = nx[p]) p = q;
-            atomicOr(&bt[p >> 5], 1u << (p & 31));
-        }
-        wave_sync();
-        if (lane < W) bits[h * (int64_t)W + lane] = bt[lane];
-        wave_sync();
-    }
+    for (int64_t h = rs.g_lo + (int64_t)blockIdx.x * 4 + wv; h < (int64_t)rs.g_real; h += (int64_t)gridDim.x * 4)
+        rand_set_row<MR>(P, jbuf + h * (int64_t)S, bits + h * (int64_t)W, s_next[wv], s_bits[wv], lane);
 }
 
 hipError_t launch_mask_rand(const RowParams &P, const uint32_t *row_off, const uint32_t *row_rec, SegSel sel,

@@ -329,6 +329,7 @@ struct sdl_batcher {
     uint32_t pin_u32_err = 0;
     uint32_t pin_u32_2[2] = {0, 0};
     uint64_t n_records = 0;
+    int64_t first_override = -1;  // sdl_multi: the global index of the next call's first record
 
     bool profiling = false;
     hipEvent_t ev[kStages + 1] = {};
@@ -598,7 +599,9 @@ struct sdl_batcher {
         h2d_off.ensure((size_t)R + 1);
         HIP_TRY(hipMemcpyAsync(h2d_text.p, pin_text.p, (size_t)N, hipMemcpyHostToDevice, stream));
         HIP_TRY(hipMemcpyAsync(h2d_off.p, pin_off.p, sizeof(uint64_t) * (size_t)(R + 1), hipMemcpyHostToDevice, stream));
-        run_device(h2d_text.p, N, h2d_off.p, R, cfg.first_record + n_records, stream, d_labels, d_label_off);
+        run_device(h2d_text.p, N, h2d_off.p, R,
+                   first_override >= 0 ? (uint64_t)first_override : cfg.first_record + n_records, stream, d_labels,
+                   d_label_off);
         hc.lap("enqueue");
         pin_u32.ensure((size_t)R + 3);
         HIP_TRY(hipMemcpyAsync(pin_u32.p, row_off.p, sizeof(uint32_t) * (size_t)(R + 1), hipMemcpyDeviceToHost, stream));
@@ -2056,3 +2059,92 @@ int sdl_stage_times(sdl_batcher *h, const char **names, float *ms, int cap) {
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------
+// Several GPUs, one record stream (the reference runs one Batcher task,
+// rust/src/tasks/runner_simple.rs:68-112): byte-balanced contiguous record ranges, one
+// handle + stream + host thread per device, masks keyed by the global record index.
+// ---------------------------------------------------------------------------
+int sdl_shard_records(const uint64_t *offsets, uint64_t n_records, uint32_t n_shards, uint64_t *bounds) {
+    if (!offsets || !bounds || n_shards == 0) return fail(SDL_ERR_ARG, "null argument or zero shards");
+    for (uint64_t r = 0; r < n_records; ++r)
+        if (offsets[r + 1] < offsets[r]) return fail(SDL_ERR_ARG, "offsets must be non-decreasing");
+    const uint64_t base = offsets[0], total = offsets[n_records] - base;
+    bounds[0] = 0;
+    for (uint32_t k = 1; k < n_shards; ++k) {
+        // the first record starting at or past k * total / n_shards
+        const unsigned __int128 t = (unsigned __int128)total * k / n_shards;
+        const uint64_t want = base + (uint64_t)t;
+        bounds[k] = (uint64_t)(std::lower_bound(offsets, offsets + n_records, want) - offsets);
+        if (bounds[k] < bounds[k - 1]) bounds[k] = bounds[k - 1];
+    }
+    bounds[n_shards] = n_records;
+    return SDL_OK;
+}
+
+struct sdl_multi {
+    std::vector<sdl_batcher *> h;
+    uint64_t next_record = 0;  // global index of the next call's first record
+    ~sdl_multi() {
+        for (sdl_batcher *x : h) sdl_batcher_destroy(x);
+    }
+};
+
+int sdl_multi_create(const sdl_config *cfg, const char *tokenizer_path, const char *data_dir, const int32_t *devices,
+                     uint32_t n_devices, sdl_multi **out) {
+    if (!cfg || !devices || !out || n_devices == 0) return fail(SDL_ERR_ARG, "null argument or no devices");
+    std::unique_ptr<sdl_multi> m(new sdl_multi());
+    m->next_record = cfg->first_record;
+    for (uint32_t k = 0; k < n_devices; ++k) {
+        sdl_config c = *cfg;
+        c.device = devices[k];
+        sdl_batcher *h = nullptr;
+        if (int rc = sdl_batcher_create(&c, tokenizer_path, data_dir, &h)) return rc;
+        m->h.push_back(h);
+    }
+    *out = m.release();
+    return SDL_OK;
+}
+
+void sdl_multi_destroy(sdl_multi *m) { delete m; }
+
+sdl_batcher *sdl_multi_handle(sdl_multi *m, uint32_t k) { return m && k < m->h.size() ? m->h[k] : nullptr; }
+
+int sdl_multi_push_many(sdl_multi *m, const uint8_t *arena, const uint64_t *offsets, size_t n_records,
+                        const uint32_t *labels, const uint64_t *label_offsets, size_t *n_emitted) {
+    if (!m || !offsets || (!arena && n_records && offsets[n_records])) return fail(SDL_ERR_ARG, "null argument");
+    if (offsets[0] != 0) return fail(SDL_ERR_ARG, "offsets must start at 0");
+    const uint32_t n = (uint32_t)m->h.size();
+    std::vector<uint64_t> bounds(n + 1);
+    if (int rc = sdl_shard_records(offsets, n_records, n, bounds.data())) return rc;
+    std::vector<int> rcs(n, SDL_OK);
+    std::vector<std::string> errs(n);
+    std::vector<size_t> emitted(n, 0);
+    auto run = [&](uint32_t k) {
+        const uint64_t r0 = bounds[k], r1 = bounds[k + 1];
+        sdl_batcher *h = m->h[k];
+        if (hipSetDevice(h->device) != hipSuccess) {
+            rcs[k] = SDL_ERR_HIP;
+            errs[k] = "hipSetDevice failed";
+            return;
+        }
+        std::vector<uint64_t> off(r1 - r0 + 1);
+        for (uint64_t r = r0; r <= r1; ++r) off[r - r0] = offsets[r] - offsets[r0];
+        h->first_override = (int64_t)(m->next_record + r0);
+        rcs[k] = sdl_batcher_push_many(h, arena ? arena + offsets[r0] : nullptr, off.data(), (size_t)(r1 - r0), labels,
+                                       label_offsets ? label_offsets + r0 : nullptr, &emitted[k]);
+        h->first_override = -1;
+        if (rcs[k] != SDL_OK) errs[k] = g_err;  // (the message is thread-local)
+        // the handle's own counter follows its records; the next call's shard starts are global
+    };
+    std::vector<std::thread> th;
+    for (uint32_t k = 1; k < n; ++k) th.emplace_back(run, k);
+    run(0);
+    for (auto &t : th) t.join();
+    for (uint32_t k = 0; k < n; ++k)
+        if (rcs[k] != SDL_OK) return fail(rcs[k], "shard " + std::to_string(k) + ": " + errs[k]);
+    m->next_record += n_records;
+    if (n_emitted)
+        for (uint32_t k = 0; k < n; ++k) n_emitted[k] = emitted[k];
+    return SDL_OK;
+}

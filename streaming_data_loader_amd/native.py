@@ -25,6 +25,7 @@ EXPORTS = [
     "sdl_process_device", "sdl_process_device_labels", "sdl_json_text_device", "sdl_pickle_frames_device", "sdl_device_to_host", "sdl_set_profiling", "sdl_stage_times",
     "sdl_tokenizer_info_get", "sdl_last_error", "sdl_abi_version", "sdl_json_to_frames",
     "sdl_gzip_inflate_device", "sdl_gzip_split_members", "sdl_build_id",
+    "sdl_shard_records", "sdl_multi_create", "sdl_multi_destroy", "sdl_multi_push_many", "sdl_multi_handle",
 ]
 
 
@@ -181,6 +182,17 @@ def load(path=LIB_PATH):
     L.sdl_gzip_inflate_device.restype = i64
     L.sdl_gzip_split_members.argtypes = [vp, u64, vp, u64, ctypes.POINTER(u64)]
     L.sdl_gzip_split_members.restype = i64
+    L.sdl_shard_records.argtypes = [vp, u64, ctypes.c_uint32, vp]
+    L.sdl_shard_records.restype = i64
+    L.sdl_multi_create.argtypes = [ctypes.POINTER(Config), ctypes.c_char_p, ctypes.c_char_p, vp, ctypes.c_uint32,
+                                   ctypes.POINTER(vp)]
+    L.sdl_multi_create.restype = i64
+    L.sdl_multi_destroy.argtypes = [vp]
+    L.sdl_multi_destroy.restype = None
+    L.sdl_multi_push_many.argtypes = [vp, vp, vp, sz, vp, vp, vp]
+    L.sdl_multi_push_many.restype = i64
+    L.sdl_multi_handle.argtypes = [vp, ctypes.c_uint32]
+    L.sdl_multi_handle.restype = vp
     L.sdl_set_profiling.argtypes = [vp, i64]
     L.sdl_stage_times.argtypes = [vp, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_float), i64]
     L.sdl_last_error.restype = ctypes.c_char_p
@@ -219,6 +231,16 @@ def default_config(task):
     c = Config()
     load().sdl_config_default(ctypes.byref(c), task)
     return c
+
+
+def shard_records(offsets, n_shards):
+    """sdl_shard_records (host only): record bounds (numpy u64 [n_shards + 1]) cutting the
+    stream described by `offsets` (u64 [n + 1]) into byte-balanced contiguous ranges."""
+    import numpy as np
+    off = np.ascontiguousarray(offsets, np.uint64)
+    bounds = np.zeros(int(n_shards) + 1, np.uint64)
+    check(load().sdl_shard_records(off.ctypes.data, len(off) - 1, int(n_shards), bounds.ctypes.data))
+    return bounds
 
 
 def gzip_split_members(buf):

@@ -26,7 +26,7 @@ def test_header_and_exports_agree(native_lib):
 
 
 def test_abi_version(native_lib):
-    assert native_lib.sdl_abi_version() == 8
+    assert native_lib.sdl_abi_version() == 9
 
 
 def test_config_defaults_mirror_masking_cases(native_lib):

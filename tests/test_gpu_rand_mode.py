@@ -47,3 +47,22 @@ def test_rand_mode_rejects_long_rows(native_lib):
         DeviceBatcher(batch_size=8, sequence_length=4096, rng_mode=1)
     with pytest.raises(native.SDLError):
         DeviceBatcher(batch_size=8, sequence_length=128, rng_mode=2)
+
+
+def test_rand_mode_dense_records_match_oracle(torch, native_lib, oracle_tok, records):
+    """Dense records (digit and punctuation runs, ~0.5 ids per byte: many chunks per record)
+    under rng_mode 1, against the oracle."""
+    rng = np.random.default_rng(77)
+    dense = [" ".join(str(int(x)) for x in rng.integers(0, 10, n)) + " , ." * (n // 7)
+             for n in (40, 300, 700, 1500, 3000)]
+    texts = [records[i] for i in rng.integers(0, len(records), 120)] + dense + [records[3]] + dense[::-1]
+    S, B, seed, first = 128, 8, 99, 5
+    k = int(np.float32(S) * np.float32(0.15))
+    db = DeviceBatcher(batch_size=B, sequence_length=S, seed=seed, rng_mode=1)
+    res = run_device(torch, db, texts, first_record=first)
+    G = res.rows()
+    got = res.planes(G)
+    want = oracle_lib.oracle_rows(oracle_tok, texts, S, k, 103, seed=seed, B=B, first_record=first, rng_mode=1)
+    assert want.shape[1] == G
+    for j in range(4):
+        np.testing.assert_array_equal(got[j], want[j])

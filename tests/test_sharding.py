@@ -1,7 +1,7 @@
 """The N>1 path of bench.py on the CPU (gloo, world_size 2): each rank owns a
-disjoint shard of the record stream (its own seeded arena, global record
-indices first_record = rank * 10^7), there is no data-path collective, and the
-harness only barriers and max-reduces the time.  Because mask keys depend on
+contiguous byte-balanced shard of one record stream (the product's
+sdl_shard_records; first_record = the global index of its first record), there
+is no data-path collective, and the harness only barriers and max-reduces the time.  Because mask keys depend on
 (seed, global record index, chunk) only, a shard's rows are the rows the whole
 stream would give those records: checked here with the CPU oracle (the GPU
 kernels are bit-exact to it, tests/test_gpu_*.py)."""
@@ -22,7 +22,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def shard_rows(rank, nbytes=48 << 10, S=128, B=8):
+def shard_rows(rank, nbytes=48 << 10, S=128, B=8, world=2):
     """What rank `rank` of bench.py computes, on the oracle: its arena, its
     global record indices, every row it yields."""
     import sys
@@ -31,7 +31,7 @@ def shard_rows(rank, nbytes=48 << 10, S=128, B=8):
     import bench
     import oracle_lib
     # bench.shard is the rank logic bench.py runs: this rank's arena and record indices
-    _, arena, offs, order, first = bench.shard(rank, nbytes)
+    _, arena, offs, order, first = bench.shard(rank, nbytes, world=world)
     texts = [bytes(arena[int(offs[i]):int(offs[i + 1])]) for i in range(len(order))]
     rows = oracle_lib.oracle_rows(oracle_lib.Tok(), texts, S, int(np.float32(S) * np.float32(0.15)), seed=1234, B=B,
                                   first_record=first)
@@ -67,7 +67,7 @@ def test_two_rank_shards_gloo():
         assert p.exitcode == 0
     assert tmax == 2.0  # max over ranks
     (f0, n0, g0, s0), (f1, n1, g1, s1) = meta
-    assert f1 >= f0 + n0  # disjoint global record indices
+    assert f0 == 0 and f1 == n0  # contiguous ranges of one stream
     assert g0 > 0 and g1 > 0
     # each shard's rows, recomputed in this process, match what the rank reported
     for r, (f, n, g, sm) in enumerate(meta):
@@ -120,8 +120,9 @@ def test_bench_gpus_flag_launches_ranks():
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["scaling"] == "weak"
     r0, r1 = d["ranks"]
-    assert (r0["first_record"], r1["first_record"]) == (0, 10_000_000)
-    assert r0["checksum"] != r1["checksum"]  # different seeded shards
+    assert (r0["first_record"], r1["first_record"]) == (0, r0["records"])  # one stream, cut in two
+    assert r0["checksum"] != r1["checksum"]  # different records
+    assert abs(r0["bytes"] - r1["bytes"]) < 20_000  # byte-balanced (within a record)
     total = r0["bytes"] + r1["bytes"]
     assert abs(d["value"] - d["config"]["arena_bytes_per_gpu"] * 2 / d["ms_per_step"] / 1e3) / d["value"] < 0.01
     assert total > 0
