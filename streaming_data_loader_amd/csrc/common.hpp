@@ -196,7 +196,7 @@ struct RowParams {
     uint64_t seed;
     uint64_t first_record;
     int32_t rng_mode;              // MLM masks: 0 Philox contract, 1 rand 0.8.5 StdRng (k_mask_rand)
-    const uint32_t *mask_bits;     // rng_mode 1: per row, ceil(S/32) words of mask bits
+    const uint16_t *mask_j;        // rng_mode 1: per row, S shuffle swap indices (k_mask_rand_walk)
     // span (T5Data): trunc(avg - z) draws as CDF tables (RNG contract) and
     // the <extra_id_k> ids (device pointer, 100 entries)
     int32_t gap_kmin, gap_n, size_kmin, size_n;

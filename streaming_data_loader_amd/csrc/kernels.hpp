@@ -235,7 +235,7 @@ hipError_t launch_rows(const RowParams &P, const uint32_t *tok, const uint32_t *
                        const uint32_t *row_off, const uint32_t *row_rec, SegSel sel, int64_t rows_cap, RowOut out,
                        hipStream_t st);
 hipError_t launch_mask_rand(const RowParams &P, const uint32_t *row_off, const uint32_t *row_rec, SegSel sel,
-                            int64_t rows_cap, uint16_t *jbuf, uint32_t *bits, hipStream_t st);
+                            int64_t rows_cap, uint16_t *jbuf, hipStream_t st);
 
 // BertData MultiLabel labels_f32 plane (bert_data.rs:66-78)
 hipError_t launch_multi_labels(const uint32_t *labels, const uint64_t *label_off, const uint32_t *row_rec,

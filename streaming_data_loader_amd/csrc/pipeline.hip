@@ -521,9 +521,12 @@ __device__ __forceinline__ void store4(int32_t *p, int j0, int S, bool vec, int3
 #define SDL_ROWS_WAVES4 1
 #endif
 #ifndef SDL_ROWS_WAVES_RM1
-#define SDL_ROWS_WAVES_RM1 7  // (r04: left to the compiler it took 103 VGPRs, 4 waves: rows 0.347 -> 0.274 ms)
+#define SDL_ROWS_WAVES_RM1 6  // (r04: left to the compiler, 103 VGPRs, 4 waves: rows 0.347 ms; 7 spills 20 B)
 #endif
-// RM1: MLM under rng_mode 1 (mask bits from k_mask_rand).  A template flag, not
+template <int MR>
+__device__ void rand_set_bits(const RowParams &P, const uint16_t *__restrict__ jr, uint32_t *nx, uint32_t *bt,
+                              int lane);
+// RM1: MLM under rng_mode 1 (mask bits from k_mask_rand_walk's swap indices, phase B fused).  A template flag, not
 // a runtime branch: the mask-word registers would cost the Philox path a wave
 // per SIMD (k_rows<2>: 80 -> 82 VGPRs, 6 -> 5 waves, 0.267 -> 0.295 ms).
 template <int MR, bool RM1>
@@ -538,6 +541,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MR >= 4 ? S
     const bool vec_lb = (P.label_width & 3) == 0;
     const RowSpan rs = row_span(sel, row_off, P.B, rows_cap);
     const int64_t G = rs.g_real;
+    // (rng_mode 1) phase B of the rand masks, fused: per wave, next() and the row's mask bits
+    __shared__ uint32_t s_nx[4][RM1 ? 256 * MR : 1];
+    __shared__ uint32_t s_bt[4][RM1 ? 8 * MR : 1];
     for (int64_t g = rs.g_lo + (int64_t)blockIdx.x * 4 + wid; g < rs.g_end; g += (int64_t)gridDim.x * 4) {
         int32_t *ids_o = out.input_ids + g * S;
         int32_t *am_o = out.attention_mask + g * S;
@@ -556,20 +562,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MR >= 4 ? S
         }
         const int64_t r = row_rec[g];
         const uint32_t k = (uint32_t)(g - row_off[r]);
-        const uint32_t *mb = RM1 ? P.mask_bits + g * (int64_t)((S + 31) >> 5) : nullptr;
         const uint32_t cnt = rec_cnt[r];
         const uint32_t t0 = rec_tok[r];
         const int64_t n = (int64_t)cnt + P.n_pre + P.n_post;
         const int64_t base = P.chunk ? (int64_t)k * S : 0;
         const int l = (int)((n - base) < S ? (n - base) : S);
-        // (rng_mode 1) the row's mask words, loaded with the ids below: one memory round trip
+        // (rng_mode 1) the row's mask words from its swap indices (k_mask_rand_walk)
         uint32_t mwd[MR];
         if (RM1) {
+            rand_set_bits<4 * MR>(P, P.mask_j + g * (int64_t)S, s_nx[wid], s_bt[wid], lane);
 #pragma unroll
             for (int m = 0; m < MR; ++m) {
                 const int j0 = 256 * m + 4 * lane;
-                mwd[m] = j0 < S ? mb[j0 >> 5] : 0u;
+                mwd[m] = j0 < S ? s_bt[wid][j0 >> 5] : 0u;
             }
+            __builtin_amdgcn_wave_barrier();  // (s_bt is rewritten by the wave's next row)
         }
 
         int32_t id[MR][4];
@@ -682,8 +689,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MR >= 4 ? S
 // rows per wave): the lane computes its ChaCha12 blocks in registers, 16 words
 // per block in an unrolled loop, and writes each swap index j_i to the row's
 // slice of `jbuf`; the walk stops after step k (steps k-1 .. 1 only permute
-// [0, k) among itself).  Phase B (k_mask_rand_set, its own launch so that every
-// row is a wave and the waves hide each other's LDS latency), a wave per row: mask_batch only uses the SET of the first k shuffled
+// [0, k) among itself).  Phase B (rand_set_bits, r04: fused into k_rows<MR, true>, which
+// takes a wave per row anyway -- its own launch plus a bits plane had cost 0.05 ms), a
+// wave per row: mask_batch only uses the SET of the first k shuffled
 // positions, and Fisher-Yates from the end never moves a value out of [0, k)
 // once steps i < k begin (j_i <= i), so the set is what [0, k) holds after steps
 // S-1 .. k.  The value at position p just before step p came from the latest
@@ -780,7 +788,6 @@ __device__ __forceinline__ void rand_walk_lane(const RowParams &P, bool active, 
 }
 
 // Phase A: one lane per row, 64 rows per wave
-template <int MR>
 __global__ __launch_bounds__(64) void k_mask_rand_walk(RowParams P, const uint32_t *__restrict__ row_off,
                                                        const uint32_t *__restrict__ row_rec, SegSel sel,
                                                        int64_t rows_cap, uint16_t *__restrict__ jbuf) {
@@ -801,11 +808,12 @@ __global__ __launch_bounds__(64) void k_mask_rand_walk(RowParams P, const uint32
     }
 }
 
-// Phase B for one row, one wave: jr = the row's swap indices -> its mask bits
+// Phase B for one row, one wave: jr = the row's swap indices -> its mask bits in bt
+// (ceil(S/32) words of the wave's LDS; nx: 64 * MR words, MR >= S / 64)
 template <int MR>
-__device__ __forceinline__ void rand_set_row(const RowParams &P, const uint16_t *__restrict__ jr,
-                                             uint32_t *__restrict__ bits_out, uint32_t *nx, uint32_t *bt, int lane) {
-    const int S = P.S, W = (S + 31) >> 5, kmask = P.mask_length < S ? P.mask_length : S;
+__device__ __forceinline__ void rand_set_bits(const RowParams &P, const uint16_t *__restrict__ jr, uint32_t *nx,
+                                              uint32_t *bt, int lane) {
+    const int S = P.S, kmask = P.mask_length < S ? P.mask_length : S;
     const int i0 = kmask > 1 ? kmask : 1;
     constexpr uint32_t NONE = 0xFFFFFFFFu;
     auto wave_sync = [] {
@@ -835,45 +843,16 @@ __device__ __forceinline__ void rand_set_row(const RowParams &P, const uint16_t 
         atomicOr(&bt[p >> 5], 1u << (p & 31));
     }
     wave_sync();
-    if (lane < W) bits_out[lane] = bt[lane];
-    wave_sync();
-}
-
-// Phase B: one wave per row (four rows per block, each wave on its own LDS); the
-// waves of a block run different row counts, so they meet only through wave
-// barriers
-template <int MR>
-__global__ __launch_bounds__(256) void k_mask_rand_set(RowParams P, const uint32_t *__restrict__ row_off,
-                                                      SegSel sel, int64_t rows_cap,
-                                                      const uint16_t *__restrict__ jbuf, uint32_t *__restrict__ bits) {
-    __shared__ uint32_t s_next[4][64 * MR];
-    __shared__ uint32_t s_bits[4][2 * MR];
-    const int lane = lane_id(), wv = (int)(threadIdx.x >> 6);
-    const int S = P.S, W = (S + 31) >> 5;
-    const RowSpan rs = row_span(sel, row_off, P.B, rows_cap);
-    for (int64_t h = rs.g_lo + (int64_t)blockIdx.x * 4 + wv; h < (int64_t)rs.g_real; h += (int64_t)gridDim.x * 4)
-        rand_set_row<MR>(P, jbuf + h * (int64_t)S, bits + h * (int64_t)W, s_next[wv], s_bits[wv], lane);
 }
 
 hipError_t launch_mask_rand(const RowParams &P, const uint32_t *row_off, const uint32_t *row_rec, SegSel sel,
-                            int64_t rows_cap, uint16_t *jbuf, uint32_t *bits, hipStream_t st) {
+                            int64_t rows_cap, uint16_t *jbuf, hipStream_t st) {
     if (rows_cap <= 0) return hipSuccess;
     if (P.S > RAND_MAX_S) return hipErrorInvalidValue;
     const int64_t want = (rows_cap + 63) / 64;
     const int64_t grid = want < 4096 ? want : 4096;
-    const int64_t want_b = (rows_cap + 3) / 4;
-    const int64_t grid_b = want_b < 32768 ? want_b : 32768;
-#define SDL_MASK_RAND(MR)                                                                                            \
-    do {                                                                                                             \
-        hipLaunchKernelGGL(k_mask_rand_walk<MR>, dim3((unsigned)grid), dim3(64), 0, st, P, row_off, row_rec, sel,   \
-                           rows_cap, jbuf);                                                                          \
-        hipLaunchKernelGGL(k_mask_rand_set<MR>, dim3((unsigned)grid_b), dim3(256), 0, st, P, row_off, sel, rows_cap, \
-                           (const uint16_t *)jbuf, bits);                                                            \
-    } while (0)
-    if (P.S <= 512) SDL_MASK_RAND(8);
-    else if (P.S <= 1024) SDL_MASK_RAND(16);
-    else SDL_MASK_RAND(RAND_MAX_S / 64);
-#undef SDL_MASK_RAND
+    hipLaunchKernelGGL(k_mask_rand_walk, dim3((unsigned)grid), dim3(64), 0, st, P, row_off, row_rec, sel, rows_cap,
+                       jbuf);
     return hipGetLastError();
 }
 
@@ -927,7 +906,7 @@ hipError_t launch_rows(const RowParams &P, const uint32_t *tok, const uint32_t *
     const int MR = (P.S + 255) / 256;
     if (P.label_width > 256 * MR) return hipErrorInvalidValue;
     const bool rm1 = P.task == 0 && P.rng_mode == 1;
-    if (rm1 && !P.mask_bits) return hipErrorInvalidValue;
+    if (rm1 && !P.mask_j) return hipErrorInvalidValue;
 #define SDL_ROWS(MM)                                                                                                 \
     if (rm1)                                                                                                          \
         hipLaunchKernelGGL((k_rows<MM, true>), dim3(grid), dim3(256), 0, st, P, tok, rec_tok, rec_cnt, row_off,      \

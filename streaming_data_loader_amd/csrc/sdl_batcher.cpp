@@ -269,7 +269,6 @@ struct sdl_batcher {
     DevBuf<uint32_t> ranges, tokc, chunk_cnt, chunk_off, rec_local, tok_ids, rec_tok, rec_cnt, rec_rows, row_off,
         row_rec, scan_tmp;
     DevBuf<int32_t> o_ids, o_am, o_tt, o_lab;
-    DevBuf<uint32_t> mask_bits;  // rng_mode 1: per-row mask bits (k_mask_rand)
     DevBuf<uint16_t> mask_j;     // rng_mode 1: per-row shuffle swap indices (k_mask_rand phase A)
     DevBuf<float> o_f32;
     DevBuf<uint32_t> lab_err;
@@ -427,13 +426,12 @@ struct sdl_batcher {
         row_rec.ensure((size_t)std::max<int64_t>(rows_cap, 1));
         if (P.task == SDL_TASK_MLM && P.rng_mode == 1)
         {
-            mask_bits.ensure((size_t)std::max<int64_t>(rows_cap, 1) * (size_t)((P.S + 31) / 32));
             mask_j.ensure((size_t)std::max<int64_t>(rows_cap, 1) * (size_t)P.S);
         }
 
         RowParams p = P;
         p.first_record = first_record;
-        p.mask_bits = mask_bits.p;
+        p.mask_j = mask_j.p;
         const bool bpe = dt.kind == TOK_BYTE_BPE;
         const bool uni = dt.kind == TOK_UNIGRAM;
         // Pipelined segments (WordPiece): the tokenize launches of the chunk
@@ -494,7 +492,7 @@ struct sdl_batcher {
                                          span_err.p, s));
             } else {
                 if (p.task == SDL_TASK_MLM && p.rng_mode == 1)
-                    HIP_TRY(launch_mask_rand(p, row_off.p, row_rec.p, sel, rows_cap, mask_j.p, mask_bits.p, s));
+                    HIP_TRY(launch_mask_rand(p, row_off.p, row_rec.p, sel, rows_cap, mask_j.p, s));
                 HIP_TRY(launch_rows(p, tok_ids.p, rec_tok.p, rec_cnt.p, row_off.p, row_rec.p, sel, rows_cap, out, s));
             }
             if (multi())
