@@ -29,6 +29,8 @@
 //      for rank-monotone merges (checked on the host);
 //   5. longer pieces (or pieces running past the window) are appended to a
 //      global list and finished by k_bpe_long; the chunk list holds a marker.
+#include <algorithm>
+
 #include "common.hpp"
 #include "device_util.hpp"
 #include "kernels.hpp"
@@ -736,12 +738,20 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
 // each, symbols in `scratch` at the piece's own byte positions (u16), the same
 // merge steps as bpe_wave in 64-symbol tiles.  The ids stay in `scratch`;
 // the chunk's count and the local offsets of its later records grow by k - 1.
+// (r04) A piece of <= LONG_LDS symbols runs in LDS with every pair's merge value cached: a merge
+// step reads the cached ranks for its minimum and its candidates, carries the values of pairs no
+// merge touched through the compaction, and probes the merge table only for the pairs next to a
+// merged symbol -- O(merges) probes per step instead of O(symbols) twice.  Longer pieces use the
+// global scratch as before.
+constexpr int LONG_LDS = 1024;
 __global__ __launch_bounds__(64) void k_bpe_long(DevTok T, const uint8_t *__restrict__ text, int64_t N,
                                                  const uint64_t *__restrict__ off, int64_t R,
                                                  const uint32_t *__restrict__ long_count, BpeLong *__restrict__ list,
                                                  uint32_t long_cap, uint16_t *__restrict__ scratch,
                                                  uint32_t *__restrict__ chunk_cnt, uint32_t *__restrict__ rec_local,
                                                  uint32_t *__restrict__ err) {
+    __shared__ uint16_t s_sym[LONG_LDS + 64];
+    __shared__ uint32_t s_val[LONG_LDS + 64];  // merge_val of pair (j, j + 1); NOVAL: not known
     __shared__ uint16_t s_byte_id[256];
     for (int i = threadIdx.x; i < 256; i += 64) s_byte_id[i] = T.byte_id[i];
     __syncthreads();
@@ -764,10 +774,80 @@ __global__ __launch_bounds__(64) void k_bpe_long(DevTok T, const uint8_t *__rest
         }
         const int64_t rec = lo;
         if (n == 0) n = bpe_piece_end(C, p) - p;  // ran past its chunk's window
+        int64_t m = n;
+        if (n <= LONG_LDS) {
+            // not known: merged / right neighbour changed (NOVAL), left neighbour of a merge (NOVAL2);
+            // merge_val's "no merge" is 0xFFFFFFFF, its ranks stay below 0xFFFD
+            constexpr uint32_t NOVAL = 0xFFFFFFFEu, NOVAL2 = 0xFFFFFFFDu;
+            const int nn = (int)n;
+            for (int j = lane; j < nn; j += 64) s_sym[j] = s_byte_id[text[p + j]];
+            __syncthreads();
+            for (int j = lane; j + 1 < nn; j += 64) s_val[j] = merge_val(T, s_sym[j], s_sym[j + 1]);
+            __syncthreads();
+            int mm = nn;
+            for (;;) {
+                uint32_t rmin = 0xFFFFu;
+                for (int j = lane; j + 1 < mm; j += 64) {
+                    const uint32_t r = s_val[j] >> 16;
+                    rmin = r < rmin ? r : rmin;
+                }
+                rmin = wave_min_u32(rmin);
+                if (rmin == 0xFFFFu) break;
+                // merge its occurrences left to right, compact in place; a kept symbol keeps its
+                // pair's value when neither it nor its right neighbour changes
+                bool blocked = false;
+                int outp = 0;
+                for (int t0 = 0; t0 < mm; t0 += 64) {
+                    const int j = t0 + lane;
+                    const uint32_t sym = j < mm ? s_sym[j] : 0u;
+                    const uint32_t v = j + 1 < mm ? s_val[j] : 0xFFFFFFFFu;
+                    const uint64_t cand = __ballot(j + 1 < mm && (v >> 16) == rmin);
+                    const uint64_t sel = leftmost_alternating(cand, blocked);
+                    const uint64_t tile = (mm - t0 >= 64) ? ~0ull : ((1ull << (mm - t0)) - 1ull);
+                    uint64_t live = tile & ~(sel << 1);
+                    if (blocked) live &= ~1ull;
+                    const bool me = (sel >> lane) & 1ull;
+                    // the right neighbour of a kept symbol changes when it is merged away (my
+                    // pair selected) or merges with its own right neighbour (lane + 1 selected)
+                    const bool next_sel = lane < 63 ? ((sel >> (lane + 1)) & 1ull) : false;
+                    const uint32_t out = me ? (v & 0xFFFFu) : sym;
+                    const uint32_t outv = (me || next_sel) ? NOVAL : v;
+                    __syncthreads();  // every lane has read its tile before any lane writes
+                    if ((live >> lane) & 1ull) {
+                        const int o = outp + __popcll(live & lt);
+                        s_sym[o] = (uint16_t)out;
+                        s_val[o] = outv;
+                    }
+                    __syncthreads();
+                    outp += __popcll(live);
+                    blocked = (sel >> 63) & 1ull;
+                }
+                // (a tile's last kept symbol whose neighbour sat in the next tile, and a merge
+                // reaching across a tile edge, leave the value at NOVAL through next_sel / me; a
+                // symbol whose left neighbour merged keeps its own pair, which is unchanged)
+                mm = outp;
+                // the left neighbour of a merged symbol: its pair changed too (the tile's last
+                // kept symbol cannot see a merge at the next tile's first pair); runs before the
+                // last symbol's value is cleared, which may be the merged one
+                for (int j = lane; j + 1 < mm; j += 64) {
+                    const uint32_t nx = s_val[j + 1], cur = s_val[j];
+                    if (nx == NOVAL && cur != NOVAL && cur != NOVAL2) s_val[j] = NOVAL2;
+                }
+                __syncthreads();
+                if (mm > 0 && lane == 0) s_val[mm - 1] = 0xFFFFFFFFu;  // (no pair past the end)
+                __syncthreads();
+                for (int j = lane; j + 1 < mm; j += 64) {
+                    const uint32_t cur = s_val[j];
+                    if (cur == NOVAL || cur == NOVAL2) s_val[j] = merge_val(T, s_sym[j], s_sym[j + 1]);
+                }
+                __syncthreads();
+            }
+            for (int j = lane; j < mm; j += 64) scratch[p + j] = s_sym[j];
+            m = mm;
+        } else {
         // initial symbols
         for (int64_t j = lane; j < n; j += 64) scratch[p + j] = s_byte_id[text[p + j]];
         __syncthreads();
-        int64_t m = n;
         for (;;) {
             // pass 1: lowest rank over all adjacent pairs
             uint32_t rmin = 0xFFFFu;
@@ -802,6 +882,7 @@ __global__ __launch_bounds__(64) void k_bpe_long(DevTok T, const uint8_t *__rest
             m = outp;
             __syncthreads();
         }
+        }
         if (lane == 0) {
             list[li].k = (uint32_t)m;
             list[li].len = (uint32_t)n;
@@ -829,8 +910,16 @@ hipError_t launch_bpe_chunks(const DevTok &T, const uint8_t *text, int64_t N, co
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_bpe_chunks, dim3((unsigned)n_chunks), dim3(TOK_THREADS), 0, st, T, text, N, off, R, ranges,
                        tokc, chunk_cnt, chunk_ent, rec_local, long_count, long_list, long_cap);
-    hipLaunchKernelGGL(k_bpe_long, dim3(1024), dim3(64), 0, st, T, text, N, off, R, long_count, long_list, long_cap,
-                       scratch, chunk_cnt, rec_local, err);
+    // one wave per long piece: the merges of one piece are a dependent chain of L2 round trips,
+    // so the pieces in flight are what it runs on (r04: 1024 waves, one per SIMD, was 1.70 ms on
+    // the held-out corpus); a block finds no piece and exits at once when there are fewer
+#ifndef SDL_BPE_LONG_GRID
+#define SDL_BPE_LONG_GRID 8192
+#endif
+    const int64_t grid = std::min<int64_t>((int64_t)long_cap, SDL_BPE_LONG_GRID);
+    if (grid > 0)
+        hipLaunchKernelGGL(k_bpe_long, dim3((unsigned)grid), dim3(64), 0, st, T, text, N, off, R, long_count, long_list,
+                           long_cap, scratch, chunk_cnt, rec_local, err);
     return hipGetLastError();
 }
 
