@@ -253,15 +253,57 @@ def load_pmc(task, arena_mib, kernel, corpus="fixture"):
         return None, f"{os.path.relpath(p, REPO)}: {e}"
 
 
-def pmc_roofline(pmc, launch_ms, alg_bytes):
-    """traffic = HBM bytes per launch (2 x FETCH_SIZE gfx950 correction +
-    WRITE_SIZE, MI355X_MICROARCH.md §HBM); issue = VALU and SALU wave-
+def stream_calibration():
+    """What FETCH_SIZE reports for the chunk kernels' text + offsets stream alone, per byte of
+    it: the load-only WordPiece build (SDL_ABLATE=3: stage the 1,088-byte windows, tokenize
+    nothing) over the fixture 256 MiB arena (tools/gpu_pmc_load.sh, tools/pmc_calibration.py
+    -> profiles/pmc/stream_calibration.json).  None if absent."""
+    p = os.path.join(REPO, "profiles", "pmc", "stream_calibration.json")
+    try:
+        with open(p) as f:
+            return json.load(f)
+    except (OSError, ValueError):
+        return None
+
+
+def pmc_traffic(pmc, stream_bytes):
+    """HBM bytes per launch from FETCH_SIZE / WRITE_SIZE (KiB units), split by source.
+
+    The guide's gfx950 correction (MI355X_MICROARCH.md §HBM: FETCH_SIZE reports half the bytes
+    of a 16 B/lane streaming read) does not describe these kernels' reads as a whole: the
+    load-only build measures FETCH_SIZE = 0.70 x the stream's bytes (the 1 KiB lane loads
+    under-reported, the 32-byte halo loads and offsets not), so a uniform x2 states the stream
+    at 1.4x its size.  The stream is therefore counted as its own bytes (`stream_bytes`, text +
+    offsets, read once), the calibrated share of FETCH_SIZE (ratio x stream_bytes) is taken
+    out, and the rest of FETCH_SIZE -- vocabulary / merge-table probes, list reads, scattered
+    4-64 B accesses the x2 does not apply to -- is added as reported, with WRITE_SIZE.  The
+    split also keeps the uniform-x2 figure as an upper bound."""
+    c = pmc["counters"]
+    if "FETCH_SIZE" not in c or "WRITE_SIZE" not in c:
+        return pmc.get("hbm_bytes_per_launch"), None
+    fetch, write = c["FETCH_SIZE"] * 1024, c["WRITE_SIZE"] * 1024
+    cal = stream_calibration()
+    ratio = cal["ratio"] if cal else 0.5
+    other = max(fetch - ratio * stream_bytes, 0.0)
+    traffic = int(stream_bytes + other + write)
+    split = {"stream_read": int(stream_bytes), "probe_and_list_read": int(other), "write": int(write),
+             "fetch_size_reported": int(fetch), "stream_fetch_ratio": round(ratio, 4),
+             "stream_fetch_ratio_from": "load-only build FETCH_SIZE (profiles/pmc/stream_calibration.json)"
+             if cal else "guide's 1/2 (no calibration file)",
+             "uniform_x2_upper_bound": int(2 * fetch + write)}
+    return traffic, split
+
+
+def pmc_roofline(pmc, launch_ms, alg_bytes, stream_bytes=0):
+    """traffic = HBM bytes per launch (pmc_traffic: FETCH_SIZE with the gfx950 x2 applied to the
+    streamed text only, + WRITE_SIZE); issue = VALU and SALU wave-
     instructions per launch over this run's HIP-event launch time against
     their issue peaks (the byte-walking kernels are bound by the scalar unit:
     one per CU, shared by its four SIMDs); `bound` names the busier one.
     A figure that cannot describe the timed launch (issue above its peak) is
     dropped with the reason."""
-    traffic = pmc.get("hbm_bytes_per_launch")
+    traffic, split = pmc_traffic(pmc, stream_bytes)
+    pmc["_split"] = split
     c = pmc["counters"]
     valu, salu = c.get("SQ_INSTS_VALU"), c.get("SQ_INSTS_SALU")
     issue, note = None, None
@@ -605,7 +647,7 @@ def main(argv=None):
     pmc, pmc_note = load_pmc(args.task, args.arena_mib, task["kernel"], args.corpus)
     traffic, issue = None, None
     if pmc is not None:
-        traffic, issue, pmc_note = pmc_roofline(pmc, tok_ms, tok_bytes)
+        traffic, issue, pmc_note = pmc_roofline(pmc, tok_ms, tok_bytes, stream_bytes=N + 8 * (R + 1))
     # achieved / peak / frac are against HBM (the metric's roofline); `bound`
     # names the roofline that binds the kernel: the busier issue unit when the
     # PMC summary shows it closer to its peak than HBM traffic is to its own
@@ -616,6 +658,7 @@ def main(argv=None):
     line["roofline"] = {"bound": bound, "kernel": task["kernel"], "achieved": round(achieved, 2),
                         "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(hbm_frac, 5),
                         "traffic": traffic, "issue": issue,
+                        "traffic_split": pmc.get("_split") if pmc is not None else None,
                         "algorithmic_bytes_per_launch": tok_bytes, "avg_launch_ms": round(tok_ms, 4)}
     if bound != "hbm":
         line["roofline"]["bound_note"] = (f"{bound} at {issue['frac']:.2f} of its issue peak binds this kernel; "

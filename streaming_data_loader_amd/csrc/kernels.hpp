@@ -10,7 +10,9 @@
 namespace sdl {
 
 // pipeline.hip: per chunk, the record ranges touching its window (3 words per chunk)
-hipError_t launch_chunk_ranges(const uint64_t *off, int64_t R, int64_t N, uint32_t *ranges, hipStream_t st);
+// (rb1: also write the one-segment record bounds {0, R} there; zero1: a word to zero)
+hipError_t launch_chunk_ranges(const uint64_t *off, int64_t R, int64_t N, uint32_t *ranges, hipStream_t st,
+                               uint32_t *rb1 = nullptr, uint32_t *zero1 = nullptr);
 
 // tokenize_wordpiece.hip: text arena -> per-chunk token lists + boundary offsets
 // (after launch_chunk_ranges), for chunks [c_begin, c_end) (c_end < 0: all).
@@ -216,6 +218,23 @@ struct RowOut {
     float *labels_f32;
 };
 
+// Small calls: chunk scan + compaction + records + row scan + row map in one
+// single-workgroup launch (one segment, n_chunks <= SMALL_CHUNKS, R <= 8192).
+constexpr int64_t SMALL_CHUNKS = 64;
+struct SmallDown {
+    const uint32_t *tokc, *chunk_cnt;
+    uint32_t *chunk_off, *tok;
+    const uint32_t *long_count, *chunk_ent;
+    const BpeLong *long_list;
+    const uint16_t *long_scratch;
+    const uint32_t *long_pool;
+    int64_t stride;
+    const uint32_t *rec_local;
+    uint32_t *rec_tok, *rec_cnt, *rec_rows, *row_off, *row_rec;
+};
+hipError_t launch_downstream_small(const SmallDown &d, const RowParams &P, const uint64_t *off, int64_t R, int64_t N,
+                                   hipStream_t st);
+
 // row -> record map (row_rec needs one word per row)
 hipError_t launch_row_map(const uint32_t *row_off, int64_t R, uint32_t *row_rec, SegSel sel, hipStream_t st);
 
@@ -231,6 +250,18 @@ hipError_t launch_rows_to_host(const RowSeg *segs, int n_segs, uint32_t rows_per
                                const int32_t *am, const int32_t *tt, const int32_t *lab, int S, int LW,
                                hipStream_t st);
 
+// Small pushes, no second round trip: global row g of the call goes to slot
+// base + g of the back batch (slots >= B: the next, pre-allocated one), rows
+// g < cap only; the same launch writes row_off[0..R] and the two error words to
+// `stat` (mapped pinned host memory) so the host needs no D2H copy.
+struct DirectDst {
+    int32_t *ids[2], *am[2], *tt[2], *lab[2];  // back batch, next batch (device-mapped host)
+    uint32_t base, cap, B, pad;
+};
+hipError_t launch_rows_direct(const DirectDst &d, const uint32_t *row_off, int64_t R, const int32_t *ids,
+                              const int32_t *am, const int32_t *tt, const int32_t *lab, int S, int LW,
+                              const uint32_t *err0, const uint32_t *err1, uint32_t *stat, hipStream_t st);
+
 hipError_t launch_rows(const RowParams &P, const uint32_t *tok, const uint32_t *rec_tok, const uint32_t *rec_cnt,
                        const uint32_t *row_off, const uint32_t *row_rec, SegSel sel, int64_t rows_cap, RowOut out,
                        hipStream_t st);
@@ -242,10 +273,19 @@ hipError_t launch_multi_labels(const uint32_t *labels, const uint64_t *label_off
                                const uint32_t *row_off, SegSel sel, int64_t rows_cap, int B, int NL, float *out,
                                uint32_t *err, hipStream_t st);
 
-// T5Data::put_data rows for task=span (models/t5_data.rs:162-226)
+// T5Data::put_data rows for task=span (models/t5_data.rs:162-226).  With a
+// plan (pipeline.hip "Span rows in two phases"): rows_cap x capr entries,
+// rows_cap meta words, an overflow row list of rows_cap entries and its count;
+// without one, the one-pass kernel.
+struct SpanPlan {
+    uint2 *tab;
+    uint2 *meta;
+    int32_t capr;  // plan entries per row: LW / 2 + 2
+    uint32_t *ovf_list, *ovf_n;
+};
 hipError_t launch_rows_span(const RowParams &P, const uint32_t *tok, const uint32_t *rec_tok, const uint32_t *rec_cnt,
                             const uint32_t *row_off, const uint32_t *row_rec, SegSel sel, int64_t rows_cap,
-                            RowOut out, uint32_t *err, hipStream_t st);
+                            RowOut out, uint32_t *err, hipStream_t st, const SpanPlan *plan = nullptr);
 
 hipError_t launch_single_labels(const uint32_t *labels, const uint64_t *label_off, const uint32_t *row_rec,
                                 const uint32_t *row_off, SegSel sel, int64_t rows_cap, int B, int32_t *out,

@@ -81,11 +81,41 @@ __global__ __launch_bounds__(SCAN_NT) void k_scan_apply(const uint32_t *__restri
     if (blockIdx.x == 0 && threadIdx.x == 0) out[n] = sums[nb];
 }
 
+// n <= SCAN_SMALL: one workgroup, one launch (a per-record push scans a handful
+// of chunk and record counts; three dependent launches would cost more than the scan)
+constexpr int SCAN_SMALL_NT = 1024, SCAN_SMALL_PER = 8;
+constexpr int64_t SCAN_SMALL = (int64_t)SCAN_SMALL_NT * SCAN_SMALL_PER;
+__global__ __launch_bounds__(SCAN_SMALL_NT) void k_scan_small(const uint32_t *__restrict__ in, int64_t n,
+                                                              uint32_t *__restrict__ out, const uint32_t *carry_in) {
+    __shared__ uint32_t scratch[SCAN_SMALL_NT / 64];
+    const uint32_t carry = carry_in ? *carry_in : 0u;
+    __syncthreads();  // (the carry may be out[0] itself, rewritten below)
+    const int64_t base = (int64_t)threadIdx.x * SCAN_SMALL_PER;
+    uint32_t v[SCAN_SMALL_PER], s = 0;
+#pragma unroll
+    for (int k = 0; k < SCAN_SMALL_PER; ++k) {
+        v[k] = base + k < n ? in[base + k] : 0u;
+        s += v[k];
+    }
+    uint32_t tot;
+    uint32_t ex = block_excl_sum<SCAN_SMALL_NT>(s, &tot, scratch) + carry;
+#pragma unroll
+    for (int k = 0; k < SCAN_SMALL_PER; ++k) {
+        if (base + k < n) out[base + k] = ex;
+        ex += v[k];
+    }
+    if (threadIdx.x == 0) out[n] = carry + tot;
+}
+
 int64_t scan_tmp_words(int64_t n) { return (n + SCAN_TILE - 1) / SCAN_TILE + 1; }
 
 hipError_t launch_exclusive_scan(const uint32_t *in, uint32_t *out, int64_t n, uint32_t *tmp, hipStream_t st,
                                  const uint32_t *carry_in) {
     if (n <= 0) return carry_in ? hipSuccess : hipMemsetAsync(out, 0, sizeof(uint32_t), st);
+    if (n <= SCAN_SMALL) {
+        hipLaunchKernelGGL(k_scan_small, dim3(1), dim3(SCAN_SMALL_NT), 0, st, in, n, out, carry_in);
+        return hipGetLastError();
+    }
     const int64_t nb = (n + SCAN_TILE - 1) / SCAN_TILE;
     hipLaunchKernelGGL(k_scan_reduce, dim3((unsigned)nb), dim3(SCAN_NT), 0, st, in, n, tmp);
     hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(SCAN_NT), 0, st, tmp, nb, carry_in);
@@ -172,9 +202,19 @@ __device__ __forceinline__ RowSpan row_span(const SegSel &s, const uint32_t *row
 // ---------------------------------------------------------------------------
 // Per chunk: record ranges touching its window (so the tokenize kernel never
 // binary-searches the offsets serially).
+// Also (thread 0) the one-segment record bounds rb = {0, R} and a zeroed error word,
+// when given: two launches fewer per call.
 __global__ __launch_bounds__(256) void k_chunk_ranges(const uint64_t *__restrict__ off, int64_t R, int64_t n_chunks,
-                                                      uint32_t *__restrict__ ranges) {
+                                                      uint32_t *__restrict__ ranges, uint32_t *__restrict__ rb1,
+                                                      uint32_t *__restrict__ zero1) {
     const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (c == 0) {
+        if (rb1) {
+            rb1[0] = 0u;
+            rb1[1] = (uint32_t)R;
+        }
+        if (zero1) *zero1 = 0u;
+    }
     if (c >= n_chunks) return;
     auto lower = [&](int64_t x) {  // first r in [0, R] with off[r] >= x (R+1 if none)
         int64_t lo = 0, hi = R + 1;
@@ -190,11 +230,12 @@ __global__ __launch_bounds__(256) void k_chunk_ranges(const uint64_t *__restrict
     ranges[3 * c + 2] = (uint32_t)lower(c0);
 }
 
-hipError_t launch_chunk_ranges(const uint64_t *off, int64_t R, int64_t N, uint32_t *ranges, hipStream_t st) {
+hipError_t launch_chunk_ranges(const uint64_t *off, int64_t R, int64_t N, uint32_t *ranges, hipStream_t st,
+                               uint32_t *rb1, uint32_t *zero1) {
     const int64_t n_chunks = (N + CHUNK - 1) / CHUNK;
     if (n_chunks == 0) return hipSuccess;
     hipLaunchKernelGGL(k_chunk_ranges, dim3((unsigned)((n_chunks + 255) / 256)), dim3(256), 0, st, off, R, n_chunks,
-                       ranges);
+                       ranges, rb1, zero1);
     return hipGetLastError();
 }
 
@@ -205,16 +246,15 @@ hipError_t launch_chunk_ranges(const uint64_t *off, int64_t R, int64_t N, uint32
 #define SDL_COMPACT_CPW 4
 #endif
 constexpr int COMPACT_CPW = SDL_COMPACT_CPW;  // chunks per wave: their loads are in flight together
-__global__ __launch_bounds__(256) void k_compact_tokens(const uint32_t *__restrict__ tokc,
-                                                        const uint32_t *__restrict__ chunk_cnt,
-                                                        const uint32_t *__restrict__ chunk_off, int64_t n_chunks,
-                                                        uint32_t *__restrict__ tok, const uint32_t *long_count,
-                                                        const uint32_t *__restrict__ chunk_ent,
-                                                        const BpeLong *__restrict__ long_list,
-                                                        const uint16_t *__restrict__ long_scratch,
-                                                        const uint32_t *__restrict__ long_pool, int64_t stride) {
-    const int64_t cb = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * COMPACT_CPW;  // the wave's first chunk
-    if (cb >= n_chunks) return;
+// one wave: chunks [cb, cb + COMPACT_CPW)
+__device__ __forceinline__ void compact_wave(int64_t cb, const uint32_t *__restrict__ tokc,
+                                             const uint32_t *__restrict__ chunk_cnt,
+                                             const uint32_t *__restrict__ chunk_off, int64_t n_chunks,
+                                             uint32_t *__restrict__ tok, const uint32_t *long_count,
+                                             const uint32_t *__restrict__ chunk_ent,
+                                             const BpeLong *__restrict__ long_list,
+                                             const uint16_t *__restrict__ long_scratch,
+                                             const uint32_t *__restrict__ long_pool, int64_t stride) {
     const int lane = threadIdx.x & 63;
     uint32_t n[COMPACT_CPW], o[COMPACT_CPW];
 #pragma unroll
@@ -293,6 +333,20 @@ __global__ __launch_bounds__(256) void k_compact_tokens(const uint32_t *__restri
     }
 }
 
+__global__ __launch_bounds__(256) void k_compact_tokens(const uint32_t *__restrict__ tokc,
+                                                        const uint32_t *__restrict__ chunk_cnt,
+                                                        const uint32_t *__restrict__ chunk_off, int64_t n_chunks,
+                                                        uint32_t *__restrict__ tok, const uint32_t *long_count,
+                                                        const uint32_t *__restrict__ chunk_ent,
+                                                        const BpeLong *__restrict__ long_list,
+                                                        const uint16_t *__restrict__ long_scratch,
+                                                        const uint32_t *__restrict__ long_pool, int64_t stride) {
+    const int64_t cb = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * COMPACT_CPW;  // the wave's first chunk
+    if (cb >= n_chunks) return;
+    compact_wave(cb, tokc, chunk_cnt, chunk_off, n_chunks, tok, long_count, chunk_ent, long_list, long_scratch,
+                 long_pool, stride);
+}
+
 hipError_t launch_compact_tokens(const uint32_t *tokc, const uint32_t *chunk_cnt, const uint32_t *chunk_off,
                                  int64_t n_chunks, uint32_t *tok, const uint32_t *long_count,
                                  const uint32_t *chunk_ent, const BpeLong *long_list, const uint16_t *long_scratch,
@@ -307,28 +361,34 @@ hipError_t launch_compact_tokens(const uint32_t *tokc, const uint32_t *chunk_cnt
 // ---------------------------------------------------------------------------
 // Per record: where its ids start, how many, and how many rows it yields.
 // ---------------------------------------------------------------------------
+__device__ __forceinline__ void record_one(const RowParams &P, const uint64_t *__restrict__ off, int64_t r, int64_t N,
+                                           const uint32_t *__restrict__ chunk_off, int64_t n_chunks,
+                                           const uint32_t *__restrict__ rec_local, uint32_t *__restrict__ rec_tok,
+                                           uint32_t *__restrict__ rec_cnt, uint32_t *__restrict__ rec_rows) {
+    auto tok_off = [&](int64_t q) -> uint32_t {
+        const int64_t p = (int64_t)off[q];
+        // (chunk_off[n_chunks], the total, is final once the last segment is scanned:
+        // only the last segment holds records that end at N)
+        return p >= N ? chunk_off[n_chunks] : chunk_off[p / CHUNK] + rec_local[q];
+    };
+    const uint32_t a = tok_off(r), b = tok_off(r + 1);
+    const uint32_t cnt = b - a;
+    const uint32_t n = cnt + (uint32_t)(P.n_pre + P.n_post);  // encode_mask framing
+    uint32_t rows = 0;
+    if (n >= (uint32_t)P.min_ids) rows = P.chunk ? ceil_div_u32(n, (uint32_t)P.S) : 1u;  // gen_batcher.rs:74-80
+    rec_tok[r] = a;
+    rec_cnt[r] = cnt;
+    rec_rows[r] = rows;
+}
+
 __global__ __launch_bounds__(256) void k_records(RowParams P, const uint64_t *__restrict__ off, int64_t R, int64_t N,
                                                  const uint32_t *__restrict__ chunk_off, int64_t n_chunks,
                                                  const uint32_t *__restrict__ rec_local, uint32_t *__restrict__ rec_tok,
                                                  uint32_t *__restrict__ rec_cnt, uint32_t *__restrict__ rec_rows,
                                                  SegSel sel) {
     const int64_t r_lo = sel.rb[sel.k], r_hi = sel.rb[sel.k + 1];
-    for (int64_t r = r_lo + (int64_t)blockIdx.x * 256 + threadIdx.x; r < r_hi; r += (int64_t)gridDim.x * 256) {
-        auto tok_off = [&](int64_t q) -> uint32_t {
-            const int64_t p = (int64_t)off[q];
-            // (chunk_off[n_chunks], the total, is final once the last segment is scanned:
-            // only the last segment holds records that end at N)
-            return p >= N ? chunk_off[n_chunks] : chunk_off[p / CHUNK] + rec_local[q];
-        };
-        const uint32_t a = tok_off(r), b = tok_off(r + 1);
-        const uint32_t cnt = b - a;
-        const uint32_t n = cnt + (uint32_t)(P.n_pre + P.n_post);  // encode_mask framing
-        uint32_t rows = 0;
-        if (n >= (uint32_t)P.min_ids) rows = P.chunk ? ceil_div_u32(n, (uint32_t)P.S) : 1u;  // gen_batcher.rs:74-80
-        rec_tok[r] = a;
-        rec_cnt[r] = cnt;
-        rec_rows[r] = rows;
-    }
+    for (int64_t r = r_lo + (int64_t)blockIdx.x * 256 + threadIdx.x; r < r_hi; r += (int64_t)gridDim.x * 256)
+        record_one(P, off, r, N, chunk_off, n_chunks, rec_local, rec_tok, rec_cnt, rec_rows);
 }
 
 hipError_t launch_records(const RowParams &P, const uint64_t *off, int64_t R, int64_t N, const uint32_t *chunk_off,
@@ -347,6 +407,58 @@ __global__ __launch_bounds__(256) void k_row_map(const uint32_t *__restrict__ ro
     const int64_t r_lo = sel.rb[sel.k], r_hi = sel.rb[sel.k + 1];
     for (int64_t r = r_lo + (int64_t)blockIdx.x * 256 + threadIdx.x; r < r_hi; r += (int64_t)gridDim.x * 256)
         for (uint32_t g = row_off[r]; g < row_off[r + 1]; ++g) row_rec[g] = (uint32_t)r;
+}
+
+// ---------------------------------------------------------------------------
+// Small calls (one segment, <= SMALL_CHUNKS chunks, <= SCAN_SMALL records): the
+// chunk scan, compaction, per-record framing, row scan and row map of one
+// workgroup in one launch instead of five (a per-record push is bound by
+// launches, not by these few thousand ids).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void block_scan_small(const uint32_t *__restrict__ in, int64_t n, uint32_t *__restrict__ out,
+                                                 uint32_t *scratch) {
+    const int64_t base = (int64_t)threadIdx.x * SCAN_SMALL_PER;
+    uint32_t v[SCAN_SMALL_PER], s = 0;
+#pragma unroll
+    for (int k = 0; k < SCAN_SMALL_PER; ++k) {
+        v[k] = base + k < n ? in[base + k] : 0u;
+        s += v[k];
+    }
+    uint32_t tot;
+    uint32_t ex = block_excl_sum<SCAN_SMALL_NT>(s, &tot, scratch);
+#pragma unroll
+    for (int k = 0; k < SCAN_SMALL_PER; ++k) {
+        if (base + k < n) out[base + k] = ex;
+        ex += v[k];
+    }
+    if (threadIdx.x == 0) out[n] = tot;
+}
+
+__global__ __launch_bounds__(SCAN_SMALL_NT) void k_downstream_small(SmallDown d, RowParams P,
+                                                                    const uint64_t *__restrict__ off, int64_t R,
+                                                                    int64_t N, int64_t n_chunks) {
+    __shared__ uint32_t scratch[SCAN_SMALL_NT / 64];
+    block_scan_small(d.chunk_cnt, n_chunks, d.chunk_off, scratch);
+    __syncthreads();
+    for (int64_t cb = (int64_t)(threadIdx.x >> 6) * COMPACT_CPW; cb < n_chunks;
+         cb += (int64_t)(SCAN_SMALL_NT / 64) * COMPACT_CPW)
+        compact_wave(cb, d.tokc, d.chunk_cnt, d.chunk_off, n_chunks, d.tok, d.long_count, d.chunk_ent, d.long_list,
+                     d.long_scratch, d.long_pool, d.stride);
+    for (int64_t r = threadIdx.x; r < R; r += SCAN_SMALL_NT)
+        record_one(P, off, r, N, d.chunk_off, n_chunks, d.rec_local, d.rec_tok, d.rec_cnt, d.rec_rows);
+    __syncthreads();
+    block_scan_small(d.rec_rows, R, d.row_off, scratch);
+    __syncthreads();
+    for (int64_t r = threadIdx.x; r < R; r += SCAN_SMALL_NT)
+        for (uint32_t g = d.row_off[r]; g < d.row_off[r + 1]; ++g) d.row_rec[g] = (uint32_t)r;
+}
+
+hipError_t launch_downstream_small(const SmallDown &d, const RowParams &P, const uint64_t *off, int64_t R, int64_t N,
+                                   hipStream_t st) {
+    const int64_t n_chunks = (N + CHUNK - 1) / CHUNK;
+    if (n_chunks > SMALL_CHUNKS || R > SCAN_SMALL) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_downstream_small, dim3(1), dim3(SCAN_SMALL_NT), 0, st, d, P, off, R, N, n_chunks);
+    return hipGetLastError();
 }
 
 hipError_t launch_row_map(const uint32_t *row_off, int64_t R, uint32_t *row_rec, SegSel sel, hipStream_t st) {
@@ -894,6 +1006,51 @@ hipError_t launch_rows_to_host(const RowSeg *segs, int n_segs, uint32_t rows_per
     return hipGetLastError();
 }
 
+// (kernels.hpp DirectDst) block b copies rows b, b + gridDim.x, ... below
+// min(row_off[R], cap), its four waves taking the four planes; block 0 also
+// copies the row offsets and error words out.
+__global__ __launch_bounds__(256) void k_rows_direct(DirectDst d, const uint32_t *__restrict__ row_off, int64_t R,
+                                                     const int32_t *__restrict__ ids, const int32_t *__restrict__ am,
+                                                     const int32_t *__restrict__ tt, const int32_t *__restrict__ lab,
+                                                     int S, int LW, const uint32_t *__restrict__ err0,
+                                                     const uint32_t *__restrict__ err1, uint32_t *__restrict__ stat) {
+    if (blockIdx.x == 0) {
+        for (int64_t r = threadIdx.x; r <= R; r += 256) stat[r] = row_off[r];
+        if (threadIdx.x == 0) {
+            stat[R + 1] = err0 ? *err0 : 0u;
+            stat[R + 2] = err1 ? *err1 : 0u;
+        }
+    }
+    const uint32_t total = row_off[R];
+    const uint32_t n = total < d.cap ? total : d.cap;
+    const int plane = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63);
+    const int32_t *src = plane == 0 ? ids : plane == 1 ? am : plane == 2 ? tt : lab;
+    if (!src) return;
+    const int W = plane == 3 ? LW : S;  // ints per row
+    const bool vec = (W & 3) == 0;
+    for (uint32_t g = blockIdx.x; g < n; g += gridDim.x) {
+        const uint32_t slot = d.base + g, bi = slot >= d.B ? 1u : 0u, row = slot - bi * d.B;
+        int32_t *dst = plane == 0 ? d.ids[bi] : plane == 1 ? d.am[bi] : plane == 2 ? d.tt[bi] : d.lab[bi];
+        const int32_t *s = src + (size_t)g * W;
+        int32_t *o = dst + (size_t)row * W;
+        if (vec) {
+            for (int j = 4 * lane; j < W; j += 256)
+                *reinterpret_cast<int4 *>(o + j) = *reinterpret_cast<const int4 *>(s + j);
+        } else {
+            for (int j = lane; j < W; j += 64) o[j] = s[j];
+        }
+    }
+}
+
+hipError_t launch_rows_direct(const DirectDst &d, const uint32_t *row_off, int64_t R, const int32_t *ids,
+                              const int32_t *am, const int32_t *tt, const int32_t *lab, int S, int LW,
+                              const uint32_t *err0, const uint32_t *err1, uint32_t *stat, hipStream_t st) {
+    const unsigned grid = d.cap < 64u ? (d.cap ? d.cap : 1u) : 64u;
+    hipLaunchKernelGGL(k_rows_direct, dim3(grid), dim3(256), 0, st, d, row_off, R, ids, am, tt, lab, S, LW, err0, err1,
+                       stat);
+    return hipGetLastError();
+}
+
 hipError_t launch_rows(const RowParams &P, const uint32_t *tok, const uint32_t *rec_tok, const uint32_t *rec_cnt,
                        const uint32_t *row_off, const uint32_t *row_rec, SegSel sel, int64_t rows_cap, RowOut out,
                        hipStream_t st) {
@@ -997,7 +1154,8 @@ __device__ __forceinline__ bool zig_fast(uint64_t bits, const double *__restrict
 }
 
 // The whole draw starting at stream word k: value and u64 words consumed.
-__device__ double zig_normal(SpanStream &s, uint64_t k, const double *__restrict__ ZX,
+template <class Stream>
+__device__ double zig_normal(Stream &s, uint64_t k, const double *__restrict__ ZX,
                              const double *__restrict__ ZF, uint32_t *len) {
 #pragma clang fp contract(off)
     const uint64_t k0 = k;
@@ -1144,7 +1302,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RAND ? 1 : 
                                                    const uint32_t *__restrict__ rec_cnt,
                                                    const uint32_t *__restrict__ row_off,
                                                    const uint32_t *__restrict__ row_rec, SegSel sel,
-                                                   int64_t rows_cap, RowOut out, uint32_t *__restrict__ err) {
+                                                   int64_t rows_cap, RowOut out, uint32_t *__restrict__ err,
+                                                   const uint32_t *__restrict__ list,
+                                                   const uint32_t *__restrict__ list_n) {
     __shared__ SpanPass s_pass[4][64];
     __shared__ uint32_t s_win[4][SPAN_WBLK * 16];
     __shared__ double s_draw[4][128];
@@ -1159,7 +1319,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RAND ? 1 : 
     const RowSpan rs = row_span(sel, row_off, P.B, rows_cap);
     const int64_t G = rs.g_real;
     SpanPass *sp = s_pass[wid];
-    for (int64_t g = rs.g_lo + (int64_t)blockIdx.x * 4 + wid; g < rs.g_end; g += (int64_t)gridDim.x * 4) {
+    // list mode (the two-phase path's rows with more passes than its plan holds): those rows only
+    const int64_t i_end = list ? (int64_t)*list_n : rs.g_end;
+    for (int64_t i = (list ? 0 : rs.g_lo) + (int64_t)blockIdx.x * 4 + wid; i < i_end; i += (int64_t)gridDim.x * 4) {
+        const int64_t g = list ? (int64_t)list[i] : i;
         int32_t *ids_o = out.input_ids + g * S;
         int32_t *am_o = out.attention_mask + g * S;
         int32_t *lb_o = out.labels + g * (int64_t)LW;
@@ -1324,24 +1487,321 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RAND ? 1 : 
     }
 }
 
+// ---------------------------------------------------------------------------
+// Span rows in two phases.
+//  1. k_span_plan, one lane per row: the row's passes drawn and walked
+//     serially (the cursor recurrence above, lane-local), each pass written to
+//     the row's plan as {lp | gg << 16, ip | sz << 16}; the row's pass count
+//     and its ids / labels ends to meta.  A row whose passes overrun the plan
+//     (capr = LW / 2 + 2: every row within the label width fits, so only rows
+//     the reference panics on can) is listed for the one-pass kernel instead.
+//  2. k_span_write, one wave per row: framed ids and plan in LDS, the pass
+//     starts scattered into per-position marks, a max-scan gives every
+//     position its pass, and each lane writes 4 contiguous positions per
+//     store -- the row writer of k_rows, no serial walk.
+// ---------------------------------------------------------------------------
+struct LaneStream {  // rng_mode 1: one lane's StdRng stream, its current ChaCha12 block in LDS
+    uint32_t key[8];
+    uint32_t *blk;  // 16 words (LDS, this lane's)
+    int64_t have;
+    __device__ uint64_t at(uint64_t k) {
+        const int64_t b = (int64_t)(k >> 3);
+        if (b != have) {
+            uint32_t o[16];
+            chacha12_block(key, (uint32_t)b, o);
+#pragma unroll
+            for (int q = 0; q < 16; ++q) blk[q] = o[q];
+            have = b;
+        }
+        const uint32_t w = 2u * (uint32_t)(k & 7u);
+        return (uint64_t)blk[w + 1] << 32 | blk[w];
+    }
+};
+
+template <int RAND>
+__global__ __launch_bounds__(256) void k_span_plan(RowParams P, const uint32_t *__restrict__ rec_cnt,
+                                                   const uint32_t *__restrict__ row_off,
+                                                   const uint32_t *__restrict__ row_rec, SegSel sel, int64_t rows_cap,
+                                                   SpanPlan pl, uint32_t *__restrict__ err) {
+    __shared__ uint32_t s_blk[RAND ? 256 : 1][17];
+    const int S = P.S, LW = P.label_width;
+    const RowSpan rs = row_span(sel, row_off, P.B, rows_cap);
+    uint32_t bad = 0;
+    for (int64_t g = rs.g_lo + (int64_t)blockIdx.x * 256 + threadIdx.x; g < rs.g_real;
+         g += (int64_t)gridDim.x * 256) {
+        const int64_t r = row_rec[g];
+        const uint32_t k = (uint32_t)(g - row_off[r]);
+        const int64_t nf = (int64_t)rec_cnt[r] + P.n_pre + P.n_post;
+        const int64_t base = P.chunk ? (int64_t)k * S : 0;
+        const int n = (int)((nf - base) < S ? (nf - base) : S);
+        if (n <= 0) {
+            pl.meta[g] = make_uint2(0u, 0u);
+            continue;
+        }
+        const uint64_t rec = P.first_record + (uint64_t)r;
+        LaneStream ls;
+        uint64_t spos = 0;
+        if (RAND) {
+            const uint32_t kk[8] = {(uint32_t)P.seed, (uint32_t)(P.seed >> 32), (uint32_t)rec, (uint32_t)(rec >> 32),
+                                    k, 0u, 0u, 0u};
+#pragma unroll
+            for (int q = 0; q < 8; ++q) ls.key[q] = kk[q];
+            ls.blk = s_blk[RAND ? threadIdx.x : 0];
+            ls.have = -1;
+        }
+        uint2 *tab = pl.tab + g * (int64_t)pl.capr;
+        uint32_t rbad = 0;
+        int Ip = 0, Ap = 0;
+        bool over = false;
+        for (uint32_t p = 0;; ++p) {
+            uint32_t gr, sr;
+            if (RAND) {
+                uint32_t l1, l2;
+                const double d1 = zig_normal(ls, spos, P.zig_x, P.zig_f, &l1);
+                const double d2 = zig_normal(ls, spos + l1, P.zig_x, P.zig_f, &l2);
+                spos += l1 + l2;
+                gr = sat_draw(P.avg_span_gap - d1, n);
+                const uint32_t sz = sat_draw(P.avg_span_size - d2, n);
+                sr = sz > 1u ? sz : 1u;  // std::cmp::max(distance as usize, 1)
+            } else {
+                const uint4 c = philox4x32_10(make_uint4(p, k | 0x40000000u, (uint32_t)rec, (uint32_t)(rec >> 32)),
+                                              (uint32_t)P.seed, (uint32_t)(P.seed >> 32));
+                gr = span_pick(P.gap_kmin, P.gap_n, P.gap_thr, c.x);
+                sr = span_pick(P.size_kmin, P.size_n, P.size_thr, c.y);
+            }
+            const int gs = gr > (uint32_t)n ? n : (int)gr, ss = sr > (uint32_t)n ? n : (int)sr;
+            const bool last = Ip + gs + ss >= n;
+            const int gg = last ? (gs < n - Ip ? gs : n - Ip) : gs;
+            const int sz = last ? (ss < n - Ip - gg ? ss : n - Ip - gg) : ss;
+            const int lp = Ip - Ap + (int)p, ap = Ap + (int)p;
+            if ((int)p >= pl.capr) {
+                over = true;
+                break;
+            }
+            tab[p] = make_uint2((uint32_t)lp | (uint32_t)gg << 16, (uint32_t)Ip | (uint32_t)sz << 16);
+            // the reference's panics, counted as k_rows_span counts them
+            if (sz > 0) {
+                rbad += p >= 100u ? 1u : 0u;
+                const int lo = ap > LW ? ap : LW, hi = ap + sz + 1;
+                rbad += hi > lo ? (uint32_t)(hi - lo) : 0u;
+            }
+            if (last) {
+                rbad += p + 1u >= 100u ? 1u : 0u;
+                rbad += ap + (sz > 0 ? sz + 1 : 0) >= LW ? 1u : 0u;
+                const uint32_t lp_end = (uint32_t)(lp + gg + (sz > 0 ? 1 : 0));
+                const uint32_t ap_end = (uint32_t)(ap + (sz > 0 ? sz + 1 : 0));
+                pl.meta[g] = make_uint2(p + 1u, lp_end | ap_end << 16);
+                break;
+            }
+            Ip += gs + ss;
+            Ap += ss;
+        }
+        if (over) {  // the one-pass kernel takes this row (and counts its errors)
+            pl.meta[g] = make_uint2(0xFFFFFFFFu, 0u);
+            pl.ovf_list[atomicAdd(pl.ovf_n, 1u)] = (uint32_t)g;
+        } else {
+            bad += rbad;
+        }
+    }
+    for (int d = 32; d >= 1; d >>= 1) bad += __shfl_xor(bad, d, 64);
+    if ((threadIdx.x & 63) == 0 && bad) atomicAdd(err, bad);
+}
+
+#define SDL_MAXU(a, b) ((a) > (b) ? (a) : (b))
+// Positions [0, W) of one plane of a row, lane L holding 256 m + 4 L + w: the
+// owner pass of each position = the max-scan of `mk` (pass p marked at its
+// first position); val(q, owner) gives the value; positions >= end get
+// tail(q).  Stores of 16 B per lane when W is a multiple of 4.
+template <class Val, class Tail>
+__device__ __forceinline__ void span_plane(int32_t *__restrict__ o, int W, int end, const uint16_t *mk, Val val,
+                                           Tail tail) {
+    const int lane = lane_id();
+    uint32_t carry = 0;
+    const bool vec = (W & 3) == 0;
+    for (int b = 0; b < W; b += 256) {
+        const int q0 = b + 4 * lane;
+        uint32_t own[4], run = 0;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            const int q = q0 + w;
+            const uint32_t m = q < end ? (uint32_t)mk[q] : 0u;
+            run = SDL_MAXU(run, m);
+            own[w] = run;
+        }
+        uint32_t x = run;
+        SDL_DPP_SCAN(x, SDL_MAXU);
+        const uint32_t before = SDL_MAXU(wave_prev(x), carry);
+        carry = SDL_MAXU(carry, (uint32_t)lane_bcast((int)x, 63));
+        int32_t v[4];
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            const int q = q0 + w;
+            v[w] = q < end ? val(q, SDL_MAXU(own[w], before)) : tail(q);
+        }
+        if (vec) {
+            typedef int32_t v4i __attribute__((ext_vector_type(4)));
+            if (q0 < W) __builtin_nontemporal_store(v4i{v[0], v[1], v[2], v[3]}, reinterpret_cast<v4i *>(o + q0));
+        } else {
+#pragma unroll
+            for (int w = 0; w < 4; ++w)
+                if (q0 + w < W) st_nt(o + q0 + w, v[w]);
+        }
+    }
+}
+
+constexpr int SPAN_TABL = 128;  // plan entries per row held in LDS (the rest read from the plan)
+
+__global__ __launch_bounds__(256) void k_span_write(RowParams P, const uint32_t *__restrict__ tok,
+                                                    const uint32_t *__restrict__ rec_tok,
+                                                    const uint32_t *__restrict__ rec_cnt,
+                                                    const uint32_t *__restrict__ row_off,
+                                                    const uint32_t *__restrict__ row_rec, SegSel sel,
+                                                    int64_t rows_cap, RowOut out, SpanPlan pl) {
+    __shared__ int32_t s_extra[100];
+    __shared__ uint2 s_tab[4][SPAN_TABL];
+    extern __shared__ int32_t s_dyn[];  // per wave: rid[S] | mk[S] u16 | mk2[LW] u16 (rounded)
+    const int lane = lane_id();
+    const int wid = (int)(threadIdx.x >> 6);
+    if (threadIdx.x < 100) s_extra[threadIdx.x] = P.extra_ids[threadIdx.x];
+    __syncthreads();
+    const int S = P.S, LW = P.label_width;
+    const int wave_words = S + ((S + LW + 1) >> 1);
+    int32_t *rid = s_dyn + (size_t)wid * wave_words;
+    uint16_t *mk = reinterpret_cast<uint16_t *>(rid + S);
+    uint16_t *mk2 = mk + S;
+    uint2 *tl = s_tab[wid];
+    const RowSpan rs = row_span(sel, row_off, P.B, rows_cap);
+    const int64_t G = rs.g_real;
+    auto extra = [&](uint32_t q) -> int32_t { return s_extra[q < 100u ? q : 99u]; };
+    auto fence = [] {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    };
+    for (int64_t g = rs.g_lo + (int64_t)blockIdx.x * 4 + wid; g < rs.g_end; g += (int64_t)gridDim.x * 4) {
+        int32_t *ids_o = out.input_ids + g * S;
+        int32_t *am_o = out.attention_mask + g * S;
+        int32_t *lb_o = out.labels + g * (int64_t)LW;
+        const uint2 m = g < G ? pl.meta[g] : make_uint2(0u, 0u);
+        if (m.x == 0xFFFFFFFFu) continue;  // the one-pass kernel's row
+        for (int j = lane; j < S; j += 64) st_nt(am_o + j, 1);  // attention stays 1 (the zeroing loop is empty)
+        const int np = (int)m.x;
+        if (np == 0) {  // past the last row (or an empty one): T5Data::new's values
+            for (int j = lane; j < S; j += 64) st_nt(ids_o + j, 0);
+            for (int j = lane; j < LW; j += 64) st_nt(lb_o + j, -100);
+            continue;
+        }
+        const int lp_end = (int)(m.y & 0xFFFFu), ap_end = (int)(m.y >> 16);
+        const int64_t r = row_rec[g];
+        const uint32_t k = (uint32_t)(g - row_off[r]);
+        const uint32_t cnt = rec_cnt[r];
+        const uint32_t t0 = rec_tok[r];
+        const int64_t nf = (int64_t)cnt + P.n_pre + P.n_post;
+        const int64_t base = P.chunk ? (int64_t)k * S : 0;
+        const int n = (int)((nf - base) < S ? (nf - base) : S);
+        const uint2 *tab = pl.tab + g * (int64_t)pl.capr;
+        auto fid = [&](int j) -> int32_t {  // framed id j of this chunk
+            const int64_t f = base + j;
+            if (f < P.n_pre) return frame_id(P.pre, (int)f);
+            if (f < P.n_pre + (int64_t)cnt) return (int32_t)tok[t0 + (f - P.n_pre)];
+            return frame_id(P.post, (int)(f - P.n_pre - cnt));
+        };
+        // framed ids, plan and zeroed marks into LDS: every load in flight together
+        for (int j0 = 0; j0 < n; j0 += 64 * 8) {
+            int32_t v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int j = j0 + 64 * u + lane;
+                v[u] = j < n ? fid(j) : 0;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int j = j0 + 64 * u + lane;
+                if (j < n) rid[j] = v[u];
+            }
+        }
+        for (int p = lane; p < np && p < SPAN_TABL; p += 64) tl[p] = tab[p];
+        for (int j = 2 * lane; j < S + LW; j += 128) *reinterpret_cast<uint32_t *>(mk + j) = 0u;
+        fence();
+        auto ent = [&](int p) -> uint2 { return p < SPAN_TABL ? tl[p] : tab[p]; };
+        // pass starts: ids at lp, labels at ap = ip - lp + 2 p (within the label width)
+        for (int p = lane; p < np; p += 64) {
+            const uint2 e = ent(p);
+            const int lp = (int)(e.x & 0xFFFFu), ip = (int)(e.y & 0xFFFFu);
+            const int ap = ip - lp + 2 * p;
+            if (lp < S) mk[lp] = (uint16_t)p;
+            if (ap < LW) mk2[ap] = (uint16_t)p;
+        }
+        fence();
+        span_plane(
+            ids_o, S, lp_end, mk,
+            [&](int q, uint32_t o) -> int32_t {
+                const uint2 e = ent((int)o);
+                const int off = q - (int)(e.x & 0xFFFFu), ge = (int)(e.x >> 16);
+                return off < ge ? rid[(int)(e.y & 0xFFFFu) + off] : extra(o);
+            },
+            [&](int) -> int32_t { return 0; });
+        const int apLim = ap_end < LW ? ap_end : LW;
+        const int32_t fin = extra((uint32_t)np);  // <extra_id_{last pass + 1}>
+        span_plane(
+            lb_o, LW, apLim, mk2,
+            [&](int q, uint32_t o) -> int32_t {
+                const uint2 e = ent((int)o);
+                const int lp = (int)(e.x & 0xFFFFu), ge = (int)(e.x >> 16), ip = (int)(e.y & 0xFFFFu);
+                const int off = q - (ip - lp + 2 * (int)o);
+                return off == 0 ? extra(o) : rid[ip + ge + off - 1];
+            },
+            [&](int q) -> int32_t { return q == ap_end ? fin : -100; });
+        fence();  // (the next row rewrites rid / marks)
+    }
+}
+
 hipError_t launch_rows_span(const RowParams &P, const uint32_t *tok, const uint32_t *rec_tok, const uint32_t *rec_cnt,
                             const uint32_t *row_off, const uint32_t *row_rec, SegSel sel, int64_t rows_cap,
-                            RowOut out, uint32_t *err, hipStream_t st) {
+                            RowOut out, uint32_t *err, hipStream_t st, const SpanPlan *pl) {
     if (rows_cap == 0) return hipSuccess;
     if (P.S > 65535 || (P.rng_mode == 1 && (!P.zig_x || !P.zig_f))) return hipErrorInvalidValue;
-    const int64_t want = (rows_cap + 3) / 4;
-    const unsigned grid = (unsigned)(want < SDL_SPAN_GRID_CAP ? want : SDL_SPAN_GRID_CAP);
     if (sel.k == 0) {  // the error count covers the whole call
         hipError_t e = hipMemsetAsync(err, 0, sizeof(uint32_t), st);
         if (e != hipSuccess) return e;
     }
+    if (pl) {
+        if (P.S > 16384 || pl->capr < 1) return hipErrorInvalidValue;
+        hipError_t e = hipMemsetAsync(pl->ovf_n, 0, sizeof(uint32_t), st);
+        if (e != hipSuccess) return e;
+        const int64_t pb = (rows_cap + 255) / 256;
+        const unsigned pgrid = (unsigned)(pb < 8192 ? pb : 8192);
+        if (P.rng_mode == 1)
+            hipLaunchKernelGGL(k_span_plan<1>, dim3(pgrid), dim3(256), 0, st, P, rec_cnt, row_off, row_rec, sel,
+                               rows_cap, *pl, err);
+        else
+            hipLaunchKernelGGL(k_span_plan<0>, dim3(pgrid), dim3(256), 0, st, P, rec_cnt, row_off, row_rec, sel,
+                               rows_cap, *pl, err);
+        const int64_t want = (rows_cap + 3) / 4;
+        const unsigned grid = (unsigned)(want < SDL_SPAN_GRID_CAP ? want : SDL_SPAN_GRID_CAP);
+        const size_t dyn = (size_t)4 * 4 * (P.S + ((P.S + P.label_width + 1) >> 1));
+        hipLaunchKernelGGL(k_span_write, dim3(grid), dim3(256), dyn, st, P, tok, rec_tok, rec_cnt, row_off, row_rec,
+                           sel, rows_cap, out, *pl);
+        // rows whose passes overran the plan: the one-pass kernel over the list
+        const size_t dyn1 = (size_t)4 * P.S * sizeof(int32_t);
+        const unsigned lgrid = 256;
+        if (P.rng_mode == 1)
+            hipLaunchKernelGGL(k_rows_span<1>, dim3(lgrid), dim3(256), dyn1, st, P, tok, rec_tok, rec_cnt, row_off,
+                               row_rec, sel, rows_cap, out, err, pl->ovf_list, pl->ovf_n);
+        else
+            hipLaunchKernelGGL(k_rows_span<0>, dim3(lgrid), dim3(256), dyn1, st, P, tok, rec_tok, rec_cnt, row_off,
+                               row_rec, sel, rows_cap, out, err, pl->ovf_list, pl->ovf_n);
+        return hipGetLastError();
+    }
+    const int64_t want = (rows_cap + 3) / 4;
+    const unsigned grid = (unsigned)(want < SDL_SPAN_GRID_CAP ? want : SDL_SPAN_GRID_CAP);
     const size_t dyn = (size_t)4 * P.S * sizeof(int32_t);  // s_rid
     if (P.rng_mode == 1)
         hipLaunchKernelGGL(k_rows_span<1>, dim3(grid), dim3(256), dyn, st, P, tok, rec_tok, rec_cnt, row_off, row_rec,
-                           sel, rows_cap, out, err);
+                           sel, rows_cap, out, err, nullptr, nullptr);
     else
         hipLaunchKernelGGL(k_rows_span<0>, dim3(grid), dim3(256), dyn, st, P, tok, rec_tok, rec_cnt, row_off, row_rec,
-                           sel, rows_cap, out, err);
+                           sel, rows_cap, out, err, nullptr, nullptr);
     return hipGetLastError();
 }
 

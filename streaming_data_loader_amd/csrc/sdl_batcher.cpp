@@ -278,6 +278,11 @@ struct sdl_batcher {
     DevBuf<uint16_t> long_scratch;
     // unigram long items
     DevBuf<uint32_t> uni_counters, uni_pool, uni_err, span_err;
+    // span rows in two phases: per-row pass plans, row meta, overflow rows
+    DevBuf<uint2> span_tab, span_meta;
+    DevBuf<uint32_t> span_ovf;
+    bool span_two_phase = env_int("SDL_SPAN_TWO_PHASE", 0) != 0;
+    bool small_calls = env_int("SDL_SMALL_CALLS", 0) != 0;  // k_downstream_small + folded record bounds
     // JsonText provider step (sdl_json_text_device)
     DevBuf<uint32_t> j_cnt, j_base, j_nl, j_len, j_rec, j_toff, j_ridx, j_inv, j_tail;
     DevBuf<uint2> j_span;
@@ -311,20 +316,27 @@ struct sdl_batcher {
     DevBuf<uint8_t> x_json_all;       // ... every chunk, 32 zero bytes after each
     DevBuf<uint4> uni_items, uni_items2, uni_huge;
     DevBuf<uint8_t> uni_scratch;
-    DevBuf<uint8_t> h2d_text;
-    DevBuf<uint64_t> h2d_off, h2d_label_off;
-    DevBuf<uint32_t> h2d_labels;
 
     // host streaming path (GenTokenizer.store + emitted batches)
     std::deque<HostBatch *> store;
     std::deque<HostBatch *> outbox;
-    PinBuf<uint8_t> pin_text;
-    PinBuf<uint64_t> pin_off;
+    PinBuf<uint8_t> pin_blob;  // staged call input: text | offsets | labels | label offsets
+    DevBuf<uint8_t> h2d_blob;
     PinBuf<uint32_t> pin_u32;
-    PinBuf<uint32_t> pin_labels;
+    PinBuf<uint32_t> pin_stat;  // direct pass: row offsets + error words (mapped)
+    uint32_t *stat_dev = nullptr;
+    HostBatch *spare = nullptr;  // direct pass: the next batch, allocated ahead
     PinBuf<RowSeg> seg_pin;
     DevBuf<RowSeg> seg_dev;
-    PinBuf<uint64_t> pin_label_off;
+    void ensure_stat(size_t n) {
+        const uint32_t *was = pin_stat.p;
+        pin_stat.ensure(n);
+        if (pin_stat.p != was || !stat_dev) {
+            void *d = nullptr;
+            HIP_TRY(hipHostGetDevicePointer(&d, pin_stat.p, 0));
+            stat_dev = static_cast<uint32_t *>(d);
+        }
+    }
     uint32_t pin_u32_err = 0;
     uint32_t pin_u32_2[2] = {0, 0};
     uint64_t n_records = 0;
@@ -362,6 +374,7 @@ struct sdl_batcher {
 #endif
         for (auto *b : store) delete b;
         for (auto *b : outbox) delete b;
+        delete spare;
         for (auto &e : ev)
             if (e) (void)hipEventDestroy(e);
         for (auto &e : pipe_ev) (void)hipEventDestroy(e);
@@ -454,10 +467,14 @@ struct sdl_batcher {
         auto mark = [&](int i) {
             if (profiling) HIP_TRY(hipEventRecord(ev[i], st));
         };
+        const bool small = small_calls && !piped && !profiling && n_chunks <= SMALL_CHUNKS && R <= 8192;
         mark(0);
-        HIP_TRY(launch_chunk_ranges(d_off, R, N, ranges.p, st));
-        HIP_TRY(launch_seg_bounds(ranges.p, sc, R, seg_rb.p, st));
-        if (multi() || single()) HIP_TRY(hipMemsetAsync(lab_err.p, 0, 4, st));
+        // (one segment: k_chunk_ranges also writes its record bounds and zeroes the label error word)
+        const bool fold = small_calls && sc.K == 1 && n_chunks > 0;
+        HIP_TRY(launch_chunk_ranges(d_off, R, N, ranges.p, st, fold ? seg_rb.p : nullptr,
+                                    fold && (multi() || single()) ? lab_err.p : nullptr));
+        if (!fold) HIP_TRY(launch_seg_bounds(ranges.p, sc, R, seg_rb.p, st));
+        if (!fold && (multi() || single())) HIP_TRY(hipMemsetAsync(lab_err.p, 0, 4, st));
         mark(1);
         RowOut out{o_ids.p, o_am.p, with_tt() ? o_tt.p : nullptr, multi() ? nullptr : o_lab.p,
                    multi() ? o_f32.p : nullptr};
@@ -465,6 +482,15 @@ struct sdl_batcher {
         auto downstream = [&](int k, hipStream_t s) {
             const SegSel sel{seg_rb.p, k, k == sc.K - 1 ? 1 : 0};
             const int64_t ca = sc.cb[k], cz = sc.cb[k + 1];
+            if (small) {  // one launch for the five below
+                const SmallDown d{tokc.p, chunk_cnt.p, chunk_off.p, tok_ids.p,
+                                  uni ? uni_counters.p : bpe ? long_count.p : nullptr,
+                                  uni || bpe ? chunk_ent.p : nullptr, bpe ? long_list.p : nullptr,
+                                  bpe ? long_scratch.p : nullptr, uni ? uni_pool.p : nullptr,
+                                  uni ? (int64_t)UNI_STAGE : (int64_t)STAGE, rec_local.p, rec_tok.p, rec_cnt.p,
+                                  rec_rows.p, row_off.p, row_rec.p};
+                HIP_TRY(launch_downstream_small(d, p, d_off, R, N, s));
+            } else {
             if (!piped) mark(2);
             HIP_TRY(launch_exclusive_scan(chunk_cnt.p + ca, chunk_off.p + ca, cz - ca, scan_tmp.p, s,
                                           k > 0 ? chunk_off.p + ca : nullptr));
@@ -485,11 +511,24 @@ struct sdl_batcher {
             if (piped) HIP_TRY(launch_scan_range(rec_rows.p, row_off.p, seg_rb.p, k, s));
             else HIP_TRY(launch_exclusive_scan(rec_rows.p, row_off.p, R, scan_tmp.p, s));
             HIP_TRY(launch_row_map(row_off.p, R, row_rec.p, sel, s));
+            }
             if (!piped) mark(6);
             if (span()) {
                 span_err.ensure(1);
+                SpanPlan pl{};
+                const bool two_phase = span_two_phase;
+                if (two_phase) {
+                    pl.capr = P.label_width / 2 + 2;
+                    span_tab.ensure((size_t)std::max<int64_t>(rows_cap, 1) * (size_t)pl.capr);
+                    span_meta.ensure((size_t)std::max<int64_t>(rows_cap, 1));
+                    span_ovf.ensure((size_t)std::max<int64_t>(rows_cap, 1) + 1);
+                    pl.tab = span_tab.p;
+                    pl.meta = span_meta.p;
+                    pl.ovf_n = span_ovf.p;
+                    pl.ovf_list = span_ovf.p + 1;
+                }
                 HIP_TRY(launch_rows_span(p, tok_ids.p, rec_tok.p, rec_cnt.p, row_off.p, row_rec.p, sel, rows_cap, out,
-                                         span_err.p, s));
+                                         span_err.p, s, two_phase ? &pl : nullptr));
             } else {
                 if (p.task == SDL_TASK_MLM && p.rng_mode == 1)
                     HIP_TRY(launch_mask_rand(p, row_off.p, row_rec.p, sel, rows_cap, mask_j.p, s));
@@ -571,68 +610,109 @@ struct sdl_batcher {
     void process_host(const uint8_t *arena, const uint64_t *offsets, int64_t R, const uint32_t *labels,
                       const uint64_t *label_off) {
         const int64_t N = (int64_t)offsets[R];
+        // one pinned staging blob, one H2D: text | offsets | labels | label offsets
+        const bool with_labels = simple() && labels && label_off;  // validated by the caller
+        const uint64_t L = with_labels ? label_off[R] - label_off[0] : 0;
+        auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
+        const size_t x_off = up((size_t)N + 16), x_lab = up(x_off + 8 * (size_t)(R + 1)),
+                     x_loff = up(x_lab + 4 * (size_t)L + 4), blob = x_loff + 8 * (size_t)(R + 1);
+        pin_blob.ensure(blob);
+        h2d_blob.ensure(blob);
+        HostClock hc;
+        par_copy(pin_blob.p, arena, (size_t)N);
+        hc.lap("stage");
+        std::memcpy(pin_blob.p + x_off, offsets, sizeof(uint64_t) * (size_t)(R + 1));
         const uint32_t *d_labels = nullptr;
         const uint64_t *d_label_off = nullptr;
-        if (simple() && labels && label_off) {  // Label::Multi indices / Label::Single, validated by the caller
-            const uint64_t L = label_off[R];
-            pin_labels.ensure((size_t)L + 1);
-            pin_label_off.ensure((size_t)R + 1);
-            std::memcpy(pin_labels.p, labels, sizeof(uint32_t) * (size_t)L);
-            for (int64_t r = 0; r <= R; ++r) pin_label_off.p[r] = label_off[r] - label_off[0];
-            h2d_labels.ensure((size_t)L + 1);
-            h2d_label_off.ensure((size_t)R + 1);
-            if (L) HIP_TRY(hipMemcpyAsync(h2d_labels.p, pin_labels.p, sizeof(uint32_t) * L, hipMemcpyHostToDevice, stream));
-            HIP_TRY(hipMemcpyAsync(h2d_label_off.p, pin_label_off.p, sizeof(uint64_t) * (size_t)(R + 1),
-                                   hipMemcpyHostToDevice, stream));
-            d_labels = h2d_labels.p;
-            d_label_off = h2d_label_off.p;
+        size_t h2d_bytes = x_off + 8 * (size_t)(R + 1);
+        if (with_labels) {  // Label::Multi indices / Label::Single
+            std::memcpy(pin_blob.p + x_lab, labels, sizeof(uint32_t) * (size_t)L);
+            uint64_t *lo = reinterpret_cast<uint64_t *>(pin_blob.p + x_loff);
+            for (int64_t r = 0; r <= R; ++r) lo[r] = label_off[r] - label_off[0];
+            d_labels = reinterpret_cast<const uint32_t *>(h2d_blob.p + x_lab);
+            d_label_off = reinterpret_cast<const uint64_t *>(h2d_blob.p + x_loff);
+            h2d_bytes = blob;
         }
-        pin_text.ensure((size_t)N + 16);
-        pin_off.ensure((size_t)R + 1);
-        HostClock hc;
-        par_copy(pin_text.p, arena, (size_t)N);
-        hc.lap("stage");
-        std::memcpy(pin_off.p, offsets, sizeof(uint64_t) * (size_t)(R + 1));
-        h2d_text.ensure((size_t)N + 16);
-        h2d_off.ensure((size_t)R + 1);
-        HIP_TRY(hipMemcpyAsync(h2d_text.p, pin_text.p, (size_t)N, hipMemcpyHostToDevice, stream));
-        HIP_TRY(hipMemcpyAsync(h2d_off.p, pin_off.p, sizeof(uint64_t) * (size_t)(R + 1), hipMemcpyHostToDevice, stream));
-        run_device(h2d_text.p, N, h2d_off.p, R,
-                   first_override >= 0 ? (uint64_t)first_override : cfg.first_record + n_records, stream, d_labels,
-                   d_label_off);
-        hc.lap("enqueue");
-        pin_u32.ensure((size_t)R + 3);
-        HIP_TRY(hipMemcpyAsync(pin_u32.p, row_off.p, sizeof(uint32_t) * (size_t)(R + 1), hipMemcpyDeviceToHost, stream));
-        pin_u32.p[R + 1] = pin_u32.p[R + 2] = 0;
-        if (span()) HIP_TRY(hipMemcpyAsync(pin_u32.p + R + 1, span_err.p, 4, hipMemcpyDeviceToHost, stream));
-        if (dt.kind == TOK_UNIGRAM) HIP_TRY(hipMemcpyAsync(pin_u32.p + R + 2, uni_err.p, 4, hipMemcpyDeviceToHost, stream));
-        HIP_TRY(hipStreamSynchronize(stream));
-        hc.lap("h2d+kernels");
+        HIP_TRY(hipMemcpyAsync(h2d_blob.p, pin_blob.p, h2d_bytes, hipMemcpyHostToDevice, stream));
+        const uint8_t *d_text = h2d_blob.p;
+        const uint64_t *d_off = reinterpret_cast<const uint64_t *>(h2d_blob.p + x_off);
+        run_device(d_text, N, d_off, R, first_override >= 0 ? (uint64_t)first_override : cfg.first_record + n_records,
+                   stream, d_labels, d_label_off);
+        // Small calls (a per-record push): the rows go straight to the back batch
+        // and a pre-allocated next one in the same pass, and the row offsets and
+        // error words come back through mapped memory -- one synchronisation.
+        const bool direct = R <= 4096 && N <= ((int64_t)1 << 20) && !store.empty() && !profiling;
+        uint32_t cap = 0;
+        const uint32_t *stat;
+        if (direct) {
+            if (!spare) spare = new_batch();
+            HostBatch *b0 = store.back(), *b1 = spare;
+            cap = (uint32_t)(2 * P.B - b0->rows);
+            DirectDst d{};
+            for (int i = 0; i < 2; ++i) {
+                HostBatch *b = i ? b1 : b0;
+                d.ids[i] = b->on_dev(b->ids);
+                d.am[i] = b->on_dev(b->am);
+                d.tt[i] = b->on_dev(b->tt);
+                d.lab[i] = b->on_dev(multi() ? (int32_t *)b->f32 : b->lab);
+            }
+            d.base = (uint32_t)b0->rows;
+            d.cap = cap;
+            d.B = (uint32_t)P.B;
+            ensure_stat((size_t)R + 3);
+            HIP_TRY(launch_rows_direct(d, row_off.p, R, o_ids.p, o_am.p, with_tt() ? o_tt.p : nullptr,
+                                       multi() ? reinterpret_cast<const int32_t *>(o_f32.p) : o_lab.p, P.S,
+                                       P.label_width, span() ? span_err.p : nullptr,
+                                       dt.kind == TOK_UNIGRAM ? uni_err.p : nullptr, stat_dev, stream));
+            hc.lap("enqueue");
+            HIP_TRY(hipStreamSynchronize(stream));
+            hc.lap("h2d+kernels+rows");
+            stat = pin_stat.p;
+        } else {
+            hc.lap("enqueue");
+            pin_u32.ensure((size_t)R + 3);
+            HIP_TRY(hipMemcpyAsync(pin_u32.p, row_off.p, sizeof(uint32_t) * (size_t)(R + 1), hipMemcpyDeviceToHost,
+                                   stream));
+            pin_u32.p[R + 1] = pin_u32.p[R + 2] = 0;
+            if (span()) HIP_TRY(hipMemcpyAsync(pin_u32.p + R + 1, span_err.p, 4, hipMemcpyDeviceToHost, stream));
+            if (dt.kind == TOK_UNIGRAM)
+                HIP_TRY(hipMemcpyAsync(pin_u32.p + R + 2, uni_err.p, 4, hipMemcpyDeviceToHost, stream));
+            HIP_TRY(hipStreamSynchronize(stream));
+            hc.lap("h2d+kernels");
+            stat = pin_u32.p;
+        }
         // where the reference panics (t5_data.rs:205-216: a label past S/4 or a
         // 101st sentinel) the host path fails the call before any batch is queued
-        if (pin_u32.p[R + 1])
-            throw ArgError("span: " + std::to_string(pin_u32.p[R + 1]) +
+        if (stat[R + 1])
+            throw ArgError("span: " + std::to_string(stat[R + 1]) +
                            " label/sentinel writes out of range (the reference panics)");
-        if (pin_u32.p[R + 2])
-            throw CapacityError("t5 tokenizer capacity exceeded (flags " + std::to_string(pin_u32.p[R + 2]) + ")");
-        const size_t S = (size_t)P.S, LW = (size_t)P.label_width;
+        if (stat[R + 2])
+            throw CapacityError("t5 tokenizer capacity exceeded (flags " + std::to_string(stat[R + 2]) + ")");
         // GenTokenizer::create_sync_batch per record (gen_batcher.rs:69-94):
         // rows fill the back batch (handle_internal_batch per chunk), at most
         // one finished batch is emitted per record.  Each run of rows landing
-        // contiguously in one batch is one segment, copied D2H below.
+        // contiguously in one batch and not written by the direct pass is one
+        // segment, copied D2H below.
         struct Seg {
             HostBatch *b;
             uint32_t dst, g0, n;
         };
         std::vector<Seg> segs;
         for (int64_t r = 0; r < R; ++r) {
-            const uint32_t g0 = pin_u32.p[r], g1 = pin_u32.p[r + 1];
+            const uint32_t g0 = stat[r], g1 = stat[r + 1];
+            if (g1 > g0 && store.empty())  // store.back_mut().unwrap() (gen_batcher.rs:45) panics
+                throw ArgError("a record after get_working_batch emptied the batch store (the reference panics)");
             for (uint32_t g = g0; g < g1; ++g) {
                 HostBatch *b = store.back();
-                if (!segs.empty() && segs.back().b == b && segs.back().g0 + segs.back().n == g) ++segs.back().n;
-                else segs.push_back(Seg{b, (uint32_t)b->rows, g, 1u});
+                if (g >= cap) {
+                    if (!segs.empty() && segs.back().b == b && segs.back().g0 + segs.back().n == g) ++segs.back().n;
+                    else segs.push_back(Seg{b, (uint32_t)b->rows, g, 1u});
+                }
                 b->rows++;
-                if (b->rows == P.B) store.push_back(new_batch());
+                if (b->rows == P.B) {
+                    store.push_back(spare ? spare : new_batch());
+                    spare = nullptr;
+                }
             }
             if (!store.empty() && store.front()->rows == P.B) {  // at most one batch per call
                 outbox.push_back(store.front());

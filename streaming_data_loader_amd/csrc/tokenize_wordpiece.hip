@@ -479,7 +479,11 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
     const Ctx C{&T, win, rbits, w0, text, N, off, R};
 #if defined(SDL_ABLATE) && SDL_ABLATE >= 3
     // diagnostic: load only; every record gets 0 ids (so later stages stay in bounds)
-    if (tid == 0) chunk_cnt[ci] = s_win[HALO_L + (ci & 1023)] & 0u;
+    {  // (an opaque use of the window keeps its loads: `x & 0u` let the compiler drop them all)
+        const uint32_t x = s_win[HALO_L + (ci & 1023)];
+        asm volatile("" ::"v"(x));
+    }
+    if (tid == 0) chunk_cnt[ci] = 0u;
     for (int64_t r = r_lo + tid; r <= R && (int64_t)off[r] < c1; r += TOK_THREADS) rec_local[r] = 0;
     return;
 #endif

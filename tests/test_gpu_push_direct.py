@@ -1,0 +1,83 @@
+"""Small calls on the host path (sdl_batcher_push / push_many of a few records).
+
+They take two shortcuts the large path does not: one workgroup runs the chunk scan,
+compaction, record framing, row scan and row map (k_downstream_small), and the rows go
+straight into the back batch and a pre-allocated next one in the same pass
+(k_rows_direct), rows past those two batches through the segment copy.  Checked here
+against the C oracle where a record's rows overrun the two batches many times over
+(S=16, B=1..3), for every tokenizer; and the reference's panic when a record arrives
+after get_working_batch emptied the store (gen_batcher.rs:45, store.back_mut().unwrap())."""
+import numpy as np
+import pytest
+
+import oracle_lib
+from streaming_data_loader_amd import batcher as Bt
+from streaming_data_loader_amd import native
+
+pytestmark = pytest.mark.gpu
+
+
+def drain(gt, texts):
+    got = []
+    for t in texts:
+        d = gt.create_sync_batch(t)
+        if d is not None:
+            got.append(d)
+    while True:
+        d = gt.get_working_batch()
+        if d is None or not d.rows:
+            break
+        got.append(d)
+    return got
+
+
+def planes(batches):
+    keys = ("input_ids", "attention_mask", "token_type_ids", "labels")
+    return [np.concatenate([np.asarray(getattr(d, k))[:d.rows] for d in batches]) for k in keys]
+
+
+@pytest.mark.parametrize("B", [1, 2, 3])
+def test_per_record_rows_past_the_direct_window_match_oracle(native_lib, records, B):
+    texts = records[:10]
+    S, k, seed = 16, 2, 77
+    gt = Bt.GenTokenizer(Bt.ModelType.Bert, Bt.BatchConfig(B, S), Bt.Mask(k, 103), Bt.TokenizerConfig(),
+                         chunk=True, seed=seed)
+    got = planes(drain(gt, texts))
+    want = oracle_lib.oracle_rows(oracle_lib.Tok(), texts, S, k, seed=seed, B=B)
+    assert got[0].shape[0] > 3 * B * len(texts)  # most rows went through the segment copy
+    for g, w in zip(got, want):
+        np.testing.assert_array_equal(g, w)
+
+
+@pytest.mark.parametrize("task", [Bt.TaskType.Clm, Bt.TaskType.Span])
+def test_per_record_equals_one_call_other_tokenizers(native_lib, records, task):
+    """byte-BPE (clm) and Unigram (span) through the small-call kernels, per record, equal
+    one push_many of the same records (> 1 MiB: the large path)."""
+    texts = [records[i % len(records)] for i in range(700)]
+    assert sum(len(t.encode()) for t in texts) > (1 << 20)
+    S, B = (128, 4)
+    a = Bt.GenTokenizer.from_config(Bt.get_case(task, False, S, B, 1234))
+    per = drain(a, texts)
+    b = Bt.GenTokenizer.from_config(Bt.get_case(task, False, S, B, 1234))
+    one = b.create_sync_batches(texts)
+    while True:
+        d = b.get_working_batch()
+        if d is None or not d.rows:
+            break
+        one.append(d)
+    keys = ("input_ids", "attention_mask", "labels")
+    for key in keys:
+        x = np.concatenate([np.asarray(getattr(d, key))[:d.rows] for d in per])
+        y = np.concatenate([np.asarray(getattr(d, key))[:d.rows] for d in one])
+        np.testing.assert_array_equal(x, y)
+
+
+def test_record_after_the_store_is_emptied_fails_like_the_reference(native_lib, records):
+    gt = Bt.GenTokenizer(Bt.ModelType.Bert, Bt.BatchConfig(2, 128), Bt.Mask(19, 103), Bt.TokenizerConfig(),
+                         chunk=True, seed=1)
+    drain(gt, records[:3])
+    assert gt.get_working_batch() is None
+    # fewer than 64 ids: the reference returns None before touching the store
+    assert gt.create_sync_batch("a short record") is None
+    with pytest.raises(native.SDLError, match="store"):
+        gt.create_sync_batch(records[0])

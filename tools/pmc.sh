@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 TASK="${1:-mlm}"
 ARENA="${2:-256}"
 CORPUS="${3:-fixture}"
-D=gpurun_out/pmc_${TASK}_${ARENA}_${CORPUS}
+D=gpurun_out/pmc_${TASK}_${ARENA}_${CORPUS}${PMC_TAG:-}
 mkdir -p $D
 export TMPDIR=/tmp
 ARGS="--task $TASK --steps 2 --warmup 1 --arena-mib $ARENA --corpus $CORPUS --no-cpu-baseline"
@@ -14,7 +14,8 @@ i=0
 while IFS= read -r group; do
   [[ -z "$group" ]] && continue
   i=$((i+1))
-  timeout -k 10 240 rocprofv3 --pmc $group --kernel-trace --output-format csv -d $D/p$i -o run -- python3 bench.py $ARGS > $D/p$i.out 2> $D/p$i.err
+  [[ -n "${PMC_ONLY:-}" && "$group" != "$PMC_ONLY" ]] && continue
+  SDL_LIB=${PMC_LIB:-} timeout -k 10 240 rocprofv3 --pmc $group --kernel-trace --output-format csv -d $D/p$i -o run -- python3 bench.py $ARGS > $D/p$i.out 2> $D/p$i.err
   rc=$?
   echo "pass $i [$group] exit $rc" | tee -a $D/passes.log
   case $rc in 0) ;; *) exit $rc;; esac

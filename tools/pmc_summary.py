@@ -25,8 +25,9 @@ def main():
     task = sys.argv[2] if len(sys.argv) > 2 else "mlm"
     arena = int(sys.argv[3]) if len(sys.argv) > 3 else 256
     corpus = sys.argv[4] if len(sys.argv) > 4 else "fixture"
-    os.makedirs("profiles/pmc", exist_ok=True)
-    dst = f"profiles/pmc/{task}_{arena}mib" + ("" if corpus == "fixture" else f"_{corpus}") + ".json"
+    out_dir = os.environ.get("PMC_SUMMARY_DIR", "profiles/pmc")  # (on a GPU box: under gpurun_out/)
+    os.makedirs(out_dir, exist_ok=True)
+    dst = f"{out_dir}/{task}_{arena}mib" + ("" if corpus == "fixture" else f"_{corpus}") + ".json"
     vals = defaultdict(lambda: defaultdict(list))  # kernel -> counter -> per-dispatch values
     for f in sorted(glob.glob(os.path.join(src, "**", "*counter_collection.csv"), recursive=True)):
         per = defaultdict(float)
@@ -45,6 +46,7 @@ def main():
         avg = {c: sum(v) / len(v) for c, v in cs.items()}
         ent = {"launches": max(len(v) for v in cs.values()), "counters": avg}
         if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
+            # (the uniform x2 upper bound; bench.py pmc_traffic splits the stream from the rest)
             ent["hbm_bytes_per_launch"] = int((2 * avg["FETCH_SIZE"] + avg["WRITE_SIZE"]) * 1024)
         out["kernels"][k] = ent
     with open(dst, "w") as fh:
