@@ -1630,8 +1630,12 @@ __device__ __forceinline__ void span_plane(int32_t *__restrict__ o, int W, int e
         }
         uint32_t x = run;
         SDL_DPP_SCAN(x, SDL_MAXU);
-        const uint32_t before = SDL_MAXU(wave_prev(x), carry);
-        carry = SDL_MAXU(carry, (uint32_t)lane_bcast((int)x, 63));
+        // (the DPP read once, unconditionally: inside the macro's ternary it was evaluated
+        // twice and the compiler made the second a branch -- a cross-lane read under a
+        // partial exec mask, which reads 0 from the inactive neighbours)
+        const uint32_t prev = wave_prev(x), last = (uint32_t)lane_bcast((int)x, 63);
+        const uint32_t before = prev > carry ? prev : carry;
+        carry = carry > last ? carry : last;
         int32_t v[4];
 #pragma unroll
         for (int w = 0; w < 4; ++w) {
@@ -1649,7 +1653,10 @@ __device__ __forceinline__ void span_plane(int32_t *__restrict__ o, int W, int e
     }
 }
 
-constexpr int SPAN_TABL = 128;  // plan entries per row held in LDS (the rest read from the plan)
+#ifndef SDL_SPAN_TABL
+#define SDL_SPAN_TABL 128
+#endif
+constexpr int SPAN_TABL = SDL_SPAN_TABL;  // plan entries per row held in LDS (the rest read from the plan)
 
 __global__ __launch_bounds__(256) void k_span_write(RowParams P, const uint32_t *__restrict__ tok,
                                                     const uint32_t *__restrict__ rec_tok,
@@ -1658,7 +1665,7 @@ __global__ __launch_bounds__(256) void k_span_write(RowParams P, const uint32_t 
                                                     const uint32_t *__restrict__ row_rec, SegSel sel,
                                                     int64_t rows_cap, RowOut out, SpanPlan pl) {
     __shared__ int32_t s_extra[100];
-    __shared__ uint2 s_tab[4][SPAN_TABL];
+    __shared__ uint2 s_tab[4][SPAN_TABL > 0 ? SPAN_TABL : 1];
     extern __shared__ int32_t s_dyn[];  // per wave: rid[S] | mk[S] u16 | mk2[LW] u16 (rounded)
     const int lane = lane_id();
     const int wid = (int)(threadIdx.x >> 6);

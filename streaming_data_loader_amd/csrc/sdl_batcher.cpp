@@ -282,7 +282,7 @@ struct sdl_batcher {
     DevBuf<uint2> span_tab, span_meta;
     DevBuf<uint32_t> span_ovf;
     bool span_two_phase = env_int("SDL_SPAN_TWO_PHASE", 0) != 0;
-    bool small_calls = env_int("SDL_SMALL_CALLS", 0) != 0;  // k_downstream_small + folded record bounds
+    bool small_calls = env_int("SDL_SMALL_CALLS", 1) != 0;  // k_downstream_small + folded record bounds
     // JsonText provider step (sdl_json_text_device)
     DevBuf<uint32_t> j_cnt, j_base, j_nl, j_len, j_rec, j_toff, j_ridx, j_inv, j_tail;
     DevBuf<uint2> j_span;

@@ -189,3 +189,28 @@ def test_host_path_fails_where_the_reference_panics(native_lib, records):
     with pytest.raises(native.SDLError, match="reference panics"):
         for t in records:
             gt.create_sync_batch(t)
+
+
+@pytest.mark.parametrize("rng_mode", [0, 1])
+@pytest.mark.parametrize("S,B_,gap,size", [(512, 256, 16.0, 2.0), (128, 8, 16.0, 2.0), (64, 16, 1.0, 1.0)])
+def test_span_two_phase_rows_match_oracle(torch, native_lib, t5tok, records, S, B_, gap, size, rng_mode,
+                                          monkeypatch):
+    """The two-phase span rows (SDL_SPAN_TWO_PHASE=1: k_span_plan + k_span_write, the rows
+    whose passes overrun the plan through the one-pass kernel's list mode) equal the oracle,
+    error counts included -- the (64, 1.0, 1.0) config overruns the plan on most rows."""
+    monkeypatch.setenv("SDL_SPAN_TWO_PHASE", "1")
+    rng = random.Random(S + B_ + 1)
+    blobs = [r.encode() for r in records] * 2 + hard_blobs(5, 150)
+    rng.shuffle(blobs)
+    db = DeviceBatcher(task=native.SDL_TASK_SPAN, batch_size=B_, sequence_length=S, seed=78,
+                       tokenizer=native.T5_PROXY_TOKENIZER, avg_span_gap=gap, avg_span_size=size, rng_mode=rng_mode)
+    res = run(torch, db, blobs, first_record=3)
+    G = res.rows()
+    ids, am, tt, lab = res.planes(G + (-G) % B_)
+    want, errs = oracle_span_rows(t5tok, blobs, B_, S, 78, gap, size, first_record=3, rng_mode=rng_mode)
+    assert G == want["input_ids"].shape[0]
+    np.testing.assert_array_equal(ids[:G], want["input_ids"])
+    np.testing.assert_array_equal(am[:G], want["attention_mask"])
+    np.testing.assert_array_equal(lab[:G], want["labels"])
+    assert res.label_errors() == errs
+    assert (ids[G:] == 0).all() and (am[G:] == 1).all() and (lab[G:] == -100).all()
