@@ -565,7 +565,7 @@ struct sdl_batcher {
         } else if (bpe) {
             // long pieces are > 64 bytes or run past their chunk's window (<= 1 per chunk)
             const uint32_t cap = (uint32_t)(N / 64 + n_chunks + 1);
-            long_count.ensure(1);
+            long_count.ensure(2);  // (count, k_bpe_long cursor)
             bpe_err.ensure(1);
             long_list.ensure(cap);
             long_scratch.ensure((size_t)N + 64);

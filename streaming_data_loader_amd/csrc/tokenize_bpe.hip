@@ -294,13 +294,19 @@ __device__ int bpe_wave(const DevTok &T, uint32_t &sym, int n, lds_u16 *tmp) {
 // right.  Pairs never straddle a word, so the runs of candidate bits do not
 // either and one leftmost_alternating serves every word.  Returns the final
 // symbol count; `heads` then marks where each word's ids start.
-__device__ int bpe_wave_seg(const DevTok &T, uint32_t &sym, int n, uint64_t &heads, lds_u32 *tmp) {
+//
+// A pair's merge value travels with its left symbol through the compaction; only
+// the pairs a step changed -- a merged symbol's, and its left neighbour's -- are
+// probed again (each probe is an L2 round trip on the step's critical path).
+__device__ int bpe_wave_seg(const DevTok &T, uint32_t &sym, int n, uint64_t &heads, lds_u32 *tmp, lds_u32 *tmpv) {
     const int lane = lane_id();
     const uint64_t lt = (1ull << lane) - 1ull;
+    bool need = true;  // this lane's pair value is not known
+    uint32_t vk = 0;   // ... or this
     for (;;) {
         const uint32_t nxt = wave_next(sym);
         const bool pair = lane < n - 1 && !((heads >> (lane + 1)) & 1ull);
-        const uint32_t v = pair ? merge_val(T, sym, nxt) : 0xFFFFFFFFu;
+        const uint32_t v = !pair ? 0xFFFFFFFFu : need ? merge_val(T, sym, nxt) : vk;
         const uint32_t rank = v >> 16;
         // segmented inclusive min scan (DPP), then each lane takes its word's last value
         uint32_t x = rank | ((uint32_t)((heads >> lane) & 1ull) << 16);
@@ -316,12 +322,20 @@ __device__ int bpe_wave_seg(const DevTok &T, uint32_t &sym, int n, uint64_t &hea
         const uint64_t live = (n == 64 ? ~0ull : ((1ull << n) - 1ull)) & ~(sel << 1);
         // heads are never merged away (no pair straddles one): each travels with
         // its symbol through the compaction and is re-balloted at its new lane
-        if ((live >> lane) & 1ull) tmp[__popcll(live & lt)] = (sym & 0xFFFFu) | (uint32_t)((heads >> lane) & 1ull) << 16;
+        // the pair changes for a merged symbol and for the lane left of one
+        const bool nd = ((sel >> lane) & 1ull) || (lane < 63 && ((sel >> (lane + 1)) & 1ull));
+        if ((live >> lane) & 1ull) {
+            const int at = __popcll(live & lt);
+            tmp[at] = (sym & 0xFFFFu) | (uint32_t)((heads >> lane) & 1ull) << 16 | (nd ? 1u : 0u) << 17;
+            tmpv[at] = v;
+        }
         __builtin_amdgcn_wave_barrier();
         n = __popcll(live);
         const uint32_t w = lane < n ? tmp[lane] : 0u;
         sym = w & 0xFFFFu;
-        heads = __ballot(w >> 16);
+        heads = __ballot((w >> 16) & 1u);
+        need = ((w >> 17) & 1u) != 0u;
+        vk = lane < n ? tmpv[lane] : 0xFFFFFFFFu;
         __builtin_amdgcn_wave_barrier();
     }
     return n;
@@ -373,6 +387,7 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
     __shared__ uint16_t s_stage[STAGE];       // ids staged at their piece's byte position
     __shared__ uint8_t s_cnt[CHUNK];          // ids per piece (<= BPE_MAX_WAVE), CNT_LONG = long piece
     __shared__ uint32_t s_tmp[64];
+    __shared__ uint32_t s_tmpv[64];  // bpe_wave_seg: pair values travelling with their symbols
     __shared__ uint32_t s_scratch[8];
 
     const int tid = threadIdx.x;
@@ -649,7 +664,7 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
             ++nw;
             ++q;
         }
-        const int k = bpe_wave_seg(T, sym, total, heads, (lds_u32 *)s_tmp);
+        const int k = bpe_wave_seg(T, sym, total, heads, (lds_u32 *)s_tmp, (lds_u32 *)s_tmpv);
         const uint64_t upto = lane == 63 ? heads : heads & ((2ull << lane) - 1ull);
         const int seg = __popcll(upto) - 1;
         const int start = upto ? 63 - __builtin_clzll(upto) : 0;
@@ -753,17 +768,26 @@ __global__ __launch_bounds__(64) void k_bpe_long(DevTok T, const uint8_t *__rest
     __shared__ uint16_t s_sym[LONG_LDS + 64];
     __shared__ uint32_t s_val[LONG_LDS + 64];  // merge_val of pair (j, j + 1); NOVAL: not known
     __shared__ uint16_t s_byte_id[256];
+    uint32_t n_long = *long_count;
+    if (n_long > long_cap) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(err, 1u);
+        n_long = long_cap;
+    }
+    if (blockIdx.x >= n_long) return;  // (the grid is sized for the held-out corpus; most texts have few)
     for (int i = threadIdx.x; i < 256; i += 64) s_byte_id[i] = T.byte_id[i];
     __syncthreads();
     const Ctx C{&T, nullptr, nullptr, INT64_MIN / 4, text, N, off, R};  // no window: global reads
     const int lane = lane_id();
     const uint64_t lt = (1ull << lane) - 1ull;
-    uint32_t n_long = *long_count;
-    if (n_long > long_cap) {
-        if (blockIdx.x == 0 && lane == 0) atomicOr(err, 1u);
-        n_long = long_cap;
-    }
-    for (uint32_t li = blockIdx.x; li < n_long; li += gridDim.x) {
+    // pieces are taken from a shared cursor (long_count[1]): their lengths vary a lot, and a
+    // static stride left waves idle behind the longest
+    uint32_t *cursor = const_cast<uint32_t *>(long_count) + 1;
+    auto next_piece = [&]() -> uint32_t {
+        uint32_t v = 0;
+        if (lane == 0) v = atomicAdd(cursor, 1u) + gridDim.x;
+        return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+    };
+    for (uint32_t li = blockIdx.x; li < n_long; li = next_piece()) {
         const int64_t p = (int64_t)list[li].pos;
         int64_t n = list[li].len;
         // record containing p (its end bounds the piece)
@@ -906,7 +930,7 @@ hipError_t launch_bpe_chunks(const DevTok &T, const uint8_t *text, int64_t N, co
                              uint16_t *scratch, uint32_t *err, hipStream_t st) {
     const int64_t n_chunks = (N + CHUNK - 1) / CHUNK;
     if (n_chunks == 0) return hipSuccess;
-    hipError_t e = hipMemsetAsync(long_count, 0, sizeof(uint32_t), st);
+    hipError_t e = hipMemsetAsync(long_count, 0, 2 * sizeof(uint32_t), st);  // count, k_bpe_long's cursor
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_bpe_chunks, dim3((unsigned)n_chunks), dim3(TOK_THREADS), 0, st, T, text, N, off, R, ranges,
                        tokc, chunk_cnt, chunk_ent, rec_local, long_count, long_list, long_cap);
@@ -914,7 +938,7 @@ hipError_t launch_bpe_chunks(const DevTok &T, const uint8_t *text, int64_t N, co
     // so the pieces in flight are what it runs on (r04: 1024 waves, one per SIMD, was 1.70 ms on
     // the held-out corpus); a block finds no piece and exits at once when there are fewer
 #ifndef SDL_BPE_LONG_GRID
-#define SDL_BPE_LONG_GRID 8192
+#define SDL_BPE_LONG_GRID 2048
 #endif
     const int64_t grid = std::min<int64_t>((int64_t)long_cap, SDL_BPE_LONG_GRID);
     if (grid > 0)

@@ -10,6 +10,7 @@ if [ "${PART:-a}" = a ]; then
     timeout -k 10 240 python bench.py --task $t > $O/bench_$t.json 2> $O/bench_$t.err || exit $?
     tail -c 300 $O/bench_$t.json; echo
     timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$t -o run -- python3 bench.py --task $t --no-cpu-baseline > $O/prof_$t.out 2>&1 || exit $?
+    find $O/prof_$t -name '*kernel_trace.csv' -delete  # (the per-dispatch trace: > 64 MiB over the tasks; the stats stay)
   done
 else
   for t in mlm clm span; do
