@@ -6,7 +6,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 O=gpurun_out/final_r04; mkdir -p $O; export TMPDIR=/tmp
 if [ "${PART:-a}" = a ]; then
-  for t in mlm clm span multi-label single-class; do
+  for t in ${TASKS:-mlm clm span multi-label single-class}; do
     timeout -k 10 240 python bench.py --task $t > $O/bench_$t.json 2> $O/bench_$t.err || exit $?
     tail -c 300 $O/bench_$t.json; echo
     timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$t -o run -- python3 bench.py --task $t --no-cpu-baseline > $O/prof_$t.out 2>&1 || exit $?

@@ -19,13 +19,21 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--task", default="mlm")
     ap.add_argument("--records", type=int, default=2000)
+    ap.add_argument("--dump", help="write the records length-prefixed (for tools/diag/push_bench) and exit")
     a = ap.parse_args()
     import bench
-    from streaming_data_loader_amd import batcher as Bt
     records = bench.corpus_records("fixture")
     order = bench.build_order(records, 4 << 20, 0x5D1B)
     texts = [records[i] for i in order][:a.records + 1]
+    if a.dump:
+        import struct
+        with open(a.dump, "wb") as f:
+            for x in texts:
+                b = x.encode()
+                f.write(struct.pack("<I", len(b)) + b)
+        return
     t = bench.TASKS[a.task]
+    from streaming_data_loader_amd import batcher as Bt
     tt = {"mlm": Bt.TaskType.Mlm, "clm": Bt.TaskType.Clm, "span": Bt.TaskType.Span}[a.task]
     gt = Bt.GenTokenizer.from_config(Bt.get_case(tt, False, t["S"], t["B"], 1234))
     gt.create_sync_batch(texts[0])  # warm
