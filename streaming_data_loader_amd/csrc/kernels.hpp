@@ -213,9 +213,20 @@ hipError_t launch_records(const RowParams &P, const uint64_t *off, int64_t R, in
                           int64_t n_chunks, const uint32_t *rec_local, uint32_t *rec_tok, uint32_t *rec_cnt,
                           uint32_t *rec_rows, SegSel sel, hipStream_t st);
 
+// Small pushes, no second round trip: global row g of the call goes to slot
+// base + g of the back batch (slots >= B: the next, pre-allocated one), rows
+// g < cap only (cap 0: off).  k_rows_direct copies them there and writes
+// row_off[0..R] and the two error words to `stat` (mapped pinned host memory) so
+// the host needs no D2H copy; for mlm / clm on the small-call path k_rows writes
+// them there itself (RowOut.direct) and k_downstream_small writes `stat`.
+struct DirectDst {
+    int32_t *ids[2], *am[2], *tt[2], *lab[2];  // back batch, next batch (device-mapped host)
+    uint32_t base, cap, B, pad;
+};
 struct RowOut {
     int32_t *input_ids, *attention_mask, *token_type_ids, *labels;
     float *labels_f32;
+    DirectDst direct;  // (k_rows) rows g < direct.cap go to the host batches; padding rows are skipped
 };
 
 // Small calls: chunk scan + compaction + records + row scan + row map in one
@@ -231,6 +242,7 @@ struct SmallDown {
     int64_t stride;
     const uint32_t *rec_local;
     uint32_t *rec_tok, *rec_cnt, *rec_rows, *row_off, *row_rec;
+    uint32_t *stat;  // or null: row_off[0..R] and two zero error words (mapped host memory, DirectDst)
 };
 hipError_t launch_downstream_small(const SmallDown &d, const RowParams &P, const uint64_t *off, int64_t R, int64_t N,
                                    hipStream_t st);
@@ -250,14 +262,7 @@ hipError_t launch_rows_to_host(const RowSeg *segs, int n_segs, uint32_t rows_per
                                const int32_t *am, const int32_t *tt, const int32_t *lab, int S, int LW,
                                hipStream_t st);
 
-// Small pushes, no second round trip: global row g of the call goes to slot
-// base + g of the back batch (slots >= B: the next, pre-allocated one), rows
-// g < cap only; the same launch writes row_off[0..R] and the two error words to
-// `stat` (mapped pinned host memory) so the host needs no D2H copy.
-struct DirectDst {
-    int32_t *ids[2], *am[2], *tt[2], *lab[2];  // back batch, next batch (device-mapped host)
-    uint32_t base, cap, B, pad;
-};
+// (DirectDst: see RowOut)
 hipError_t launch_rows_direct(const DirectDst &d, const uint32_t *row_off, int64_t R, const int32_t *ids,
                               const int32_t *am, const int32_t *tt, const int32_t *lab, int S, int LW,
                               const uint32_t *err0, const uint32_t *err1, uint32_t *stat, hipStream_t st);

@@ -451,6 +451,10 @@ __global__ __launch_bounds__(SCAN_SMALL_NT) void k_downstream_small(SmallDown d,
     __syncthreads();
     for (int64_t r = threadIdx.x; r < R; r += SCAN_SMALL_NT)
         for (uint32_t g = d.row_off[r]; g < d.row_off[r + 1]; ++g) d.row_rec[g] = (uint32_t)r;
+    if (d.stat) {
+        for (int64_t r = threadIdx.x; r <= R; r += SCAN_SMALL_NT) d.stat[r] = d.row_off[r];
+        if (threadIdx.x == 0) d.stat[R + 1] = d.stat[R + 2] = 0u;
+    }
 }
 
 hipError_t launch_downstream_small(const SmallDown &d, const RowParams &P, const uint64_t *off, int64_t R, int64_t N,
@@ -656,11 +660,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MR >= 4 ? S
     // (rng_mode 1) phase B of the rand masks, fused: per wave, next() and the row's mask bits
     __shared__ uint32_t s_nx[4][RM1 ? 256 * MR : 1];
     __shared__ uint32_t s_bt[4][RM1 ? 8 * MR : 1];
-    for (int64_t g = rs.g_lo + (int64_t)blockIdx.x * 4 + wid; g < rs.g_end; g += (int64_t)gridDim.x * 4) {
+    const DirectDst &dd = out.direct;
+    const int64_t g_end = dd.cap ? rs.g_real : rs.g_end;  // (direct: the host batch keeps its own padding)
+    for (int64_t g = rs.g_lo + (int64_t)blockIdx.x * 4 + wid; g < g_end; g += (int64_t)gridDim.x * 4) {
         int32_t *ids_o = out.input_ids + g * S;
         int32_t *am_o = out.attention_mask + g * S;
         int32_t *tt_o = out.token_type_ids ? out.token_type_ids + g * S : nullptr;
         int32_t *lb_o = out.labels ? out.labels + g * (int64_t)P.label_width : nullptr;
+        if (g < (int64_t)dd.cap) {  // a small push's row: straight into its host batch
+            const uint32_t slot = dd.base + (uint32_t)g, bi = slot >= dd.B ? 1u : 0u, row = slot - bi * dd.B;
+            ids_o = dd.ids[bi] + (size_t)row * S;
+            am_o = dd.am[bi] + (size_t)row * S;
+            tt_o = dd.tt[bi] ? dd.tt[bi] + (size_t)row * S : nullptr;
+            lb_o = dd.lab[bi] ? dd.lab[bi] + (size_t)row * P.label_width : nullptr;
+        }
         if (g >= (int64_t)G) {  // rows of the last batch nobody filled: initial values
 #pragma unroll
             for (int m = 0; m < MR; ++m) {

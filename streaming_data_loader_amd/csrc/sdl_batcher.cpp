@@ -326,6 +326,9 @@ struct sdl_batcher {
     PinBuf<uint32_t> pin_stat;  // direct pass: row offsets + error words (mapped)
     uint32_t *stat_dev = nullptr;
     HostBatch *spare = nullptr;  // direct pass: the next batch, allocated ahead
+    DirectDst fuse_dd{};          // ... its destinations, for run_device's fused small path
+    uint32_t *fuse_stat = nullptr;
+    bool fused_done = false;      // run_device wrote the direct rows and the row offsets
     PinBuf<RowSeg> seg_pin;
     DevBuf<RowSeg> seg_dev;
     void ensure_stat(size_t n) {
@@ -477,7 +480,11 @@ struct sdl_batcher {
         if (!fold && (multi() || single())) HIP_TRY(hipMemsetAsync(lab_err.p, 0, 4, st));
         mark(1);
         RowOut out{o_ids.p, o_am.p, with_tt() ? o_tt.p : nullptr, multi() ? nullptr : o_lab.p,
-                   multi() ? o_f32.p : nullptr};
+                   multi() ? o_f32.p : nullptr, DirectDst{}};
+        // a small mlm / clm push with its host batches ready (process_host): k_rows writes them
+        // and k_downstream_small the row offsets -- no k_rows_direct launch
+        fused_done = small && fuse_stat && (P.task == SDL_TASK_MLM || P.task == SDL_TASK_CLM);
+        if (fused_done) out.direct = fuse_dd;
         // everything after the tokenizer, for segment k, on stream s
         auto downstream = [&](int k, hipStream_t s) {
             const SegSel sel{seg_rb.p, k, k == sc.K - 1 ? 1 : 0};
@@ -488,7 +495,7 @@ struct sdl_batcher {
                                   uni || bpe ? chunk_ent.p : nullptr, bpe ? long_list.p : nullptr,
                                   bpe ? long_scratch.p : nullptr, uni ? uni_pool.p : nullptr,
                                   uni ? (int64_t)UNI_STAGE : (int64_t)STAGE, rec_local.p, rec_tok.p, rec_cnt.p,
-                                  rec_rows.p, row_off.p, row_rec.p};
+                                  rec_rows.p, row_off.p, row_rec.p, fused_done ? fuse_stat : nullptr};
                 HIP_TRY(launch_downstream_small(d, p, d_off, R, N, s));
             } else {
             if (!piped) mark(2);
@@ -636,34 +643,45 @@ struct sdl_batcher {
         HIP_TRY(hipMemcpyAsync(h2d_blob.p, pin_blob.p, h2d_bytes, hipMemcpyHostToDevice, stream));
         const uint8_t *d_text = h2d_blob.p;
         const uint64_t *d_off = reinterpret_cast<const uint64_t *>(h2d_blob.p + x_off);
-        run_device(d_text, N, d_off, R, first_override >= 0 ? (uint64_t)first_override : cfg.first_record + n_records,
-                   stream, d_labels, d_label_off);
         // Small calls (a per-record push): the rows go straight to the back batch
         // and a pre-allocated next one in the same pass, and the row offsets and
         // error words come back through mapped memory -- one synchronisation.
         const bool direct = R <= 4096 && N <= ((int64_t)1 << 20) && !store.empty() && !profiling;
         uint32_t cap = 0;
         const uint32_t *stat;
+        DirectDst dd{};
         if (direct) {
             if (!spare) spare = new_batch();
             HostBatch *b0 = store.back(), *b1 = spare;
             cap = (uint32_t)(2 * P.B - b0->rows);
-            DirectDst d{};
             for (int i = 0; i < 2; ++i) {
                 HostBatch *b = i ? b1 : b0;
-                d.ids[i] = b->on_dev(b->ids);
-                d.am[i] = b->on_dev(b->am);
-                d.tt[i] = b->on_dev(b->tt);
-                d.lab[i] = b->on_dev(multi() ? (int32_t *)b->f32 : b->lab);
+                dd.ids[i] = b->on_dev(b->ids);
+                dd.am[i] = b->on_dev(b->am);
+                dd.tt[i] = b->on_dev(b->tt);
+                dd.lab[i] = b->on_dev(multi() ? (int32_t *)b->f32 : b->lab);
             }
-            d.base = (uint32_t)b0->rows;
-            d.cap = cap;
-            d.B = (uint32_t)P.B;
+            dd.base = (uint32_t)b0->rows;
+            dd.cap = cap;
+            dd.B = (uint32_t)P.B;
             ensure_stat((size_t)R + 3);
-            HIP_TRY(launch_rows_direct(d, row_off.p, R, o_ids.p, o_am.p, with_tt() ? o_tt.p : nullptr,
-                                       multi() ? reinterpret_cast<const int32_t *>(o_f32.p) : o_lab.p, P.S,
-                                       P.label_width, span() ? span_err.p : nullptr,
-                                       dt.kind == TOK_UNIGRAM ? uni_err.p : nullptr, stat_dev, stream));
+            fuse_dd = dd;
+            fuse_stat = stat_dev;
+        }
+        fused_done = false;
+        struct FuseReset {  // (no other entry point may see this call's destinations, also on a throw)
+            uint32_t *&p;
+            ~FuseReset() { p = nullptr; }
+        } fuse_reset{fuse_stat};
+        run_device(d_text, N, d_off, R, first_override >= 0 ? (uint64_t)first_override : cfg.first_record + n_records,
+                   stream, d_labels, d_label_off);
+        fuse_stat = nullptr;
+        if (direct) {
+            if (!fused_done)
+                HIP_TRY(launch_rows_direct(dd, row_off.p, R, o_ids.p, o_am.p, with_tt() ? o_tt.p : nullptr,
+                                           multi() ? reinterpret_cast<const int32_t *>(o_f32.p) : o_lab.p, P.S,
+                                           P.label_width, span() ? span_err.p : nullptr,
+                                           dt.kind == TOK_UNIGRAM ? uni_err.p : nullptr, stat_dev, stream));
             hc.lap("enqueue");
             HIP_TRY(hipStreamSynchronize(stream));
             hc.lap("h2d+kernels+rows");
