@@ -295,8 +295,8 @@ def pmc_traffic(pmc, stream_bytes):
 
 
 def pmc_roofline(pmc, launch_ms, alg_bytes, stream_bytes=0):
-    """traffic = HBM bytes per launch (pmc_traffic: FETCH_SIZE with the gfx950 x2 applied to the
-    streamed text only, + WRITE_SIZE); issue = VALU and SALU wave-
+    """traffic = HBM bytes per launch (pmc_traffic: the text + offsets stream at its own bytes, the
+    rest of FETCH_SIZE past its calibrated share, + WRITE_SIZE); issue = VALU and SALU wave-
     instructions per launch over this run's HIP-event launch time against
     their issue peaks (the byte-walking kernels are bound by the scalar unit:
     one per CU, shared by its four SIMDs); `bound` names the busier one.
