@@ -395,7 +395,8 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
     unsigned long long stamp_prev_ = __builtin_amdgcn_s_memtime();
 #endif
     const int lane = tid;
-    const int64_t c0 = (int64_t)blockIdx.x * CHUNK;
+    const int64_t ci = xcd_chunk();  // this block's chunk
+    const int64_t c0 = ci * CHUNK;
     const int64_t c1 = c0 + CHUNK < N ? c0 + CHUNK : N;
     const int64_t w0 = c0 - HALO_L;
     const lds_u8 *win = (const lds_u8 *)s_win;
@@ -413,7 +414,7 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
         *reinterpret_cast<uint4 *>(s_win + (hp - w0)) = hv;
     }
     if (tid <= RBITS_WORDS) s_rbits[tid] = 0;
-    const int64_t ra = ranges[3 * blockIdx.x], rz = ranges[3 * blockIdx.x + 1], r_lo = ranges[3 * blockIdx.x + 2];
+    const int64_t ra = ranges[3 * ci], rz = ranges[3 * ci + 1], r_lo = ranges[3 * ci + 2];
     const int nrb = (int)(rz - ra);
     if (tid == 0) s_scratch[0] = s_scratch[1] = 0;
     __syncthreads();
@@ -578,7 +579,7 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
             if (li < long_cap) {
                 long_list[li].pos = (uint64_t)(c0 + prel);
                 long_list[li].len = nxt < 0 ? 0u : (uint32_t)(nxt - prel);  // 0: find the end
-                long_list[li].chunk = (uint32_t)blockIdx.x;
+                long_list[li].chunk = (uint32_t)ci;
                 long_list[li].k = 0;
             }
             stage[prel] = (uint16_t)(li & 0xFFFFu);
@@ -687,7 +688,7 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
     for (int i = a0; i < a1; ++i) mine += s_cnt[i] == CNT_LONG ? 1u : s_cnt[i];
     uint32_t total;
     const uint32_t base0 = block_excl_sum<TOK_THREADS>(mine, &total, s_scratch + 2);
-    uint32_t *dst = tokc + (int64_t)blockIdx.x * STAGE;
+    uint32_t *dst = tokc + ci * STAGE;
     uint32_t base = base0;
     // the list is packed in LDS first (window and classes are dead now) and
     // written as whole 16-B lanes: scattered 4-B non-temporal stores cost ~3.5x
@@ -731,7 +732,7 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
     }
     __syncthreads();
     BPE_STAMP(5);
-    if (tid == 0) chunk_cnt[blockIdx.x] = chunk_ent[blockIdx.x] = total;
+    if (tid == 0) chunk_cnt[ci] = chunk_ent[ci] = total;
     // record boundaries owned by this chunk: local entry offset of the first
     // piece at or after the boundary (k_bpe_long adds long pieces' extra ids)
     const int k_lo = (int)(r_lo - ra);

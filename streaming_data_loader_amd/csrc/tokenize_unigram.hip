@@ -615,7 +615,8 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
 
     const int tid = threadIdx.x;
     const int lane = tid;
-    const int64_t c0 = (int64_t)blockIdx.x * CHUNK;
+    const int64_t ci = xcd_chunk();  // this block's chunk
+    const int64_t c0 = ci * CHUNK;
     const int64_t c1 = c0 + CHUNK < N ? c0 + CHUNK : N;
     const int64_t w0 = c0 - HALO_L;
     const lds_u8 *win = (const lds_u8 *)s_bytes;
@@ -640,7 +641,7 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
     }
     if (tid < 2) *reinterpret_cast<uint4 *>(s_bytes + WIN + 16 * tid) = make_uint4(0, 0, 0, 0);
     if (tid <= RBITS_WORDS) s_rbits[tid] = 0;
-    const int64_t ra = ranges[3 * blockIdx.x], rz = ranges[3 * blockIdx.x + 1], r_lo = ranges[3 * blockIdx.x + 2];
+    const int64_t ra = ranges[3 * ci], rz = ranges[3 * ci + 1], r_lo = ranges[3 * ci + 2];
     const int nrb = (int)(rz - ra);
     if (tid < 8) s_scratch[tid] = 0;
     __syncthreads();
@@ -1204,7 +1205,7 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
     for (int i = a0; i < a1; ++i) mine += s_cnt[i] == CNT_LONG ? 1u : s_cnt[i];
     uint32_t total;
     uint32_t base = block_excl_sum<TOK_THREADS>(mine, &total, s_scratch + 8);
-    uint32_t *dst = tokc + (int64_t)blockIdx.x * UNI_STAGE;
+    uint32_t *dst = tokc + ci * UNI_STAGE;
     const uint32_t base0 = base;
     // the list is packed in LDS first (window and arena are dead now) and
     // written as whole 16-B lanes: scattered 4-B non-temporal stores cost ~3x
@@ -1217,7 +1218,7 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
         const int k = s_cnt[i];
         if (k == CNT_LONG) {
             const uint32_t it = atomicAdd(&counters[0], 1u);
-            if (it < item_cap) items[it] = make_uint4((uint32_t)blockIdx.x, base, (uint32_t)prel, s_stage[prel]);
+            if (it < item_cap) items[it] = make_uint4((uint32_t)ci, base, (uint32_t)prel, s_stage[prel]);
             else atomicOr(err, 8u);
             if (packed) pk[base] = LMARK;
             else dst[base] = LMARK;
@@ -1250,7 +1251,7 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
         base += s_cnt[i] == CNT_LONG ? 1u : s_cnt[i];
     }
     __syncthreads();
-    if (tid == 0) chunk_cnt[blockIdx.x] = chunk_ent[blockIdx.x] = total;
+    if (tid == 0) chunk_cnt[ci] = chunk_ent[ci] = total;
     // record boundaries owned by this chunk: entry offset of the first piece at
     // or after the boundary (k_unigram_long adds long items' extra ids)
     const int k_lo = (int)(r_lo - ra);

@@ -445,7 +445,7 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
 #ifdef SDL_STAMPS
     unsigned long long stamp_prev_ = __builtin_amdgcn_s_memtime();
 #endif
-    const int64_t ci = c_begin + (int64_t)blockIdx.x;  // this block's chunk
+    const int64_t ci = c_begin + xcd_chunk();  // this block's chunk
     const int64_t c0 = ci * CHUNK;
     const int64_t c1 = c0 + CHUNK < N ? c0 + CHUNK : N;
     const int64_t w0 = c0 - HALO_L;
