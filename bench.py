@@ -290,7 +290,10 @@ def pmc_traffic(pmc, stream_bytes):
              "fetch_size_reported": int(fetch), "stream_fetch_ratio": round(ratio, 4),
              "stream_fetch_ratio_from": "load-only build FETCH_SIZE (profiles/pmc/stream_calibration.json)"
              if cal else "guide's 1/2 (no calibration file)",
-             "uniform_x2_upper_bound": int(2 * fetch + write)}
+             "uniform_x2_upper_bound": int(2 * fetch + write),
+             "estimate": "the stream ratio is measured on the WordPiece load-only build and applied to every "
+                         "chunk kernel (they share the window geometry); `traffic` is an estimate between "
+                         "FETCH_SIZE + WRITE_SIZE as reported and uniform_x2_upper_bound"}
     return traffic, split
 
 
@@ -652,14 +655,22 @@ def main(argv=None):
     # names the roofline that binds the kernel: the busier issue unit when the
     # PMC summary shows it closer to its peak than HBM traffic is to its own
     hbm_frac = achieved / HBM_PEAK_GBPS
-    bound = issue["bound"] if issue is not None and issue["frac"] > hbm_frac else "hbm"
+    # the HBM side of the verdict takes the largest of the algorithmic bytes, the calibrated
+    # traffic and the uniform-x2 upper bound, so the calibration cannot tip it toward "issue"
+    hbm_frac_hi = hbm_frac
+    if traffic is not None:
+        hbm_frac_hi = max(hbm_frac_hi, traffic / (tok_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS)
+    if pmc is not None and pmc.get("_split"):
+        hbm_frac_hi = max(hbm_frac_hi, pmc["_split"]["uniform_x2_upper_bound"] / (tok_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS)
+    bound = issue["bound"] if issue is not None and issue["frac"] > hbm_frac_hi else "hbm"
     if soak is not None:
         line["determinism"] = soak
     line["roofline"] = {"bound": bound, "kernel": task["kernel"], "achieved": round(achieved, 2),
                         "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(hbm_frac, 5),
                         "traffic": traffic, "issue": issue,
                         "traffic_split": pmc.get("_split") if pmc is not None else None,
-                        "algorithmic_bytes_per_launch": tok_bytes, "avg_launch_ms": round(tok_ms, 4)}
+                        "algorithmic_bytes_per_launch": tok_bytes, "avg_launch_ms": round(tok_ms, 4),
+                        "hbm_frac_upper": round(hbm_frac_hi, 5)}
     if bound != "hbm":
         line["roofline"]["bound_note"] = (f"{bound} at {issue['frac']:.2f} of its issue peak binds this kernel; "
                                           "achieved/peak/frac are its algorithmic HBM bytes against 8 TB/s")

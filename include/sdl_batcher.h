@@ -303,7 +303,11 @@ void sdl_multi_destroy(sdl_multi *m);
  * devices[0]), shard k's records keyed from the global index of its first record.
  * n_emitted[k] (n_devices entries, may be NULL) = batches shard k queued; pop them
  * with sdl_batcher_next / sdl_batcher_flush on sdl_multi_handle(m, k).  The global
- * record index continues across calls. */
+ * record index continues across calls.  When a shard fails, the shards that
+ * succeeded have queued their batches: n_emitted is written for every shard either
+ * way (0 for a failed one), and the multi handle is poisoned -- later pushes return
+ * SDL_ERR_STATE -- since re-pushing the records would duplicate the committed
+ * shards' rows. */
 int sdl_multi_push_many(sdl_multi *m, const uint8_t *arena, const uint64_t *offsets, size_t n_records,
                         const uint32_t *labels, const uint64_t *label_offsets, size_t *n_emitted);
 /* Shard k's handle (also for sdl_process_device on a device-resident shard with

@@ -516,14 +516,19 @@ class ShardedGenTokenizer:
         """Shard k's sdl_batcher handle (owned by this object)."""
         return native.load().sdl_multi_handle(self._m, k)
 
-    def push_arena(self, arena, offsets):
-        """sdl_multi_push_many: returns, per shard, the batches it emitted (in order)."""
+    def push_arena(self, arena, offsets, labels=None, label_offsets=None):
+        """sdl_multi_push_many: returns, per shard, the batches it emitted (in order).
+        labels / label_offsets (uint32 values, uint64 offsets into them) for the
+        multi-label and single-class tasks, as sdl_batcher_push_many takes them."""
         arena = np.ascontiguousarray(arena, np.uint8)
         offsets = np.ascontiguousarray(offsets, np.uint64)
+        lv = None if labels is None else np.ascontiguousarray(labels, np.uint32)
+        lo = None if label_offsets is None else np.ascontiguousarray(label_offsets, np.uint64)
         n = (ctypes.c_size_t * self.n)()
         L = native.load()
         native.check(L.sdl_multi_push_many(self._m, arena.ctypes.data, offsets.ctypes.data, offsets.size - 1,
-                                           None, None, n))
+                                           None if lv is None or lv.size == 0 else lv.ctypes.data,
+                                           None if lo is None else lo.ctypes.data, n))
         out = []
         for k in range(self.n):
             got, b, h = [], native.Batch(), self.handle(k)

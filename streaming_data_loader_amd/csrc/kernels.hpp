@@ -242,7 +242,9 @@ struct SmallDown {
     int64_t stride;
     const uint32_t *rec_local;
     uint32_t *rec_tok, *rec_cnt, *rec_rows, *row_off, *row_rec;
-    uint32_t *stat;  // or null: row_off[0..R] and two zero error words (mapped host memory, DirectDst)
+    uint32_t *stat;  // or null: row_off[0..R], a zero label-error word and the tokenizer's error word
+                     // (mapped host memory, DirectDst)
+    const uint32_t *tok_err;  // or null: the Unigram capacity flags (uni_err), copied to stat[R + 2]
 };
 hipError_t launch_downstream_small(const SmallDown &d, const RowParams &P, const uint64_t *off, int64_t R, int64_t N,
                                    hipStream_t st);

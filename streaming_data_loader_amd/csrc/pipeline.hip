@@ -453,7 +453,10 @@ __global__ __launch_bounds__(SCAN_SMALL_NT) void k_downstream_small(SmallDown d,
         for (uint32_t g = d.row_off[r]; g < d.row_off[r + 1]; ++g) d.row_rec[g] = (uint32_t)r;
     if (d.stat) {
         for (int64_t r = threadIdx.x; r <= R; r += SCAN_SMALL_NT) d.stat[r] = d.row_off[r];
-        if (threadIdx.x == 0) d.stat[R + 1] = d.stat[R + 2] = 0u;
+        if (threadIdx.x == 0) {
+            d.stat[R + 1] = 0u;
+            d.stat[R + 2] = d.tok_err ? *d.tok_err : 0u;  // a t5 tokenizer under mlm / clm
+        }
     }
 }
 

@@ -283,6 +283,9 @@ struct sdl_batcher {
     DevBuf<uint32_t> span_ovf;
     bool span_two_phase = env_int("SDL_SPAN_TWO_PHASE", 0) != 0;
     bool small_calls = env_int("SDL_SMALL_CALLS", 1) != 0;  // k_downstream_small + folded record bounds
+    // test hook: clamp the Unigram long-item list (0 = its N / 8 + chunks bound), so the capacity
+    // flag can be raised through every path that reports it
+    uint32_t uni_item_cap = (uint32_t)std::max(0, env_int("SDL_UNI_ITEM_CAP", 0));
     // JsonText provider step (sdl_json_text_device)
     DevBuf<uint32_t> j_cnt, j_base, j_nl, j_len, j_rec, j_toff, j_ridx, j_inv, j_tail;
     DevBuf<uint2> j_span;
@@ -495,7 +498,8 @@ struct sdl_batcher {
                                   uni || bpe ? chunk_ent.p : nullptr, bpe ? long_list.p : nullptr,
                                   bpe ? long_scratch.p : nullptr, uni ? uni_pool.p : nullptr,
                                   uni ? (int64_t)UNI_STAGE : (int64_t)STAGE, rec_local.p, rec_tok.p, rec_cnt.p,
-                                  rec_rows.p, row_off.p, row_rec.p, fused_done ? fuse_stat : nullptr};
+                                  rec_rows.p, row_off.p, row_rec.p, fused_done ? fuse_stat : nullptr,
+                                  uni ? uni_err.p : nullptr};
                 HIP_TRY(launch_downstream_small(d, p, d_off, R, N, s));
             } else {
             if (!piped) mark(2);
@@ -563,7 +567,9 @@ struct sdl_batcher {
             uni_pool.ensure((size_t)N + 1024 * 1024);
             uni_scratch.ensure(unigram_scratch_bytes(lane_blocks, huge_blocks));
             chunk_ent.ensure((size_t)n_chunks + 1);
-            UniWork W{uni_counters.p, uni_items.p, (uint32_t)std::min<size_t>(uni_items.cap, 0xFFFFFFFFu), uni_pool.p,
+            uint32_t item_cap = (uint32_t)std::min<size_t>(uni_items.cap, 0xFFFFFFFFu);
+            if (uni_item_cap) item_cap = std::min(item_cap, uni_item_cap);
+            UniWork W{uni_counters.p, uni_items.p, item_cap, uni_pool.p,
                       (uint32_t)std::min<size_t>(uni_pool.cap, 0x3FFFFFFF), uni_huge.p, (uint32_t)uni_huge.cap,
                       uni_items2.p, (uint32_t)uni_items2.cap, uni_scratch.p, lane_blocks, huge_blocks, uni_err.p};
             HIP_TRY(launch_unigram_chunks(dt, d_text, N, d_off, R, ranges.p, tokc.p, chunk_cnt.p, chunk_ent.p,
@@ -915,8 +921,9 @@ int sdl_batcher_create(const sdl_config *cfg, const char *tokenizer_path, const 
                 const int adj = t.uscore_adj[(size_t)v.id];
                 if (adj == 0) continue;
                 const float f = t.uscore32[(size_t)v.id];
-                if (v.id > 0x7FFF || !(f < 0.0f))
-                    throw std::runtime_error("Unigram: a score off its f32 needs id < 32768 and a negative score");
+                // (0x7FFF | 0x8000 is the chunk kernel's "no piece" word: tokenize_unigram.hip NO_PIECE)
+                if (v.id >= 0x7FFF || !(f < 0.0f))
+                    throw std::runtime_error("Unigram: a score off its f32 needs id < 32767 and a negative score");
                 v.id |= 0x8000;
                 if (adj < 0) {
                     const float g = -f;
@@ -2181,6 +2188,7 @@ int sdl_shard_records(const uint64_t *offsets, uint64_t n_records, uint32_t n_sh
 struct sdl_multi {
     std::vector<sdl_batcher *> h;
     uint64_t next_record = 0;  // global index of the next call's first record
+    bool poisoned = false;     // a shard failed: the others committed their part of that push
     ~sdl_multi() {
         for (sdl_batcher *x : h) sdl_batcher_destroy(x);
     }
@@ -2210,6 +2218,7 @@ int sdl_multi_push_many(sdl_multi *m, const uint8_t *arena, const uint64_t *offs
                         const uint32_t *labels, const uint64_t *label_offsets, size_t *n_emitted) {
     if (!m || !offsets || (!arena && n_records && offsets[n_records])) return fail(SDL_ERR_ARG, "null argument");
     if (offsets[0] != 0) return fail(SDL_ERR_ARG, "offsets must start at 0");
+    if (m->poisoned) return fail(SDL_ERR_STATE, "an earlier push failed on a shard; the stream is not resumable");
     const uint32_t n = (uint32_t)m->h.size();
     std::vector<uint64_t> bounds(n + 1);
     if (int rc = sdl_shard_records(offsets, n_records, n, bounds.data())) return rc;
@@ -2237,10 +2246,13 @@ int sdl_multi_push_many(sdl_multi *m, const uint8_t *arena, const uint64_t *offs
     for (uint32_t k = 1; k < n; ++k) th.emplace_back(run, k);
     run(0);
     for (auto &t : th) t.join();
+    if (n_emitted)  // also on failure: the shards that succeeded have queued these
+        for (uint32_t k = 0; k < n; ++k) n_emitted[k] = rcs[k] == SDL_OK ? emitted[k] : 0;
     for (uint32_t k = 0; k < n; ++k)
-        if (rcs[k] != SDL_OK) return fail(rcs[k], "shard " + std::to_string(k) + ": " + errs[k]);
+        if (rcs[k] != SDL_OK) {
+            m->poisoned = true;
+            return fail(rcs[k], "shard " + std::to_string(k) + ": " + errs[k]);
+        }
     m->next_record += n_records;
-    if (n_emitted)
-        for (uint32_t k = 0; k < n; ++k) n_emitted[k] = emitted[k];
     return SDL_OK;
 }

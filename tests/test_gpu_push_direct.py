@@ -81,3 +81,52 @@ def test_record_after_the_store_is_emptied_fails_like_the_reference(native_lib, 
     assert gt.create_sync_batch("a short record") is None
     with pytest.raises(native.SDLError, match="store"):
         gt.create_sync_batch(records[0])
+
+
+@pytest.mark.parametrize("model", [Bt.ModelType.Bert, Bt.ModelType.Gpt2])
+def test_unigram_capacity_flag_on_the_fused_small_push(native_lib, records, model, monkeypatch):
+    """mlm / clm on the t5 tokenizer take the fused small push (k_rows writes the host
+    batches, k_downstream_small the status words): a Unigram capacity overflow must still
+    fail the call, as it does on the direct and large paths.  SDL_UNI_ITEM_CAP clamps the
+    long-item list so a record with a few > 16-byte words overflows it."""
+    monkeypatch.setenv("SDL_UNI_ITEM_CAP", "1")
+    gt = Bt.GenTokenizer(model, Bt.BatchConfig(4, 128), Bt.Mask(19, 103) if model == Bt.ModelType.Bert else
+                         Bt.Gpt(), Bt.TokenizerConfig(native.T5_PROXY_TOKENIZER), chunk=True, seed=3)
+    long_words = " ".join(["internationalization", "characteristically", "uncharacteristically"])
+    with pytest.raises(native.SDLError, match="capacity"):
+        gt.create_sync_batch(records[0] + " " + long_words)
+
+
+def test_unigram_small_push_without_overflow_raises_nothing(native_lib, records):
+    """The same pairing without the clamp: long words are items, no error word is set."""
+    gt = Bt.GenTokenizer(Bt.ModelType.Bert, Bt.BatchConfig(4, 128), Bt.Mask(19, 103),
+                         Bt.TokenizerConfig(native.T5_PROXY_TOKENIZER), chunk=True, seed=3)
+    for t in records[:8]:
+        gt.create_sync_batch(t + " internationalization characteristically")
+
+
+def test_short_calls_after_long_ones_read_no_stale_status(native_lib, records):
+    """The mapped status words (row offsets, label and tokenizer error words) are rewritten
+    by every call: push_many of many records, then single records, then a few, equal the
+    per-record sequence row for row and raise nothing."""
+    S, B, seed = 128, 4, 21
+    seq = [records[:40], records[40:41], records[41:44], records[44:45], records[45:50]]
+    a = Bt.GenTokenizer(Bt.ModelType.Bert, Bt.BatchConfig(B, S), Bt.Mask(19, 103), Bt.TokenizerConfig(),
+                        chunk=True, seed=seed)
+    mixed = []
+    for part in seq:
+        if len(part) == 1:
+            d = a.create_sync_batch(part[0])
+            mixed += [d] if d is not None else []
+        else:
+            mixed += a.create_sync_batches(part)
+    while True:
+        d = a.get_working_batch()
+        if d is None or not d.rows:
+            break
+        mixed.append(d)
+    b = Bt.GenTokenizer(Bt.ModelType.Bert, Bt.BatchConfig(B, S), Bt.Mask(19, 103), Bt.TokenizerConfig(),
+                        chunk=True, seed=seed)
+    per = drain(b, records[:50])
+    for g, w in zip(planes(mixed), planes(per)):
+        np.testing.assert_array_equal(g, w)

@@ -1,10 +1,10 @@
 #!/bin/bash
-# r04 bench lines (fixture, every task; PMC traffic from profiles/pmc) + rocprof kernel stats.
+# bench lines (fixture, every task; PMC traffic from profiles/pmc) + rocprof kernel stats.
 # PART=a: mlm clm span multi-label single-class with CPU baselines and rocprof; PART=b: held-out
 # and rng_mode 1 lines.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-O=gpurun_out/final_r04; mkdir -p $O; export TMPDIR=/tmp
+O=gpurun_out/${OUT:-final}; mkdir -p $O; export TMPDIR=/tmp
 if [ "${PART:-a}" = a ]; then
   for t in ${TASKS:-mlm clm span multi-label single-class}; do
     timeout -k 10 240 python bench.py --task $t > $O/bench_$t.json 2> $O/bench_$t.err || exit $?
