@@ -223,6 +223,19 @@ typedef struct sdl_inflated {
 int sdl_gzip_inflate_device(sdl_batcher *h, const uint8_t *d_gz, uint64_t gz_len, const uint64_t *d_member_offsets,
                             uint64_t n_members, void *stream, sdl_inflated *out);
 
+/* The reference-exact variant (opt-in): every range [d_file_offsets[f],
+ * d_file_offsets[f+1]) is one FILE, and only its first gzip member is inflated --
+ * what async-compression's GzipDecoder with multiple_members off returns
+ * (gzip_file_provider.rs:18, 64): `cat a.gz b.gz` yields a's lines, a BGZF file its
+ * first block's.  The member's end is found on the device (the next offset where a
+ * member header could start, else the file's end; a candidate inside the member's
+ * own compressed data fails its decode and the next one is tried).  Output and
+ * status as sdl_gzip_inflate_device, one member per file.  Limit: a first member
+ * followed by bytes that hold no gzip header (trailing garbage) fails with
+ * SDL_ERR_DATA (GZ_E_TRAIL) instead of being ignored. */
+int sdl_gzip_inflate_first_device(sdl_batcher *h, const uint8_t *d_gz, uint64_t gz_len, const uint64_t *d_file_offsets,
+                                  uint64_t n_files, void *stream, sdl_inflated *out);
+
 /* Host only (no GPU): member byte ranges of one gzip file for
  * sdl_gzip_inflate_device.  BGZF files (every member carries the 'BC' extra
  * subfield with its size, as bgzip writes them) split into their members; any

@@ -196,7 +196,11 @@ struct RowParams {
     uint64_t seed;
     uint64_t first_record;
     int32_t rng_mode;              // MLM masks: 0 Philox contract, 1 rand 0.8.5 StdRng (k_mask_rand)
-    const uint16_t *mask_j;        // rng_mode 1: per row, S shuffle swap indices (k_mask_rand_walk)
+    // rng_mode 1: the rows' mask bits (S/32 words a row, bit p = position p masked): rows of
+    // chunk k < mask_kmin from mask_bits0 (per record: k_mask_rand_rec + k_mask_bits_rec, run
+    // beside the tokenizer), the others from mask_bitsg (per row: k_mask_rand16)
+    const uint32_t *mask_bits0, *mask_bitsg;
+    int32_t mask_w, mask_kmin;
     // span (T5Data): trunc(avg - z) draws as CDF tables (RNG contract) and
     // the <extra_id_k> ids (device pointer, 100 entries)
     int32_t gap_kmin, gap_n, size_kmin, size_n;

@@ -159,10 +159,11 @@ void print_gz_cycles() {
 
 // ---- lane per member: header magic + ISIZE ------------------------------------
 __global__ void k_gz_size(const uint8_t *__restrict__ in, uint64_t in_len, const uint64_t *__restrict__ moff, uint64_t n,
-                          uint32_t *__restrict__ size, int32_t *__restrict__ status, unsigned long long *__restrict__ total) {
+                          uint32_t *__restrict__ size, int32_t *__restrict__ status, unsigned long long *__restrict__ total,
+                          const uint64_t *__restrict__ mend) {
     const uint64_t m = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (m >= n) return;
-    const uint64_t a = moff[m], z = moff[m + 1];
+    const uint64_t a = moff[m], z = mend ? mend[m] : moff[m + 1];
     int32_t st = GZ_OK;
     uint32_t sz = 0;
     if (a > z || z > in_len) st = GZ_E_RANGE;
@@ -229,7 +230,7 @@ __global__ __launch_bounds__(64) void k_inflate_t(const uint8_t *__restrict__ in
     } else {
         if (status[m] != GZ_OK) return;  // sizing found the member unusable
         ma = moff[m];
-        mz = moff[m + 1];
+        mz = ca.mend ? ca.mend[m] : moff[m + 1];
         dst = out + ooff[m];
         cap = ooff[m + 1] - ooff[m];
     }
@@ -1398,18 +1399,49 @@ hipError_t launch_gz_crc_fold(const uint32_t *crc, const uint32_t *shift, uint64
 }
 
 hipError_t launch_gz_size(const uint8_t *in, uint64_t in_len, const uint64_t *moff, uint64_t n, uint32_t *size,
-                          int32_t *status, unsigned long long *total, hipStream_t st) {
+                          int32_t *status, unsigned long long *total, hipStream_t st, const uint64_t *mend) {
     if (!n) return hipSuccess;
     hipLaunchKernelGGL(k_gz_size, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, in, in_len, moff, n, size, status,
-                       total);
+                       total, mend);
     return hipGetLastError();
 }
 
 hipError_t launch_inflate(const uint8_t *in, const uint64_t *moff, uint64_t n, const uint32_t *ooff, uint8_t *out,
-                          int32_t *status, uint32_t *tcrc, hipStream_t st) {
+                          int32_t *status, uint32_t *tcrc, hipStream_t st, const uint64_t *mend) {
     if (!n) return hipSuccess;
-    hipLaunchKernelGGL(k_inflate_t<false>, dim3((unsigned)n), dim3(64), 0, st, in, moff, n, ooff, out, status, tcrc,
-                       GzChunkArgs{});
+    GzChunkArgs a{};
+    a.mend = mend;
+    hipLaunchKernelGGL(k_inflate_t<false>, dim3((unsigned)n), dim3(64), 0, st, in, moff, n, ooff, out, status, tcrc, a);
+    return hipGetLastError();
+}
+
+// ---- where a file's first member may end -----------------------------------------
+// async-compression's GzipDecoder (gzip_file_provider.rs:18, 64; no multiple_members) decodes
+// a file's first member and stops.  Without decoding, the member's end is only known as a
+// candidate: the next offset where a member header could start (or the file's end).  A thread
+// per 16 bytes tests every offset; candidates are rare in DEFLATE data (a 3-byte pattern plus
+// the flag byte), so the file lookup (binary search) and atomicMin run for few of them.
+__global__ void k_gz_next_header(const uint8_t *__restrict__ in, uint64_t in_len, const uint64_t *__restrict__ foff,
+                                 uint64_t n, const uint64_t *__restrict__ from, unsigned long long *__restrict__ next) {
+    const uint64_t q0 = 16 * ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x);
+    if (q0 >= in_len) return;
+    for (uint64_t p = q0; p < q0 + 16 && p + 4 <= in_len; ++p) {
+        if (in[p] != 0x1f || in[p + 1] != 0x8b || in[p + 2] != 8 || (in[p + 3] & 0xE0u)) continue;
+        uint64_t lo = 0, hi = n;  // the file holding p: foff[f] <= p < foff[f + 1]
+        while (lo < hi) {
+            const uint64_t mid = (lo + hi) >> 1;
+            if (foff[mid + 1] <= p) lo = mid + 1; else hi = mid;
+        }
+        if (lo < n && p > from[lo]) atomicMin(&next[lo], (unsigned long long)p);
+    }
+}
+
+hipError_t launch_gz_next_header(const uint8_t *in, uint64_t in_len, const uint64_t *foff, uint64_t n,
+                                 const uint64_t *from, unsigned long long *next, hipStream_t st) {
+    if (!n || !in_len) return hipSuccess;
+    const uint64_t threads = (in_len + 15) / 16;
+    hipLaunchKernelGGL(k_gz_next_header, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, in, in_len, foff, n,
+                       from, next);
     return hipGetLastError();
 }
 

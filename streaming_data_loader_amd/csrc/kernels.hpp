@@ -105,10 +105,17 @@ enum : int32_t {
 struct X2N {
     uint32_t t[32];  // x^(2^k) mod P (zlib's x2n_table)
 };
+// mend (or null): member m is [moff[m], mend[m]) instead of [moff[m], moff[m + 1]) -- a file's
+// first member inside the file's range (sdl_gzip_inflate_first_device)
 hipError_t launch_gz_size(const uint8_t *in, uint64_t in_len, const uint64_t *moff, uint64_t n, uint32_t *size,
-                          int32_t *status, unsigned long long *total, hipStream_t st);
+                          int32_t *status, unsigned long long *total, hipStream_t st, const uint64_t *mend = nullptr);
 hipError_t launch_inflate(const uint8_t *in, const uint64_t *moff, uint64_t n, const uint32_t *ooff, uint8_t *out,
-                          int32_t *status, uint32_t *tcrc, hipStream_t st);
+                          int32_t *status, uint32_t *tcrc, hipStream_t st, const uint64_t *mend = nullptr);
+// Per file f (bytes [foff[f], foff[f + 1])): next[f] = min(next[f], the first offset p > from[f] in the
+// file where a gzip member header could start (1f 8b 08, no reserved flag bits)) -- where the file's
+// first member may end; next[] holds the file end on entry
+hipError_t launch_gz_next_header(const uint8_t *in, uint64_t in_len, const uint64_t *foff, uint64_t n,
+                                 const uint64_t *from, unsigned long long *next, hipStream_t st);
 hipError_t launch_gz_crc(const uint32_t *ooff, const uint8_t *out, uint64_t n, const uint32_t *tcrc, const X2N &x2n,
                          int32_t *status, uint32_t *bad, hipStream_t st);
 
@@ -143,6 +150,7 @@ struct GzChunkArgs {
     uint32_t *len;              // out: values produced
     uint32_t *flags;            // out: GZC_*
     int32_t *status;            // out: GZ_*
+    const uint64_t *mend;       // (one-wave members) member m ends at mend[m] instead of moff[m + 1], or null
 };
 // first dynamic-block header at or past nominal[c] (bits), searching `span` bits;
 // found[c] = its bit or GZ_NO_BIT
@@ -272,8 +280,14 @@ hipError_t launch_rows_direct(const DirectDst &d, const uint32_t *row_off, int64
 hipError_t launch_rows(const RowParams &P, const uint32_t *tok, const uint32_t *rec_tok, const uint32_t *rec_cnt,
                        const uint32_t *row_off, const uint32_t *row_rec, SegSel sel, int64_t rows_cap, RowOut out,
                        hipStream_t st);
-hipError_t launch_mask_rand(const RowParams &P, const uint32_t *row_off, const uint32_t *row_rec, SegSel sel,
-                            int64_t rows_cap, uint16_t *jbuf, hipStream_t st);
+// rng_mode 1 masks (pipeline.hip): every record's chunk-0 row from (seed, first_record + r, 0)
+// alone -- launched beside the tokenizer: swap indices (lane per record) into jbuf [R, S], then
+// the mask bits into bits [R, ceil(S/32)]
+hipError_t launch_mask_rand_rec(const RowParams &P, int64_t R, uint16_t *jbuf, uint32_t *bits, hipStream_t st);
+// ... and the rows g of the segment whose chunk k >= kmin, after the row map: listed (list[0] =
+// count, list[1..] = rows; rows_cap + 1 words), then 16 lanes per row, bits into bitsg [rows, S/32]
+hipError_t launch_mask_rand_rows(const RowParams &P, const uint32_t *row_off, const uint32_t *row_rec, SegSel sel,
+                                 int64_t rows_cap, int kmin, uint32_t *list, uint32_t *bitsg, hipStream_t st);
 
 // BertData MultiLabel labels_f32 plane (bert_data.rs:66-78)
 hipError_t launch_multi_labels(const uint32_t *labels, const uint64_t *label_off, const uint32_t *row_rec,

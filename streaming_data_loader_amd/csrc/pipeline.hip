@@ -642,10 +642,7 @@ __device__ __forceinline__ void store4(int32_t *p, int j0, int S, bool vec, int3
 #ifndef SDL_ROWS_WAVES_RM1
 #define SDL_ROWS_WAVES_RM1 6  // (r04: left to the compiler, 103 VGPRs, 4 waves: rows 0.347 ms; 7 spills 20 B)
 #endif
-template <int MR>
-__device__ void rand_set_bits(const RowParams &P, const uint16_t *__restrict__ jr, uint32_t *nx, uint32_t *bt,
-                              int lane);
-// RM1: MLM under rng_mode 1 (mask bits from k_mask_rand_walk's swap indices, phase B fused).  A template flag, not
+// RM1: MLM under rng_mode 1 (the rows' mask words from k_mask_bits_rec / k_mask_rand16).  A template flag, not
 // a runtime branch: the mask-word registers would cost the Philox path a wave
 // per SIMD (k_rows<2>: 80 -> 82 VGPRs, 6 -> 5 waves, 0.267 -> 0.295 ms).
 template <int MR, bool RM1>
@@ -660,9 +657,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MR >= 4 ? S
     const bool vec_lb = (P.label_width & 3) == 0;
     const RowSpan rs = row_span(sel, row_off, P.B, rows_cap);
     const int64_t G = rs.g_real;
-    // (rng_mode 1) phase B of the rand masks, fused: per wave, next() and the row's mask bits
-    __shared__ uint32_t s_nx[4][RM1 ? 256 * MR : 1];
-    __shared__ uint32_t s_bt[4][RM1 ? 8 * MR : 1];
     const DirectDst &dd = out.direct;
     const int64_t g_end = dd.cap ? rs.g_real : rs.g_end;  // (direct: the host batch keeps its own padding)
     for (int64_t g = rs.g_lo + (int64_t)blockIdx.x * 4 + wid; g < g_end; g += (int64_t)gridDim.x * 4) {
@@ -695,16 +689,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MR >= 4 ? S
         const int64_t n = (int64_t)cnt + P.n_pre + P.n_post;
         const int64_t base = P.chunk ? (int64_t)k * S : 0;
         const int l = (int)((n - base) < S ? (n - base) : S);
-        // (rng_mode 1) the row's mask words from its swap indices (k_mask_rand_walk)
+        // (rng_mode 1) the row's mask words (k_mask_bits_rec / k_mask_rand16): one dword a lane
         uint32_t mwd[MR];
         if (RM1) {
-            rand_set_bits<4 * MR>(P, P.mask_j + g * (int64_t)S, s_nx[wid], s_bt[wid], lane);
+            const uint32_t *bw = (int)k < P.mask_kmin ? P.mask_bits0 + r * (int64_t)P.mask_w
+                                                      : P.mask_bitsg + g * (int64_t)P.mask_w;
 #pragma unroll
             for (int m = 0; m < MR; ++m) {
                 const int j0 = 256 * m + 4 * lane;
-                mwd[m] = j0 < S ? s_bt[wid][j0 >> 5] : 0u;
+                mwd[m] = j0 < S ? bw[j0 >> 5] : 0u;
             }
-            __builtin_amdgcn_wave_barrier();  // (s_bt is rewritten by the wave's next row)
         }
 
         int32_t id[MR][4];
@@ -813,12 +807,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MR >= 4 ? S
 // accepted, lo32(v * n) <= zone(n) = (n << lz(n)) - 1 with n = i + 1 -- rand's
 // "conservative" zone rejects up to half the words for n just above a power of
 // two, so about 30 % of a row's ~730 words are rejected and every row has
-// rejections.  Phase A (k_mask_rand_walk) runs each row's walk in one lane (64
-// rows per wave): the lane computes its ChaCha12 blocks in registers, 16 words
-// per block in an unrolled loop, and writes each swap index j_i to the row's
-// slice of `jbuf`; the walk stops after step k (steps k-1 .. 1 only permute
-// [0, k) among itself).  Phase B (rand_set_bits, r04: fused into k_rows<MR, true>, which
-// takes a wave per row anyway -- its own launch plus a bits plane had cost 0.05 ms), a
+// rejections.  Phase A runs each row's walk in one lane: the lane computes its
+// ChaCha12 blocks in registers, 16 words per block in an unrolled loop, and writes
+// each swap index j_i to the row's slice of `jbuf`; the walk stops after step k
+// (steps k-1 .. 1 only permute [0, k) among itself).  A row is keyed by (seed,
+// record, chunk) alone, so the chunk-0 row of every record (86 % of the bench's
+// rows) is walked by k_mask_rand_rec (64 records per wave) on a second stream beside
+// the tokenizer, and phase B (k_mask_bits_rec) turns them into mask bits there too;
+// the rows of chunk >= 1, known after the row map, are listed and walked 16 lanes
+// per row (k_mask_rand16).  k_rows<MR, true> reads the bits.  Phase B (rand_set_bits), a
 // wave per row: mask_batch only uses the SET of the first k shuffled
 // positions, and Fisher-Yates from the end never moves a value out of [0, k)
 // once steps i < k begin (j_i <= i), so the set is what [0, k) holds after steps
@@ -915,27 +912,6 @@ __device__ __forceinline__ void rand_walk_lane(const RowParams &P, bool active, 
     }
 }
 
-// Phase A: one lane per row, 64 rows per wave
-__global__ __launch_bounds__(64) void k_mask_rand_walk(RowParams P, const uint32_t *__restrict__ row_off,
-                                                       const uint32_t *__restrict__ row_rec, SegSel sel,
-                                                       int64_t rows_cap, uint16_t *__restrict__ jbuf) {
-    const int lane = lane_id();
-    const int S = P.S;
-    const RowSpan rs = row_span(sel, row_off, P.B, rows_cap);
-    for (int64_t g0 = rs.g_lo + (int64_t)blockIdx.x * 64; g0 < (int64_t)rs.g_real; g0 += (int64_t)gridDim.x * 64) {
-        const int64_t g = g0 + lane;
-        const bool active = g < (int64_t)rs.g_real;
-        uint64_t rec = 0;
-        uint32_t chunk = 0;
-        if (active) {
-            const int64_t r = row_rec[g];
-            chunk = (uint32_t)(g - row_off[r]);
-            rec = P.first_record + (uint64_t)r;
-        }
-        rand_walk_lane(P, active, rec, chunk, jbuf + (active ? g : 0) * (int64_t)S);
-    }
-}
-
 // Phase B for one row, one wave: jr = the row's swap indices -> its mask bits in bt
 // (ceil(S/32) words of the wave's LDS; nx: 64 * MR words, MR >= S / 64)
 template <int MR>
@@ -973,14 +949,170 @@ __device__ __forceinline__ void rand_set_bits(const RowParams &P, const uint16_t
     wave_sync();
 }
 
-hipError_t launch_mask_rand(const RowParams &P, const uint32_t *row_off, const uint32_t *row_rec, SegSel sel,
-                            int64_t rows_cap, uint16_t *jbuf, hipStream_t st) {
+// Chunk-0 rows, one lane per record, 64 records per wave: the same walk (rand_walk_lane) keyed
+// by (first_record + r, chunk 0) -- which needs nothing the tokenizer computes, so the host runs
+// it on a second stream beside the tokenizer (sdl_batcher.cpp run_device): its ChaCha12 work
+// fills VALU slots the latency-bound tokenizer leaves idle instead of sitting on the step's
+// critical path.  (86 % of the bench's rows are chunk 0.)
+__global__ __launch_bounds__(64) void k_mask_rand_rec(RowParams P, int64_t R, uint16_t *__restrict__ jbuf) {
+    const int lane = lane_id();
+    for (int64_t r0 = (int64_t)blockIdx.x * 64; r0 < R; r0 += (int64_t)gridDim.x * 64) {
+        const int64_t r = r0 + lane;
+        const bool active = r < R;
+        rand_walk_lane(P, active, P.first_record + (uint64_t)(active ? r : 0), 0u, jbuf + (active ? r : 0) * (int64_t)P.S);
+    }
+}
+
+// Phase B for those rows: a wave per record, its mask bits -> bits[r]
+template <int MR4>
+__global__ __launch_bounds__(256) void k_mask_bits_rec(RowParams P, int64_t R, const uint16_t *__restrict__ jbuf,
+                                                       uint32_t *__restrict__ bits) {
+    __shared__ uint32_t s_nx[4][64 * MR4];
+    __shared__ uint32_t s_bt[4][2 * MR4];
+    const int lane = lane_id(), wid = (int)(threadIdx.x >> 6);
+    for (int64_t r = (int64_t)blockIdx.x * 4 + wid; r < R; r += (int64_t)gridDim.x * 4) {
+        rand_set_bits<MR4>(P, jbuf + r * (int64_t)P.S, s_nx[wid], s_bt[wid], lane);
+        for (int w = lane; w < P.mask_w; w += 64) bits[r * (int64_t)P.mask_w + w] = s_bt[wid][w];
+        __builtin_amdgcn_wave_barrier();  // (s_bt is rewritten by the wave's next record)
+    }
+}
+
+hipError_t launch_mask_rand_rec(const RowParams &P, int64_t R, uint16_t *jbuf, uint32_t *bits, hipStream_t st) {
+    if (R <= 0) return hipSuccess;
+    if (P.S > RAND_MAX_S || P.mask_w * 32 < P.S) return hipErrorInvalidValue;
+    const int64_t want = (R + 63) / 64;
+    hipLaunchKernelGGL(k_mask_rand_rec, dim3((unsigned)(want < 8192 ? want : 8192)), dim3(64), 0, st, P, R, jbuf);
+    const int64_t wb = (R + 3) / 4;
+    const dim3 g((unsigned)(wb < 16384 ? wb : 16384));
+    const int MR4 = (P.S + 63) / 64;
+#define SDL_BITS(M) hipLaunchKernelGGL(k_mask_bits_rec<M>, g, dim3(256), 0, st, P, R, (const uint16_t *)jbuf, bits)
+    if (MR4 <= 2) SDL_BITS(2);
+    else if (MR4 <= 4) SDL_BITS(4);
+    else if (MR4 <= 8) SDL_BITS(8);
+    else if (MR4 <= 16) SDL_BITS(16);
+    else SDL_BITS(32);
+#undef SDL_BITS
+    return hipGetLastError();
+}
+
+// The rows of the segment with chunk k >= kmin (k_rand_list), then 16 lanes per row, 4 rows per
+// wave (k_mask_rand16): so few rows that one lane per row would leave the launch as long as one
+// row's whole ChaCha12 chain.  Per window of 16 blocks the row's 16 lanes each compute one block
+// into LDS; lane 0 of the row walks the 256 words (rand's acceptance test, the same sequence as
+// rand_walk_lane) and puts each swap straight into next() (an LDS atomicMin, as rand_set_bits
+// does from the stored indices); the row's lanes then follow the chains and write its bits.
+__global__ __launch_bounds__(256) void k_rand_list(const uint32_t *__restrict__ row_off,
+                                                   const uint32_t *__restrict__ row_rec, SegSel sel, int64_t rows_cap,
+                                                   int B, int kmin, uint32_t *__restrict__ list) {
+    const RowSpan rs = row_span(sel, row_off, B, rows_cap);
+    for (int64_t g = rs.g_lo + (int64_t)blockIdx.x * 256 + threadIdx.x; g < rs.g_real; g += (int64_t)gridDim.x * 256) {
+        const uint32_t r = row_rec[g];
+        if ((int64_t)(g - row_off[r]) >= kmin) list[1 + atomicAdd(&list[0], 1u)] = (uint32_t)g;
+    }
+}
+
+template <int MR4>
+__global__ __launch_bounds__(64) void k_mask_rand16(RowParams P, const uint32_t *__restrict__ row_off,
+                                                    const uint32_t *__restrict__ row_rec,
+                                                    const uint32_t *__restrict__ list, uint32_t *__restrict__ bitsg) {
+    constexpr uint32_t NONE = 0xFFFFFFFFu;
+    __shared__ __attribute__((aligned(16))) uint32_t s_win[4][256];  // a row's window of 16 ChaCha12 blocks
+    __shared__ uint32_t s_nx[4][64 * MR4];
+    __shared__ uint32_t s_bt[4][2 * MR4];
+    const int lane = lane_id(), grp = lane >> 4, gl = lane & 15;
+    const int S = P.S, kmask = P.mask_length < S ? P.mask_length : S;
+    const int i0 = kmask > 1 ? kmask : 1;
+    auto wave_sync = [] {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    };
+    const uint32_t count = list[0];
+    // (the loop is wave-uniform; a row slot past the list runs with no row: its chain is empty)
+    for (uint32_t q0 = blockIdx.x * 4; q0 < count; q0 += gridDim.x * 4) {
+        const uint32_t q = q0 + (uint32_t)grp;
+        const bool active = q < count;
+        int64_t g = 0;
+        uint32_t key[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+        if (active) {
+            g = list[1 + q];
+            const uint32_t r = row_rec[g];
+            const uint64_t rec = P.first_record + (uint64_t)r;
+            key[0] = (uint32_t)P.seed;
+            key[1] = (uint32_t)(P.seed >> 32);
+            key[2] = (uint32_t)rec;
+            key[3] = (uint32_t)(rec >> 32);
+            key[4] = (uint32_t)(g - row_off[r]);
+        }
+        for (int x = gl; x < 64 * MR4; x += 16) s_nx[grp][x] = NONE;
+        if (gl < 2 * MR4) s_bt[grp][gl] = 0u;
+        // the walk's state lives in lane 0 of the row
+        int i = active ? S - 1 : 0;
+        uint32_t n = (uint32_t)i + 1u, zone = (n << __builtin_clz(n)) - 1u;
+        for (uint32_t blk = 0;; blk += 16) {
+            // wave-uniform: stop when no row of the wave has steps left
+            const int irow = __builtin_amdgcn_update_dpp(0, i, 0x150, 0xF, 0xF, false);  // row_newbcast:0
+            if (!__any(irow >= i0)) break;
+            uint32_t o[16];
+            chacha12_block(key, blk + (uint32_t)gl, o);
+            uint4 *wv = reinterpret_cast<uint4 *>(&s_win[grp][16 * gl]);
+            wv[0] = make_uint4(o[0], o[1], o[2], o[3]);
+            wv[1] = make_uint4(o[4], o[5], o[6], o[7]);
+            wv[2] = make_uint4(o[8], o[9], o[10], o[11]);
+            wv[3] = make_uint4(o[12], o[13], o[14], o[15]);
+            wave_sync();
+            if (gl == 0 && i >= i0) {
+                const uint4 *w4 = reinterpret_cast<const uint4 *>(&s_win[grp][0]);
+                for (int t = 0; t < 64 && i >= i0; ++t) {
+                    const uint4 x = w4[t];
+                    const uint32_t xs[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const uint64_t m = (uint64_t)xs[u] * n;
+                        if (i >= i0 && (uint32_t)m <= zone) {
+                            const uint32_t j = (uint32_t)(m >> 32);
+                            if (j != (uint32_t)i) atomicMin(&s_nx[grp][j], (uint32_t)i);
+                            --i;
+                            n = (uint32_t)i + 1u;
+                            zone = (n << __builtin_clz(n)) - 1u;
+                        }
+                    }
+                }
+            }
+            wave_sync();  // (the window is rewritten next)
+        }
+        // [0, k) holds val(next(x)) (or x): follow each chain to its end
+        for (int x = gl; x < kmask; x += 16) {
+            uint32_t p = (uint32_t)x;
+            for (uint32_t nq = s_nx[grp][p]; nq != NONE; nq = s_nx[grp][p]) p = nq;
+            atomicOr(&s_bt[grp][p >> 5], 1u << (p & 31));
+        }
+        wave_sync();
+        if (active)
+            for (int w = gl; w < P.mask_w; w += 16) bitsg[g * (int64_t)P.mask_w + w] = s_bt[grp][w];
+        wave_sync();  // (s_nx / s_bt are reset for the next rows)
+    }
+}
+
+hipError_t launch_mask_rand_rows(const RowParams &P, const uint32_t *row_off, const uint32_t *row_rec, SegSel sel,
+                                 int64_t rows_cap, int kmin, uint32_t *list, uint32_t *bitsg, hipStream_t st) {
     if (rows_cap <= 0) return hipSuccess;
-    if (P.S > RAND_MAX_S) return hipErrorInvalidValue;
-    const int64_t want = (rows_cap + 63) / 64;
-    const int64_t grid = want < 4096 ? want : 4096;
-    hipLaunchKernelGGL(k_mask_rand_walk, dim3((unsigned)grid), dim3(64), 0, st, P, row_off, row_rec, sel, rows_cap,
-                       jbuf);
+    if (P.S > RAND_MAX_S || P.mask_w * 32 < P.S) return hipErrorInvalidValue;
+    hipError_t e = hipMemsetAsync(list, 0, 4, st);
+    if (e != hipSuccess) return e;
+    const int64_t want = (rows_cap + 255) / 256;
+    hipLaunchKernelGGL(k_rand_list, dim3((unsigned)(want < 2048 ? want : 2048)), dim3(256), 0, st, row_off, row_rec,
+                       sel, rows_cap, P.B, kmin, list);
+    const int64_t w4 = (rows_cap + 3) / 4;
+    const dim3 g((unsigned)(w4 < 16384 ? w4 : 16384));
+    const int MR4 = (P.S + 63) / 64;
+#define SDL_R16(M) hipLaunchKernelGGL(k_mask_rand16<M>, g, dim3(64), 0, st, P, row_off, row_rec, (const uint32_t *)list, bitsg)
+    if (MR4 <= 2) SDL_R16(2);
+    else if (MR4 <= 4) SDL_R16(4);
+    else if (MR4 <= 8) SDL_R16(8);
+    else if (MR4 <= 16) SDL_R16(16);
+    else SDL_R16(32);
+#undef SDL_R16
     return hipGetLastError();
 }
 
@@ -1079,7 +1211,7 @@ hipError_t launch_rows(const RowParams &P, const uint32_t *tok, const uint32_t *
     const int MR = (P.S + 255) / 256;
     if (P.label_width > 256 * MR) return hipErrorInvalidValue;
     const bool rm1 = P.task == 0 && P.rng_mode == 1;
-    if (rm1 && !P.mask_j) return hipErrorInvalidValue;
+    if (rm1 && (!P.mask_bitsg || (P.mask_kmin > 0 && !P.mask_bits0) || P.mask_w * 32 < P.S)) return hipErrorInvalidValue;
 #define SDL_ROWS(MM)                                                                                                 \
     if (rm1)                                                                                                          \
         hipLaunchKernelGGL((k_rows<MM, true>), dim3(grid), dim3(256), 0, st, P, tok, rec_tok, rec_cnt, row_off,      \

@@ -269,7 +269,11 @@ struct sdl_batcher {
     DevBuf<uint32_t> ranges, tokc, chunk_cnt, chunk_off, rec_local, tok_ids, rec_tok, rec_cnt, rec_rows, row_off,
         row_rec, scan_tmp;
     DevBuf<int32_t> o_ids, o_am, o_tt, o_lab;
-    DevBuf<uint16_t> mask_j;     // rng_mode 1: per-row shuffle swap indices (k_mask_rand phase A)
+    // rng_mode 1: per-record chunk-0 swap indices and mask bits (k_mask_rand_rec, beside the
+    // tokenizer on stream2), the later rows' list and bits (k_mask_rand16)
+    DevBuf<uint16_t> mask_j0;
+    DevBuf<uint32_t> mask_bits0, mask_bitsg, rand_list;
+    hipEvent_t rand_ev[2] = {nullptr, nullptr};
     DevBuf<float> o_f32;
     DevBuf<uint32_t> lab_err;
     // byte-level BPE long pieces
@@ -283,6 +287,8 @@ struct sdl_batcher {
     DevBuf<uint32_t> span_ovf;
     bool span_two_phase = env_int("SDL_SPAN_TWO_PHASE", 0) != 0;
     bool small_calls = env_int("SDL_SMALL_CALLS", 1) != 0;  // k_downstream_small + folded record bounds
+    // rng_mode 1: chunk-0 rows walked beside the tokenizer (0: every row after the row map, 16 lanes each)
+    bool rand_rec0 = env_int("SDL_RAND_REC0", 1) != 0;
     // test hook: clamp the Unigram long-item list (0 = its N / 8 + chunks bound), so the capacity
     // flag can be raised through every path that reports it
     uint32_t uni_item_cap = (uint32_t)std::max(0, env_int("SDL_UNI_ITEM_CAP", 0));
@@ -293,6 +299,7 @@ struct sdl_batcher {
     DevBuf<uint64_t> j_off;
     // gzip inflate provider step (sdl_gzip_inflate_device)
     DevBuf<uint32_t> z_size, z_off, z_tcrc, z_bad;
+    DevBuf<uint64_t> z_from, z_mend;  // (sdl_gzip_inflate_first_device) candidate search start, member ends
     DevBuf<int32_t> z_status;
     DevBuf<unsigned long long> z_total;
     DevBuf<uint8_t> z_out;
@@ -384,6 +391,8 @@ struct sdl_batcher {
         for (auto &e : ev)
             if (e) (void)hipEventDestroy(e);
         for (auto &e : pipe_ev) (void)hipEventDestroy(e);
+        for (auto &e : rand_ev)
+            if (e) (void)hipEventDestroy(e);
         for (auto &e : x_ev)
             if (e) (void)hipEventDestroy(e);
         for (auto &e : x_in_ev) (void)hipEventDestroy(e);
@@ -443,14 +452,19 @@ struct sdl_batcher {
             if (single()) lab_err.ensure(1);
         }
         row_rec.ensure((size_t)std::max<int64_t>(rows_cap, 1));
-        if (P.task == SDL_TASK_MLM && P.rng_mode == 1)
-        {
-            mask_j.ensure((size_t)std::max<int64_t>(rows_cap, 1) * (size_t)P.S);
+        const bool rm1 = P.task == SDL_TASK_MLM && P.rng_mode == 1;
+        const int mask_w = (P.S + 31) / 32;
+        if (rm1) {
+            mask_bitsg.ensure((size_t)std::max<int64_t>(rows_cap, 1) * (size_t)mask_w);
+            rand_list.ensure((size_t)std::max<int64_t>(rows_cap, 1) + 1);
         }
 
         RowParams p = P;
         p.first_record = first_record;
-        p.mask_j = mask_j.p;
+        p.mask_w = mask_w;
+        p.mask_kmin = 0;
+        p.mask_bits0 = nullptr;
+        p.mask_bitsg = mask_bitsg.p;
         const bool bpe = dt.kind == TOK_BYTE_BPE;
         const bool uni = dt.kind == TOK_UNIGRAM;
         // Pipelined segments (WordPiece): the tokenize launches of the chunk
@@ -475,6 +489,22 @@ struct sdl_batcher {
         };
         const bool small = small_calls && !piped && !profiling && n_chunks <= SMALL_CHUNKS && R <= 8192;
         mark(0);
+        // rng_mode 1: every record's chunk-0 row depends on (seed, record) alone -- its walk and mask
+        // bits run on stream2 beside the tokenizer (k_mask_rand_rec); k_rows waits for them
+        const bool rec0 = rm1 && !piped && !small && R > 0 && rand_rec0;
+        if (rec0) {
+            mask_j0.ensure((size_t)R * (size_t)P.S);
+            mask_bits0.ensure((size_t)R * (size_t)mask_w);
+            if (!stream2) HIP_TRY(hipStreamCreateWithFlags(&stream2, hipStreamNonBlocking));
+            for (auto &e : rand_ev)
+                if (!e) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            HIP_TRY(hipEventRecord(rand_ev[0], st));  // (the last call's rows have read mask_bits0)
+            HIP_TRY(hipStreamWaitEvent(stream2, rand_ev[0], 0));
+            HIP_TRY(launch_mask_rand_rec(p, R, mask_j0.p, mask_bits0.p, stream2));
+            HIP_TRY(hipEventRecord(rand_ev[1], stream2));
+            p.mask_bits0 = mask_bits0.p;
+            p.mask_kmin = 1;
+        }
         // (one segment: k_chunk_ranges also writes its record bounds and zeroes the label error word)
         const bool fold = small_calls && sc.K == 1 && n_chunks > 0;
         HIP_TRY(launch_chunk_ranges(d_off, R, N, ranges.p, st, fold ? seg_rb.p : nullptr,
@@ -541,8 +571,11 @@ struct sdl_batcher {
                 HIP_TRY(launch_rows_span(p, tok_ids.p, rec_tok.p, rec_cnt.p, row_off.p, row_rec.p, sel, rows_cap, out,
                                          span_err.p, s, two_phase ? &pl : nullptr));
             } else {
-                if (p.task == SDL_TASK_MLM && p.rng_mode == 1)
-                    HIP_TRY(launch_mask_rand(p, row_off.p, row_rec.p, sel, rows_cap, mask_j.p, s));
+                if (rm1) {
+                    HIP_TRY(launch_mask_rand_rows(p, row_off.p, row_rec.p, sel, rows_cap, p.mask_kmin, rand_list.p,
+                                                  mask_bitsg.p, s));
+                    if (rec0) HIP_TRY(hipStreamWaitEvent(s, rand_ev[1], 0));
+                }
                 HIP_TRY(launch_rows(p, tok_ids.p, rec_tok.p, rec_cnt.p, row_off.p, row_rec.p, sel, rows_cap, out, s));
             }
             if (multi())
@@ -1613,8 +1646,11 @@ void inflate_chunked(sdl_batcher *h, const uint8_t *d_gz, uint64_t m, uint64_t m
     }
 }
 
-int sdl_gzip_inflate_device(sdl_batcher *h, const uint8_t *d_gz, uint64_t gz_len, const uint64_t *d_member_offsets,
-                            uint64_t n_members, void *stream, sdl_inflated *out) {
+namespace {
+// sdl_gzip_inflate_device, members [d_member_offsets[m], d_member_ends[m]) when d_member_ends is
+// given (device, u64[n]; else [offsets[m], offsets[m + 1]))
+int gzip_inflate_impl(sdl_batcher *h, const uint8_t *d_gz, uint64_t gz_len, const uint64_t *d_member_offsets,
+                      const uint64_t *d_member_ends, uint64_t n_members, void *stream, sdl_inflated *out) {
     if (!h || !out || (n_members && (!d_gz || !d_member_offsets))) return fail(SDL_ERR_ARG, "null argument");
     if (gz_len >= (1ull << 32)) return fail(SDL_ERR_CAPACITY, "gzip buffer must be < 4 GiB per call");
     if (n_members >= (1ull << 31)) return fail(SDL_ERR_CAPACITY, "too many gzip members in one call");
@@ -1632,7 +1668,8 @@ int sdl_gzip_inflate_device(sdl_batcher *h, const uint8_t *d_gz, uint64_t gz_len
         HIP_TRY(hipMemsetAsync(h->z_total.p, 0, sizeof(unsigned long long), st));
         unsigned long long total = 0;
         if (n) {
-            HIP_TRY(launch_gz_size(d_gz, gz_len, d_member_offsets, n_members, h->z_size.p, h->z_status.p, h->z_total.p, st));
+            HIP_TRY(launch_gz_size(d_gz, gz_len, d_member_offsets, n_members, h->z_size.p, h->z_status.p, h->z_total.p, st,
+                                   d_member_ends));
             HIP_TRY(launch_exclusive_scan(h->z_size.p, h->z_off.p, (int64_t)n, h->scan_tmp.p, st));
             HIP_TRY(hipMemcpyAsync(&total, h->z_total.p, sizeof(total), hipMemcpyDeviceToHost, st));
             HIP_TRY(hipStreamSynchronize(st));
@@ -1643,12 +1680,15 @@ int sdl_gzip_inflate_device(sdl_batcher *h, const uint8_t *d_gz, uint64_t gz_len
         HIP_TRY(hipMemsetAsync(h->z_out.p + total, 0, 32, st));
         uint32_t bad[2] = {0, 0xFFFFFFFFu};
         if (n) {  // large members first, in chunks (they leave GZ_VERIFIED statuses)
-            std::vector<uint64_t> mo(n + 1);
-            HIP_TRY(hipMemcpyAsync(mo.data(), d_member_offsets, (n + 1) * 8, hipMemcpyDeviceToHost, st));
+            std::vector<uint64_t> mo(n + 1), me(n);
+            HIP_TRY(hipMemcpyAsync(mo.data(), d_member_offsets, (d_member_ends ? n : n + 1) * 8, hipMemcpyDeviceToHost, st));
+            if (d_member_ends) HIP_TRY(hipMemcpyAsync(me.data(), d_member_ends, n * 8, hipMemcpyDeviceToHost, st));
             HIP_TRY(hipStreamSynchronize(st));
+            if (!d_member_ends)
+                for (size_t m = 0; m < n; ++m) me[m] = mo[m + 1];
             std::vector<uint64_t> big;
             for (size_t m = 0; m < n; ++m)
-                if (mo[m + 1] > mo[m] && mo[m + 1] - mo[m] >= GZ_SPLIT_MIN && mo[m + 1] <= gz_len) big.push_back(m);
+                if (me[m] > mo[m] && me[m] - mo[m] >= GZ_SPLIT_MIN && me[m] <= gz_len) big.push_back(m);
             if (!big.empty()) {
                 std::vector<uint32_t> sz(n), oo(n);
                 std::vector<int32_t> zs(n);
@@ -1657,12 +1697,13 @@ int sdl_gzip_inflate_device(sdl_batcher *h, const uint8_t *d_gz, uint64_t gz_len
                 HIP_TRY(hipMemcpyAsync(zs.data(), h->z_status.p, n * 4, hipMemcpyDeviceToHost, st));
                 HIP_TRY(hipStreamSynchronize(st));
                 for (uint64_t m : big)
-                    if (zs[m] == GZ_OK) inflate_chunked(h, d_gz, m, mo[m], mo[m + 1], sz[m], oo[m], st);
+                    if (zs[m] == GZ_OK) inflate_chunked(h, d_gz, m, mo[m], me[m], sz[m], oo[m], st);
             }
         }
         if (n) {
             HIP_TRY(hipMemcpyAsync(h->z_bad.p, bad, sizeof(bad), hipMemcpyHostToDevice, st));
-            HIP_TRY(launch_inflate(d_gz, d_member_offsets, n_members, h->z_off.p, h->z_out.p, h->z_status.p, h->z_tcrc.p, st));
+            HIP_TRY(launch_inflate(d_gz, d_member_offsets, n_members, h->z_off.p, h->z_out.p, h->z_status.p, h->z_tcrc.p, st,
+                                   d_member_ends));
             static const X2N x2n = make_x2n();
             HIP_TRY(launch_gz_crc(h->z_off.p, h->z_out.p, n_members, h->z_tcrc.p, x2n, h->z_status.p, h->z_bad.p, st));
             HIP_TRY(hipMemcpyAsync(bad, h->z_bad.p, sizeof(bad), hipMemcpyDeviceToHost, st));
@@ -1686,6 +1727,65 @@ int sdl_gzip_inflate_device(sdl_batcher *h, const uint8_t *d_gz, uint64_t gz_len
                                           " members failed)");
         }
         return SDL_OK;
+    } catch (HipError &e) {
+        return fail(SDL_ERR_HIP, e.what());
+    } catch (std::exception &e) {
+        return fail(SDL_ERR_ARG, e.what());
+    }
+}
+}  // namespace
+
+int sdl_gzip_inflate_device(sdl_batcher *h, const uint8_t *d_gz, uint64_t gz_len, const uint64_t *d_member_offsets,
+                            uint64_t n_members, void *stream, sdl_inflated *out) {
+    return gzip_inflate_impl(h, d_gz, gz_len, d_member_offsets, nullptr, n_members, stream, out);
+}
+
+int sdl_gzip_inflate_first_device(sdl_batcher *h, const uint8_t *d_gz, uint64_t gz_len, const uint64_t *d_file_offsets,
+                                  uint64_t n_files, void *stream, sdl_inflated *out) {
+    if (!h || !out || (n_files && (!d_gz || !d_file_offsets))) return fail(SDL_ERR_ARG, "null argument");
+    if (n_files >= (1ull << 31)) return fail(SDL_ERR_CAPACITY, "too many gzip files in one call");
+    try {
+        hipStream_t st = stream ? (hipStream_t)stream : h->stream;
+        const size_t n = (size_t)n_files;
+        if (n == 0) return gzip_inflate_impl(h, d_gz, gz_len, d_file_offsets, nullptr, 0, stream, out);
+        std::vector<uint64_t> fo(n + 1), from(n), ends(n);
+        HIP_TRY(hipMemcpyAsync(fo.data(), d_file_offsets, (n + 1) * 8, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        for (size_t f = 0; f < n; ++f) {
+            if (fo[f + 1] < fo[f] || fo[f + 1] > gz_len) return fail(SDL_ERR_ARG, "file offsets out of order or range");
+            from[f] = fo[f] + 19;  // a member is >= 20 bytes: header 10, a final block >= 2, trailer 8
+        }
+        h->z_from.ensure(n);
+        h->z_mend.ensure(n);
+        // The first member of file f ends at the next offset where a member header could start, or at
+        // the file's end.  A candidate inside the member's own DEFLATE data fails its decode (the
+        // range ends early); the file then retries from the next candidate.  Every try decodes every
+        // file again (such candidates are rare: ~2^-27 per compressed byte).
+        for (int attempt = 0;; ++attempt) {
+            for (size_t f = 0; f < n; ++f) ends[f] = fo[f + 1];
+            HIP_TRY(hipMemcpyAsync(h->z_from.p, from.data(), n * 8, hipMemcpyHostToDevice, st));
+            HIP_TRY(hipMemcpyAsync(h->z_mend.p, ends.data(), n * 8, hipMemcpyHostToDevice, st));
+            HIP_TRY(launch_gz_next_header(d_gz, gz_len, d_file_offsets, n, h->z_from.p,
+                                          reinterpret_cast<unsigned long long *>(h->z_mend.p), st));
+            HIP_TRY(hipMemcpyAsync(ends.data(), h->z_mend.p, n * 8, hipMemcpyDeviceToHost, st));
+            HIP_TRY(hipStreamSynchronize(st));
+            const int rc = gzip_inflate_impl(h, d_gz, gz_len, d_file_offsets, h->z_mend.p, n_files, stream, out);
+            if (rc != SDL_ERR_DATA || attempt >= 63) return rc;
+            std::vector<int32_t> zs(n);
+            HIP_TRY(hipMemcpy(zs.data(), h->z_status.p, n * 4, hipMemcpyDeviceToHost));
+            bool again = false;
+            for (size_t f = 0; f < n; ++f) {
+                const int32_t s = zs[f] & 0xFFFF;
+                // a failure that a later end can change: not the header, and not a stream that ended
+                // before the range (trailing bytes with no member header: the limit of this mode)
+                if (s != GZ_OK && s != GZ_E_HEADER && s != GZ_E_HCRC && s != GZ_E_RANGE && s != GZ_E_TRAIL &&
+                    ends[f] < fo[f + 1]) {
+                    from[f] = ends[f];
+                    again = true;
+                }
+            }
+            if (!again) return rc;
+        }
     } catch (HipError &e) {
         return fail(SDL_ERR_HIP, e.what());
     } catch (std::exception &e) {

@@ -29,6 +29,7 @@
 // global list, ids into a pool the compaction expands; items whose normalized
 // text exceeds a lane's scratch go to k_unigram_huge (one wave each).
 #include <cstdio>
+#include <type_traits>
 
 #include "common.hpp"
 #include "device_util.hpp"
@@ -56,7 +57,10 @@ constexpr int WIN_PAD = WIN + 32;   // window + gather padding; the arena follow
 #endif
 constexpr int JOB_CAP = SDL_UNI_JOB_CAP;  // words waiting for the DP (more: long items)
 constexpr int VP_CAP = JOB_CAP + JOB_CAP / 2;  // Viterbi pieces per chunk
-constexpr int MED_CAP = 128;        // medium words per chunk (more: long items)
+#ifndef SDL_UNI_MED_CAP
+#define SDL_UNI_MED_CAP 128
+#endif
+constexpr int MED_CAP = SDL_UNI_MED_CAP;  // medium words per chunk (more: long items)
 #ifndef SDL_UNI_WT_UNROLL
 #define SDL_UNI_WT_UNROLL 2
 #endif
@@ -70,7 +74,10 @@ constexpr int TASK_CAP = SDL_UNI_TASK_CAP;  // probe tasks per round (>= one job
 #endif
 constexpr int DPG = SDL_UNI_DPG;  // lanes relaxing one job's candidates together
 constexpr uint8_t CNT_LONG = 0xFF;   // s_cnt of a long item        // lanes running the DP (a round holds few jobs)
-constexpr int TASK_UNROLL = 4;      // probes in flight per lane
+#ifndef SDL_UNI_TASK_UNROLL
+#define SDL_UNI_TASK_UNROLL 4
+#endif
+constexpr int TASK_UNROLL = SDL_UNI_TASK_UNROLL;  // probes in flight per lane
 
 typedef __attribute__((address_space(3))) double lds_f64;
 
@@ -144,6 +151,8 @@ __device__ __forceinline__ int probe_result_w3(const Probe &P, uint32_t key, con
 // are negative log-probabilities: stored as is, one ulp further from zero;
 // negated, one ulp nearer); LDS keeps the 16-bit id and the f32 as before.
 constexpr uint32_t UNI_ID_MASK = 0x7FFFu;
+constexpr uint16_t NO_PIECE = 0xFFFFu;  // a round's task with no vocab piece (ids are < 0xFFFF: the host
+                                        // refuses a marked piece id >= 0x7FFF and vocabularies > 65,535)
 __device__ __forceinline__ double uni_score64(float f, uint32_t id16) {
     double d = (double)f;
     if (id16 & 0x8000u) {
@@ -153,6 +162,23 @@ __device__ __forceinline__ double uni_score64(float f, uint32_t id16) {
     return d;
 }
 __device__ __forceinline__ int uni_piece_id(int y) { return y < 0 ? y : (int)((uint32_t)y & UNI_ID_MASK); }
+
+// Lane I of every 16-lane row's f64, to the whole row (DPP row_newbcast: in the VALU, no LDS).
+template <int I>
+__device__ __forceinline__ double row_bcast_f64(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)b, 0x150 + I, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x150 + I, 0xF, 0xF, false);
+    return __longlong_as_double((long long)((uint64_t)(uint32_t)hi << 32 | (uint32_t)lo));
+}
+// f(std::integral_constant<int, i>) for i = A .. B - 1, in order (a compile-time index for DPP controls)
+template <int A, int B, class F>
+__device__ __forceinline__ void static_for(const F &f) {
+    if constexpr (A < B) {
+        f(std::integral_constant<int, A>{});
+        static_for<A + 1, B>(f);
+    }
+}
 
 // Added token "<...>" starting at p: the bytes up to the first '>' (within
 // max_special_len, not crossing a boundary) probed as UC_ADDED.  Returns the id
@@ -538,7 +564,21 @@ __device__ unsigned long long sdl_uni_cycles[8];
             stamp_prev_ = t_;                                                         \
         }                                                                             \
     } while (0)
+// counts (stamps build): 0 chunks 1 pieces 2 jobs 3 vps 4 rounds 5 tasks 6 medium words 7 jobs with > 1 vp
+// 8.. 8+16: vps by payload length 1..17
+__device__ unsigned long long sdl_uni_counts[32];
+#define UNI_COUNT(k, v) do { atomicAdd(&sdl_uni_counts[k], (unsigned long long)(v)); } while (0)
 void print_uni_cycles() {
+    unsigned long long cn[32];
+    if (hipMemcpyFromSymbol(cn, HIP_SYMBOL(sdl_uni_counts), sizeof(cn)) == hipSuccess && cn[0]) {
+        fprintf(stderr, "[uni counts] chunks %llu pieces/chunk %.1f jobs/chunk %.2f vps/chunk %.2f rounds/chunk %.2f "
+                        "tasks/chunk %.1f medium/chunk %.2f multi-vp jobs/chunk %.3f\n", cn[0], (double)cn[1] / cn[0],
+                (double)cn[2] / cn[0], (double)cn[3] / cn[0], (double)cn[4] / cn[0], (double)cn[5] / cn[0],
+                (double)cn[6] / cn[0], (double)cn[7] / cn[0]);
+        fprintf(stderr, "[uni counts] vp payload length histogram:");
+        for (int i = 0; i < 17; ++i) fprintf(stderr, " %d:%llu", i, cn[8 + i]);
+        fprintf(stderr, "\n");
+    }
     unsigned long long h[8];
     if (hipMemcpyFromSymbol(h, HIP_SYMBOL(sdl_uni_cycles), sizeof(h)) != hipSuccess) return;
     static const char *names[] = {"", "load+classify+specials", "piece starts", "word table+medium", "task bases",
@@ -571,6 +611,7 @@ void print_long_cycles() {
             c[3]);
 }
 #else
+#define UNI_COUNT(k, v) do {} while (0)
 #define UNI_STAMP(k) do {} while (0)
 #define LONG_STAMP(k) do {} while (0)
 #define LONG_COUNT(k, v) do {} while (0)
@@ -586,32 +627,46 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
     uint32_t *__restrict__ chunk_ent, uint32_t *__restrict__ rec_local, uint32_t *__restrict__ counters,
     uint4 *__restrict__ items, uint32_t item_cap, uint32_t *__restrict__ err) {
     __shared__ __attribute__((aligned(16))) uint8_t s_bytes[WIN_PAD + ARENA + 32];  // window | arena
-    // s_cls / s_plen / s_med are dead during the Viterbi rounds (long-item
+    // s_cls / s_med are dead during the Viterbi rounds (long-item
     // lengths move to their stage slot), which reuse them for the DP nodes:
     // LDS per one-wave block decides how many chunks a CU keeps in flight.
-    constexpr int U_CLS = 0, U_PLEN = (WIN + 15) & ~15, U_MED = U_PLEN + CHUNK, U_MED_END = U_MED + 2 * MED_CAP;
+    constexpr int U_CLS = 0, U_MED = (WIN + 15) & ~15, U_MED_END = U_MED + 2 * MED_CAP;
+#ifdef SDL_UNI_OLD_DP
     constexpr int DP_BYTES = (64 / DPG) * UNI_NODES * 12;
+#else
+    // the rounds' probe results and the DP rows' back pointers (s_tsc f32, s_tid u16, s_bp u32)
+    constexpr int DP_BYTES = TASK_CAP * 6 + 4 * 17 * 4;
+#endif
     constexpr int U_END = U_MED_END > DP_BYTES ? U_MED_END : DP_BYTES;
     __shared__ __attribute__((aligned(16))) uint8_t s_u[U_END];
     uint8_t *const s_cls = s_u + U_CLS;
     __shared__ uint32_t s_rbits[RBITS_WORDS + 1];
     __shared__ uint16_t s_pieces[CHUNK + 1];  // prel | SPEC << 12
-    uint8_t *const s_plen = s_u + U_PLEN;  // piece length, settled pieces only (0 = runs past the window)
     // ids staged at their piece's byte offset: a piece may use the bytes up to
     // the next piece (stage_room); one that needs more becomes a long item
     __shared__ uint16_t s_stage[STAGE];
     __shared__ uint8_t s_cnt[CHUNK];              // ids per piece (<= 2 UNI_WMAX), CNT_LONG = long item
-    uint16_t *const s_med = (uint16_t *)(s_u + U_MED);  // medium words (piece indices)
+    uint16_t *const s_med = (uint16_t *)(s_u + U_MED);  // medium words: piece index | length << 11
     __shared__ uint32_t s_scratch[16];  // 0 jobs 1 vps 2 arena used 3 medium words; 8.. scan scratch
     __shared__ uint16_t s_job_pi[JOB_CAP], s_job_vp[JOB_CAP];
     __shared__ uint8_t s_job_nvp[JOB_CAP];
     __shared__ uint16_t s_job_tb[JOB_CAP + 1];  // task base of each job (job order; < 2^16)
     __shared__ uint16_t s_job_rb[JOB_CAP + 1];  // candidate-row base of each job
+#ifdef SDL_UNI_OLD_DP
     __shared__ uint32_t s_rowmask[TASK_CAP];    // per row: which candidate ends exist (<= UNI_WMAX + 1)
+#else
+    uint32_t *const s_bp = (uint32_t *)(s_u + TASK_CAP * 6);  // the DP rows' back pointers (start | id << 16)
+#endif
     __shared__ uint16_t s_vp_src[VP_CAP];
     __shared__ uint8_t s_vp_len[VP_CAP];
+#ifdef SDL_UNI_OLD_DP
     __shared__ uint16_t s_tid[TASK_CAP];
     __shared__ float s_tsc[TASK_CAP];
+#else
+    // (overlaid on s_u: s_cls / s_med are dead once the rounds start)
+    float *const s_tsc = (float *)s_u;
+    uint16_t *const s_tid = (uint16_t *)(s_u + TASK_CAP * 4);
+#endif
 
     const int tid = threadIdx.x;
     const int lane = tid;
@@ -780,7 +835,6 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
             bool simple = false;
             const int len = word_len(wi0, &simple);
             len_u[u] = len;
-            s_plen[pi] = (uint8_t)(len <= UNI_WMAX ? len : 0);
             if (len > 0 && len <= UNI_WMAX && simple) {
                 W[u] = lds_w16(w32, wi0, len);
                 P[u] = probe_load_words(T, hash16(W[u], (uint32_t)len, UC_WORD));
@@ -831,7 +885,7 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
                 // medium word: normalized in the next pass, all lanes at once
                 const uint32_t mq = atomicAdd(&s_scratch[3], 1u);
                 if (mq < (uint32_t)MED_CAP) {
-                    s_med[mq] = (uint16_t)pi;
+                    s_med[mq] = (uint16_t)(pi | len << 11);  // (pi < 2^11, len <= UNI_WMAX)
                     cnt[pi] = 0;
                     done = true;
                 }
@@ -849,10 +903,10 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
     // arena (at most UNI_WMAX bytes each), split, list their Viterbi pieces
     const int nmed = (int)(s_scratch[3] < (uint32_t)MED_CAP ? s_scratch[3] : (uint32_t)MED_CAP);
     for (int mq = lane; mq < nmed; mq += 64) {
-        const int pi = s_med[mq];
+        const int pi = s_med[mq] & 0x7FF;
         const int prel = (int)(s_pieces[pi] & 0xFFFu);
         const int wi0 = HALO_L + prel;
-        const int len = s_plen[pi];
+        const int len = s_med[mq] >> 11;
         bool done = false;
         const uint32_t a = atomicAdd(&s_scratch[2], (uint32_t)UNI_WMAX);
         if (a + UNI_WMAX <= (uint32_t)ARENA) {
@@ -964,6 +1018,18 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
     if (lane == 0) {
         s_job_tb[nj] = (uint16_t)carry;
         s_job_rb[nj] = (uint16_t)rcarry;
+#ifdef SDL_STAMPS
+        UNI_COUNT(0, 1);
+        UNI_COUNT(1, np);
+        UNI_COUNT(2, nj);
+        UNI_COUNT(5, carry);
+        UNI_COUNT(6, s_scratch[3]);
+        for (int q = 0; q < nj; ++q) {
+            UNI_COUNT(3, s_job_nvp[q]);
+            if (s_job_nvp[q] > 1) UNI_COUNT(7, 1);
+            for (int z = 0; z < s_job_nvp[q]; ++z) UNI_COUNT(8 + (s_vp_len[s_job_vp[q] + z] < 16 ? s_vp_len[s_job_vp[q] + z] : 16), 1);
+        }
+#endif
     }
     __syncthreads();
     // Rounds are software-pipelined: round r + 1's probes are issued right after
@@ -1069,21 +1135,45 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
     int j0 = 0, j1 = nj > 0 ? round_end(0) : 0;
     if (nj > 0) issue(j0, j1);
     while (j0 < nj) {
+#ifdef SDL_STAMPS
+        if (lane == 0) UNI_COUNT(4, 1);
+#endif
         const uint32_t T0 = s_job_tb[j0], RB0 = s_job_rb[j0];
+#ifdef SDL_UNI_OLD_DP
         for (int r = lane; r < (int)(s_job_rb[j1] - RB0); r += 64) s_rowmask[r] = 0u;
         __syncthreads();
+#else
+        const int nt_round = (int)(s_job_tb[j1] - T0);
+        (void)RB0;
+#endif
         // -- this round's probe results -> LDS --
 #pragma unroll
         for (int u = 0; u < TASK_UNROLL; ++u) {
+#ifdef SDL_UNI_OLD_DP
             if (meta[u] == ~0u) continue;
+#else
+            // every task of the round gets its word: the id, or NO_PIECE (no vocab piece, or
+            // a candidate that starts or ends inside a char)
+            const int t = TASK_UNROLL * lane + u;
+            if (t >= nt_round) continue;
+            if (meta[u] == ~0u) {
+                s_tid[t] = NO_PIECE;
+                continue;
+            }
+#endif
             uint32_t w3 = gw3[u];
             const uint32_t key = ((meta[u] >> 22) & 0x7Fu) | ((meta[u] >> 29) << 8);
             const int id = gen[u] != -2 ? gen[u] : probe_result_w3(P[u], key, W[u], &w3);
+#ifdef SDL_UNI_OLD_DP
             if (id < 0) continue;
             const int t = TASK_UNROLL * lane + u;
             s_tid[t] = (uint16_t)id;
             s_tsc[t] = __uint_as_float(w3);  // the slot's f32 score, decoded with s_tid by uni_score64
             atomicOr(&s_rowmask[meta[u] & 0xFFFFu], 1u << ((meta[u] >> 16) & 0x3Fu));
+#else
+            s_tid[t] = id < 0 ? NO_PIECE : (uint16_t)id;
+            s_tsc[t] = __uint_as_float(w3);  // the slot's f32 score, decoded with s_tid by uni_score64
+#endif
         }
         __syncthreads();
         UNI_STAMP(6);
@@ -1091,6 +1181,104 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
 #ifndef SDL_UNI_NO_PIPE
         if (n0 < nj) issue(n0, n1);  // the next round's probes fly during this DP
 #endif
+#ifndef SDL_UNI_OLD_DP
+        // -- DP: a 16-lane DPP row per job (4 jobs at a time), one Viterbi piece after the
+        //    other.  Lane gl of the row holds node p = gl + 1 -- "▁" and the payload's first
+        //    p bytes -- in registers: its score (f64) and back pointer.  Every candidate
+        //    ending at p is read from the round's results in LDS up front; the starts are
+        //    visited in order (S, then payload start 0, 1, ...), the base of payload start
+        //    i >= 1 is node i's score, which row_newbcast:(i - 1) hands to the whole row in
+        //    the same instruction stream -- no LDS node array, no per-start barrier.  Same
+        //    candidates, visit order, strict-> replacement and f64 sums as
+        //    unigram_viterbi_masked (unigram.hpp); the unk relaxation of a start whose
+        //    one-char piece is missing lands on the same node as that piece would, so it
+        //    takes the piece's slot.  Lane 0 of the row then backtracks with unk fusion. --
+        {
+            const int grp = lane >> 4, gl = lane & 15;
+            lds_u32 *gbp = (lds_u32 *)s_bp + grp * 17;  // p = 1..16 at gl, node 3 ("▁") at 16
+            auto wave_sync = [] {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            };
+            for (int jb = j0 + grp; jb < j1; jb += 4) {  // (row-uniform: all 16 lanes of a row together)
+                const int pi = s_job_pi[jb];
+                const int prel = (int)(s_pieces[pi] & 0xFFFu);
+                int toff = (int)(s_job_tb[jb] - T0);
+                int ktot = 0;
+                for (int q = 0; q < s_job_nvp[jb]; ++q) {
+                    const int vp = s_job_vp[jb] + q;
+                    const int L = s_vp_len[vp], src = s_vp_src[vp];
+                    const int c0 = vp_c0(L, Mm);
+                    const int p = gl + 1;
+                    const bool live = p <= L;
+                    // the char ending at p (if p is a char boundary) starts at payload byte qs
+                    const bool bnd = live && (p == L || (bytes[src + p] & 0xC0u) != 0x80u);
+                    int qs = p - 1;
+                    if (bnd)
+                        while (qs > 0 && (bytes[src + qs] & 0xC0u) == 0x80u) --qs;
+                    // node 3 (after "▁"): the "▁" piece (meta task 0), else its unk
+                    const uint32_t id3 = s_tid[toff];
+                    const double c3 = id3 != NO_PIECE ? uni_score64(s_tsc[toff], id3) : T.unk_score;
+                    const uint32_t bp3 = (id3 != NO_PIECE ? (id3 & UNI_ID_MASK) : (uint32_t)T.unk_id) << 16;
+                    // candidate (start, p): score (f64, -inf when none) and its id; the unk of a
+                    // start whose one-char piece is missing is no piece (Mm / Mf do not bound it)
+                    auto cand_sc = [&](bool piece_ok, int t, bool unk_ok, uint32_t *id) -> double {
+                        const uint32_t x = piece_ok ? s_tid[toff + t] : NO_PIECE;  // (t < the vp's tasks then)
+                        if (x != NO_PIECE) {
+                            *id = x & UNI_ID_MASK;
+                            return uni_score64(s_tsc[toff + t], x);
+                        }
+                        *id = (uint32_t)T.unk_id;
+                        return unk_ok ? T.unk_score : -__builtin_inf();
+                    };
+                    uint32_t cid;
+                    // start S (base 0.0): the meta piece "▁" + payload[0, p)
+                    double best = cand_sc(live && p <= Mm, live ? p : 0, false, &cid) + 0.0;
+                    uint32_t bp = best > -__builtin_inf() ? cid << 16 : 0xFFFFFFFFu;
+                    {  // payload start 0 (node 3, base c3)
+                        const double c = cand_sc(live && p <= Mf, live ? c0 + p - 1 : 0, bnd && qs == 0, &cid) + c3;
+                        const bool up = c > best;
+                        best = up ? c : best;
+                        bp = up ? (3u | cid << 16) : bp;
+                    }
+                    static_for<1, UNI_WMAX>([&](auto ic) {  // payload start i (node 3 + i = lane i - 1)
+                        constexpr int i = decltype(ic)::value;
+                        const double base = row_bcast_f64<i - 1>(best);
+                        const bool valid = live && i < p && p - i <= Mf;
+                        const int t = valid ? c0 + vp_rowoff(i, L, Mf) + (p - i - 1) : 0;
+                        const double c = cand_sc(valid, t, bnd && qs == i, &cid) + base;
+                        const bool up = c > best;
+                        best = up ? c : best;
+                        bp = up ? ((uint32_t)(3 + i) | cid << 16) : bp;
+                    });
+                    gbp[gl] = bp;
+                    if (gl == 0) gbp[16] = bp3;
+                    wave_sync();
+                    if (gl == 0) {
+                        struct {
+                            lds_u32 *bp;
+                            __device__ uint32_t at(int x) const { return x == 3 ? bp[16] : bp[x - 4]; }
+                            __device__ int start(int x) const { return at(x) == 0xFFFFFFFFu ? -1 : (int)(at(x) & 0xFFFFu); }
+                            __device__ int id(int x) const { return at(x) == 0xFFFFFFFFu ? -1 : (int)(at(x) >> 16); }
+                        } gnodes{gbp};
+                        auto cand = [&](int st, int e, double *sc) -> int {  // the fused-unk lookup
+                            const int loc = vp_local(st == 0 ? -1 : st - 3, e - 3, L, Mm, Mf);
+                            if (loc < 0 || s_tid[toff + loc] == NO_PIECE) return -1;
+                            *sc = uni_score64(s_tsc[toff + loc], s_tid[toff + loc]);
+                            return (int)(s_tid[toff + loc] & UNI_ID_MASK);
+                        };
+                        const int base = ktot;
+                        ktot += unigram_backtrack(L + 3, cand, gnodes, T.unk_id,
+                                                  [&](int x, int id) { stage[prel + base + x] = (uint16_t)id; });
+                    }
+                    wave_sync();  // (the row's back pointers are rewritten for the next piece)
+                    toff += vp_tasks(L, Mm, Mf);
+                }
+                if (gl == 0) cnt[pi] = (uint8_t)ktot;
+            }
+        }
+#else
         // -- DP: a group of DPG lanes per job.  Starts are visited in order; the
         //    candidates of one start end at distinct nodes, so the group's lanes
         //    relax them together (same visit order and strict-> replacement as
@@ -1187,6 +1375,7 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
                 if (gl == 0) cnt[pi] = (uint8_t)ktot;
             }
         }
+#endif
         __syncthreads();
         UNI_STAMP(7);
         j0 = n0;

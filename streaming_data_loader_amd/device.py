@@ -221,6 +221,18 @@ class DeviceBatcher:
             return out
         return rc, out
 
+    def gzip_inflate_first(self, gz_ptr, gz_len, file_offsets_ptr, n_files, stream=0, check=True):
+        """Reference-exact gzip (sdl_gzip_inflate_first_device): every range is a file and only its
+        first member is inflated, as async-compression's GzipDecoder reads a file."""
+        out = native.Inflated()
+        rc = native.load().sdl_gzip_inflate_first_device(self._h, ctypes.c_void_p(gz_ptr), gz_len,
+                                                         ctypes.c_void_p(file_offsets_ptr), n_files,
+                                                         ctypes.c_void_p(stream or None), ctypes.byref(out))
+        if check:
+            native.check(rc)
+            return out
+        return rc, out
+
     def pickle_frames(self, result, n_rows=None, flush_partial=True, stream=0):
         """Transport step on the device: the batches of `result` (the last
         process*() call) as serde_pickle frames (DeviceFrames)."""

@@ -24,7 +24,7 @@ EXPORTS = [
     "sdl_batcher_push_many", "sdl_batcher_next", "sdl_batcher_flush", "sdl_batch_release",
     "sdl_process_device", "sdl_process_device_labels", "sdl_json_text_device", "sdl_pickle_frames_device", "sdl_device_to_host", "sdl_set_profiling", "sdl_stage_times",
     "sdl_tokenizer_info_get", "sdl_last_error", "sdl_abi_version", "sdl_json_to_frames",
-    "sdl_gzip_inflate_device", "sdl_gzip_split_members", "sdl_build_id",
+    "sdl_gzip_inflate_device", "sdl_gzip_inflate_first_device", "sdl_gzip_split_members", "sdl_build_id",
     "sdl_shard_records", "sdl_multi_create", "sdl_multi_destroy", "sdl_multi_push_many", "sdl_multi_handle",
 ]
 
@@ -180,6 +180,8 @@ def load(path=LIB_PATH):
     L.sdl_json_to_frames.restype = i64
     L.sdl_gzip_inflate_device.argtypes = [vp, vp, u64, vp, u64, vp, ctypes.POINTER(Inflated)]
     L.sdl_gzip_inflate_device.restype = i64
+    L.sdl_gzip_inflate_first_device.argtypes = [vp, vp, u64, vp, u64, vp, ctypes.POINTER(Inflated)]
+    L.sdl_gzip_inflate_first_device.restype = i64
     L.sdl_gzip_split_members.argtypes = [vp, u64, vp, u64, ctypes.POINTER(u64)]
     L.sdl_gzip_split_members.restype = i64
     L.sdl_shard_records.argtypes = [vp, u64, ctypes.c_uint32, vp]

@@ -220,7 +220,8 @@ def torch():
     return t
 
 
-def device_inflate(torch, db, members, check=True):
+def device_inflate(torch, db, members, check=True, first=False):
+    """members: gzip members (or, with first=True, whole files for sdl_gzip_inflate_first_device)"""
     from streaming_data_loader_amd import native
     buf = b"".join(members)
     off = np.zeros(len(members) + 1, np.uint64)
@@ -229,7 +230,8 @@ def device_inflate(torch, db, members, check=True):
     a[:len(buf)] = np.frombuffer(buf, np.uint8)
     d_gz = torch.from_numpy(a).cuda()
     d_off = torch.from_numpy(off.view(np.int64)).cuda()
-    rc, out = db.gzip_inflate(d_gz.data_ptr(), len(buf), d_off.data_ptr(), len(members), check=False)
+    call = db.gzip_inflate_first if first else db.gzip_inflate
+    rc, out = call(d_gz.data_ptr(), len(buf), d_off.data_ptr(), len(members), check=False)
     if check:
         native.check(rc)
     n = len(members)
@@ -256,6 +258,62 @@ def test_device_inflate_matches_oracle(torch, native_lib, records):
         assert ost == 0 and st == 0, name
         assert g == ogot == want, name
     assert arena[:int(out.out_bytes)].tobytes() == b"".join(w for _, _, w in cases)
+
+
+@pytest.mark.gpu
+def test_first_member_mode_matches_the_reference_decoder(torch, native_lib, records):
+    """sdl_gzip_inflate_first_device: one range per FILE, only its first member -- what
+    async-compression's GzipDecoder (multiple_members off, gzip_file_provider.rs:18, 64)
+    returns, restated by zlib's decompressobj(31) (first_member): `cat a.gz b.gz` -> a,
+    a BGZF file -> its first block, a plain file -> all of it, a large single member (the
+    chunked path) -> all of it; files of every kind side by side in one call."""
+    from streaming_data_loader_amd.device import DeviceBatcher
+    db = DeviceBatcher(batch_size=8, sequence_length=128)
+    p = payloads(records)
+    data = p["jsonl_x3"]
+    a, c = gz_member(data[:7000]), gz_member(data[7000:9000])
+    files = [
+        a + c,                                   # cat a.gz b.gz
+        bgzf(data, block=20000),                 # BGZF: the first block
+        gz_member(data),                         # one member
+        gz_member(p["random"], level=1) + a,     # stored blocks, then another member
+        gz_member(b"") + c,                      # an empty first member
+        gz_member(p["jsonl"] * 40, level=6),     # >= 1 MiB compressed: the chunked path
+        c + a + c,                               # three members
+    ]
+    assert len(files[5]) >= (1 << 20) // 4
+    rc, out, status, got, _ = device_inflate(torch, db, files, first=True)
+    assert rc == 0 and (status & 0xFFFF == 0).all(), status
+    for i, f in enumerate(files):
+        want, _ = first_member(f)
+        assert got[i] == want, i
+        st, o = oracle_lib.gz_inflate(f[:len(f) - len(first_member(f)[1])])
+        assert st == 0 and o == want, i
+
+
+@pytest.mark.gpu
+def test_first_member_mode_false_header_candidates(torch, native_lib, records):
+    """A member whose compressed bytes contain the header pattern 1f 8b 08 (stored blocks of
+    data that spell it): the first candidate end fails its decode and the next is taken."""
+    from streaming_data_loader_amd.device import DeviceBatcher
+    db = DeviceBatcher(batch_size=8, sequence_length=128)
+    pat = b"\x1f\x8b\x08\x00"
+    body = b"x" * 1000 + pat + b"abc" + b"y" * 1000 + pat + b"def" + b"z" * 500  # stored (level 0): in the stream
+    first = gz_member(body, level=0)
+    assert first.find(b"\x1f\x8b\x08\x00", 10) > 0
+    files = [first + gz_member(b"second member"), first]
+    rc, out, status, got, _ = device_inflate(torch, db, files, first=True)
+    assert rc == 0, status
+    assert got == [body, body]
+
+
+@pytest.mark.gpu
+def test_first_member_mode_trailing_garbage_is_the_stated_limit(torch, native_lib, records):
+    from streaming_data_loader_amd.device import DeviceBatcher
+    db = DeviceBatcher(batch_size=8, sequence_length=128)
+    files = [gz_member(b"hello\n") + b"no header in these trailing bytes"]
+    rc, out, status, got, _ = device_inflate(torch, db, files, first=True, check=False)
+    assert rc != 0 and int(status[0]) & 0xFFFF != 0
 
 
 @pytest.mark.gpu

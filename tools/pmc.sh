@@ -9,7 +9,7 @@ CORPUS="${3:-fixture}"
 D=gpurun_out/pmc_${TASK}_${ARENA}_${CORPUS}${PMC_TAG:-}
 mkdir -p $D
 export TMPDIR=/tmp
-ARGS="--task $TASK --steps 2 --warmup 1 --arena-mib $ARENA --corpus $CORPUS --no-cpu-baseline"
+ARGS="--task $TASK --steps 2 --warmup 1 --arena-mib $ARENA --corpus $CORPUS --no-cpu-baseline ${PMC_EXTRA:-}"
 i=0
 while IFS= read -r group; do
   [[ -z "$group" ]] && continue
