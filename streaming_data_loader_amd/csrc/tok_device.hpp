@@ -12,6 +12,7 @@ namespace {
 typedef __attribute__((address_space(3))) uint8_t lds_u8;
 typedef __attribute__((address_space(3))) uint16_t lds_u16;
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
+typedef __attribute__((address_space(3))) uint64_t lds_u64;
 
 constexpr int RBITS_WORDS = WIN / 32;  // 34
 

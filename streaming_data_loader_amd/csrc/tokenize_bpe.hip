@@ -341,6 +341,60 @@ __device__ int bpe_wave_seg(const DevTok &T, uint32_t &sym, int n, uint64_t &hea
     return n;
 }
 
+// One word of 2..LANE_BPE byte symbols per lane, tokenizers' order: BPE::merge_word pops its
+// heap of (rank, position), i.e. the lowest-rank pair, leftmost among equal ranks, one merge at a
+// time.  The symbols and their pairs' merge values stay in registers (static indices: a merge at
+// lane-varying j is a select per slot); only the two pairs a merge creates are probed again.  A
+// wave runs 64 words at once and pays the longest word's merge count in probe latencies, where
+// the segmented wave BPE pays every packed batch's.  s[0 .. returned count) = the word's ids.
+constexpr int LANE_BPE = 16;
+__device__ __forceinline__ int bpe_lane(const DevTok &T, uint32_t (&s)[LANE_BPE], int n) {
+    constexpr uint32_t NOV = 0xFFFFFFFFu;
+    uint32_t v[LANE_BPE - 1];
+#pragma unroll
+    for (int k = 0; k < LANE_BPE - 1; ++k) v[k] = k < n - 1 ? merge_val(T, s[k], s[k + 1]) : NOV;
+    for (;;) {
+        // the lowest rank, leftmost on ties (strict <, ascending k)
+        uint32_t br = 0xFFFFu, bv = 0;
+        int j = -1;
+#pragma unroll
+        for (int k = 0; k < LANE_BPE - 1; ++k) {
+            const uint32_t r = v[k] >> 16;
+            const bool lt = r < br;
+            br = lt ? r : br;
+            bv = lt ? v[k] : bv;
+            j = lt ? k : j;
+        }
+        if (!__any(j >= 0)) break;
+        if (j >= 0) {
+            const uint32_t m = bv & 0xFFFFu;
+            uint32_t left = 0, right = 0;  // the symbols beside the merged pair
+#pragma unroll
+            for (int k = 0; k < LANE_BPE; ++k) {
+                left = k == j - 1 ? s[k] : left;
+                right = k == j + 2 ? s[k] : right;
+            }
+#pragma unroll
+            for (int k = 0; k < LANE_BPE; ++k) {
+                const uint32_t nx = k + 1 < LANE_BPE ? s[k + 1] : 0u;
+                s[k] = k < j ? s[k] : k == j ? m : nx;
+            }
+#pragma unroll
+            for (int k = 0; k < LANE_BPE - 1; ++k) {
+                const uint32_t nx = k + 1 < LANE_BPE - 1 ? v[k + 1] : NOV;
+                v[k] = k < j - 1 ? v[k] : k <= j ? NOV : nx;
+            }
+            --n;
+            // the two new pairs: (left, m) at j - 1 and (m, right) at j
+            const uint32_t vl = j > 0 ? merge_val(T, left, m) : NOV;
+            const uint32_t vr = j < n - 1 ? merge_val(T, m, right) : NOV;
+#pragma unroll
+            for (int k = 0; k < LANE_BPE - 1; ++k) v[k] = k == j - 1 ? vl : k == j ? vr : v[k];
+        }
+    }
+    return n;
+}
+
 }  // namespace
 
 // Diagnostic build (-DSDL_STAMPS): lane 0 of every block adds the s_memtime
@@ -643,8 +697,34 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
     __syncthreads();
 
     BPE_STAMP(3);
-    // ---- 4. wave BPE of the misses, packed: consecutive misses share the lanes --
     const int npend = (int)s_scratch[1];
+#ifndef SDL_BPE_NO_LANE
+    // ---- 4a. misses of <= LANE_BPE bytes: one word per lane (bpe_lane) ----------
+    for (int q0 = 0; q0 < npend; q0 += TOK_THREADS) {  // (wave-uniform)
+        const int q = q0 + lane;
+        int pi = 0, prel = 0, n = 0;
+        if (q < npend) {
+            pi = s_pend[q];
+            prel = (int)(s_pieces[pi] & 0xFFFu);
+            const int nxt = pi + 1 < np ? (int)(s_pieces[pi + 1] & 0xFFFu) : e_last;
+            n = nxt - prel;
+        }
+        const bool mine = n >= 2 && n <= LANE_BPE;
+        if (!__any(mine)) continue;
+        uint32_t sy[LANE_BPE];
+#pragma unroll
+        for (int k = 0; k < LANE_BPE; ++k) sy[k] = mine && k < n ? (uint32_t)T.byte_id[win[prel + HALO_L + k]] : 0u;
+        const int k_out = bpe_lane(T, sy, mine ? n : 0);
+        if (mine) {
+#pragma unroll
+            for (int k = 0; k < LANE_BPE; ++k)
+                if (k < k_out) stage[prel + k] = (uint16_t)sy[k];
+            cnt[pi] = (uint8_t)k_out;
+        }
+    }
+    __syncthreads();
+#endif
+    // ---- 4. wave BPE of the (longer) misses, packed: consecutive misses share the lanes --
     for (int q = 0; q < npend;) {
         int total = 0, nw = 0, wprel = 0, wpi = 0;
         uint32_t sym = 0;
@@ -654,6 +734,12 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
             const int prel = (int)(s_pieces[pi] & 0xFFFu);
             const int nxt = pi + 1 < np ? (int)(s_pieces[pi + 1] & 0xFFFu) : e_last;
             const int n = nxt - prel;
+#ifndef SDL_BPE_NO_LANE
+            if (n <= LANE_BPE) {  // (done in 4a)
+                ++q;
+                continue;
+            }
+#endif
             if (total + n > 64) break;
             if (lane >= total && lane < total + n) sym = (uint32_t)T.byte_id[win[prel + HALO_L + lane - total]];
             if (lane == nw) {
@@ -665,6 +751,7 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
             ++nw;
             ++q;
         }
+        if (total == 0) continue;  // (only short misses were left: 4a took them)
         const int k = bpe_wave_seg(T, sym, total, heads, (lds_u32 *)s_tmp, (lds_u32 *)s_tmpv);
         const uint64_t upto = lane == 63 ? heads : heads & ((2ull << lane) - 1ull);
         const int seg = __popcll(upto) - 1;

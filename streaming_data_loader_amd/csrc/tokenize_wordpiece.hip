@@ -700,9 +700,22 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
     // word setup shared by (a) and (b): returns false if the general path is needed
     auto word_setup = [&](int prel, W16 &lw, int &Lout) -> bool {
         const int wr = prel + HALO_L;
+#ifdef SDL_WP_B64
+        // (A/B) three 8-byte reads at the word's 8-aligned base: ds_read_b64 banks 64 dwords, so
+        // a wave's ~200 bytes of words never meet on a bank (5 ds_read_b32 use 32 banks)
+        const uint32_t sh = (uint32_t)(wr & 3);
+        const int a8 = wr >> 3;
+        const lds_u64 *w64 = (const lds_u64 *)s_win;
+        const uint64_t y0 = w64[a8], y1 = w64[a8 + 1], y2 = w64[a8 + 2];
+        const bool hi = (wr & 4) != 0;
+        const uint32_t x0 = hi ? (uint32_t)(y0 >> 32) : (uint32_t)y0, x1 = hi ? (uint32_t)y1 : (uint32_t)(y0 >> 32),
+                       x2 = hi ? (uint32_t)(y1 >> 32) : (uint32_t)y1, x3 = hi ? (uint32_t)y2 : (uint32_t)(y1 >> 32),
+                       x4 = hi ? (uint32_t)(y2 >> 32) : (uint32_t)y2;
+#else
         const int a = wr >> 2;
         const uint32_t sh = (uint32_t)(wr & 3);
         const uint32_t x0 = w32[a], x1 = w32[a + 1], x2 = w32[a + 2], x3 = w32[a + 3], x4 = w32[a + 4];
+#endif
         const W16 raw{__builtin_amdgcn_alignbyte(x1, x0, sh), __builtin_amdgcn_alignbyte(x2, x1, sh),
                       __builtin_amdgcn_alignbyte(x3, x2, sh), __builtin_amdgcn_alignbyte(x4, x3, sh)};
         const uint32_t b16 = (x4 >> (8 * sh)) & 0xFFu;  // byte at p + 16
