@@ -196,11 +196,16 @@ struct RowParams {
     uint64_t seed;
     uint64_t first_record;
     int32_t rng_mode;              // MLM masks: 0 Philox contract, 1 rand 0.8.5 StdRng (k_mask_rand)
-    // rng_mode 1: the rows' mask bits (S/32 words a row, bit p = position p masked): rows of
-    // chunk k < mask_kmin from mask_bits0 (per record: k_mask_rand_rec + k_mask_bits_rec, run
-    // beside the tokenizer), the others from mask_bitsg (per row: k_mask_rand16)
+    // rng_mode 1: the rows' mask bits (S/32 words a row, bit p = position p masked).  Rows known
+    // before tokenizing -- chunk 0 of every record, chunk 1 of records of >= mask_spec1 bytes
+    // (rand_pre_slot) -- are walked beside the tokenizer (k_mask_rand_rec + k_mask_bits_rec) into
+    // mask_bits0 (slot r, R + r; null: none); the others after the row map into mask_bitsg (per
+    // row: k_mask_rand16).  mask_off / mask_R: the call's record offsets and count.
     const uint32_t *mask_bits0, *mask_bitsg;
-    int32_t mask_w, mask_kmin;
+    const uint64_t *mask_off;
+    int64_t mask_R, mask_spec1;
+    int32_t mask_w;
+    int32_t mask_pass;  // k_rows<MR, true>: 0 every row, 1 rows in mask_bits0 (+ padding), 2 the others
     // span (T5Data): trunc(avg - z) draws as CDF tables (RNG contract) and
     // the <extra_id_k> ids (device pointer, 100 entries)
     int32_t gap_kmin, gap_n, size_kmin, size_n;
@@ -212,6 +217,15 @@ struct RowParams {
 };
 
 __host__ __device__ inline uint32_t ceil_div_u32(uint32_t a, uint32_t b) { return (a + b - 1) / b; }
+
+// rng_mode 1: mask_bits0 slot of row (record r, chunk k) when it was walked beside the tokenizer,
+// else -1 (no text is read: the record's byte length from its offsets)
+__device__ __forceinline__ int64_t rand_pre_slot(const RowParams &P, int64_t r, uint32_t k) {
+    if (!P.mask_bits0) return -1;
+    if (k == 0) return r;
+    if (k == 1 && P.mask_spec1 > 0 && (int64_t)(P.mask_off[r + 1] - P.mask_off[r]) >= P.mask_spec1) return P.mask_R + r;
+    return -1;
+}
 
 // The chunk kernels' block -> chunk map.  Workgroups go to the 8 XCDs round-robin
 // (block b on XCD b % 8): each XCD gets a contiguous run of chunks instead, so a chunk's

@@ -280,14 +280,14 @@ hipError_t launch_rows_direct(const DirectDst &d, const uint32_t *row_off, int64
 hipError_t launch_rows(const RowParams &P, const uint32_t *tok, const uint32_t *rec_tok, const uint32_t *rec_cnt,
                        const uint32_t *row_off, const uint32_t *row_rec, SegSel sel, int64_t rows_cap, RowOut out,
                        hipStream_t st);
-// rng_mode 1 masks (pipeline.hip): every record's chunk-0 row from (seed, first_record + r, 0)
-// alone -- launched beside the tokenizer: swap indices (lane per record) into jbuf [R, S], then
-// the mask bits into bits [R, ceil(S/32)]
-hipError_t launch_mask_rand_rec(const RowParams &P, int64_t R, uint16_t *jbuf, uint32_t *bits, hipStream_t st);
-// ... and the rows g of the segment whose chunk k >= kmin, after the row map: listed (list[0] =
-// count, list[1..] = rows; rows_cap + 1 words), then 16 lanes per row, bits into bitsg [rows, S/32]
+// rng_mode 1 masks (pipeline.hip): the rows rand_pre_slot names (chunk 0 of every record, chunk 1
+// of long ones) from (seed, first_record + r, chunk) alone -- launched beside the tokenizer: swap
+// indices (lane per row) into jbuf [2 R, S], then the mask bits into P.mask_bits0 slots
+hipError_t launch_mask_rand_rec(const RowParams &P, uint16_t *jbuf, uint32_t *bits, hipStream_t st);
+// ... and the other rows g of the segment, after the row map: listed (list[0] = count, list[1..] =
+// rows; rows_cap + 1 words), then 16 lanes per row, bits into bitsg [rows, S/32]
 hipError_t launch_mask_rand_rows(const RowParams &P, const uint32_t *row_off, const uint32_t *row_rec, SegSel sel,
-                                 int64_t rows_cap, int kmin, uint32_t *list, uint32_t *bitsg, hipStream_t st);
+                                 int64_t rows_cap, uint32_t *list, uint32_t *bitsg, hipStream_t st);
 
 // BertData MultiLabel labels_f32 plane (bert_data.rs:66-78)
 hipError_t launch_multi_labels(const uint32_t *labels, const uint64_t *label_off, const uint32_t *row_rec,

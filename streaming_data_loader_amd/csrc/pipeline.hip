@@ -672,6 +672,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MR >= 4 ? S
             lb_o = dd.lab[bi] ? dd.lab[bi] + (size_t)row * P.label_width : nullptr;
         }
         if (g >= (int64_t)G) {  // rows of the last batch nobody filled: initial values
+            if (RM1 && P.mask_pass == 2) continue;  // (written by pass 1)
 #pragma unroll
             for (int m = 0; m < MR; ++m) {
                 const int j0 = 256 * m + 4 * lane;
@@ -684,6 +685,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MR >= 4 ? S
         }
         const int64_t r = row_rec[g];
         const uint32_t k = (uint32_t)(g - row_off[r]);
+        // (rng_mode 1, two passes: the chunk-0 rows while the later rows' masks are walked)
+        const int64_t pre = RM1 ? rand_pre_slot(P, r, k) : -1;
+        if (RM1 && P.mask_pass && ((pre >= 0) != (P.mask_pass == 1))) continue;
         const uint32_t cnt = rec_cnt[r];
         const uint32_t t0 = rec_tok[r];
         const int64_t n = (int64_t)cnt + P.n_pre + P.n_post;
@@ -692,8 +696,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MR >= 4 ? S
         // (rng_mode 1) the row's mask words (k_mask_bits_rec / k_mask_rand16): one dword a lane
         uint32_t mwd[MR];
         if (RM1) {
-            const uint32_t *bw = (int)k < P.mask_kmin ? P.mask_bits0 + r * (int64_t)P.mask_w
-                                                      : P.mask_bitsg + g * (int64_t)P.mask_w;
+            const uint32_t *bw = pre >= 0 ? P.mask_bits0 + pre * (int64_t)P.mask_w : P.mask_bitsg + g * (int64_t)P.mask_w;
 #pragma unroll
             for (int m = 0; m < MR; ++m) {
                 const int j0 = 256 * m + 4 * lane;
@@ -954,38 +957,47 @@ __device__ __forceinline__ void rand_set_bits(const RowParams &P, const uint16_t
 // it on a second stream beside the tokenizer (sdl_batcher.cpp run_device): its ChaCha12 work
 // fills VALU slots the latency-bound tokenizer leaves idle instead of sitting on the step's
 // critical path.  (86 % of the bench's rows are chunk 0.)
-__global__ __launch_bounds__(64) void k_mask_rand_rec(RowParams P, int64_t R, uint16_t *__restrict__ jbuf) {
+// (slot s < R: record s, chunk 0; s = R + r: record r, chunk 1 when rand_pre_slot says so)
+__device__ __forceinline__ bool rand_pre_active(const RowParams &P, int64_t s) {
+    return s < P.mask_R || (s < 2 * P.mask_R && rand_pre_slot(P, s - P.mask_R, 1u) == s);
+}
+__global__ __launch_bounds__(64) void k_mask_rand_rec(RowParams P, uint16_t *__restrict__ jbuf) {
     const int lane = lane_id();
-    for (int64_t r0 = (int64_t)blockIdx.x * 64; r0 < R; r0 += (int64_t)gridDim.x * 64) {
-        const int64_t r = r0 + lane;
-        const bool active = r < R;
-        rand_walk_lane(P, active, P.first_record + (uint64_t)(active ? r : 0), 0u, jbuf + (active ? r : 0) * (int64_t)P.S);
+    const int64_t R = P.mask_R, ns = P.mask_spec1 > 0 ? 2 * R : R;
+    for (int64_t s0 = (int64_t)blockIdx.x * 64; s0 < ns; s0 += (int64_t)gridDim.x * 64) {
+        const int64_t s = s0 + lane;
+        const bool active = s < ns && rand_pre_active(P, s);
+        const int64_t r = active ? (s < R ? s : s - R) : 0;
+        rand_walk_lane(P, active, P.first_record + (uint64_t)r, s < R ? 0u : 1u, jbuf + (active ? s : 0) * (int64_t)P.S);
     }
 }
 
 // Phase B for those rows: a wave per record, its mask bits -> bits[r]
 template <int MR4>
-__global__ __launch_bounds__(256) void k_mask_bits_rec(RowParams P, int64_t R, const uint16_t *__restrict__ jbuf,
+__global__ __launch_bounds__(256) void k_mask_bits_rec(RowParams P, const uint16_t *__restrict__ jbuf,
                                                        uint32_t *__restrict__ bits) {
     __shared__ uint32_t s_nx[4][64 * MR4];
     __shared__ uint32_t s_bt[4][2 * MR4];
     const int lane = lane_id(), wid = (int)(threadIdx.x >> 6);
-    for (int64_t r = (int64_t)blockIdx.x * 4 + wid; r < R; r += (int64_t)gridDim.x * 4) {
-        rand_set_bits<MR4>(P, jbuf + r * (int64_t)P.S, s_nx[wid], s_bt[wid], lane);
-        for (int w = lane; w < P.mask_w; w += 64) bits[r * (int64_t)P.mask_w + w] = s_bt[wid][w];
+    const int64_t ns = P.mask_spec1 > 0 ? 2 * P.mask_R : P.mask_R;
+    for (int64_t s = (int64_t)blockIdx.x * 4 + wid; s < ns; s += (int64_t)gridDim.x * 4) {
+        if (!rand_pre_active(P, s)) continue;  // (wave-uniform)
+        rand_set_bits<MR4>(P, jbuf + s * (int64_t)P.S, s_nx[wid], s_bt[wid], lane);
+        for (int w = lane; w < P.mask_w; w += 64) bits[s * (int64_t)P.mask_w + w] = s_bt[wid][w];
         __builtin_amdgcn_wave_barrier();  // (s_bt is rewritten by the wave's next record)
     }
 }
 
-hipError_t launch_mask_rand_rec(const RowParams &P, int64_t R, uint16_t *jbuf, uint32_t *bits, hipStream_t st) {
+hipError_t launch_mask_rand_rec(const RowParams &P, uint16_t *jbuf, uint32_t *bits, hipStream_t st) {
+    const int64_t R = P.mask_R, ns = P.mask_spec1 > 0 ? 2 * R : R;
     if (R <= 0) return hipSuccess;
-    if (P.S > RAND_MAX_S || P.mask_w * 32 < P.S) return hipErrorInvalidValue;
-    const int64_t want = (R + 63) / 64;
-    hipLaunchKernelGGL(k_mask_rand_rec, dim3((unsigned)(want < 8192 ? want : 8192)), dim3(64), 0, st, P, R, jbuf);
-    const int64_t wb = (R + 3) / 4;
+    if (P.S > RAND_MAX_S || P.mask_w * 32 < P.S || !P.mask_off) return hipErrorInvalidValue;
+    const int64_t want = (ns + 63) / 64;
+    hipLaunchKernelGGL(k_mask_rand_rec, dim3((unsigned)(want < 8192 ? want : 8192)), dim3(64), 0, st, P, jbuf);
+    const int64_t wb = (ns + 3) / 4;
     const dim3 g((unsigned)(wb < 16384 ? wb : 16384));
     const int MR4 = (P.S + 63) / 64;
-#define SDL_BITS(M) hipLaunchKernelGGL(k_mask_bits_rec<M>, g, dim3(256), 0, st, P, R, (const uint16_t *)jbuf, bits)
+#define SDL_BITS(M) hipLaunchKernelGGL(k_mask_bits_rec<M>, g, dim3(256), 0, st, P, (const uint16_t *)jbuf, bits)
     if (MR4 <= 2) SDL_BITS(2);
     else if (MR4 <= 4) SDL_BITS(4);
     else if (MR4 <= 8) SDL_BITS(8);
@@ -1001,13 +1013,27 @@ hipError_t launch_mask_rand_rec(const RowParams &P, int64_t R, uint16_t *jbuf, u
 // into LDS; lane 0 of the row walks the 256 words (rand's acceptance test, the same sequence as
 // rand_walk_lane) and puts each swap straight into next() (an LDS atomicMin, as rand_set_bits
 // does from the stored indices); the row's lanes then follow the chains and write its bits.
-__global__ __launch_bounds__(256) void k_rand_list(const uint32_t *__restrict__ row_off,
+__global__ __launch_bounds__(256) void k_rand_list(RowParams P, const uint32_t *__restrict__ row_off,
                                                    const uint32_t *__restrict__ row_rec, SegSel sel, int64_t rows_cap,
-                                                   int B, int kmin, uint32_t *__restrict__ list) {
-    const RowSpan rs = row_span(sel, row_off, B, rows_cap);
-    for (int64_t g = rs.g_lo + (int64_t)blockIdx.x * 256 + threadIdx.x; g < rs.g_real; g += (int64_t)gridDim.x * 256) {
-        const uint32_t r = row_rec[g];
-        if ((int64_t)(g - row_off[r]) >= kmin) list[1 + atomicAdd(&list[0], 1u)] = (uint32_t)g;
+                                                   uint32_t *__restrict__ list) {
+    const RowSpan rs = row_span(sel, row_off, P.B, rows_cap);
+    const int lane = lane_id();
+    // (wave-uniform trip count; one atomic per wave: a counter hit by every row serialized the launch)
+    for (int64_t g0 = rs.g_lo + (int64_t)blockIdx.x * 256 + (threadIdx.x & ~63u); g0 < rs.g_real;
+         g0 += (int64_t)gridDim.x * 256) {
+        const int64_t g = g0 + lane;
+        bool take = false;
+        if (g < rs.g_real) {
+            const uint32_t r = row_rec[g];
+            take = rand_pre_slot(P, r, (uint32_t)(g - row_off[r])) < 0;
+        }
+        const uint64_t m = __ballot(take);
+        if (!m) continue;
+        const int leader = __builtin_ctzll(m);
+        uint32_t base = 0;
+        if (lane == leader) base = atomicAdd(&list[0], (uint32_t)__popcll(m));
+        base = (uint32_t)lane_bcast((int)base, leader);
+        if (take) list[1 + base + __popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)g;
     }
 }
 
@@ -1017,7 +1043,7 @@ __global__ __launch_bounds__(64) void k_mask_rand16(RowParams P, const uint32_t 
                                                     const uint32_t *__restrict__ list, uint32_t *__restrict__ bitsg) {
     constexpr uint32_t NONE = 0xFFFFFFFFu;
     __shared__ __attribute__((aligned(16))) uint32_t s_win[4][256];  // a row's window of 16 ChaCha12 blocks
-    __shared__ uint32_t s_nx[4][64 * MR4];
+    __shared__ uint32_t s_nx[4][64 * MR4 + 1];  // (+ the DUMMY slot)
     __shared__ uint32_t s_bt[4][2 * MR4];
     const int lane = lane_id(), grp = lane >> 4, gl = lane & 15;
     const int S = P.S, kmask = P.mask_length < S ? P.mask_length : S;
@@ -1045,10 +1071,11 @@ __global__ __launch_bounds__(64) void k_mask_rand16(RowParams P, const uint32_t 
             key[4] = (uint32_t)(g - row_off[r]);
         }
         for (int x = gl; x < 64 * MR4; x += 16) s_nx[grp][x] = NONE;
-        if (gl < 2 * MR4) s_bt[grp][gl] = 0u;
+        for (int x = gl; x < 2 * MR4; x += 16) s_bt[grp][x] = 0u;  // (S > 512: more words than lanes)
         // the walk's state lives in lane 0 of the row
         int i = active ? S - 1 : 0;
         uint32_t n = (uint32_t)i + 1u, zone = (n << __builtin_clz(n)) - 1u;
+        constexpr uint32_t DUMMY = 64 * MR4;  // a swap that moves nothing lands here (never read)
         for (uint32_t blk = 0;; blk += 16) {
             // wave-uniform: stop when no row of the wave has steps left
             const int irow = __builtin_amdgcn_update_dpp(0, i, 0x150, 0xF, 0xF, false);  // row_newbcast:0
@@ -1061,22 +1088,26 @@ __global__ __launch_bounds__(64) void k_mask_rand16(RowParams P, const uint32_t 
             wv[2] = make_uint4(o[8], o[9], o[10], o[11]);
             wv[3] = make_uint4(o[12], o[13], o[14], o[15]);
             wave_sync();
-            if (gl == 0 && i >= i0) {
+            if (gl == 0) {
+                // branch-free over the window's 256 words (rand_walk_lane's test per word, the
+                // LDS atomic unconditional: a rejected word or a self swap targets DUMMY), the
+                // next 4 words' load in flight during these 4
                 const uint4 *w4 = reinterpret_cast<const uint4 *>(&s_win[grp][0]);
-                for (int t = 0; t < 64 && i >= i0; ++t) {
-                    const uint4 x = w4[t];
+                uint4 x = w4[0];
+                for (int t = 0; t < 64; ++t) {
+                    const uint4 xn = w4[t + 1 < 64 ? t + 1 : 63];
                     const uint32_t xs[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
                     for (int u = 0; u < 4; ++u) {
                         const uint64_t m = (uint64_t)xs[u] * n;
-                        if (i >= i0 && (uint32_t)m <= zone) {
-                            const uint32_t j = (uint32_t)(m >> 32);
-                            if (j != (uint32_t)i) atomicMin(&s_nx[grp][j], (uint32_t)i);
-                            --i;
-                            n = (uint32_t)i + 1u;
-                            zone = (n << __builtin_clz(n)) - 1u;
-                        }
+                        const bool acc = i >= i0 && (uint32_t)m <= zone;
+                        const uint32_t j = (uint32_t)(m >> 32);
+                        atomicMin(&s_nx[grp][acc && j != (uint32_t)i ? j : DUMMY], (uint32_t)i);
+                        i -= acc ? 1 : 0;
+                        n = (uint32_t)i + 1u;
+                        zone = (n << __builtin_clz(n)) - 1u;
                     }
+                    x = xn;
                 }
             }
             wave_sync();  // (the window is rewritten next)
@@ -1095,14 +1126,14 @@ __global__ __launch_bounds__(64) void k_mask_rand16(RowParams P, const uint32_t 
 }
 
 hipError_t launch_mask_rand_rows(const RowParams &P, const uint32_t *row_off, const uint32_t *row_rec, SegSel sel,
-                                 int64_t rows_cap, int kmin, uint32_t *list, uint32_t *bitsg, hipStream_t st) {
+                                 int64_t rows_cap, uint32_t *list, uint32_t *bitsg, hipStream_t st) {
     if (rows_cap <= 0) return hipSuccess;
     if (P.S > RAND_MAX_S || P.mask_w * 32 < P.S) return hipErrorInvalidValue;
     hipError_t e = hipMemsetAsync(list, 0, 4, st);
     if (e != hipSuccess) return e;
     const int64_t want = (rows_cap + 255) / 256;
-    hipLaunchKernelGGL(k_rand_list, dim3((unsigned)(want < 2048 ? want : 2048)), dim3(256), 0, st, row_off, row_rec,
-                       sel, rows_cap, P.B, kmin, list);
+    hipLaunchKernelGGL(k_rand_list, dim3((unsigned)(want < 2048 ? want : 2048)), dim3(256), 0, st, P, row_off, row_rec,
+                       sel, rows_cap, list);
     const int64_t w4 = (rows_cap + 3) / 4;
     const dim3 g((unsigned)(w4 < 16384 ? w4 : 16384));
     const int MR4 = (P.S + 63) / 64;
@@ -1211,7 +1242,7 @@ hipError_t launch_rows(const RowParams &P, const uint32_t *tok, const uint32_t *
     const int MR = (P.S + 255) / 256;
     if (P.label_width > 256 * MR) return hipErrorInvalidValue;
     const bool rm1 = P.task == 0 && P.rng_mode == 1;
-    if (rm1 && (!P.mask_bitsg || (P.mask_kmin > 0 && !P.mask_bits0) || P.mask_w * 32 < P.S)) return hipErrorInvalidValue;
+    if (rm1 && (!P.mask_bitsg || (P.mask_bits0 && !P.mask_off) || P.mask_w * 32 < P.S)) return hipErrorInvalidValue;
 #define SDL_ROWS(MM)                                                                                                 \
     if (rm1)                                                                                                          \
         hipLaunchKernelGGL((k_rows<MM, true>), dim3(grid), dim3(256), 0, st, P, tok, rec_tok, rec_cnt, row_off,      \

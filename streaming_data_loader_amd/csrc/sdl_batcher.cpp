@@ -234,6 +234,11 @@ int env_int(const char *name, int dflt) {
     const char *e = std::getenv(name);
     return e ? std::max(1, std::atoi(e)) : dflt;
 }
+// the same for switches and values where 0 means something (env_int reads "0" as 1)
+int env_int0(const char *name, int dflt) {
+    const char *e = std::getenv(name);
+    return e ? std::max(0, std::atoi(e)) : dflt;
+}
 
 }  // namespace
 
@@ -273,7 +278,7 @@ struct sdl_batcher {
     // tokenizer on stream2), the later rows' list and bits (k_mask_rand16)
     DevBuf<uint16_t> mask_j0;
     DevBuf<uint32_t> mask_bits0, mask_bitsg, rand_list;
-    hipEvent_t rand_ev[2] = {nullptr, nullptr};
+    hipEvent_t rand_ev[4] = {nullptr, nullptr, nullptr, nullptr};
     DevBuf<float> o_f32;
     DevBuf<uint32_t> lab_err;
     // byte-level BPE long pieces
@@ -285,13 +290,16 @@ struct sdl_batcher {
     // span rows in two phases: per-row pass plans, row meta, overflow rows
     DevBuf<uint2> span_tab, span_meta;
     DevBuf<uint32_t> span_ovf;
-    bool span_two_phase = env_int("SDL_SPAN_TWO_PHASE", 0) != 0;
-    bool small_calls = env_int("SDL_SMALL_CALLS", 1) != 0;  // k_downstream_small + folded record bounds
+    bool span_two_phase = env_int0("SDL_SPAN_TWO_PHASE", 0) != 0;
+    bool small_calls = env_int0("SDL_SMALL_CALLS", 1) != 0;  // k_downstream_small + folded record bounds
     // rng_mode 1: chunk-0 rows walked beside the tokenizer (0: every row after the row map, 16 lanes each)
-    bool rand_rec0 = env_int("SDL_RAND_REC0", 1) != 0;
+    bool rand_rec0 = env_int0("SDL_RAND_REC0", 1) != 0;
+    // ... and chunk 1 of records of >= (S - frame + 1) / rho bytes (WordPiece/BPE give ~0.2-0.3 ids
+    // per byte; SDL_RAND_SPEC_RHO_PCT=0: chunk 0 only)
+    double rand_spec_rho = env_int0("SDL_RAND_SPEC_RHO_PCT", 25) / 100.0;
     // test hook: clamp the Unigram long-item list (0 = its N / 8 + chunks bound), so the capacity
     // flag can be raised through every path that reports it
-    uint32_t uni_item_cap = (uint32_t)std::max(0, env_int("SDL_UNI_ITEM_CAP", 0));
+    uint32_t uni_item_cap = (uint32_t)std::max(0, env_int0("SDL_UNI_ITEM_CAP", 0));
     // JsonText provider step (sdl_json_text_device)
     DevBuf<uint32_t> j_cnt, j_base, j_nl, j_len, j_rec, j_toff, j_ridx, j_inv, j_tail;
     DevBuf<uint2> j_span;
@@ -462,9 +470,12 @@ struct sdl_batcher {
         RowParams p = P;
         p.first_record = first_record;
         p.mask_w = mask_w;
-        p.mask_kmin = 0;
         p.mask_bits0 = nullptr;
         p.mask_bitsg = mask_bitsg.p;
+        p.mask_off = d_off;
+        p.mask_R = R;
+        p.mask_spec1 = 0;
+        p.mask_pass = 0;
         const bool bpe = dt.kind == TOK_BYTE_BPE;
         const bool uni = dt.kind == TOK_UNIGRAM;
         // Pipelined segments (WordPiece): the tokenize launches of the chunk
@@ -489,26 +500,31 @@ struct sdl_batcher {
         };
         const bool small = small_calls && !piped && !profiling && n_chunks <= SMALL_CHUNKS && R <= 8192;
         mark(0);
-        // rng_mode 1: every record's chunk-0 row depends on (seed, record) alone -- its walk and mask
-        // bits run on stream2 beside the tokenizer (k_mask_rand_rec); k_rows waits for them
-        const bool rec0 = rm1 && !piped && !small && R > 0 && rand_rec0;
-        if (rec0) {
-            mask_j0.ensure((size_t)R * (size_t)P.S);
-            mask_bits0.ensure((size_t)R * (size_t)mask_w);
-            if (!stream2) HIP_TRY(hipStreamCreateWithFlags(&stream2, hipStreamNonBlocking));
-            for (auto &e : rand_ev)
-                if (!e) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-            HIP_TRY(hipEventRecord(rand_ev[0], st));  // (the last call's rows have read mask_bits0)
-            HIP_TRY(hipStreamWaitEvent(stream2, rand_ev[0], 0));
-            HIP_TRY(launch_mask_rand_rec(p, R, mask_j0.p, mask_bits0.p, stream2));
-            HIP_TRY(hipEventRecord(rand_ev[1], stream2));
-            p.mask_bits0 = mask_bits0.p;
-            p.mask_kmin = 1;
-        }
         // (one segment: k_chunk_ranges also writes its record bounds and zeroes the label error word)
         const bool fold = small_calls && sc.K == 1 && n_chunks > 0;
         HIP_TRY(launch_chunk_ranges(d_off, R, N, ranges.p, st, fold ? seg_rb.p : nullptr,
                                     fold && (multi() || single()) ? lab_err.p : nullptr));
+        // rng_mode 1: a row's masks depend on (seed, record, chunk) alone, so the rows known before
+        // tokenizing -- chunk 0 of every record, chunk 1 of records long enough to need one at
+        // <= rand_spec_rho ids per byte -- are walked, and their mask bits made, on stream2 beside
+        // the tokenizer (queued after k_chunk_ranges: launched first, their long waves held it back
+        // 0.12 ms); k_rows waits for them.  Rows past the guess take the late path (correct either way).
+        const bool rec0 = rm1 && !piped && !small && R > 0 && rand_rec0;
+        if (rec0) {
+            const int64_t F = P.n_pre + P.n_post;
+            p.mask_spec1 = P.chunk && rand_spec_rho > 0 ? (int64_t)((double)(P.S - F + 1) / rand_spec_rho) : 0;
+            const int64_t ns = p.mask_spec1 > 0 ? 2 * R : R;
+            mask_j0.ensure((size_t)ns * (size_t)P.S);
+            mask_bits0.ensure((size_t)ns * (size_t)mask_w);
+            ensure_stream2();
+            for (auto &e : rand_ev)
+                if (!e) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            HIP_TRY(hipEventRecord(rand_ev[0], st));  // (the last call's rows have read mask_bits0)
+            HIP_TRY(hipStreamWaitEvent(stream2, rand_ev[0], 0));
+            p.mask_bits0 = mask_bits0.p;
+            HIP_TRY(launch_mask_rand_rec(p, mask_j0.p, mask_bits0.p, stream2));
+            HIP_TRY(hipEventRecord(rand_ev[1], stream2));
+        }
         if (!fold) HIP_TRY(launch_seg_bounds(ranges.p, sc, R, seg_rb.p, st));
         if (!fold && (multi() || single())) HIP_TRY(hipMemsetAsync(lab_err.p, 0, 4, st));
         mark(1);
@@ -571,12 +587,27 @@ struct sdl_batcher {
                 HIP_TRY(launch_rows_span(p, tok_ids.p, rec_tok.p, rec_cnt.p, row_off.p, row_rec.p, sel, rows_cap, out,
                                          span_err.p, s, two_phase ? &pl : nullptr));
             } else {
-                if (rm1) {
-                    HIP_TRY(launch_mask_rand_rows(p, row_off.p, row_rec.p, sel, rows_cap, p.mask_kmin, rand_list.p,
-                                                  mask_bitsg.p, s));
-                    if (rec0) HIP_TRY(hipStreamWaitEvent(s, rand_ev[1], 0));
+                if (rm1 && rec0) {
+                    // the later rows' masks (chunk >= 1, known now) are walked on stream2 while the
+                    // chunk-0 rows -- their bits made beside the tokenizer -- are written here
+                    HIP_TRY(hipEventRecord(rand_ev[2], s));
+                    HIP_TRY(hipStreamWaitEvent(stream2, rand_ev[2], 0));
+                    HIP_TRY(launch_mask_rand_rows(p, row_off.p, row_rec.p, sel, rows_cap, rand_list.p, mask_bitsg.p,
+                                                  stream2));
+                    HIP_TRY(hipEventRecord(rand_ev[3], stream2));
+                    HIP_TRY(hipStreamWaitEvent(s, rand_ev[1], 0));
+                    RowParams p1 = p;
+                    p1.mask_pass = 1;
+                    HIP_TRY(launch_rows(p1, tok_ids.p, rec_tok.p, rec_cnt.p, row_off.p, row_rec.p, sel, rows_cap, out, s));
+                    HIP_TRY(hipStreamWaitEvent(s, rand_ev[3], 0));
+                    p1.mask_pass = 2;
+                    HIP_TRY(launch_rows(p1, tok_ids.p, rec_tok.p, rec_cnt.p, row_off.p, row_rec.p, sel, rows_cap, out, s));
+                } else {
+                    if (rm1)
+                        HIP_TRY(launch_mask_rand_rows(p, row_off.p, row_rec.p, sel, rows_cap, rand_list.p,
+                                                      mask_bitsg.p, s));
+                    HIP_TRY(launch_rows(p, tok_ids.p, rec_tok.p, rec_cnt.p, row_off.p, row_rec.p, sel, rows_cap, out, s));
                 }
-                HIP_TRY(launch_rows(p, tok_ids.p, rec_tok.p, rec_cnt.p, row_off.p, row_rec.p, sel, rows_cap, out, s));
             }
             if (multi())
                 HIP_TRY(launch_multi_labels(d_labels, d_label_off, row_rec.p, row_off.p, sel, rows_cap, P.B,
@@ -646,7 +677,15 @@ struct sdl_batcher {
             HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
             pipe_ev.push_back(e);
         }
-        if (!stream2) HIP_TRY(hipStreamCreateWithFlags(&stream2, hipStreamNonBlocking));
+        ensure_stream2();
+    }
+    // stream2 runs background work (rng_mode 1 mask walks, pipelined segments) at the lowest
+    // priority, so the dispatcher hands CUs to the handle's stream first
+    void ensure_stream2() {
+        if (stream2) return;
+        int least = 0, greatest = 0;
+        if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) least = 0;
+        HIP_TRY(hipStreamCreateWithPriority(&stream2, hipStreamNonBlocking, least));
     }
     int64_t last_segments = 1;
     int64_t last_rows_cap = 0, last_R = 0;
@@ -927,7 +966,11 @@ int sdl_batcher_create(const sdl_config *cfg, const char *tokenizer_path, const 
         h->device = cfg->device;
         load_tokenizer(tokenizer_path, data_dir ? std::string(data_dir) : default_data_dir(), h->tok);
         HIP_TRY(hipSetDevice(h->device));
-        HIP_TRY(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+        {  // the handle's stream at the highest priority (stream2's background work yields to it)
+            int least = 0, greatest = 0;
+            if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) greatest = 0;
+            HIP_TRY(hipStreamCreateWithPriority(&h->stream, hipStreamNonBlocking, greatest));
+        }
         for (auto &e : h->ev) HIP_TRY(hipEventCreate(&e));
         auto &t = h->tok;
         h->d_ubmp.ensure(t.ubmp.size());
@@ -2149,7 +2192,7 @@ int sdl_json_to_frames(sdl_batcher *h, const uint8_t *jsonl, uint64_t len, uint6
                 h->f_dry = false;
                 if (rc) return rc;
                 h->x_pin_out[slot].ensure((size_t)fr.total_bytes + 16);
-                const bool mapped = env_int("SDL_FRAMES_MAPPED", 0) != 0;
+                const bool mapped = env_int0("SDL_FRAMES_MAPPED", 0) != 0;
                 const hipStream_t fs = mapped ? h->x_out : sc;
                 if (mapped) {
                     void *dp = nullptr;

@@ -66,3 +66,28 @@ def test_rand_mode_dense_records_match_oracle(torch, native_lib, oracle_tok, rec
     assert want.shape[1] == G
     for j in range(4):
         np.testing.assert_array_equal(got[j], want[j])
+
+
+@pytest.mark.parametrize("env", [{"SDL_RAND_REC0": "0"}, {"SDL_RAND_SPEC_RHO_PCT": "0"},
+                                 {"SDL_RAND_SPEC_RHO_PCT": "100"}, {"SDL_RAND_SPEC_RHO_PCT": "5"}])
+def test_rand_mode_mask_paths_agree(torch, native_lib, oracle_tok, records, env, monkeypatch):
+    """The rows' masks come from three places (pipeline.hip rand_pre_slot): chunk 0 and guessed
+    chunk-1 rows walked beside the tokenizer, the rest after the row map 16 lanes a row.  Every
+    split -- nothing beside the tokenizer, chunk 0 only, chunk 1 of every record long enough at 1
+    id per byte (every chunk-1 row there), at 0.05 ids per byte (chunk 1 guessed for few
+    records) -- gives the oracle's rows."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    rng = np.random.default_rng(31)
+    texts = [records[i] for i in rng.integers(0, len(records), 200)]
+    texts += [" ".join(records[i] for i in rng.integers(0, len(records), 4)) for _ in range(20)]  # 3+ rows
+    S, B, seed, first = 256, 16, 1234, 40
+    k = int(np.float32(S) * np.float32(0.15))
+    db = DeviceBatcher(batch_size=B, sequence_length=S, seed=seed, rng_mode=1)
+    res = run_device(torch, db, texts, first_record=first)
+    G = res.rows()
+    got = res.planes(G)
+    want = oracle_lib.oracle_rows(oracle_tok, texts, S, k, 103, seed=seed, B=B, first_record=first, rng_mode=1)
+    assert want.shape[1] == G
+    for j in range(4):
+        np.testing.assert_array_equal(got[j], want[j])
