@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <type_traits>
 
 namespace sdl {
 
@@ -199,13 +200,12 @@ struct RowParams {
     // rng_mode 1: the rows' mask bits (S/32 words a row, bit p = position p masked).  Rows known
     // before tokenizing -- chunk 0 of every record, chunk 1 of records of >= mask_spec1 bytes
     // (rand_pre_slot) -- are walked beside the tokenizer (k_mask_rand_rec + k_mask_bits_rec) into
-    // mask_bits0 (slot r, R + r; null: none); the others after the row map into mask_bitsg (per
-    // row: k_mask_rand16).  mask_off / mask_R: the call's record offsets and count.
-    const uint32_t *mask_bits0, *mask_bitsg;
+    // mask_bits0 (slot r, R + r; null: none); k_rows' LATE pass walks the others (rand_rows16).
+    // mask_off / mask_R: the call's record offsets and count.
+    const uint32_t *mask_bits0;
     const uint64_t *mask_off;
     int64_t mask_R, mask_spec1;
     int32_t mask_w;
-    int32_t mask_pass;  // k_rows<MR, true>: 0 every row, 1 rows in mask_bits0 (+ padding), 2 the others
     // span (T5Data): trunc(avg - z) draws as CDF tables (RNG contract) and
     // the <extra_id_k> ids (device pointer, 100 entries)
     int32_t gap_kmin, gap_n, size_kmin, size_n;
@@ -217,6 +217,15 @@ struct RowParams {
 };
 
 __host__ __device__ inline uint32_t ceil_div_u32(uint32_t a, uint32_t b) { return (a + b - 1) / b; }
+
+// f(std::integral_constant<int, i>) for i = A .. B - 1, in order (a compile-time index for DPP controls)
+template <int A, int B, class F>
+__device__ __forceinline__ void static_for(const F &f) {
+    if constexpr (A < B) {
+        f(std::integral_constant<int, A>{});
+        static_for<A + 1, B>(f);
+    }
+}
 
 // rng_mode 1: mask_bits0 slot of row (record r, chunk k) when it was walked beside the tokenizer,
 // else -1 (no text is read: the record's byte length from its offsets)

@@ -253,6 +253,8 @@ struct SmallDown {
     uint32_t *stat;  // or null: row_off[0..R], a zero label-error word and the tokenizer's error word
                      // (mapped host memory, DirectDst)
     const uint32_t *tok_err;  // or null: the Unigram capacity flags (uni_err), copied to stat[R + 2]
+    int rows;                 // 1: also the call's rows (k_rows' body) into `out` -- mlm (Philox) / clm
+    RowOut out;
 };
 hipError_t launch_downstream_small(const SmallDown &d, const RowParams &P, const uint64_t *off, int64_t R, int64_t N,
                                    hipStream_t st);
@@ -279,16 +281,14 @@ hipError_t launch_rows_direct(const DirectDst &d, const uint32_t *row_off, int64
 
 hipError_t launch_rows(const RowParams &P, const uint32_t *tok, const uint32_t *rec_tok, const uint32_t *rec_cnt,
                        const uint32_t *row_off, const uint32_t *row_rec, SegSel sel, int64_t rows_cap, RowOut out,
-                       hipStream_t st);
+                       hipStream_t st,
+                       hipStream_t st_late = nullptr);
 // rng_mode 1 masks (pipeline.hip): the rows rand_pre_slot names (chunk 0 of every record, chunk 1
 // of long ones) from (seed, first_record + r, chunk) alone -- launched beside the tokenizer: swap
 // indices (lane per row) into jbuf [2 R, S], then the mask bits into P.mask_bits0 slots
-hipError_t launch_mask_rand_rec(const RowParams &P, uint16_t *jbuf, uint32_t *bits, hipStream_t st);
+hipError_t launch_mask_rand_rec(const RowParams &P, uint32_t *list, uint16_t *jbuf, uint32_t *bits, hipStream_t st);
 // ... and the other rows g of the segment, after the row map: listed (list[0] = count, list[1..] =
 // rows; rows_cap + 1 words), then 16 lanes per row, bits into bitsg [rows, S/32]
-hipError_t launch_mask_rand_rows(const RowParams &P, const uint32_t *row_off, const uint32_t *row_rec, SegSel sel,
-                                 int64_t rows_cap, uint32_t *list, uint32_t *bitsg, hipStream_t st);
-
 // BertData MultiLabel labels_f32 plane (bert_data.rs:66-78)
 hipError_t launch_multi_labels(const uint32_t *labels, const uint64_t *label_off, const uint32_t *row_rec,
                                const uint32_t *row_off, SegSel sel, int64_t rows_cap, int B, int NL, float *out,

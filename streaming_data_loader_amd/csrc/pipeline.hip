@@ -434,40 +434,6 @@ __device__ __forceinline__ void block_scan_small(const uint32_t *__restrict__ in
     if (threadIdx.x == 0) out[n] = tot;
 }
 
-__global__ __launch_bounds__(SCAN_SMALL_NT) void k_downstream_small(SmallDown d, RowParams P,
-                                                                    const uint64_t *__restrict__ off, int64_t R,
-                                                                    int64_t N, int64_t n_chunks) {
-    __shared__ uint32_t scratch[SCAN_SMALL_NT / 64];
-    block_scan_small(d.chunk_cnt, n_chunks, d.chunk_off, scratch);
-    __syncthreads();
-    for (int64_t cb = (int64_t)(threadIdx.x >> 6) * COMPACT_CPW; cb < n_chunks;
-         cb += (int64_t)(SCAN_SMALL_NT / 64) * COMPACT_CPW)
-        compact_wave(cb, d.tokc, d.chunk_cnt, d.chunk_off, n_chunks, d.tok, d.long_count, d.chunk_ent, d.long_list,
-                     d.long_scratch, d.long_pool, d.stride);
-    for (int64_t r = threadIdx.x; r < R; r += SCAN_SMALL_NT)
-        record_one(P, off, r, N, d.chunk_off, n_chunks, d.rec_local, d.rec_tok, d.rec_cnt, d.rec_rows);
-    __syncthreads();
-    block_scan_small(d.rec_rows, R, d.row_off, scratch);
-    __syncthreads();
-    for (int64_t r = threadIdx.x; r < R; r += SCAN_SMALL_NT)
-        for (uint32_t g = d.row_off[r]; g < d.row_off[r + 1]; ++g) d.row_rec[g] = (uint32_t)r;
-    if (d.stat) {
-        for (int64_t r = threadIdx.x; r <= R; r += SCAN_SMALL_NT) d.stat[r] = d.row_off[r];
-        if (threadIdx.x == 0) {
-            d.stat[R + 1] = 0u;
-            d.stat[R + 2] = d.tok_err ? *d.tok_err : 0u;  // a t5 tokenizer under mlm / clm
-        }
-    }
-}
-
-hipError_t launch_downstream_small(const SmallDown &d, const RowParams &P, const uint64_t *off, int64_t R, int64_t N,
-                                   hipStream_t st) {
-    const int64_t n_chunks = (N + CHUNK - 1) / CHUNK;
-    if (n_chunks > SMALL_CHUNKS || R > SCAN_SMALL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_downstream_small, dim3(1), dim3(SCAN_SMALL_NT), 0, st, d, P, off, R, N, n_chunks);
-    return hipGetLastError();
-}
-
 hipError_t launch_row_map(const uint32_t *row_off, int64_t R, uint32_t *row_rec, SegSel sel, hipStream_t st) {
     if (R == 0) return hipSuccess;
     const int64_t want = (R + 255) / 256;
@@ -642,192 +608,6 @@ __device__ __forceinline__ void store4(int32_t *p, int j0, int S, bool vec, int3
 #ifndef SDL_ROWS_WAVES_RM1
 #define SDL_ROWS_WAVES_RM1 6  // (r04: left to the compiler, 103 VGPRs, 4 waves: rows 0.347 ms; 7 spills 20 B)
 #endif
-// RM1: MLM under rng_mode 1 (the rows' mask words from k_mask_bits_rec / k_mask_rand16).  A template flag, not
-// a runtime branch: the mask-word registers would cost the Philox path a wave
-// per SIMD (k_rows<2>: 80 -> 82 VGPRs, 6 -> 5 waves, 0.267 -> 0.295 ms).
-template <int MR, bool RM1>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MR >= 4 ? SDL_ROWS_WAVES4 : RM1 ? SDL_ROWS_WAVES_RM1 : SDL_ROWS_WAVES, 8))) void k_rows(RowParams P, const uint32_t *__restrict__ tok,
-                                              const uint32_t *__restrict__ rec_tok, const uint32_t *__restrict__ rec_cnt,
-                                              const uint32_t *__restrict__ row_off, const uint32_t *__restrict__ row_rec,
-                                              SegSel sel, int64_t rows_cap, RowOut out) {
-    const int lane = lane_id();
-    const int wid = (int)(threadIdx.x >> 6);
-    const int S = P.S;
-    const bool vec = (S & 3) == 0;  // 16-byte aligned rows
-    const bool vec_lb = (P.label_width & 3) == 0;
-    const RowSpan rs = row_span(sel, row_off, P.B, rows_cap);
-    const int64_t G = rs.g_real;
-    const DirectDst &dd = out.direct;
-    const int64_t g_end = dd.cap ? rs.g_real : rs.g_end;  // (direct: the host batch keeps its own padding)
-    for (int64_t g = rs.g_lo + (int64_t)blockIdx.x * 4 + wid; g < g_end; g += (int64_t)gridDim.x * 4) {
-        int32_t *ids_o = out.input_ids + g * S;
-        int32_t *am_o = out.attention_mask + g * S;
-        int32_t *tt_o = out.token_type_ids ? out.token_type_ids + g * S : nullptr;
-        int32_t *lb_o = out.labels ? out.labels + g * (int64_t)P.label_width : nullptr;
-        if (g < (int64_t)dd.cap) {  // a small push's row: straight into its host batch
-            const uint32_t slot = dd.base + (uint32_t)g, bi = slot >= dd.B ? 1u : 0u, row = slot - bi * dd.B;
-            ids_o = dd.ids[bi] + (size_t)row * S;
-            am_o = dd.am[bi] + (size_t)row * S;
-            tt_o = dd.tt[bi] ? dd.tt[bi] + (size_t)row * S : nullptr;
-            lb_o = dd.lab[bi] ? dd.lab[bi] + (size_t)row * P.label_width : nullptr;
-        }
-        if (g >= (int64_t)G) {  // rows of the last batch nobody filled: initial values
-            if (RM1 && P.mask_pass == 2) continue;  // (written by pass 1)
-#pragma unroll
-            for (int m = 0; m < MR; ++m) {
-                const int j0 = 256 * m + 4 * lane;
-                store4(ids_o, j0, S, vec, 0, 0, 0, 0);
-                store4(am_o, j0, S, vec, 1, 1, 1, 1);
-                if (tt_o) store4(tt_o, j0, S, vec, 0, 0, 0, 0);
-                if (lb_o) store4(lb_o, j0, P.label_width, vec_lb, -100, -100, -100, -100);
-            }
-            continue;
-        }
-        const int64_t r = row_rec[g];
-        const uint32_t k = (uint32_t)(g - row_off[r]);
-        // (rng_mode 1, two passes: the chunk-0 rows while the later rows' masks are walked)
-        const int64_t pre = RM1 ? rand_pre_slot(P, r, k) : -1;
-        if (RM1 && P.mask_pass && ((pre >= 0) != (P.mask_pass == 1))) continue;
-        const uint32_t cnt = rec_cnt[r];
-        const uint32_t t0 = rec_tok[r];
-        const int64_t n = (int64_t)cnt + P.n_pre + P.n_post;
-        const int64_t base = P.chunk ? (int64_t)k * S : 0;
-        const int l = (int)((n - base) < S ? (n - base) : S);
-        // (rng_mode 1) the row's mask words (k_mask_bits_rec / k_mask_rand16): one dword a lane
-        uint32_t mwd[MR];
-        if (RM1) {
-            const uint32_t *bw = pre >= 0 ? P.mask_bits0 + pre * (int64_t)P.mask_w : P.mask_bitsg + g * (int64_t)P.mask_w;
-#pragma unroll
-            for (int m = 0; m < MR; ++m) {
-                const int j0 = 256 * m + 4 * lane;
-                mwd[m] = j0 < S ? bw[j0 >> 5] : 0u;
-            }
-        }
-
-        int32_t id[MR][4];
-#pragma unroll
-        for (int m = 0; m < MR; ++m)
-#pragma unroll
-            for (int w = 0; w < 4; ++w) {
-                const int j = 256 * m + 4 * lane + w;
-                int32_t v = 0;
-                if (j < l) {
-                    const int64_t f = base + j;
-                    if (f < P.n_pre) v = frame_id(P.pre, (int)f);
-                    else if (f < P.n_pre + (int64_t)cnt) v = (int32_t)tok[t0 + (f - P.n_pre)];
-                    else v = frame_id(P.post, (int)(f - P.n_pre - cnt));
-                }
-                id[m][w] = v;
-            }
-        // attention: 0 on [S-l, S) when l < S (reversed-range quirk, bert_data.rs:58-63 / gpt_data.rs:33-41)
-        const int tail0 = l < S ? S - l : S;
-        const uint64_t rec = P.first_record + (uint64_t)r;
-        if (P.task == 0) {  // MLM: BertData::mask_batch
-            bool sel[MR][4];
-            if (RM1) {  // rand-compatible mode: the row's bits from k_mask_rand
-#pragma unroll
-                for (int m = 0; m < MR; ++m) {
-                    const int j0 = 256 * m + 4 * lane;
-#pragma unroll
-                    for (int w = 0; w < 4; ++w) sel[m][w] = (mwd[m] >> ((j0 + w) & 31)) & 1u;
-                }
-            } else {
-                uint32_t key[MR][4];
-#pragma unroll
-                for (int m = 0; m < MR; ++m) {
-                    const uint4 c = philox4x32_10(make_uint4((uint32_t)(64 * m + lane), k, (uint32_t)rec,
-                                                             (uint32_t)(rec >> 32)),
-                                                  (uint32_t)P.seed, (uint32_t)(P.seed >> 32));
-                    const int j0 = 256 * m + 4 * lane;
-                    key[m][0] = j0 < S ? c.x : 0xFFFFFFFFu;
-                    key[m][1] = j0 + 1 < S ? c.y : 0xFFFFFFFFu;
-                    key[m][2] = j0 + 2 < S ? c.z : 0xFFFFFFFFu;
-                    key[m][3] = j0 + 3 < S ? c.w : 0xFFFFFFFFu;
-                }
-#if SDL_ROWS_INTERP_STEPS > 0
-                select_k_smallest_interp<MR>(key, P.mask_length, S < 256 * MR ? S : 256 * MR, sel);
-#else
-                select_k_smallest<MR>(key, P.mask_length, sel);
-#endif
-            }
-#pragma unroll
-            for (int m = 0; m < MR; ++m) {
-                const int j0 = 256 * m + 4 * lane;
-                int32_t v[4], lab[4], am[4];
-#pragma unroll
-                for (int w = 0; w < 4; ++w) {
-                    v[w] = id[m][w];
-                    lab[w] = -100;
-                    if (sel[m][w] && v[w] != 0) {
-                        lab[w] = v[w];
-                        v[w] = P.mask_id;
-                    }
-                    am[w] = j0 + w >= tail0 ? 0 : 1;
-                }
-                store4(ids_o, j0, S, vec, v[0], v[1], v[2], v[3]);
-                store4(am_o, j0, S, vec, am[0], am[1], am[2], am[3]);
-                if (tt_o) store4(tt_o, j0, S, vec, 0, 0, 0, 0);
-                store4(lb_o, j0, P.label_width, vec_lb, lab[0], lab[1], lab[2], lab[3]);
-            }
-        } else if (P.task == 3 || P.task == 4) {  // Multi/SingleClass: BertData::put_data rows; labels by k_*_labels
-#pragma unroll
-            for (int m = 0; m < MR; ++m) {
-                const int j0 = 256 * m + 4 * lane;
-                int32_t am[4];
-#pragma unroll
-                for (int w = 0; w < 4; ++w) am[w] = j0 + w >= tail0 ? 0 : 1;
-                store4(ids_o, j0, S, vec, id[m][0], id[m][1], id[m][2], id[m][3]);
-                store4(am_o, j0, S, vec, am[0], am[1], am[2], am[3]);
-                if (tt_o) store4(tt_o, j0, S, vec, 0, 0, 0, 0);
-            }
-        } else {  // CLM: GptData::put_data, labels = row as i32 (no shift)
-#pragma unroll
-            for (int m = 0; m < MR; ++m) {
-                const int j0 = 256 * m + 4 * lane;
-                int32_t am[4], lab[4];
-#pragma unroll
-                for (int w = 0; w < 4; ++w) {
-                    const bool tail = j0 + w >= tail0;
-                    am[w] = tail ? 0 : 1;
-                    lab[w] = tail ? -100 : id[m][w];
-                }
-                store4(ids_o, j0, S, vec, id[m][0], id[m][1], id[m][2], id[m][3]);
-                store4(am_o, j0, S, vec, am[0], am[1], am[2], am[3]);
-                if (tt_o) store4(tt_o, j0, S, vec, 0, 0, 0, 0);
-                store4(lb_o, j0, P.label_width, vec_lb, lab[0], lab[1], lab[2], lab[3]);
-            }
-        }
-    }
-}
-
-// ---------------------------------------------------------------------------
-// rand-compatible MLM masks (rng_mode 1, oracle/orc_batcher.c orc_rand_positions):
-// BertData::mask_batch's position_base.shuffle (bert_data.rs:40-43; rand 0.8.5
-// SliceRandom::shuffle -> gen_index -> UniformInt<u32>::sample_single_inclusive)
-// driven by StdRng::from_seed(seed | record | chunk) (rand_chacha 0.3.1 ChaCha12:
-// 64-bit block counter, stream 0, words in block order).
-// The draws are sequential: swap i = S-1 .. 1 takes words until one is
-// accepted, lo32(v * n) <= zone(n) = (n << lz(n)) - 1 with n = i + 1 -- rand's
-// "conservative" zone rejects up to half the words for n just above a power of
-// two, so about 30 % of a row's ~730 words are rejected and every row has
-// rejections.  Phase A runs each row's walk in one lane: the lane computes its
-// ChaCha12 blocks in registers, 16 words per block in an unrolled loop, and writes
-// each swap index j_i to the row's slice of `jbuf`; the walk stops after step k
-// (steps k-1 .. 1 only permute [0, k) among itself).  A row is keyed by (seed,
-// record, chunk) alone, so the chunk-0 row of every record (86 % of the bench's
-// rows) is walked by k_mask_rand_rec (64 records per wave) on a second stream beside
-// the tokenizer, and phase B (k_mask_bits_rec) turns them into mask bits there too;
-// the rows of chunk >= 1, known after the row map, are listed and walked 16 lanes
-// per row (k_mask_rand16).  k_rows<MR, true> reads the bits.  Phase B (rand_set_bits), a
-// wave per row: mask_batch only uses the SET of the first k shuffled
-// positions, and Fisher-Yates from the end never moves a value out of [0, k)
-// once steps i < k begin (j_i <= i), so the set is what [0, k) holds after steps
-// S-1 .. k.  The value at position p just before step p came from the latest
-// earlier swap into p -- step next(p) = min{i > p : j_i = p, j_i != i} -- so it
-// is val(next(p)), or p; [0, k) receives val(min{i >= k : j_i = x}) at each x.
-// next() is one LDS atomicMin per step; each x follows a chain of ~2 hops
-// (S=512, k=76).  Output: the row's mask bits.
-// ---------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
 #define CC_QR(a, b, c, d)                                                         \
     a += b; d ^= a; d = rotl32(d, 16); c += d; b ^= c; b = rotl32(b, 12);         \
@@ -848,71 +628,494 @@ __device__ __forceinline__ void chacha12_block(const uint32_t (&k)[8], uint32_t 
     o[12] = x12 + ctr; o[13] = x13; o[14] = x14; o[15] = x15;
 }
 
-// Phase A for one row per lane: the lane's row is (rec, chunk) when `active`; writes the swap
-// indices j_i, i = S-1 .. k, to jrow.  Every lane of the wave calls it (the block loop is
-// wave-uniform).
-__device__ __forceinline__ void rand_walk_lane(const RowParams &P, bool active, uint64_t rec, uint32_t chunk,
-                                               uint16_t *__restrict__ jrow) {
-    const int S = P.S, kmask = P.mask_length < S ? P.mask_length : S;
-    // only steps i >= k move values into or out of [0, k): the walk stops there
-    const int i0 = kmask > 1 ? kmask : 1;
-    int i = 0;
-    uint32_t key[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
-    if (active) {
-        key[0] = (uint32_t)P.seed;
-        key[1] = (uint32_t)(P.seed >> 32);
-        key[2] = (uint32_t)rec;
-        key[3] = (uint32_t)(rec >> 32);
-        key[4] = chunk;
-        i = S - 1;
+// A row's blocks differ only in the counter word x12, so of the first column round only the
+// quarter round through x12 changes from block to block: ChaRow holds the other three's results
+// (x13 = x14 = x15 = 0: the counter's high word and stream 0), computed once per row.
+struct ChaRow {
+    uint32_t k[8];
+    uint32_t c[12];  // (x1, x5, x9, x13), (x2, x6, x10, x14), (x3, x7, x11, x15) after round 1's column QRs
+};
+__device__ __forceinline__ void chacha_row_init(ChaRow &R, const uint32_t (&k)[8]) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) R.k[q] = k[q];
+    uint32_t x1 = 0x3320646eu, x5 = k[1], x9 = k[5], x13 = 0u;
+    uint32_t x2 = 0x79622d32u, x6 = k[2], x10 = k[6], x14 = 0u;
+    uint32_t x3 = 0x6b206574u, x7 = k[3], x11 = k[7], x15 = 0u;
+    CC_QR(x1, x5, x9, x13) CC_QR(x2, x6, x10, x14) CC_QR(x3, x7, x11, x15)
+    R.c[0] = x1; R.c[1] = x5; R.c[2] = x9; R.c[3] = x13;
+    R.c[4] = x2; R.c[5] = x6; R.c[6] = x10; R.c[7] = x14;
+    R.c[8] = x3; R.c[9] = x7; R.c[10] = x11; R.c[11] = x15;
+}
+// = chacha12_block(R.k, ctr, o)
+__device__ __forceinline__ void chacha12_block_row(const ChaRow &R, uint32_t ctr, uint32_t (&o)[16]) {
+    uint32_t x0 = 0x61707865u, x4 = R.k[0], x8 = R.k[4], x12 = ctr;
+    CC_QR(x0, x4, x8, x12)
+    uint32_t x1 = R.c[0], x5 = R.c[1], x9 = R.c[2], x13 = R.c[3];
+    uint32_t x2 = R.c[4], x6 = R.c[5], x10 = R.c[6], x14 = R.c[7];
+    uint32_t x3 = R.c[8], x7 = R.c[9], x11 = R.c[10], x15 = R.c[11];
+    CC_QR(x0, x5, x10, x15) CC_QR(x1, x6, x11, x12) CC_QR(x2, x7, x8, x13) CC_QR(x3, x4, x9, x14)
+#pragma unroll
+    for (int r = 1; r < 6; ++r) {
+        CC_QR(x0, x4, x8, x12) CC_QR(x1, x5, x9, x13) CC_QR(x2, x6, x10, x14) CC_QR(x3, x7, x11, x15)
+        CC_QR(x0, x5, x10, x15) CC_QR(x1, x6, x11, x12) CC_QR(x2, x7, x8, x13) CC_QR(x3, x4, x9, x14)
     }
+    const uint32_t (&k)[8] = R.k;
+    o[0] = x0 + 0x61707865u; o[1] = x1 + 0x3320646eu; o[2] = x2 + 0x79622d32u; o[3] = x3 + 0x6b206574u;
+    o[4] = x4 + k[0]; o[5] = x5 + k[1]; o[6] = x6 + k[2]; o[7] = x7 + k[3];
+    o[8] = x8 + k[4]; o[9] = x9 + k[5]; o[10] = x10 + k[6]; o[11] = x11 + k[7];
+    o[12] = x12 + ctr; o[13] = x13; o[14] = x14; o[15] = x15;
+}
+
+// rng_mode 1, rows that were not walked beside the tokenizer (rand_pre_slot < 0: chunk >= 1 past
+// the byte-length guess, or every row when nothing was): k_rows' LATE pass walks them in place, up
+// to 4 rows a wave, 16 lanes a row.  Per window of 16 ChaCha12 blocks the row's 16 lanes each
+// compute one block into LDS; lane 0 of the row walks the 256 words (rand_walk_lanes' acceptance
+// test) and puts each swap straight into next() (an LDS atomicMin, as rand_set_bits does from
+// stored indices; a rejected word or a self swap targets the dummy slot S); then the row's lanes
+// follow [0, k)'s chains into its mask bits.  The walk is one dependent chain per row (a word's
+// test needs the previous word's outcome: lo32(v * n) moves with n like a hash, so guessing n for
+// later words and iterating to a fixed point converged lane by lane and measured ~25 us a row);
+// these rows are few (~3 % of the bench's), so the chains' latency hides across the waves.
+// win: [4][256] words, nx: [4][S + 1], bt: [4][bw] (wave LDS); a lane's group's row is (rec, chunk)
+// when its group < nrows.
+__device__ __forceinline__ void rand_rows16(const RowParams &P, int nrows, uint64_t rec, uint32_t chunk,
+                                            uint32_t *__restrict__ win, uint32_t *__restrict__ nx,
+                                            uint32_t *__restrict__ bt, int bw, int lane) {
+    constexpr uint32_t NONE = 0xFFFFFFFFu;
+    const int grp = lane >> 4, gl = lane & 15;
+    const int S = P.S, kmask = P.mask_length < S ? P.mask_length : S;
+    const int i0 = kmask > 1 ? kmask : 1;
+    auto wave_sync = [] {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    };
+    const bool active = grp < nrows;
+    const uint32_t key[8] = {(uint32_t)P.seed, (uint32_t)(P.seed >> 32), (uint32_t)rec, (uint32_t)(rec >> 32), chunk,
+                             0u, 0u, 0u};
+    ChaRow cr;
+    chacha_row_init(cr, key);
+    (void)win;
+    uint32_t *gnx = nx + (S + 1) * grp, *gbt = bt + bw * grp;
+    for (int x = gl; x <= S; x += 16) gnx[x] = NONE;
+    for (int x = gl; x < bw; x += 16) gbt[x] = 0u;
+    int i = active ? S - 1 : 0;  // (the walk's state: lane 0 of the row's)
     uint32_t n = (uint32_t)i + 1u, zone = (n << __builtin_clz(n)) - 1u;
-    // (S % 8 == 0) indices are collected eight at a time -- positions 8b .. 8b + 7, the
-    // walk runs downwards -- in a 128-bit shift register and stored as one 16-B store:
-    // a lane's own row, so each per-index 2-B store would touch its own line
-    const bool vec = (S & 7) == 0;
-    uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
-    for (uint32_t blk = 0; __any(i >= i0); ++blk) {
+    for (uint32_t blk = 0;; blk += 16) {
+        // wave-uniform: stop when no row of the wave has steps left
+        const int irow = __builtin_amdgcn_update_dpp(0, i, 0x150, 0xF, 0xF, false);  // row_newbcast:0
+        if (!__any(irow >= i0)) break;
         uint32_t o[16];
-        chacha12_block(key, blk, o);
-        if (vec) {
-            // branch-free per word (selects, no exec-mask work on the one scalar unit per
-            // CU); only the store of a completed group of eight is predicated
+        chacha12_block_row(cr, blk + (uint32_t)gl, o);
+        // the row's 256 words in order -- block (lane) b's word q by row_newbcast:b, in registers:
+        // no LDS round trip on the chain.  Every lane runs the walk; lane 0's is the row's.
+        static_for<0, 16>([&](auto bc) {
+            constexpr int b = decltype(bc)::value;
 #pragma unroll
             for (int q = 0; q < 16; ++q) {
-                const uint64_t m = (uint64_t)o[q] * n;
+                const uint32_t x = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)o[q], 0x150 + b, 0xF, 0xF, false);
+                const uint64_t m = (uint64_t)x * n;
                 const bool acc = i >= i0 && (uint32_t)m <= zone;
-                const uint32_t v = (uint32_t)(m >> 32);
-                a3 = acc ? (a3 << 16) | (a2 >> 16) : a3;
-                a2 = acc ? (a2 << 16) | (a1 >> 16) : a2;
-                a1 = acc ? (a1 << 16) | (a0 >> 16) : a1;
-                a0 = acc ? (a0 << 16) | v : a0;
-                if (acc && (i & 7) == 0)  // positions i .. i + 7 are complete
-                    *reinterpret_cast<uint4 *>(jrow + i) = make_uint4(a0, a1, a2, a3);
+                const uint32_t j = (uint32_t)(m >> 32);
+                if (gl == 0) atomicMin(&gnx[acc && j != (uint32_t)i ? j : (uint32_t)S], (uint32_t)i);
                 i -= acc ? 1 : 0;
                 n = (uint32_t)i + 1u;
                 zone = (n << __builtin_clz(n)) - 1u;
             }
-        } else {
+        });
+    }
+    wave_sync();
+    if (active)
+        for (int x = gl; x < kmask; x += 16) {
+            uint32_t p = (uint32_t)x;
+            for (uint32_t q = gnx[p]; q != NONE; q = gnx[p]) p = q;
+            atomicOr(&gbt[p >> 5], 1u << (p & 31));
+        }
+    wave_sync();
+}
+
+// One row g of the call (a wave): BertData::put_data (+ mask_batch) / GptData::put_data framing and
+// planes; g >= G: a padding row of the last batch.  late_bits: the row's mask words (LATE).
+template <int MR, bool RM1, bool LATE>
+__device__ __forceinline__ void row_one(const RowParams &P, const uint32_t *__restrict__ tok,
+                                        const uint32_t *__restrict__ rec_tok, const uint32_t *__restrict__ rec_cnt,
+                                        const uint32_t *__restrict__ row_off, const uint32_t *__restrict__ row_rec,
+                                        int64_t g, int64_t G, const RowOut &out, const uint32_t *late_bits,
+                                        int lane) {
+    const int S = P.S;
+    const bool vec = (S & 3) == 0;  // 16-byte aligned rows
+    const bool vec_lb = (P.label_width & 3) == 0;
+    const DirectDst &dd = out.direct;
+    int32_t *ids_o = out.input_ids + g * S;
+    int32_t *am_o = out.attention_mask + g * S;
+    int32_t *tt_o = out.token_type_ids ? out.token_type_ids + g * S : nullptr;
+    int32_t *lb_o = out.labels ? out.labels + g * (int64_t)P.label_width : nullptr;
+    if (g < (int64_t)dd.cap) {  // a small push's row: straight into its host batch
+        const uint32_t slot = dd.base + (uint32_t)g, bi = slot >= dd.B ? 1u : 0u, row = slot - bi * dd.B;
+        ids_o = dd.ids[bi] + (size_t)row * S;
+        am_o = dd.am[bi] + (size_t)row * S;
+        tt_o = dd.tt[bi] ? dd.tt[bi] + (size_t)row * S : nullptr;
+        lb_o = dd.lab[bi] ? dd.lab[bi] + (size_t)row * P.label_width : nullptr;
+    }
+    if (g >= (int64_t)G) {  // rows of the last batch nobody filled: initial values
 #pragma unroll
-            for (int q = 0; q < 16; ++q) {
-                const uint64_t m = (uint64_t)o[q] * n;
-                if (i >= i0 && (uint32_t)m <= zone) {
-                    jrow[i] = (uint16_t)(m >> 32);
-                    --i;
-                    n = (uint32_t)i + 1u;
-                    zone = (n << __builtin_clz(n)) - 1u;
+        for (int m = 0; m < MR; ++m) {
+            const int j0 = 256 * m + 4 * lane;
+            store4(ids_o, j0, S, vec, 0, 0, 0, 0);
+            store4(am_o, j0, S, vec, 1, 1, 1, 1);
+            if (tt_o) store4(tt_o, j0, S, vec, 0, 0, 0, 0);
+            if (lb_o) store4(lb_o, j0, P.label_width, vec_lb, -100, -100, -100, -100);
+        }
+        return;
+    }
+    const int64_t r = row_rec[g];
+    const uint32_t k = (uint32_t)(g - row_off[r]);
+    const uint32_t cnt = rec_cnt[r];
+    const uint32_t t0 = rec_tok[r];
+    const int64_t n = (int64_t)cnt + P.n_pre + P.n_post;
+    const int64_t base = P.chunk ? (int64_t)k * S : 0;
+    const int l = (int)((n - base) < S ? (n - base) : S);
+    // (rng_mode 1) the row's mask words, one dword a lane: walked beside the tokenizer
+    // (k_mask_bits_rec), else by the LATE pass (late_bits, LDS).  A row the first pass leaves to
+    // the LATE one returns only after its loads are issued: the mask words' load, a dependent
+    // step after row_rec / row_off, then overlaps the ids' (wave-uniform: a wave per row).
+    uint32_t mwd[MR];
+    bool mine = true;
+    if (RM1) {
+        const int64_t pre = rand_pre_slot(P, r, k);
+        mine = LATE || pre >= 0;
+        const uint32_t *bw = LATE ? late_bits : P.mask_bits0 + (pre >= 0 ? pre : 0) * (int64_t)P.mask_w;
+#pragma unroll
+        for (int m = 0; m < MR; ++m) {
+            const int j0 = 256 * m + 4 * lane;
+            mwd[m] = j0 < S && mine ? bw[j0 >> 5] : 0u;
+        }
+        if (LATE) __builtin_amdgcn_wave_barrier();  // (the LDS bits are rewritten by the wave's next rows)
+    }
+
+    int32_t id[MR][4];
+#pragma unroll
+    for (int m = 0; m < MR; ++m)
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            const int j = 256 * m + 4 * lane + w;
+            int32_t v = 0;
+            if (j < l) {
+                const int64_t f = base + j;
+                if (f < P.n_pre) v = frame_id(P.pre, (int)f);
+                else if (f < P.n_pre + (int64_t)cnt) v = (int32_t)tok[t0 + (f - P.n_pre)];
+                else v = frame_id(P.post, (int)(f - P.n_pre - cnt));
+            }
+            id[m][w] = v;
+        }
+    if (RM1 && !mine) return;  // (the LATE pass's row)
+    // attention: 0 on [S-l, S) when l < S (reversed-range quirk, bert_data.rs:58-63 / gpt_data.rs:33-41)
+    const int tail0 = l < S ? S - l : S;
+    const uint64_t rec = P.first_record + (uint64_t)r;
+    if (P.task == 0) {  // MLM: BertData::mask_batch
+        bool sel[MR][4];
+        if (RM1) {  // rand-compatible mode: the row's bits from k_mask_rand
+#pragma unroll
+            for (int m = 0; m < MR; ++m) {
+                const int j0 = 256 * m + 4 * lane;
+#pragma unroll
+                for (int w = 0; w < 4; ++w) sel[m][w] = (mwd[m] >> ((j0 + w) & 31)) & 1u;
+            }
+        } else {
+            uint32_t key[MR][4];
+#pragma unroll
+            for (int m = 0; m < MR; ++m) {
+                const uint4 c = philox4x32_10(make_uint4((uint32_t)(64 * m + lane), k, (uint32_t)rec,
+                                                         (uint32_t)(rec >> 32)),
+                                              (uint32_t)P.seed, (uint32_t)(P.seed >> 32));
+                const int j0 = 256 * m + 4 * lane;
+                key[m][0] = j0 < S ? c.x : 0xFFFFFFFFu;
+                key[m][1] = j0 + 1 < S ? c.y : 0xFFFFFFFFu;
+                key[m][2] = j0 + 2 < S ? c.z : 0xFFFFFFFFu;
+                key[m][3] = j0 + 3 < S ? c.w : 0xFFFFFFFFu;
+            }
+#if SDL_ROWS_INTERP_STEPS > 0
+            select_k_smallest_interp<MR>(key, P.mask_length, S < 256 * MR ? S : 256 * MR, sel);
+#else
+            select_k_smallest<MR>(key, P.mask_length, sel);
+#endif
+        }
+#pragma unroll
+        for (int m = 0; m < MR; ++m) {
+            const int j0 = 256 * m + 4 * lane;
+            int32_t v[4], lab[4], am[4];
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                v[w] = id[m][w];
+                lab[w] = -100;
+                if (sel[m][w] && v[w] != 0) {
+                    lab[w] = v[w];
+                    v[w] = P.mask_id;
                 }
+                am[w] = j0 + w >= tail0 ? 0 : 1;
+            }
+            store4(ids_o, j0, S, vec, v[0], v[1], v[2], v[3]);
+            store4(am_o, j0, S, vec, am[0], am[1], am[2], am[3]);
+            if (tt_o) store4(tt_o, j0, S, vec, 0, 0, 0, 0);
+            store4(lb_o, j0, P.label_width, vec_lb, lab[0], lab[1], lab[2], lab[3]);
+        }
+    } else if (P.task == 3 || P.task == 4) {  // Multi/SingleClass: BertData::put_data rows; labels by k_*_labels
+#pragma unroll
+        for (int m = 0; m < MR; ++m) {
+            const int j0 = 256 * m + 4 * lane;
+            int32_t am[4];
+#pragma unroll
+            for (int w = 0; w < 4; ++w) am[w] = j0 + w >= tail0 ? 0 : 1;
+            store4(ids_o, j0, S, vec, id[m][0], id[m][1], id[m][2], id[m][3]);
+            store4(am_o, j0, S, vec, am[0], am[1], am[2], am[3]);
+            if (tt_o) store4(tt_o, j0, S, vec, 0, 0, 0, 0);
+        }
+    } else {  // CLM: GptData::put_data, labels = row as i32 (no shift)
+#pragma unroll
+        for (int m = 0; m < MR; ++m) {
+            const int j0 = 256 * m + 4 * lane;
+            int32_t am[4], lab[4];
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                const bool tail = j0 + w >= tail0;
+                am[w] = tail ? 0 : 1;
+                lab[w] = tail ? -100 : id[m][w];
+            }
+            store4(ids_o, j0, S, vec, id[m][0], id[m][1], id[m][2], id[m][3]);
+            store4(am_o, j0, S, vec, am[0], am[1], am[2], am[3]);
+            if (tt_o) store4(tt_o, j0, S, vec, 0, 0, 0, 0);
+            store4(lb_o, j0, P.label_width, vec_lb, lab[0], lab[1], lab[2], lab[3]);
+        }
+    }
+}
+
+// RM1: MLM under rng_mode 1 (the rows' mask words from k_mask_bits_rec, or walked here).  A template flag, not
+// a runtime branch: the mask-word registers would cost the Philox path a wave
+// per SIMD (k_rows<2>: 80 -> 82 VGPRs, 6 -> 5 waves, 0.267 -> 0.295 ms).
+// LATE (RM1 only): the second pass over the rows the first one left (no mask bits from beside the
+// tokenizer): its waves walk their masks in place, 4 rows at a time (rand_rows16).
+template <int MR, bool RM1, bool LATE = false>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MR >= 4 ? SDL_ROWS_WAVES4 : LATE ? 4 : RM1 ? SDL_ROWS_WAVES_RM1 : SDL_ROWS_WAVES, 8))) void k_rows(RowParams P, const uint32_t *__restrict__ tok,
+                                              const uint32_t *__restrict__ rec_tok, const uint32_t *__restrict__ rec_cnt,
+                                              const uint32_t *__restrict__ row_off, const uint32_t *__restrict__ row_rec,
+                                              SegSel sel, int64_t rows_cap, RowOut out) {
+    const int lane = lane_id();
+    const int wid = (int)(threadIdx.x >> 6);
+    // (LATE: a wave's LDS for rand_rows16 -- 4 windows, 4 next() arrays + dummy slots, 4 rows' bits)
+    constexpr int NXS = 256 * MR + 1, BW = 8 * MR;
+    __shared__ __attribute__((aligned(16))) uint32_t s_rw[LATE ? 4 : 1][LATE ? 4 * (256 + NXS + BW) : 1];
+    const RowSpan rs = row_span(sel, row_off, P.B, rows_cap);
+    const int64_t G = rs.g_real;
+    const DirectDst &dd = out.direct;
+    const int64_t g_end = dd.cap ? rs.g_real : rs.g_end;  // (direct: the host batch keeps its own padding)
+    if constexpr (LATE) {  // 64 rows a wave: the rows the first pass left, found by a ballot
+        for (int64_t g0 = rs.g_lo + ((int64_t)blockIdx.x * 4 + wid) * 64; g0 < G; g0 += (int64_t)gridDim.x * 256) {
+            const int64_t gl = g0 + lane;
+            bool late = false;
+            if (gl < G) {
+                const int64_t r = row_rec[gl];
+                late = rand_pre_slot(P, r, (uint32_t)(gl - row_off[r])) < 0;
+            }
+            uint32_t *const rw = s_rw[LATE ? wid : 0];
+            uint32_t *const bits = rw + 4 * (256 + NXS);
+            for (uint64_t m = __ballot(late); m;) {
+                // up to 4 of them: group q of 16 lanes walks the q-th
+                const int nr = __popcll(m) < 4 ? __popcll(m) : 4;
+                uint64_t mm = m;
+                for (int q = 0; q < (lane >> 4) && mm; ++q) mm &= mm - 1;
+                const int64_t gq = g0 + (mm ? __builtin_ctzll(mm) : 0);
+                uint64_t rec = 0;
+                uint32_t kq = 0;
+                if ((lane >> 4) < nr) {
+                    const int64_t r = row_rec[gq];
+                    rec = P.first_record + (uint64_t)r;
+                    kq = (uint32_t)(gq - row_off[r]);
+                }
+                rand_rows16(P, nr, rec, kq, rw, rw + 4 * 256, bits, BW, lane);
+                for (int q = 0; q < nr; ++q, m &= m - 1)
+                    row_one<MR, RM1, LATE>(P, tok, rec_tok, rec_cnt, row_off, row_rec, g0 + __builtin_ctzll(m), G, out,
+                                           bits + BW * q, lane);
+                __builtin_amdgcn_wave_barrier();  // (the LDS is rewritten by the next rows)
             }
         }
+    } else {
+        for (int64_t g = rs.g_lo + (int64_t)blockIdx.x * 4 + wid; g < g_end; g += (int64_t)gridDim.x * 4)
+            row_one<MR, RM1, LATE>(P, tok, rec_tok, rec_cnt, row_off, row_rec, g, G, out, nullptr, lane);
     }
-    if (vec && active && (i0 & 7) != 0) {  // the partial block [i0, (i0 | 7)]
-        const uint32_t w[4] = {a0, a1, a2, a3};
-        for (int p = i0; p <= (i0 | 7); ++p) {  // position p is the (p - i0)-th newest value
-            const int d = p - i0;
-            jrow[p] = (uint16_t)(w[d >> 1] >> (16 * (d & 1)));
+}
+
+template <int MR>  // 0: no rows; else the call's rows too (d.rows: Philox mlm / clm)
+__global__ __launch_bounds__(SCAN_SMALL_NT) void k_downstream_small(SmallDown d, RowParams P,
+                                                                    const uint64_t *__restrict__ off, int64_t R,
+                                                                    int64_t N, int64_t n_chunks) {
+    __shared__ uint32_t scratch[SCAN_SMALL_NT / 64];
+    block_scan_small(d.chunk_cnt, n_chunks, d.chunk_off, scratch);
+    __syncthreads();
+    for (int64_t cb = (int64_t)(threadIdx.x >> 6) * COMPACT_CPW; cb < n_chunks;
+         cb += (int64_t)(SCAN_SMALL_NT / 64) * COMPACT_CPW)
+        compact_wave(cb, d.tokc, d.chunk_cnt, d.chunk_off, n_chunks, d.tok, d.long_count, d.chunk_ent, d.long_list,
+                     d.long_scratch, d.long_pool, d.stride);
+    for (int64_t r = threadIdx.x; r < R; r += SCAN_SMALL_NT)
+        record_one(P, off, r, N, d.chunk_off, n_chunks, d.rec_local, d.rec_tok, d.rec_cnt, d.rec_rows);
+    __syncthreads();
+    block_scan_small(d.rec_rows, R, d.row_off, scratch);
+    __syncthreads();
+    for (int64_t r = threadIdx.x; r < R; r += SCAN_SMALL_NT)
+        for (uint32_t g = d.row_off[r]; g < d.row_off[r + 1]; ++g) d.row_rec[g] = (uint32_t)r;
+    if (d.stat) {
+        for (int64_t r = threadIdx.x; r <= R; r += SCAN_SMALL_NT) d.stat[r] = d.row_off[r];
+        if (threadIdx.x == 0) {
+            d.stat[R + 1] = 0u;
+            d.stat[R + 2] = d.tok_err ? *d.tok_err : 0u;  // a t5 tokenizer under mlm / clm
         }
     }
+    if constexpr (MR > 0) {  // the rows, a wave each (k_rows' body), without a launch of their own
+        __syncthreads();  // (this workgroup's row_off / row_rec / rec_* / ids are visible)
+        const int64_t G = (int64_t)d.row_off[R];
+        const int64_t g_end = d.out.direct.cap ? G : (G + P.B - 1) / P.B * P.B;
+        for (int64_t g = (int64_t)(threadIdx.x >> 6); g < g_end; g += SCAN_SMALL_NT / 64)
+            row_one<MR, false, false>(P, d.tok, d.rec_tok, d.rec_cnt, d.row_off, d.row_rec, g, G, d.out, nullptr,
+                                      lane_id());
+    }
+}
+
+hipError_t launch_downstream_small(const SmallDown &d, const RowParams &P, const uint64_t *off, int64_t R, int64_t N,
+                                   hipStream_t st) {
+    const int64_t n_chunks = (N + CHUNK - 1) / CHUNK;
+    if (n_chunks > SMALL_CHUNKS || R > SCAN_SMALL) return hipErrorInvalidValue;
+    const int MR = (P.S + 255) / 256;
+    if (d.rows && ((P.rng_mode == 1 && P.task == 0) || (P.task != 0 && P.task != 1)))
+        return hipErrorInvalidValue;  // (rng_mode 1 masks need k_rows' passes; span has its own rows)
+#define SDL_DS(M) hipLaunchKernelGGL(k_downstream_small<M>, dim3(1), dim3(SCAN_SMALL_NT), 0, st, d, P, off, R, N, n_chunks)
+    if (!d.rows) SDL_DS(0);
+    else if (MR <= 1) SDL_DS(1);
+    else if (MR <= 2) SDL_DS(2);
+    else if (MR <= 4) SDL_DS(4);
+    else if (MR <= 8) SDL_DS(8);
+    else return hipErrorInvalidValue;
+#undef SDL_DS
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// rand-compatible MLM masks (rng_mode 1, oracle/orc_batcher.c orc_rand_positions):
+// BertData::mask_batch's position_base.shuffle (bert_data.rs:40-43; rand 0.8.5
+// SliceRandom::shuffle -> gen_index -> UniformInt<u32>::sample_single_inclusive)
+// driven by StdRng::from_seed(seed | record | chunk) (rand_chacha 0.3.1 ChaCha12:
+// 64-bit block counter, stream 0, words in block order).
+// The draws are sequential: swap i = S-1 .. 1 takes words until one is
+// accepted, lo32(v * n) <= zone(n) = (n << lz(n)) - 1 with n = i + 1 -- rand's
+// "conservative" zone rejects up to half the words for n just above a power of
+// two, so about 30 % of a row's ~730 words are rejected and every row has
+// rejections.  Phase A runs each row's walk in one lane: the lane computes its
+// ChaCha12 blocks in registers, 16 words per block in an unrolled loop, and writes
+// each swap index j_i to the row's slice of `jbuf`; the walk stops after step k
+// (steps k-1 .. 1 only permute [0, k) among itself).  A row is keyed by (seed,
+// record, chunk) alone, so the chunk-0 row of every record (86 % of the bench's
+// rows) is walked by k_mask_rand_rec (64 records per wave) on a second stream beside
+// the tokenizer, and phase B (k_mask_bits_rec) turns them into mask bits there too;
+// k_rows<MR, true> reads the bits, and walks the few rows left (chunk >= 1 past the
+// byte-length guess) in a second pass (rand_rows16).  Phase B (rand_set_bits), a
+// wave per row: mask_batch only uses the SET of the first k shuffled
+// positions, and Fisher-Yates from the end never moves a value out of [0, k)
+// once steps i < k begin (j_i <= i), so the set is what [0, k) holds after steps
+// S-1 .. k.  The value at position p just before step p came from the latest
+// earlier swap into p -- step next(p) = min{i > p : j_i = p, j_i != i} -- so it
+// is val(next(p)), or p; [0, k) receives val(min{i >= k : j_i = x}) at each x.
+// next() is one LDS atomicMin per step; each x follows a chain of ~2 hops
+// (S=512, k=76).  Output: the row's mask bits.
+// ---------------------------------------------------------------------------
+// Phase A, NR rows per lane: row r of the lane is (rec[r], chunk[r]) when active[r]; writes its
+// swap indices j_i, i = S-1 .. k, to jrow[r].  Every lane of the wave calls it (the block loop is
+// wave-uniform).  The rows' ChaCha12 rounds and acceptance chains are independent, so NR > 1
+// gives the scheduler NR-fold ILP: a lane's walk is a chain of dependent 64-bit multiplies and
+// selects, and one row per lane leaves the SIMD waiting on it.
+template <int NR>
+__device__ __forceinline__ void rand_walk_lanes(const RowParams &P, const bool (&active)[NR], const uint64_t (&rec)[NR],
+                                                const uint32_t (&chunk)[NR], uint16_t *const (&jrow)[NR]) {
+    const int S = P.S, kmask = P.mask_length < S ? P.mask_length : S;
+    // only steps i >= k move values into or out of [0, k): the walk stops there
+    const int i0 = kmask > 1 ? kmask : 1;
+    int i[NR];
+    uint32_t n[NR], zone[NR];
+    ChaRow cr[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        uint32_t key[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+        i[r] = 0;
+        if (active[r]) {
+            key[0] = (uint32_t)P.seed;
+            key[1] = (uint32_t)(P.seed >> 32);
+            key[2] = (uint32_t)rec[r];
+            key[3] = (uint32_t)(rec[r] >> 32);
+            key[4] = chunk[r];
+            i[r] = S - 1;
+        }
+        chacha_row_init(cr[r], key);
+        n[r] = (uint32_t)i[r] + 1u;
+        zone[r] = (n[r] << __builtin_clz(n[r])) - 1u;
+    }
+    // (S % 8 == 0) indices are collected eight at a time -- positions 8b .. 8b + 7, the
+    // walk runs downwards -- in a 128-bit shift register and stored as one 16-B store:
+    // a lane's own row, so each per-index 2-B store would touch its own line
+    const bool vec = (S & 7) == 0;
+    uint32_t a0[NR], a1[NR], a2[NR], a3[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) a0[r] = a1[r] = a2[r] = a3[r] = 0u;
+    auto live = [&] {
+        bool x = false;
+#pragma unroll
+        for (int r = 0; r < NR; ++r) x |= i[r] >= i0;
+        return x;
+    };
+    for (uint32_t blk = 0; __any(live()); ++blk) {
+        uint32_t o[NR][16];
+#pragma unroll
+        for (int r = 0; r < NR; ++r) chacha12_block_row(cr[r], blk, o[r]);
+        if (vec) {
+            // branch-free per word (selects, no exec-mask work on the one scalar unit per
+            // CU); only the store of a completed group of eight is predicated
+#pragma unroll
+            for (int q = 0; q < 16; ++q)
+#pragma unroll
+                for (int r = 0; r < NR; ++r) {
+                    const uint64_t m = (uint64_t)o[r][q] * n[r];
+                    const bool acc = i[r] >= i0 && (uint32_t)m <= zone[r];
+                    const uint32_t v = (uint32_t)(m >> 32);
+                    a3[r] = acc ? (a3[r] << 16) | (a2[r] >> 16) : a3[r];
+                    a2[r] = acc ? (a2[r] << 16) | (a1[r] >> 16) : a2[r];
+                    a1[r] = acc ? (a1[r] << 16) | (a0[r] >> 16) : a1[r];
+                    a0[r] = acc ? (a0[r] << 16) | v : a0[r];
+                    if (acc && (i[r] & 7) == 0)  // positions i .. i + 7 are complete
+                        *reinterpret_cast<uint4 *>(jrow[r] + i[r]) = make_uint4(a0[r], a1[r], a2[r], a3[r]);
+                    i[r] -= acc ? 1 : 0;
+                    n[r] = (uint32_t)i[r] + 1u;
+                    zone[r] = (n[r] << __builtin_clz(n[r])) - 1u;
+                }
+        } else {
+#pragma unroll
+            for (int q = 0; q < 16; ++q)
+#pragma unroll
+                for (int r = 0; r < NR; ++r) {
+                    const uint64_t m = (uint64_t)o[r][q] * n[r];
+                    if (i[r] >= i0 && (uint32_t)m <= zone[r]) {
+                        jrow[r][i[r]] = (uint16_t)(m >> 32);
+                        --i[r];
+                        n[r] = (uint32_t)i[r] + 1u;
+                        zone[r] = (n[r] << __builtin_clz(n[r])) - 1u;
+                    }
+                }
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < NR; ++r)
+        if (vec && active[r] && (i0 & 7) != 0) {  // the partial block [i0, (i0 | 7)]
+            const uint32_t w[4] = {a0[r], a1[r], a2[r], a3[r]};
+            for (int p = i0; p <= (i0 | 7); ++p) {  // position p is the (p - i0)-th newest value
+                const int d = p - i0;
+                jrow[r][p] = (uint16_t)(w[d >> 1] >> (16 * (d & 1)));
+            }
+        }
 }
 
 // Phase B for one row, one wave: jr = the row's swap indices -> its mask bits in bt
@@ -952,198 +1155,100 @@ __device__ __forceinline__ void rand_set_bits(const RowParams &P, const uint16_t
     wave_sync();
 }
 
-// Chunk-0 rows, one lane per record, 64 records per wave: the same walk (rand_walk_lane) keyed
+// Chunk-0 rows, RAND_NR records per lane, 64 RAND_NR per wave: the walk (rand_walk_lanes) keyed
 // by (first_record + r, chunk 0) -- which needs nothing the tokenizer computes, so the host runs
 // it on a second stream beside the tokenizer (sdl_batcher.cpp run_device): its ChaCha12 work
 // fills VALU slots the latency-bound tokenizer leaves idle instead of sitting on the step's
 // critical path.  (86 % of the bench's rows are chunk 0.)
-// (slot s < R: record s, chunk 0; s = R + r: record r, chunk 1 when rand_pre_slot says so)
-__device__ __forceinline__ bool rand_pre_active(const RowParams &P, int64_t s) {
-    return s < P.mask_R || (s < 2 * P.mask_R && rand_pre_slot(P, s - P.mask_R, 1u) == s);
-}
-__global__ __launch_bounds__(64) void k_mask_rand_rec(RowParams P, uint16_t *__restrict__ jbuf) {
+// (slot s < R: record s, chunk 0; s = R + r: record r, chunk 1 when rand_pre_slot says so.)  The
+// walk runs over t in [0, R + n_spec): t < R is slot t, the rest the slots k_rand_spec_list
+// collected -- a wave holding any chunk-1 slot costs a whole walk, and ~1 record in 5 has one.
+__global__ __launch_bounds__(256) void k_rand_spec_list(RowParams P, uint32_t *__restrict__ list) {
     const int lane = lane_id();
-    const int64_t R = P.mask_R, ns = P.mask_spec1 > 0 ? 2 * R : R;
-    for (int64_t s0 = (int64_t)blockIdx.x * 64; s0 < ns; s0 += (int64_t)gridDim.x * 64) {
-        const int64_t s = s0 + lane;
-        const bool active = s < ns && rand_pre_active(P, s);
-        const int64_t r = active ? (s < R ? s : s - R) : 0;
-        rand_walk_lane(P, active, P.first_record + (uint64_t)r, s < R ? 0u : 1u, jbuf + (active ? s : 0) * (int64_t)P.S);
-    }
-}
-
-// Phase B for those rows: a wave per record, its mask bits -> bits[r]
-template <int MR4>
-__global__ __launch_bounds__(256) void k_mask_bits_rec(RowParams P, const uint16_t *__restrict__ jbuf,
-                                                       uint32_t *__restrict__ bits) {
-    __shared__ uint32_t s_nx[4][64 * MR4];
-    __shared__ uint32_t s_bt[4][2 * MR4];
-    const int lane = lane_id(), wid = (int)(threadIdx.x >> 6);
-    const int64_t ns = P.mask_spec1 > 0 ? 2 * P.mask_R : P.mask_R;
-    for (int64_t s = (int64_t)blockIdx.x * 4 + wid; s < ns; s += (int64_t)gridDim.x * 4) {
-        if (!rand_pre_active(P, s)) continue;  // (wave-uniform)
-        rand_set_bits<MR4>(P, jbuf + s * (int64_t)P.S, s_nx[wid], s_bt[wid], lane);
-        for (int w = lane; w < P.mask_w; w += 64) bits[s * (int64_t)P.mask_w + w] = s_bt[wid][w];
-        __builtin_amdgcn_wave_barrier();  // (s_bt is rewritten by the wave's next record)
-    }
-}
-
-hipError_t launch_mask_rand_rec(const RowParams &P, uint16_t *jbuf, uint32_t *bits, hipStream_t st) {
-    const int64_t R = P.mask_R, ns = P.mask_spec1 > 0 ? 2 * R : R;
-    if (R <= 0) return hipSuccess;
-    if (P.S > RAND_MAX_S || P.mask_w * 32 < P.S || !P.mask_off) return hipErrorInvalidValue;
-    const int64_t want = (ns + 63) / 64;
-    hipLaunchKernelGGL(k_mask_rand_rec, dim3((unsigned)(want < 8192 ? want : 8192)), dim3(64), 0, st, P, jbuf);
-    const int64_t wb = (ns + 3) / 4;
-    const dim3 g((unsigned)(wb < 16384 ? wb : 16384));
-    const int MR4 = (P.S + 63) / 64;
-#define SDL_BITS(M) hipLaunchKernelGGL(k_mask_bits_rec<M>, g, dim3(256), 0, st, P, (const uint16_t *)jbuf, bits)
-    if (MR4 <= 2) SDL_BITS(2);
-    else if (MR4 <= 4) SDL_BITS(4);
-    else if (MR4 <= 8) SDL_BITS(8);
-    else if (MR4 <= 16) SDL_BITS(16);
-    else SDL_BITS(32);
-#undef SDL_BITS
-    return hipGetLastError();
-}
-
-// The rows of the segment with chunk k >= kmin (k_rand_list), then 16 lanes per row, 4 rows per
-// wave (k_mask_rand16): so few rows that one lane per row would leave the launch as long as one
-// row's whole ChaCha12 chain.  Per window of 16 blocks the row's 16 lanes each compute one block
-// into LDS; lane 0 of the row walks the 256 words (rand's acceptance test, the same sequence as
-// rand_walk_lane) and puts each swap straight into next() (an LDS atomicMin, as rand_set_bits
-// does from the stored indices); the row's lanes then follow the chains and write its bits.
-__global__ __launch_bounds__(256) void k_rand_list(RowParams P, const uint32_t *__restrict__ row_off,
-                                                   const uint32_t *__restrict__ row_rec, SegSel sel, int64_t rows_cap,
-                                                   uint32_t *__restrict__ list) {
-    const RowSpan rs = row_span(sel, row_off, P.B, rows_cap);
-    const int lane = lane_id();
-    // (wave-uniform trip count; one atomic per wave: a counter hit by every row serialized the launch)
-    for (int64_t g0 = rs.g_lo + (int64_t)blockIdx.x * 256 + (threadIdx.x & ~63u); g0 < rs.g_real;
-         g0 += (int64_t)gridDim.x * 256) {
-        const int64_t g = g0 + lane;
-        bool take = false;
-        if (g < rs.g_real) {
-            const uint32_t r = row_rec[g];
-            take = rand_pre_slot(P, r, (uint32_t)(g - row_off[r])) < 0;
-        }
+    const int64_t R = P.mask_R;
+    for (int64_t r0 = (int64_t)blockIdx.x * 256 + (threadIdx.x & ~63u); r0 < R; r0 += (int64_t)gridDim.x * 256) {
+        const int64_t r = r0 + lane;
+        const bool take = r < R && rand_pre_slot(P, r, 1u) >= 0;
         const uint64_t m = __ballot(take);
         if (!m) continue;
         const int leader = __builtin_ctzll(m);
         uint32_t base = 0;
         if (lane == leader) base = atomicAdd(&list[0], (uint32_t)__popcll(m));
         base = (uint32_t)lane_bcast((int)base, leader);
-        if (take) list[1 + base + __popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)g;
+        if (take) list[1 + base + __popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)(R + r);
     }
 }
-
-template <int MR4>
-__global__ __launch_bounds__(64) void k_mask_rand16(RowParams P, const uint32_t *__restrict__ row_off,
-                                                    const uint32_t *__restrict__ row_rec,
-                                                    const uint32_t *__restrict__ list, uint32_t *__restrict__ bitsg) {
-    constexpr uint32_t NONE = 0xFFFFFFFFu;
-    __shared__ __attribute__((aligned(16))) uint32_t s_win[4][256];  // a row's window of 16 ChaCha12 blocks
-    __shared__ uint32_t s_nx[4][64 * MR4 + 1];  // (+ the DUMMY slot)
-    __shared__ uint32_t s_bt[4][2 * MR4];
-    const int lane = lane_id(), grp = lane >> 4, gl = lane & 15;
-    const int S = P.S, kmask = P.mask_length < S ? P.mask_length : S;
-    const int i0 = kmask > 1 ? kmask : 1;
-    auto wave_sync = [] {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    };
-    const uint32_t count = list[0];
-    // (the loop is wave-uniform; a row slot past the list runs with no row: its chain is empty)
-    for (uint32_t q0 = blockIdx.x * 4; q0 < count; q0 += gridDim.x * 4) {
-        const uint32_t q = q0 + (uint32_t)grp;
-        const bool active = q < count;
-        int64_t g = 0;
-        uint32_t key[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
-        if (active) {
-            g = list[1 + q];
-            const uint32_t r = row_rec[g];
-            const uint64_t rec = P.first_record + (uint64_t)r;
-            key[0] = (uint32_t)P.seed;
-            key[1] = (uint32_t)(P.seed >> 32);
-            key[2] = (uint32_t)rec;
-            key[3] = (uint32_t)(rec >> 32);
-            key[4] = (uint32_t)(g - row_off[r]);
-        }
-        for (int x = gl; x < 64 * MR4; x += 16) s_nx[grp][x] = NONE;
-        for (int x = gl; x < 2 * MR4; x += 16) s_bt[grp][x] = 0u;  // (S > 512: more words than lanes)
-        // the walk's state lives in lane 0 of the row
-        int i = active ? S - 1 : 0;
-        uint32_t n = (uint32_t)i + 1u, zone = (n << __builtin_clz(n)) - 1u;
-        constexpr uint32_t DUMMY = 64 * MR4;  // a swap that moves nothing lands here (never read)
-        for (uint32_t blk = 0;; blk += 16) {
-            // wave-uniform: stop when no row of the wave has steps left
-            const int irow = __builtin_amdgcn_update_dpp(0, i, 0x150, 0xF, 0xF, false);  // row_newbcast:0
-            if (!__any(irow >= i0)) break;
-            uint32_t o[16];
-            chacha12_block(key, blk + (uint32_t)gl, o);
-            uint4 *wv = reinterpret_cast<uint4 *>(&s_win[grp][16 * gl]);
-            wv[0] = make_uint4(o[0], o[1], o[2], o[3]);
-            wv[1] = make_uint4(o[4], o[5], o[6], o[7]);
-            wv[2] = make_uint4(o[8], o[9], o[10], o[11]);
-            wv[3] = make_uint4(o[12], o[13], o[14], o[15]);
-            wave_sync();
-            if (gl == 0) {
-                // branch-free over the window's 256 words (rand_walk_lane's test per word, the
-                // LDS atomic unconditional: a rejected word or a self swap targets DUMMY), the
-                // next 4 words' load in flight during these 4
-                const uint4 *w4 = reinterpret_cast<const uint4 *>(&s_win[grp][0]);
-                uint4 x = w4[0];
-                for (int t = 0; t < 64; ++t) {
-                    const uint4 xn = w4[t + 1 < 64 ? t + 1 : 63];
-                    const uint32_t xs[4] = {x.x, x.y, x.z, x.w};
+__device__ __forceinline__ int64_t rand_rec_slot(const RowParams &P, const uint32_t *list, int64_t t) {
+    return t < P.mask_R ? t : (int64_t)list[1 + (t - P.mask_R)];
+}
+#ifndef SDL_RAND_NR
+#define SDL_RAND_NR 1
+#endif
+constexpr int RAND_NR = SDL_RAND_NR;  // rows per lane in k_mask_rand_rec
+__global__ __launch_bounds__(256) void k_mask_rand_rec(RowParams P, const uint32_t *__restrict__ list,
+                                                       uint16_t *__restrict__ jbuf) {
+    const int lane = lane_id();
+    const int64_t R = P.mask_R, nt = R + (P.mask_spec1 > 0 ? (int64_t)list[0] : 0);
+    const int64_t waves = (int64_t)gridDim.x * 4;
+    constexpr int64_t W = 64 * RAND_NR;
+    for (int64_t t0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * W; t0 < nt; t0 += waves * W) {
+        bool active[RAND_NR];
+        uint64_t rec[RAND_NR];
+        uint32_t chunk[RAND_NR];
+        uint16_t *jrow[RAND_NR];
 #pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        const uint64_t m = (uint64_t)xs[u] * n;
-                        const bool acc = i >= i0 && (uint32_t)m <= zone;
-                        const uint32_t j = (uint32_t)(m >> 32);
-                        atomicMin(&s_nx[grp][acc && j != (uint32_t)i ? j : DUMMY], (uint32_t)i);
-                        i -= acc ? 1 : 0;
-                        n = (uint32_t)i + 1u;
-                        zone = (n << __builtin_clz(n)) - 1u;
-                    }
-                    x = xn;
-                }
-            }
-            wave_sync();  // (the window is rewritten next)
+        for (int r = 0; r < RAND_NR; ++r) {
+            const int64_t t = t0 + 64 * r + lane;
+            active[r] = t < nt;
+            const int64_t s = active[r] ? rand_rec_slot(P, list, t) : 0;
+            rec[r] = P.first_record + (uint64_t)(s < R ? s : s - R);
+            chunk[r] = s < R ? 0u : 1u;
+            jrow[r] = jbuf + s * (int64_t)P.S;
         }
-        // [0, k) holds val(next(x)) (or x): follow each chain to its end
-        for (int x = gl; x < kmask; x += 16) {
-            uint32_t p = (uint32_t)x;
-            for (uint32_t nq = s_nx[grp][p]; nq != NONE; nq = s_nx[grp][p]) p = nq;
-            atomicOr(&s_bt[grp][p >> 5], 1u << (p & 31));
-        }
-        wave_sync();
-        if (active)
-            for (int w = gl; w < P.mask_w; w += 16) bitsg[g * (int64_t)P.mask_w + w] = s_bt[grp][w];
-        wave_sync();  // (s_nx / s_bt are reset for the next rows)
+        rand_walk_lanes<RAND_NR>(P, active, rec, chunk, jrow);
     }
 }
 
-hipError_t launch_mask_rand_rows(const RowParams &P, const uint32_t *row_off, const uint32_t *row_rec, SegSel sel,
-                                 int64_t rows_cap, uint32_t *list, uint32_t *bitsg, hipStream_t st) {
-    if (rows_cap <= 0) return hipSuccess;
-    if (P.S > RAND_MAX_S || P.mask_w * 32 < P.S) return hipErrorInvalidValue;
+// Phase B for those rows: a wave per row, its mask bits -> bits[slot]
+template <int MR4>
+__global__ __launch_bounds__(256) void k_mask_bits_rec(RowParams P, const uint32_t *__restrict__ list,
+                                                       const uint16_t *__restrict__ jbuf, uint32_t *__restrict__ bits) {
+    __shared__ uint32_t s_nx[4][64 * MR4];
+    __shared__ uint32_t s_bt[4][2 * MR4];
+    const int lane = lane_id(), wid = (int)(threadIdx.x >> 6);
+    const int64_t nt = P.mask_R + (P.mask_spec1 > 0 ? (int64_t)list[0] : 0);
+    for (int64_t t = (int64_t)blockIdx.x * 4 + wid; t < nt; t += (int64_t)gridDim.x * 4) {
+        const int64_t s = rand_rec_slot(P, list, t);
+        rand_set_bits<MR4>(P, jbuf + s * (int64_t)P.S, s_nx[wid], s_bt[wid], lane);
+        for (int w = lane; w < P.mask_w; w += 64) bits[s * (int64_t)P.mask_w + w] = s_bt[wid][w];
+        __builtin_amdgcn_wave_barrier();  // (s_bt is rewritten by the wave's next row)
+    }
+}
+
+hipError_t launch_mask_rand_rec(const RowParams &P, uint32_t *list, uint16_t *jbuf, uint32_t *bits, hipStream_t st) {
+    const int64_t R = P.mask_R, ns = P.mask_spec1 > 0 ? 2 * R : R;
+    if (R <= 0) return hipSuccess;
+    if (P.S > RAND_MAX_S || P.mask_w * 32 < P.S || !P.mask_off) return hipErrorInvalidValue;
     hipError_t e = hipMemsetAsync(list, 0, 4, st);
     if (e != hipSuccess) return e;
-    const int64_t want = (rows_cap + 255) / 256;
-    hipLaunchKernelGGL(k_rand_list, dim3((unsigned)(want < 2048 ? want : 2048)), dim3(256), 0, st, P, row_off, row_rec,
-                       sel, rows_cap, list);
-    const int64_t w4 = (rows_cap + 3) / 4;
-    const dim3 g((unsigned)(w4 < 16384 ? w4 : 16384));
+    if (P.mask_spec1 > 0) {
+        const int64_t lb = (R + 255) / 256;
+        hipLaunchKernelGGL(k_rand_spec_list, dim3((unsigned)(lb < 2048 ? lb : 2048)), dim3(256), 0, st, P, list);
+    }
+    // (sized for every slot; the waves past R + n_spec leave at once)
+    const int64_t want = (ns + 256 * RAND_NR - 1) / (256 * RAND_NR);
+    hipLaunchKernelGGL(k_mask_rand_rec, dim3((unsigned)(want < 4096 ? want : 4096)), dim3(256), 0, st, P,
+                       (const uint32_t *)list, jbuf);
+    const int64_t wb = (ns + 3) / 4;
+    const dim3 g((unsigned)(wb < 16384 ? wb : 16384));
     const int MR4 = (P.S + 63) / 64;
-#define SDL_R16(M) hipLaunchKernelGGL(k_mask_rand16<M>, g, dim3(64), 0, st, P, row_off, row_rec, (const uint32_t *)list, bitsg)
-    if (MR4 <= 2) SDL_R16(2);
-    else if (MR4 <= 4) SDL_R16(4);
-    else if (MR4 <= 8) SDL_R16(8);
-    else if (MR4 <= 16) SDL_R16(16);
-    else SDL_R16(32);
-#undef SDL_R16
+#define SDL_BITS(M) hipLaunchKernelGGL(k_mask_bits_rec<M>, g, dim3(256), 0, st, P, (const uint32_t *)list, (const uint16_t *)jbuf, bits)
+    if (MR4 <= 2) SDL_BITS(2);
+    else if (MR4 <= 4) SDL_BITS(4);
+    else if (MR4 <= 8) SDL_BITS(8);
+    else if (MR4 <= 16) SDL_BITS(16);
+    else SDL_BITS(32);
+#undef SDL_BITS
     return hipGetLastError();
 }
 
@@ -1232,7 +1337,8 @@ hipError_t launch_rows_direct(const DirectDst &d, const uint32_t *row_off, int64
 
 hipError_t launch_rows(const RowParams &P, const uint32_t *tok, const uint32_t *rec_tok, const uint32_t *rec_cnt,
                        const uint32_t *row_off, const uint32_t *row_rec, SegSel sel, int64_t rows_cap, RowOut out,
-                       hipStream_t st) {
+                       hipStream_t st, hipStream_t st_late) {
+    if (!st_late) st_late = st;
     if (rows_cap == 0) return hipSuccess;
 #ifndef SDL_ROWS_GRID_CAP
 #define SDL_ROWS_GRID_CAP 16384
@@ -1242,12 +1348,18 @@ hipError_t launch_rows(const RowParams &P, const uint32_t *tok, const uint32_t *
     const int MR = (P.S + 255) / 256;
     if (P.label_width > 256 * MR) return hipErrorInvalidValue;
     const bool rm1 = P.task == 0 && P.rng_mode == 1;
-    if (rm1 && (!P.mask_bitsg || (P.mask_bits0 && !P.mask_off) || P.mask_w * 32 < P.S)) return hipErrorInvalidValue;
+    if (rm1 && ((P.mask_bits0 && !P.mask_off) || P.mask_w * 32 < P.S || P.S > RAND_MAX_S))
+        return hipErrorInvalidValue;
+    // (rng_mode 1: the late pass scans 256 rows a block)
+    const int64_t want_late = (rows_cap + 255) / 256;
+    const unsigned grid_late = (unsigned)(want_late < 2048 ? want_late : 2048);
 #define SDL_ROWS(MM)                                                                                                 \
-    if (rm1)                                                                                                          \
+    if (rm1) {                                                                                                        \
         hipLaunchKernelGGL((k_rows<MM, true>), dim3(grid), dim3(256), 0, st, P, tok, rec_tok, rec_cnt, row_off,      \
                            row_rec, sel, rows_cap, out);                                                              \
-    else                                                                                                              \
+        hipLaunchKernelGGL((k_rows<MM, true, true>), dim3(grid_late), dim3(256), 0, st_late, P, tok, rec_tok, rec_cnt, \
+                           row_off, row_rec, sel, rows_cap, out);                                                     \
+    } else                                                                                                            \
         hipLaunchKernelGGL((k_rows<MM, false>), dim3(grid), dim3(256), 0, st, P, tok, rec_tok, rec_cnt, row_off,     \
                            row_rec, sel, rows_cap, out)
     if (MR <= 1) SDL_ROWS(1);

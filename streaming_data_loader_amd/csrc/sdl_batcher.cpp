@@ -274,10 +274,11 @@ struct sdl_batcher {
     DevBuf<uint32_t> ranges, tokc, chunk_cnt, chunk_off, rec_local, tok_ids, rec_tok, rec_cnt, rec_rows, row_off,
         row_rec, scan_tmp;
     DevBuf<int32_t> o_ids, o_am, o_tt, o_lab;
-    // rng_mode 1: per-record chunk-0 swap indices and mask bits (k_mask_rand_rec, beside the
-    // tokenizer on stream2), the later rows' list and bits (k_mask_rand16)
+    // rng_mode 1: the swap indices and mask bits of the rows walked beside the tokenizer on stream2
+    // (k_mask_rand_rec: chunk 0 of every record, chunk 1 of the spec_list records); k_rows walks the
+    // rest in a second pass
     DevBuf<uint16_t> mask_j0;
-    DevBuf<uint32_t> mask_bits0, mask_bitsg, rand_list;
+    DevBuf<uint32_t> mask_bits0, spec_list;
     hipEvent_t rand_ev[4] = {nullptr, nullptr, nullptr, nullptr};
     DevBuf<float> o_f32;
     DevBuf<uint32_t> lab_err;
@@ -292,8 +293,11 @@ struct sdl_batcher {
     DevBuf<uint32_t> span_ovf;
     bool span_two_phase = env_int0("SDL_SPAN_TWO_PHASE", 0) != 0;
     bool small_calls = env_int0("SDL_SMALL_CALLS", 1) != 0;  // k_downstream_small + folded record bounds
-    // rng_mode 1: chunk-0 rows walked beside the tokenizer (0: every row after the row map, 16 lanes each)
+    bool small_rows = env_int0("SDL_SMALL_ROWS", 1) != 0;    // ... which also writes mlm (Philox) / clm rows
+    // rng_mode 1: chunk-0 rows walked beside the tokenizer (0: every row by its k_rows wave)
     bool rand_rec0 = env_int0("SDL_RAND_REC0", 1) != 0;
+    bool rand_rec_serial = env_int0("SDL_RAND_REC_SERIAL", 0) != 0;  // (diagnostic: the walk on the main stream)
+    bool rand_late_s2 = env_int0("SDL_RAND_LATE_S2", 0) != 0;  // (diagnostic: the late pass on stream2)
     // ... and chunk 1 of records of >= (S - frame + 1) / rho bytes (WordPiece/BPE give ~0.2-0.3 ids
     // per byte; SDL_RAND_SPEC_RHO_PCT=0: chunk 0 only)
     double rand_spec_rho = env_int0("SDL_RAND_SPEC_RHO_PCT", 25) / 100.0;
@@ -462,20 +466,14 @@ struct sdl_batcher {
         row_rec.ensure((size_t)std::max<int64_t>(rows_cap, 1));
         const bool rm1 = P.task == SDL_TASK_MLM && P.rng_mode == 1;
         const int mask_w = (P.S + 31) / 32;
-        if (rm1) {
-            mask_bitsg.ensure((size_t)std::max<int64_t>(rows_cap, 1) * (size_t)mask_w);
-            rand_list.ensure((size_t)std::max<int64_t>(rows_cap, 1) + 1);
-        }
 
         RowParams p = P;
         p.first_record = first_record;
         p.mask_w = mask_w;
         p.mask_bits0 = nullptr;
-        p.mask_bitsg = mask_bitsg.p;
         p.mask_off = d_off;
         p.mask_R = R;
         p.mask_spec1 = 0;
-        p.mask_pass = 0;
         const bool bpe = dt.kind == TOK_BYTE_BPE;
         const bool uni = dt.kind == TOK_UNIGRAM;
         // Pipelined segments (WordPiece): the tokenize launches of the chunk
@@ -516,14 +514,16 @@ struct sdl_batcher {
             const int64_t ns = p.mask_spec1 > 0 ? 2 * R : R;
             mask_j0.ensure((size_t)ns * (size_t)P.S);
             mask_bits0.ensure((size_t)ns * (size_t)mask_w);
+            spec_list.ensure((size_t)R + 1);
             ensure_stream2();
             for (auto &e : rand_ev)
                 if (!e) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
             HIP_TRY(hipEventRecord(rand_ev[0], st));  // (the last call's rows have read mask_bits0)
             HIP_TRY(hipStreamWaitEvent(stream2, rand_ev[0], 0));
             p.mask_bits0 = mask_bits0.p;
-            HIP_TRY(launch_mask_rand_rec(p, mask_j0.p, mask_bits0.p, stream2));
-            HIP_TRY(hipEventRecord(rand_ev[1], stream2));
+            hipStream_t rs = rand_rec_serial ? st : stream2;
+            HIP_TRY(launch_mask_rand_rec(p, spec_list.p, mask_j0.p, mask_bits0.p, rs));
+            HIP_TRY(hipEventRecord(rand_ev[1], rs));
         }
         if (!fold) HIP_TRY(launch_seg_bounds(ranges.p, sc, R, seg_rb.p, st));
         if (!fold && (multi() || single())) HIP_TRY(hipMemsetAsync(lab_err.p, 0, 4, st));
@@ -538,14 +538,18 @@ struct sdl_batcher {
         auto downstream = [&](int k, hipStream_t s) {
             const SegSel sel{seg_rb.p, k, k == sc.K - 1 ? 1 : 0};
             const int64_t ca = sc.cb[k], cz = sc.cb[k + 1];
+            bool rows_done = false;
             if (small) {  // one launch for the five below
-                const SmallDown d{tokc.p, chunk_cnt.p, chunk_off.p, tok_ids.p,
+                SmallDown d{tokc.p, chunk_cnt.p, chunk_off.p, tok_ids.p,
                                   uni ? uni_counters.p : bpe ? long_count.p : nullptr,
                                   uni || bpe ? chunk_ent.p : nullptr, bpe ? long_list.p : nullptr,
                                   bpe ? long_scratch.p : nullptr, uni ? uni_pool.p : nullptr,
                                   uni ? (int64_t)UNI_STAGE : (int64_t)STAGE, rec_local.p, rec_tok.p, rec_cnt.p,
                                   rec_rows.p, row_off.p, row_rec.p, fused_done ? fuse_stat : nullptr,
-                                  uni ? uni_err.p : nullptr};
+                                  uni ? uni_err.p : nullptr, 0, out};
+                // mlm (Philox) / clm rows in the same workgroup, no k_rows launch
+                d.rows = small_rows && fused_done && !rm1 ? 1 : 0;
+                rows_done = d.rows != 0;
                 HIP_TRY(launch_downstream_small(d, p, d_off, R, N, s));
             } else {
             if (!piped) mark(2);
@@ -587,25 +591,20 @@ struct sdl_batcher {
                 HIP_TRY(launch_rows_span(p, tok_ids.p, rec_tok.p, rec_cnt.p, row_off.p, row_rec.p, sel, rows_cap, out,
                                          span_err.p, s, two_phase ? &pl : nullptr));
             } else {
-                if (rm1 && rec0) {
-                    // the later rows' masks (chunk >= 1, known now) are walked on stream2 while the
-                    // chunk-0 rows -- their bits made beside the tokenizer -- are written here
+                // rng_mode 1: k_rows waits for the rows walked beside the tokenizer and walks the rest
+                // (and walks the rows past the guess in a second pass)
+                if (rm1 && rec0 && rand_late_s2) {  // (diagnostic: measured slower, the late pass starved)
+                    HIP_TRY(hipStreamWaitEvent(s, rand_ev[1], 0));
                     HIP_TRY(hipEventRecord(rand_ev[2], s));
                     HIP_TRY(hipStreamWaitEvent(stream2, rand_ev[2], 0));
-                    HIP_TRY(launch_mask_rand_rows(p, row_off.p, row_rec.p, sel, rows_cap, rand_list.p, mask_bitsg.p,
-                                                  stream2));
+                    HIP_TRY(launch_rows(p, tok_ids.p, rec_tok.p, rec_cnt.p, row_off.p, row_rec.p, sel, rows_cap, out, s,
+                                        stream2));
                     HIP_TRY(hipEventRecord(rand_ev[3], stream2));
-                    HIP_TRY(hipStreamWaitEvent(s, rand_ev[1], 0));
-                    RowParams p1 = p;
-                    p1.mask_pass = 1;
-                    HIP_TRY(launch_rows(p1, tok_ids.p, rec_tok.p, rec_cnt.p, row_off.p, row_rec.p, sel, rows_cap, out, s));
                     HIP_TRY(hipStreamWaitEvent(s, rand_ev[3], 0));
-                    p1.mask_pass = 2;
-                    HIP_TRY(launch_rows(p1, tok_ids.p, rec_tok.p, rec_cnt.p, row_off.p, row_rec.p, sel, rows_cap, out, s));
-                } else {
-                    if (rm1)
-                        HIP_TRY(launch_mask_rand_rows(p, row_off.p, row_rec.p, sel, rows_cap, rand_list.p,
-                                                      mask_bitsg.p, s));
+                } else if (rm1 && rec0) {
+                    HIP_TRY(hipStreamWaitEvent(s, rand_ev[1], 0));
+                    HIP_TRY(launch_rows(p, tok_ids.p, rec_tok.p, rec_cnt.p, row_off.p, row_rec.p, sel, rows_cap, out, s));
+                } else if (!rows_done) {
                     HIP_TRY(launch_rows(p, tok_ids.p, rec_tok.p, rec_cnt.p, row_off.p, row_rec.p, sel, rows_cap, out, s));
                 }
             }

@@ -171,14 +171,6 @@ __device__ __forceinline__ double row_bcast_f64(double v) {
     const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x150 + I, 0xF, 0xF, false);
     return __longlong_as_double((long long)((uint64_t)(uint32_t)hi << 32 | (uint32_t)lo));
 }
-// f(std::integral_constant<int, i>) for i = A .. B - 1, in order (a compile-time index for DPP controls)
-template <int A, int B, class F>
-__device__ __forceinline__ void static_for(const F &f) {
-    if constexpr (A < B) {
-        f(std::integral_constant<int, A>{});
-        static_for<A + 1, B>(f);
-    }
-}
 
 // Added token "<...>" starting at p: the bytes up to the first '>' (within
 // max_special_len, not crossing a boundary) probed as UC_ADDED.  Returns the id

@@ -71,10 +71,10 @@ def test_rand_mode_dense_records_match_oracle(torch, native_lib, oracle_tok, rec
 @pytest.mark.parametrize("env", [{"SDL_RAND_REC0": "0"}, {"SDL_RAND_SPEC_RHO_PCT": "0"},
                                  {"SDL_RAND_SPEC_RHO_PCT": "100"}, {"SDL_RAND_SPEC_RHO_PCT": "5"}])
 def test_rand_mode_mask_paths_agree(torch, native_lib, oracle_tok, records, env, monkeypatch):
-    """The rows' masks come from three places (pipeline.hip rand_pre_slot): chunk 0 and guessed
-    chunk-1 rows walked beside the tokenizer, the rest after the row map 16 lanes a row.  Every
-    split -- nothing beside the tokenizer, chunk 0 only, chunk 1 of every record long enough at 1
-    id per byte (every chunk-1 row there), at 0.05 ids per byte (chunk 1 guessed for few
+    """The rows' masks come from two places (pipeline.hip rand_pre_slot): chunk 0 and guessed
+    chunk-1 rows walked beside the tokenizer, the rest by k_rows' LATE pass (rand_rows16).
+    Every split -- nothing beside the tokenizer, chunk 0 only, chunk 1 of every record long enough
+    at 1 id per byte (every chunk-1 row there), at 0.05 ids per byte (chunk 1 guessed for few
     records) -- gives the oracle's rows."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
