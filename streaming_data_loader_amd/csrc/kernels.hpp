@@ -12,7 +12,8 @@ namespace sdl {
 // pipeline.hip: per chunk, the record ranges touching its window (3 words per chunk)
 // (rb1: also write the one-segment record bounds {0, R} there; zero1: a word to zero)
 hipError_t launch_chunk_ranges(const uint64_t *off, int64_t R, int64_t N, uint32_t *ranges, hipStream_t st,
-                               uint32_t *rb1 = nullptr, uint32_t *zero1 = nullptr);
+                               uint32_t *rb1 = nullptr, uint32_t *zero1 = nullptr, const void *copy_src = nullptr,
+                               void *copy_dst = nullptr, size_t copy_bytes = 0);
 
 // tokenize_wordpiece.hip: text arena -> per-chunk token lists + boundary offsets
 // (after launch_chunk_ranges), for chunks [c_begin, c_end) (c_end < 0: all).

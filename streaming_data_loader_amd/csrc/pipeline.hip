@@ -203,11 +203,15 @@ __device__ __forceinline__ RowSpan row_span(const SegSel &s, const uint32_t *row
 // Per chunk: record ranges touching its window (so the tokenize kernel never
 // binary-searches the offsets serially).
 // Also (thread 0) the one-segment record bounds rb = {0, R} and a zeroed error word,
-// when given: two launches fewer per call.
+// when given: two launches fewer per call.  And, for a small push, its H2D: the grid copies the
+// staged blob from mapped pinned memory (cn16 16-B units; the offsets are then read from there
+// too) -- no copy in the stream before it.
 __global__ __launch_bounds__(256) void k_chunk_ranges(const uint64_t *__restrict__ off, int64_t R, int64_t n_chunks,
                                                       uint32_t *__restrict__ ranges, uint32_t *__restrict__ rb1,
-                                                      uint32_t *__restrict__ zero1) {
+                                                      uint32_t *__restrict__ zero1, const uint4 *__restrict__ csrc,
+                                                      uint4 *__restrict__ cdst, int64_t cn16) {
     const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    for (int64_t x = c; x < cn16; x += (int64_t)gridDim.x * 256) cdst[x] = csrc[x];
     if (c == 0) {
         if (rb1) {
             rb1[0] = 0u;
@@ -231,11 +235,16 @@ __global__ __launch_bounds__(256) void k_chunk_ranges(const uint64_t *__restrict
 }
 
 hipError_t launch_chunk_ranges(const uint64_t *off, int64_t R, int64_t N, uint32_t *ranges, hipStream_t st,
-                               uint32_t *rb1, uint32_t *zero1) {
+                               uint32_t *rb1, uint32_t *zero1, const void *copy_src, void *copy_dst, size_t copy_bytes) {
     const int64_t n_chunks = (N + CHUNK - 1) / CHUNK;
-    if (n_chunks == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_chunk_ranges, dim3((unsigned)((n_chunks + 255) / 256)), dim3(256), 0, st, off, R, n_chunks,
-                       ranges, rb1, zero1);
+    const int64_t cn16 = copy_src ? (int64_t)((copy_bytes + 15) / 16) : 0;
+    if (n_chunks == 0 && cn16 == 0) return hipSuccess;
+    int64_t blocks = (n_chunks + 255) / 256;
+    const int64_t cb = (cn16 + 255) / 256;
+    if (cb > blocks) blocks = cb < 64 ? cb : 64;
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL(k_chunk_ranges, dim3((unsigned)blocks), dim3(256), 0, st, off, R, n_chunks, ranges, rb1, zero1,
+                       (const uint4 *)copy_src, (uint4 *)copy_dst, cn16);
     return hipGetLastError();
 }
 

@@ -343,6 +343,14 @@ struct sdl_batcher {
     std::deque<HostBatch *> store;
     std::deque<HostBatch *> outbox;
     PinBuf<uint8_t> pin_blob;  // staged call input: text | offsets | labels | label offsets
+    // a small push's H2D done by k_chunk_ranges from the mapped blob (process_host -> run_device)
+    struct FusedH2D {
+        const void *src = nullptr;
+        void *dst = nullptr;
+        size_t bytes = 0;
+        const uint64_t *h_off = nullptr;  // the offsets in the mapped blob
+    } fused_h2d;
+    bool fused_h2d_on = env_int0("SDL_FUSED_H2D", 1) != 0;
     DevBuf<uint8_t> h2d_blob;
     PinBuf<uint32_t> pin_u32;
     PinBuf<uint32_t> pin_stat;  // direct pass: row offsets + error words (mapped)
@@ -500,8 +508,11 @@ struct sdl_batcher {
         mark(0);
         // (one segment: k_chunk_ranges also writes its record bounds and zeroes the label error word)
         const bool fold = small_calls && sc.K == 1 && n_chunks > 0;
-        HIP_TRY(launch_chunk_ranges(d_off, R, N, ranges.p, st, fold ? seg_rb.p : nullptr,
-                                    fold && (multi() || single()) ? lab_err.p : nullptr));
+        // (a small push's H2D rides along: fused_h2d, set by process_host)
+        HIP_TRY(launch_chunk_ranges(fused_h2d.bytes ? fused_h2d.h_off : d_off, R, N, ranges.p, st,
+                                    fold ? seg_rb.p : nullptr, fold && (multi() || single()) ? lab_err.p : nullptr,
+                                    fused_h2d.src, fused_h2d.dst, fused_h2d.bytes));
+        fused_h2d = FusedH2D{};
         // rng_mode 1: a row's masks depend on (seed, record, chunk) alone, so the rows known before
         // tokenizing -- chunk 0 of every record, chunk 1 of records long enough to need one at
         // <= rand_spec_rho ids per byte -- are walked, and their mask bits made, on stream2 beside
@@ -700,8 +711,8 @@ struct sdl_batcher {
         auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
         const size_t x_off = up((size_t)N + 16), x_lab = up(x_off + 8 * (size_t)(R + 1)),
                      x_loff = up(x_lab + 4 * (size_t)L + 4), blob = x_loff + 8 * (size_t)(R + 1);
-        pin_blob.ensure(blob);
-        h2d_blob.ensure(blob);
+        pin_blob.ensure(blob + 16);  // (+16: k_chunk_ranges copies whole 16-B units)
+        h2d_blob.ensure(blob + 16);
         HostClock hc;
         par_copy(pin_blob.p, arena, (size_t)N);
         hc.lap("stage");
@@ -717,7 +728,19 @@ struct sdl_batcher {
             d_label_off = reinterpret_cast<const uint64_t *>(h2d_blob.p + x_loff);
             h2d_bytes = blob;
         }
-        HIP_TRY(hipMemcpyAsync(h2d_blob.p, pin_blob.p, h2d_bytes, hipMemcpyHostToDevice, stream));
+        // a small push (<= 64 KiB staged): k_chunk_ranges copies the blob itself, so the stream has
+        // one operation fewer before the tokenizer (the few KB cross PCIe as the kernel's loads)
+        fused_h2d = FusedH2D{};
+        if (fused_h2d_on && h2d_bytes <= (64u << 10) && !profiling) {
+            void *dsrc = nullptr;
+            HIP_TRY(hipHostGetDevicePointer(&dsrc, pin_blob.p, 0));
+            fused_h2d.src = dsrc;
+            fused_h2d.dst = h2d_blob.p;
+            fused_h2d.bytes = h2d_bytes;
+            fused_h2d.h_off = reinterpret_cast<const uint64_t *>(static_cast<const uint8_t *>(dsrc) + x_off);
+        } else {
+            HIP_TRY(hipMemcpyAsync(h2d_blob.p, pin_blob.p, h2d_bytes, hipMemcpyHostToDevice, stream));
+        }
         const uint8_t *d_text = h2d_blob.p;
         const uint64_t *d_off = reinterpret_cast<const uint64_t *>(h2d_blob.p + x_off);
         // Small calls (a per-record push): the rows go straight to the back batch
@@ -750,8 +773,14 @@ struct sdl_batcher {
             uint32_t *&p;
             ~FuseReset() { p = nullptr; }
         } fuse_reset{fuse_stat};
-        run_device(d_text, N, d_off, R, first_override >= 0 ? (uint64_t)first_override : cfg.first_record + n_records,
-                   stream, d_labels, d_label_off);
+        {
+            struct Clear {  // (never left set for a later call, also on a throw)
+                FusedH2D &f;
+                ~Clear() { f = FusedH2D{}; }
+            } clear{fused_h2d};
+            run_device(d_text, N, d_off, R, first_override >= 0 ? (uint64_t)first_override : cfg.first_record + n_records,
+                       stream, d_labels, d_label_off);
+        }
         fuse_stat = nullptr;
         if (direct) {
             if (!fused_done)
