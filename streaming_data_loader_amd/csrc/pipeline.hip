@@ -988,6 +988,72 @@ __global__ __launch_bounds__(SCAN_SMALL_NT) void k_downstream_small(SmallDown d,
     }
 }
 
+// A per-record push (<= 64 records, <= 64 chunks): the same steps on one wave -- wave scans, no
+// workgroup barriers.  With the rows fused (MR > 0: nothing after this kernel reads the call's
+// record / row tables) those tables live in LDS, so the only global round trip between steps is
+// the compacted ids (a push is bound by such dependent round trips: 10.6 us with every table in
+// global memory).  Lane order is program order within the wave; a fence between steps makes one
+// lane's writes visible to the others' reads.
+template <int MR>
+__global__ __launch_bounds__(64) void k_downstream_tiny(SmallDown d, RowParams P, const uint64_t *__restrict__ off,
+                                                        int64_t R, int64_t N, int64_t n_chunks) {
+    constexpr int ROWS_LDS = 1024;
+    __shared__ uint32_t s_coff[65], s_rtok[64], s_rcnt[64], s_rrows[64], s_roff[65];
+    __shared__ uint32_t s_rrec[MR > 0 ? ROWS_LDS : 1];
+    const int lane = lane_id();
+    auto step = [] {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    };
+    uint32_t *const coff = MR > 0 ? s_coff : d.chunk_off;
+    uint32_t *const rtok = MR > 0 ? s_rtok : d.rec_tok, *const rcnt = MR > 0 ? s_rcnt : d.rec_cnt;
+    uint32_t *const rrows = MR > 0 ? s_rrows : d.rec_rows, *const roff = MR > 0 ? s_roff : d.row_off;
+    {
+        const uint32_t c = lane < n_chunks ? d.chunk_cnt[lane] : 0u;
+        const uint32_t incl = wave_incl_sum(c);
+        if (lane < n_chunks) coff[lane] = incl - c;
+        if (lane == 63) coff[n_chunks] = incl;
+    }
+    step();
+    // (the records' loads before the compaction's stores: independent, in flight together)
+    if (lane < R) record_one(P, off, lane, N, coff, n_chunks, d.rec_local, rtok, rcnt, rrows);
+    for (int64_t cb = 0; cb < n_chunks; cb += COMPACT_CPW)
+        compact_wave(cb, d.tokc, d.chunk_cnt, coff, n_chunks, d.tok, d.long_count, d.chunk_ent, d.long_list,
+                     d.long_scratch, d.long_pool, d.stride);
+    step();
+    uint32_t G;
+    {
+        const uint32_t c = lane < R ? rrows[lane] : 0u;
+        const uint32_t incl = wave_incl_sum(c);
+        G = (uint32_t)lane_bcast((int)incl, 63);
+        if (lane < R) roff[lane] = incl - c;
+        if (lane == 63) roff[R] = incl;
+        uint32_t *const rrec = MR > 0 && G <= (uint32_t)ROWS_LDS ? s_rrec : d.row_rec;
+        if (lane < R)
+            for (uint32_t g = incl - c; g < incl; ++g) rrec[g] = (uint32_t)lane;
+        if (d.stat) {
+            if (lane < R) d.stat[lane] = incl - c;
+            if (lane == 63) {
+                d.stat[R] = incl;
+                d.stat[R + 1] = 0u;
+                d.stat[R + 2] = d.tok_err ? *d.tok_err : 0u;  // a t5 tokenizer under mlm / clm
+            }
+        }
+    }
+    if constexpr (MR > 0) {
+        step();
+        const uint32_t *const rrec = G <= (uint32_t)ROWS_LDS ? s_rrec : d.row_rec;
+        const int64_t g_end = d.out.direct.cap ? (int64_t)G : ((int64_t)G + P.B - 1) / P.B * P.B;
+        for (int64_t g = 0; g < g_end; ++g)
+            row_one<MR, false, false>(P, d.tok, rtok, rcnt, roff, rrec, g, (int64_t)G, d.out, nullptr, lane);
+    }
+}
+
+static const bool tiny_downstream = [] {
+    const char *e = std::getenv("SDL_TINY_DOWNSTREAM");
+    return !e || std::atoi(e) != 0;
+}();
 hipError_t launch_downstream_small(const SmallDown &d, const RowParams &P, const uint64_t *off, int64_t R, int64_t N,
                                    hipStream_t st) {
     const int64_t n_chunks = (N + CHUNK - 1) / CHUNK;
@@ -995,7 +1061,10 @@ hipError_t launch_downstream_small(const SmallDown &d, const RowParams &P, const
     const int MR = (P.S + 255) / 256;
     if (d.rows && ((P.rng_mode == 1 && P.task == 0) || (P.task != 0 && P.task != 1)))
         return hipErrorInvalidValue;  // (rng_mode 1 masks need k_rows' passes; span has its own rows)
-#define SDL_DS(M) hipLaunchKernelGGL(k_downstream_small<M>, dim3(1), dim3(SCAN_SMALL_NT), 0, st, d, P, off, R, N, n_chunks)
+    const bool tiny = tiny_downstream && R <= 64 && n_chunks <= 64;
+#define SDL_DS(M)                                                                                                    \
+    if (tiny) hipLaunchKernelGGL(k_downstream_tiny<M>, dim3(1), dim3(64), 0, st, d, P, off, R, N, n_chunks);        \
+    else hipLaunchKernelGGL(k_downstream_small<M>, dim3(1), dim3(SCAN_SMALL_NT), 0, st, d, P, off, R, N, n_chunks)
     if (!d.rows) SDL_DS(0);
     else if (MR <= 1) SDL_DS(1);
     else if (MR <= 2) SDL_DS(2);

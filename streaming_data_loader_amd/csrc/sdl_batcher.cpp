@@ -351,6 +351,10 @@ struct sdl_batcher {
         const uint64_t *h_off = nullptr;  // the offsets in the mapped blob
     } fused_h2d;
     bool fused_h2d_on = env_int0("SDL_FUSED_H2D", 1) != 0;
+    bool self_ranges_on = env_int0("SDL_SELF_RANGES", 0) != 0;  // (measured neutral: 43.0 vs 43.0 us)
+    bool self_ranges = false;  // this push: zero-copy, the WordPiece kernel finds its ranges
+    void *blob_dev = nullptr;               // pin_blob's device address ...
+    const uint8_t *blob_dev_host = nullptr;  // ... for this host buffer
     DevBuf<uint8_t> h2d_blob;
     PinBuf<uint32_t> pin_u32;
     PinBuf<uint32_t> pin_stat;  // direct pass: row offsets + error words (mapped)
@@ -508,10 +512,12 @@ struct sdl_batcher {
         mark(0);
         // (one segment: k_chunk_ranges also writes its record bounds and zeroes the label error word)
         const bool fold = small_calls && sc.K == 1 && n_chunks > 0;
-        // (a small push's H2D rides along: fused_h2d, set by process_host)
-        HIP_TRY(launch_chunk_ranges(fused_h2d.bytes ? fused_h2d.h_off : d_off, R, N, ranges.p, st,
-                                    fold ? seg_rb.p : nullptr, fold && (multi() || single()) ? lab_err.p : nullptr,
-                                    fused_h2d.src, fused_h2d.dst, fused_h2d.bytes));
+        // (a small push's H2D rides along: fused_h2d, set by process_host; or none at all: self_ranges)
+        const bool self = self_ranges && small && fold && dt.kind == TOK_WORDPIECE && R <= 63;
+        if (!self)
+            HIP_TRY(launch_chunk_ranges(fused_h2d.bytes ? fused_h2d.h_off : d_off, R, N, ranges.p, st,
+                                        fold ? seg_rb.p : nullptr, fold && (multi() || single()) ? lab_err.p : nullptr,
+                                        fused_h2d.src, fused_h2d.dst, fused_h2d.bytes));
         fused_h2d = FusedH2D{};
         // rng_mode 1: a row's masks depend on (seed, record, chunk) alone, so the rows known before
         // tokenizing -- chunk 0 of every record, chunk 1 of records long enough to need one at
@@ -661,7 +667,9 @@ struct sdl_batcher {
                                       rec_local.p, long_count.p, long_list.p, cap, long_scratch.p, bpe_err.p, st));
             downstream(0, st);
         } else if (!piped) {
-            HIP_TRY(launch_wordpiece_chunks(dt, d_text, N, d_off, R, ranges.p, tokc.p, chunk_cnt.p, rec_local.p, st));
+            HIP_TRY(launch_wordpiece_chunks(dt, d_text, N, d_off, R, ranges.p, tokc.p, chunk_cnt.p, rec_local.p, st, 0,
+                                            -1, self, self ? seg_rb.p : nullptr,
+                                            self && (multi() || single()) ? lab_err.p : nullptr));
             downstream(0, st);
         } else {
             ensure_pipe_events(sc.K);
@@ -731,18 +739,35 @@ struct sdl_batcher {
         // a small push (<= 64 KiB staged): k_chunk_ranges copies the blob itself, so the stream has
         // one operation fewer before the tokenizer (the few KB cross PCIe as the kernel's loads)
         fused_h2d = FusedH2D{};
+        self_ranges = false;
+        const uint8_t *d_text = h2d_blob.p;
+        const uint64_t *d_off = reinterpret_cast<const uint64_t *>(h2d_blob.p + x_off);
         if (fused_h2d_on && h2d_bytes <= (64u << 10) && !profiling) {
-            void *dsrc = nullptr;
-            HIP_TRY(hipHostGetDevicePointer(&dsrc, pin_blob.p, 0));
-            fused_h2d.src = dsrc;
-            fused_h2d.dst = h2d_blob.p;
-            fused_h2d.bytes = h2d_bytes;
-            fused_h2d.h_off = reinterpret_cast<const uint64_t *>(static_cast<const uint8_t *>(dsrc) + x_off);
+            if (blob_dev_host != pin_blob.p) {  // (once per staging buffer)
+                HIP_TRY(hipHostGetDevicePointer(&blob_dev, pin_blob.p, 0));
+                blob_dev_host = pin_blob.p;
+            }
+            const uint8_t *dsrc = static_cast<const uint8_t *>(blob_dev);
+            if (self_ranges_on && dt.kind == TOK_WORDPIECE && R <= 63) {
+                // a per-record WordPiece push: the kernels read the mapped blob itself and the
+                // tokenizer finds its record ranges (k_wordpiece_chunks<true>): no copy, no
+                // k_chunk_ranges -- the tokenizer is the stream's first operation
+                self_ranges = true;
+                d_text = dsrc;
+                d_off = reinterpret_cast<const uint64_t *>(dsrc + x_off);
+                if (with_labels) {
+                    d_labels = reinterpret_cast<const uint32_t *>(dsrc + x_lab);
+                    d_label_off = reinterpret_cast<const uint64_t *>(dsrc + x_loff);
+                }
+            } else {
+                fused_h2d.src = dsrc;
+                fused_h2d.dst = h2d_blob.p;
+                fused_h2d.bytes = h2d_bytes;
+                fused_h2d.h_off = reinterpret_cast<const uint64_t *>(dsrc + x_off);
+            }
         } else {
             HIP_TRY(hipMemcpyAsync(h2d_blob.p, pin_blob.p, h2d_bytes, hipMemcpyHostToDevice, stream));
         }
-        const uint8_t *d_text = h2d_blob.p;
-        const uint64_t *d_off = reinterpret_cast<const uint64_t *>(h2d_blob.p + x_off);
         // Small calls (a per-record push): the rows go straight to the back batch
         // and a pre-allocated next one in the same pass, and the row offsets and
         // error words come back through mapped memory -- one synchronisation.
@@ -778,6 +803,10 @@ struct sdl_batcher {
                 FusedH2D &f;
                 ~Clear() { f = FusedH2D{}; }
             } clear{fused_h2d};
+            struct ClearSelf {
+                bool &f;
+                ~ClearSelf() { f = false; }
+            } clear_self{self_ranges};
             run_device(d_text, N, d_off, R, first_override >= 0 ? (uint64_t)first_override : cfg.first_record + n_records,
                        stream, d_labels, d_label_off);
         }

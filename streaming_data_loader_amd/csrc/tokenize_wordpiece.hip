@@ -418,10 +418,15 @@ __device__ unsigned long long sdl_phase_cycles[16];
 // machine is bound by its lanes' probe latency, not by its step count.
 constexpr int WP_NPROBE = SDL_WP_NPROBE;
 static_assert(WP_NPROBE >= 1, "at least one candidate per step");
+// SELF (a push of <= 63 records read straight from mapped pinned memory): each block finds its
+// record ranges itself -- lane r holds off[r], three ballots count the offsets below the window's
+// edges -- so no k_chunk_ranges launch (and no copy) precedes it; block 0 also writes the
+// one-segment record bounds and zeroes the label error word (k_chunk_ranges' fold).
+template <bool SELF>
 __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL_WP_WAVES, 8))) void k_wordpiece_chunks(
     DevTok T, const uint8_t *__restrict__ text, int64_t N, const uint64_t *__restrict__ off, int64_t R,
     const uint32_t *__restrict__ ranges, uint32_t *__restrict__ tokc, uint32_t *__restrict__ chunk_cnt,
-    uint32_t *__restrict__ rec_local, int64_t c_begin) {
+    uint32_t *__restrict__ rec_local, int64_t c_begin, uint32_t *__restrict__ rb1, uint32_t *__restrict__ zero1) {
     __shared__ __attribute__((aligned(16))) uint8_t s_win[WIN];
     __shared__ uint32_t s_rbits[RBITS_WORDS + 1];
     __shared__ uint16_t s_pieces[CHUNK];   // (pos - c0) | kind << 12
@@ -460,7 +465,25 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
         hp = tid < HALO_L / 16 ? w0 + 16 * tid : c0 + CHUNK + 16 * (tid - HALO_L / 16);
         hv = load16(text, hp, N);
     }
-    const int64_t ra = ranges[3 * ci], rz = ranges[3 * ci + 1], r_lo = ranges[3 * ci + 2];
+    int64_t ra, rz, r_lo;
+    if constexpr (SELF) {  // (TOK_THREADS == 64: one wave, R <= 63)
+        const bool in = tid <= R;
+        const int64_t o = in ? (int64_t)off[tid] : 0;
+        ra = __popcll(__ballot(in && o < w0));
+        rz = __popcll(__ballot(in && o < w0 + WIN));
+        r_lo = __popcll(__ballot(in && o < c0));
+        if (ci == 0 && tid == 0) {
+            if (rb1) {
+                rb1[0] = 0u;
+                rb1[1] = (uint32_t)R;
+            }
+            if (zero1) *zero1 = 0u;
+        }
+    } else {
+        ra = ranges[3 * ci];
+        rz = ranges[3 * ci + 1];
+        r_lo = ranges[3 * ci + 2];
+    }
     *reinterpret_cast<uint4 *>(s_win + HALO_L + 16 * tid) = v;
     if (tid < (WIN - CHUNK) / 16) *reinterpret_cast<uint4 *>(s_win + (hp - w0)) = hv;
     if (tid <= RBITS_WORDS) s_rbits[tid] = 0;
@@ -1145,13 +1168,19 @@ void print_phase_cycles() {
 
 hipError_t launch_wordpiece_chunks(const DevTok &T, const uint8_t *text, int64_t N, const uint64_t *off, int64_t R,
                                    uint32_t *ranges, uint32_t *tokc, uint32_t *chunk_cnt, uint32_t *rec_local,
-                                   hipStream_t st, int64_t c_begin, int64_t c_end) {
+                                   hipStream_t st, int64_t c_begin, int64_t c_end, bool self, uint32_t *rb1,
+                                   uint32_t *zero1) {
     const int64_t n_chunks = (N + CHUNK - 1) / CHUNK;
     if (c_end < 0 || c_end > n_chunks) c_end = n_chunks;
     if (c_begin < 0) c_begin = 0;
     if (c_end <= c_begin) return hipSuccess;
-    hipLaunchKernelGGL(k_wordpiece_chunks, dim3((unsigned)(c_end - c_begin)), dim3(TOK_THREADS), 0, st, T, text, N, off,
-                       R, ranges, tokc, chunk_cnt, rec_local, c_begin);
+    if (self && (R > TOK_THREADS - 1 || c_begin != 0)) return hipErrorInvalidValue;
+    if (self)
+        hipLaunchKernelGGL(k_wordpiece_chunks<true>, dim3((unsigned)(c_end - c_begin)), dim3(TOK_THREADS), 0, st, T, text,
+                           N, off, R, ranges, tokc, chunk_cnt, rec_local, c_begin, rb1, zero1);
+    else
+        hipLaunchKernelGGL(k_wordpiece_chunks<false>, dim3((unsigned)(c_end - c_begin)), dim3(TOK_THREADS), 0, st, T,
+                           text, N, off, R, ranges, tokc, chunk_cnt, rec_local, c_begin, rb1, zero1);
     return hipGetLastError();
 }
 
