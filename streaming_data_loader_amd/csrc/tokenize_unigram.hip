@@ -50,7 +50,10 @@ __device__ __forceinline__ uint32_t meta_byte(int x) { return x == 0 ? 0xE2u : x
 
 // LDS budget: 3 one-wave blocks per SIMD (<= 13.3 KB each) -- the kernel waits
 // on probe latency, so resident waves are what it runs on
-constexpr int ARENA = 768;          // LDS bytes for normalized medium words
+#ifndef SDL_UNI_ARENA
+#define SDL_UNI_ARENA 768
+#endif
+constexpr int ARENA = SDL_UNI_ARENA;  // LDS bytes for normalized medium words
 constexpr int WIN_PAD = WIN + 32;   // window + gather padding; the arena follows
 #ifndef SDL_UNI_JOB_CAP
 #define SDL_UNI_JOB_CAP 112
