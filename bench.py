@@ -246,7 +246,9 @@ def load_pmc(task, arena_mib, kernel, corpus="fixture"):
         if d.get("task") != task or int(d.get("arena_mib", -1)) != arena_mib or d.get("corpus", "fixture") != corpus:
             return None, (f"{os.path.relpath(p, REPO)} was collected for task={d.get('task')} "
                           f"arena={d.get('arena_mib')} corpus={d.get('corpus', 'fixture')}")
-        k = d["kernels"]["sdl::" + kernel]
+        # (a template instance is named with its arguments: sdl::k_wordpiece_chunks<false>)
+        name = next(n for n in d["kernels"] if n == "sdl::" + kernel or n.startswith("sdl::" + kernel + "<"))
+        k = d["kernels"][name]
         k["_file"] = os.path.relpath(p, REPO)
         return k, None
     except Exception as e:  # a malformed summary is reported, not used

@@ -1,5 +1,5 @@
 #!/bin/bash
-# r04 PMC: every task's counter passes at 256 MiB (fixture), mlm/clm/span held-out fetch/write,
+# PMC: every task's counter passes at 256 MiB (fixture), mlm/clm/span held-out fetch/write,
 # (the stream calibration is tools/gpu_pmc_load.sh).  Summarised on the
 # box (gpurun_out/pmcsum/*.json -> profiles/pmc/) and the raw counter CSVs dropped (> 64 MiB).
 set -u
