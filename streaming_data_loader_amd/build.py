@@ -23,7 +23,8 @@ ARCH = os.environ.get("SDL_OFFLOAD_ARCH", "gfx950")
 
 SOURCES = ["tokenize_wordpiece.hip", "tokenize_bpe.hip", "tokenize_unigram.hip", "pipeline.hip", "json_text.hip", "transport_frame.hip", "inflate.hip",
            "assets.cpp", "sdl_batcher.cpp"]
-HEADERS = ["common.hpp", "device_util.hpp", "kernels.hpp", "tok_device.hpp", "assets.hpp", "json.hpp", "unigram.hpp"]
+HEADERS = ["common.hpp", "device_util.hpp", "kernels.hpp", "tok_device.hpp", "assets.hpp", "json.hpp", "unigram.hpp",
+           "rows_device.hpp"]
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
          "-I", os.path.join(REPO, "include"), "-I", CSRC]
 

@@ -552,20 +552,24 @@ struct sdl_batcher {
         fused_done = small && fuse_stat && (P.task == SDL_TASK_MLM || P.task == SDL_TASK_CLM);
         if (fused_done) out.direct = fuse_dd;
         // everything after the tokenizer, for segment k, on stream s
+        auto small_down = [&]() {
+            SmallDown d{tokc.p, chunk_cnt.p, chunk_off.p, tok_ids.p,
+                        uni ? uni_counters.p : bpe ? long_count.p : nullptr,
+                        uni || bpe ? chunk_ent.p : nullptr, bpe ? long_list.p : nullptr,
+                        bpe ? long_scratch.p : nullptr, uni ? uni_pool.p : nullptr,
+                        uni ? (int64_t)UNI_STAGE : (int64_t)STAGE, rec_local.p, rec_tok.p, rec_cnt.p,
+                        rec_rows.p, row_off.p, row_rec.p, fused_done ? fuse_stat : nullptr,
+                        uni ? uni_err.p : nullptr, 0, out};
+            // mlm (Philox) / clm rows in the same workgroup, no k_rows launch
+            d.rows = small_rows && fused_done && !rm1 ? 1 : 0;
+            return d;
+        };
         auto downstream = [&](int k, hipStream_t s) {
             const SegSel sel{seg_rb.p, k, k == sc.K - 1 ? 1 : 0};
             const int64_t ca = sc.cb[k], cz = sc.cb[k + 1];
             bool rows_done = false;
             if (small) {  // one launch for the five below
-                SmallDown d{tokc.p, chunk_cnt.p, chunk_off.p, tok_ids.p,
-                                  uni ? uni_counters.p : bpe ? long_count.p : nullptr,
-                                  uni || bpe ? chunk_ent.p : nullptr, bpe ? long_list.p : nullptr,
-                                  bpe ? long_scratch.p : nullptr, uni ? uni_pool.p : nullptr,
-                                  uni ? (int64_t)UNI_STAGE : (int64_t)STAGE, rec_local.p, rec_tok.p, rec_cnt.p,
-                                  rec_rows.p, row_off.p, row_rec.p, fused_done ? fuse_stat : nullptr,
-                                  uni ? uni_err.p : nullptr, 0, out};
-                // mlm (Philox) / clm rows in the same workgroup, no k_rows launch
-                d.rows = small_rows && fused_done && !rm1 ? 1 : 0;
+                const SmallDown d = small_down();
                 rows_done = d.rows != 0;
                 HIP_TRY(launch_downstream_small(d, p, d_off, R, N, s));
             } else {
