@@ -347,7 +347,10 @@ __device__ int bpe_wave_seg(const DevTok &T, uint32_t &sym, int n, uint64_t &hea
 // lane-varying j is a select per slot); only the two pairs a merge creates are probed again.  A
 // wave runs 64 words at once and pays the longest word's merge count in probe latencies, where
 // the segmented wave BPE pays every packed batch's.  s[0 .. returned count) = the word's ids.
-constexpr int LANE_BPE = 16;
+#ifndef SDL_LANE_BPE
+#define SDL_LANE_BPE 12  // (16: held-out clm -1.3 %, fixture -1.7 %: its registers cost the common path; 8: held-out -3.5 %)
+#endif
+constexpr int LANE_BPE = SDL_LANE_BPE;
 __device__ __forceinline__ int bpe_lane(const DevTok &T, uint32_t (&s)[LANE_BPE], int n) {
     constexpr uint32_t NOV = 0xFFFFFFFFu;
     uint32_t v[LANE_BPE - 1];
