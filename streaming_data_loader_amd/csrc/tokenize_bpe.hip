@@ -416,10 +416,10 @@ void print_bpe_cycles() {
     unsigned long long h[8];
     if (hipMemcpyFromSymbol(h, HIP_SYMBOL(sdl_bpe_cycles), sizeof(h)) != hipSuccess) return;
     static const char *names[] = {"", "load+classify", "pre-token starts", "word-table probes", "wave BPE",
-                                  "compact", "-", "-"};
+                                  "compact", "lane BPE", "-"};
     unsigned long long tot = 0;
-    for (int i = 1; i < 6; ++i) tot += h[i];
-    for (int i = 1; i < 6; ++i)
+    for (int i = 1; i < 7; ++i) tot += h[i];
+    for (int i = 1; i < 7; ++i)
         fprintf(stderr, "[bpe stamps] %-18s %6.2f%%\n", names[i], tot ? 100.0 * (double)h[i] / (double)tot : 0.0);
 }
 #else
@@ -726,6 +726,7 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
         }
     }
     __syncthreads();
+    BPE_STAMP(6);
 #endif
     // ---- 4. wave BPE of the (longer) misses, packed: consecutive misses share the lanes --
     for (int q = 0; q < npend;) {
