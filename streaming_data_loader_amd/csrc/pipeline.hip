@@ -411,17 +411,17 @@ __device__ __forceinline__ void chacha12_block_row(const ChaRow &R, uint32_t ctr
 // rng_mode 1, rows that were not walked beside the tokenizer (rand_pre_slot < 0: chunk >= 1 past
 // the byte-length guess, or every row when nothing was): k_rows' LATE pass walks them in place, up
 // to 4 rows a wave, 16 lanes a row.  Per window of 16 ChaCha12 blocks the row's 16 lanes each
-// compute one block into LDS; lane 0 of the row walks the 256 words (rand_walk_lanes' acceptance
-// test) and puts each swap straight into next() (an LDS atomicMin, as rand_set_bits does from
-// stored indices; a rejected word or a self swap targets the dummy slot S); then the row's lanes
-// follow [0, k)'s chains into its mask bits.  The walk is one dependent chain per row (a word's
+// compute one block in registers; the row walks the 256 words (rand_walk_lanes' acceptance test),
+// each handed to the whole row by DPP row_newbcast, and lane 0 puts each swap straight into next()
+// (an LDS atomicMin, as rand_set_bits does from stored indices; a rejected word or a self swap
+// targets the dummy slot S); then the row's lanes follow [0, k)'s chains into its mask bits.  The walk is one dependent chain per row (a word's
 // test needs the previous word's outcome: lo32(v * n) moves with n like a hash, so guessing n for
 // later words and iterating to a fixed point converged lane by lane and measured ~25 us a row);
 // these rows are few (~3 % of the bench's), so the chains' latency hides across the waves.
-// win: [4][256] words, nx: [4][S + 1], bt: [4][bw] (wave LDS); a lane's group's row is (rec, chunk)
-// when its group < nrows.
+// nx: [4][S + 1], bt: [4][bw] (wave LDS); a lane's group's row is (rec, chunk) when its group <
+// nrows.
 __device__ __forceinline__ void rand_rows16(const RowParams &P, int nrows, uint64_t rec, uint32_t chunk,
-                                            uint32_t *__restrict__ win, uint32_t *__restrict__ nx,
+                                            uint32_t *__restrict__ nx,
                                             uint32_t *__restrict__ bt, int bw, int lane) {
     constexpr uint32_t NONE = 0xFFFFFFFFu;
     const int grp = lane >> 4, gl = lane & 15;
@@ -437,7 +437,6 @@ __device__ __forceinline__ void rand_rows16(const RowParams &P, int nrows, uint6
                              0u, 0u, 0u};
     ChaRow cr;
     chacha_row_init(cr, key);
-    (void)win;
     uint32_t *gnx = nx + (S + 1) * grp, *gbt = bt + bw * grp;
     for (int x = gl; x <= S; x += 16) gnx[x] = NONE;
     for (int x = gl; x < bw; x += 16) gbt[x] = 0u;
@@ -490,7 +489,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MR >= 4 ? S
     const int wid = (int)(threadIdx.x >> 6);
     // (LATE: a wave's LDS for rand_rows16 -- 4 windows, 4 next() arrays + dummy slots, 4 rows' bits)
     constexpr int NXS = 256 * MR + 1, BW = 8 * MR;
-    __shared__ __attribute__((aligned(16))) uint32_t s_rw[LATE ? 4 : 1][LATE ? 4 * (256 + NXS + BW) : 1];
+    __shared__ __attribute__((aligned(16))) uint32_t s_rw[LATE ? 4 : 1][LATE ? 4 * (NXS + BW) : 1];
     const RowSpan rs = row_span(sel, row_off, P.B, rows_cap);
     const int64_t G = rs.g_real;
     const DirectDst &dd = out.direct;
@@ -504,7 +503,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MR >= 4 ? S
                 late = rand_pre_slot(P, r, (uint32_t)(gl - row_off[r])) < 0;
             }
             uint32_t *const rw = s_rw[LATE ? wid : 0];
-            uint32_t *const bits = rw + 4 * (256 + NXS);
+            uint32_t *const bits = rw + 4 * NXS;
             for (uint64_t m = __ballot(late); m;) {
                 // up to 4 of them: group q of 16 lanes walks the q-th
                 const int nr = __popcll(m) < 4 ? __popcll(m) : 4;
@@ -518,7 +517,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MR >= 4 ? S
                     rec = P.first_record + (uint64_t)r;
                     kq = (uint32_t)(gq - row_off[r]);
                 }
-                rand_rows16(P, nr, rec, kq, rw, rw + 4 * 256, bits, BW, lane);
+                rand_rows16(P, nr, rec, kq, rw, bits, BW, lane);
                 for (int q = 0; q < nr; ++q, m &= m - 1)
                     row_one<MR, RM1, LATE>(P, tok, rec_tok, rec_cnt, row_off, row_rec, g0 + __builtin_ctzll(m), G, out,
                                            bits + BW * q, lane);

@@ -19,7 +19,8 @@ def torch():
 
 
 @pytest.mark.parametrize("S,B,first_record,seed", [(128, 8, 0, 5), (512, 256, 1000, 1234), (1024, 16, 7, 2 ** 63 + 3),
-                                                  (100, 8, 3, 11)])  # (S % 8 != 0: 2-B index stores)
+                                                  (100, 8, 3, 11),  # (S % 8 != 0: 2-B index stores)
+                                                  (2048, 4, 2, 99)])  # (RAND_MAX_S: the largest rows kernels)
 def test_rand_mode_rows_match_oracle(torch, native_lib, oracle_tok, records, S, B, first_record, seed):
     rng = np.random.default_rng(S)
     texts = [records[i] for i in rng.integers(0, len(records), 300)] + hard_records(2)[:40]
