@@ -130,3 +130,18 @@ def test_short_calls_after_long_ones_read_no_stale_status(native_lib, records):
     per = drain(b, records[:50])
     for g, w in zip(planes(mixed), planes(per)):
         np.testing.assert_array_equal(g, w)
+
+
+@pytest.mark.parametrize("B", [1, 4])
+def test_per_record_rng_mode_1_matches_oracle(native_lib, records, B):
+    """rng_mode 1 on the per-record push: nothing is walked beside the tokenizer on the small
+    path, so k_rows' first pass skips every row and its late pass walks them all, writing them
+    straight into the host batches (rows past the two batches through the segment copy)."""
+    texts = records[:12]
+    S, k, seed = 64, 9, 31
+    gt = Bt.GenTokenizer(Bt.ModelType.Bert, Bt.BatchConfig(B, S), Bt.Mask(k, 103), Bt.TokenizerConfig(),
+                         chunk=True, seed=seed, rng_mode=1)
+    got = planes(drain(gt, texts))
+    want = oracle_lib.oracle_rows(oracle_lib.Tok(), texts, S, k, seed=seed, B=B, rng_mode=1)
+    for g, w in zip(got, want):
+        np.testing.assert_array_equal(g, w)
