@@ -600,6 +600,7 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
             atomicOr(&s_nabits[CHUNK / 32 + (rel >> 5)], 1u << (rel & 31));
         }
     }
+    SDL_STAMP(12);
     if (n_opens) {  // block-uniform
         __syncthreads();
         for (uint32_t k = n_leads + tid; k < n_leads + n_opens; k += TOK_THREADS) {
@@ -1155,12 +1156,13 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
 void print_phase_cycles() {
     unsigned long long h[16];
     if (hipMemcpyFromSymbol(h, HIP_SYMBOL(sdl_phase_cycles), sizeof(h)) != hipSuccess) return;
-    static const char *names[] = {"", "load+rbits", "classify+lists", "rare-passes", "merge+lookback", "scan+pieces",
-                                  "-", "wp-pending", "compact", "rec_local", "wp-init", "wp-first-probes"};
+    static const char *names[] = {"", "load+rbits", "classify+lists", "rare-openers+sync", "merge+lookback",
+                                  "scan+pieces", "-", "wp-pending", "compact", "rec_local", "wp-init",
+                                  "wp-first-probes", "rare-leads"};
     unsigned long long tot = 0;
-    for (int k = 1; k <= 11; ++k) tot += h[k];
+    for (int k = 1; k <= 12; ++k) tot += h[k];
     fprintf(stderr, "[stamps] block-cycles by phase (wave 0, all blocks, all calls):");
-    for (int k = 1; k <= 11; ++k)
+    for (int k = 1; k <= 12; ++k)
         if (k != 6) fprintf(stderr, " %s=%.1f%%", names[k], 100.0 * h[k] / (tot ? tot : 1));
     fprintf(stderr, " total=%llu\n", tot);
 }
