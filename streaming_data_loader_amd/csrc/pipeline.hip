@@ -252,6 +252,7 @@ hipError_t launch_chunk_ranges(const uint64_t *off, int64_t R, int64_t N, uint32
 // ---------------------------------------------------------------------------
 // Per-chunk token lists -> one dense token array in arena order.
 // ---------------------------------------------------------------------------
+template <int PART>
 __global__ __launch_bounds__(256) void k_compact_tokens(const uint32_t *__restrict__ tokc,
                                                         const uint32_t *__restrict__ chunk_cnt,
                                                         const uint32_t *__restrict__ chunk_off, int64_t n_chunks,
@@ -262,8 +263,8 @@ __global__ __launch_bounds__(256) void k_compact_tokens(const uint32_t *__restri
                                                         const uint32_t *__restrict__ long_pool, int64_t stride) {
     const int64_t cb = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * COMPACT_CPW;  // the wave's first chunk
     if (cb >= n_chunks) return;
-    compact_wave(cb, tokc, chunk_cnt, chunk_off, n_chunks, tok, long_count, chunk_ent, long_list, long_scratch,
-                 long_pool, stride);
+    compact_wave<PART>(cb, tokc, chunk_cnt, chunk_off, n_chunks, tok, long_count, chunk_ent, long_list, long_scratch,
+                       long_pool, stride);
 }
 
 hipError_t launch_compact_tokens(const uint32_t *tokc, const uint32_t *chunk_cnt, const uint32_t *chunk_off,
@@ -272,8 +273,12 @@ hipError_t launch_compact_tokens(const uint32_t *tokc, const uint32_t *chunk_cnt
                                  hipStream_t st, const uint32_t *long_pool, int64_t stride) {
     if (n_chunks == 0) return hipSuccess;
     const int64_t waves = (n_chunks + COMPACT_CPW - 1) / COMPACT_CPW;
-    hipLaunchKernelGGL(k_compact_tokens, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, tokc, chunk_cnt,
+    // (byte-level BPE / unigram: the long-item copy as its own kernel; one of the two has work)
+    hipLaunchKernelGGL(k_compact_tokens<1>, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, tokc, chunk_cnt,
                        chunk_off, n_chunks, tok, long_count, chunk_ent, long_list, long_scratch, long_pool, stride);
+    if (long_count)
+        hipLaunchKernelGGL(k_compact_tokens<2>, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, tokc, chunk_cnt,
+                           chunk_off, n_chunks, tok, long_count, chunk_ent, long_list, long_scratch, long_pool, stride);
     return hipGetLastError();
 }
 

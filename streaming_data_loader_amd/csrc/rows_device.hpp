@@ -12,7 +12,9 @@ namespace sdl {
 #define SDL_COMPACT_CPW 4
 #endif
 constexpr int COMPACT_CPW = SDL_COMPACT_CPW;  // chunks per wave: their loads are in flight together
-// one wave: chunks [cb, cb + COMPACT_CPW)
+// one wave: chunks [cb, cb + COMPACT_CPW).  PART 1: only when the call has no long items, 2: only
+// when it has (separate kernels keep the plain copy's registers), 0: either.
+template <int PART = 0>
 __device__ __forceinline__ void compact_wave(int64_t cb, const uint32_t *__restrict__ tokc,
                                              const uint32_t *__restrict__ chunk_cnt,
                                              const uint32_t *__restrict__ chunk_off, int64_t n_chunks,
@@ -29,7 +31,9 @@ __device__ __forceinline__ void compact_wave(int64_t cb, const uint32_t *__restr
         n[j] = in ? chunk_cnt[cb + j] : 0u;
         o[j] = in ? chunk_off[cb + j] : 0u;
     }
-    if (!long_count || *long_count == 0) {
+    const bool has_long = long_count && *long_count != 0;
+    if ((PART == 1 && has_long) || (PART == 2 && !has_long)) return;
+    if (!has_long) {
         // lane-contiguous dwords: every store instruction writes 256 B of the
         // dense array back to back (at any alignment); the first 256 ids of all
         // the wave's chunks are loaded before any is stored
@@ -68,33 +72,43 @@ __device__ __forceinline__ void compact_wave(int64_t cb, const uint32_t *__restr
     }
     // byte-level BPE / unigram with long items: an entry LONG_MARK | i stands
     // for the k ids of long piece i (in long_scratch at its byte position) or
-    // of pool item i
+    // of pool item i.  The wave's chunks go in lockstep, 64 entries of each a
+    // step, so their dependent loads (entry -> item -> ids) are in flight together.
+    uint32_t ne[COMPACT_CPW], written[COMPACT_CPW], nemax = 0;
+#pragma unroll
     for (int j = 0; j < COMPACT_CPW; ++j) {
-        const int64_t c = cb + j;
-        if (c >= n_chunks) break;
-        const uint32_t *src = tokc + c * stride;
-        uint32_t *dst = tok + o[j];
-        const uint32_t ne = chunk_ent[c];  // entries written by the chunk kernel
-        uint32_t written = 0;
-        for (uint32_t e0 = 0; e0 < ne; e0 += 64) {
-            const uint32_t e = e0 + lane;
-            const uint32_t x = e < ne ? __builtin_nontemporal_load(src + e) : 0u;
-            const bool mark = (x & 0x80000000u) != 0u;
-            const uint32_t w = e >= ne ? 0u : !mark ? 1u : long_pool ? long_pool[x & 0x7FFFFFFFu] : long_list[x & 0x7FFFFFFFu].k;
-            const uint32_t incl = wave_incl_sum(w);
-            const uint32_t at = written + incl - w;
-            if (e < ne && at < n[j]) {
-                if (!mark) {
-                    dst[at] = x;
+        ne[j] = cb + j < n_chunks ? chunk_ent[cb + j] : 0u;  // entries written by the chunk kernel
+        written[j] = 0;
+        nemax = ne[j] > nemax ? ne[j] : nemax;
+    }
+    for (uint32_t e0 = 0; e0 < nemax; e0 += 64) {
+        const uint32_t e = e0 + lane;
+        uint32_t x[COMPACT_CPW], w[COMPACT_CPW];
+#pragma unroll
+        for (int j = 0; j < COMPACT_CPW; ++j)
+            x[j] = e < ne[j] ? __builtin_nontemporal_load(tokc + (cb + j) * stride + e) : 0u;
+#pragma unroll
+        for (int j = 0; j < COMPACT_CPW; ++j) {
+            const bool mark = (x[j] & 0x80000000u) != 0u;
+            w[j] = e >= ne[j] ? 0u : !mark ? 1u : long_pool ? long_pool[x[j] & 0x7FFFFFFFu] : long_list[x[j] & 0x7FFFFFFFu].k;
+        }
+#pragma unroll
+        for (int j = 0; j < COMPACT_CPW; ++j) {
+            const uint32_t incl = wave_incl_sum(w[j]);
+            const uint32_t at = written[j] + incl - w[j];
+            uint32_t *dst = tok + o[j];
+            if (e < ne[j] && at < n[j]) {
+                if (!(x[j] & 0x80000000u)) {
+                    dst[at] = x[j];
                 } else if (long_pool) {  // unigram long item: [k, ids...] in the pool
-                    const uint32_t po = x & 0x7FFFFFFFu;
-                    for (uint32_t q = 0; q < w; ++q) dst[at + q] = long_pool[po + 1 + q];
+                    const uint32_t po = x[j] & 0x7FFFFFFFu;
+                    for (uint32_t q = 0; q < w[j]; ++q) dst[at + q] = long_pool[po + 1 + q];
                 } else {
-                    const BpeLong L = long_list[x & 0x7FFFFFFFu];
-                    for (uint32_t q = 0; q < L.k; ++q) dst[at + q] = long_scratch[L.pos + q];
+                    const uint64_t pos = long_list[x[j] & 0x7FFFFFFFu].pos;
+                    for (uint32_t q = 0; q < w[j]; ++q) dst[at + q] = long_scratch[pos + q];
                 }
             }
-            written += (uint32_t)lane_bcast((int)incl, 63);
+            written[j] += (uint32_t)lane_bcast((int)incl, 63);
         }
     }
 }
