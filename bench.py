@@ -345,6 +345,9 @@ def parse_args(argv=None):
                          "the proxy vocabularies were not trained on (tests/golden/heldout_records.jsonl; "
                          "a second kernel-tuning corpus, not an untouched one)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-heldout", action="store_true",
+                    help="skip the held-out corpus leg (by default a fixture run also times the same config on "
+                         "the held-out corpus and reports it under `heldout`, beside `value`)")
     ap.add_argument("--rng-mode", type=int, default=0, choices=[0, 1],
                     help="0 the Philox contract (default); 1 the reference's own draws on a per-row StdRng: "
                          "rand 0.8.5 shuffle (mlm masks), rand_distr StandardNormal (span gaps / sizes)")
@@ -538,6 +541,82 @@ def dry_run(args, world, rank):
         dist.destroy_process_group()
 
 
+def make_step(task_name, db, records, arena, offs, order, first_record, dev, stream):
+    """One step of the hot path over a resident arena: sdl_process_device[_labels]
+    (the tensors stay alive in the closure)."""
+    import torch
+    N, R = len(arena) - 16, len(order)
+    text = torch.from_numpy(arena).to(dev)
+    offsets = torch.from_numpy(offs.astype(np.int64)).to(dev)
+    if task_name == "single-class":  # Label::Single: record i's label is i & 1 (imdb: 2 classes)
+        t_lab = torch.from_numpy((np.asarray(order, np.int64) & 1).astype(np.int32)).to(dev)
+        t_loff = torch.arange(R + 1, dtype=torch.int64, device=dev)
+    elif task_name == "multi-label":
+        lv, lo = record_labels(len(records))
+        per = [lv[int(lo[i]):int(lo[i + 1])] for i in range(len(records))]
+        vals = np.concatenate([per[i] for i in order]).astype(np.int32)
+        loff = np.zeros(R + 1, np.int64)
+        np.cumsum([len(per[i]) for i in order], out=loff[1:])
+        t_lab = torch.from_numpy(vals).to(dev)
+        t_loff = torch.from_numpy(loff).to(dev)
+    else:
+        def step():
+            return db.process(text.data_ptr(), N, offsets.data_ptr(), R, first_record, stream.cuda_stream)
+        return step
+
+    def step():
+        return db.process_labels(text.data_ptr(), N, offsets.data_ptr(), R, t_lab.data_ptr(), t_loff.data_ptr(),
+                                 first_record, stream.cuda_stream)
+    return step
+
+
+def heldout_leg(args, db, dev, stream, task, world, rank, barrier):
+    """The same config on the held-out corpus (text the proxy vocabularies were not
+    trained on), timed like the headline (warmup, barrier + synchronize around
+    exactly K steps, max over ranks).  Reported beside `value`, never in its place."""
+    import torch
+    records, arena, offs, order, first = shard(rank, args.arena_mib << 20, "heldout", world)
+    N, R = len(arena) - 16, len(order)
+    step = make_step(args.task, db, records, arena, offs, order, first, dev, stream)
+    for _ in range(args.warmup):
+        res = step()
+        torch.cuda.synchronize(dev)
+    db.set_profiling(True)
+    tok_sum = 0.0
+    barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res = step()
+        tok_sum += db.stage_times().get("tokenize", 0.0)
+    torch.cuda.synchronize(dev)
+    barrier()
+    dt = max_over_ranks(time.perf_counter() - t0, world, dev)
+    db.set_profiling(False)
+    tok_err, lab_err = res.tokenize_errors(), res.label_errors()
+    toks = res.tokens()
+    tok_ms = tok_sum / args.steps
+    tok_bytes = N + 8 * (R + 1) + 4 * toks
+    achieved = tok_bytes / (tok_ms * 1e-3) / 1e9
+    out = {"corpus": "heldout (tests/golden/heldout_records.jsonl tiled, seeded)",
+           "value": round(N * world * args.steps / dt / 1e6, 2), "unit": "MB/s",
+           "ms_per_step": round(dt / args.steps * 1e3, 4), "arena_bytes_per_gpu": N, "records_per_gpu": R,
+           "rows_per_gpu": res.rows(), "ids_per_gpu": toks,
+           "errors": {"tokenize": tok_err, "label": lab_err},
+           "roofline": {"kernel": task["kernel"], "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS,
+                        "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 5),
+                        "algorithmic_bytes_per_launch": tok_bytes, "avg_launch_ms": round(tok_ms, 4)}}
+    pmc, note = load_pmc(args.task, args.arena_mib, task["kernel"], "heldout")
+    if pmc is not None:
+        traffic, issue, note = pmc_roofline(pmc, tok_ms, tok_bytes, stream_bytes=N + 8 * (R + 1))
+        out["roofline"]["traffic"] = traffic
+        out["roofline"]["issue"] = issue
+    if note:
+        out["roofline"]["pmc_note"] = note
+    log(f"held-out: {out['value']} MB/s, tokenize {tok_ms:.4f} ms")
+    return out
+
+
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else argv
     args = parse_args(argv)
@@ -571,8 +650,6 @@ def main(argv=None):
     N, R = len(arena) - 16, len(order)
     log(f"rank {rank}/{world}: task {args.task}, corpus {args.corpus}, arena {N} bytes, {R} records, "
         f"first record {first_record}")
-    text = torch.from_numpy(arena).to(dev)
-    offsets = torch.from_numpy(offs.astype(np.int64)).to(dev)
     stream = torch.cuda.Stream(device=dev)
     kind = {"mlm": native.SDL_TASK_MLM, "clm": native.SDL_TASK_CLM, "span": native.SDL_TASK_SPAN,
             "multi-label": native.SDL_TASK_MULTI_LABEL, "single-class": native.SDL_TASK_SINGLE_CLASS}
@@ -580,28 +657,7 @@ def main(argv=None):
                                                                                           native.BERT_PROXY_TOKENIZER)
     db = DeviceBatcher(task=kind[args.task], batch_size=B, sequence_length=S, seed=1234, device=local,
                        tokenizer=tok_path, rng_mode=args.rng_mode)
-    if args.task == "single-class":  # Label::Single: record i's label is i & 1 (imdb: 2 classes)
-        t_lab = torch.from_numpy((np.asarray(order, np.int64) & 1).astype(np.int32)).to(dev)
-        t_loff = torch.arange(R + 1, dtype=torch.int64, device=dev)
-
-        def step():
-            return db.process_labels(text.data_ptr(), N, offsets.data_ptr(), R, t_lab.data_ptr(), t_loff.data_ptr(),
-                                     first_record, stream.cuda_stream)
-    elif args.task == "multi-label":
-        lv, lo = record_labels(len(records))
-        per = [lv[int(lo[i]):int(lo[i + 1])] for i in range(len(records))]
-        vals = np.concatenate([per[i] for i in order]).astype(np.int32)
-        loff = np.zeros(R + 1, np.int64)
-        np.cumsum([len(per[i]) for i in order], out=loff[1:])
-        t_lab = torch.from_numpy(vals).to(dev)
-        t_loff = torch.from_numpy(loff).to(dev)
-
-        def step():
-            return db.process_labels(text.data_ptr(), N, offsets.data_ptr(), R, t_lab.data_ptr(), t_loff.data_ptr(),
-                                     first_record, stream.cuda_stream)
-    else:
-        def step():
-            return db.process(text.data_ptr(), N, offsets.data_ptr(), R, first_record, stream.cuda_stream)
+    step = make_step(args.task, db, records, arena, offs, order, first_record, dev, stream)
 
     for i in range(args.warmup):
         res = step()
@@ -695,6 +751,8 @@ def main(argv=None):
     if args.e2e_frames and rank == 0 and args.task in ("mlm", "clm", "span"):
         # last: it reuses the handle's workspace (the step's planes are overwritten)
         line["end_to_end_frames"] = end_to_end_frames(db, records, order, dev, stream, args.task)
+    if args.corpus == "fixture" and not args.no_heldout:  # (after the legs that reuse the step's result)
+        line["heldout"] = heldout_leg(args, db, dev, stream, task, world, rank, barrier)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("cpu baseline ...")
         line["cpu_baseline"] = cpu_baseline(args.task, records, order)

@@ -108,6 +108,18 @@ enum : uint32_t { UC_PIECE = 0, UC_META = 1, UC_WORD = 2, UC_ADDED = 3 };
 constexpr int UNI_STAGE = 2 * CHUNK + 128; // tokc entries per chunk (a 1-byte word can yield 2 ids)
 constexpr int UNI_WMAX = 16;        // longest word (bytes) the chunk kernel settles itself
 constexpr int UNI_NODES = UNI_WMAX + 4;
+// A chunk's tokc slice (UNI_STAGE u32): its entry list (<= STAGE entries: every piece's ids fit
+// the stage slots up to the next piece) and, behind it, the Viterbi jobs the chunk kernel hands
+// to k_unigram_viterbi -- a job's ids land as u16 at its stage position in the results region,
+// and its list entry becomes LMARK | UNI_JOB_BIT | k << 24 | position (k_compact_tokens expands it).
+constexpr int UNI_VPC = 88;                           // Viterbi jobs per chunk (more: long items)
+constexpr int UNI_JR_OFF = STAGE;                     // results: u16 [STAGE] at the stage positions
+constexpr int UNI_JP_OFF = STAGE + STAGE / 2;         // job payloads: uint4 [UNI_VPC]
+constexpr int UNI_JM_OFF = UNI_JP_OFF + 4 * UNI_VPC;  // job metas: L | pos << 5 | entry << 17
+constexpr int UNI_JN_OFF = UNI_JM_OFF + UNI_VPC;      // the chunk's job count
+constexpr uint32_t UNI_JOB_BIT = 0x40000000u;
+static_assert(UNI_JN_OFF < UNI_STAGE && (UNI_JP_OFF * 4) % 16 == 0 && (UNI_STAGE * 4) % 16 == 0,
+              "the Viterbi jobs fit the tokc slice behind its list");
 constexpr int UNI_LANE_NORM = 256;  // normalized bytes per lane of the long-item kernel
 constexpr int UNI_HUGE_NORM = 1 << 18;  // ... per wave of the huge-item kernel
 // grapheme / whitespace properties (tools/make_t5_tables.py)

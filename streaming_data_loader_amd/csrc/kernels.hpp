@@ -65,6 +65,7 @@ hipError_t launch_unigram_chunks(const DevTok &T, const uint8_t *text, int64_t N
 void print_phase_cycles();  // diagnostic builds only
 void print_uni_cycles();
 void print_long_cycles();
+void print_vit_cycles();
 void print_gz_cycles();
 void print_bpe_cycles();
 #endif

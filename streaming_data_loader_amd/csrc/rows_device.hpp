@@ -31,7 +31,8 @@ __device__ __forceinline__ void compact_wave(int64_t cb, const uint32_t *__restr
         n[j] = in ? chunk_cnt[cb + j] : 0u;
         o[j] = in ? chunk_off[cb + j] : 0u;
     }
-    const bool has_long = long_count && *long_count != 0;
+    // (unigram: Viterbi job markers are in every call's lists)
+    const bool has_long = long_count && (long_pool != nullptr || *long_count != 0);
     if ((PART == 1 && has_long) || (PART == 2 && !has_long)) return;
     if (!has_long) {
         // lane-contiguous dwords: every store instruction writes 256 B of the
@@ -72,8 +73,10 @@ __device__ __forceinline__ void compact_wave(int64_t cb, const uint32_t *__restr
     }
     // byte-level BPE / unigram with long items: an entry LONG_MARK | i stands
     // for the k ids of long piece i (in long_scratch at its byte position) or
-    // of pool item i.  The wave's chunks go in lockstep, 64 entries of each a
-    // step, so their dependent loads (entry -> item -> ids) are in flight together.
+    // of pool item i; a unigram Viterbi job's entry LONG_MARK | UNI_JOB_BIT |
+    // k << 24 | pos for the k u16 ids at pos of its chunk's results region.
+    // The wave's chunks go in lockstep, 64 entries of each a step, so their
+    // dependent loads (entry -> item -> ids) are in flight together.
     uint32_t ne[COMPACT_CPW], written[COMPACT_CPW], nemax = 0;
 #pragma unroll
     for (int j = 0; j < COMPACT_CPW; ++j) {
@@ -90,7 +93,9 @@ __device__ __forceinline__ void compact_wave(int64_t cb, const uint32_t *__restr
 #pragma unroll
         for (int j = 0; j < COMPACT_CPW; ++j) {
             const bool mark = (x[j] & 0x80000000u) != 0u;
-            w[j] = e >= ne[j] ? 0u : !mark ? 1u : long_pool ? long_pool[x[j] & 0x7FFFFFFFu] : long_list[x[j] & 0x7FFFFFFFu].k;
+            const bool job = long_pool && (x[j] & UNI_JOB_BIT);
+            w[j] = e >= ne[j] ? 0u : !mark ? 1u : job ? (x[j] >> 24) & 31u : long_pool ? long_pool[x[j] & 0x7FFFFFFFu]
+                                                                                    : long_list[x[j] & 0x7FFFFFFFu].k;
         }
 #pragma unroll
         for (int j = 0; j < COMPACT_CPW; ++j) {
@@ -100,6 +105,10 @@ __device__ __forceinline__ void compact_wave(int64_t cb, const uint32_t *__restr
             if (e < ne[j] && at < n[j]) {
                 if (!(x[j] & 0x80000000u)) {
                     dst[at] = x[j];
+                } else if (long_pool && (x[j] & UNI_JOB_BIT)) {  // unigram Viterbi job
+                    const uint16_t *jr = reinterpret_cast<const uint16_t *>(tokc + (cb + j) * stride + UNI_JR_OFF) +
+                                         (x[j] & 0xFFFu);
+                    for (uint32_t q = 0; q < w[j]; ++q) dst[at + q] = jr[q];
                 } else if (long_pool) {  // unigram long item: [k, ids...] in the pool
                     const uint32_t po = x[j] & 0x7FFFFFFFu;
                     for (uint32_t q = 0; q < w[j]; ++q) dst[at + q] = long_pool[po + 1 + q];

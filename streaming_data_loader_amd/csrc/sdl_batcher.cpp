@@ -396,6 +396,7 @@ struct sdl_batcher {
         print_phase_cycles();
         print_uni_cycles();
         print_long_cycles();
+        print_vit_cycles();
         print_bpe_cycles();
         if (uni_counters.p) {
             uint32_t c[4] = {0, 0, 0, 0}, e = 0;

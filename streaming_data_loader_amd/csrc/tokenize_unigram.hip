@@ -55,11 +55,7 @@ __device__ __forceinline__ uint32_t meta_byte(int x) { return x == 0 ? 0xE2u : x
 #endif
 constexpr int ARENA = SDL_UNI_ARENA;  // LDS bytes for normalized medium words
 constexpr int WIN_PAD = WIN + 32;   // window + gather padding; the arena follows
-#ifndef SDL_UNI_JOB_CAP
-#define SDL_UNI_JOB_CAP 112
-#endif
-constexpr int JOB_CAP = SDL_UNI_JOB_CAP;  // words waiting for the DP (more: long items)
-constexpr int VP_CAP = JOB_CAP + JOB_CAP / 2;  // Viterbi pieces per chunk
+constexpr int VP_CAP = UNI_VPC;  // Viterbi jobs per chunk (more: long items)
 #ifndef SDL_UNI_MED_CAP
 #define SDL_UNI_MED_CAP 128
 #endif
@@ -68,19 +64,21 @@ constexpr int MED_CAP = SDL_UNI_MED_CAP;  // medium words per chunk (more: long 
 #define SDL_UNI_WT_UNROLL 2
 #endif
 constexpr int UNI_WT_UNROLL = SDL_UNI_WT_UNROLL;  // word-table probes in flight per lane
-#ifndef SDL_UNI_TASK_CAP
-#define SDL_UNI_TASK_CAP 256
+constexpr uint8_t CNT_LONG = 0xFF;  // s_cnt of a long item
+constexpr uint8_t CNT_JOB = 0x80;   // s_cnt of a piece handed to k_unigram_viterbi: CNT_JOB | its jobs (< 0x7F)
+// k_unigram_viterbi: a pass takes the chunk's next jobs whose candidates fit VTCAP (one job
+// always does: vp_tasks(UNI_WMAX) = 17 + 16 * 16 < VTCAP) and at most VJP of them (a DP lane each)
+#ifndef SDL_UNI_VJP
+#define SDL_UNI_VJP 64
 #endif
-constexpr int TASK_CAP = SDL_UNI_TASK_CAP;  // probe tasks per round (>= one job's: L <= UNI_WMAX)
-#ifndef SDL_UNI_DPG
-#define SDL_UNI_DPG 8
+#ifndef SDL_UNI_VTCAP
+#define SDL_UNI_VTCAP 1024
 #endif
-constexpr int DPG = SDL_UNI_DPG;  // lanes relaxing one job's candidates together
-constexpr uint8_t CNT_LONG = 0xFF;   // s_cnt of a long item        // lanes running the DP (a round holds few jobs)
-#ifndef SDL_UNI_TASK_UNROLL
-#define SDL_UNI_TASK_UNROLL 4
+#ifndef SDL_UNI_VU
+#define SDL_UNI_VU 2
 #endif
-constexpr int TASK_UNROLL = SDL_UNI_TASK_UNROLL;  // probes in flight per lane
+constexpr int VJP = SDL_UNI_VJP, VTCAP = SDL_UNI_VTCAP, VU = SDL_UNI_VU;  // VU: probes in flight per lane
+static_assert(VJP <= 64 && VTCAP % (64 * VU) == 0 && VTCAP < 0x7FF, "a hit index fits a back pointer's 11 bits");
 
 typedef __attribute__((address_space(3))) double lds_f64;
 
@@ -154,8 +152,6 @@ __device__ __forceinline__ int probe_result_w3(const Probe &P, uint32_t key, con
 // are negative log-probabilities: stored as is, one ulp further from zero;
 // negated, one ulp nearer); LDS keeps the 16-bit id and the f32 as before.
 constexpr uint32_t UNI_ID_MASK = 0x7FFFu;
-constexpr uint16_t NO_PIECE = 0xFFFFu;  // a round's task with no vocab piece (ids are < 0xFFFF: the host
-                                        // refuses a marked piece id >= 0x7FFF and vocabularies > 65,535)
 __device__ __forceinline__ double uni_score64(float f, uint32_t id16) {
     double d = (double)f;
     if (id16 & 0x8000u) {
@@ -559,29 +555,46 @@ __device__ unsigned long long sdl_uni_cycles[8];
             stamp_prev_ = t_;                                                         \
         }                                                                             \
     } while (0)
-// counts (stamps build): 0 chunks 1 pieces 2 jobs 3 vps 4 rounds 5 tasks 6 medium words 7 jobs with > 1 vp
-// 8.. 8+16: vps by payload length 1..17
+// counts (stamps build): 0 chunks 1 pieces 2 Viterbi jobs 3 their candidates 4 Viterbi passes 5 hits
+// 6 medium words
 __device__ unsigned long long sdl_uni_counts[32];
 #define UNI_COUNT(k, v) do { atomicAdd(&sdl_uni_counts[k], (unsigned long long)(v)); } while (0)
 void print_uni_cycles() {
     unsigned long long cn[32];
     if (hipMemcpyFromSymbol(cn, HIP_SYMBOL(sdl_uni_counts), sizeof(cn)) == hipSuccess && cn[0]) {
-        fprintf(stderr, "[uni counts] chunks %llu pieces/chunk %.1f jobs/chunk %.2f vps/chunk %.2f rounds/chunk %.2f "
-                        "tasks/chunk %.1f medium/chunk %.2f multi-vp jobs/chunk %.3f\n", cn[0], (double)cn[1] / cn[0],
+        fprintf(stderr, "[uni counts] chunks %llu pieces/chunk %.1f jobs/chunk %.2f tasks/chunk %.1f "
+                        "viterbi passes/chunk %.2f hits/chunk %.1f medium/chunk %.2f\n", cn[0], (double)cn[1] / cn[0],
                 (double)cn[2] / cn[0], (double)cn[3] / cn[0], (double)cn[4] / cn[0], (double)cn[5] / cn[0],
-                (double)cn[6] / cn[0], (double)cn[7] / cn[0]);
-        fprintf(stderr, "[uni counts] vp payload length histogram:");
-        for (int i = 0; i < 17; ++i) fprintf(stderr, " %d:%llu", i, cn[8 + i]);
-        fprintf(stderr, "\n");
+                (double)cn[6] / cn[0]);
     }
     unsigned long long h[8];
     if (hipMemcpyFromSymbol(h, HIP_SYMBOL(sdl_uni_cycles), sizeof(h)) != hipSuccess) return;
-    static const char *names[] = {"", "load+classify+specials", "piece starts", "word table+medium", "task bases",
-                                  "compact+rec_local", "candidate probes", "DP"};
+    static const char *names[] = {"", "load+classify+specials", "piece starts", "word table+medium", "-",
+                                  "compact+jobs+rec_local", "-", "-"};
     unsigned long long tot = 0;
     for (int i = 1; i < 8; ++i) tot += h[i];
     for (int i = 1; i < 8; ++i)
         fprintf(stderr, "[uni stamps] %-24s %6.2f%%\n", names[i], tot ? 100.0 * (double)h[i] / (double)tot : 0.0);
+}
+__device__ unsigned long long sdl_vit_cycles[8];
+#define VIT_STAMP(k)                                                                  \
+    do {                                                                              \
+        if (threadIdx.x == 0) {                                                       \
+            const unsigned long long t_ = __builtin_amdgcn_s_memtime();              \
+            atomicAdd(&sdl_vit_cycles[k], t_ - vstamp_);                              \
+            vstamp_ = t_;                                                             \
+        }                                                                             \
+    } while (0)
+void print_vit_cycles() {
+    unsigned long long h[8];
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(sdl_vit_cycles), sizeof(h)) != hipSuccess) return;
+    static const char *names[] = {"", "jobs load+task bases", "candidate probes", "DP", "backtrack+write",
+                                  "count fixups", "-", "-"};
+    unsigned long long tot = 0;
+    for (int i = 1; i < 8; ++i) tot += h[i];
+    for (int i = 1; i < 6; ++i)
+        fprintf(stderr, "[vit stamps] %-24s %6.2f%%\n", names[i], tot ? 100.0 * (double)h[i] / (double)tot : 0.0);
+    fprintf(stderr, "[vit stamps] total cycles %llu\n", tot);
 }
 __device__ unsigned long long sdl_long_cycles[8], sdl_long_counts[4];
 #define LONG_STAMP(k)                                                                 \
@@ -608,6 +621,7 @@ void print_long_cycles() {
 #else
 #define UNI_COUNT(k, v) do {} while (0)
 #define UNI_STAMP(k) do {} while (0)
+#define VIT_STAMP(k) do {} while (0)
 #define LONG_STAMP(k) do {} while (0)
 #define LONG_COUNT(k, v) do {} while (0)
 #endif
@@ -622,46 +636,21 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
     uint32_t *__restrict__ chunk_ent, uint32_t *__restrict__ rec_local, uint32_t *__restrict__ counters,
     uint4 *__restrict__ items, uint32_t item_cap, uint32_t *__restrict__ err) {
     __shared__ __attribute__((aligned(16))) uint8_t s_bytes[WIN_PAD + ARENA + 32];  // window | arena
-    // s_cls / s_med are dead during the Viterbi rounds (long-item
-    // lengths move to their stage slot), which reuse them for the DP nodes:
-    // LDS per one-wave block decides how many chunks a CU keeps in flight.
     constexpr int U_CLS = 0, U_MED = (WIN + 15) & ~15, U_MED_END = U_MED + 2 * MED_CAP;
-#ifdef SDL_UNI_OLD_DP
-    constexpr int DP_BYTES = (64 / DPG) * UNI_NODES * 12;
-#else
-    // the rounds' probe results and the DP rows' back pointers (s_tsc f32, s_tid u16, s_bp u32)
-    constexpr int DP_BYTES = TASK_CAP * 6 + 4 * 17 * 4;
-#endif
-    constexpr int U_END = U_MED_END > DP_BYTES ? U_MED_END : DP_BYTES;
-    __shared__ __attribute__((aligned(16))) uint8_t s_u[U_END];
+    __shared__ __attribute__((aligned(16))) uint8_t s_u[U_MED_END];  // classes | medium words
     uint8_t *const s_cls = s_u + U_CLS;
     __shared__ uint32_t s_rbits[RBITS_WORDS + 1];
     __shared__ uint16_t s_pieces[CHUNK + 1];  // prel | SPEC << 12
     // ids staged at their piece's byte offset: a piece may use the bytes up to
-    // the next piece (stage_room); one that needs more becomes a long item
+    // the next piece (stage_room); one that needs more becomes a long item.  A
+    // Viterbi piece's slot holds its first job's index.
     __shared__ uint16_t s_stage[STAGE];
-    __shared__ uint8_t s_cnt[CHUNK];              // ids per piece (<= 2 UNI_WMAX), CNT_LONG = long item
+    // ids per piece (<= 2 UNI_WMAX), CNT_LONG = long item, CNT_JOB | n = n Viterbi jobs
+    __shared__ uint8_t s_cnt[CHUNK];
     uint16_t *const s_med = (uint16_t *)(s_u + U_MED);  // medium words: piece index | length << 11
-    __shared__ uint32_t s_scratch[16];  // 0 jobs 1 vps 2 arena used 3 medium words; 8.. scan scratch
-    __shared__ uint16_t s_job_pi[JOB_CAP], s_job_vp[JOB_CAP];
-    __shared__ uint8_t s_job_nvp[JOB_CAP];
-    __shared__ uint16_t s_job_tb[JOB_CAP + 1];  // task base of each job (job order; < 2^16)
-    __shared__ uint16_t s_job_rb[JOB_CAP + 1];  // candidate-row base of each job
-#ifdef SDL_UNI_OLD_DP
-    __shared__ uint32_t s_rowmask[TASK_CAP];    // per row: which candidate ends exist (<= UNI_WMAX + 1)
-#else
-    uint32_t *const s_bp = (uint32_t *)(s_u + TASK_CAP * 6);  // the DP rows' back pointers (start | id << 16)
-#endif
-    __shared__ uint16_t s_vp_src[VP_CAP];
+    __shared__ uint32_t s_scratch[16];  // 1 jobs 2 arena used 3 medium words; 8.. scan scratch
+    __shared__ uint16_t s_vp_src[VP_CAP];  // Viterbi jobs: payload in LDS (window or arena) and length
     __shared__ uint8_t s_vp_len[VP_CAP];
-#ifdef SDL_UNI_OLD_DP
-    __shared__ uint16_t s_tid[TASK_CAP];
-    __shared__ float s_tsc[TASK_CAP];
-#else
-    // (overlaid on s_u: s_cls / s_med are dead once the rounds start)
-    float *const s_tsc = (float *)s_u;
-    uint16_t *const s_tid = (uint16_t *)(s_u + TASK_CAP * 4);
-#endif
 
     const int tid = threadIdx.x;
     const int lane = tid;
@@ -674,7 +663,6 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
     lds_u8 *cls = (lds_u8 *)s_cls;
     const lds_u32 *rbits = (const lds_u32 *)s_rbits;
     const lds_u32 *w32 = (const lds_u32 *)s_bytes;
-    const int Mm = T.maxlen_meta, Mf = T.maxlen_first;
 #ifdef SDL_STAMPS
     unsigned long long stamp_prev_ = __builtin_amdgcn_s_memtime();
 #endif
@@ -861,16 +849,11 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
                     // miss: one Viterbi piece, the word's bytes in the window
                     const uint32_t vp = atomicAdd(&s_scratch[1], 1u);
                     if (vp < VP_CAP) {
-                        const uint32_t jb = atomicAdd(&s_scratch[0], 1u);
-                        if (jb < JOB_CAP) {
-                            s_vp_src[vp] = (uint16_t)wi0;
-                            s_vp_len[vp] = (uint8_t)len;
-                            s_job_pi[jb] = (uint16_t)pi;
-                            s_job_vp[jb] = (uint16_t)vp;
-                            s_job_nvp[jb] = 1;
-                            cnt[pi] = 0;
-                            done = true;
-                        }
+                        s_vp_src[vp] = (uint16_t)wi0;
+                        s_vp_len[vp] = (uint8_t)len;
+                        stage[prel] = (uint16_t)vp;
+                        cnt[pi] = CNT_JOB | 1u;
+                        done = true;
                     }
                 }
             } else if (kind[u] == 2) {
@@ -924,7 +907,7 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
                 for (int pass = 0; pass < 2 && fits; ++pass) {
                     if (pass == 1) {
                         if (nvp == 0) break;
-                        if (bound > stage_room(pi) || nvp > 255) { fits = false; break; }
+                        if (bound > stage_room(pi) || nvp >= (int)CNT_JOB - 1) { fits = false; break; }
                         vp0 = atomicAdd(&s_scratch[1], (uint32_t)nvp);
                         if (vp0 + (uint32_t)nvp > (uint32_t)VP_CAP) { fits = false; break; }
                     }
@@ -960,15 +943,10 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
                 if (fits && nvp == 0) {  // nothing left after normalization
                     cnt[pi] = 0;
                     done = true;
-                } else if (fits) {
-                    const uint32_t jb = atomicAdd(&s_scratch[0], 1u);
-                    if (jb < JOB_CAP) {
-                        s_job_pi[jb] = (uint16_t)pi;
-                        s_job_vp[jb] = (uint16_t)vp0;
-                        s_job_nvp[jb] = (uint8_t)nvp;
-                        cnt[pi] = 0;
-                        done = true;
-                    }
+                } else if (fits) {  // its Viterbi pieces: consecutive jobs vp0 ..
+                    stage[prel] = (uint16_t)vp0;
+                    cnt[pi] = (uint8_t)(CNT_JOB | (uint32_t)nvp);
+                    done = true;
                 }
             }
         }
@@ -979,418 +957,55 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
     }
     __syncthreads();
     UNI_STAMP(3);
-    // ---- 4./5. batched Viterbi of the pending words, in rounds ------------------
-    int nj = (int)(s_scratch[0] < (uint32_t)JOB_CAP ? s_scratch[0] : (uint32_t)JOB_CAP);
-#if defined(SDL_ABLATE_UNI)
-    // diagnostic: every Viterbi job yields one [UNK] (2: no candidate probes either)
-    for (int jb = lane; jb < nj; jb += 64) {
-        const int pi = s_job_pi[jb];
-        stage[s_pieces[pi] & 0xFFFu] = (uint16_t)T.unk_id;
-        cnt[pi] = 1;
-    }
-#if SDL_ABLATE_UNI == 2
-    nj = 0;
-#endif
-#endif
-    uint32_t carry = 0, rcarry = 0;  // task and row bases per job (job order)
-    for (int j0 = 0; j0 < nj; j0 += 64) {
-        const int j = j0 + lane;
-        uint32_t t = 0, rw = 0;
-        if (j < nj)
-            for (int q = 0; q < s_job_nvp[j]; ++q) {
-                const int L = s_vp_len[s_job_vp[j] + q];
-                t += (uint32_t)vp_tasks(L, Mm, Mf);
-                rw += (uint32_t)L + 1u;
-            }
-        const uint32_t incl = wave_incl_sum(t), rincl = wave_incl_sum(rw);
-        if (j < nj) {
-            s_job_tb[j] = (uint16_t)(carry + incl - t);
-            s_job_rb[j] = (uint16_t)(rcarry + rincl - rw);
-        }
-        carry += (uint32_t)lane_bcast((int)incl, 63);
-        rcarry += (uint32_t)lane_bcast((int)rincl, 63);
-    }
-    if (lane == 0) {
-        s_job_tb[nj] = (uint16_t)carry;
-        s_job_rb[nj] = (uint16_t)rcarry;
-#ifdef SDL_STAMPS
-        UNI_COUNT(0, 1);
-        UNI_COUNT(1, np);
-        UNI_COUNT(2, nj);
-        UNI_COUNT(5, carry);
-        UNI_COUNT(6, s_scratch[3]);
-        for (int q = 0; q < nj; ++q) {
-            UNI_COUNT(3, s_job_nvp[q]);
-            if (s_job_nvp[q] > 1) UNI_COUNT(7, 1);
-            for (int z = 0; z < s_job_nvp[q]; ++z) UNI_COUNT(8 + (s_vp_len[s_job_vp[q] + z] < 16 ? s_vp_len[s_job_vp[q] + z] : 16), 1);
-        }
-#endif
-    }
-    __syncthreads();
-    // Rounds are software-pipelined: round r + 1's probes are issued right after
-    // round r's results land in LDS, and are in flight while round r's DP runs.
-    static_assert(TASK_CAP <= 64 * TASK_UNROLL, "a round's tasks are one probe batch");
-    auto round_end = [&](int a) -> int {  // jobs [a, end) whose tasks fit TASK_CAP (one job always does)
-        int lo = a + 1, hi = nj;
-        while (lo < hi) {
-            const int m = (lo + hi + 1) >> 1;
-            if (s_job_tb[m] - s_job_tb[a] <= (uint32_t)TASK_CAP) lo = m; else hi = m - 1;
-        }
-        return lo;
-    };
-    // candidate probes: task t of the round is one candidate (start, end) of one
-    // piece, TASK_UNROLL in flight per lane
-    Probe P[TASK_UNROLL];
-    W16 W[TASK_UNROLL];
-    uint32_t meta[TASK_UNROLL];  // row | k << 16 | n << 22 | cont << 29; ~0u: no probe
-    int gen[TASK_UNROLL];        // generic probe result (payload > 16 bytes); -2: use P
-    uint32_t gw3[TASK_UNROLL];
-    // A lane takes TASK_UNROLL consecutive tasks (4 lane + u): one job/vp search
-    // and one candidate decode per lane, then (i, j) steps along the rows, and
-    // the 16 payload bytes of a row are read from LDS once for its candidates.
-    auto issue = [&](int ja, int jz) {
-        const uint32_t T0 = s_job_tb[ja], RB0 = s_job_rb[ja];
-        const int nt = (int)(s_job_tb[jz] - T0);
-        const int t0 = TASK_UNROLL * lane;
-        int a = ja, vp = 0, q = 0, row = 0, L = 0, src = 0, i = -1, j = 0;
-        if (t0 < nt) {
-            const uint32_t gt = T0 + (uint32_t)t0;
-            int b = jz - 1;  // the job holding task gt
-            while (a < b) {
-                const int m = (a + b + 1) >> 1;
-                if (s_job_tb[m] <= gt) a = m; else b = m - 1;
-            }
-            int lt = (int)(gt - s_job_tb[a]);
-            row = (int)(s_job_rb[a] - RB0);
-            vp = s_job_vp[a];
-            for (; q + 1 < s_job_nvp[a]; ++q) {
-                const int Lq = s_vp_len[vp];
-                const int tk = vp_tasks(Lq, Mm, Mf);
-                if (lt < tk) break;
-                lt -= tk;
-                row += Lq + 1;
-                ++vp;
-            }
-            L = s_vp_len[vp];
-            src = s_vp_src[vp];
-            vp_decode(lt, L, Mm, Mf, &i, &j);
-        }
-        int cur_ps = -1;
-        W16 rowb{0, 0, 0, 0};
-#pragma unroll
-        for (int u = 0; u < TASK_UNROLL; ++u) {
-            meta[u] = ~0u;
-            gen[u] = -2;
-            gw3[u] = 0;
-            W[u] = W16{0, 0, 0, 0};
-            if (t0 + u >= nt) continue;
-            if (u > 0) {  // the next candidate: (i, j + 1), else the next row / vp / job
-                ++j;
-                const int jmax = i < 0 ? (L < Mm ? L : Mm) : (L < i + Mf ? L : i + Mf);
-                if (j > jmax) {
-                    ++i;
-                    j = i + 1;
-                    if (i >= L) {  // past this vp's last row
-                        row += L + 1;
-                        if (q + 1 < s_job_nvp[a]) {
-                            ++q;
-                            ++vp;
-                        } else {
-                            ++a;
-                            q = 0;
-                            vp = s_job_vp[a];
-                        }
-                        L = s_vp_len[vp];
-                        src = s_vp_src[vp];
-                        i = -1;
-                        j = 0;
-                    }
-                }
-            }
-            // candidates start and end on char boundaries
-            if ((i > 0 && (bytes[src + i] & 0xC0u) == 0x80u) || (j < L && (bytes[src + j] & 0xC0u) == 0x80u))
-                continue;
-            const int ps = i < 0 ? 0 : i;
-            const int n = j - ps;
-            const uint32_t cont = i < 0 ? UC_META : UC_PIECE;
-            meta[u] = (uint32_t)(row + i + 1) | (uint32_t)(j - (i < 0 ? 0 : i + 1)) << 16 | (uint32_t)n << 22 |
-                      cont << 29;
-            if (n <= 16) {
-                if (src + ps != cur_ps) {
-                    cur_ps = src + ps;
-                    rowb = lds_w16(w32, cur_ps, 16);
-                }
-                W[u] = keep_bytes(rowb, n);
-                P[u] = probe_load(T, hash16(W[u], (uint32_t)n, cont));
-            } else {
-                gen[u] = probe_acc(T, [&](int x) -> uint32_t { return bytes[src + x]; }, ps, n, cont, &gw3[u]);
-            }
-        }
-    };
-    int j0 = 0, j1 = nj > 0 ? round_end(0) : 0;
-    if (nj > 0) issue(j0, j1);
-    while (j0 < nj) {
-#ifdef SDL_STAMPS
-        if (lane == 0) UNI_COUNT(4, 1);
-#endif
-        const uint32_t T0 = s_job_tb[j0], RB0 = s_job_rb[j0];
-#ifdef SDL_UNI_OLD_DP
-        for (int r = lane; r < (int)(s_job_rb[j1] - RB0); r += 64) s_rowmask[r] = 0u;
-        __syncthreads();
-#else
-        const int nt_round = (int)(s_job_tb[j1] - T0);
-        (void)RB0;
-#endif
-        // -- this round's probe results -> LDS --
-#pragma unroll
-        for (int u = 0; u < TASK_UNROLL; ++u) {
-#ifdef SDL_UNI_OLD_DP
-            if (meta[u] == ~0u) continue;
-#else
-            // every task of the round gets its word: the id, or NO_PIECE (no vocab piece, or
-            // a candidate that starts or ends inside a char)
-            const int t = TASK_UNROLL * lane + u;
-            if (t >= nt_round) continue;
-            if (meta[u] == ~0u) {
-                s_tid[t] = NO_PIECE;
-                continue;
-            }
-#endif
-            uint32_t w3 = gw3[u];
-            const uint32_t key = ((meta[u] >> 22) & 0x7Fu) | ((meta[u] >> 29) << 8);
-            const int id = gen[u] != -2 ? gen[u] : probe_result_w3(P[u], key, W[u], &w3);
-#ifdef SDL_UNI_OLD_DP
-            if (id < 0) continue;
-            const int t = TASK_UNROLL * lane + u;
-            s_tid[t] = (uint16_t)id;
-            s_tsc[t] = __uint_as_float(w3);  // the slot's f32 score, decoded with s_tid by uni_score64
-            atomicOr(&s_rowmask[meta[u] & 0xFFFFu], 1u << ((meta[u] >> 16) & 0x3Fu));
-#else
-            s_tid[t] = id < 0 ? NO_PIECE : (uint16_t)id;
-            s_tsc[t] = __uint_as_float(w3);  // the slot's f32 score, decoded with s_tid by uni_score64
-#endif
-        }
-        __syncthreads();
-        UNI_STAMP(6);
-        const int n0 = j1, n1 = n0 < nj ? round_end(n0) : n0;
-#ifndef SDL_UNI_NO_PIPE
-        if (n0 < nj) issue(n0, n1);  // the next round's probes fly during this DP
-#endif
-#ifndef SDL_UNI_OLD_DP
-        // -- DP: a 16-lane DPP row per job (4 jobs at a time), one Viterbi piece after the
-        //    other.  Lane gl of the row holds node p = gl + 1 -- "▁" and the payload's first
-        //    p bytes -- in registers: its score (f64) and back pointer.  Every candidate
-        //    ending at p is read from the round's results in LDS up front; the starts are
-        //    visited in order (S, then payload start 0, 1, ...), the base of payload start
-        //    i >= 1 is node i's score, which row_newbcast:(i - 1) hands to the whole row in
-        //    the same instruction stream -- no LDS node array, no per-start barrier.  Same
-        //    candidates, visit order, strict-> replacement and f64 sums as
-        //    unigram_viterbi_masked (unigram.hpp); the unk relaxation of a start whose
-        //    one-char piece is missing lands on the same node as that piece would, so it
-        //    takes the piece's slot.  Lane 0 of the row then backtracks with unk fusion. --
-        {
-            const int grp = lane >> 4, gl = lane & 15;
-            lds_u32 *gbp = (lds_u32 *)s_bp + grp * 17;  // p = 1..16 at gl, node 3 ("▁") at 16
-            auto wave_sync = [] {
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-            };
-            for (int jb = j0 + grp; jb < j1; jb += 4) {  // (row-uniform: all 16 lanes of a row together)
-                const int pi = s_job_pi[jb];
-                const int prel = (int)(s_pieces[pi] & 0xFFFu);
-                int toff = (int)(s_job_tb[jb] - T0);
-                int ktot = 0;
-                for (int q = 0; q < s_job_nvp[jb]; ++q) {
-                    const int vp = s_job_vp[jb] + q;
-                    const int L = s_vp_len[vp], src = s_vp_src[vp];
-                    const int c0 = vp_c0(L, Mm);
-                    const int p = gl + 1;
-                    const bool live = p <= L;
-                    // the char ending at p (if p is a char boundary) starts at payload byte qs
-                    const bool bnd = live && (p == L || (bytes[src + p] & 0xC0u) != 0x80u);
-                    int qs = p - 1;
-                    if (bnd)
-                        while (qs > 0 && (bytes[src + qs] & 0xC0u) == 0x80u) --qs;
-                    // node 3 (after "▁"): the "▁" piece (meta task 0), else its unk
-                    const uint32_t id3 = s_tid[toff];
-                    const double c3 = id3 != NO_PIECE ? uni_score64(s_tsc[toff], id3) : T.unk_score;
-                    const uint32_t bp3 = (id3 != NO_PIECE ? (id3 & UNI_ID_MASK) : (uint32_t)T.unk_id) << 16;
-                    // candidate (start, p): score (f64, -inf when none) and its id; the unk of a
-                    // start whose one-char piece is missing is no piece (Mm / Mf do not bound it)
-                    auto cand_sc = [&](bool piece_ok, int t, bool unk_ok, uint32_t *id) -> double {
-                        const uint32_t x = piece_ok ? s_tid[toff + t] : NO_PIECE;  // (t < the vp's tasks then)
-                        if (x != NO_PIECE) {
-                            *id = x & UNI_ID_MASK;
-                            return uni_score64(s_tsc[toff + t], x);
-                        }
-                        *id = (uint32_t)T.unk_id;
-                        return unk_ok ? T.unk_score : -__builtin_inf();
-                    };
-                    uint32_t cid;
-                    // start S (base 0.0): the meta piece "▁" + payload[0, p)
-                    double best = cand_sc(live && p <= Mm, live ? p : 0, false, &cid) + 0.0;
-                    uint32_t bp = best > -__builtin_inf() ? cid << 16 : 0xFFFFFFFFu;
-                    {  // payload start 0 (node 3, base c3)
-                        const double c = cand_sc(live && p <= Mf, live ? c0 + p - 1 : 0, bnd && qs == 0, &cid) + c3;
-                        const bool up = c > best;
-                        best = up ? c : best;
-                        bp = up ? (3u | cid << 16) : bp;
-                    }
-                    static_for<1, UNI_WMAX>([&](auto ic) {  // payload start i (node 3 + i = lane i - 1)
-                        constexpr int i = decltype(ic)::value;
-                        const double base = row_bcast_f64<i - 1>(best);
-                        const bool valid = live && i < p && p - i <= Mf;
-                        const int t = valid ? c0 + vp_rowoff(i, L, Mf) + (p - i - 1) : 0;
-                        const double c = cand_sc(valid, t, bnd && qs == i, &cid) + base;
-                        const bool up = c > best;
-                        best = up ? c : best;
-                        bp = up ? ((uint32_t)(3 + i) | cid << 16) : bp;
-                    });
-                    gbp[gl] = bp;
-                    if (gl == 0) gbp[16] = bp3;
-                    wave_sync();
-                    if (gl == 0) {
-                        struct {
-                            lds_u32 *bp;
-                            __device__ uint32_t at(int x) const { return x == 3 ? bp[16] : bp[x - 4]; }
-                            __device__ int start(int x) const { return at(x) == 0xFFFFFFFFu ? -1 : (int)(at(x) & 0xFFFFu); }
-                            __device__ int id(int x) const { return at(x) == 0xFFFFFFFFu ? -1 : (int)(at(x) >> 16); }
-                        } gnodes{gbp};
-                        auto cand = [&](int st, int e, double *sc) -> int {  // the fused-unk lookup
-                            const int loc = vp_local(st == 0 ? -1 : st - 3, e - 3, L, Mm, Mf);
-                            if (loc < 0 || s_tid[toff + loc] == NO_PIECE) return -1;
-                            *sc = uni_score64(s_tsc[toff + loc], s_tid[toff + loc]);
-                            return (int)(s_tid[toff + loc] & UNI_ID_MASK);
-                        };
-                        const int base = ktot;
-                        ktot += unigram_backtrack(L + 3, cand, gnodes, T.unk_id,
-                                                  [&](int x, int id) { stage[prel + base + x] = (uint16_t)id; });
-                    }
-                    wave_sync();  // (the row's back pointers are rewritten for the next piece)
-                    toff += vp_tasks(L, Mm, Mf);
-                }
-                if (gl == 0) cnt[pi] = (uint8_t)ktot;
-            }
-        }
-#else
-        // -- DP: a group of DPG lanes per job.  Starts are visited in order; the
-        //    candidates of one start end at distinct nodes, so the group's lanes
-        //    relax them together (same visit order and strict-> replacement as
-        //    unigram_viterbi_masked), then lane 0 of the group backtracks.  The
-        //    groups' loops diverge; lanes of a group meet through LDS in program
-        //    order (wave_sync: one wave per block) --
-        {
-            const int grp = lane / DPG, gl = lane % DPG;
-            lds_f64 *gsc = (lds_f64 *)s_u + grp * UNI_NODES;
-            lds_u32 *gbp = (lds_u32 *)(s_u + (64 / DPG) * UNI_NODES * 8) + grp * UNI_NODES;
-            // (A wavefront-scope fence -- enough for one wave's LDS, which executes
-            // in program order -- measured 1% slower than this workgroup fence.)
-            auto wave_sync = [] {
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-            };
-#if defined(SDL_ABLATE_UNI)
-            for (int jb = j1; jb < j1; jb += 64 / DPG) {
-#else
-            for (int jb = j0 + grp; jb < j1; jb += 64 / DPG) {
-#endif
-                const int pi = s_job_pi[jb];
-                const int prel = (int)(s_pieces[pi] & 0xFFFu);
-                int toff = (int)(s_job_tb[jb] - T0);
-                int roff = (int)(s_job_rb[jb] - RB0);
-                int ktot = 0;
-                for (int q = 0; q < s_job_nvp[jb]; ++q) {
-                    const int vp = s_job_vp[jb] + q;
-                    const int L = s_vp_len[vp], src = s_vp_src[vp];
-                    const int n = L + 3;  // "▁" + payload
-                    auto acc = [&](int x) -> uint32_t { return x < 3 ? meta_byte(x) : (uint32_t)bytes[src + x - 3]; };
-                    auto rowmask = [&](int st) -> uint32_t { return s_rowmask[roff + (st == 0 ? 0 : st - 2)]; };
-                    // (unreached nodes at -inf: every candidate beats them; a start
-                    // is always reached -- by its char's [UNK] at least -- before it
-                    // is visited)
-                    for (int x = gl; x <= n; x += DPG) {
-                        gsc[x] = x == 0 ? 0.0 : -__builtin_inf();
-                        gbp[x] = 0xFFFFFFFFu;
-                    }
-                    wave_sync();
-                    for (int st = 0; st < n;) {
-                        const int l0 = u8len_lead(acc(st));
-                        const int mb = l0 < n - st ? l0 : n - st;
-                        const double base = gsc[st];
-                        const int fe = st == 0 ? 3 : st + 1;
-                        const uint32_t m = rowmask(st);
-                        const bool single = (m >> (st + mb - fe)) & 1u;
-                        // the start's candidates are consecutive tasks: candidate k
-                        // (ending at fe + k) is task rb + k
-                        const int rb = toff + (st == 0 ? 0 : vp_c0(L, Mm) + vp_rowoff(st - 3, L, Mf));
-                        int k = gl;
-                        for (uint32_t mm = m >> gl; mm; mm >>= DPG, k += DPG) {
-                            if (!(mm & 1u)) continue;
-                            const int e = fe + k;
-                            const uint32_t id16 = s_tid[rb + k];
-                            const double c = uni_score64(s_tsc[rb + k], id16) + base;
-                            if (c > gsc[e]) {
-                                gsc[e] = c;
-                                gbp[e] = (uint32_t)st | ((id16 & UNI_ID_MASK) << 16);
-                            }
-                        }
-                        if (!single && gl == DPG - 1) {  // unk: ends where no piece candidate does
-                            const double c = T.unk_score + base;
-                            const int e = st + mb;
-                            if (c > gsc[e]) {
-                                gsc[e] = c;
-                                gbp[e] = (uint32_t)st | ((uint32_t)T.unk_id << 16);
-                            }
-                        }
-                        wave_sync();
-                        st += mb;
-                    }
-                    if (gl == 0) {
-                        struct {
-                            lds_u32 *bp;
-                            __device__ int start(int x) const { return bp[x] == 0xFFFFFFFFu ? -1 : (int)(bp[x] & 0xFFFFu); }
-                            __device__ int id(int x) const { return bp[x] == 0xFFFFFFFFu ? -1 : (int)(bp[x] >> 16); }
-                        } gnodes{gbp};
-                        auto cand = [&](int st, int e, double *sc) -> int {  // the fused-unk lookup
-                            const int loc = vp_local(st == 0 ? -1 : st - 3, e - 3, L, Mm, Mf);
-                            if (loc < 0 || !((rowmask(st) >> (e - (st == 0 ? 3 : st + 1))) & 1u)) return -1;
-                            *sc = uni_score64(s_tsc[toff + loc], s_tid[toff + loc]);
-                            return (int)(s_tid[toff + loc] & UNI_ID_MASK);
-                        };
-                        const int base = ktot;
-                        ktot += unigram_backtrack(n, cand, gnodes, T.unk_id,
-                                                  [&](int x, int id) { stage[prel + base + x] = (uint16_t)id; });
-                    }
-                    wave_sync();  // the nodes are re-initialised for the next piece
-                    toff += vp_tasks(L, Mm, Mf);
-                    roff += L + 1;
-                }
-                if (gl == 0) cnt[pi] = (uint8_t)ktot;
-            }
-        }
-#endif
-        __syncthreads();
-        UNI_STAMP(7);
-        j0 = n0;
-        j1 = n1;
-#ifdef SDL_UNI_NO_PIPE
-        if (j0 < nj) issue(j0, j1);  // (diagnostic) the next round's probes after this DP
-#endif
-    }
-
-    UNI_STAMP(4);
-    // ---- 6. compact ids into this chunk's tokc slice; list the long items -------
+    // ---- 4. compact ids into this chunk's tokc slice; hand the Viterbi pieces to
+    //         k_unigram_viterbi; list the long items --------------------------------
+    auto ents = [](uint32_t c) -> uint32_t { return c == CNT_LONG ? 1u : (c & CNT_JOB) ? (c & 0x7Fu) : c; };
     const int per = (np + TOK_THREADS - 1) / TOK_THREADS;
     const int a0 = tid * per < np ? tid * per : np;
     const int a1 = a0 + per < np ? a0 + per : np;
-    uint32_t mine = 0;
-    for (int i = a0; i < a1; ++i) mine += s_cnt[i] == CNT_LONG ? 1u : s_cnt[i];
-    uint32_t total;
+    uint32_t mine = 0, myjobs = 0;
+    for (int i = a0; i < a1; ++i) {
+        const uint32_t c = s_cnt[i];
+        mine += ents(c);
+        myjobs += c != CNT_LONG && (c & CNT_JOB) ? (c & 0x7Fu) : 0u;
+    }
+    uint32_t total, njobs;
     uint32_t base = block_excl_sum<TOK_THREADS>(mine, &total, s_scratch + 8);
+    uint32_t jb = block_excl_sum<TOK_THREADS>(myjobs, &njobs, s_scratch + 8);
     uint32_t *dst = tokc + ci * UNI_STAGE;
     const uint32_t base0 = base;
+    // jobs: payload (<= UNI_WMAX bytes from the window or the arena) and meta = length |
+    // stage position of its ids << 5 | list entry << 17; a word's pieces' ids follow each
+    // other from its stage slot, each piece bounded by its chars + 1
+    for (int i = a0; i < a1; ++i) {
+        const uint32_t c = s_cnt[i];
+        if (c == CNT_LONG || !(c & CNT_JOB)) {
+            base += ents(c);
+            continue;
+        }
+        const int prel = s_pieces[i] & 0xFFF;
+        const int vp0 = s_stage[prel];
+        int pos = prel;
+        for (uint32_t q = 0; q < (c & 0x7Fu); ++q, ++base, ++jb) {
+            const int L = s_vp_len[vp0 + q];
+            const W16 w = lds_w16(w32, s_vp_src[vp0 + q], L);
+            *reinterpret_cast<uint4 *>(dst + UNI_JP_OFF + 4 * jb) = make_uint4(w.x, w.y, w.z, w.w);
+            dst[UNI_JM_OFF + jb] = (uint32_t)L | (uint32_t)pos << 5 | base << 17;
+            auto conts = [](uint32_t x) { return __builtin_popcount(x & ~(x << 1) & 0x80808080u); };
+            pos += L - (conts(w.x) + conts(w.y) + conts(w.z) + conts(w.w)) + 1;
+        }
+    }
+    if (tid == 0) dst[UNI_JN_OFF] = njobs;
+#ifdef SDL_STAMPS
+    if (tid == 0) {
+        UNI_COUNT(0, 1);
+        UNI_COUNT(1, np);
+        UNI_COUNT(2, njobs);
+        UNI_COUNT(6, s_scratch[3]);
+    }
+#endif
+    __syncthreads();  // (the payloads are read before the list is packed over the window)
+    base = base0;
     // the list is packed in LDS first (window and arena are dead now) and
     // written as whole 16-B lanes: scattered 4-B non-temporal stores cost ~3x
     // the list's bytes in HBM writes
@@ -1399,8 +1014,8 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
     lds_u32 *pk = (lds_u32 *)s_bytes;
     for (int i = a0; i < a1; ++i) {
         const int prel = s_pieces[i] & 0xFFF;
-        const int k = s_cnt[i];
-        if (k == CNT_LONG) {
+        const uint32_t c = s_cnt[i];
+        if (c == CNT_LONG) {
             const uint32_t it = atomicAdd(&counters[0], 1u);
             if (it < item_cap) items[it] = make_uint4((uint32_t)ci, base, (uint32_t)prel, s_stage[prel]);
             else atomicOr(err, 8u);
@@ -1409,10 +1024,16 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
             ++base;
             continue;
         }
-        if (packed) {
-            for (int j = 0; j < k; ++j) pk[base + j] = (uint32_t)s_stage[prel + j];
+        const uint32_t k = ents(c);
+        if (c & CNT_JOB) {  // placeholders: k_unigram_viterbi writes the entries
+            for (uint32_t j = 0; j < k; ++j) {
+                if (packed) pk[base + j] = LMARK | UNI_JOB_BIT;
+                else dst[base + j] = LMARK | UNI_JOB_BIT;
+            }
+        } else if (packed) {
+            for (uint32_t j = 0; j < k; ++j) pk[base + j] = (uint32_t)s_stage[prel + j];
         } else {
-            for (int j = 0; j < k; ++j) __builtin_nontemporal_store((uint32_t)s_stage[prel + j], dst + base + j);
+            for (uint32_t j = 0; j < k; ++j) __builtin_nontemporal_store((uint32_t)s_stage[prel + j], dst + base + j);
         }
         base += k;
     }
@@ -1432,7 +1053,7 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
     base = base0;
     for (int i = a0; i < a1; ++i) {
         s_poff[i] = (uint16_t)base;
-        base += s_cnt[i] == CNT_LONG ? 1u : s_cnt[i];
+        base += ents(s_cnt[i]);
     }
     __syncthreads();
     if (tid == 0) chunk_cnt[ci] = chunk_ent[ci] = total;
@@ -1451,6 +1072,259 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
         rec_local[ra + k] = lo < np ? (uint32_t)s_poff[lo] : total;
     }
     UNI_STAMP(5);
+}
+
+// ---------------------------------------------------------------------------
+// k_unigram_viterbi: the Viterbi of every job the chunk kernel handed over -- word-table
+// misses and medium words' pieces, "▁" + a payload of <= UNI_WMAX bytes -- one wave per
+// chunk, the chunk's jobs in passes (its next jobs whose candidates fit VTCAP, <= VJP):
+//   - candidate probes: every (start, end) candidate of every job of the pass is one task,
+//     VU consecutive tasks a lane with all VU probes in flight; each task's exact f64 score
+//     (-inf: no piece there) and id land in LDS at the task's index;
+//   - DP, a lane per job, the nodes' f64 scores and back pointers in registers: the starts
+//     ("▁", then payload bytes 0 .. 15) and their candidates' ends are compile-time loops,
+//     so a node is a register and a candidate is one LDS load (its row's task base + end)
+//     and a compare -- unigram_viterbi's visit order (starts, then ends ascending, then the
+//     start's unk when no one-char piece starts there), strict-> and f64 sums;
+//   - backtrack with unk fusion (a fused run is probed whole) from the back pointers in LDS;
+//     the ids go to the chunk's results region at the job's stage position and its list
+//     entry becomes LMARK | UNI_JOB_BIT | k << 24 | pos (k_compact_tokens expands it).
+// Then the chunk's id count and its records' local offsets grow by the jobs' k - 1.
+#ifndef SDL_UNI_VWAVES
+#define SDL_UNI_VWAVES 3
+#endif
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDL_UNI_VWAVES, 8))) void k_unigram_viterbi(DevTok T, int64_t N, const uint64_t *__restrict__ off,
+                                                        int64_t R, const uint32_t *__restrict__ ranges,
+                                                        uint32_t *__restrict__ tokc, uint32_t *__restrict__ chunk_cnt,
+                                                        uint32_t *__restrict__ rec_local) {
+    __shared__ __attribute__((aligned(16))) uint8_t s_pb[VP_CAP * 16 + 16];  // payloads (+ lds_w16's 5th dword)
+    __shared__ uint32_t s_jm[VP_CAP];      // metas: L | pos << 5 | entry << 17
+    __shared__ uint16_t s_tb[VP_CAP + 1];  // task base of each job
+    __shared__ uint8_t s_k[VP_CAP];        // ids of each job
+    __shared__ double s_sc[VTCAP];         // per task of the pass: the candidate's score, -inf: no piece
+    __shared__ uint16_t s_id[VTCAP];       // ... its id
+    // after the DP: back pointers [node][lane], start node << 11 | task (UNK_T: unk); 0xFFFF: unset
+    uint16_t *const s_bp = reinterpret_cast<uint16_t *>(s_sc);
+    static_assert(UNI_NODES * 64 * 2 <= VTCAP * 8, "the back pointers fit the scores' LDS");
+    constexpr uint32_t UNK_T = 0x7FFu;
+    const int lane = lane_id();
+    const int64_t c = blockIdx.x;
+    uint32_t *const slice = tokc + c * UNI_STAGE;
+#ifdef SDL_STAMPS
+    unsigned long long vstamp_ = __builtin_amdgcn_s_memtime();
+#endif
+    const uint32_t nj = slice[UNI_JN_OFF];
+    if (nj == 0) return;
+    const int Mm = T.maxlen_meta, Mf = T.maxlen_first;
+    const int njobs = (int)(nj < (uint32_t)VP_CAP ? nj : (uint32_t)VP_CAP);
+    for (int v = lane; v < njobs; v += 64) {
+        *reinterpret_cast<uint4 *>(s_pb + 16 * v) = *reinterpret_cast<const uint4 *>(slice + UNI_JP_OFF + 4 * v);
+        s_jm[v] = slice[UNI_JM_OFF + v];
+    }
+    if (lane < 4) reinterpret_cast<uint32_t *>(s_pb + 16 * VP_CAP)[lane] = 0u;
+    __syncthreads();
+    {
+        uint32_t carry = 0;
+        for (int v0 = 0; v0 < njobs; v0 += 64) {
+            const int v = v0 + lane;
+            const uint32_t t = v < njobs ? (uint32_t)vp_tasks((int)(s_jm[v] & 31u), Mm, Mf) : 0u;
+            const uint32_t incl = wave_incl_sum(t);
+            if (v < njobs) s_tb[v] = (uint16_t)(carry + incl - t);
+            carry += (uint32_t)lane_bcast((int)incl, 63);
+        }
+        if (lane == 0) s_tb[njobs] = (uint16_t)carry;
+#ifdef SDL_STAMPS
+        if (lane == 0) UNI_COUNT(3, carry);
+#endif
+    }
+    __syncthreads();
+    const lds_u8 *pb = (const lds_u8 *)s_pb;
+    const lds_u32 *pb32 = (const lds_u32 *)s_pb;
+    VIT_STAMP(1);
+    for (int a = 0; a < njobs;) {
+        int b = a + 1;  // the pass: jobs [a, b)
+        while (b < njobs && b - a < VJP && (int)s_tb[b + 1] - (int)s_tb[a] <= VTCAP) ++b;
+        const int T0 = s_tb[a], TZ = s_tb[b];
+        for (int r0 = T0; r0 < TZ; r0 += 64 * VU) {
+            Probe P[VU];
+            W16 W[VU];
+            uint32_t meta[VU];  // n | cont << 8; ~0u: no probe
+            const int t0 = r0 + VU * lane;
+            int jv = a, i = -1, j = 0, L = 0;
+            if (t0 < TZ) {
+                int lo = a, hi = b - 1;  // the job holding task t0
+                while (lo < hi) {
+                    const int m = (lo + hi + 1) >> 1;
+                    if ((int)s_tb[m] <= t0) lo = m; else hi = m - 1;
+                }
+                jv = lo;
+                L = (int)(s_jm[jv] & 31u);
+                vp_decode(t0 - (int)s_tb[jv], L, Mm, Mf, &i, &j);
+            }
+            int cur_ps = -1;
+            W16 rowb{0, 0, 0, 0};
+#pragma unroll
+            for (int u = 0; u < VU; ++u) {
+                meta[u] = ~0u;
+                W[u] = W16{0, 0, 0, 0};
+                if (t0 + u >= TZ) continue;
+                if (u > 0) {  // the next candidate: (i, j + 1), else the next row / job
+                    ++j;
+                    const int jmax = i < 0 ? (L < Mm ? L : Mm) : (L < i + Mf ? L : i + Mf);
+                    if (j > jmax) {
+                        ++i;
+                        j = i + 1;
+                        if (i >= L) {
+                            ++jv;
+                            L = (int)(s_jm[jv] & 31u);
+                            i = -1;
+                            j = 0;
+                        }
+                    }
+                }
+                const int src = 16 * jv;
+                // candidates start and end on char boundaries
+                if ((i > 0 && (pb[src + i] & 0xC0u) == 0x80u) || (j < L && (pb[src + j] & 0xC0u) == 0x80u)) continue;
+                const int ps = i < 0 ? 0 : i;
+                const int n = j - ps;
+                const uint32_t cont = i < 0 ? UC_META : UC_PIECE;
+                if (src + ps != cur_ps) {
+                    cur_ps = src + ps;
+                    rowb = lds_w16(pb32, cur_ps, 16);
+                }
+                W[u] = keep_bytes(rowb, n);
+                P[u] = probe_load(T, hash16(W[u], (uint32_t)n, cont));
+                meta[u] = (uint32_t)n | cont << 8;
+            }
+#pragma unroll
+            for (int u = 0; u < VU; ++u) {
+                const int t = t0 + u;
+                if (t >= TZ) continue;
+                double sc = -__builtin_inf();
+                if (meta[u] != ~0u) {
+                    uint32_t w3;
+                    const int id = probe_result_w3(P[u], meta[u], W[u], &w3);
+                    if (id >= 0) {
+                        sc = uni_score64(__uint_as_float(w3), (uint32_t)id);
+                        s_id[t - T0] = (uint16_t)((uint32_t)id & UNI_ID_MASK);
+                    }
+                }
+                s_sc[t - T0] = sc;
+            }
+        }
+        __syncthreads();
+        VIT_STAMP(2);
+        // -- DP: a lane per job --
+        const bool act = lane < b - a;
+        const int v = act ? a + lane : a;
+        const uint32_t jm = act ? s_jm[v] : 0u;
+        const int L = (int)(jm & 31u), n = L + 3;
+        uint32_t lm = 1u << L;  // the pass's longest payload (wave-uniform bound of the loops)
+#pragma unroll
+        for (int k = 1; k < 64; k <<= 1) lm |= (uint32_t)__shfl_xor((int)lm, k);
+        const int Lmax = 31 - __builtin_clz(lm);
+        const uint4 pw = *reinterpret_cast<const uint4 *>(s_pb + 16 * v);
+        const int tj = (int)s_tb[v] - T0;  // the job's first task in the pass
+        const int c0 = vp_c0(L, Mm);
+        double best[UNI_NODES];
+        uint32_t bp[UNI_NODES];  // start node << 11 | task (UNK_T: unk); 0xFFFF: unset
+        static_for<0, UNI_NODES>([&](auto X) {
+            best[X] = -__builtin_inf();
+            bp[X] = 0xFFFFu;
+        });
+        auto relax = [&](auto E, double cc, uint32_t bb) {
+            const bool up = cc > best[E];
+            best[E] = up ? cc : best[E];
+            bp[E] = up ? bb : bp[E];
+        };
+        {  // start 0: "▁" + payload[0, j), j = 0 .. min(L, Mm) = tasks tj + j, ending at node 3 + j
+            const int jz = L < Mm ? L : Mm;
+            static_for<0, UNI_WMAX + 1>([&](auto J) {
+                constexpr int jj = decltype(J)::value;
+                if (jj <= Lmax && act && jj <= jz) relax(std::integral_constant<int, 3 + jj>{}, s_sc[tj + jj],
+                                                          (uint32_t)(tj + jj));
+            });
+            // the "▁" char's unk when "▁" is no piece
+            if (act && !(s_sc[tj] > -__builtin_inf())) relax(std::integral_constant<int, 3>{}, T.unk_score, UNK_T);
+        }
+        static_for<0, UNI_WMAX>([&](auto I) {  // payload start i = node 3 + i
+            constexpr int i = decltype(I)::value, st = 3 + i;
+            if (i < Lmax) {
+                const uint32_t by = ((i < 4 ? pw.x : i < 8 ? pw.y : i < 12 ? pw.z : pw.w) >> (8 * (i & 3))) & 0xFFu;
+                const bool on = act && i < L && (i == 0 || (by & 0xC0u) != 0x80u);
+                const double base = best[st];
+                const int rlen = L - i < Mf ? L - i : Mf;
+                const int rb = tj + c0 + vp_rowoff(i, L, Mf);
+                static_for<1, UNI_WMAX - i + 1>([&](auto D) {
+                    constexpr int d = decltype(D)::value;
+                    if (on && d <= rlen)
+                        relax(std::integral_constant<int, st + d>{}, s_sc[rb + d - 1] + base,
+                              (uint32_t)st << 11 | (uint32_t)(rb + d - 1));
+                });
+                const int l0 = u8len_lead(by), mb = l0 < L - i ? l0 : L - i;
+                if (on && !(mb <= rlen && s_sc[rb + mb - 1] > -__builtin_inf())) {  // unk: no one-char piece
+                    static_for<1, 5>([&](auto M) {
+                        constexpr int m = decltype(M)::value;
+                        if constexpr (st + m < UNI_NODES)
+                            if (mb == m) relax(std::integral_constant<int, st + m>{}, T.unk_score + base,
+                                               (uint32_t)st << 11 | UNK_T);
+                    });
+                }
+            }
+        });
+        // -- backtrack (the back pointers to LDS: the scores are dead) --
+        static_for<0, UNI_NODES>([&](auto X) { s_bp[X * 64 + lane] = (uint16_t)bp[X]; });
+        VIT_STAMP(3);
+        if (act) {
+            struct {
+                const uint16_t *bp;
+                const uint16_t *id16;
+                int lane, unk;
+                __device__ int start(int x) const {
+                    const uint32_t b = bp[x * 64 + lane];
+                    return b == 0xFFFFu ? -1 : (int)(b >> 11);
+                }
+                __device__ int id(int x) const {
+                    const uint32_t b = bp[x * 64 + lane];
+                    return b == 0xFFFFu ? -1 : (b & 0x7FFu) == UNK_T ? unk : (int)id16[b & 0x7FFu];
+                }
+            } nodes{s_bp, s_id, lane, T.unk_id};
+            auto acc = [&](int x) -> uint32_t { return x < 3 ? meta_byte(x) : (uint32_t)pb[16 * v + x - 3]; };
+            auto cand = [&](int st2, int e2, double *) -> int {  // the fused-unk lookup
+                int id;
+                if (st2 == 0) id = e2 - 3 <= Mm ? probe_acc(T, acc, 3, e2 - 3, UC_META) : -1;
+                else id = e2 - st2 <= Mf ? probe_acc(T, acc, st2, e2 - st2, UC_PIECE) : -1;
+                return uni_piece_id(id);
+            };
+            const uint32_t pos = (jm >> 5) & 0xFFFu;
+            uint16_t *const jr = reinterpret_cast<uint16_t *>(slice + UNI_JR_OFF) + pos;
+            const int k = unigram_backtrack(n, cand, nodes, T.unk_id, [&](int x, int id) { jr[x] = (uint16_t)id; });
+            slice[jm >> 17] = LMARK | UNI_JOB_BIT | (uint32_t)k << 24 | pos;
+            s_k[v] = (uint8_t)k;
+        }
+#ifdef SDL_STAMPS
+        if (lane == 0) UNI_COUNT(4, 1);
+#endif
+        __syncthreads();
+        VIT_STAMP(4);
+        a = b;
+    }
+    // the chunk's id count and its records' local offsets: + (k - 1) of every job before them
+    uint32_t ext = 0;
+    for (int v = lane; v < njobs; v += 64) ext += (uint32_t)s_k[v] - 1u;
+    ext = (uint32_t)lane_bcast((int)wave_incl_sum(ext), 63);
+    if (lane == 0 && ext) atomicAdd(&chunk_cnt[c], ext);
+    const int64_t c0 = c * CHUNK, c1 = c0 + CHUNK < N ? c0 + CHUNK : N;
+    for (int64_t r = ranges[3 * c + 2]; r <= R; ++r) {
+        const int64_t p = (int64_t)off[r];
+        if (p >= c1) break;
+        uint32_t add = 0;
+        for (int v = lane; v < njobs; v += 64)
+            if ((int64_t)((s_jm[v] >> 5) & 0xFFFu) < p - c0) add += (uint32_t)s_k[v] - 1u;
+        add = (uint32_t)lane_bcast((int)wave_incl_sum(add), 63);
+        if (lane == 0 && add) atomicAdd(&rec_local[r], add);
+    }
+    VIT_STAMP(5);
 }
 
 namespace {
@@ -1816,6 +1690,8 @@ hipError_t launch_unigram_chunks(const DevTok &T, const uint8_t *text, int64_t N
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_unigram_chunks, dim3((unsigned)n_chunks), dim3(TOK_THREADS), 0, st, T, text, N, off, R, ranges,
                        tokc, chunk_cnt, chunk_ent, rec_local, W.counters, W.items, W.item_cap, W.err);
+    hipLaunchKernelGGL(k_unigram_viterbi, dim3((unsigned)n_chunks), dim3(64), 0, st, T, N, off, R, ranges, tokc,
+                       chunk_cnt, rec_local);
     // a row's candidate ends: <= Mm + 1 ("▁" row) or <= Mf.  Two stages: items of <= 128
     // normalized bytes (nearly all) with a small LDS footprint and more of them in
     // flight, then the rest (<= 512) from the first stage's overflow list.

@@ -145,3 +145,6 @@ def test_bench_spawn_path_reports_one_gpu(native_lib):
     assert p.returncode == 0, p.stderr[-3000:]
     d = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
     assert d["n_gpus"] == 1 and d["value"] > 0 and d["errors"] == {"tokenize": 0, "label": 0}
+    # the held-out leg rides along with a fixture run, beside `value`
+    h = d["heldout"]
+    assert h["value"] > 0 and h["errors"] == {"tokenize": 0, "label": 0} and h["roofline"]["avg_launch_ms"] > 0
