@@ -108,7 +108,14 @@ __device__ __forceinline__ void compact_wave(int64_t cb, const uint32_t *__restr
                 } else if (long_pool && (x[j] & UNI_JOB_BIT)) {  // unigram Viterbi job
                     const uint16_t *jr = reinterpret_cast<const uint16_t *>(tokc + (cb + j) * stride + UNI_JR_OFF) +
                                          (x[j] & 0xFFFu);
-                    for (uint32_t q = 0; q < w[j]; ++q) dst[at + q] = jr[q];
+                    for (uint32_t q0 = 0; q0 < w[j]; q0 += 8) {  // (8 loads in flight, then 8 stores)
+                        uint32_t id[8];
+#pragma unroll
+                        for (uint32_t r = 0; r < 8; ++r) id[r] = q0 + r < w[j] ? jr[q0 + r] : 0u;
+#pragma unroll
+                        for (uint32_t r = 0; r < 8; ++r)
+                            if (q0 + r < w[j]) dst[at + q0 + r] = id[r];
+                    }
                 } else if (long_pool) {  // unigram long item: [k, ids...] in the pool
                     const uint32_t po = x[j] & 0x7FFFFFFFu;
                     for (uint32_t q = 0; q < w[j]; ++q) dst[at + q] = long_pool[po + 1 + q];

@@ -1101,6 +1101,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDL_UNI_VWAV
     __shared__ uint32_t s_jm[VP_CAP];      // metas: L | pos << 5 | entry << 17
     __shared__ uint16_t s_tb[VP_CAP + 1];  // task base of each job
     __shared__ uint8_t s_k[VP_CAP];        // ids of each job
+    __shared__ uint16_t s_cm[VP_CAP];      // bit x: payload byte x continues a char
     __shared__ double s_sc[VTCAP];         // per task of the pass: the candidate's score, -inf: no piece
     __shared__ uint16_t s_id[VTCAP];       // ... its id
     // after the DP: back pointers [node][lane], start node << 11 | task (UNK_T: unk); 0xFFFF: unset
@@ -1118,8 +1119,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDL_UNI_VWAV
     const int Mm = T.maxlen_meta, Mf = T.maxlen_first;
     const int njobs = (int)(nj < (uint32_t)VP_CAP ? nj : (uint32_t)VP_CAP);
     for (int v = lane; v < njobs; v += 64) {
-        *reinterpret_cast<uint4 *>(s_pb + 16 * v) = *reinterpret_cast<const uint4 *>(slice + UNI_JP_OFF + 4 * v);
+        const uint4 p = *reinterpret_cast<const uint4 *>(slice + UNI_JP_OFF + 4 * v);
+        *reinterpret_cast<uint4 *>(s_pb + 16 * v) = p;
         s_jm[v] = slice[UNI_JM_OFF + v];
+        auto cb = [](uint32_t x) { return gather4(x & ~(x << 1) & B7); };  // 10xxxxxx bytes
+        s_cm[v] = (uint16_t)(cb(p.x) | cb(p.y) << 4 | cb(p.z) << 8 | cb(p.w) << 12);
     }
     if (lane < 4) reinterpret_cast<uint32_t *>(s_pb + 16 * VP_CAP)[lane] = 0u;
     __syncthreads();
@@ -1145,51 +1149,56 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDL_UNI_VWAV
         int b = a + 1;  // the pass: jobs [a, b)
         while (b < njobs && b - a < VJP && (int)s_tb[b + 1] - (int)s_tb[a] <= VTCAP) ++b;
         const int T0 = s_tb[a], TZ = s_tb[b];
-        for (int r0 = T0; r0 < TZ; r0 += 64 * VU) {
+        {  // lane l takes the pass's tasks [T0 + l K, T0 + (l + 1) K) in rounds of VU: one
+        // decode per pass, then (i, j) steps along the rows; a row's 16 bytes are read once
+        const int K = (TZ - T0 + 63) >> 6;
+        const int tl0 = T0 + lane * K, tl1 = tl0 + K < TZ ? tl0 + K : TZ;
+        int jv = a, i = -1, j = -1, L = 0;
+        uint32_t cm = 0;  // the job's continuation-byte mask
+        if (tl0 < tl1) {
+            int lo = a, hi = b - 1;  // the job holding task tl0
+            while (lo < hi) {
+                const int m = (lo + hi + 1) >> 1;
+                if ((int)s_tb[m] <= tl0) lo = m; else hi = m - 1;
+            }
+            jv = lo;
+            L = (int)(s_jm[jv] & 31u);
+            cm = s_cm[jv];
+            vp_decode(tl0 - (int)s_tb[jv], L, Mm, Mf, &i, &j);
+            --j;  // (the first step lands on it)
+        }
+        int cur_ps = -1;
+        W16 rowb{0, 0, 0, 0};
+        for (int r0 = tl0; r0 < tl0 + K; r0 += VU) {  // (K is wave-uniform)
             Probe P[VU];
             W16 W[VU];
             uint32_t meta[VU];  // n | cont << 8; ~0u: no probe
-            const int t0 = r0 + VU * lane;
-            int jv = a, i = -1, j = 0, L = 0;
-            if (t0 < TZ) {
-                int lo = a, hi = b - 1;  // the job holding task t0
-                while (lo < hi) {
-                    const int m = (lo + hi + 1) >> 1;
-                    if ((int)s_tb[m] <= t0) lo = m; else hi = m - 1;
-                }
-                jv = lo;
-                L = (int)(s_jm[jv] & 31u);
-                vp_decode(t0 - (int)s_tb[jv], L, Mm, Mf, &i, &j);
-            }
-            int cur_ps = -1;
-            W16 rowb{0, 0, 0, 0};
 #pragma unroll
             for (int u = 0; u < VU; ++u) {
                 meta[u] = ~0u;
                 W[u] = W16{0, 0, 0, 0};
-                if (t0 + u >= TZ) continue;
-                if (u > 0) {  // the next candidate: (i, j + 1), else the next row / job
-                    ++j;
-                    const int jmax = i < 0 ? (L < Mm ? L : Mm) : (L < i + Mf ? L : i + Mf);
-                    if (j > jmax) {
-                        ++i;
-                        j = i + 1;
-                        if (i >= L) {
-                            ++jv;
-                            L = (int)(s_jm[jv] & 31u);
-                            i = -1;
-                            j = 0;
-                        }
+                if (r0 + u >= tl1) continue;
+                // the next candidate: (i, j + 1), else the next row / job
+                ++j;
+                const int jmax = i < 0 ? (L < Mm ? L : Mm) : (L < i + Mf ? L : i + Mf);
+                if (j > jmax) {
+                    ++i;
+                    j = i + 1;
+                    if (i >= L) {
+                        ++jv;
+                        L = (int)(s_jm[jv] & 31u);
+                        cm = s_cm[jv];
+                        i = -1;
+                        j = 0;
                     }
                 }
-                const int src = 16 * jv;
                 // candidates start and end on char boundaries
-                if ((i > 0 && (pb[src + i] & 0xC0u) == 0x80u) || (j < L && (pb[src + j] & 0xC0u) == 0x80u)) continue;
+                if (((i > 0 ? cm >> i : 0u) | cm >> j) & 1u) continue;
                 const int ps = i < 0 ? 0 : i;
                 const int n = j - ps;
                 const uint32_t cont = i < 0 ? UC_META : UC_PIECE;
-                if (src + ps != cur_ps) {
-                    cur_ps = src + ps;
+                if (16 * jv + ps != cur_ps) {
+                    cur_ps = 16 * jv + ps;
                     rowb = lds_w16(pb32, cur_ps, 16);
                 }
                 W[u] = keep_bytes(rowb, n);
@@ -1198,8 +1207,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDL_UNI_VWAV
             }
 #pragma unroll
             for (int u = 0; u < VU; ++u) {
-                const int t = t0 + u;
-                if (t >= TZ) continue;
+                const int t = r0 + u;
+                if (t >= tl1) continue;
                 double sc = -__builtin_inf();
                 if (meta[u] != ~0u) {
                     uint32_t w3;
@@ -1211,6 +1220,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDL_UNI_VWAV
                 }
                 s_sc[t - T0] = sc;
             }
+        }
         }
         __syncthreads();
         VIT_STAMP(2);
