@@ -111,11 +111,14 @@ constexpr int UNI_NODES = UNI_WMAX + 4;
 // A chunk's tokc slice (UNI_STAGE u32): its entry list (<= STAGE entries: every piece's ids fit
 // the stage slots up to the next piece) and, behind it, the Viterbi jobs the chunk kernel hands
 // to k_unigram_viterbi -- a job's ids land as u16 at its stage position in the results region,
-// and its list entry becomes LMARK | UNI_JOB_BIT | k << 24 | position (k_compact_tokens expands it).
-constexpr int UNI_VPC = 88;                           // Viterbi jobs per chunk (more: long items)
+// and its list entry becomes LMARK | UNI_JOB_BIT | k << 24 (6 bits) | position (k_compact_tokens expands it).
+constexpr int UNI_VPC = 88;                           // Viterbi jobs per chunk, and 16-B payload units (more: long items)
+constexpr int UNI_VMAX = 48;                          // longest job payload (printable ASCII words past UNI_WMAX)
+constexpr int UNI_VRING = 20;                         // the Viterbi DP's node ring: jobs past UNI_WMAX need
+                                                      // maxlen_first < UNI_VRING and maxlen_meta + 3 < UNI_VRING
 constexpr int UNI_JR_OFF = STAGE;                     // results: u16 [STAGE] at the stage positions
-constexpr int UNI_JP_OFF = STAGE + STAGE / 2;         // job payloads: uint4 [UNI_VPC]
-constexpr int UNI_JM_OFF = UNI_JP_OFF + 4 * UNI_VPC;  // job metas: L | pos << 5 | entry << 17
+constexpr int UNI_JP_OFF = STAGE + STAGE / 2;         // job payloads: uint4 [UNI_VPC], ceil(L / 16) (>= 1) each
+constexpr int UNI_JM_OFF = UNI_JP_OFF + 4 * UNI_VPC;  // job metas: L | pos << 6 | entry << 18
 constexpr int UNI_JN_OFF = UNI_JM_OFF + UNI_VPC;      // the chunk's job count
 constexpr uint32_t UNI_JOB_BIT = 0x40000000u;
 static_assert(UNI_JN_OFF < UNI_STAGE && (UNI_JP_OFF * 4) % 16 == 0 && (UNI_STAGE * 4) % 16 == 0,
@@ -212,9 +215,11 @@ struct RowParams {
     // rng_mode 1: the rows' mask bits (S/32 words a row, bit p = position p masked).  Rows known
     // before tokenizing -- chunk 0 of every record, chunk 1 of records of >= mask_spec1 bytes
     // (rand_pre_slot) -- are walked beside the tokenizer (k_mask_rand_rec + k_mask_bits_rec) into
-    // mask_bits0 (slot r, R + r; null: none); k_rows' LATE pass walks the others (rand_rows16).
+    // mask_bits0 (slot r, and R + mask_spos[r] for chunk 1: the record's place in the list of
+    // those, k_rand_spec_list; null: none); k_rows' LATE pass walks the others (rand_rows16).
     // mask_off / mask_R: the call's record offsets and count.
     const uint32_t *mask_bits0;
+    const uint32_t *mask_spos;
     const uint64_t *mask_off;
     int64_t mask_R, mask_spec1;
     int32_t mask_w;
@@ -244,7 +249,8 @@ __device__ __forceinline__ void static_for(const F &f) {
 __device__ __forceinline__ int64_t rand_pre_slot(const RowParams &P, int64_t r, uint32_t k) {
     if (!P.mask_bits0) return -1;
     if (k == 0) return r;
-    if (k == 1 && P.mask_spec1 > 0 && (int64_t)(P.mask_off[r + 1] - P.mask_off[r]) >= P.mask_spec1) return P.mask_R + r;
+    if (k == 1 && P.mask_spec1 > 0 && (int64_t)(P.mask_off[r + 1] - P.mask_off[r]) >= P.mask_spec1)
+        return P.mask_R + P.mask_spos[r];
     return -1;
 }
 

@@ -55,6 +55,10 @@ struct UniWork {
     uint8_t *scratch;     // unigram_scratch_bytes(lane_blocks, huge_blocks)
     int lane_blocks, huge_blocks;
     uint32_t *err;        // bit 1 ids overflow, 2 pool, 3 item lists, 4 item too large
+    // (optional) a second stream and two events: the wide-job Viterbi and the long items run
+    // there beside the narrow-job Viterbi (they touch other entries; their counts add atomically)
+    hipStream_t side;
+    hipEvent_t ev_fork, ev_join;
 };
 size_t unigram_scratch_bytes(int lane_blocks, int huge_blocks);
 hipError_t launch_unigram_chunks(const DevTok &T, const uint8_t *text, int64_t N, const uint64_t *off, int64_t R,
@@ -289,7 +293,8 @@ hipError_t launch_rows(const RowParams &P, const uint32_t *tok, const uint32_t *
 // rng_mode 1 masks (pipeline.hip): the rows rand_pre_slot names (chunk 0 of every record, chunk 1
 // of long ones) from (seed, first_record + r, chunk) alone -- launched beside the tokenizer: swap
 // indices (lane per row) into jbuf [2 R, S], then the mask bits into P.mask_bits0 slots
-hipError_t launch_mask_rand_rec(const RowParams &P, uint32_t *list, uint16_t *jbuf, uint32_t *bits, hipStream_t st);
+hipError_t launch_mask_rand_rec(const RowParams &P, uint32_t *list, uint32_t *spos, uint16_t *jbuf, uint32_t *bits,
+                                hipStream_t st);
 // ... and the other rows g of the segment, after the row map: listed (list[0] = count, list[1..] =
 // rows; rows_cap + 1 words), then 16 lanes per row, bits into bitsg [rows, S/32]
 // BertData MultiLabel labels_f32 plane (bert_data.rs:66-78)

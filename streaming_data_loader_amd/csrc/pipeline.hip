@@ -576,10 +576,6 @@ __global__ __launch_bounds__(64) void k_downstream_tiny(SmallDown d, RowParams P
     downstream_tiny<MR>(d, P, off, R, N, n_chunks);
 }
 
-static const bool tiny_downstream = [] {
-    const char *e = std::getenv("SDL_TINY_DOWNSTREAM");
-    return !e || std::atoi(e) != 0;
-}();
 hipError_t launch_downstream_small(const SmallDown &d, const RowParams &P, const uint64_t *off, int64_t R, int64_t N,
                                    hipStream_t st) {
     const int64_t n_chunks = (N + CHUNK - 1) / CHUNK;
@@ -587,7 +583,7 @@ hipError_t launch_downstream_small(const SmallDown &d, const RowParams &P, const
     const int MR = (P.S + 255) / 256;
     if (d.rows && ((P.rng_mode == 1 && P.task == 0) || (P.task != 0 && P.task != 1)))
         return hipErrorInvalidValue;  // (rng_mode 1 masks need k_rows' passes; span has its own rows)
-    const bool tiny = tiny_downstream && R <= 64 && n_chunks <= 64;
+    const bool tiny = R <= 64 && n_chunks <= 64;
 #define SDL_DS(M)                                                                                                    \
     if (tiny) hipLaunchKernelGGL(k_downstream_tiny<M>, dim3(1), dim3(64), 0, st, d, P, off, R, N, n_chunks);        \
     else hipLaunchKernelGGL(k_downstream_small<M>, dim3(1), dim3(SCAN_SMALL_NT), 0, st, d, P, off, R, N, n_chunks)
@@ -764,25 +760,32 @@ __device__ __forceinline__ void rand_set_bits(const RowParams &P, const uint16_t
 // it on a second stream beside the tokenizer (sdl_batcher.cpp run_device): its ChaCha12 work
 // fills VALU slots the latency-bound tokenizer leaves idle instead of sitting on the step's
 // critical path.  (86 % of the bench's rows are chunk 0.)
-// (slot s < R: record s, chunk 0; s = R + r: record r, chunk 1 when rand_pre_slot says so.)  The
-// walk runs over t in [0, R + n_spec): t < R is slot t, the rest the slots k_rand_spec_list
-// collected -- a wave holding any chunk-1 slot costs a whole walk, and ~1 record in 5 has one.
-__global__ __launch_bounds__(256) void k_rand_spec_list(RowParams P, uint32_t *__restrict__ list) {
+// (slot s < R: record s, chunk 0; s = R + i: chunk 1 of the list's i-th record, the records of
+// >= mask_spec1 bytes, in no particular order; mask_spos[r] = i.)  The walk runs over the slots
+// t in [0, R + n_spec) -- a wave holding any chunk-1 slot costs a whole walk, and ~1 record in 5
+// has one -- and the slots take R + (the records past mask_spec1 bytes), not 2 R, of the buffers.
+__global__ __launch_bounds__(256) void k_rand_spec_list(RowParams P, uint32_t *__restrict__ list,
+                                                        uint32_t *__restrict__ spos) {
     const int lane = lane_id();
     const int64_t R = P.mask_R;
     for (int64_t r0 = (int64_t)blockIdx.x * 256 + (threadIdx.x & ~63u); r0 < R; r0 += (int64_t)gridDim.x * 256) {
         const int64_t r = r0 + lane;
-        const bool take = r < R && rand_pre_slot(P, r, 1u) >= 0;
+        const bool take = r < R && (int64_t)(P.mask_off[r + 1] - P.mask_off[r]) >= P.mask_spec1;
         const uint64_t m = __ballot(take);
         if (!m) continue;
         const int leader = __builtin_ctzll(m);
         uint32_t base = 0;
         if (lane == leader) base = atomicAdd(&list[0], (uint32_t)__popcll(m));
         base = (uint32_t)lane_bcast((int)base, leader);
-        if (take) list[1 + base + __popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)(R + r);
+        if (take) {
+            const uint32_t i = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+            list[1 + i] = (uint32_t)r;
+            spos[r] = i;
+        }
     }
 }
-__device__ __forceinline__ int64_t rand_rec_slot(const RowParams &P, const uint32_t *list, int64_t t) {
+// record of slot t (chunk 0 below R, chunk 1 above)
+__device__ __forceinline__ int64_t rand_rec_of(const RowParams &P, const uint32_t *list, int64_t t) {
     return t < P.mask_R ? t : (int64_t)list[1 + (t - P.mask_R)];
 }
 #ifndef SDL_RAND_NR
@@ -804,8 +807,8 @@ __global__ __launch_bounds__(256) void k_mask_rand_rec(RowParams P, const uint32
         for (int r = 0; r < RAND_NR; ++r) {
             const int64_t t = t0 + 64 * r + lane;
             active[r] = t < nt;
-            const int64_t s = active[r] ? rand_rec_slot(P, list, t) : 0;
-            rec[r] = P.first_record + (uint64_t)(s < R ? s : s - R);
+            const int64_t s = active[r] ? t : 0;
+            rec[r] = P.first_record + (uint64_t)(active[r] ? rand_rec_of(P, list, t) : 0);
             chunk[r] = s < R ? 0u : 1u;
             jrow[r] = jbuf + s * (int64_t)P.S;
         }
@@ -822,14 +825,15 @@ __global__ __launch_bounds__(256) void k_mask_bits_rec(RowParams P, const uint32
     const int lane = lane_id(), wid = (int)(threadIdx.x >> 6);
     const int64_t nt = P.mask_R + (P.mask_spec1 > 0 ? (int64_t)list[0] : 0);
     for (int64_t t = (int64_t)blockIdx.x * 4 + wid; t < nt; t += (int64_t)gridDim.x * 4) {
-        const int64_t s = rand_rec_slot(P, list, t);
+        const int64_t s = t;
         rand_set_bits<MR4>(P, jbuf + s * (int64_t)P.S, s_nx[wid], s_bt[wid], lane);
         for (int w = lane; w < P.mask_w; w += 64) bits[s * (int64_t)P.mask_w + w] = s_bt[wid][w];
         __builtin_amdgcn_wave_barrier();  // (s_bt is rewritten by the wave's next row)
     }
 }
 
-hipError_t launch_mask_rand_rec(const RowParams &P, uint32_t *list, uint16_t *jbuf, uint32_t *bits, hipStream_t st) {
+hipError_t launch_mask_rand_rec(const RowParams &P, uint32_t *list, uint32_t *spos, uint16_t *jbuf, uint32_t *bits,
+                                hipStream_t st) {
     const int64_t R = P.mask_R, ns = P.mask_spec1 > 0 ? 2 * R : R;
     if (R <= 0) return hipSuccess;
     if (P.S > RAND_MAX_S || P.mask_w * 32 < P.S || !P.mask_off) return hipErrorInvalidValue;
@@ -837,7 +841,7 @@ hipError_t launch_mask_rand_rec(const RowParams &P, uint32_t *list, uint16_t *jb
     if (e != hipSuccess) return e;
     if (P.mask_spec1 > 0) {
         const int64_t lb = (R + 255) / 256;
-        hipLaunchKernelGGL(k_rand_spec_list, dim3((unsigned)(lb < 2048 ? lb : 2048)), dim3(256), 0, st, P, list);
+        hipLaunchKernelGGL(k_rand_spec_list, dim3((unsigned)(lb < 2048 ? lb : 2048)), dim3(256), 0, st, P, list, spos);
     }
     // (sized for every slot; the waves past R + n_spec leave at once)
     const int64_t want = (ns + 256 * RAND_NR - 1) / (256 * RAND_NR);

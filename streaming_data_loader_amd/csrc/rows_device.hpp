@@ -94,7 +94,7 @@ __device__ __forceinline__ void compact_wave(int64_t cb, const uint32_t *__restr
         for (int j = 0; j < COMPACT_CPW; ++j) {
             const bool mark = (x[j] & 0x80000000u) != 0u;
             const bool job = long_pool && (x[j] & UNI_JOB_BIT);
-            w[j] = e >= ne[j] ? 0u : !mark ? 1u : job ? (x[j] >> 24) & 31u : long_pool ? long_pool[x[j] & 0x7FFFFFFFu]
+            w[j] = e >= ne[j] ? 0u : !mark ? 1u : job ? (x[j] >> 24) & 63u : long_pool ? long_pool[x[j] & 0x7FFFFFFFu]
                                                                                     : long_list[x[j] & 0x7FFFFFFFu].k;
         }
 #pragma unroll

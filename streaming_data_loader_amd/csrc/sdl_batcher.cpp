@@ -278,7 +278,7 @@ struct sdl_batcher {
     // (k_mask_rand_rec: chunk 0 of every record, chunk 1 of the spec_list records); k_rows walks the
     // rest in a second pass
     DevBuf<uint16_t> mask_j0;
-    DevBuf<uint32_t> mask_bits0, spec_list;
+    DevBuf<uint32_t> mask_bits0, spec_list, spec_pos;
     hipEvent_t rand_ev[4] = {nullptr, nullptr, nullptr, nullptr};
     DevBuf<float> o_f32;
     DevBuf<uint32_t> lab_err;
@@ -386,6 +386,9 @@ struct sdl_batcher {
     const char **stage_names = kStageNames;
     // pipelined segments: second stream, cross-stream events, record bounds
     hipStream_t stream2 = nullptr;
+    hipStream_t stream_u = nullptr;  // unigram: the wide-job Viterbi and the long items beside the narrow jobs
+    hipEvent_t uni_ev[2] = {nullptr, nullptr};
+    bool uni_side = env_int0("SDL_UNI_SIDE", 1) != 0;  // (A/B: 0 runs them all on the handle's stream)
     std::vector<hipEvent_t> pipe_ev;
     DevBuf<uint32_t> seg_rb;
     int seg_target = env_int("SDL_SEGMENTS", 1);
@@ -424,6 +427,9 @@ struct sdl_batcher {
         if (x_in) (void)hipStreamDestroy(x_in);
         if (x_out) (void)hipStreamDestroy(x_out);
         if (stream2) (void)hipStreamDestroy(stream2);
+        for (auto &e : uni_ev)
+            if (e) (void)hipEventDestroy(e);
+        if (stream_u) (void)hipStreamDestroy(stream_u);
         if (stream) (void)hipStreamDestroy(stream);
     }
 
@@ -484,6 +490,7 @@ struct sdl_batcher {
         p.first_record = first_record;
         p.mask_w = mask_w;
         p.mask_bits0 = nullptr;
+        p.mask_spos = nullptr;
         p.mask_off = d_off;
         p.mask_R = R;
         p.mask_spec1 = 0;
@@ -529,10 +536,13 @@ struct sdl_batcher {
         if (rec0) {
             const int64_t F = P.n_pre + P.n_post;
             p.mask_spec1 = P.chunk && rand_spec_rho > 0 ? (int64_t)((double)(P.S - F + 1) / rand_spec_rho) : 0;
-            const int64_t ns = p.mask_spec1 > 0 ? 2 * R : R;
+            // chunk-1 slots: the records of >= mask_spec1 bytes, at most N / mask_spec1 of them
+            const int64_t ns = R + (p.mask_spec1 > 0 ? std::min<int64_t>(R, N / p.mask_spec1 + 1) : 0);
             mask_j0.ensure((size_t)ns * (size_t)P.S);
             mask_bits0.ensure((size_t)ns * (size_t)mask_w);
             spec_list.ensure((size_t)R + 1);
+            spec_pos.ensure((size_t)R + 1);
+            p.mask_spos = spec_pos.p;
             ensure_stream2();
             for (auto &e : rand_ev)
                 if (!e) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -540,7 +550,7 @@ struct sdl_batcher {
             HIP_TRY(hipStreamWaitEvent(stream2, rand_ev[0], 0));
             p.mask_bits0 = mask_bits0.p;
             hipStream_t rs = rand_rec_serial ? st : stream2;
-            HIP_TRY(launch_mask_rand_rec(p, spec_list.p, mask_j0.p, mask_bits0.p, rs));
+            HIP_TRY(launch_mask_rand_rec(p, spec_list.p, spec_pos.p, mask_j0.p, mask_bits0.p, rs));
             HIP_TRY(hipEventRecord(rand_ev[1], rs));
         }
         if (!fold) HIP_TRY(launch_seg_bounds(ranges.p, sc, R, seg_rb.p, st));
@@ -654,9 +664,14 @@ struct sdl_batcher {
             chunk_ent.ensure((size_t)n_chunks + 1);
             uint32_t item_cap = (uint32_t)std::min<size_t>(uni_items.cap, 0xFFFFFFFFu);
             if (uni_item_cap) item_cap = std::min(item_cap, uni_item_cap);
+            if (uni_side && !stream_u) {
+                HIP_TRY(hipStreamCreateWithFlags(&stream_u, hipStreamNonBlocking));
+                for (auto &e : uni_ev) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            }
             UniWork W{uni_counters.p, uni_items.p, item_cap, uni_pool.p,
                       (uint32_t)std::min<size_t>(uni_pool.cap, 0x3FFFFFFF), uni_huge.p, (uint32_t)uni_huge.cap,
-                      uni_items2.p, (uint32_t)uni_items2.cap, uni_scratch.p, lane_blocks, huge_blocks, uni_err.p};
+                      uni_items2.p, (uint32_t)uni_items2.cap, uni_scratch.p, lane_blocks, huge_blocks, uni_err.p,
+                      uni_side ? stream_u : nullptr, uni_ev[0], uni_ev[1]};
             HIP_TRY(launch_unigram_chunks(dt, d_text, N, d_off, R, ranges.p, tokc.p, chunk_cnt.p, chunk_ent.p,
                                           rec_local.p, W, st));
             downstream(0, st);
@@ -1875,6 +1890,30 @@ int sdl_gzip_inflate_first_device(sdl_batcher *h, const uint8_t *d_gz, uint64_t 
             HIP_TRY(hipMemcpyAsync(ends.data(), h->z_mend.p, n * 8, hipMemcpyDeviceToHost, st));
             HIP_TRY(hipStreamSynchronize(st));
             const int rc = gzip_inflate_impl(h, d_gz, gz_len, d_file_offsets, h->z_mend.p, n_files, stream, out);
+            if (rc == SDL_ERR_CAPACITY && attempt < 63) {
+                // A range that ends at a candidate inside its member's DEFLATE data read its "ISIZE"
+                // from 4 arbitrary bytes, which the 1032:1 bound no longer rejects once the range
+                // is a few MB: the sizes overflowed the arena.  Advance the candidate-ended files
+                // with the largest sizes until the rest fits, and try again (a real first member
+                // this large could not be inflated in one call anyway).
+                std::vector<uint32_t> sz(n);
+                HIP_TRY(hipMemcpy(sz.data(), h->z_size.p, n * 4, hipMemcpyDeviceToHost));
+                unsigned long long tot = 0;
+                std::vector<size_t> cand;
+                for (size_t f = 0; f < n; ++f) {
+                    tot += sz[f];
+                    if (ends[f] < fo[f + 1]) cand.push_back(f);
+                }
+                std::sort(cand.begin(), cand.end(), [&](size_t x, size_t y) { return sz[x] > sz[y]; });
+                bool moved = false;
+                for (size_t f : cand) {
+                    if (tot < (1ull << 32) - 64) break;
+                    tot -= sz[f];
+                    from[f] = ends[f];
+                    moved = true;
+                }
+                if (moved) continue;
+            }
             if (rc != SDL_ERR_DATA || attempt >= 63) return rc;
             std::vector<int32_t> zs(n);
             HIP_TRY(hipMemcpy(zs.data(), h->z_status.p, n * 4, hipMemcpyDeviceToHost));

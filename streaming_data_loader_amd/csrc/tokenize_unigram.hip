@@ -65,7 +65,9 @@ constexpr int MED_CAP = SDL_UNI_MED_CAP;  // medium words per chunk (more: long 
 #endif
 constexpr int UNI_WT_UNROLL = SDL_UNI_WT_UNROLL;  // word-table probes in flight per lane
 constexpr uint8_t CNT_LONG = 0xFF;  // s_cnt of a long item
-constexpr uint8_t CNT_JOB = 0x80;   // s_cnt of a piece handed to k_unigram_viterbi: CNT_JOB | its jobs (< 0x7F)
+// s_cnt of a piece handed to k_unigram_viterbi: CNT_JOB | its jobs (<= 0x3F), or, a word past UNI_WMAX
+// bytes (one job), CNT_JOB | CNT_WIDE | its payload units; the low 6 bits are the payload units either way
+constexpr uint8_t CNT_JOB = 0x80, CNT_WIDE = 0x40;
 // k_unigram_viterbi: a pass takes the chunk's next jobs whose candidates fit VTCAP (one job
 // always does: vp_tasks(UNI_WMAX) = 17 + 16 * 16 < VTCAP) and at most VJP of them (a DP lane each)
 #ifndef SDL_UNI_VJP
@@ -639,7 +641,7 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
     constexpr int U_CLS = 0, U_MED = (WIN + 15) & ~15, U_MED_END = U_MED + 2 * MED_CAP;
     __shared__ __attribute__((aligned(16))) uint8_t s_u[U_MED_END];  // classes | medium words
     uint8_t *const s_cls = s_u + U_CLS;
-    __shared__ uint32_t s_rbits[RBITS_WORDS + 1];
+    __shared__ uint32_t s_rbits[RBITS_WORDS + 3];  // (+2: word_len's 64-bit windows)
     __shared__ uint16_t s_pieces[CHUNK + 1];  // prel | SPEC << 12
     // ids staged at their piece's byte offset: a piece may use the bytes up to
     // the next piece (stage_room); one that needs more becomes a long item.  A
@@ -678,10 +680,10 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
         *reinterpret_cast<uint4 *>(s_bytes + (hp - w0)) = hv;
     }
     if (tid < 2) *reinterpret_cast<uint4 *>(s_bytes + WIN + 16 * tid) = make_uint4(0, 0, 0, 0);
-    if (tid <= RBITS_WORDS) s_rbits[tid] = 0;
+    if (tid <= RBITS_WORDS + 2) s_rbits[tid] = 0;
     const int64_t ra = ranges[3 * ci], rz = ranges[3 * ci + 1], r_lo = ranges[3 * ci + 2];
     const int nrb = (int)(rz - ra);
-    if (tid < 8) s_scratch[tid] = 0;
+    if (tid < 8) s_scratch[tid] = 0;  // (1 jobs 2 arena used 3 medium words 4 payload units)
     __syncthreads();
     for (int k = tid; k < nrb; k += TOK_THREADS) {
         const int rel = (int)((int64_t)off[ra + k] - w0);
@@ -764,33 +766,75 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
         return (pi + 1 < np ? (int)(s_pieces[pi + 1] & 0xFFFu) : STAGE) - prel;
     };
     const lds_u32 *cls32 = (const lds_u32 *)s_cls;
-    // Length of the raw word starting at window index wi0: 1..UNI_WMAX, 0 when it
-    // runs past the window, UNI_WMAX + 1 when longer (its end is found by the
+    // Length of the raw word starting at window index wi0: 1..UNI_VMAX, 0 when it
+    // runs past the window, UNI_VMAX + 1 when longer (its end is found by the
     // long-item kernel); *simple = printable ASCII only.  Its first 20 classes
-    // come in 6 independent dword loads, the end is a bit scan.
+    // come in 6 independent dword loads, the end is a bit scan; a word with no end
+    // among them takes 7 more loads (52 classes).
     auto word_len = [&](int wi0, bool *simple) -> int {
         const int a = wi0 >> 2;
         const uint32_t sh = (uint32_t)(wi0 & 3);
-        uint32_t d[6];
-#pragma unroll
-        for (int k = 0; k < 6; ++k) d[k] = cls32[a + k];
-        uint32_t bnd = 0, nonp = 0;  // bit q: class at offset q is a word boundary / not U_P
-#pragma unroll
-        for (int k = 0; k < 5; ++k) {
-            const uint32_t c = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
-            bnd |= gather4(nzb(c & 0x09090909u)) << (4 * k);  // U_WS, U_SPEC
-            nonp |= gather4(~bit7(c, 1)) << (4 * k);          // not U_P
-        }
-        const uint64_t rw = ((uint64_t)rbits[(wi0 >> 5) + 1] << 32) | rbits[wi0 >> 5];
-        bnd |= (uint32_t)(rw >> (wi0 & 31));            // record starts
-        const int64_t lim_n = N - (w0 + wi0);           // offsets >= lim_n: past the text
-        if (lim_n <= (int64_t)UNI_WMAX) bnd |= ~0u << (int)lim_n;
-        bnd &= ((2u << UNI_WMAX) - 1u) & ~1u;           // offsets 1 .. UNI_WMAX
-        const int qb = bnd ? __builtin_ctz(bnd) : UNI_WMAX + 1;
         const int qp = WIN - 8 - wi0;                   // first offset past the window
+        const int64_t lim_n = N - (w0 + wi0);           // offsets >= lim_n: past the text
+        {
+            uint32_t d[6];
+#pragma unroll
+            for (int k = 0; k < 6; ++k) d[k] = cls32[a + k];
+            uint32_t bnd = 0, nonp = 0;  // bit q: class at offset q is a word boundary / not U_P
+#pragma unroll
+            for (int k = 0; k < 5; ++k) {
+                const uint32_t c = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
+                bnd |= gather4(nzb(c & 0x09090909u)) << (4 * k);  // U_WS, U_SPEC
+                nonp |= gather4(~bit7(c, 1)) << (4 * k);          // not U_P
+            }
+            const uint64_t rw = ((uint64_t)rbits[(wi0 >> 5) + 1] << 32) | rbits[wi0 >> 5];
+            bnd |= (uint32_t)(rw >> (wi0 & 31));            // record starts
+            if (lim_n <= (int64_t)UNI_WMAX) bnd |= ~0u << (int)lim_n;
+            bnd &= ((2u << UNI_WMAX) - 1u) & ~1u;           // offsets 1 .. UNI_WMAX
+            if (bnd) {
+                const int qb = __builtin_ctz(bnd);
+                if (qp <= qb) return 0;
+                *simple = (nonp & ((1u << qb) - 1u)) == 0u;
+                return qb;
+            }
+        }
+        uint32_t d[13];
+#pragma unroll
+        for (int k = 0; k < 13; ++k) d[k] = cls32[a + k];
+        uint64_t bnd = 0, nonp = 0;
+#pragma unroll
+        for (int k = 0; k < 12; ++k) {
+            const uint32_t c = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
+            bnd |= (uint64_t)gather4(nzb(c & 0x09090909u)) << (4 * k);
+            nonp |= (uint64_t)gather4(~bit7(c, 1)) << (4 * k);
+        }
+        {  // record starts
+            const int w = wi0 >> 5, r = wi0 & 31;
+            const uint64_t lo = ((uint64_t)rbits[w + 1] << 32) | rbits[w];
+            bnd |= r ? lo >> r | (uint64_t)rbits[w + 2] << (64 - r) : lo;
+        }
+        if (lim_n <= (int64_t)UNI_VMAX) bnd |= ~0ull << lim_n;
+        bnd &= ((2ull << UNI_VMAX) - 1u) & ~1ull;       // offsets 1 .. UNI_VMAX
+        const int qb = bnd ? __builtin_ctzll(bnd) : UNI_VMAX + 1;
         if (qp <= qb) return 0;
-        *simple = qb <= UNI_WMAX && (nonp & ((1u << qb) - 1u)) == 0u;
+        *simple = qb <= UNI_VMAX && (nonp & ((1ull << qb) - 1u)) == 0u;
         return qb;
+    };
+    // jobs past UNI_WMAX bytes fit the Viterbi kernel's node ring
+    const bool wide_ok = T.maxlen_first < UNI_VRING && T.maxlen_meta + 3 < UNI_VRING;
+    // a Viterbi job: its payload in LDS (window or arena) and length; false when the chunk's
+    // jobs or payload units are used up (a long item then)
+    auto new_job = [&](int src, int len, int nvp, uint32_t *vp0) -> bool {
+        const uint32_t units = (uint32_t)(len > 16 ? (len + 15) >> 4 : 1) * (uint32_t)nvp;  // (nvp > 1: medium, <= 16 each)
+        const uint32_t vu = atomicAdd(&s_scratch[1], (uint32_t)nvp | units << 16);  // (one LDS atomic: jobs | units)
+        const uint32_t v = vu & 0xFFFFu;
+        if ((vu >> 16) + units > (uint32_t)UNI_VPC || v + (uint32_t)nvp > (uint32_t)VP_CAP) return false;
+        if (src >= 0) {
+            s_vp_src[v] = (uint16_t)src;
+            s_vp_len[v] = (uint8_t)len;
+        }
+        *vp0 = v;
+        return true;
     };
     for (int p0 = 0; p0 < np; p0 += TOK_THREADS * UNI_WT_UNROLL) {
         // word-table probes of this lane's next UNI_WT_UNROLL pieces, in flight together
@@ -822,8 +866,10 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
                 W[u] = lds_w16(w32, wi0, len);
                 P[u] = probe_load_words(T, hash16(W[u], (uint32_t)len, UC_WORD));
                 kind[u] = 1;
-            } else {
-                kind[u] = len > 0 && len <= UNI_WMAX ? 2u : 3u;
+            } else if (len > 0 && len <= UNI_WMAX) {
+                kind[u] = 2;
+            } else {  // a printable ASCII word past UNI_WMAX: a (wide) Viterbi job, else a long item
+                kind[u] = len > UNI_WMAX && len <= UNI_VMAX && simple && wide_ok ? 4u : 3u;
             }
         }
 #pragma unroll
@@ -847,14 +893,19 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
                     done = true;
                 } else if (packed < 0 && len + 1 <= room) {  // Viterbi yields <= len + 1 ids
                     // miss: one Viterbi piece, the word's bytes in the window
-                    const uint32_t vp = atomicAdd(&s_scratch[1], 1u);
-                    if (vp < VP_CAP) {
-                        s_vp_src[vp] = (uint16_t)wi0;
-                        s_vp_len[vp] = (uint8_t)len;
+                    uint32_t vp;
+                    if (new_job(wi0, len, 1, &vp)) {
                         stage[prel] = (uint16_t)vp;
                         cnt[pi] = CNT_JOB | 1u;
                         done = true;
                     }
+                }
+            } else if (kind[u] == 4) {
+                uint32_t vp;
+                if (len + 1 <= room && new_job(wi0, len, 1, &vp)) {
+                    stage[prel] = (uint16_t)vp;
+                    cnt[pi] = (uint8_t)(CNT_JOB | CNT_WIDE | (uint32_t)((len + 15) >> 4));
+                    done = true;
                 }
             } else if (kind[u] == 2) {
 #ifdef SDL_UNI_MEDIUM_LONG  // diagnostic: medium words go to the long-item kernel
@@ -870,7 +921,7 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
             }
             if (!done) {  // long item: finished by k_unigram_long; its length (0: unknown) in its stage slot
                 cnt[pi] = CNT_LONG;
-                stage[prel] = (uint16_t)(len <= UNI_WMAX ? len : 0);
+                stage[prel] = (uint16_t)(len <= UNI_VMAX ? len : 0);
             }
         }
     }
@@ -907,9 +958,8 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
                 for (int pass = 0; pass < 2 && fits; ++pass) {
                     if (pass == 1) {
                         if (nvp == 0) break;
-                        if (bound > stage_room(pi) || nvp >= (int)CNT_JOB - 1) { fits = false; break; }
-                        vp0 = atomicAdd(&s_scratch[1], (uint32_t)nvp);
-                        if (vp0 + (uint32_t)nvp > (uint32_t)VP_CAP) { fits = false; break; }
+                        if (bound > stage_room(pi) || nvp > 0x3F) { fits = false; break; }
+                        if (!new_job(-1, 0, nvp, &vp0)) { fits = false; break; }
                     }
                     int k = 0, i = 0;
                     while (i < nl) {
@@ -959,43 +1009,61 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
     UNI_STAMP(3);
     // ---- 4. compact ids into this chunk's tokc slice; hand the Viterbi pieces to
     //         k_unigram_viterbi; list the long items --------------------------------
-    auto ents = [](uint32_t c) -> uint32_t { return c == CNT_LONG ? 1u : (c & CNT_JOB) ? (c & 0x7Fu) : c; };
+    // list entries / Viterbi jobs of a piece (its payload units: c & 0x3F)
+    auto ents = [](uint32_t c) -> uint32_t {
+        return c == CNT_LONG ? 1u : (c & CNT_JOB) ? ((c & CNT_WIDE) ? 1u : (c & 0x3Fu)) : c;
+    };
+    auto jobs_of = [](uint32_t c) -> uint32_t { return c != CNT_LONG && (c & CNT_JOB) ? ((c & CNT_WIDE) ? 1u : (c & 0x3Fu)) : 0u; };
     const int per = (np + TOK_THREADS - 1) / TOK_THREADS;
     const int a0 = tid * per < np ? tid * per : np;
     const int a1 = a0 + per < np ? a0 + per : np;
-    uint32_t mine = 0, myjobs = 0;
+    auto units = [](int L) -> uint32_t { return L > 16 ? (uint32_t)(L + 15) >> 4 : 1u; };  // payload units of a job
+    uint32_t mine = 0;  // entries | jobs << 11 | payload units << 19 (one scan)
     for (int i = a0; i < a1; ++i) {
         const uint32_t c = s_cnt[i];
-        mine += ents(c);
-        myjobs += c != CNT_LONG && (c & CNT_JOB) ? (c & 0x7Fu) : 0u;
+        mine += ents(c) | jobs_of(c) << 11 | (jobs_of(c) ? (c & 0x3Fu) : 0u) << 19;
     }
-    uint32_t total, njobs;
-    uint32_t base = block_excl_sum<TOK_THREADS>(mine, &total, s_scratch + 8);
-    uint32_t jb = block_excl_sum<TOK_THREADS>(myjobs, &njobs, s_scratch + 8);
+    uint32_t tot3;
+    const uint32_t ex3 = block_excl_sum<TOK_THREADS>(mine, &tot3, s_scratch + 8);
+    const uint32_t total = tot3 & 0x7FFu, njobs = (tot3 >> 11) & 0xFFu;
+    uint32_t base = ex3 & 0x7FFu, jb = (ex3 >> 11) & 0xFFu, ub = ex3 >> 19;
     uint32_t *dst = tokc + ci * UNI_STAGE;
     const uint32_t base0 = base;
-    // jobs: payload (<= UNI_WMAX bytes from the window or the arena) and meta = length |
-    // stage position of its ids << 5 | list entry << 17; a word's pieces' ids follow each
+    uint32_t mywide = 0;
+    // jobs: payload (<= UNI_VMAX bytes from the window or the arena) and meta = length |
+    // stage position of its ids << 6 | list entry << 18; a word's pieces' ids follow each
     // other from its stage slot, each piece bounded by its chars + 1
     for (int i = a0; i < a1; ++i) {
         const uint32_t c = s_cnt[i];
-        if (c == CNT_LONG || !(c & CNT_JOB)) {
+        if (!jobs_of(c)) {
             base += ents(c);
             continue;
         }
         const int prel = s_pieces[i] & 0xFFF;
         const int vp0 = s_stage[prel];
         int pos = prel;
-        for (uint32_t q = 0; q < (c & 0x7Fu); ++q, ++base, ++jb) {
-            const int L = s_vp_len[vp0 + q];
-            const W16 w = lds_w16(w32, s_vp_src[vp0 + q], L);
-            *reinterpret_cast<uint4 *>(dst + UNI_JP_OFF + 4 * jb) = make_uint4(w.x, w.y, w.z, w.w);
-            dst[UNI_JM_OFF + jb] = (uint32_t)L | (uint32_t)pos << 5 | base << 17;
-            auto conts = [](uint32_t x) { return __builtin_popcount(x & ~(x << 1) & 0x80808080u); };
-            pos += L - (conts(w.x) + conts(w.y) + conts(w.z) + conts(w.w)) + 1;
+        for (uint32_t q = 0; q < jobs_of(c); ++q, ++base, ++jb) {
+            const int L = s_vp_len[vp0 + q], src = s_vp_src[vp0 + q];
+            int chars = 0;
+            for (uint32_t k = 0; k < units(L); ++k, ++ub) {
+                const int lk = L - 16 * (int)k;
+                const W16 w = lds_w16(w32, src + 16 * (int)k, lk < 16 ? lk : 16);
+                *reinterpret_cast<uint4 *>(dst + UNI_JP_OFF + 4 * ub) = make_uint4(w.x, w.y, w.z, w.w);
+                auto conts = [](uint32_t x) { return __builtin_popcount(x & ~(x << 1) & 0x80808080u); };
+                chars -= conts(w.x) + conts(w.y) + conts(w.z) + conts(w.w);
+            }
+            dst[UNI_JM_OFF + jb] = (uint32_t)L | (uint32_t)pos << 6 | base << 18;
+            mywide += L > UNI_WMAX ? 1u : 0u;
+            pos += L + chars + 1;
         }
     }
-    if (tid == 0) dst[UNI_JN_OFF] = njobs;
+    {  // (and how many of them are wide: k_unigram_viterbi<true>'s)
+        const uint32_t w = (uint32_t)lane_bcast((int)wave_incl_sum(mywide), 63);
+        if (tid == 0) {
+            dst[UNI_JN_OFF] = njobs;
+            dst[UNI_JN_OFF + 1] = w;
+        }
+    }
 #ifdef SDL_STAMPS
     if (tid == 0) {
         UNI_COUNT(0, 1);
@@ -1093,50 +1161,68 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
 #ifndef SDL_UNI_VWAVES
 #define SDL_UNI_VWAVES 3
 #endif
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDL_UNI_VWAVES, 8))) void k_unigram_viterbi(DevTok T, int64_t N, const uint64_t *__restrict__ off,
-                                                        int64_t R, const uint32_t *__restrict__ ranges,
-                                                        uint32_t *__restrict__ tokc, uint32_t *__restrict__ chunk_cnt,
-                                                        uint32_t *__restrict__ rec_local) {
-    __shared__ __attribute__((aligned(16))) uint8_t s_pb[VP_CAP * 16 + 16];  // payloads (+ lds_w16's 5th dword)
-    __shared__ uint32_t s_jm[VP_CAP];      // metas: L | pos << 5 | entry << 17
+// WIDE = false: the jobs of <= UNI_WMAX payload bytes (20 nodes, every one a register); true: the
+// printable ASCII words of UNI_WMAX < L <= UNI_VMAX (nodes in a ring of UNI_VRING registers).  Two
+// launches over the same job lists, so the common narrow jobs keep the small DP.
+template <bool WIDE>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDL_UNI_VWAVES, 8))) void k_unigram_viterbi(
+    DevTok T, int64_t N, const uint64_t *__restrict__ off, int64_t R, const uint32_t *__restrict__ ranges,
+    uint32_t *__restrict__ tokc, uint32_t *__restrict__ chunk_cnt, uint32_t *__restrict__ rec_local) {
+    __shared__ __attribute__((aligned(16))) uint8_t s_pb[UNI_VPC * 16 + 32];  // payload units (+ lds_w16's reach)
+    __shared__ uint32_t s_jm[VP_CAP];      // this launch's jobs: metas (L | pos << 6 | entry << 18)
     __shared__ uint16_t s_tb[VP_CAP + 1];  // task base of each job
+    __shared__ uint8_t s_uo[VP_CAP];       // first payload unit of each job
     __shared__ uint8_t s_k[VP_CAP];        // ids of each job
-    __shared__ uint16_t s_cm[VP_CAP];      // bit x: payload byte x continues a char
+    using CM = std::conditional_t<WIDE, uint64_t, uint32_t>;  // (<= UNI_VMAX / UNI_WMAX payload bytes)
+    __shared__ CM s_cm[VP_CAP];            // bit x: payload byte x continues a char
     __shared__ double s_sc[VTCAP];         // per task of the pass: the candidate's score, -inf: no piece
     __shared__ uint16_t s_id[VTCAP];       // ... its id
-    // after the DP: back pointers [node][lane], start node << 11 | task (UNK_T: unk); 0xFFFF: unset
+    // after the DP: back pointers (narrow: start node << 11 | task, UNK_T: unk, 0xFFFF: unset, per
+    // node; wide: the words of 6-bit fields) [..][lane], over the dead scores
+    constexpr int BPW = (UNI_VMAX + 4 + 4) / 5;
     uint16_t *const s_bp = reinterpret_cast<uint16_t *>(s_sc);
-    static_assert(UNI_NODES * 64 * 2 <= VTCAP * 8, "the back pointers fit the scores' LDS");
+    uint32_t *const s_bpw = reinterpret_cast<uint32_t *>(s_sc);
+    static_assert(UNI_NODES * 64 * 2 <= VTCAP * 8 && BPW * 64 * 4 <= VTCAP * 8, "the back pointers fit the scores' LDS");
     constexpr uint32_t UNK_T = 0x7FFu;
+    constexpr int RG = UNI_VRING;
+    static_assert(UNI_WMAX + 3 < UNI_NODES && UNI_NODES <= RG, "narrow jobs' nodes");
     const int lane = lane_id();
     const int64_t c = blockIdx.x;
     uint32_t *const slice = tokc + c * UNI_STAGE;
 #ifdef SDL_STAMPS
     unsigned long long vstamp_ = __builtin_amdgcn_s_memtime();
 #endif
-    const uint32_t nj = slice[UNI_JN_OFF];
-    if (nj == 0) return;
+    const uint32_t nall = slice[UNI_JN_OFF], nw = slice[UNI_JN_OFF + 1];
+    if ((WIDE ? nw : nall - nw) == 0) return;
     const int Mm = T.maxlen_meta, Mf = T.maxlen_first;
-    const int njobs = (int)(nj < (uint32_t)VP_CAP ? nj : (uint32_t)VP_CAP);
-    for (int v = lane; v < njobs; v += 64) {
-        const uint4 p = *reinterpret_cast<const uint4 *>(slice + UNI_JP_OFF + 4 * v);
-        *reinterpret_cast<uint4 *>(s_pb + 16 * v) = p;
-        s_jm[v] = slice[UNI_JM_OFF + v];
-        auto cb = [](uint32_t x) { return gather4(x & ~(x << 1) & B7); };  // 10xxxxxx bytes
-        s_cm[v] = (uint16_t)(cb(p.x) | cb(p.y) << 4 | cb(p.z) << 8 | cb(p.w) << 12);
-    }
-    if (lane < 4) reinterpret_cast<uint32_t *>(s_pb + 16 * VP_CAP)[lane] = 0u;
-    __syncthreads();
+    const int nj_all = (int)(nall < (uint32_t)VP_CAP ? nall : (uint32_t)VP_CAP);
+    auto units = [](int L) -> uint32_t { return L > 16 ? (uint32_t)(L + 15) >> 4 : 1u; };
+    int njobs;  // this launch's jobs, in list order
     {
-        uint32_t carry = 0;
-        for (int v0 = 0; v0 < njobs; v0 += 64) {
+        uint32_t carry = 0, ucarry = 0, xcarry = 0;
+        for (int v0 = 0; v0 < nj_all; v0 += 64) {
             const int v = v0 + lane;
-            const uint32_t t = v < njobs ? (uint32_t)vp_tasks((int)(s_jm[v] & 31u), Mm, Mf) : 0u;
-            const uint32_t incl = wave_incl_sum(t);
-            if (v < njobs) s_tb[v] = (uint16_t)(carry + incl - t);
-            carry += (uint32_t)lane_bcast((int)incl, 63);
+            const uint32_t jm = v < nj_all ? slice[UNI_JM_OFF + v] : 0u;
+            const int L = (int)(jm & 63u);
+            const bool mine = v < nj_all && (L > UNI_WMAX) == WIDE;
+            const uint32_t un = v < nj_all ? units(L) : 0u, t = mine ? (uint32_t)vp_tasks(L, Mm, Mf) : 0u;
+            const uint32_t uincl = wave_incl_sum(un), tincl = wave_incl_sum(t), xincl = wave_incl_sum(mine ? 1u : 0u);
+            if (mine) {
+                const uint32_t x = xcarry + xincl - 1u;
+                s_jm[x] = jm;
+                s_tb[x] = (uint16_t)(carry + tincl - t);
+                s_uo[x] = (uint8_t)(ucarry + uincl - un);
+            }
+            carry += (uint32_t)lane_bcast((int)tincl, 63);
+            ucarry += (uint32_t)lane_bcast((int)uincl, 63);
+            xcarry += (uint32_t)lane_bcast((int)xincl, 63);
         }
+        njobs = (int)xcarry;
         if (lane == 0) s_tb[njobs] = (uint16_t)carry;
+        const int nu = (int)(ucarry < (uint32_t)UNI_VPC ? ucarry : (uint32_t)UNI_VPC);
+        for (int q = lane; q < nu; q += 64)
+            *reinterpret_cast<uint4 *>(s_pb + 16 * q) = *reinterpret_cast<const uint4 *>(slice + UNI_JP_OFF + 4 * q);
+        if (lane < 8) reinterpret_cast<uint32_t *>(s_pb + 16 * UNI_VPC)[lane] = 0u;
 #ifdef SDL_STAMPS
         if (lane == 0) UNI_COUNT(3, carry);
 #endif
@@ -1144,17 +1230,27 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDL_UNI_VWAV
     __syncthreads();
     const lds_u8 *pb = (const lds_u8 *)s_pb;
     const lds_u32 *pb32 = (const lds_u32 *)s_pb;
+    for (int v = lane; v < njobs; v += 64) {  // continuation bytes (10xxxxxx) of each payload
+        const int L = (int)(s_jm[v] & 63u), u0 = s_uo[v];
+        uint64_t m = 0;
+        for (int k = 0; k < (L + 3) >> 2; ++k) {
+            const uint32_t x = pb32[4 * u0 + k];
+            m |= (uint64_t)gather4(x & ~(x << 1) & B7) << (4 * k);
+        }
+        s_cm[v] = (CM)(L < 64 ? m & ((1ull << L) - 1u) : m);
+    }
+    __syncthreads();
     VIT_STAMP(1);
     for (int a = 0; a < njobs;) {
         int b = a + 1;  // the pass: jobs [a, b)
         while (b < njobs && b - a < VJP && (int)s_tb[b + 1] - (int)s_tb[a] <= VTCAP) ++b;
         const int T0 = s_tb[a], TZ = s_tb[b];
         {  // lane l takes the pass's tasks [T0 + l K, T0 + (l + 1) K) in rounds of VU: one
-        // decode per pass, then (i, j) steps along the rows; a row's 16 bytes are read once
+           // decode per pass, then (i, j) steps along the rows; a row's 16 bytes are read once
         const int K = (TZ - T0 + 63) >> 6;
         const int tl0 = T0 + lane * K, tl1 = tl0 + K < TZ ? tl0 + K : TZ;
-        int jv = a, i = -1, j = -1, L = 0;
-        uint32_t cm = 0;  // the job's continuation-byte mask
+        int jv = a, i = -1, j = -1, L = 0, src = 0;
+        CM cm = 0;  // the job's continuation-byte mask
         if (tl0 < tl1) {
             int lo = a, hi = b - 1;  // the job holding task tl0
             while (lo < hi) {
@@ -1162,7 +1258,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDL_UNI_VWAV
                 if ((int)s_tb[m] <= tl0) lo = m; else hi = m - 1;
             }
             jv = lo;
-            L = (int)(s_jm[jv] & 31u);
+            L = (int)(s_jm[jv] & 63u);
+            src = 16 * s_uo[jv];
             cm = s_cm[jv];
             vp_decode(tl0 - (int)s_tb[jv], L, Mm, Mf, &i, &j);
             --j;  // (the first step lands on it)
@@ -1172,7 +1269,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDL_UNI_VWAV
         for (int r0 = tl0; r0 < tl0 + K; r0 += VU) {  // (K is wave-uniform)
             Probe P[VU];
             W16 W[VU];
-            uint32_t meta[VU];  // n | cont << 8; ~0u: no probe
+            uint32_t meta[VU];  // n | cont << 8 | (n > 16: payload byte of its start) << 12; ~0u: no probe
 #pragma unroll
             for (int u = 0; u < VU; ++u) {
                 meta[u] = ~0u;
@@ -1186,24 +1283,35 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDL_UNI_VWAV
                     j = i + 1;
                     if (i >= L) {
                         ++jv;
-                        L = (int)(s_jm[jv] & 31u);
+                        L = (int)(s_jm[jv] & 63u);
+                        src = 16 * s_uo[jv];
                         cm = s_cm[jv];
                         i = -1;
                         j = 0;
                     }
                 }
                 // candidates start and end on char boundaries
-                if (((i > 0 ? cm >> i : 0u) | cm >> j) & 1u) continue;
+                if (((i > 0 ? cm >> i : (CM)0) | cm >> j) & 1u) continue;
                 const int ps = i < 0 ? 0 : i;
                 const int n = j - ps;
                 const uint32_t cont = i < 0 ? UC_META : UC_PIECE;
-                if (16 * jv + ps != cur_ps) {
-                    cur_ps = 16 * jv + ps;
+                meta[u] = (uint32_t)n | cont << 8;
+                if (src + ps != cur_ps) {
+                    cur_ps = src + ps;
                     rowb = lds_w16(pb32, cur_ps, 16);
                 }
                 W[u] = keep_bytes(rowb, n);
-                P[u] = probe_load(T, hash16(W[u], (uint32_t)n, cont));
-                meta[u] = (uint32_t)n | cont << 8;
+                if (!WIDE || n <= 16) {
+                    P[u] = probe_load(T, hash16(W[u], (uint32_t)n, cont));
+                } else {  // (rows of wide jobs: pieces of 17 .. maxlen_first bytes) two blocks; the
+                          // bytes past 16 are checked against the vocab pool on a header match
+                    const W16 w2 = lds_w16(pb32, cur_ps + 16, n - 16);
+                    uint32_t h = hinit((uint32_t)n, cont);
+                    h = hmix(hmix(hmix(hmix(h, W[u].x), W[u].y), W[u].z), W[u].w);
+                    h = hmix(hmix(hmix(hmix(h, w2.x), w2.y), w2.z), w2.w);
+                    P[u] = probe_load(T, hfinal(h));
+                    meta[u] |= (uint32_t)cur_ps << 12;
+                }
             }
 #pragma unroll
             for (int u = 0; u < VU; ++u) {
@@ -1211,8 +1319,25 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDL_UNI_VWAV
                 if (t >= tl1) continue;
                 double sc = -__builtin_inf();
                 if (meta[u] != ~0u) {
-                    uint32_t w3;
-                    const int id = probe_result_w3(P[u], meta[u], W[u], &w3);
+                    uint32_t w3 = 0;
+                    int id = probe_result_w3(P[u], meta[u] & 0x3FFu, W[u], &w3);
+                    if constexpr (WIDE) {
+                        const uint32_t n = meta[u] & 31u;
+                        if (n > 16 && id >= 0) {  // (the slot matched length, cont and the first 16 bytes)
+                            const int q0 = (int)(meta[u] >> 12);
+                            const uint32_t key = meta[u] & 0x3FFu;
+                            const bool m1 = slot_match(P[u].a1, P[u].b1, key, W[u]);
+                            const uint32_t z = m1 ? P[u].a1.z : P[u].a2.z;
+                            for (uint32_t x = 16; x < n && id >= 0; ++x)
+                                if (T.vpool[z + x] != pb[q0 + (int)x]) id = -1;
+                            if (id < 0 && m1 && slot_match(P[u].a2, P[u].b2, key, W[u])) {  // (both: the second)
+                                id = (int32_t)P[u].a2.y;
+                                w3 = P[u].a2.w;
+                                for (uint32_t x = 16; x < n && id >= 0; ++x)
+                                    if (T.vpool[P[u].a2.z + x] != pb[q0 + (int)x]) id = -1;
+                            }
+                        }
+                    }
                     if (id >= 0) {
                         sc = uni_score64(__uint_as_float(w3), (uint32_t)id);
                         s_id[t - T0] = (uint16_t)((uint32_t)id & UNI_ID_MASK);
@@ -1228,88 +1353,191 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDL_UNI_VWAV
         const bool act = lane < b - a;
         const int v = act ? a + lane : a;
         const uint32_t jm = act ? s_jm[v] : 0u;
-        const int L = (int)(jm & 31u), n = L + 3;
-        uint32_t lm = 1u << L;  // the pass's longest payload (wave-uniform bound of the loops)
+        const int L = (int)(jm & 63u), n = L + 3;
+        int Lmax = L;  // the pass's longest payload (wave-uniform bound of the loops)
 #pragma unroll
-        for (int k = 1; k < 64; k <<= 1) lm |= (uint32_t)__shfl_xor((int)lm, k);
-        const int Lmax = 31 - __builtin_clz(lm);
-        const uint4 pw = *reinterpret_cast<const uint4 *>(s_pb + 16 * v);
+        for (int k = 1; k < 64; k <<= 1) {
+            const int o = __shfl_xor(Lmax, k);
+            Lmax = o > Lmax ? o : Lmax;
+        }
+        const int src = 16 * s_uo[v];
         const int tj = (int)s_tb[v] - T0;  // the job's first task in the pass
         const int c0 = vp_c0(L, Mm);
-        double best[UNI_NODES];
-        uint32_t bp[UNI_NODES];  // start node << 11 | task (UNK_T: unk); 0xFFFF: unset
-        static_for<0, UNI_NODES>([&](auto X) {
-            best[X] = -__builtin_inf();
-            bp[X] = 0xFFFFu;
-        });
-        auto relax = [&](auto E, double cc, uint32_t bb) {
-            const bool up = cc > best[E];
-            best[E] = up ? cc : best[E];
-            bp[E] = up ? bb : bp[E];
+        const uint32_t pos = (jm >> 6) & 0xFFFu;
+        uint16_t *const jr = reinterpret_cast<uint16_t *>(slice + UNI_JR_OFF) + pos;
+        auto acc = [&](int x) -> uint32_t { return x < 3 ? meta_byte(x) : (uint32_t)pb[src + x - 3]; };
+        auto cand = [&](int st2, int e2, double *) -> int {  // the fused-unk lookup
+            int id;
+            if (st2 == 0) id = e2 - 3 <= Mm ? probe_acc(T, acc, 3, e2 - 3, UC_META) : -1;
+            else id = e2 - st2 <= Mf ? probe_acc(T, acc, st2, e2 - st2, UC_PIECE) : -1;
+            return uni_piece_id(id);
         };
-        {  // start 0: "▁" + payload[0, j), j = 0 .. min(L, Mm) = tasks tj + j, ending at node 3 + j
-            const int jz = L < Mm ? L : Mm;
-            static_for<0, UNI_WMAX + 1>([&](auto J) {
-                constexpr int jj = decltype(J)::value;
-                if (jj <= Lmax && act && jj <= jz) relax(std::integral_constant<int, 3 + jj>{}, s_sc[tj + jj],
-                                                          (uint32_t)(tj + jj));
+        int k = 0;
+        if constexpr (!WIDE) {
+            // The nodes' f64 scores and back pointers in registers: the starts ("▁", then payload
+            // bytes 0 .. 15) and their candidates' ends are compile-time loops, so a node is a
+            // register and a candidate is one LDS load (its row's task base + end) and a compare
+            // -- unigram_viterbi's visit order (starts, then ends ascending, then the start's unk
+            // when no one-char piece starts there), strict-> and f64 sums.
+            const uint4 pw = *reinterpret_cast<const uint4 *>(s_pb + src);
+            double best[UNI_NODES];
+            uint32_t bp[UNI_NODES];
+            static_for<0, UNI_NODES>([&](auto X) {
+                best[X] = -__builtin_inf();
+                bp[X] = 0xFFFFu;
             });
-            // the "▁" char's unk when "▁" is no piece
-            if (act && !(s_sc[tj] > -__builtin_inf())) relax(std::integral_constant<int, 3>{}, T.unk_score, UNK_T);
-        }
-        static_for<0, UNI_WMAX>([&](auto I) {  // payload start i = node 3 + i
-            constexpr int i = decltype(I)::value, st = 3 + i;
-            if (i < Lmax) {
-                const uint32_t by = ((i < 4 ? pw.x : i < 8 ? pw.y : i < 12 ? pw.z : pw.w) >> (8 * (i & 3))) & 0xFFu;
-                const bool on = act && i < L && (i == 0 || (by & 0xC0u) != 0x80u);
-                const double base = best[st];
-                const int rlen = L - i < Mf ? L - i : Mf;
-                const int rb = tj + c0 + vp_rowoff(i, L, Mf);
-                static_for<1, UNI_WMAX - i + 1>([&](auto D) {
-                    constexpr int d = decltype(D)::value;
-                    if (on && d <= rlen)
-                        relax(std::integral_constant<int, st + d>{}, s_sc[rb + d - 1] + base,
-                              (uint32_t)st << 11 | (uint32_t)(rb + d - 1));
-                });
-                const int l0 = u8len_lead(by), mb = l0 < L - i ? l0 : L - i;
-                if (on && !(mb <= rlen && s_sc[rb + mb - 1] > -__builtin_inf())) {  // unk: no one-char piece
-                    static_for<1, 5>([&](auto M) {
-                        constexpr int m = decltype(M)::value;
-                        if constexpr (st + m < UNI_NODES)
-                            if (mb == m) relax(std::integral_constant<int, st + m>{}, T.unk_score + base,
-                                               (uint32_t)st << 11 | UNK_T);
-                    });
-                }
-            }
-        });
-        // -- backtrack (the back pointers to LDS: the scores are dead) --
-        static_for<0, UNI_NODES>([&](auto X) { s_bp[X * 64 + lane] = (uint16_t)bp[X]; });
-        VIT_STAMP(3);
-        if (act) {
-            struct {
-                const uint16_t *bp;
-                const uint16_t *id16;
-                int lane, unk;
-                __device__ int start(int x) const {
-                    const uint32_t b = bp[x * 64 + lane];
-                    return b == 0xFFFFu ? -1 : (int)(b >> 11);
-                }
-                __device__ int id(int x) const {
-                    const uint32_t b = bp[x * 64 + lane];
-                    return b == 0xFFFFu ? -1 : (b & 0x7FFu) == UNK_T ? unk : (int)id16[b & 0x7FFu];
-                }
-            } nodes{s_bp, s_id, lane, T.unk_id};
-            auto acc = [&](int x) -> uint32_t { return x < 3 ? meta_byte(x) : (uint32_t)pb[16 * v + x - 3]; };
-            auto cand = [&](int st2, int e2, double *) -> int {  // the fused-unk lookup
-                int id;
-                if (st2 == 0) id = e2 - 3 <= Mm ? probe_acc(T, acc, 3, e2 - 3, UC_META) : -1;
-                else id = e2 - st2 <= Mf ? probe_acc(T, acc, st2, e2 - st2, UC_PIECE) : -1;
-                return uni_piece_id(id);
+            auto relax = [&](auto E, double cc, uint32_t bb) {
+                const bool up = cc > best[E];
+                best[E] = up ? cc : best[E];
+                bp[E] = up ? bb : bp[E];
             };
-            const uint32_t pos = (jm >> 5) & 0xFFFu;
-            uint16_t *const jr = reinterpret_cast<uint16_t *>(slice + UNI_JR_OFF) + pos;
-            const int k = unigram_backtrack(n, cand, nodes, T.unk_id, [&](int x, int id) { jr[x] = (uint16_t)id; });
-            slice[jm >> 17] = LMARK | UNI_JOB_BIT | (uint32_t)k << 24 | pos;
+            {  // start 0: "▁" + payload[0, j), j = 0 .. min(L, Mm) = tasks tj + j, ending at node 3 + j
+                const int jz = L < Mm ? L : Mm;
+                static_for<0, UNI_WMAX + 1>([&](auto J) {
+                    constexpr int jj = decltype(J)::value;
+                    if (jj <= Lmax && act && jj <= jz) relax(std::integral_constant<int, 3 + jj>{}, s_sc[tj + jj],
+                                                              (uint32_t)(tj + jj));
+                });
+                // the "▁" char's unk when "▁" is no piece
+                if (act && !(s_sc[tj] > -__builtin_inf())) relax(std::integral_constant<int, 3>{}, T.unk_score, UNK_T);
+            }
+            static_for<0, UNI_WMAX>([&](auto I) {  // payload start i = node 3 + i
+                constexpr int i = decltype(I)::value, st = 3 + i;
+                if (i < Lmax) {
+                    const uint32_t by = ((i < 4 ? pw.x : i < 8 ? pw.y : i < 12 ? pw.z : pw.w) >> (8 * (i & 3))) & 0xFFu;
+                    const bool on = act && i < L && (i == 0 || (by & 0xC0u) != 0x80u);
+                    const double base = best[st];
+                    const int rlen = L - i < Mf ? L - i : Mf;
+                    const int rb = tj + c0 + vp_rowoff(i, L, Mf);
+                    static_for<1, UNI_WMAX - i + 1>([&](auto D) {
+                        constexpr int d = decltype(D)::value;
+                        if (on && d <= rlen)
+                            relax(std::integral_constant<int, st + d>{}, s_sc[rb + d - 1] + base,
+                                  (uint32_t)st << 11 | (uint32_t)(rb + d - 1));
+                    });
+                    const int l0 = u8len_lead(by), mb = l0 < L - i ? l0 : L - i;
+                    if (on && !(mb <= rlen && s_sc[rb + mb - 1] > -__builtin_inf())) {  // unk: no one-char piece
+                        static_for<1, 5>([&](auto M) {
+                            constexpr int m = decltype(M)::value;
+                            if constexpr (st + m < UNI_NODES)
+                                if (mb == m) relax(std::integral_constant<int, st + m>{}, T.unk_score + base,
+                                                   (uint32_t)st << 11 | UNK_T);
+                        });
+                    }
+                }
+            });
+            // -- backtrack (the back pointers to LDS: the scores are dead) --
+            static_for<0, UNI_NODES>([&](auto X) { s_bp[X * 64 + lane] = (uint16_t)bp[X]; });
+            VIT_STAMP(3);
+            if (act) {
+                struct {
+                    const uint16_t *bp;
+                    const uint16_t *id16;
+                    int lane, unk;
+                    __device__ int start(int x) const {
+                        const uint32_t b = bp[x * 64 + lane];
+                        return b == 0xFFFFu ? -1 : (int)(b >> 11);
+                    }
+                    __device__ int id(int x) const {
+                        const uint32_t b = bp[x * 64 + lane];
+                        return b == 0xFFFFu ? -1 : (b & 0x7FFu) == UNK_T ? unk : (int)id16[b & 0x7FFu];
+                    }
+                } nodes{s_bp, s_id, lane, T.unk_id};
+                k = unigram_backtrack(n, cand, nodes, T.unk_id, [&](int x, int id) { jr[x] = (uint16_t)id; });
+            }
+        } else {
+            // Few jobs a pass (~3 a held-out chunk), each up to UNI_VMAX + 3 nodes: a group of 21
+            // lanes per job, 3 jobs at a time.  The starts are visited in order; lane d of the
+            // group relaxes the start's candidate ending d + 1 bytes on (distinct nodes), its last
+            // lane the start's unk (when no one-char piece starts there, so never a node a piece
+            // of the same start reaches) -- unigram_viterbi's relaxations, strict-> and f64 sums,
+            // the nodes (f64 score, start << 16 | task) in LDS; lane 0 of the group backtracks.
+            constexpr int GN = UNI_VMAX + 4, GL = 21;
+            __shared__ double s_gb[3 * GN];
+            __shared__ uint32_t s_gp[3 * GN];
+            auto wave_sync = [] {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            };
+            const int grp = lane / GL, gl = lane - GL * grp;  // (lane 63: no group)
+            for (int j0 = a; j0 < b; j0 += 3) {
+                const int vj = j0 + grp;
+                const bool gact = grp < 3 && vj < b;
+                const uint32_t jmg = gact ? s_jm[vj] : 0u;
+                const int Lg = (int)(jmg & 63u), ng = gact ? Lg + 3 : 0;
+                const int srcg = gact ? 16 * s_uo[vj] : 0, tjg = gact ? (int)s_tb[vj] - T0 : 0;
+                const int c0g = vp_c0(Lg, Mm);
+                const uint64_t cmg = gact ? s_cm[vj] : 0ull;
+                lds_f64 *gb = (lds_f64 *)s_gb + (grp < 3 ? grp : 0) * GN;
+                lds_u32 *gp = (lds_u32 *)s_gp + (grp < 3 ? grp : 0) * GN;
+                for (int x = gl; gact && x <= ng; x += GL) {
+                    gb[x] = x == 0 ? 0.0 : -__builtin_inf();
+                    gp[x] = 0xFFFFFFFFu;
+                }
+                int nmax = ng;  // (wave-uniform bound of the start loop)
+#pragma unroll
+                for (int q = 1; q < 64; q <<= 1) {
+                    const int o = __shfl_xor(nmax, q);
+                    nmax = o > nmax ? o : nmax;
+                }
+                wave_sync();
+                auto relaxg = [&](int e, double cc, uint32_t bb) {
+                    if (gp[e] == 0xFFFFFFFFu || cc > gb[e]) {
+                        gb[e] = cc;
+                        gp[e] = bb;
+                    }
+                };
+                for (int st = 0; st < nmax; st = st == 0 ? 3 : st + 1) {
+                    const int i = st - 3;
+                    if (gact && st < ng && (st == 0 || !((cmg >> i) & 1u))) {
+                        const double base = gb[st];
+                        const int rlen = st == 0 ? (Lg < Mm ? Lg : Mm) + 1 : (Lg - i < Mf ? Lg - i : Mf);
+                        const int rb = st == 0 ? tjg : tjg + c0g + vp_rowoff(i, Lg, Mf);
+                        if (gl < rlen && gl < GL - 1) {  // candidate (st, e): "▁" row ends 3 + gl, else st + gl + 1
+                            const int t = rb + gl, e = st == 0 ? 3 + gl : st + gl + 1;
+                            const double sv = s_sc[t];
+                            if (sv > -__builtin_inf()) relaxg(e, sv + base, (uint32_t)st << 16 | (uint32_t)t);
+                        }
+                        if (gl == GL - 1) {  // unk
+                            const int l0 = st == 0 ? 3 : u8len_lead(pb[srcg + i]), mb = l0 < ng - st ? l0 : ng - st;
+                            const int ts = st == 0 ? rb : rb + mb - 1;  // the one-char piece's task
+                            if (!((st == 0 || mb <= rlen) && s_sc[ts] > -__builtin_inf()))
+                                relaxg(st + mb, T.unk_score + base, (uint32_t)st << 16 | UNK_T);
+                        }
+                    }
+                    wave_sync();
+                }
+                if (gact && gl == 0) {
+                    struct {
+                        const uint32_t *gp;
+                        const uint16_t *id16;
+                        int unk;
+                        __device__ int start(int x) const { return gp[x] == 0xFFFFFFFFu ? -1 : (int)(gp[x] >> 16); }
+                        __device__ int id(int x) const {
+                            const uint32_t b = gp[x];
+                            return b == 0xFFFFFFFFu ? -1 : (b & 0xFFFFu) == UNK_T ? unk : (int)id16[b & 0xFFFFu];
+                        }
+                    } nodes{(const uint32_t *)gp, s_id, T.unk_id};
+                    auto accg = [&](int x) -> uint32_t { return x < 3 ? meta_byte(x) : (uint32_t)pb[srcg + x - 3]; };
+                    auto candg = [&](int st2, int e2, double *) -> int {
+                        int id;
+                        if (st2 == 0) id = e2 - 3 <= Mm ? probe_acc(T, accg, 3, e2 - 3, UC_META) : -1;
+                        else id = e2 - st2 <= Mf ? probe_acc(T, accg, st2, e2 - st2, UC_PIECE) : -1;
+                        return uni_piece_id(id);
+                    };
+                    const uint32_t posg = (jmg >> 6) & 0xFFFu;
+                    uint16_t *const jrg = reinterpret_cast<uint16_t *>(slice + UNI_JR_OFF) + posg;
+                    const int kg = unigram_backtrack(ng, candg, nodes, T.unk_id, [&](int x, int id) { jrg[x] = (uint16_t)id; });
+                    slice[jmg >> 18] = LMARK | UNI_JOB_BIT | (uint32_t)kg << 24 | posg;
+                    s_k[vj] = (uint8_t)kg;
+                }
+                wave_sync();
+            }
+            VIT_STAMP(3);
+        }
+        if (!WIDE && act) {
+            slice[jm >> 18] = LMARK | UNI_JOB_BIT | (uint32_t)k << 24 | pos;
             s_k[v] = (uint8_t)k;
         }
 #ifdef SDL_STAMPS
@@ -1330,7 +1558,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDL_UNI_VWAV
         if (p >= c1) break;
         uint32_t add = 0;
         for (int v = lane; v < njobs; v += 64)
-            if ((int64_t)((s_jm[v] >> 5) & 0xFFFu) < p - c0) add += (uint32_t)s_k[v] - 1u;
+            if ((int64_t)((s_jm[v] >> 6) & 0xFFFu) < p - c0) add += (uint32_t)s_k[v] - 1u;
         add = (uint32_t)lane_bcast((int)wave_incl_sum(add), 63);
         if (lane == 0 && add) atomicAdd(&rec_local[r], add);
     }
@@ -1700,17 +1928,27 @@ hipError_t launch_unigram_chunks(const DevTok &T, const uint8_t *text, int64_t N
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_unigram_chunks, dim3((unsigned)n_chunks), dim3(TOK_THREADS), 0, st, T, text, N, off, R, ranges,
                        tokc, chunk_cnt, chunk_ent, rec_local, W.counters, W.items, W.item_cap, W.err);
-    hipLaunchKernelGGL(k_unigram_viterbi, dim3((unsigned)n_chunks), dim3(64), 0, st, T, N, off, R, ranges, tokc,
+    // the narrow jobs' Viterbi on st; the wide jobs' and the long items beside it on W.side
+    hipStream_t side = st;
+    if (W.side && W.ev_fork && W.ev_join) {
+        e = hipEventRecord(W.ev_fork, st);
+        if (e == hipSuccess) e = hipStreamWaitEvent(W.side, W.ev_fork, 0);
+        if (e != hipSuccess) return e;
+        side = W.side;
+    }
+    hipLaunchKernelGGL(k_unigram_viterbi<false>, dim3((unsigned)n_chunks), dim3(64), 0, st, T, N, off, R, ranges, tokc,
+                       chunk_cnt, rec_local);
+    hipLaunchKernelGGL(k_unigram_viterbi<true>, dim3((unsigned)n_chunks), dim3(64), 0, side, T, N, off, R, ranges, tokc,
                        chunk_cnt, rec_local);
     // a row's candidate ends: <= Mm + 1 ("▁" row) or <= Mf.  Two stages: items of <= 128
     // normalized bytes (nearly all) with a small LDS footprint and more of them in
     // flight, then the rest (<= 512) from the first stage's overflow list.
     const int g1 = W.lane_blocks * 4 / 3;
 #define SDL_UNI_LONG_STAGES(KM)                                                                                     \
-    hipLaunchKernelGGL((k_unigram_long<KM, LONG_NORM1>), dim3((unsigned)g1), dim3(64), 0, st, T, text, N, off, R,    \
+    hipLaunchKernelGGL((k_unigram_long<KM, LONG_NORM1>), dim3((unsigned)g1), dim3(64), 0, side, T, text, N, off, R,  \
                        ranges, W.items, W.item_cap, W.counters, W.counters, tokc, chunk_cnt, rec_local, W.pool,      \
                        W.pool_cap, W.items2, W.items2_cap, W.counters + 4, W.err);                                    \
-    hipLaunchKernelGGL((k_unigram_long<KM, LONG_NORM>), dim3((unsigned)W.lane_blocks), dim3(64), 0, st, T, text, N,  \
+    hipLaunchKernelGGL((k_unigram_long<KM, LONG_NORM>), dim3((unsigned)W.lane_blocks), dim3(64), 0, side, T, text, N,\
                        off, R, ranges, W.items2, W.items2_cap, W.counters + 4, W.counters, tokc, chunk_cnt,           \
                        rec_local, W.pool, W.pool_cap, W.huge, W.huge_cap, W.counters + 3, W.err);
     if (T.maxlen_meta + 1 <= 20 && T.maxlen_first <= 20) {  // smaller LDS: more items in flight
@@ -1721,8 +1959,13 @@ hipError_t launch_unigram_chunks(const DevTok &T, const uint8_t *text, int64_t N
         SDL_UNI_LONG_STAGES(64)
     }
 #undef SDL_UNI_LONG_STAGES
-    hipLaunchKernelGGL(k_unigram_huge, dim3((unsigned)W.huge_blocks), dim3(64), 0, st, T, text, N, off, R, W.counters,
+    hipLaunchKernelGGL(k_unigram_huge, dim3((unsigned)W.huge_blocks), dim3(64), 0, side, T, text, N, off, R, W.counters,
                        tokc, chunk_cnt, rec_local, W.scratch, W.pool, W.pool_cap, W.huge, W.huge_cap, W.err);
+    if (side != st) {
+        e = hipEventRecord(W.ev_join, side);
+        if (e == hipSuccess) e = hipStreamWaitEvent(st, W.ev_join, 0);
+        if (e != hipSuccess) return e;
+    }
     return hipGetLastError();
 }
 

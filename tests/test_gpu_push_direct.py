@@ -88,11 +88,12 @@ def test_unigram_capacity_flag_on_the_fused_small_push(native_lib, records, mode
     """mlm / clm on the t5 tokenizer take the fused small push (k_rows writes the host
     batches, k_downstream_small the status words): a Unigram capacity overflow must still
     fail the call, as it does on the direct and large paths.  SDL_UNI_ITEM_CAP clamps the
-    long-item list so a record with a few > 16-byte words overflows it."""
+    long-item list so a record with a few long items (words past the 48 bytes a Viterbi job
+    takes) overflows it."""
     monkeypatch.setenv("SDL_UNI_ITEM_CAP", "1")
     gt = Bt.GenTokenizer(model, Bt.BatchConfig(4, 128), Bt.Mask(19, 103) if model == Bt.ModelType.Bert else
                          Bt.Gpt(), Bt.TokenizerConfig(native.T5_PROXY_TOKENIZER), chunk=True, seed=3)
-    long_words = " ".join(["internationalization", "characteristically", "uncharacteristically"])
+    long_words = " ".join(["internationalization" * 3, "characteristically" * 3, "uncharacteristically" * 3])
     with pytest.raises(native.SDLError, match="capacity"):
         gt.create_sync_batch(records[0] + " " + long_words)
 

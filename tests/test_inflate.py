@@ -308,6 +308,25 @@ def test_first_member_mode_false_header_candidates(torch, native_lib, records):
 
 
 @pytest.mark.gpu
+def test_first_member_mode_false_header_in_a_large_member(torch, native_lib, records):
+    """A >= 4 MiB member with a planted header pattern whose 4 preceding bytes, read as the
+    false range's ISIZE, pass the 1032:1 bound and overflow the 4 GiB arena: the call must
+    retry past that candidate, not fail with a capacity error."""
+    from streaming_data_loader_amd.device import DeviceBatcher
+    db = DeviceBatcher(batch_size=8, sequence_length=128)
+    rng = np.random.default_rng(7)
+    plant = b"\xf0\xff\xff\xff" + b"\x1f\x8b\x08\x00"  # stored blocks: spelled in the stream (one
+    parts = [rng.integers(0, 256, 700_001, dtype=np.uint8).tobytes() for _ in range(8)]  # may straddle a block)
+    body = plant.join(parts)
+    first = gz_member(body, level=0)
+    assert first.find(plant) > 0 and len(first) >= 4 << 20
+    files = [first + gz_member(b"second member")]
+    rc, out, status, got, _ = device_inflate(torch, db, files, first=True)
+    assert rc == 0, status
+    assert got == [body]
+
+
+@pytest.mark.gpu
 def test_first_member_mode_trailing_garbage_is_the_stated_limit(torch, native_lib, records):
     from streaming_data_loader_amd.device import DeviceBatcher
     db = DeviceBatcher(batch_size=8, sequence_length=128)

@@ -6,5 +6,5 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export OUT=${OUT:-r06prof} TASK=${TASK:-span}
 O=gpurun_out/$OUT; mkdir -p $O
 for c in ${CORPORA:-fixture heldout}; do
-  CORPUS=$c BENCH_ARGS="--no-heldout" bash tools/gpu_prof.sh streaming_data_loader_amd/libsdl_batcher.so "$@" || exit $?
+  CORPUS=$c BENCH_ARGS="--no-heldout" bash tools/gpu_prof.sh ${BASELIB:-streaming_data_loader_amd/libsdl_batcher.so} "$@" || exit $?
 done
