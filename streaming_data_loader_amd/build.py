@@ -136,9 +136,9 @@ def build_gz256():
                  build_dir=os.path.join(REPO, "build", "var", "gz256", "obj"))
 
 
-def build_ablations(levels=(1, 2, 3)):
-    """Diagnostic builds with phases of the tokenize kernel compiled out
-    (SDL_ABLATE=1: first probes only; 2: no WordPiece; 3: load only) -> var/abl<N>/libsdl_batcher.so."""
+def build_ablations(levels=(3,)):
+    """Diagnostic load-only build of the WordPiece chunk kernel (SDL_ABLATE: the window and
+    record bits staged, nothing tokenized) -> var/abl3/libsdl_batcher.so (tools/pmc_calibration.py)."""
     return [build(defines=(f"SDL_ABLATE={n}",), lib=os.path.join(REPO, "var", f"abl{n}", "libsdl_batcher.so"),
                   build_dir=os.path.join(REPO, "build", f"abl{n}")) for n in levels]
 

@@ -205,8 +205,8 @@ static void to_device_entries(HostTokenizer &t) {
             e = cls | 8u | ((nb - 1) << 4) | ((nc - 1) << 6) | (bytes << 8);
         }
     }
-    t.ubmp.resize(0x10000);
-    for (uint32_t cp = 0; cp < 0x10000; ++cp) t.ubmp[cp] = t.uentry[(size_t)t.upage[cp >> 7] * 128 + (cp & 127)];
+    t.ubmp.assign(2 * 0x10000, 0u);  // (entry, WordPiece ISO id: wp_iso_ids) per code point
+    for (uint32_t cp = 0; cp < 0x10000; ++cp) t.ubmp[2 * cp] = t.uentry[(size_t)t.upage[cp >> 7] * 128 + (cp & 127)];
 }
 
 // ---------------------------------------------------------------------------
@@ -233,6 +233,30 @@ static void utf8_append(std::string &o, uint32_t cp) {
     } else {
         o += (char)(0xF0 | (cp >> 18)); o += (char)(0x80 | ((cp >> 12) & 63));
         o += (char)(0x80 | ((cp >> 6) & 63)); o += (char)(0x80 | (cp & 63));
+    }
+}
+
+// The one-char WordPiece id of every BMP char k_wordpiece_chunks' rare pass would probe
+// itself -- ISO class, not a canonical-ordering entry, normalizing to one char (identity:
+// the char's own UTF-8; inline: the entry's bytes) -- as bit 31 | the id of that string as a
+// non-"##" piece of <= maxlen_first bytes, else of [UNK]; 0 for every other char.  The kernel
+// reads it with the char's entry (EARLY_LEADS), so such a char costs one load and no probe.
+static void wp_iso_ids(HostTokenizer &t) {
+    std::unordered_map<std::string, int> ids;
+    for (size_t i = 0; i < t.pieces.size(); ++i) ids[t.pieces[i]] = (int)i;  // (a duplicate keeps its last id)
+    for (uint32_t cp = 0x80; cp < 0x10000; ++cp) {
+        const uint32_t e = t.ubmp[2 * cp];
+        if ((e & 3u) != UC_ISO || (e & 24u) == 16u || !((e & 4u) || ((e & 8u) && ((e >> 6) & 3u) == 0u))) continue;
+        std::string w;
+        if (e & 4u) utf8_append(w, cp);
+        else
+            for (uint32_t q = 0; q <= ((e >> 4) & 3u); ++q) w += (char)((e >> (8 + 8 * q)) & 0xFFu);
+        int id = -1;
+        if ((int)w.size() <= t.maxlen_first) {
+            const auto it = ids.find(w);
+            if (it != ids.end()) id = it->second;
+        }
+        t.ubmp[2 * cp + 1] = 0x80000000u | (uint32_t)(id >= 0 ? id : t.unk_id);
     }
 }
 
@@ -883,7 +907,6 @@ static void load_unigram(const JValue &root, const std::string &data_dir, HostTo
     for (const std::string &w : base_words) {
         add_word(w + ",");
         add_word(w + ".");
-#ifndef SDL_T5_SHORT_WORD_TABLE
         // the next commonest word-table misses in running text: quoted,
         // parenthesised and colon/question/exclamation-ended words, possessives
         if ((int)w.size() + 2 <= UNI_WMAX) {
@@ -892,9 +915,7 @@ static void load_unigram(const JValue &root, const std::string &data_dir, HostTo
             add_word("\"" + w);
             add_word("(" + w);
         }
-#endif
     }
-#ifndef SDL_T5_SHORT_WORD_TABLE
     // sentence-initial and all-caps spellings of the base words (bare, and
     // comma/period-ended): a fifth of the held-out corpus's word-table misses,
     // and 50k entries that still fit the 2^20-slot table
@@ -909,7 +930,6 @@ static void load_unigram(const JValue &root, const std::string &data_dir, HostTo
             add_word(v + ".");
         }
     }
-#endif
     if (t.wres.size() >= (1u << 24)) throw std::runtime_error("word table too large");
     t.wres.push_back(0);
     t.word_table_entries = entries.size() + wentries.size();
@@ -1039,6 +1059,7 @@ void load_tokenizer(const std::string &path, const std::string &data_dir, HostTo
     load_unicode(data_dir + "/bert_uncased_unicode.bin", t);
     check_ascii_and_ids(t);
     to_device_entries(t);
+    wp_iso_ids(t);
 }
 
 }  // namespace sdl

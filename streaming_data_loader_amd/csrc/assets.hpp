@@ -23,7 +23,7 @@ struct HostTokenizer {
     std::vector<uint16_t> upage;
     std::vector<uint32_t> uentry;
     std::vector<uint8_t> upool;
-    std::vector<uint32_t> ubmp;  // device-format entries of the BMP (flat)
+    std::vector<uint32_t> ubmp;  // per BMP code point: device-format entry, WordPiece ISO id (wp_iso_ids)
 
     // ---- device image of the vocabulary ------------------------------------
     std::vector<VSlot> slots;

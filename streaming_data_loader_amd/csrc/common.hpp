@@ -23,14 +23,8 @@ constexpr int HALO_L = 32;                        // look-back bytes staged in L
 constexpr int HALO_R = 32;                        // look-ahead bytes staged in LDS
 constexpr int WIN = HALO_L + CHUNK + HALO_R;      // 1088 bytes of text in LDS
 constexpr int STAGE = CHUNK + 128;                // token slots per chunk (>= tokens owned)
-#ifndef SDL_TOK_UNROLL
-#define SDL_TOK_UNROLL 2
-#endif
-constexpr int TOK_UNROLL = SDL_TOK_UNROLL;        // first probes in flight per lane (2: no spills at 5 waves/SIMD)
-#ifndef SDL_PEND_CAP
-#define SDL_PEND_CAP 256
-#endif
-constexpr int PEND_CAP = SDL_PEND_CAP;            // WordPiece pieces pending the state machine (LDS)
+constexpr int TOK_UNROLL = 2;        // first probes in flight per lane (2: no spills at 5 waves/SIMD)
+constexpr int PEND_CAP = 256;            // WordPiece pieces pending the state machine (LDS)
 constexpr int RB_CAP = 256;                       // record starts listed in LDS per window
 constexpr int MAX_WORD_CHARS = 100;               // WordPiece max_input_chars_per_word
 constexpr int MAX_WORD_BYTES = 4 * MAX_WORD_CHARS + 8;
@@ -151,7 +145,7 @@ constexpr uint32_t CP_KEY = 1u << 8, CP_PREFIX = 1u << 9, CP_INLINE = 1u << 10;
 // Everything a tokenize kernel needs, passed by value as a kernel argument.
 struct DevTok {
     int32_t kind;            // TOK_*
-    const uint32_t *ubmp;    // device Unicode entries of U+0000..U+FFFF (flat)
+    const uint2 *ubmp;       // U+0000..U+FFFF (flat): device Unicode entry, WordPiece one-char ISO id (assets.cpp)
     const uint16_t *upage;   // Unicode page table  [0x110000/128]
     const uint32_t *uentry;  // Unicode blocks      [n_blocks*128]
     const uint8_t *upool;    // normalized strings  (u8 nbytes, u8 nchars, bytes)
@@ -258,16 +252,9 @@ __device__ __forceinline__ int64_t rand_pre_slot(const RowParams &P, int64_t r, 
 // (block b on XCD b % 8): each XCD gets a contiguous run of chunks instead, so a chunk's
 // halo bytes are its neighbours' (the same L2) and each XCD streams its own region of
 // the arena (r04: held-out mlm tokenize 2.33 -> 2.25 ms).  A bijection on [0, gridDim.x).
-#ifndef SDL_XCD_REMAP
-#define SDL_XCD_REMAP 1
-#endif
 __device__ __forceinline__ int64_t xcd_chunk() {
-#if SDL_XCD_REMAP
     const int64_t G = gridDim.x, b = blockIdx.x, x = b & 7, q = G >> 3, rem = G & 7;
     return x * q + (x < rem ? x : rem) + (b >> 3);
-#else
-    return (int64_t)blockIdx.x;
-#endif
 }
 
 }  // namespace sdl

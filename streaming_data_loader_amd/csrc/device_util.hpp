@@ -18,42 +18,41 @@ __device__ __forceinline__ T lane_bcast(T x, int l) {
 
 // DPP data movement for the wave scans below: lanes without a source (or rows
 // outside row_mask) read 0, the identity of every scan here.
-#define SDL_DPP(v, ctrl, rows) ((uint32_t)__builtin_amdgcn_update_dpp(0, (int)(v), (ctrl), (rows), 0xF, false))
+#define DPP_MOV(v, ctrl, rows) ((uint32_t)__builtin_amdgcn_update_dpp(0, (int)(v), (ctrl), (rows), 0xF, false))
 // Inclusive wave64 scan of an associative op with identity 0 in six DPP steps.
-#define SDL_DPP_SCAN(v, COMBINE)                          \
+#define DPP_SCAN(v, COMBINE)                          \
     do {                                                  \
         uint32_t y_;                                      \
-        y_ = SDL_DPP(v, 0x111, 0xF); v = COMBINE(y_, v);  \
-        y_ = SDL_DPP(v, 0x112, 0xF); v = COMBINE(y_, v);  \
-        y_ = SDL_DPP(v, 0x114, 0xF); v = COMBINE(y_, v);  \
-        y_ = SDL_DPP(v, 0x118, 0xF); v = COMBINE(y_, v);  \
-        y_ = SDL_DPP(v, 0x142, 0xA); v = COMBINE(y_, v);  \
-        y_ = SDL_DPP(v, 0x143, 0xC); v = COMBINE(y_, v);  \
+        y_ = DPP_MOV(v, 0x111, 0xF); v = COMBINE(y_, v);  \
+        y_ = DPP_MOV(v, 0x112, 0xF); v = COMBINE(y_, v);  \
+        y_ = DPP_MOV(v, 0x114, 0xF); v = COMBINE(y_, v);  \
+        y_ = DPP_MOV(v, 0x118, 0xF); v = COMBINE(y_, v);  \
+        y_ = DPP_MOV(v, 0x142, 0xA); v = COMBINE(y_, v);  \
+        y_ = DPP_MOV(v, 0x143, 0xC); v = COMBINE(y_, v);  \
     } while (0)
 // The same with identity `id` (DPP lanes without a source read `id`).
-#define SDL_DPP_ID(v, ctrl, rows, id) \
+#define DPP_ID(v, ctrl, rows, id) \
     ((uint32_t)__builtin_amdgcn_update_dpp((int)(id), (int)(v), (ctrl), (rows), 0xF, false))
-#define SDL_DPP_SCAN_ID(v, COMBINE, id)                              \
+#define DPP_SCAN_ID(v, COMBINE, id)                              \
     do {                                                             \
         uint32_t y_;                                                 \
-        y_ = SDL_DPP_ID(v, 0x111, 0xF, id); v = COMBINE(y_, v);      \
-        y_ = SDL_DPP_ID(v, 0x112, 0xF, id); v = COMBINE(y_, v);      \
-        y_ = SDL_DPP_ID(v, 0x114, 0xF, id); v = COMBINE(y_, v);      \
-        y_ = SDL_DPP_ID(v, 0x118, 0xF, id); v = COMBINE(y_, v);      \
-        y_ = SDL_DPP_ID(v, 0x142, 0xA, id); v = COMBINE(y_, v);      \
-        y_ = SDL_DPP_ID(v, 0x143, 0xC, id); v = COMBINE(y_, v);      \
+        y_ = DPP_ID(v, 0x111, 0xF, id); v = COMBINE(y_, v);      \
+        y_ = DPP_ID(v, 0x112, 0xF, id); v = COMBINE(y_, v);      \
+        y_ = DPP_ID(v, 0x114, 0xF, id); v = COMBINE(y_, v);      \
+        y_ = DPP_ID(v, 0x118, 0xF, id); v = COMBINE(y_, v);      \
+        y_ = DPP_ID(v, 0x142, 0xA, id); v = COMBINE(y_, v);      \
+        y_ = DPP_ID(v, 0x143, 0xC, id); v = COMBINE(y_, v);      \
     } while (0)
 // next lane's value (lane 63: 0): DPP wave_shl:1
-__device__ __forceinline__ uint32_t wave_next(uint32_t v) { return SDL_DPP(v, 0x130, 0xF); }
+__device__ __forceinline__ uint32_t wave_next(uint32_t v) { return DPP_MOV(v, 0x130, 0xF); }
 // previous lane's value (lane 0: 0): DPP wave_shr:1
-__device__ __forceinline__ uint32_t wave_prev(uint32_t v) { return SDL_DPP(v, 0x138, 0xF); }
+__device__ __forceinline__ uint32_t wave_prev(uint32_t v) { return DPP_MOV(v, 0x138, 0xF); }
 
 // Inclusive wave64 prefix sum in six DPP steps (the GFX9 wave scan): row_shr
 // 1, 2, 4, 8 within each 16-lane row (lanes without a source add 0), then
 // row_bcast:15 adds row 0's total to row 1 and row 2's to row 3, and
 // row_bcast:31 adds lane 31's running total to rows 2 and 3.  DPP moves data
 // inside the VALU -- no ds_bpermute round trip through the LDS crossbar per step.
-#ifndef SDL_SCAN_SHFL
 __device__ __forceinline__ uint32_t wave_incl_sum(uint32_t x) {
     int v = (int)x;
     v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, false);  // row_shr:1
@@ -64,17 +63,6 @@ __device__ __forceinline__ uint32_t wave_incl_sum(uint32_t x) {
     v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
     return (uint32_t)v;
 }
-#else  // (diagnostic A/B) six ds_bpermute shuffle steps
-__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t x) {
-    const int lane = lane_id();
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        uint32_t y = __shfl_up(x, d, 64);
-        if (lane >= d) x += y;
-    }
-    return x;
-}
-#endif
 
 // Exclusive prefix sum over a workgroup of NT threads; *total = sum of all.
 // `scratch` needs NT/64 words.  Contains two barriers.
@@ -112,7 +100,7 @@ template <int NT>
 __device__ __forceinline__ uint32_t block_excl_last_scan(uint32_t v, uint32_t *scratch) {
     const int lane = lane_id(), wid = (int)(threadIdx.x >> 6);
     uint32_t x = v;  // (0 = pass-through: the DPP scan's identity)
-    SDL_DPP_SCAN(x, last_set);
+    DPP_SCAN(x, last_set);
     const uint32_t ex = wave_prev(x);
     if constexpr (NT == 64) {  // one wave: nothing carries in (one barrier kept, as above)
         (void)lane;

@@ -41,13 +41,10 @@ namespace sdl {
 namespace {
 
 constexpr int LB = 10, DB = 10;    // primary table bits: lit/len, dist (long_decode covers 11..15)
-#ifndef SDL_GZ_STAGE
-#define SDL_GZ_STAGE 1024
-#endif
 #ifndef SDL_GZ_OBUF
 #define SDL_GZ_OBUF 512
 #endif
-constexpr int IN_STAGE = SDL_GZ_STAGE;  // staged compressed bytes per wave
+constexpr int IN_STAGE = 1024;  // staged compressed bytes per wave
 constexpr int OBUF = SDL_GZ_OBUF;       // output batch bytes
 constexpr int MLCAP = OBUF / 8;         // matches per batch
 #ifndef SDL_GZ_ALLOW_SMALL_OBUF  // (diagnostic builds only: exercises the no-progress exit below)
@@ -1006,7 +1003,7 @@ __device__ bool wave_header_ok(const Peek &peek, uint32_t at, int64_t lim, uint1
         const uint32_t endP = (uint32_t)__builtin_amdgcn_readlane((int)(P + nn), lv);
         if (endP > total) return false;                   // a repeat past the last length
         uint32_t sc = valid && s != 16 ? 0x100u | (s < 16 ? s : 0u) : 0u;
-        SDL_DPP_SCAN(sc, last_set);
+        DPP_SCAN(sc, last_set);
         const uint32_t ex = wave_prev(sc);
         const uint32_t before = (ex & 0x100u) ? ex : prev;
         if (__ballot(valid && s == 16 && !(before & 0x100u))) return false;  // '16' with no length before it

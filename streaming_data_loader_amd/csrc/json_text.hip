@@ -430,13 +430,13 @@ __device__ __forceinline__ JMask jmask(const uint4 &x, int64_t p0, int64_t s, in
 // Exclusive "last set wins" scan over the wave: x = 0x100 | bit sets the carry,
 // 0 passes through; returns the carry before this lane (0 if none).
 __device__ __forceinline__ uint32_t wave_excl_last(uint32_t x) {
-    SDL_DPP_SCAN(x, last_set);  // (DPP steps, device_util.hpp)
+    DPP_SCAN(x, last_set);  // (DPP steps, device_util.hpp)
     return wave_prev(x);
 }
 __device__ __forceinline__ uint32_t xor_op(uint32_t a, uint32_t b) { return a ^ b; }
 __device__ __forceinline__ uint32_t wave_excl_xor(uint32_t x) {
     uint32_t v = x;
-    SDL_DPP_SCAN(v, xor_op);
+    DPP_SCAN(v, xor_op);
     return v ^ x;
 }
 

@@ -19,8 +19,7 @@ hipError_t launch_chunk_ranges(const uint64_t *off, int64_t R, int64_t N, uint32
 // (after launch_chunk_ranges), for chunks [c_begin, c_end) (c_end < 0: all).
 hipError_t launch_wordpiece_chunks(const DevTok &T, const uint8_t *text, int64_t N, const uint64_t *off, int64_t R,
                                    uint32_t *ranges, uint32_t *tokc, uint32_t *chunk_cnt, uint32_t *rec_local,
-                                   hipStream_t st, int64_t c_begin = 0, int64_t c_end = -1, bool self = false,
-                                   uint32_t *rb1 = nullptr, uint32_t *zero1 = nullptr);
+                                   hipStream_t st, int64_t c_begin = 0, int64_t c_end = -1);
 
 // tokenize_bpe.hip: same outputs for a byte-level BPE (gpt2) tokenizer.  Pieces
 // longer than 64 bytes go through `long_list` (capacity long_cap) and are

@@ -346,15 +346,9 @@ hipError_t launch_row_map(const uint32_t *row_off, int64_t R, uint32_t *row_rec,
 // (k_rows<2>: 74 -> 71 VGPRs, no spills; mlm rows 0.270 -> 0.262 ms, multi-label
 // 0.080 -> 0.074; 8 spills and is slower); MR >= 4 and rng_mode 1 as they come
 // (asking 5-6 of them spills)
-#ifndef SDL_ROWS_WAVES
-#define SDL_ROWS_WAVES 7
-#endif
-#ifndef SDL_ROWS_WAVES4
-#define SDL_ROWS_WAVES4 1
-#endif
-#ifndef SDL_ROWS_WAVES_RM1
-#define SDL_ROWS_WAVES_RM1 6  // (r04: left to the compiler, 103 VGPRs, 4 waves: rows 0.347 ms; 7 spills 20 B)
-#endif
+constexpr int ROWS_WAVES = 7;
+constexpr int ROWS_WAVES4 = 1;
+constexpr int ROWS_WAVES_RM1 = 6;  // (r04: left to the compiler, 103 VGPRs, 4 waves: rows 0.347 ms; 7 spills 20 B)
 __device__ __forceinline__ uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
 #define CC_QR(a, b, c, d)                                                         \
     a += b; d ^= a; d = rotl32(d, 16); c += d; b ^= c; b = rotl32(b, 12);         \
@@ -486,7 +480,7 @@ __device__ __forceinline__ void rand_rows16(const RowParams &P, int nrows, uint6
 // LATE (RM1 only): the second pass over the rows the first one left (no mask bits from beside the
 // tokenizer): its waves walk their masks in place, 4 rows at a time (rand_rows16).
 template <int MR, bool RM1, bool LATE = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MR >= 4 ? SDL_ROWS_WAVES4 : LATE ? 4 : RM1 ? SDL_ROWS_WAVES_RM1 : SDL_ROWS_WAVES, 8))) void k_rows(RowParams P, const uint32_t *__restrict__ tok,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MR >= 4 ? ROWS_WAVES4 : LATE ? 4 : RM1 ? ROWS_WAVES_RM1 : ROWS_WAVES, 8))) void k_rows(RowParams P, const uint32_t *__restrict__ tok,
                                               const uint32_t *__restrict__ rec_tok, const uint32_t *__restrict__ rec_cnt,
                                               const uint32_t *__restrict__ row_off, const uint32_t *__restrict__ row_rec,
                                               SegSel sel, int64_t rows_cap, RowOut out) {
@@ -584,16 +578,16 @@ hipError_t launch_downstream_small(const SmallDown &d, const RowParams &P, const
     if (d.rows && ((P.rng_mode == 1 && P.task == 0) || (P.task != 0 && P.task != 1)))
         return hipErrorInvalidValue;  // (rng_mode 1 masks need k_rows' passes; span has its own rows)
     const bool tiny = R <= 64 && n_chunks <= 64;
-#define SDL_DS(M)                                                                                                    \
+#define LAUNCH_DS(M)                                                                                                    \
     if (tiny) hipLaunchKernelGGL(k_downstream_tiny<M>, dim3(1), dim3(64), 0, st, d, P, off, R, N, n_chunks);        \
     else hipLaunchKernelGGL(k_downstream_small<M>, dim3(1), dim3(SCAN_SMALL_NT), 0, st, d, P, off, R, N, n_chunks)
-    if (!d.rows) SDL_DS(0);
-    else if (MR <= 1) SDL_DS(1);
-    else if (MR <= 2) SDL_DS(2);
-    else if (MR <= 4) SDL_DS(4);
-    else if (MR <= 8) SDL_DS(8);
+    if (!d.rows) LAUNCH_DS(0);
+    else if (MR <= 1) LAUNCH_DS(1);
+    else if (MR <= 2) LAUNCH_DS(2);
+    else if (MR <= 4) LAUNCH_DS(4);
+    else if (MR <= 8) LAUNCH_DS(8);
     else return hipErrorInvalidValue;
-#undef SDL_DS
+#undef LAUNCH_DS
     return hipGetLastError();
 }
 
@@ -788,10 +782,7 @@ __global__ __launch_bounds__(256) void k_rand_spec_list(RowParams P, uint32_t *_
 __device__ __forceinline__ int64_t rand_rec_of(const RowParams &P, const uint32_t *list, int64_t t) {
     return t < P.mask_R ? t : (int64_t)list[1 + (t - P.mask_R)];
 }
-#ifndef SDL_RAND_NR
-#define SDL_RAND_NR 1
-#endif
-constexpr int RAND_NR = SDL_RAND_NR;  // rows per lane in k_mask_rand_rec
+constexpr int RAND_NR = 1;  // rows per lane in k_mask_rand_rec
 __global__ __launch_bounds__(256) void k_mask_rand_rec(RowParams P, const uint32_t *__restrict__ list,
                                                        uint16_t *__restrict__ jbuf) {
     const int lane = lane_id();
@@ -850,13 +841,13 @@ hipError_t launch_mask_rand_rec(const RowParams &P, uint32_t *list, uint32_t *sp
     const int64_t wb = (ns + 3) / 4;
     const dim3 g((unsigned)(wb < 16384 ? wb : 16384));
     const int MR4 = (P.S + 63) / 64;
-#define SDL_BITS(M) hipLaunchKernelGGL(k_mask_bits_rec<M>, g, dim3(256), 0, st, P, (const uint32_t *)list, (const uint16_t *)jbuf, bits)
-    if (MR4 <= 2) SDL_BITS(2);
-    else if (MR4 <= 4) SDL_BITS(4);
-    else if (MR4 <= 8) SDL_BITS(8);
-    else if (MR4 <= 16) SDL_BITS(16);
-    else SDL_BITS(32);
-#undef SDL_BITS
+#define LAUNCH_BITS(M) hipLaunchKernelGGL(k_mask_bits_rec<M>, g, dim3(256), 0, st, P, (const uint32_t *)list, (const uint16_t *)jbuf, bits)
+    if (MR4 <= 2) LAUNCH_BITS(2);
+    else if (MR4 <= 4) LAUNCH_BITS(4);
+    else if (MR4 <= 8) LAUNCH_BITS(8);
+    else if (MR4 <= 16) LAUNCH_BITS(16);
+    else LAUNCH_BITS(32);
+#undef LAUNCH_BITS
     return hipGetLastError();
 }
 
@@ -948,11 +939,9 @@ hipError_t launch_rows(const RowParams &P, const uint32_t *tok, const uint32_t *
                        hipStream_t st, hipStream_t st_late) {
     if (!st_late) st_late = st;
     if (rows_cap == 0) return hipSuccess;
-#ifndef SDL_ROWS_GRID_CAP
-#define SDL_ROWS_GRID_CAP 16384
-#endif
+constexpr int ROWS_GRID_CAP = 16384;
     const int64_t want = (rows_cap + 3) / 4;
-    const unsigned grid = (unsigned)(want < SDL_ROWS_GRID_CAP ? want : SDL_ROWS_GRID_CAP);
+    const unsigned grid = (unsigned)(want < ROWS_GRID_CAP ? want : ROWS_GRID_CAP);
     const int MR = (P.S + 255) / 256;
     if (P.label_width > 256 * MR) return hipErrorInvalidValue;
     const bool rm1 = P.task == 0 && P.rng_mode == 1;
@@ -961,7 +950,7 @@ hipError_t launch_rows(const RowParams &P, const uint32_t *tok, const uint32_t *
     // (rng_mode 1: the late pass scans 256 rows a block)
     const int64_t want_late = (rows_cap + 255) / 256;
     const unsigned grid_late = (unsigned)(want_late < 2048 ? want_late : 2048);
-#define SDL_ROWS(MM)                                                                                                 \
+#define LAUNCH_ROWS(MM)                                                                                                 \
     if (rm1) {                                                                                                        \
         hipLaunchKernelGGL((k_rows<MM, true>), dim3(grid), dim3(256), 0, st, P, tok, rec_tok, rec_cnt, row_off,      \
                            row_rec, sel, rows_cap, out);                                                              \
@@ -970,12 +959,12 @@ hipError_t launch_rows(const RowParams &P, const uint32_t *tok, const uint32_t *
     } else                                                                                                            \
         hipLaunchKernelGGL((k_rows<MM, false>), dim3(grid), dim3(256), 0, st, P, tok, rec_tok, rec_cnt, row_off,     \
                            row_rec, sel, rows_cap, out)
-    if (MR <= 1) SDL_ROWS(1);
-    else if (MR <= 2) SDL_ROWS(2);
-    else if (MR <= 4) SDL_ROWS(4);
-    else if (MR <= 8) SDL_ROWS(8);
+    if (MR <= 1) LAUNCH_ROWS(1);
+    else if (MR <= 2) LAUNCH_ROWS(2);
+    else if (MR <= 4) LAUNCH_ROWS(4);
+    else if (MR <= 8) LAUNCH_ROWS(8);
     else return hipErrorInvalidValue;
-#undef SDL_ROWS
+#undef LAUNCH_ROWS
     return hipGetLastError();
 }
 
@@ -1189,14 +1178,10 @@ struct SpanPass {  // one pass of a round (LDS): cursors and lengths
 
 __device__ __forceinline__ void st_nt(int32_t *p, int32_t v) { __builtin_nontemporal_store(v, p); }
 
-#ifndef SDL_SPAN_WAVES
-#define SDL_SPAN_WAVES 6  // (RAND 0) 75 VGPRs, no spills: 0.507 -> 0.428 ms; 7 and 8 spill
-#endif
-#ifndef SDL_SPAN_GRID_CAP
-#define SDL_SPAN_GRID_CAP 16384  // with 6 waves per SIMD: 0.428 -> 0.414 ms
-#endif
+constexpr int SPAN_WAVES = 6;  // (RAND 0) 75 VGPRs, no spills: 0.507 -> 0.428 ms; 7 and 8 spill
+constexpr int SPAN_GRID_CAP = 16384;  // with 6 waves per SIMD: 0.428 -> 0.414 ms
 template <int RAND>  // draws: 0 the Philox contract, 1 the row's StdRng (rng_mode 1)
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RAND ? 1 : SDL_SPAN_WAVES, 8))) void k_rows_span(RowParams P, const uint32_t *__restrict__ tok,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RAND ? 1 : SPAN_WAVES, 8))) void k_rows_span(RowParams P, const uint32_t *__restrict__ tok,
                                                    const uint32_t *__restrict__ rec_tok,
                                                    const uint32_t *__restrict__ rec_cnt,
                                                    const uint32_t *__restrict__ row_off,
@@ -1506,7 +1491,7 @@ __global__ __launch_bounds__(256) void k_span_plan(RowParams P, const uint32_t *
     if ((threadIdx.x & 63) == 0 && bad) atomicAdd(err, bad);
 }
 
-#define SDL_MAXU(a, b) ((a) > (b) ? (a) : (b))
+#define MAX_U32(a, b) ((a) > (b) ? (a) : (b))
 // Positions [0, W) of one plane of a row, lane L holding 256 m + 4 L + w: the
 // owner pass of each position = the max-scan of `mk` (pass p marked at its
 // first position); val(q, owner) gives the value; positions >= end get
@@ -1524,11 +1509,11 @@ __device__ __forceinline__ void span_plane(int32_t *__restrict__ o, int W, int e
         for (int w = 0; w < 4; ++w) {
             const int q = q0 + w;
             const uint32_t m = q < end ? (uint32_t)mk[q] : 0u;
-            run = SDL_MAXU(run, m);
+            run = MAX_U32(run, m);
             own[w] = run;
         }
         uint32_t x = run;
-        SDL_DPP_SCAN(x, SDL_MAXU);
+        DPP_SCAN(x, MAX_U32);
         // (the DPP read once, unconditionally: inside the macro's ternary it was evaluated
         // twice and the compiler made the second a branch -- a cross-lane read under a
         // partial exec mask, which reads 0 from the inactive neighbours)
@@ -1539,7 +1524,7 @@ __device__ __forceinline__ void span_plane(int32_t *__restrict__ o, int W, int e
 #pragma unroll
         for (int w = 0; w < 4; ++w) {
             const int q = q0 + w;
-            v[w] = q < end ? val(q, SDL_MAXU(own[w], before)) : tail(q);
+            v[w] = q < end ? val(q, MAX_U32(own[w], before)) : tail(q);
         }
         if (vec) {
             typedef int32_t v4i __attribute__((ext_vector_type(4)));
@@ -1552,10 +1537,7 @@ __device__ __forceinline__ void span_plane(int32_t *__restrict__ o, int W, int e
     }
 }
 
-#ifndef SDL_SPAN_TABL
-#define SDL_SPAN_TABL 128
-#endif
-constexpr int SPAN_TABL = SDL_SPAN_TABL;  // plan entries per row held in LDS (the rest read from the plan)
+constexpr int SPAN_TABL = 128;  // plan entries per row held in LDS (the rest read from the plan)
 
 __global__ __launch_bounds__(256) void k_span_write(RowParams P, const uint32_t *__restrict__ tok,
                                                     const uint32_t *__restrict__ rec_tok,
@@ -1684,7 +1666,7 @@ hipError_t launch_rows_span(const RowParams &P, const uint32_t *tok, const uint3
             hipLaunchKernelGGL(k_span_plan<0>, dim3(pgrid), dim3(256), 0, st, P, rec_cnt, row_off, row_rec, sel,
                                rows_cap, *pl, err);
         const int64_t want = (rows_cap + 3) / 4;
-        const unsigned grid = (unsigned)(want < SDL_SPAN_GRID_CAP ? want : SDL_SPAN_GRID_CAP);
+        const unsigned grid = (unsigned)(want < SPAN_GRID_CAP ? want : SPAN_GRID_CAP);
         const size_t dyn = (size_t)4 * 4 * (P.S + ((P.S + P.label_width + 1) >> 1));
         hipLaunchKernelGGL(k_span_write, dim3(grid), dim3(256), dyn, st, P, tok, rec_tok, rec_cnt, row_off, row_rec,
                            sel, rows_cap, out, *pl);
@@ -1700,7 +1682,7 @@ hipError_t launch_rows_span(const RowParams &P, const uint32_t *tok, const uint3
         return hipGetLastError();
     }
     const int64_t want = (rows_cap + 3) / 4;
-    const unsigned grid = (unsigned)(want < SDL_SPAN_GRID_CAP ? want : SDL_SPAN_GRID_CAP);
+    const unsigned grid = (unsigned)(want < SPAN_GRID_CAP ? want : SPAN_GRID_CAP);
     const size_t dyn = (size_t)4 * P.S * sizeof(int32_t);  // s_rid
     if (P.rng_mode == 1)
         hipLaunchKernelGGL(k_rows_span<1>, dim3(grid), dim3(256), dyn, st, P, tok, rec_tok, rec_cnt, row_off, row_rec,

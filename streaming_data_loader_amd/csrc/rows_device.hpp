@@ -8,10 +8,7 @@
 
 namespace sdl {
 
-#ifndef SDL_COMPACT_CPW
-#define SDL_COMPACT_CPW 4
-#endif
-constexpr int COMPACT_CPW = SDL_COMPACT_CPW;  // chunks per wave: their loads are in flight together
+constexpr int COMPACT_CPW = 4;  // chunks per wave: their loads are in flight together
 // one wave: chunks [cb, cb + COMPACT_CPW).  PART 1: only when the call has no long items, 2: only
 // when it has (separate kernels keep the plain copy's registers), 0: either.
 template <int PART = 0>
@@ -249,10 +246,8 @@ __device__ __forceinline__ void select_k_smallest(const uint32_t (&key)[MR][4], 
 // keys below it in ~3-4 counts instead of the radix descent's ~log2(S) + 2.
 // Any threshold with exactly k keys below it marks the same k-smallest set; a
 // tie at the k-th key (no such threshold) or a slow bracket falls back to the
-// radix select.  (SDL_ROWS_INTERP_STEPS=0: the radix select alone.)
-#ifndef SDL_ROWS_INTERP_STEPS
-#define SDL_ROWS_INTERP_STEPS 8
-#endif
+// radix select.
+constexpr int ROWS_INTERP_STEPS = 8;
 template <int MR>
 __device__ __forceinline__ void select_k_smallest_interp(const uint32_t (&key)[MR][4], int k, int nvalid,
                                                          bool (&sel)[MR][4]) {
@@ -260,7 +255,7 @@ __device__ __forceinline__ void select_k_smallest_interp(const uint32_t (&key)[M
         uint32_t lo = 0, hi = 0xFFFFFFFFu;  // count(key < lo) = c_lo < k < c_hi ~ count(key < hi)
         int c_lo = 0, c_hi = nvalid;
 #pragma unroll 1
-        for (int it = 0; it < SDL_ROWS_INTERP_STEPS && hi - lo > 1u; ++it) {
+        for (int it = 0; it < ROWS_INTERP_STEPS && hi - lo > 1u; ++it) {
             const float f = ((float)(k - c_lo) + 0.5f) / (float)(c_hi - c_lo);
             uint32_t cand = lo + (uint32_t)((float)(hi - lo) * f);
             cand = cand <= lo ? lo + 1u : cand >= hi ? hi - 1u : cand;
@@ -292,12 +287,8 @@ __device__ __forceinline__ void select_k_smallest_interp(const uint32_t (&key)[M
 __device__ __forceinline__ void store4(int32_t *p, int j0, int S, bool vec, int32_t a, int32_t b, int32_t c,
                                        int32_t d) {
     if (vec) {  // the planes stream out: non-temporal, they are not re-read by this pass
-#ifdef SDL_ROWS_TEMPORAL
-        if (j0 < S) *reinterpret_cast<int4 *>(p + j0) = make_int4(a, b, c, d);
-#else
         typedef int32_t v4i __attribute__((ext_vector_type(4)));
         if (j0 < S) __builtin_nontemporal_store(v4i{a, b, c, d}, reinterpret_cast<v4i *>(p + j0));
-#endif
     } else {
         if (j0 < S) p[j0] = a;
         if (j0 + 1 < S) p[j0 + 1] = b;
@@ -406,11 +397,7 @@ __device__ __forceinline__ void row_one(const RowParams &P, const uint32_t *__re
                 key[m][2] = j0 + 2 < S ? c.z : 0xFFFFFFFFu;
                 key[m][3] = j0 + 3 < S ? c.w : 0xFFFFFFFFu;
             }
-#if SDL_ROWS_INTERP_STEPS > 0
             select_k_smallest_interp<MR>(key, P.mask_length, S < 256 * MR ? S : 256 * MR, sel);
-#else
-            select_k_smallest<MR>(key, P.mask_length, sel);
-#endif
         }
 #pragma unroll
         for (int m = 0; m < MR; ++m) {

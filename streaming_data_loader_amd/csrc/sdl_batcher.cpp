@@ -292,12 +292,8 @@ struct sdl_batcher {
     DevBuf<uint2> span_tab, span_meta;
     DevBuf<uint32_t> span_ovf;
     bool span_two_phase = env_int0("SDL_SPAN_TWO_PHASE", 0) != 0;
-    bool small_calls = env_int0("SDL_SMALL_CALLS", 1) != 0;  // k_downstream_small + folded record bounds
-    bool small_rows = env_int0("SDL_SMALL_ROWS", 1) != 0;    // ... which also writes mlm (Philox) / clm rows
     // rng_mode 1: chunk-0 rows walked beside the tokenizer (0: every row by its k_rows wave)
     bool rand_rec0 = env_int0("SDL_RAND_REC0", 1) != 0;
-    bool rand_rec_serial = env_int0("SDL_RAND_REC_SERIAL", 0) != 0;  // (diagnostic: the walk on the main stream)
-    bool rand_late_s2 = env_int0("SDL_RAND_LATE_S2", 0) != 0;  // (diagnostic: the late pass on stream2)
     // ... and chunk 1 of records of >= (S - frame + 1) / rho bytes (WordPiece/BPE give ~0.2-0.3 ids
     // per byte; SDL_RAND_SPEC_RHO_PCT=0: chunk 0 only)
     double rand_spec_rho = env_int0("SDL_RAND_SPEC_RHO_PCT", 25) / 100.0;
@@ -350,9 +346,6 @@ struct sdl_batcher {
         size_t bytes = 0;
         const uint64_t *h_off = nullptr;  // the offsets in the mapped blob
     } fused_h2d;
-    bool fused_h2d_on = env_int0("SDL_FUSED_H2D", 1) != 0;
-    bool self_ranges_on = env_int0("SDL_SELF_RANGES", 0) != 0;  // (measured neutral: 43.0 vs 43.0 us)
-    bool self_ranges = false;  // this push: zero-copy, the WordPiece kernel finds its ranges
     void *blob_dev = nullptr;               // pin_blob's device address ...
     const uint8_t *blob_dev_host = nullptr;  // ... for this host buffer
     DevBuf<uint8_t> h2d_blob;
@@ -388,7 +381,6 @@ struct sdl_batcher {
     hipStream_t stream2 = nullptr;
     hipStream_t stream_u = nullptr;  // unigram: the wide-job Viterbi and the long items beside the narrow jobs
     hipEvent_t uni_ev[2] = {nullptr, nullptr};
-    bool uni_side = env_int0("SDL_UNI_SIDE", 1) != 0;  // (A/B: 0 runs them all on the handle's stream)
     std::vector<hipEvent_t> pipe_ev;
     DevBuf<uint32_t> seg_rb;
     int seg_target = env_int("SDL_SEGMENTS", 1);
@@ -516,16 +508,14 @@ struct sdl_batcher {
         auto mark = [&](int i) {
             if (profiling) HIP_TRY(hipEventRecord(ev[i], st));
         };
-        const bool small = small_calls && !piped && !profiling && n_chunks <= SMALL_CHUNKS && R <= 8192;
+        const bool small = !piped && !profiling && n_chunks <= SMALL_CHUNKS && R <= 8192;
         mark(0);
         // (one segment: k_chunk_ranges also writes its record bounds and zeroes the label error word)
-        const bool fold = small_calls && sc.K == 1 && n_chunks > 0;
-        // (a small push's H2D rides along: fused_h2d, set by process_host; or none at all: self_ranges)
-        const bool self = self_ranges && small && fold && dt.kind == TOK_WORDPIECE && R <= 63;
-        if (!self)
-            HIP_TRY(launch_chunk_ranges(fused_h2d.bytes ? fused_h2d.h_off : d_off, R, N, ranges.p, st,
-                                        fold ? seg_rb.p : nullptr, fold && (multi() || single()) ? lab_err.p : nullptr,
-                                        fused_h2d.src, fused_h2d.dst, fused_h2d.bytes));
+        const bool fold = sc.K == 1 && n_chunks > 0;
+        // (a small push's H2D rides along: fused_h2d, set by process_host)
+        HIP_TRY(launch_chunk_ranges(fused_h2d.bytes ? fused_h2d.h_off : d_off, R, N, ranges.p, st,
+                                    fold ? seg_rb.p : nullptr, fold && (multi() || single()) ? lab_err.p : nullptr,
+                                    fused_h2d.src, fused_h2d.dst, fused_h2d.bytes));
         fused_h2d = FusedH2D{};
         // rng_mode 1: a row's masks depend on (seed, record, chunk) alone, so the rows known before
         // tokenizing -- chunk 0 of every record, chunk 1 of records long enough to need one at
@@ -549,9 +539,8 @@ struct sdl_batcher {
             HIP_TRY(hipEventRecord(rand_ev[0], st));  // (the last call's rows have read mask_bits0)
             HIP_TRY(hipStreamWaitEvent(stream2, rand_ev[0], 0));
             p.mask_bits0 = mask_bits0.p;
-            hipStream_t rs = rand_rec_serial ? st : stream2;
-            HIP_TRY(launch_mask_rand_rec(p, spec_list.p, spec_pos.p, mask_j0.p, mask_bits0.p, rs));
-            HIP_TRY(hipEventRecord(rand_ev[1], rs));
+            HIP_TRY(launch_mask_rand_rec(p, spec_list.p, spec_pos.p, mask_j0.p, mask_bits0.p, stream2));
+            HIP_TRY(hipEventRecord(rand_ev[1], stream2));
         }
         if (!fold) HIP_TRY(launch_seg_bounds(ranges.p, sc, R, seg_rb.p, st));
         if (!fold && (multi() || single())) HIP_TRY(hipMemsetAsync(lab_err.p, 0, 4, st));
@@ -572,7 +561,7 @@ struct sdl_batcher {
                         rec_rows.p, row_off.p, row_rec.p, fused_done ? fuse_stat : nullptr,
                         uni ? uni_err.p : nullptr, 0, out};
             // mlm (Philox) / clm rows in the same workgroup, no k_rows launch
-            d.rows = small_rows && fused_done && !rm1 ? 1 : 0;
+            d.rows = fused_done && !rm1 ? 1 : 0;
             return d;
         };
         auto downstream = [&](int k, hipStream_t s) {
@@ -625,15 +614,7 @@ struct sdl_batcher {
             } else {
                 // rng_mode 1: k_rows waits for the rows walked beside the tokenizer and walks the rest
                 // (and walks the rows past the guess in a second pass)
-                if (rm1 && rec0 && rand_late_s2) {  // (diagnostic: measured slower, the late pass starved)
-                    HIP_TRY(hipStreamWaitEvent(s, rand_ev[1], 0));
-                    HIP_TRY(hipEventRecord(rand_ev[2], s));
-                    HIP_TRY(hipStreamWaitEvent(stream2, rand_ev[2], 0));
-                    HIP_TRY(launch_rows(p, tok_ids.p, rec_tok.p, rec_cnt.p, row_off.p, row_rec.p, sel, rows_cap, out, s,
-                                        stream2));
-                    HIP_TRY(hipEventRecord(rand_ev[3], stream2));
-                    HIP_TRY(hipStreamWaitEvent(s, rand_ev[3], 0));
-                } else if (rm1 && rec0) {
+                if (rm1 && rec0) {
                     HIP_TRY(hipStreamWaitEvent(s, rand_ev[1], 0));
                     HIP_TRY(launch_rows(p, tok_ids.p, rec_tok.p, rec_cnt.p, row_off.p, row_rec.p, sel, rows_cap, out, s));
                 } else if (!rows_done) {
@@ -653,7 +634,7 @@ struct sdl_batcher {
             // chunk's arena: N / 8 + n_chunks bounds every realistic text (an
             // overflow is flagged in d_tokenize_errors); their ids go to the pool
             // long items: one wave each; 256 CUs x 9 resident (k_unigram_long<20>: 17 KB of LDS, 154 VGPRs)
-            const int lane_blocks = (int)env_int("SDL_UNI_LONG_BLOCKS", 2304), huge_blocks = 8;
+            const int lane_blocks = 2304, huge_blocks = 8;
             uni_counters.ensure(8);
             uni_err.ensure(1);
             uni_items.ensure((size_t)(N / 8 + n_chunks + 64));
@@ -664,14 +645,14 @@ struct sdl_batcher {
             chunk_ent.ensure((size_t)n_chunks + 1);
             uint32_t item_cap = (uint32_t)std::min<size_t>(uni_items.cap, 0xFFFFFFFFu);
             if (uni_item_cap) item_cap = std::min(item_cap, uni_item_cap);
-            if (uni_side && !stream_u) {
+            if (!stream_u) {
                 HIP_TRY(hipStreamCreateWithFlags(&stream_u, hipStreamNonBlocking));
                 for (auto &e : uni_ev) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
             }
             UniWork W{uni_counters.p, uni_items.p, item_cap, uni_pool.p,
                       (uint32_t)std::min<size_t>(uni_pool.cap, 0x3FFFFFFF), uni_huge.p, (uint32_t)uni_huge.cap,
                       uni_items2.p, (uint32_t)uni_items2.cap, uni_scratch.p, lane_blocks, huge_blocks, uni_err.p,
-                      uni_side ? stream_u : nullptr, uni_ev[0], uni_ev[1]};
+                      stream_u, uni_ev[0], uni_ev[1]};
             HIP_TRY(launch_unigram_chunks(dt, d_text, N, d_off, R, ranges.p, tokc.p, chunk_cnt.p, chunk_ent.p,
                                           rec_local.p, W, st));
             downstream(0, st);
@@ -688,8 +669,7 @@ struct sdl_batcher {
             downstream(0, st);
         } else if (!piped) {
             HIP_TRY(launch_wordpiece_chunks(dt, d_text, N, d_off, R, ranges.p, tokc.p, chunk_cnt.p, rec_local.p, st, 0,
-                                            -1, self, self ? seg_rb.p : nullptr,
-                                            self && (multi() || single()) ? lab_err.p : nullptr));
+                                            -1));
             downstream(0, st);
         } else {
             ensure_pipe_events(sc.K);
@@ -759,32 +739,18 @@ struct sdl_batcher {
         // a small push (<= 64 KiB staged): k_chunk_ranges copies the blob itself, so the stream has
         // one operation fewer before the tokenizer (the few KB cross PCIe as the kernel's loads)
         fused_h2d = FusedH2D{};
-        self_ranges = false;
         const uint8_t *d_text = h2d_blob.p;
         const uint64_t *d_off = reinterpret_cast<const uint64_t *>(h2d_blob.p + x_off);
-        if (fused_h2d_on && h2d_bytes <= (64u << 10) && !profiling) {
+        if (h2d_bytes <= (64u << 10) && !profiling) {
             if (blob_dev_host != pin_blob.p) {  // (once per staging buffer)
                 HIP_TRY(hipHostGetDevicePointer(&blob_dev, pin_blob.p, 0));
                 blob_dev_host = pin_blob.p;
             }
             const uint8_t *dsrc = static_cast<const uint8_t *>(blob_dev);
-            if (self_ranges_on && dt.kind == TOK_WORDPIECE && R <= 63) {
-                // a per-record WordPiece push: the kernels read the mapped blob itself and the
-                // tokenizer finds its record ranges (k_wordpiece_chunks<true>): no copy, no
-                // k_chunk_ranges -- the tokenizer is the stream's first operation
-                self_ranges = true;
-                d_text = dsrc;
-                d_off = reinterpret_cast<const uint64_t *>(dsrc + x_off);
-                if (with_labels) {
-                    d_labels = reinterpret_cast<const uint32_t *>(dsrc + x_lab);
-                    d_label_off = reinterpret_cast<const uint64_t *>(dsrc + x_loff);
-                }
-            } else {
-                fused_h2d.src = dsrc;
-                fused_h2d.dst = h2d_blob.p;
-                fused_h2d.bytes = h2d_bytes;
-                fused_h2d.h_off = reinterpret_cast<const uint64_t *>(dsrc + x_off);
-            }
+            fused_h2d.src = dsrc;
+            fused_h2d.dst = h2d_blob.p;
+            fused_h2d.bytes = h2d_bytes;
+            fused_h2d.h_off = reinterpret_cast<const uint64_t *>(dsrc + x_off);
         } else {
             HIP_TRY(hipMemcpyAsync(h2d_blob.p, pin_blob.p, h2d_bytes, hipMemcpyHostToDevice, stream));
         }
@@ -823,10 +789,6 @@ struct sdl_batcher {
                 FusedH2D &f;
                 ~Clear() { f = FusedH2D{}; }
             } clear{fused_h2d};
-            struct ClearSelf {
-                bool &f;
-                ~ClearSelf() { f = false; }
-            } clear_self{self_ranges};
             run_device(d_text, N, d_off, R, first_override >= 0 ? (uint64_t)first_override : cfg.first_record + n_records,
                        stream, d_labels, d_label_off);
         }
@@ -1161,7 +1123,7 @@ int sdl_batcher_create(const sdl_config *cfg, const char *tokenizer_path, const 
         }
         if (cfg->task == SDL_TASK_SPAN && t.kind != TOK_UNIGRAM)
             throw std::runtime_error("task span needs the t5 (Unigram) tokenizer: TokenizerInfo.extra (tokenizer_wrapper.rs:77-80)");
-        d.ubmp = h->d_ubmp.p;
+        d.ubmp = reinterpret_cast<const uint2 *>(h->d_ubmp.p);
         d.upage = h->d_upage.p;
         d.uentry = h->d_uentry.p;
         d.upool = h->d_upool.p;
@@ -1543,12 +1505,7 @@ constexpr uint64_t GZ_EXTRA_CHUNKS = 256;    // chunks appended behind one that 
 void inflate_chunked(sdl_batcher *h, const uint8_t *d_gz, uint64_t m, uint64_t ma, uint64_t mz, uint32_t isize,
                      uint32_t ooff_m, hipStream_t st) {
     const uint64_t len = mz - ma;
-    static const uint64_t chunk0 = [] {  // (SDL_GZ_CHUNK: diagnostic override of the chunk size)
-        const char *e = std::getenv("SDL_GZ_CHUNK");
-        const uint64_t v = e ? std::strtoull(e, nullptr, 10) : 0;
-        return v >= 4096 ? v : GZ_CHUNK;
-    }();
-    uint64_t ch = chunk0;
+    uint64_t ch = GZ_CHUNK;
     while ((len + ch - 1) / ch > GZ_MAX_CHUNKS) ch *= 2;
     const uint64_t C0 = (len - 8 + ch - 1) / ch;  // nominal starts ma + c ch < mz - 8
     const uint64_t CT = C0 + GZ_EXTRA_CHUNKS;
@@ -2116,10 +2073,10 @@ int sdl_json_to_frames(sdl_batcher *h, const uint8_t *jsonl, uint64_t len, uint6
         const uint64_t B = (uint64_t)h->cfg.batch_size, S = (uint64_t)h->cfg.sequence_length;
         const uint64_t LW = (uint64_t)h->P.label_width;
         const bool tt = h->with_tt();
-        // chunks end at a '\n' (the last one at len); the first is chunk_bytes / SDL_J2F_HEAD
-        // (default 4) so the copy-out stream starts early
+        // chunks end at a '\n' (the last one at len); the first is a quarter chunk so the
+        // copy-out stream starts early
         std::vector<uint64_t> cut{0};
-        const int64_t head_div = std::max<int64_t>(1, env_int("SDL_J2F_HEAD", 4));
+        constexpr int64_t head_div = 4;
         while (cut.back() < len) {
             uint64_t e = cut.back() + (cut.size() == 1 ? std::max<uint64_t>(chunk_bytes / head_div, 4096) : chunk_bytes);
             if (e >= len) { cut.push_back(len); break; }
@@ -2282,9 +2239,8 @@ int sdl_json_to_frames(sdl_batcher *h, const uint8_t *jsonl, uint64_t len, uint6
                 x.label_width = (int32_t)LW;
                 // size the frames, write them into this slot's device buffer from the copy-out
                 // stream and copy them to pinned host memory there: the next chunk's kernels
-                // overlap the copy.  (SDL_FRAMES_MAPPED=1: the kernel writes mapped pinned host
-                // memory itself -- shader stores over PCIe measured ~25 GB/s against ~56 GB/s
-                // for the DMA copy.)
+                // overlap the copy.  (Writing mapped pinned host memory from the kernel itself
+                // measured ~25 GB/s of shader stores over PCIe against ~56 GB/s for the DMA copy.)
                 // The frames kernel runs on the compute stream, so the copy-out stream holds
                 // nothing but the copies and they run back to back.
                 sdl_frames fr;
@@ -2293,29 +2249,17 @@ int sdl_json_to_frames(sdl_batcher *h, const uint8_t *jsonl, uint64_t len, uint6
                 h->f_dry = false;
                 if (rc) return rc;
                 h->x_pin_out[slot].ensure((size_t)fr.total_bytes + 16);
-                const bool mapped = env_int0("SDL_FRAMES_MAPPED", 0) != 0;
-                const hipStream_t fs = mapped ? h->x_out : sc;
-                if (mapped) {
-                    void *dp = nullptr;
-                    HIP_TRY(hipHostGetDevicePointer(&dp, h->x_pin_out[slot].p, 0));
-                    h->f_dest = static_cast<uint8_t *>(dp);
-                    h->f_dest_cap = h->x_pin_out[slot].cap;
-                } else {
-                    h->x_frames[slot].ensure((size_t)fr.total_bytes + 16);
-                    h->f_dest = h->x_frames[slot].p;
-                    h->f_dest_cap = h->x_frames[slot].cap;
-                }
-                if (mapped) HIP_TRY(hipStreamWaitEvent(h->x_out, e_rows[slot], 0));
-                rc = sdl_pickle_frames_device(h, &x, nframe_rows, flush_now ? 1 : 0, fs, &fr);
+                h->x_frames[slot].ensure((size_t)fr.total_bytes + 16);
+                h->f_dest = h->x_frames[slot].p;
+                h->f_dest_cap = h->x_frames[slot].cap;
+                rc = sdl_pickle_frames_device(h, &x, nframe_rows, flush_now ? 1 : 0, sc, &fr);
                 h->f_dest = nullptr;
                 h->f_dest_cap = 0;
                 if (rc) return rc;
-                if (!mapped) {
-                    HIP_TRY(hipEventRecord(e_rows[slot], sc));  // frames written
-                    HIP_TRY(hipStreamWaitEvent(h->x_out, e_rows[slot], 0));
-                    HIP_TRY(hipMemcpyAsync(h->x_pin_out[slot].p, h->x_frames[slot].p, (size_t)fr.total_bytes,
-                                           hipMemcpyDeviceToHost, h->x_out));
-                }
+                HIP_TRY(hipEventRecord(e_rows[slot], sc));  // frames written
+                HIP_TRY(hipStreamWaitEvent(h->x_out, e_rows[slot], 0));
+                HIP_TRY(hipMemcpyAsync(h->x_pin_out[slot].p, h->x_frames[slot].p, (size_t)fr.total_bytes,
+                                       hipMemcpyDeviceToHost, h->x_out));
                 HIP_TRY(hipEventRecord(e_frames[slot], h->x_out));
                 pend[slot] = Pending{true, fr.n_frames, fr.frame_bytes, fr.last_frame_bytes, fr.total_bytes};
                 frames_total += fr.n_frames;

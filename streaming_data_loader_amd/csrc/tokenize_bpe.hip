@@ -90,7 +90,7 @@ __device__ __forceinline__ uint32_t merge_val(const DevTok &T, uint32_t a, uint3
 __device__ __forceinline__ uint32_t min_u32(uint32_t a, uint32_t b) { return a < b ? a : b; }
 // wave minimum: a DPP min-scan, lane 63's total read back (no ds_bpermute steps)
 __device__ __forceinline__ uint32_t wave_min_u32(uint32_t x) {
-    SDL_DPP_SCAN_ID(x, min_u32, 0xFFFFFFFFu);
+    DPP_SCAN_ID(x, min_u32, 0xFFFFFFFFu);
     return lane_bcast(x, 63);
 }
 // segmented min-scan operator on (head flag << 16 | rank <= 0xFFFF): a head
@@ -310,7 +310,7 @@ __device__ int bpe_wave_seg(const DevTok &T, uint32_t &sym, int n, uint64_t &hea
         const uint32_t rank = v >> 16;
         // segmented inclusive min scan (DPP), then each lane takes its word's last value
         uint32_t x = rank | ((uint32_t)((heads >> lane) & 1ull) << 16);
-        SDL_DPP_SCAN_ID(x, seg_min, 0xFFFFu);
+        DPP_SCAN_ID(x, seg_min, 0xFFFFu);
         x &= 0xFFFFu;
         const uint64_t after = lane == 63 ? 0ull : heads & ~((2ull << lane) - 1ull);
         const int last = after ? __builtin_ctzll(after) - 1 : n - 1;
@@ -347,10 +347,7 @@ __device__ int bpe_wave_seg(const DevTok &T, uint32_t &sym, int n, uint64_t &hea
 // lane-varying j is a select per slot); only the two pairs a merge creates are probed again.  A
 // wave runs 64 words at once and pays the longest word's merge count in probe latencies, where
 // the segmented wave BPE pays every packed batch's.  s[0 .. returned count) = the word's ids.
-#ifndef SDL_LANE_BPE
-#define SDL_LANE_BPE 12  // (16: held-out clm -1.3 %, fixture -1.7 %: its registers cost the common path; 8: held-out -3.5 %)
-#endif
-constexpr int LANE_BPE = SDL_LANE_BPE;
+constexpr int LANE_BPE = 12;  // (16: held-out clm -1.3 %, fixture -1.7 %: its registers cost the common path; 8: held-out -3.5 %)
 __device__ __forceinline__ int bpe_lane(const DevTok &T, uint32_t (&s)[LANE_BPE], int n) {
     constexpr uint32_t NOV = 0xFFFFFFFFu;
     uint32_t v[LANE_BPE - 1];
@@ -428,10 +425,8 @@ void print_bpe_cycles() {
 
 // ---------------------------------------------------------------------------
 // Register budget for 5 waves/SIMD (the 7.9 KB of LDS per one-wave block admits 5).
-#ifndef SDL_BPE_WAVES
-#define SDL_BPE_WAVES 5
-#endif
-__global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL_BPE_WAVES, 8))) void k_bpe_chunks(
+constexpr int BPE_WAVES = 5;
+__global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(BPE_WAVES, 8))) void k_bpe_chunks(
     DevTok T, const uint8_t *__restrict__ text, int64_t N, const uint64_t *__restrict__ off, int64_t R,
     const uint32_t *__restrict__ ranges, uint32_t *__restrict__ tokc, uint32_t *__restrict__ chunk_cnt,
     uint32_t *__restrict__ chunk_ent, uint32_t *__restrict__ rec_local, uint32_t *__restrict__ long_count,
@@ -701,7 +696,6 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
 
     BPE_STAMP(3);
     const int npend = (int)s_scratch[1];
-#ifndef SDL_BPE_NO_LANE
     // ---- 4a. misses of <= LANE_BPE bytes: one word per lane (bpe_lane) ----------
     for (int q0 = 0; q0 < npend; q0 += TOK_THREADS) {  // (wave-uniform)
         const int q = q0 + lane;
@@ -727,7 +721,6 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
     }
     __syncthreads();
     BPE_STAMP(6);
-#endif
     // ---- 4. wave BPE of the (longer) misses, packed: consecutive misses share the lanes --
     for (int q = 0; q < npend;) {
         int total = 0, nw = 0, wprel = 0, wpi = 0;
@@ -738,12 +731,10 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
             const int prel = (int)(s_pieces[pi] & 0xFFFu);
             const int nxt = pi + 1 < np ? (int)(s_pieces[pi + 1] & 0xFFFu) : e_last;
             const int n = nxt - prel;
-#ifndef SDL_BPE_NO_LANE
             if (n <= LANE_BPE) {  // (done in 4a)
                 ++q;
                 continue;
             }
-#endif
             if (total + n > 64) break;
             if (lane >= total && lane < total + n) sym = (uint32_t)T.byte_id[win[prel + HALO_L + lane - total]];
             if (lane == nw) {
@@ -1029,10 +1020,8 @@ hipError_t launch_bpe_chunks(const DevTok &T, const uint8_t *text, int64_t N, co
     // one wave per long piece: the merges of one piece are a dependent chain of L2 round trips,
     // so the pieces in flight are what it runs on (r04: 1024 waves, one per SIMD, was 1.70 ms on
     // the held-out corpus); a block finds no piece and exits at once when there are fewer
-#ifndef SDL_BPE_LONG_GRID
-#define SDL_BPE_LONG_GRID 2048
-#endif
-    const int64_t grid = std::min<int64_t>((int64_t)long_cap, SDL_BPE_LONG_GRID);
+constexpr int BPE_LONG_GRID = 2048;
+    const int64_t grid = std::min<int64_t>((int64_t)long_cap, BPE_LONG_GRID);
     if (grid > 0)
         hipLaunchKernelGGL(k_bpe_long, dim3((unsigned)grid), dim3(64), 0, st, T, text, N, off, R, long_count, long_list,
                            long_cap, scratch, chunk_cnt, rec_local, err);

@@ -50,36 +50,18 @@ __device__ __forceinline__ uint32_t meta_byte(int x) { return x == 0 ? 0xE2u : x
 
 // LDS budget: 3 one-wave blocks per SIMD (<= 13.3 KB each) -- the kernel waits
 // on probe latency, so resident waves are what it runs on
-#ifndef SDL_UNI_ARENA
-#define SDL_UNI_ARENA 768
-#endif
-constexpr int ARENA = SDL_UNI_ARENA;  // LDS bytes for normalized medium words
+constexpr int ARENA = 768;  // LDS bytes for normalized medium words
 constexpr int WIN_PAD = WIN + 32;   // window + gather padding; the arena follows
 constexpr int VP_CAP = UNI_VPC;  // Viterbi jobs per chunk (more: long items)
-#ifndef SDL_UNI_MED_CAP
-#define SDL_UNI_MED_CAP 128
-#endif
-constexpr int MED_CAP = SDL_UNI_MED_CAP;  // medium words per chunk (more: long items)
-#ifndef SDL_UNI_WT_UNROLL
-#define SDL_UNI_WT_UNROLL 2
-#endif
-constexpr int UNI_WT_UNROLL = SDL_UNI_WT_UNROLL;  // word-table probes in flight per lane
+constexpr int MED_CAP = 128;  // medium words per chunk (more: long items)
+constexpr int UNI_WT_UNROLL = 2;  // word-table probes in flight per lane
 constexpr uint8_t CNT_LONG = 0xFF;  // s_cnt of a long item
 // s_cnt of a piece handed to k_unigram_viterbi: CNT_JOB | its jobs (<= 0x3F), or, a word past UNI_WMAX
 // bytes (one job), CNT_JOB | CNT_WIDE | its payload units; the low 6 bits are the payload units either way
 constexpr uint8_t CNT_JOB = 0x80, CNT_WIDE = 0x40;
 // k_unigram_viterbi: a pass takes the chunk's next jobs whose candidates fit VTCAP (one job
 // always does: vp_tasks(UNI_WMAX) = 17 + 16 * 16 < VTCAP) and at most VJP of them (a DP lane each)
-#ifndef SDL_UNI_VJP
-#define SDL_UNI_VJP 64
-#endif
-#ifndef SDL_UNI_VTCAP
-#define SDL_UNI_VTCAP 1024
-#endif
-#ifndef SDL_UNI_VU
-#define SDL_UNI_VU 2
-#endif
-constexpr int VJP = SDL_UNI_VJP, VTCAP = SDL_UNI_VTCAP, VU = SDL_UNI_VU;  // VU: probes in flight per lane
+constexpr int VJP = 64, VTCAP = 768, VU = 2;  // VU: probes in flight per lane
 static_assert(VJP <= 64 && VTCAP % (64 * VU) == 0 && VTCAP < 0x7FF, "a hit index fits a back pointer's 11 bits");
 
 typedef __attribute__((address_space(3))) double lds_f64;
@@ -506,13 +488,17 @@ __device__ bool finish_long(const DevTok &T, const uint8_t *text, int64_t N, con
 // Its candidates are laid out row by row: the "▁" row (payload prefixes of
 // 0..min(L, Mm) bytes), then one row per payload start i (ends i+1 ..
 // min(L, i + Mf)).
-__device__ __forceinline__ int vp_c0(int L, int Mm) { return (L < Mm ? L : Mm) + 1; }
-__device__ __forceinline__ int vp_rowoff(int i, int L, int Mf) {  // sum_{k<i} min(L-k, Mf)
+__host__ __device__ constexpr int vp_c0(int L, int Mm) { return (L < Mm ? L : Mm) + 1; }
+__host__ __device__ constexpr int vp_rowoff(int i, int L, int Mf) {  // sum_{k<i} min(L-k, Mf)
     const int K = L > Mf ? L - Mf : 0;
     if (i <= K) return i * Mf;
     return K * Mf + (i - K) * L - (K + i - 1) * (i - K) / 2;
 }
-__device__ __forceinline__ int vp_tasks(int L, int Mm, int Mf) { return vp_c0(L, Mm) + vp_rowoff(L, L, Mf); }
+__host__ __device__ constexpr int vp_tasks(int L, int Mm, int Mf) { return vp_c0(L, Mm) + vp_rowoff(L, L, Mf); }
+// a pass always takes its first job whole: the widest job the chunk kernel hands over (wide_ok:
+// maxlen_first < UNI_VRING, maxlen_meta + 3 < UNI_VRING) has its candidates within VTCAP
+static_assert(vp_tasks(UNI_VMAX, UNI_VRING - 4, UNI_VRING - 1) <= VTCAP && vp_tasks(UNI_WMAX, UNI_WMAX, UNI_WMAX) <= VTCAP,
+              "one job fits a pass");
 // local index of candidate (i, j) (i = -1: the "▁" row), or -1 if out of range
 __device__ __forceinline__ int vp_local(int i, int j, int L, int Mm, int Mf) {
     if (i < 0) return j <= Mm && j <= L ? j : -1;
@@ -629,10 +615,8 @@ void print_long_cycles() {
 #endif
 
 // ---------------------------------------------------------------------------
-#ifndef SDL_UNI_WAVES
-#define SDL_UNI_WAVES 3
-#endif
-__global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL_UNI_WAVES, 8))) void k_unigram_chunks(
+constexpr int UNI_WAVES = 3;
+__global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(UNI_WAVES, 8))) void k_unigram_chunks(
     DevTok T, const uint8_t *__restrict__ text, int64_t N, const uint64_t *__restrict__ off, int64_t R,
     const uint32_t *__restrict__ ranges, uint32_t *__restrict__ tokc, uint32_t *__restrict__ chunk_cnt,
     uint32_t *__restrict__ chunk_ent, uint32_t *__restrict__ rec_local, uint32_t *__restrict__ counters,
@@ -908,9 +892,6 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
                     done = true;
                 }
             } else if (kind[u] == 2) {
-#ifdef SDL_UNI_MEDIUM_LONG  // diagnostic: medium words go to the long-item kernel
-                if (len > 0) { cnt[pi] = CNT_LONG; stage[prel] = (uint16_t)len; continue; }
-#endif
                 // medium word: normalized in the next pass, all lanes at once
                 const uint32_t mq = atomicAdd(&s_scratch[3], 1u);
                 if (mq < (uint32_t)MED_CAP) {
@@ -1158,14 +1139,12 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
 //     the ids go to the chunk's results region at the job's stage position and its list
 //     entry becomes LMARK | UNI_JOB_BIT | k << 24 | pos (k_compact_tokens expands it).
 // Then the chunk's id count and its records' local offsets grow by the jobs' k - 1.
-#ifndef SDL_UNI_VWAVES
-#define SDL_UNI_VWAVES 3
-#endif
+constexpr int UNI_VWAVES = 4;
 // WIDE = false: the jobs of <= UNI_WMAX payload bytes (20 nodes, every one a register); true: the
 // printable ASCII words of UNI_WMAX < L <= UNI_VMAX (nodes in a ring of UNI_VRING registers).  Two
 // launches over the same job lists, so the common narrow jobs keep the small DP.
 template <bool WIDE>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDL_UNI_VWAVES, 8))) void k_unigram_viterbi(
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(UNI_VWAVES, 8))) void k_unigram_viterbi(
     DevTok T, int64_t N, const uint64_t *__restrict__ off, int64_t R, const uint32_t *__restrict__ ranges,
     uint32_t *__restrict__ tokc, uint32_t *__restrict__ chunk_cnt, uint32_t *__restrict__ rec_local) {
     __shared__ __attribute__((aligned(16))) uint8_t s_pb[UNI_VPC * 16 + 32];  // payload units (+ lds_w16's reach)
@@ -1584,10 +1563,7 @@ __device__ Scratch make_scratch(uint8_t *mine, int cap) {
 // the LDS footprint (~20 KB at KMAX 32) sets how many items a CU keeps in flight.
 constexpr int LONG_NORM = 512;  // stage 2; stage 1 takes items of <= LONG_NORM1 normalized bytes
 constexpr int LONG_NORM1 = 128;
-#ifndef SDL_LONG_UNROLL
-#define SDL_LONG_UNROLL 2
-#endif
-constexpr int LONG_UNROLL = SDL_LONG_UNROLL;  // candidate probes in flight per lane (k_unigram_long)
+constexpr int LONG_UNROLL = 2;  // candidate probes in flight per lane (k_unigram_long)
 constexpr int LONG_RAW = 1024;
 
 template <int KMAX, int NORM>
@@ -1944,7 +1920,7 @@ hipError_t launch_unigram_chunks(const DevTok &T, const uint8_t *text, int64_t N
     // normalized bytes (nearly all) with a small LDS footprint and more of them in
     // flight, then the rest (<= 512) from the first stage's overflow list.
     const int g1 = W.lane_blocks * 4 / 3;
-#define SDL_UNI_LONG_STAGES(KM)                                                                                     \
+#define UNI_LONG_STAGES(KM)                                                                                     \
     hipLaunchKernelGGL((k_unigram_long<KM, LONG_NORM1>), dim3((unsigned)g1), dim3(64), 0, side, T, text, N, off, R,  \
                        ranges, W.items, W.item_cap, W.counters, W.counters, tokc, chunk_cnt, rec_local, W.pool,      \
                        W.pool_cap, W.items2, W.items2_cap, W.counters + 4, W.err);                                    \
@@ -1952,13 +1928,13 @@ hipError_t launch_unigram_chunks(const DevTok &T, const uint8_t *text, int64_t N
                        off, R, ranges, W.items2, W.items2_cap, W.counters + 4, W.counters, tokc, chunk_cnt,           \
                        rec_local, W.pool, W.pool_cap, W.huge, W.huge_cap, W.counters + 3, W.err);
     if (T.maxlen_meta + 1 <= 20 && T.maxlen_first <= 20) {  // smaller LDS: more items in flight
-        SDL_UNI_LONG_STAGES(20)
+        UNI_LONG_STAGES(20)
     } else if (T.maxlen_meta + 1 <= 32 && T.maxlen_first <= 32) {
-        SDL_UNI_LONG_STAGES(32)
+        UNI_LONG_STAGES(32)
     } else {
-        SDL_UNI_LONG_STAGES(64)
+        UNI_LONG_STAGES(64)
     }
-#undef SDL_UNI_LONG_STAGES
+#undef UNI_LONG_STAGES
     hipLaunchKernelGGL(k_unigram_huge, dim3((unsigned)W.huge_blocks), dim3(64), 0, side, T, text, N, off, R, W.counters,
                        tokc, chunk_cnt, rec_local, W.scratch, W.pool, W.pool_cap, W.huge, W.huge_cap, W.err);
     if (side != st) {

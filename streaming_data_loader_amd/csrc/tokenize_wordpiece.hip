@@ -62,7 +62,7 @@ __device__ __forceinline__ uint32_t vclass4(uint32_t x) {
 // identity, bit 3 inline (bits 4-5 nbytes-1, 6-7 nchars-1, 8-31 the bytes),
 // else bits 8-31 = pool offset.  One load for the BMP, two beyond it.
 __device__ __forceinline__ uint32_t uentry(const DevTok &T, uint32_t cp) {
-    if (cp < 0x10000u) return T.ubmp[cp];
+    if (cp < 0x10000u) return T.ubmp[cp].x;
     if (cp >= 0x110000u) return UC_DEL;
     return T.uentry[(uint32_t)T.upage[cp >> 7] * 128u + (cp & 127u)];
 }
@@ -387,7 +387,7 @@ __device__ __forceinline__ int64_t rec_end_of(const Ctx &C, int64_t rb_next, int
 // sdl_phase_cycles[]; the host prints them.  Never compiled into the product.
 #ifdef SDL_STAMPS
 __device__ unsigned long long sdl_phase_cycles[16];
-#define SDL_STAMP(k)                                                                  \
+#define PHASE_STAMP(k)                                                                  \
     do {                                                                              \
         if (threadIdx.x == 0) {                                                       \
             const unsigned long long t_ = __builtin_amdgcn_s_memtime();              \
@@ -396,7 +396,7 @@ __device__ unsigned long long sdl_phase_cycles[16];
         }                                                                             \
     } while (0)
 #else
-#define SDL_STAMP(k) \
+#define PHASE_STAMP(k) \
     do {             \
     } while (0)
 #endif
@@ -406,27 +406,17 @@ __device__ unsigned long long sdl_phase_cycles[16];
 // 5 measures faster on both corpora (fixture 1.868 -> 1.818 ms, held-out
 // 2.98 -> 2.86 ms).  LDS (7.1 KB per one-wave block) admits ~5.5 anyway; one
 // more 64-B array (7.7 KB) cost 7%.
-#ifndef SDL_WP_WAVES
-#define SDL_WP_WAVES 5
-#endif
-#ifndef SDL_WP_NPROBE
-#define SDL_WP_NPROBE 2
-#endif
+constexpr int WP_WAVES = 5;
 // candidate lengths the pending-word state machine probes per step (longest
 // first).  3 and 4 were measured: parity-green and no faster (4: 96 VGPRs,
 // fixture 1.14 -> 1.19 ms, held-out 2.32 -> 2.40; 3: within noise) -- the
 // machine is bound by its lanes' probe latency, not by its step count.
-constexpr int WP_NPROBE = SDL_WP_NPROBE;
-static_assert(WP_NPROBE >= 1, "at least one candidate per step");
-// SELF (a push of <= 63 records read straight from mapped pinned memory): each block finds its
-// record ranges itself -- lane r holds off[r], three ballots count the offsets below the window's
-// edges -- so no k_chunk_ranges launch (and no copy) precedes it; block 0 also writes the
-// one-segment record bounds and zeroes the label error word (k_chunk_ranges' fold).
-template <bool SELF>
-__global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL_WP_WAVES, 8))) void k_wordpiece_chunks(
+constexpr int WP_NPROBE = 2;
+constexpr int EARLY_LEADS = 0;  // non-ASCII leads a lane looks up before the rare pass
+__global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(WP_WAVES, 8))) void k_wordpiece_chunks(
     DevTok T, const uint8_t *__restrict__ text, int64_t N, const uint64_t *__restrict__ off, int64_t R,
     const uint32_t *__restrict__ ranges, uint32_t *__restrict__ tokc, uint32_t *__restrict__ chunk_cnt,
-    uint32_t *__restrict__ rec_local, int64_t c_begin, uint32_t *__restrict__ rb1, uint32_t *__restrict__ zero1) {
+    uint32_t *__restrict__ rec_local, int64_t c_begin) {
     __shared__ __attribute__((aligned(16))) uint8_t s_win[WIN];
     __shared__ uint32_t s_rbits[RBITS_WORDS + 1];
     __shared__ uint16_t s_pieces[CHUNK];   // (pos - c0) | kind << 12
@@ -438,13 +428,6 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
     // chunk position (a word before it ends there), [32, 64) an ISO char whose id
     // is already in its stage slot
     __shared__ uint32_t s_nabits[2 * CHUNK / 32];
-#ifdef SDL_LDS_PAD  // diagnostic: occupancy sensitivity
-    __shared__ uint8_t s_pad[SDL_LDS_PAD];
-    if (N < 0) {
-        s_pad[(blockIdx.x * 7 + threadIdx.x) % SDL_LDS_PAD] = (uint8_t)threadIdx.x;
-        chunk_cnt[threadIdx.x] = ((volatile uint8_t *)s_pad)[(blockIdx.x + 3 * threadIdx.x) % SDL_LDS_PAD];
-    }
-#endif
 
     const int tid = threadIdx.x;
 #ifdef SDL_STAMPS
@@ -465,25 +448,7 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
         hp = tid < HALO_L / 16 ? w0 + 16 * tid : c0 + CHUNK + 16 * (tid - HALO_L / 16);
         hv = load16(text, hp, N);
     }
-    int64_t ra, rz, r_lo;
-    if constexpr (SELF) {  // (TOK_THREADS == 64: one wave, R <= 63)
-        const bool in = tid <= R;
-        const int64_t o = in ? (int64_t)off[tid] : 0;
-        ra = __popcll(__ballot(in && o < w0));
-        rz = __popcll(__ballot(in && o < w0 + WIN));
-        r_lo = __popcll(__ballot(in && o < c0));
-        if (ci == 0 && tid == 0) {
-            if (rb1) {
-                rb1[0] = 0u;
-                rb1[1] = (uint32_t)R;
-            }
-            if (zero1) *zero1 = 0u;
-        }
-    } else {
-        ra = ranges[3 * ci];
-        rz = ranges[3 * ci + 1];
-        r_lo = ranges[3 * ci + 2];
-    }
+    const int64_t ra = ranges[3 * ci], rz = ranges[3 * ci + 1], r_lo = ranges[3 * ci + 2];
     *reinterpret_cast<uint4 *>(s_win + HALO_L + 16 * tid) = v;
     if (tid < (WIN - CHUNK) / 16) *reinterpret_cast<uint4 *>(s_win + (hp - w0)) = hv;
     if (tid <= RBITS_WORDS) s_rbits[tid] = 0;
@@ -497,11 +462,42 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
         atomicOr(&s_rbits[rel >> 5], 1u << (rel & 31));
     }
     __syncthreads();
-    SDL_STAMP(1);
+    PHASE_STAMP(1);
 
     const Ctx C{&T, win, rbits, w0, text, N, off, R};
-#if defined(SDL_ABLATE) && SDL_ABLATE >= 3
-    // diagnostic: load only; every record gets 0 ids (so later stages stay in bounds)
+    // The lane's first EARLY_LEADS non-ASCII lead bytes (canonical 2- and 3-byte chars): decoded
+    // now and their BMP entries requested -- the entry, and for an ISO char the precomputed
+    // WordPiece id of its one-char piece (assets.cpp: wp_iso_ids) -- so the loads are in flight
+    // through the classification and the block scans and land at the rare pass with no probe
+    // behind them.  Other leads (more per lane, 4-byte or malformed) take the block-wide pass.
+    const int64_t s0 = c0 + 16 * tid;
+    const int nown = s0 >= c1 ? 0 : (int)(c1 - s0 < 16 ? c1 - s0 : 16);
+    const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+    uint32_t leads = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) leads |= gather4(wv[j] & (wv[j] << 1)) << (4 * j);  // >= 0xC0
+    if (nown < 16) leads &= (1u << nown) - 1u;
+    uint2 ue[EARLY_LEADS > 0 ? EARLY_LEADS : 1];
+    uint32_t urel = 0;  // 1 + lane byte of early lead k in bits [5 k, 5 k + 5); 0: none
+    {
+        uint32_t m = leads;
+#pragma unroll
+        for (int k = 0; k < EARLY_LEADS; ++k) {
+            ue[k] = make_uint2(0u, 0u);
+            if (!m) continue;
+            const int i = __builtin_ctz(m);
+            m &= m - 1;
+            const int rel = 16 * tid + i;
+            int len;
+            const uint32_t cp = decode(C, c0 + rel, win[HALO_L + rel], &len);
+            if ((len == 2 && cp >= 0x80u) || (len == 3 && cp >= 0x800u)) {
+                ue[k] = T.ubmp[cp];
+                urel |= (uint32_t)(i + 1) << (5 * k);
+            }
+        }
+    }
+#ifdef SDL_ABLATE
+    // diagnostic build (tools/build_variants.py abl3=SDL_ABLATE, tools/pmc_calibration.py): load only; every record gets 0 ids (so later stages stay in bounds)
     {  // (an opaque use of the window keeps its loads: `x & 0u` let the compiler drop them all)
         const uint32_t x = s_win[HALO_L + (ci & 1023)];
         asm volatile("" ::"v"(x));
@@ -512,27 +508,26 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
 #endif
 
     // ---- 2. register-resident classification of the lane's 16 bytes ----------
-    const int64_t s0 = c0 + 16 * tid;
-    const int nown = s0 >= c1 ? 0 : (int)(c1 - s0 < 16 ? c1 - s0 : 16);
     const int rel0 = HALO_L + 16 * tid;  // window index of s0 (multiple of 16)
     const uint32_t rmask = (rbits[rel0 >> 5] >> (rel0 & 31)) & 0xFFFFu;
-    const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
     uint64_t cls = 0;
-    uint32_t leads = 0, opens = 0;
+    uint32_t opens = 0;
     const uint32_t o4 = T.opener * 0x01010101u;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         const uint32_t x = wv[j];
         cls |= (uint64_t)vclass4(x) << (16 * j);
-        leads |= gather4(x & (x << 1)) << (4 * j);  // >= 0xC0
         opens |= gather4(~nzb(x ^ o4)) << (4 * j);
     }
     if (!T.n_special) opens = 0;
     if (nown < 16) {
         cls &= nown ? ((1ull << (4 * nown)) - 1ull) : 0ull;
-        leads &= (1u << nown) - 1u;
         opens &= (1u << nown) - 1u;
     }
+    uint32_t late_leads = leads;  // the leads the block-wide pass classifies
+#pragma unroll
+    for (int k = 0; k < EARLY_LEADS; ++k)
+        if ((urel >> (5 * k)) & 31u) late_leads &= ~(1u << (((urel >> (5 * k)) & 31u) - 1u));
     uint8_t *s_ovr = s_cnt;
     *reinterpret_cast<uint4 *>(s_ovr + 16 * tid) = make_uint4(~0u, ~0u, ~0u, ~0u);
     // Rare bytes are classified block-parallel, one per thread, and returned as
@@ -549,13 +544,13 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
             if (c0 - d >= 0 && C.byte(c0 - d) == T.opener) opens_left |= 1u << (d - 1);
     }
     uint32_t nrare;
-    const uint32_t rare_n = (uint32_t)__builtin_popcount(leads) |
+    const uint32_t rare_n = (uint32_t)__builtin_popcount(late_leads) |
                             ((uint32_t)(__builtin_popcount(opens) + __builtin_popcount(opens_left)) << 16);
     const uint32_t rbase = block_excl_sum<TOK_THREADS>(rare_n, &nrare, s_scratch);
     const uint32_t n_leads = nrare & 0xFFFFu, n_opens = nrare >> 16;
     {
         uint32_t lb = rbase & 0xFFFFu, ob = n_leads + (rbase >> 16);
-        for (uint32_t m = leads; m;) {
+        for (uint32_t m = late_leads; m;) {
             const int i = __builtin_ctz(m);
             m &= m - 1;
             s_pieces[lb++] = (uint16_t)(HALO_L + 16 * tid + i);
@@ -572,19 +567,39 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
         }
     }
     __syncthreads();
-    SDL_STAMP(2);
+    PHASE_STAMP(2);
+#pragma unroll
+    for (int k = 0; k < EARLY_LEADS; ++k) {  // the early leads' entries have landed
+        const uint32_t i1 = (urel >> (5 * k)) & 31u;
+        if (!i1) continue;
+        const int rel = 16 * tid + (int)i1 - 1;
+        const uint32_t vc = vclass_of_entry(ue[k].x);
+        s_ovr[rel] = (uint8_t)vc;
+        if (vc == V_WS || vc == V_ISO) atomicOr(&s_nabits[rel >> 5], 1u << (rel & 31));
+        if (ue[k].y >> 31) {  // an ISO char's one-char piece (or [UNK]), as the block pass probes it
+            s_stage[rel] = (uint16_t)ue[k].y;
+            atomicOr(&s_nabits[CHUNK / 32 + (rel >> 5)], 1u << (rel & 31));
+        }
+    }
     for (uint32_t k = tid; k < n_leads; k += TOK_THREADS) {
         const int wi = s_pieces[k];
         const int rel = wi - HALO_L;
         int len;
-        const uint32_t e = uentry(T, decode(C, w0 + wi, win[wi], &len));
+        const uint32_t cp = decode(C, w0 + wi, win[wi], &len);
+        // (a canonical BMP char: its entry and its precomputed one-char id in one load)
+        const uint2 ue = (len == 2 && cp >= 0x80u) || (len == 3 && cp >= 0x800u) ? T.ubmp[cp]
+                                                                                 : make_uint2(uentry(T, cp), 0u);
+        const uint32_t e = ue.x;
         const uint32_t vc = vclass_of_entry(e);
         s_ovr[rel] = (uint8_t)vc;
         if (vc == V_WS || vc == V_ISO) atomicOr(&s_nabits[rel >> 5], 1u << (rel & 31));
         // an ISO char is a piece of its own: when it normalizes to one char of <= 16
         // bytes, its WordPiece is one probe of that char (no "##" piece can start
         // inside a char), done here so the piece skips the pending pass
-        if (vc == V_ISO && (e & 24u) != 16u && ((e & 4u) || ((e & 8u) && ((e >> 6) & 3u) == 0u))) {
+        if (ue.y >> 31) {
+            s_stage[rel] = (uint16_t)ue.y;
+            atomicOr(&s_nabits[CHUNK / 32 + (rel >> 5)], 1u << (rel & 31));
+        } else if (vc == V_ISO && (e & 24u) != 16u && ((e & 4u) || ((e & 8u) && ((e >> 6) & 3u) == 0u))) {
             W16 w{0, 0, 0, 0};
             int L;
             if (e & 4u) {
@@ -600,7 +615,7 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
             atomicOr(&s_nabits[CHUNK / 32 + (rel >> 5)], 1u << (rel & 31));
         }
     }
-    SDL_STAMP(12);
+    PHASE_STAMP(12);
     if (n_opens) {  // block-uniform
         __syncthreads();
         for (uint32_t k = n_leads + tid; k < n_leads + n_opens; k += TOK_THREADS) {
@@ -616,7 +631,7 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
         }
     }
     __syncthreads();
-    SDL_STAMP(3);
+    PHASE_STAMP(3);
     {
         const uint4 o = *reinterpret_cast<const uint4 *>(s_ovr + 16 * tid);
         const uint32_t ov[4] = {o.x, o.y, o.z, o.w};
@@ -662,7 +677,7 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
     __syncthreads();
     const uint32_t chunk_state = s_scratch[TOK_THREADS / 64];
     __syncthreads();
-    SDL_STAMP(4);
+    PHASE_STAMP(4);
     const uint32_t st_in = block_excl_last_scan<TOK_THREADS>(summ, s_scratch);
 
     // ---- 3. piece starts -------------------------------------------------------
@@ -689,7 +704,7 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
         s_pieces[pbase++] = (uint16_t)((16 * tid + i) | (c << 12));
     }
     __syncthreads();
-    SDL_STAMP(5);
+    PHASE_STAMP(5);
     const int np = (int)np_total;
 
     // ---- 4. tokenize pieces ---------------------------------------------------------
@@ -704,42 +719,20 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
     // (a) and (b) alternate in rounds so the pending list stays within
     // PEND_CAP (a round of (a) adds at most TOK_THREADS * TOK_UNROLL).
     lds_u16 *stage = (lds_u16 *)s_stage;
-#if defined(SDL_ABLATE) && SDL_ABLATE == 2
-    // diagnostic: no WordPiece at all, every piece yields one id 0
-    for (int pi = tid; pi < np; pi += TOK_THREADS) {
-        stage[s_pieces[pi] & 0xFFFu] = 0;
-        s_cnt[pi] = 1;
-    }
-    __syncthreads();
-    if (np < 0) {  // never: keeps the code below compiled in
-#endif
     if (tid == 0) {
         s_scratch[TOK_THREADS / 64 + 1] = 0;  // pending count
         s_scratch[TOK_THREADS / 64 + 2] = 0;  // deferred count
     }
     __syncthreads();
-    SDL_STAMP(10);
+    PHASE_STAMP(10);
     const int lane = tid & 63;
     const lds_u32 *w32 = (const lds_u32 *)s_win;
     // word setup shared by (a) and (b): returns false if the general path is needed
     auto word_setup = [&](int prel, W16 &lw, int &Lout) -> bool {
         const int wr = prel + HALO_L;
-#ifdef SDL_WP_B64
-        // (A/B) three 8-byte reads at the word's 8-aligned base: ds_read_b64 banks 64 dwords, so
-        // a wave's ~200 bytes of words never meet on a bank (5 ds_read_b32 use 32 banks)
-        const uint32_t sh = (uint32_t)(wr & 3);
-        const int a8 = wr >> 3;
-        const lds_u64 *w64 = (const lds_u64 *)s_win;
-        const uint64_t y0 = w64[a8], y1 = w64[a8 + 1], y2 = w64[a8 + 2];
-        const bool hi = (wr & 4) != 0;
-        const uint32_t x0 = hi ? (uint32_t)(y0 >> 32) : (uint32_t)y0, x1 = hi ? (uint32_t)y1 : (uint32_t)(y0 >> 32),
-                       x2 = hi ? (uint32_t)(y1 >> 32) : (uint32_t)y1, x3 = hi ? (uint32_t)y2 : (uint32_t)(y1 >> 32),
-                       x4 = hi ? (uint32_t)(y2 >> 32) : (uint32_t)y2;
-#else
         const int a = wr >> 2;
         const uint32_t sh = (uint32_t)(wr & 3);
         const uint32_t x0 = w32[a], x1 = w32[a + 1], x2 = w32[a + 2], x3 = w32[a + 3], x4 = w32[a + 4];
-#endif
         const W16 raw{__builtin_amdgcn_alignbyte(x1, x0, sh), __builtin_amdgcn_alignbyte(x2, x1, sh),
                       __builtin_amdgcn_alignbyte(x3, x2, sh), __builtin_amdgcn_alignbyte(x4, x3, sh)};
         const uint32_t b16 = (x4 >> (8 * sh)) & 0xFFu;  // byte at p + 16
@@ -816,21 +809,13 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
             }
         }
         Probe pr[TOK_UNROLL];
-#ifndef SDL_ABLATE_FIRST_PROBE
 #pragma unroll
         for (int u = 0; u < TOK_UNROLL; ++u) pr[u] = probe_load(T, hsh[u]);
-#endif
 #pragma unroll
         for (int u = 0; u < TOK_UNROLL; ++u) {
             const int pi = r0 + u * TOK_THREADS + tid;
             if (probe[u]) {
-#ifdef SDL_ABLATE_FIRST_PROBE
-                // diagnostic upper bound for an on-chip vocabulary: every first probe
-                // "hits" without a memory access (ids are wrong; timing only)
-                const int id = (int)(hsh[u] & 0x3FFFu) | (int)(cand[u].x & 1u);
-#else
                 const int id = probe_result(pr[u], key[u], cand[u]);
-#endif
                 if (id >= 0) {
                     stage[prel_u[u]] = (uint16_t)id;
                     s_cnt[pi] = 1;
@@ -849,18 +834,10 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
         }
         __syncthreads();  // the pending count is read by the loop test
     }
-    SDL_STAMP(11);
+    PHASE_STAMP(11);
     int npend = (int)s_scratch[TOK_THREADS / 64 + 1];
     if (tid == 0) s_scratch[TOK_THREADS / 64 + 1] = 0;  // becomes the queue head
     __syncthreads();
-#if defined(SDL_ABLATE) && SDL_ABLATE == 1
-    // diagnostic: first probes only; every pending piece yields one [UNK]
-    for (int q = tid; q < npend; q += TOK_THREADS) {
-        stage[s_pieces[s_pend[q]] & 0xFFFu] = (uint16_t)T.unk_id;
-        s_cnt[s_pend[q]] = 1;
-    }
-    npend = 0;
-#endif
     // (b) state machine over the pending pieces
     if (npend) {
         bool exhausted = false;
@@ -1077,10 +1054,7 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
     }
     __syncthreads();
     }
-    SDL_STAMP(7);
-#if defined(SDL_ABLATE) && SDL_ABLATE == 2
-    }
-#endif
+    PHASE_STAMP(7);
 
     // ---- 5. compact ids into this chunk's tokc slice ------------------------------
     const int per = (np + TOK_THREADS - 1) / TOK_THREADS;
@@ -1133,7 +1107,7 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
         base += s_cnt[i];
     }
     __syncthreads();
-    SDL_STAMP(8);
+    PHASE_STAMP(8);
     if (tid == 0) chunk_cnt[ci] = total;
     // record boundaries owned by this chunk: local id offset of the first piece
     // at or after the boundary
@@ -1149,7 +1123,7 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(SDL
         }
         rec_local[ra + k] = lo < np ? (uint32_t)s_poff[lo] : total;
     }
-    SDL_STAMP(9);
+    PHASE_STAMP(9);
 }
 
 #ifdef SDL_STAMPS
@@ -1170,19 +1144,13 @@ void print_phase_cycles() {
 
 hipError_t launch_wordpiece_chunks(const DevTok &T, const uint8_t *text, int64_t N, const uint64_t *off, int64_t R,
                                    uint32_t *ranges, uint32_t *tokc, uint32_t *chunk_cnt, uint32_t *rec_local,
-                                   hipStream_t st, int64_t c_begin, int64_t c_end, bool self, uint32_t *rb1,
-                                   uint32_t *zero1) {
+                                   hipStream_t st, int64_t c_begin, int64_t c_end) {
     const int64_t n_chunks = (N + CHUNK - 1) / CHUNK;
     if (c_end < 0 || c_end > n_chunks) c_end = n_chunks;
     if (c_begin < 0) c_begin = 0;
     if (c_end <= c_begin) return hipSuccess;
-    if (self && (R > TOK_THREADS - 1 || c_begin != 0)) return hipErrorInvalidValue;
-    if (self)
-        hipLaunchKernelGGL(k_wordpiece_chunks<true>, dim3((unsigned)(c_end - c_begin)), dim3(TOK_THREADS), 0, st, T, text,
-                           N, off, R, ranges, tokc, chunk_cnt, rec_local, c_begin, rb1, zero1);
-    else
-        hipLaunchKernelGGL(k_wordpiece_chunks<false>, dim3((unsigned)(c_end - c_begin)), dim3(TOK_THREADS), 0, st, T,
-                           text, N, off, R, ranges, tokc, chunk_cnt, rec_local, c_begin, rb1, zero1);
+    hipLaunchKernelGGL(k_wordpiece_chunks, dim3((unsigned)(c_end - c_begin)), dim3(TOK_THREADS), 0, st, T, text, N,
+                       off, R, ranges, tokc, chunk_cnt, rec_local, c_begin);
     return hipGetLastError();
 }
 
