@@ -483,12 +483,18 @@ def determinism_soak(step, res, rows, task, dev, seconds):
     return {"runs": n, "seconds": round(time.perf_counter() - t0, 2), "identical": True}
 
 
+def _build_id():
+    from streaming_data_loader_amd import build
+    return build.embedded_id(os.environ.get("SDL_LIB") or build.LIB)
+
+
 def base_line(args, world, step_ms, value, task, N, R, rows, toks):
     S, B = task["S"], task["B"]
     return {
         "metric": METRIC, "value": round(value, 2), "unit": "MB/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(step_ms, 4), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "u8->int32",
+        "library_build_id": (_build_id() or "")[:16],
         "data": ("synthetic: data/test.json.gz records tiled (seeded)" if args.corpus == "fixture" else
                  "synthetic: held-out English text on the image (not in the proxy vocabularies' training text; "
                  "also used to tune kernels) tiled (seeded)"),

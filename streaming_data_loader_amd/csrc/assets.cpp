@@ -239,8 +239,8 @@ static void utf8_append(std::string &o, uint32_t cp) {
 // The one-char WordPiece id of every BMP char k_wordpiece_chunks' rare pass would probe
 // itself -- ISO class, not a canonical-ordering entry, normalizing to one char (identity:
 // the char's own UTF-8; inline: the entry's bytes) -- as bit 31 | the id of that string as a
-// non-"##" piece of <= maxlen_first bytes, else of [UNK]; 0 for every other char.  The kernel
-// reads it with the char's entry (EARLY_LEADS), so such a char costs one load and no probe.
+// non-"##" piece of <= maxlen_first bytes, else of [UNK]; 0 for every other char.  The rare
+// pass reads it with the char's entry, so such a char costs one load and no probe.
 static void wp_iso_ids(HostTokenizer &t) {
     std::unordered_map<std::string, int> ids;
     for (size_t i = 0; i < t.pieces.size(); ++i) ids[t.pieces[i]] = (int)i;  // (a duplicate keeps its last id)

@@ -1176,27 +1176,51 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(UNI_VWAVES, 
     const int Mm = T.maxlen_meta, Mf = T.maxlen_first;
     const int nj_all = (int)(nall < (uint32_t)VP_CAP ? nall : (uint32_t)VP_CAP);
     auto units = [](int L) -> uint32_t { return L > 16 ? (uint32_t)(L + 15) >> 4 : 1u; };
-    int njobs;  // this launch's jobs, in list order
+    // This launch's jobs, longest payload first: a pass's DP walks every start of its longest
+    // job, so passes of like lengths (the short jobs together) cost less than list order's
+    // mixed ones.  The order is free: each job's ids, entry and count fixups are its own.
+    int njobs;
+    static_assert(VP_CAP <= 128, "the chunk's jobs are two lane groups at most");
     {
-        uint32_t carry = 0, ucarry = 0, xcarry = 0;
-        for (int v0 = 0; v0 < nj_all; v0 += 64) {
-            const int v = v0 + lane;
+        uint32_t ucarry = 0, jmv[2], uov[2], tv[2];
+        int keyv[2];  // payload length of a job of this launch, -1 otherwise
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+            const int v = 64 * g + lane;
             const uint32_t jm = v < nj_all ? slice[UNI_JM_OFF + v] : 0u;
             const int L = (int)(jm & 63u);
             const bool mine = v < nj_all && (L > UNI_WMAX) == WIDE;
-            const uint32_t un = v < nj_all ? units(L) : 0u, t = mine ? (uint32_t)vp_tasks(L, Mm, Mf) : 0u;
-            const uint32_t uincl = wave_incl_sum(un), tincl = wave_incl_sum(t), xincl = wave_incl_sum(mine ? 1u : 0u);
-            if (mine) {
-                const uint32_t x = xcarry + xincl - 1u;
-                s_jm[x] = jm;
-                s_tb[x] = (uint16_t)(carry + tincl - t);
-                s_uo[x] = (uint8_t)(ucarry + uincl - un);
-            }
-            carry += (uint32_t)lane_bcast((int)tincl, 63);
+            const uint32_t un = v < nj_all ? units(L) : 0u;
+            const uint32_t uincl = wave_incl_sum(un);
+            jmv[g] = jm;
+            uov[g] = ucarry + uincl - un;  // (payload units are laid out in list order)
+            tv[g] = mine ? (uint32_t)vp_tasks(L, Mm, Mf) : 0u;
+            keyv[g] = mine ? L : -1;
             ucarry += (uint32_t)lane_bcast((int)uincl, 63);
-            xcarry += (uint32_t)lane_bcast((int)xincl, 63);
         }
-        njobs = (int)xcarry;
+        int x = 0;
+        for (int k = WIDE ? UNI_VMAX : UNI_WMAX; k >= (WIDE ? UNI_WMAX + 1 : 0); --k) {
+#pragma unroll
+            for (int g = 0; g < 2; ++g) {
+                const uint64_t m = __ballot(keyv[g] == k);
+                if (keyv[g] == k) {
+                    const int at = x + __popcll(m & ((1ull << lane) - 1ull));
+                    s_jm[at] = jmv[g];
+                    s_uo[at] = (uint8_t)uov[g];
+                    s_tb[at] = (uint16_t)tv[g];
+                }
+                x += __popcll(m);
+            }
+        }
+        njobs = x;
+        __syncthreads();
+        uint32_t carry = 0;  // task bases, in the sorted order
+        for (int v0 = 0; v0 < njobs; v0 += 64) {
+            const int v = v0 + lane;
+            const uint32_t t = v < njobs ? (uint32_t)s_tb[v] : 0u, tincl = wave_incl_sum(t);
+            if (v < njobs) s_tb[v] = (uint16_t)(carry + tincl - t);
+            carry += (uint32_t)lane_bcast((int)tincl, 63);
+        }
         if (lane == 0) s_tb[njobs] = (uint16_t)carry;
         const int nu = (int)(ucarry < (uint32_t)UNI_VPC ? ucarry : (uint32_t)UNI_VPC);
         for (int q = lane; q < nu; q += 64)

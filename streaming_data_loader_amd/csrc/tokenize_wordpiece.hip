@@ -412,7 +412,6 @@ constexpr int WP_WAVES = 5;
 // fixture 1.14 -> 1.19 ms, held-out 2.32 -> 2.40; 3: within noise) -- the
 // machine is bound by its lanes' probe latency, not by its step count.
 constexpr int WP_NPROBE = 2;
-constexpr int EARLY_LEADS = 0;  // non-ASCII leads a lane looks up before the rare pass
 __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(WP_WAVES, 8))) void k_wordpiece_chunks(
     DevTok T, const uint8_t *__restrict__ text, int64_t N, const uint64_t *__restrict__ off, int64_t R,
     const uint32_t *__restrict__ ranges, uint32_t *__restrict__ tokc, uint32_t *__restrict__ chunk_cnt,
@@ -465,37 +464,6 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(WP_
     PHASE_STAMP(1);
 
     const Ctx C{&T, win, rbits, w0, text, N, off, R};
-    // The lane's first EARLY_LEADS non-ASCII lead bytes (canonical 2- and 3-byte chars): decoded
-    // now and their BMP entries requested -- the entry, and for an ISO char the precomputed
-    // WordPiece id of its one-char piece (assets.cpp: wp_iso_ids) -- so the loads are in flight
-    // through the classification and the block scans and land at the rare pass with no probe
-    // behind them.  Other leads (more per lane, 4-byte or malformed) take the block-wide pass.
-    const int64_t s0 = c0 + 16 * tid;
-    const int nown = s0 >= c1 ? 0 : (int)(c1 - s0 < 16 ? c1 - s0 : 16);
-    const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
-    uint32_t leads = 0;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) leads |= gather4(wv[j] & (wv[j] << 1)) << (4 * j);  // >= 0xC0
-    if (nown < 16) leads &= (1u << nown) - 1u;
-    uint2 ue[EARLY_LEADS > 0 ? EARLY_LEADS : 1];
-    uint32_t urel = 0;  // 1 + lane byte of early lead k in bits [5 k, 5 k + 5); 0: none
-    {
-        uint32_t m = leads;
-#pragma unroll
-        for (int k = 0; k < EARLY_LEADS; ++k) {
-            ue[k] = make_uint2(0u, 0u);
-            if (!m) continue;
-            const int i = __builtin_ctz(m);
-            m &= m - 1;
-            const int rel = 16 * tid + i;
-            int len;
-            const uint32_t cp = decode(C, c0 + rel, win[HALO_L + rel], &len);
-            if ((len == 2 && cp >= 0x80u) || (len == 3 && cp >= 0x800u)) {
-                ue[k] = T.ubmp[cp];
-                urel |= (uint32_t)(i + 1) << (5 * k);
-            }
-        }
-    }
 #ifdef SDL_ABLATE
     // diagnostic build (tools/build_variants.py abl3=SDL_ABLATE, tools/pmc_calibration.py): load only; every record gets 0 ids (so later stages stay in bounds)
     {  // (an opaque use of the window keeps its loads: `x & 0u` let the compiler drop them all)
@@ -508,26 +476,27 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(WP_
 #endif
 
     // ---- 2. register-resident classification of the lane's 16 bytes ----------
+    const int64_t s0 = c0 + 16 * tid;
+    const int nown = s0 >= c1 ? 0 : (int)(c1 - s0 < 16 ? c1 - s0 : 16);
     const int rel0 = HALO_L + 16 * tid;  // window index of s0 (multiple of 16)
     const uint32_t rmask = (rbits[rel0 >> 5] >> (rel0 & 31)) & 0xFFFFu;
+    const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
     uint64_t cls = 0;
-    uint32_t opens = 0;
+    uint32_t leads = 0, opens = 0;
     const uint32_t o4 = T.opener * 0x01010101u;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         const uint32_t x = wv[j];
         cls |= (uint64_t)vclass4(x) << (16 * j);
+        leads |= gather4(x & (x << 1)) << (4 * j);  // >= 0xC0
         opens |= gather4(~nzb(x ^ o4)) << (4 * j);
     }
     if (!T.n_special) opens = 0;
     if (nown < 16) {
         cls &= nown ? ((1ull << (4 * nown)) - 1ull) : 0ull;
+        leads &= (1u << nown) - 1u;
         opens &= (1u << nown) - 1u;
     }
-    uint32_t late_leads = leads;  // the leads the block-wide pass classifies
-#pragma unroll
-    for (int k = 0; k < EARLY_LEADS; ++k)
-        if ((urel >> (5 * k)) & 31u) late_leads &= ~(1u << (((urel >> (5 * k)) & 31u) - 1u));
     uint8_t *s_ovr = s_cnt;
     *reinterpret_cast<uint4 *>(s_ovr + 16 * tid) = make_uint4(~0u, ~0u, ~0u, ~0u);
     // Rare bytes are classified block-parallel, one per thread, and returned as
@@ -544,13 +513,13 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(WP_
             if (c0 - d >= 0 && C.byte(c0 - d) == T.opener) opens_left |= 1u << (d - 1);
     }
     uint32_t nrare;
-    const uint32_t rare_n = (uint32_t)__builtin_popcount(late_leads) |
+    const uint32_t rare_n = (uint32_t)__builtin_popcount(leads) |
                             ((uint32_t)(__builtin_popcount(opens) + __builtin_popcount(opens_left)) << 16);
     const uint32_t rbase = block_excl_sum<TOK_THREADS>(rare_n, &nrare, s_scratch);
     const uint32_t n_leads = nrare & 0xFFFFu, n_opens = nrare >> 16;
     {
         uint32_t lb = rbase & 0xFFFFu, ob = n_leads + (rbase >> 16);
-        for (uint32_t m = late_leads; m;) {
+        for (uint32_t m = leads; m;) {
             const int i = __builtin_ctz(m);
             m &= m - 1;
             s_pieces[lb++] = (uint16_t)(HALO_L + 16 * tid + i);
@@ -568,19 +537,6 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(WP_
     }
     __syncthreads();
     PHASE_STAMP(2);
-#pragma unroll
-    for (int k = 0; k < EARLY_LEADS; ++k) {  // the early leads' entries have landed
-        const uint32_t i1 = (urel >> (5 * k)) & 31u;
-        if (!i1) continue;
-        const int rel = 16 * tid + (int)i1 - 1;
-        const uint32_t vc = vclass_of_entry(ue[k].x);
-        s_ovr[rel] = (uint8_t)vc;
-        if (vc == V_WS || vc == V_ISO) atomicOr(&s_nabits[rel >> 5], 1u << (rel & 31));
-        if (ue[k].y >> 31) {  // an ISO char's one-char piece (or [UNK]), as the block pass probes it
-            s_stage[rel] = (uint16_t)ue[k].y;
-            atomicOr(&s_nabits[CHUNK / 32 + (rel >> 5)], 1u << (rel & 31));
-        }
-    }
     for (uint32_t k = tid; k < n_leads; k += TOK_THREADS) {
         const int wi = s_pieces[k];
         const int rel = wi - HALO_L;
@@ -838,22 +794,32 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(WP_
     int npend = (int)s_scratch[TOK_THREADS / 64 + 1];
     if (tid == 0) s_scratch[TOK_THREADS / 64 + 1] = 0;  // becomes the queue head
     __syncthreads();
-    // (b) state machine over the pending pieces
+    // (b) state machine over the pending pieces.  A pending word is worked by a group of G
+    //     lanes (G = 64 / pending, up to 8; wave-uniform): the group's lanes hold the same
+    //     word state, lane g probes the candidates g * WP_NPROBE .. (g + 1) * WP_NPROBE - 1
+    //     chars shorter than the longest remaining one, and the group takes the longest hit --
+    //     the lowest lane with one -- so a step covers G * WP_NPROBE candidate lengths of
+    //     WordPiece's longest-match-first walk instead of WP_NPROBE (a chunk holds ~12 pending
+    //     words on held-out text, ~1 on the fixture: most lanes would otherwise idle).
     if (npend) {
+        const int G = npend <= 8 ? 8 : npend <= 16 ? 4 : npend <= 32 ? 2 : 1;
+        const int gl = lane & (G - 1), g0 = lane - gl;  // lane in the group, the group's first lane
+        const uint64_t gmask = ((G == 8 ? 0xFFull : G == 4 ? 0xFull : G == 2 ? 0x3ull : 0x1ull)) << g0;
         bool exhausted = false;
-        bool active = false;  // a fast WordPiece state is live
+        bool active = false;  // a fast WordPiece state is live (the same in every lane of a group)
         int pi = 0, prel = 0, L = 0, start = 0, end = 0, nout = 0;
         W16 w{0, 0, 0, 0};
         for (;;) {
             const bool need = !active && !exhausted;
-            const uint64_t nm = __ballot(need);
+            const uint64_t nm = __ballot(need && gl == 0);
             if (nm) {
                 const int leader = __builtin_ctzll(nm);
                 uint32_t base = 0;
                 if (lane == leader) base = atomicAdd(&s_scratch[TOK_THREADS / 64 + 1], (uint32_t)__popcll(nm));
                 base = lane_bcast(base, leader);
+                int q = (int)base + __popcll(nm & ((1ull << lane) - 1ull));  // (valid in the group's first lane)
+                if (G > 1) q = __shfl(q, g0);
                 if (need) {
-                    const int q = (int)base + __popcll(nm & ((1ull << lane) - 1ull));
                     if (q >= npend) {
                         exhausted = true;
                     } else {
@@ -876,31 +842,42 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(WP_
                             while (end < L && end > 0 && (w16_byte(w, end) & 0xC0u) == 0x80u) --end;
                             nout = 0;
                             active = end > 0;
-                            if (!active) {  // no piece can match: the word is [UNK]
+                            if (!active && gl == 0) {  // no piece can match: the word is [UNK]
                                 out[0] = (uint16_t)T.unk_id;
                                 s_cnt[pi] = 1;
                             }
-                        } else if (kind == V_ISO) {
-                            int len;
-                            const uint32_t e = uentry(T, decode(C, p, win[prel + HALO_L], &len));
-                            uint8_t buf[16];
-                            const int nb = append_norm(C, e, p, len, buf, 0);
-                            s_cnt[pi] = (uint8_t)wordpiece_general(T, buf, nb, out);
-                        } else {  // deferred to the cooperative lattice below
-                            const uint32_t d = atomicAdd(&s_scratch[TOK_THREADS / 64 + 2], 1u);
-                            s_pend[d] = (uint16_t)pi;  // d < this round's consumed entries
+                        } else if (gl == 0) {
+                            if (kind == V_ISO) {
+                                int len;
+                                const uint32_t e = uentry(T, decode(C, p, win[prel + HALO_L], &len));
+                                uint8_t buf[16];
+                                const int nb = append_norm(C, e, p, len, buf, 0);
+                                s_cnt[pi] = (uint8_t)wordpiece_general(T, buf, nb, out);
+                            } else {  // deferred to the cooperative lattice below
+                                const uint32_t d = atomicAdd(&s_scratch[TOK_THREADS / 64 + 2], 1u);
+                                s_pend[d] = (uint16_t)pi;  // d < this round's consumed entries
+                            }
                         }
                     }
                 }
             }
             if (!__any(active || !exhausted)) break;
-            if (active) {  // probe the candidates ending at `end` and WP_NPROBE - 1 chars earlier together
+            if (active) {  // probe this lane's WP_NPROBE candidates, gl * WP_NPROBE chars below `end`
                 const W16 sh = start ? shift_right_bytes(w, start) : w;
                 const uint32_t cont = start > 0 ? 1u : 0u;
                 int ek[WP_NPROBE];
-                ek[0] = end;
+                // (an ASCII word's chars are its bytes: no walk over continuation bytes)
+                const bool ascii = ((w.x | w.y | w.z | w.w) & 0x80808080u) == 0u;
+                int e0 = end;
+                if (ascii) {
+                    e0 = end - gl * WP_NPROBE > start ? end - gl * WP_NPROBE : start;
+                } else {
+                    for (int k = 0; k < gl * WP_NPROBE; ++k) e0 = e0 > start ? w16_prev_char(w, e0, start) : start;
+                }
+                ek[0] = e0;
 #pragma unroll
-                for (int k = 1; k < WP_NPROBE; ++k) ek[k] = ek[k - 1] > start ? w16_prev_char(w, ek[k - 1], start) : start;
+                for (int k = 1; k < WP_NPROBE; ++k)
+                    ek[k] = ek[k - 1] <= start ? start : ascii ? ek[k - 1] - 1 : w16_prev_char(w, ek[k - 1], start);
                 W16 cw[WP_NPROBE];
                 Probe Pk[WP_NPROBE];
 #pragma unroll
@@ -913,18 +890,27 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(WP_
 #pragma unroll
                 for (int k = 0; k < WP_NPROBE; ++k) {
                     const int nk = ek[k] - start;
-                    if (id < 0 && (k == 0 || nk > 0)) {
+                    if (id < 0 && nk > 0) {
                         id = probe_result(Pk[k], (uint32_t)nk | (cont << 8), cw[k]);
                         got = nk;
                     }
                 }
-                const int e1 = ek[WP_NPROBE - 1], n1 = e1 - start;
+                int e1 = ek[WP_NPROBE - 1];
+                if (G > 1) {  // the group's longest hit: its lowest lane with one
+                    const uint64_t hm = __ballot(id >= 0) & gmask;
+                    const int src = hm ? __builtin_ctzll(hm) : g0;
+                    id = __shfl(id, src);
+                    got = __shfl(got, src);
+                    e1 = __shfl(e1, g0 + G - 1);
+                }
+                const int n1 = e1 - start;
                 lds_u16 *out = stage + prel;
                 if (id >= 0) {
-                    out[nout++] = (uint16_t)id;
+                    if (gl == 0) out[nout] = (uint16_t)id;
+                    ++nout;
                     start += got;
                     if (start >= L) {
-                        s_cnt[pi] = (uint8_t)nout;
+                        if (gl == 0) s_cnt[pi] = (uint8_t)nout;
                         active = false;
                     } else {
                         end = L < start + T.maxlen_cont ? L : start + T.maxlen_cont;
@@ -933,8 +919,10 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(WP_
                 } else {
                     end = n1 > 0 ? w16_prev_char(w, e1, start) : start;
                     if (end <= start) {  // no piece matches here: the whole word is [UNK]
-                        out[0] = (uint16_t)T.unk_id;
-                        s_cnt[pi] = 1;
+                        if (gl == 0) {
+                            out[0] = (uint16_t)T.unk_id;
+                            s_cnt[pi] = 1;
+                        }
                         active = false;
                     }
                 }

@@ -15,6 +15,8 @@ import os
 import sys
 from collections import defaultdict
 
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
 
 def short(name):
     return name.split("(")[0].replace("void ", "")
@@ -42,6 +44,12 @@ def main():
     out = {"source": f"rocprofv3 --pmc passes of bench.py --task {task} --arena-mib {arena} --corpus {corpus} "
                      "(tools/pmc.sh)",
            "task": task, "arena_mib": arena, "corpus": corpus, "kernels": {}}
+    # provenance: the library the passes ran (its embedded source hash) and, when the caller
+    # passes it (the GPU box has no .git), the commit
+    from streaming_data_loader_amd import build
+    out["library_build_id"] = build.embedded_id(os.environ.get("SDL_LIB") or build.LIB)
+    if os.environ.get("SDL_HEAD"):
+        out["head"] = os.environ["SDL_HEAD"]
     for k, cs in vals.items():
         avg = {c: sum(v) / len(v) for c, v in cs.items()}
         ent = {"launches": max(len(v) for v in cs.values()), "counters": avg}
