@@ -863,6 +863,17 @@ static void load_unigram(const JValue &root, const std::string &data_dir, HostTo
         else t.maxlen_first = std::max(t.maxlen_first, (int)pay.size());
         entries.push_back(make_slot(pay, m ? UC_META : UC_PIECE, (int32_t)i, t.vpool));
     }
+    // the longest plain piece (>= 4 bytes) under each hashed 4-byte prefix: k_unigram_viterbi
+    // skips a payload row's candidates of >= 4 bytes past it (a key collision only raises it)
+    t.upfx.assign((size_t)1 << UNI_PFX_BITS, 0);
+    for (size_t i = 0; i < nv; ++i) {
+        const std::string &s = t.pieces[i];
+        if (s.size() < 4 || id_of[s] != (int)i || s.compare(0, 3, meta) == 0) continue;
+        uint32_t x;
+        std::memcpy(&x, s.data(), 4);
+        uint8_t &b = t.upfx[uni_pfx_key(x)];
+        b = (uint8_t)std::max<size_t>(b, std::min<size_t>(s.size(), 255));
+    }
     // candidate rows are 64-bit masks in the kernels
     if (t.maxlen_cont > 63 || t.maxlen_first > 64)
         throw std::runtime_error("Unigram: pieces longer than 64 bytes are not supported");

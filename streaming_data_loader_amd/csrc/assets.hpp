@@ -23,7 +23,8 @@ struct HostTokenizer {
     std::vector<uint16_t> upage;
     std::vector<uint32_t> uentry;
     std::vector<uint8_t> upool;
-    std::vector<uint32_t> ubmp;  // per BMP code point: device-format entry, WordPiece ISO id (wp_iso_ids)
+    std::vector<uint32_t> ubmp;
+    std::vector<uint8_t> upfx;   // Unigram: longest plain piece under each hashed 4-byte prefix  // per BMP code point: device-format entry, WordPiece ISO id (wp_iso_ids)
 
     // ---- device image of the vocabulary ------------------------------------
     std::vector<VSlot> slots;

@@ -190,7 +190,13 @@ struct DevTok {
     int32_t maxlen_meta;     // longest "▁"-piece payload (bytes)
     int32_t maxlen_word;     // longest word-table payload
     int32_t maxlen_piece;    // longest piece, "▁" included (bytes)
+    const uint8_t *upfx;     // longest plain piece (>= 4 B) under each hashed 4-byte prefix (uni_pfx_key)
 };
+
+// Unigram prefix bound: a plain piece of >= 4 bytes starting with bytes x (little-endian u32) is
+// at most upfx[uni_pfx_key(x)] bytes long (assets.cpp; a collision only raises the bound)
+constexpr int UNI_PFX_BITS = 16;
+__host__ __device__ inline uint32_t uni_pfx_key(uint32_t x) { return (x * 0x9E3779B1u) >> (32 - UNI_PFX_BITS); }
 
 // Row assembly parameters (GenTokenizer + BertData/GptData/T5Data framing).
 struct RowParams {

@@ -263,6 +263,7 @@ struct sdl_batcher {
     // unigram (t5)
     DevBuf<double> d_uscore;
     DevBuf<uint16_t> d_wres, d_cpage;
+    DevBuf<uint8_t> d_upfx;
     DevBuf<uint2> d_cent, d_cbmp;
     DevBuf<float> d_uscore32;
     DevBuf<uint8_t> d_tnorm;
@@ -1088,6 +1089,9 @@ int sdl_batcher_create(const sdl_config *cfg, const char *tokenizer_path, const 
             HIP_TRY(hipMemcpy(h->d_wslots.p, t.wslots.data(), t.wslots.size() * sizeof(VSlot), hipMemcpyHostToDevice));
             d.wslots = h->d_wslots.p;
             d.wslot_mask = t.wslot_mask;
+            h->d_upfx.ensure(t.upfx.size());
+            HIP_TRY(hipMemcpy(h->d_upfx.p, t.upfx.data(), t.upfx.size(), hipMemcpyHostToDevice));
+            d.upfx = h->d_upfx.p;
             d.uscore = h->d_uscore.p;
             d.wres = h->d_wres.p;
             d.cpage = h->d_cpage.p;

@@ -62,6 +62,7 @@ constexpr uint8_t CNT_JOB = 0x80, CNT_WIDE = 0x40;
 // k_unigram_viterbi: a pass takes the chunk's next jobs whose candidates fit VTCAP (one job
 // always does: vp_tasks(UNI_WMAX) = 17 + 16 * 16 < VTCAP) and at most VJP of them (a DP lane each)
 constexpr int VJP = 64, VTCAP = 768, VU = 2;  // VU: probes in flight per lane
+constexpr int PFX_JOBS = 6;                    // jobs a wide pass takes at most (their prefix bounds in LDS)
 static_assert(VJP <= 64 && VTCAP % (64 * VU) == 0 && VTCAP < 0x7FF, "a hit index fits a back pointer's 11 bits");
 
 typedef __attribute__((address_space(3))) double lds_f64;
@@ -1154,6 +1155,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(UNI_VWAVES, 
     __shared__ uint8_t s_k[VP_CAP];        // ids of each job
     using CM = std::conditional_t<WIDE, uint64_t, uint32_t>;  // (<= UNI_VMAX / UNI_WMAX payload bytes)
     __shared__ CM s_cm[VP_CAP];            // bit x: payload byte x continues a char
+    // wide passes (<= PFX_JOBS jobs): each payload start's prefix bound (T.upfx)
+    __shared__ uint8_t s_pl[WIDE ? PFX_JOBS * UNI_VMAX : 1];
     __shared__ double s_sc[VTCAP];         // per task of the pass: the candidate's score, -inf: no piece
     __shared__ uint16_t s_id[VTCAP];       // ... its id
     // after the DP: back pointers (narrow: start node << 11 | task, UNK_T: unk, 0xFFFF: unset, per
@@ -1246,8 +1249,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(UNI_VWAVES, 
     VIT_STAMP(1);
     for (int a = 0; a < njobs;) {
         int b = a + 1;  // the pass: jobs [a, b)
-        while (b < njobs && b - a < VJP && (int)s_tb[b + 1] - (int)s_tb[a] <= VTCAP) ++b;
+        while (b < njobs && b - a < (WIDE ? PFX_JOBS : VJP) && (int)s_tb[b + 1] - (int)s_tb[a] <= VTCAP) ++b;
         const int T0 = s_tb[a], TZ = s_tb[b];
+        if constexpr (WIDE) {  // the pass's starts' prefix bounds: one load each, all in flight
+            for (int q = lane; q < (b - a) * UNI_VMAX; q += 64) {
+                const int jl = q / UNI_VMAX, i = q - jl * UNI_VMAX;
+                const int Lq = (int)(s_jm[a + jl] & 63u);
+                uint32_t bound = 255u;  // (fewer than 4 bytes left: no candidate to bound)
+                if (i + 4 <= Lq) bound = T.upfx[uni_pfx_key(lds_w16(pb32, 16 * s_uo[a + jl] + i, 4).x)];
+                s_pl[q] = (uint8_t)bound;
+            }
+            __syncthreads();
+        }
         {  // lane l takes the pass's tasks [T0 + l K, T0 + (l + 1) K) in rounds of VU: one
            // decode per pass, then (i, j) steps along the rows; a row's 16 bytes are read once
         const int K = (TZ - T0 + 63) >> 6;
@@ -1297,6 +1310,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(UNI_VWAVES, 
                 if (((i > 0 ? cm >> i : (CM)0) | cm >> j) & 1u) continue;
                 const int ps = i < 0 ? 0 : i;
                 const int n = j - ps;
+                // (wide rows: no plain piece this long starts with these 4 bytes)
+                if constexpr (WIDE)
+                    if (i >= 0 && n >= 4 && n > (int)s_pl[(jv - a) * UNI_VMAX + i]) continue;
                 const uint32_t cont = i < 0 ? UC_META : UC_PIECE;
                 meta[u] = (uint32_t)n | cont << 8;
                 if (src + ps != cur_ps) {
@@ -1928,7 +1944,7 @@ hipError_t launch_unigram_chunks(const DevTok &T, const uint8_t *text, int64_t N
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_unigram_chunks, dim3((unsigned)n_chunks), dim3(TOK_THREADS), 0, st, T, text, N, off, R, ranges,
                        tokc, chunk_cnt, chunk_ent, rec_local, W.counters, W.items, W.item_cap, W.err);
-    // the narrow jobs' Viterbi on st; the wide jobs' and the long items beside it on W.side
+    // the narrow jobs' Viterbi and then the long items on st; the wide jobs' Viterbi beside them on W.side
     hipStream_t side = st;
     if (W.side && W.ev_fork && W.ev_join) {
         e = hipEventRecord(W.ev_fork, st);
@@ -1940,15 +1956,18 @@ hipError_t launch_unigram_chunks(const DevTok &T, const uint8_t *text, int64_t N
                        chunk_cnt, rec_local);
     hipLaunchKernelGGL(k_unigram_viterbi<true>, dim3((unsigned)n_chunks), dim3(64), 0, side, T, N, off, R, ranges, tokc,
                        chunk_cnt, rec_local);
+    // The long items follow the narrow jobs on st: beside the wide jobs, not after them (on
+    // held-out text the wide jobs' Viterbi outlasts the narrow one).
+    const hipStream_t ls = st;
     // a row's candidate ends: <= Mm + 1 ("▁" row) or <= Mf.  Two stages: items of <= 128
     // normalized bytes (nearly all) with a small LDS footprint and more of them in
     // flight, then the rest (<= 512) from the first stage's overflow list.
     const int g1 = W.lane_blocks * 4 / 3;
 #define UNI_LONG_STAGES(KM)                                                                                     \
-    hipLaunchKernelGGL((k_unigram_long<KM, LONG_NORM1>), dim3((unsigned)g1), dim3(64), 0, side, T, text, N, off, R,  \
+    hipLaunchKernelGGL((k_unigram_long<KM, LONG_NORM1>), dim3((unsigned)g1), dim3(64), 0, ls, T, text, N, off, R,  \
                        ranges, W.items, W.item_cap, W.counters, W.counters, tokc, chunk_cnt, rec_local, W.pool,      \
                        W.pool_cap, W.items2, W.items2_cap, W.counters + 4, W.err);                                    \
-    hipLaunchKernelGGL((k_unigram_long<KM, LONG_NORM>), dim3((unsigned)W.lane_blocks), dim3(64), 0, side, T, text, N,\
+    hipLaunchKernelGGL((k_unigram_long<KM, LONG_NORM>), dim3((unsigned)W.lane_blocks), dim3(64), 0, ls, T, text, N,\
                        off, R, ranges, W.items2, W.items2_cap, W.counters + 4, W.counters, tokc, chunk_cnt,           \
                        rec_local, W.pool, W.pool_cap, W.huge, W.huge_cap, W.counters + 3, W.err);
     if (T.maxlen_meta + 1 <= 20 && T.maxlen_first <= 20) {  // smaller LDS: more items in flight
@@ -1959,7 +1978,7 @@ hipError_t launch_unigram_chunks(const DevTok &T, const uint8_t *text, int64_t N
         UNI_LONG_STAGES(64)
     }
 #undef UNI_LONG_STAGES
-    hipLaunchKernelGGL(k_unigram_huge, dim3((unsigned)W.huge_blocks), dim3(64), 0, side, T, text, N, off, R, W.counters,
+    hipLaunchKernelGGL(k_unigram_huge, dim3((unsigned)W.huge_blocks), dim3(64), 0, ls, T, text, N, off, R, W.counters,
                        tokc, chunk_cnt, rec_local, W.scratch, W.pool, W.pool_cap, W.huge, W.huge_cap, W.err);
     if (side != st) {
         e = hipEventRecord(W.ev_join, side);
