@@ -44,9 +44,14 @@ HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 TASKS = {
     "mlm": {"S": 512, "B": 256, "tok": "bert", "kernel": "k_wordpiece_chunks", "planes": 4,
             "workload": "mlm seq_len=512 batch=256 (BASELINE configs[1])"},
+    # (the tokenize stage the HIP events time: for span the chunk kernel, the two Viterbi
+    # launches and the long-item stages; for clm the chunk kernel and k_bpe_long -- their PMC
+    # counters are summed over the same launches)
     "span": {"S": 512, "B": 256, "tok": "t5", "kernel": "k_unigram_chunks", "planes": 2.25,
+             "pmc_kernels": ["k_unigram_chunks", "k_unigram_viterbi", "k_unigram_long", "k_unigram_huge"],
              "workload": "span t5 Unigram seq_len=512 batch=256 (BASELINE configs[2]; reference Span{16.0, 2.0})"},
     "clm": {"S": 1024, "B": 128, "tok": "gpt2", "kernel": "k_bpe_chunks", "planes": 3,
+            "pmc_kernels": ["k_bpe_chunks", "k_bpe_long"],
             "workload": "clm gpt2 byte-BPE seq_len=1024 batch=128 (BASELINE configs[3])"},
     "multi-label": {"S": 128, "B": 2048, "tok": "bert", "kernel": "k_wordpiece_chunks", "planes": 3,
                     "workload": "multi-label seq_len=128 batch=2048 (BASELINE configs[4], B from multi_cases.rs:22)"},
@@ -247,8 +252,18 @@ def load_pmc(task, arena_mib, kernel, corpus="fixture"):
             return None, (f"{os.path.relpath(p, REPO)} was collected for task={d.get('task')} "
                           f"arena={d.get('arena_mib')} corpus={d.get('corpus', 'fixture')}")
         # (a template instance is named with its arguments: sdl::k_wordpiece_chunks<false>)
-        name = next(n for n in d["kernels"] if n == "sdl::" + kernel or n.startswith("sdl::" + kernel + "<"))
-        k = d["kernels"][name]
+        kernels = kernel if isinstance(kernel, (list, tuple)) else [kernel]
+        names = [n for n in d["kernels"] for kk in kernels if n == "sdl::" + kk or n.startswith("sdl::" + kk + "<")]
+        if not names:
+            raise StopIteration(f"no {kernels} in the summary")
+        if len(names) == 1:
+            k = d["kernels"][names[0]]
+        else:  # the tokenize stage's launches together: counters summed per stage launch
+            k = {"launches": max(d["kernels"][n]["launches"] for n in names), "counters": {},
+                 "kernels_summed": [n.replace("sdl::", "") for n in names]}
+            for n in names:
+                for c, v in d["kernels"][n]["counters"].items():
+                    k["counters"][c] = k["counters"].get(c, 0.0) + v
         k["_file"] = os.path.relpath(p, REPO)
         return k, None
     except Exception as e:  # a malformed summary is reported, not used
@@ -612,7 +627,7 @@ def heldout_leg(args, db, dev, stream, task, world, rank, barrier):
            "roofline": {"kernel": task["kernel"], "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS,
                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 5),
                         "algorithmic_bytes_per_launch": tok_bytes, "avg_launch_ms": round(tok_ms, 4)}}
-    pmc, note = load_pmc(args.task, args.arena_mib, task["kernel"], "heldout")
+    pmc, note = load_pmc(args.task, args.arena_mib, task.get("pmc_kernels", task["kernel"]), "heldout")
     if pmc is not None:
         traffic, issue, note = pmc_roofline(pmc, tok_ms, tok_bytes, stream_bytes=N + 8 * (R + 1))
         out["roofline"]["traffic"] = traffic
@@ -711,7 +726,7 @@ def main(argv=None):
     # whole path, per step: text + offsets + the int32 [rows, S] planes
     path_bytes = N + 8 * (R + 1) + int(4 * task["planes"] * rows * S)
     line = base_line(args, world, step_ms, value, task, N, R, rows, toks)
-    pmc, pmc_note = load_pmc(args.task, args.arena_mib, task["kernel"], args.corpus)
+    pmc, pmc_note = load_pmc(args.task, args.arena_mib, task.get("pmc_kernels", task["kernel"]), args.corpus)
     traffic, issue = None, None
     if pmc is not None:
         traffic, issue, pmc_note = pmc_roofline(pmc, tok_ms, tok_bytes, stream_bytes=N + 8 * (R + 1))
@@ -735,6 +750,8 @@ def main(argv=None):
                         "traffic_split": pmc.get("_split") if pmc is not None else None,
                         "algorithmic_bytes_per_launch": tok_bytes, "avg_launch_ms": round(tok_ms, 4),
                         "hbm_frac_upper": round(hbm_frac_hi, 5)}
+    if pmc is not None and pmc.get("kernels_summed"):  # (the stage's launches: counters summed)
+        line["roofline"]["kernels"] = pmc["kernels_summed"]
     if bound != "hbm":
         line["roofline"]["bound_note"] = (f"{bound} at {issue['frac']:.2f} of its issue peak binds this kernel; "
                                           "achieved/peak/frac are its algorithmic HBM bytes against 8 TB/s")
