@@ -50,6 +50,8 @@ def main():
     out["library_build_id"] = build.embedded_id(os.environ.get("SDL_LIB") or build.LIB)
     if os.environ.get("SDL_HEAD"):
         out["head"] = os.environ["SDL_HEAD"]
+    import time
+    out["date"] = time.strftime("%Y-%m-%d") + (f" ({os.environ['SDL_ROUND']})" if os.environ.get("SDL_ROUND") else "")
     for k, cs in vals.items():
         avg = {c: sum(v) / len(v) for c, v in cs.items()}
         ent = {"launches": max(len(v) for v in cs.values()), "counters": avg}
