@@ -795,17 +795,18 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(WP_
     if (tid == 0) s_scratch[TOK_THREADS / 64 + 1] = 0;  // becomes the queue head
     __syncthreads();
     // (b) state machine over the pending pieces.  A pending word is worked by a group of G
-    //     lanes (G = 64 / pending, up to 8; wave-uniform): the group's lanes hold the same
+    //     lanes (G = 64 / pending lanes, at most 8; wave-uniform): the group's lanes hold the same
     //     word state, lane g probes the candidates g * WP_NPROBE .. (g + 1) * WP_NPROBE - 1
     //     chars shorter than the longest remaining one, and the group takes the longest hit --
     //     the lowest lane with one -- so a step covers G * WP_NPROBE candidate lengths of
     //     WordPiece's longest-match-first walk instead of WP_NPROBE (a chunk holds ~12 pending
     //     words on held-out text, ~1 on the fixture: most lanes would otherwise idle).
     if (npend) {
-        const int G = npend <= 8 ? 8 : npend <= 16 ? 4 : npend <= 32 ? 2 : 1;
-        const int gl = lane & (G - 1), g0 = lane - gl;  // lane in the group, the group's first lane
-        const uint64_t gmask = ((G == 8 ? 0xFFull : G == 4 ? 0xFull : G == 2 ? 0x3ull : 0x1ull)) << g0;
-        bool exhausted = false;
+        const int G = npend <= 8 ? 8 : npend > 32 ? 1 : 64 / npend;  // (lanes past the last group idle)
+        const int gl = lane % G, g0 = lane - gl;    // lane in the group, the group's first lane
+        const uint64_t gmask = ((1ull << G) - 1ull) << g0;
+        const bool grouped = g0 + G <= 64;
+        bool exhausted = !grouped;  // (a lane outside every group takes no word)
         bool active = false;  // a fast WordPiece state is live (the same in every lane of a group)
         int pi = 0, prel = 0, L = 0, start = 0, end = 0, nout = 0;
         W16 w{0, 0, 0, 0};
