@@ -52,3 +52,22 @@ def test_committed_summaries_give_a_split(task, kernel):
     assert split["stream_read"] + split["write"] <= traffic <= split["uniform_x2_upper_bound"]
     with open(os.path.join(REPO, "profiles", "pmc", f"{task}_256mib.json")) as f:
         assert re.search(r"\(r0[4-9]\)", json.load(f).get("date", ""))  # (a dated, current-round summary)
+
+
+@pytest.mark.parametrize("task", ["span", "clm"])
+def test_stage_counters_sum_every_launch(task):
+    """span and clm time their whole tokenize stage (the chunk kernel plus the Viterbi / long-item
+    launches): their PMC figures are the sum over those launches' per-launch counters."""
+    kernels = bench.TASKS[task]["pmc_kernels"]
+    pmc, note = bench.load_pmc(task, 256, kernels, "fixture")
+    assert pmc is not None, note
+    with open(os.path.join(REPO, "profiles", "pmc", f"{task}_256mib.json")) as f:
+        d = json.load(f)
+    names = [n for n in d["kernels"] for k in kernels if n == "sdl::" + k or n.startswith("sdl::" + k + "<")]
+    assert len(names) >= 2 and sorted(pmc["kernels_summed"]) == sorted(n.replace("sdl::", "") for n in names)
+    for c in ("SQ_INSTS_VALU", "FETCH_SIZE", "WRITE_SIZE"):
+        want = sum(d["kernels"][n]["counters"].get(c, 0.0) for n in names)
+        assert abs(pmc["counters"][c] - want) <= 1e-6 * max(want, 1.0)
+    # a single kernel name still returns that kernel's own entry
+    one, _ = bench.load_pmc(task, 256, bench.TASKS[task]["kernel"], "fixture")
+    assert "kernels_summed" not in one
